@@ -1,0 +1,291 @@
+/*
+ * tiflash_amd.h — C-ABI drop-in boundary of the MI355X (gfx950) execution layer for
+ * TiFlash's Block/Column hot path: filter / compare, arithmetic, hash GROUP BY (Aggregator),
+ * hash join build + probe, and the ExchangeSender hash repartition.
+ *
+ * Conventions (plain C, no exceptions across the ABI, no torch types):
+ *   - Every entry point returns an int status: TFG_OK (0) or a negative TFG_ERR_* code.
+ *     tfg_last_error() returns a thread-local message for the last failure.  The codes mirror
+ *     the reference's DB::ErrorCodes used on this path (SIZES_OF_COLUMNS_DOESNT_MATCH,
+ *     ILLEGAL_TYPE_OF_COLUMN_FOR_FILTER, LOGICAL_ERROR, ...).
+ *   - Column pointers are DEVICE pointers (HBM) laid out like the reference's PaddedPODArray
+ *     payload: `n` contiguous values of the column's native width.  Null maps are UInt8,
+ *     nonzero = NULL (ColumnNullable, dbms/src/Columns/ColumnNullable.h:37).  Filters are UInt8,
+ *     nonzero = keep (dbms/src/Columns/ColumnUtil.cpp:32-79).
+ *   - Work is enqueued on the context's HIP stream.  Functions that return a count to the host
+ *     (out_*_host arguments) synchronise that stream; the device-side count is always written
+ *     too, so callers that stay on the device never block.
+ *   - Inputs are never modified (COW ColumnPtr semantics of IColumn::filter et al.,
+ *     dbms/src/Columns/IColumn.h:426); every operation writes caller-provided outputs.
+ *
+ * Each entry point names the reference interface it replaces (paths relative to
+ * /root/reference/dbms/src).
+ */
+#ifndef TIFLASH_AMD_H
+#define TIFLASH_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- status codes */
+#define TFG_OK 0
+#define TFG_ERR_INVALID_ARG (-1)        /* BAD_ARGUMENTS */
+#define TFG_ERR_HIP (-2)                /* runtime failure reported by HIP */
+#define TFG_ERR_OOM (-3)                /* device allocation failed */
+#define TFG_ERR_NOT_IMPLEMENTED (-4)    /* type / op combination not supported */
+#define TFG_ERR_SIZE_MISMATCH (-5)      /* SIZES_OF_COLUMNS_DOESNT_MATCH */
+#define TFG_ERR_ILLEGAL_TYPE (-6)       /* ILLEGAL_TYPE_OF_ARGUMENT / ..._FOR_FILTER */
+#define TFG_ERR_LOGICAL (-7)            /* LOGICAL_ERROR */
+#define TFG_ERR_CAPACITY (-8)           /* output buffer too small (caller retries larger) */
+#define TFG_ERR_NO_DEVICE (-9)          /* no HIP device visible */
+#define TFG_ERR_FAULT_INJECTED (-10)    /* test-only failpoint (TFG_FAILPOINT env var) */
+
+/* ---------------------------------------------------------------- column types */
+/* Native fixed-width column payloads (ColumnVector<T> / ColumnDecimal<T>). Decimal columns
+ * carry their scale separately; values are the scaled integers (Decimal<T>{T value},
+ * dbms/src/Common/Decimal.h:209). */
+typedef enum tfg_type {
+    TFG_INT8 = 1,
+    TFG_INT16 = 2,
+    TFG_INT32 = 3,
+    TFG_INT64 = 4,
+    TFG_UINT8 = 5,
+    TFG_UINT16 = 6,
+    TFG_UINT32 = 7,
+    TFG_UINT64 = 8,
+    TFG_FLOAT32 = 9,
+    TFG_FLOAT64 = 10,
+    TFG_DECIMAL32 = 11,  /* Int32 payload  (precision <= 9)  */
+    TFG_DECIMAL64 = 12,  /* Int64 payload  (precision <= 18) */
+    TFG_DECIMAL128 = 13, /* Int128 payload (precision <= 38), little-endian two's complement */
+} tfg_type;
+
+/* Comparison ops (dbms/src/Functions/FunctionsComparison.h, accurate:: semantics of
+ * dbms/src/Core/AccurateComparison.h:33-159). */
+typedef enum tfg_cmp_op {
+    TFG_EQ = 0,
+    TFG_NE = 1,
+    TFG_LT = 2,
+    TFG_LE = 3,
+    TFG_GT = 4,
+    TFG_GE = 5,
+} tfg_cmp_op;
+
+/* Binary arithmetic (dbms/src/Functions/FunctionBinaryArithmetic.h). */
+typedef enum tfg_arith_op {
+    TFG_PLUS = 0,
+    TFG_MINUS = 1,
+    TFG_MULTIPLY = 2,
+} tfg_arith_op;
+
+/* Logical combination of UInt8 masks (dbms/src/Functions/FunctionsLogical.cpp). */
+typedef enum tfg_logic_op {
+    TFG_AND = 0,
+    TFG_OR = 1,
+    TFG_NOT = 2, /* unary: b ignored */
+} tfg_logic_op;
+
+/* Aggregate functions on the path (dbms/src/AggregateFunctions/AggregateFunctionSum.h,
+ * AggregateFunctionCount.h).  Result types follow the reference factory
+ * (AggregateFunctionSum.cpp:31-120): sum(Int*) -> Int64, sum(UInt*) -> UInt64,
+ * sum(Float*) -> Float64, sum(Decimal(p,s)) -> Decimal(min(p+22,65), s) held as Int128;
+ * count -> UInt64. */
+typedef enum tfg_agg_kind {
+    TFG_AGG_SUM = 0,
+    TFG_AGG_COUNT = 1,     /* count(arg): non-NULL rows of arg */
+    TFG_AGG_COUNT_ALL = 2, /* count(*) / count(1): arg ignored */
+} tfg_agg_kind;
+
+/* Join kinds (ASTTableJoin::Kind, dbms/src/Interpreters/Join.h). Strictness ALL. */
+typedef enum tfg_join_kind {
+    TFG_JOIN_INNER = 0,
+    TFG_JOIN_LEFT = 1,  /* unmatched probe rows emit build index -1 (default / NULL row) */
+    TFG_JOIN_SEMI = 2,  /* probe rows with at least one match, once */
+    TFG_JOIN_ANTI = 3,  /* probe rows with no match (NULL keys count as no match) */
+} tfg_join_kind;
+
+/* String collators relevant to partition hashing (dbms/src/TiDB/Collation/Collator.h). */
+typedef enum tfg_collator {
+    TFG_COLLATOR_NONE = 0,        /* raw bytes                                       */
+    TFG_COLLATOR_BINARY = 1,      /* BinCollatorSortKey<false>: raw bytes            */
+    TFG_COLLATOR_BIN_PADDING = 2, /* BinCollatorSortKey<true>: right-trim ' ' (utf8mb4_bin etc.) */
+} tfg_collator;
+
+/* ---------------------------------------------------------------- context & memory */
+typedef struct tfg_ctx tfg_ctx;
+
+/* Creates a context bound to HIP device `device` and stream `stream` (a hipStream_t; NULL =
+ * the null stream).  The context owns a growable device scratch arena. */
+int tfg_ctx_create(int device, void *stream, tfg_ctx **out);
+int tfg_ctx_destroy(tfg_ctx *ctx);
+int tfg_ctx_set_stream(tfg_ctx *ctx, void *stream);
+int tfg_ctx_sync(tfg_ctx *ctx);
+/* Pre-sizes the scratch arena so later calls never allocate (and can be graph-captured). */
+int tfg_ctx_reserve(tfg_ctx *ctx, size_t bytes);
+const char *tfg_last_error(void);
+const char *tfg_version(void);
+int tfg_device_count(int *out);
+
+int tfg_buf_alloc(tfg_ctx *ctx, size_t bytes, void **out_dev);
+int tfg_buf_free(tfg_ctx *ctx, void *dev);
+int tfg_upload(tfg_ctx *ctx, void *dst_dev, const void *src_host, size_t bytes);
+int tfg_download(tfg_ctx *ctx, void *dst_host, const void *src_dev, size_t bytes);
+
+/* Size in bytes of one value of `type`, 0 if unknown. */
+size_t tfg_type_width(int type);
+
+/* ---------------------------------------------------------------- a1/a2 comparison */
+/* out_mask[i] = Op(col[i], scalar) as 0/1.  Replaces NumComparisonImpl::vectorConstant
+ * (Functions/FunctionsComparison.h:101-114) reached from FunctionComparison::executeImpl
+ * (:1388-1440).  `scalar_host` points to one host value of `scalar_type`.  A NULL input row
+ * (col_nullmap[i] != 0) yields 0, i.e. the Nullable(UInt8) result already folded the way
+ * FilterDescription does (Columns/FilterDescription.cpp:68-108). */
+int tfg_cmp_const(tfg_ctx *ctx, int col_type, const void *col, const uint8_t *col_nullmap, int64_t n,
+                  int op, int scalar_type, const void *scalar_host, uint8_t *out_mask);
+/* Constant on the left: out[i] = Op(scalar, col[i]) (NumComparisonImpl::constantVector). */
+int tfg_cmp_const_left(tfg_ctx *ctx, int scalar_type, const void *scalar_host, int op, int col_type,
+                       const void *col, const uint8_t *col_nullmap, int64_t n, uint8_t *out_mask);
+/* out_mask[i] = Op(a[i], b[i]) (NumComparisonImpl::vectorVector, :78-99). */
+int tfg_cmp_vector(tfg_ctx *ctx, int a_type, const void *a, const uint8_t *a_nullmap, int op, int b_type,
+                   const void *b, const uint8_t *b_nullmap, int64_t n, uint8_t *out_mask);
+/* and / or / not over UInt8 masks (Functions/FunctionsLogical.cpp); any nonzero is true. */
+int tfg_mask_logic(tfg_ctx *ctx, int op, const uint8_t *a, const uint8_t *b, int64_t n, uint8_t *out_mask);
+
+/* ---------------------------------------------------------------- a3 arithmetic */
+/* out[i] = a[i] op b[i] (FunctionBinaryArithmetic.h:761-1200, DecimalBinaryOperation :231-500).
+ * Either side may be a constant (`*_is_const` != 0: the pointer is a HOST pointer to one value).
+ * Decimal operands are aligned to the result scale for +/- (applyScaled) and multiplied raw for
+ * * (result scale = a_scale + b_scale, MulDecimalInferer, Common/Decimal.h:109-163).
+ * Integer results wrap like the reference's native ops; Decimal128 results are exact Int128. */
+int tfg_arith(tfg_ctx *ctx, int op, int a_type, const void *a, int a_is_const, int a_scale, int b_type,
+              const void *b, int b_is_const, int b_scale, int res_type, int res_scale, int64_t n, void *out);
+
+/* ---------------------------------------------------------------- a5-a8 filter */
+/* Number of nonzero bytes (countBytesInFilter, Columns/countBytesInFilter.cpp:32-124); with a
+ * null map: rows with f != 0 && !null (countBytesInFilterWithNull). */
+int tfg_count_mask(tfg_ctx *ctx, const uint8_t *mask, const uint8_t *nullmap, int64_t n,
+                   uint64_t *out_count_dev, uint64_t *out_count_host);
+/* Stable compaction of `ncols` fixed-width columns by one filter (ColumnVector<T>::filter ->
+ * filterImpl, Columns/ColumnVector.cpp:659-683, Columns/filterColumn.cpp:174-305: output order =
+ * input order).  widths[j] in {1,2,4,8,16}.  outs[j] must hold count values. */
+int tfg_filter(tfg_ctx *ctx, const uint8_t *mask, int64_t n, int ncols, const void *const *cols,
+               const int *widths, void *const *outs, uint64_t *out_count_dev, uint64_t *out_count_host);
+/* Fused FilterTransformAction::transform (DataStreams/FilterTransformAction.cpp:72-173) for the
+ * predicate `pred_col Op scalar`: the mask is never materialised. */
+int tfg_filter_cmp_const(tfg_ctx *ctx, int pred_type, const void *pred_col, const uint8_t *pred_nullmap, int op,
+                         int scalar_type, const void *scalar_host, int64_t n, int ncols, const void *const *cols,
+                         const int *widths, void *const *outs, uint64_t *out_count_dev, uint64_t *out_count_host);
+/* String column compaction (filterArraysImplGeneric, Columns/filterColumn.cpp:97-171):
+ * ColumnString layout = chars (each row ends with '\0') + UInt64 end offsets
+ * (Columns/ColumnString.h:50-54).  out_chars must hold the kept rows' bytes. */
+int tfg_filter_string(tfg_ctx *ctx, const uint8_t *mask, int64_t n, const uint8_t *chars, const uint64_t *offsets,
+                      uint8_t *out_chars, uint64_t *out_offsets, uint64_t *out_rows_host, uint64_t *out_bytes_host);
+
+/* ---------------------------------------------------------------- a22-a24 hash / partition */
+/* Seeds h[i] = 0xFFFFFFFF (WeakHash32::initial_hash = ~0u, Common/WeakHash.h:33). */
+int tfg_weak_hash_init(tfg_ctx *ctx, uint32_t *h, int64_t n);
+/* h[i] = CRC32-C(h[i], value_i) exactly like IColumn::updateWeakHash32 for fixed-width columns
+ * (Columns/ColumnVector.cpp:499-535, ColumnDecimal.cpp:658, Common/HashTable/Hash.h:70-145):
+ * integers are converted to UInt64 by C++ implicit conversion (signed types sign-extend),
+ * Decimal128 hashes its two 64-bit limbs low then high.  NULL rows keep the previous h
+ * (ColumnNullable.cpp:131-173).  Float columns are rejected (implementation-defined in C++). */
+int tfg_weak_hash_update(tfg_ctx *ctx, int type, const void *col, const uint8_t *nullmap, int64_t n, uint32_t *h);
+/* String keys (ColumnString::updateWeakHash32, Columns/ColumnString.cpp:1228-1327 with
+ * ::updateWeakHash32(bytes), Common/HashTable/Hash.h:148-214). */
+int tfg_weak_hash_update_string(tfg_ctx *ctx, const uint8_t *chars, const uint64_t *offsets, const uint8_t *nullmap,
+                                int64_t n, int collator, uint32_t *h);
+/* selector[i] = (UInt64(h[i]) * part_num) >> 32 (fillSelector, Flash/Mpp/HashBaseWriterHelper.cpp:46-62);
+ * with fine_grained_stream_count > 0: selector = part * S + h % S (fillSelectorForFineGrainedShuffle, :64-84). */
+int tfg_fill_selector(tfg_ctx *ctx, const uint32_t *h, int64_t n, uint32_t part_num,
+                      uint32_t fine_grained_stream_count, uint32_t *out_selector);
+/* Stable counting partition of rows by selector (the permutation behind IColumn::scatter,
+ * Columns/IColumn.h:655-721): out_perm lists row ids partition by partition, each partition
+ * in input row order; out_offsets[p] = first slot of partition p, out_offsets[P] = n.
+ * out_offsets is a DEVICE array of P+1 uint64; out_offsets_host (optional) receives a copy. */
+int tfg_partition(tfg_ctx *ctx, const uint32_t *selector, int64_t n, uint32_t num_parts, uint32_t *out_perm,
+                  uint64_t *out_offsets, uint64_t *out_offsets_host);
+/* out_j[r] = col_j[perm[r]] for r < n (gather); used for scatter after tfg_partition and to
+ * materialise join results.  perm entries of 0xFFFFFFFF (-1) write a zero / default value. */
+int tfg_gather(tfg_ctx *ctx, const uint32_t *perm, int64_t n, int ncols, const void *const *cols, const int *widths,
+               void *const *outs);
+/* One-call HashBaseWriterHelper::scatterColumns (HashBaseWriterHelper.cpp:144-172) for
+ * fixed-width key columns: weak hash over key_cols -> fillSelector(part_num) -> stable
+ * partition -> gather of all `ncols` columns into outs (partition-major).  */
+int tfg_hash_partition(tfg_ctx *ctx, int64_t n, int nkeys, const int *key_col_idx, int ncols, const int *types,
+                       const void *const *cols, const uint8_t *const *nullmaps, uint32_t part_num,
+                       void *const *outs, uint64_t *out_offsets, uint64_t *out_offsets_host);
+
+/* ---------------------------------------------------------------- a9-a17 aggregation */
+typedef struct tfg_agg tfg_agg;
+
+typedef struct tfg_agg_params {
+    /* log2 of the number of radix buckets rows are partitioned into before the LDS-table pass
+     * (the GPU analogue of TwoLevelHashTable's 256 buckets, Common/HashTable/TwoLevelHashTable.h:47-71).
+     * 0 = choose from expected_groups. */
+    int bucket_bits;
+    /* hint for the number of distinct keys (0 = unknown: 2^20 assumed). */
+    int64_t expected_groups;
+} tfg_agg_params;
+
+/* Aggregator with one fixed-width GROUP BY key (method key8..key64 / nullable, Interpreters/
+ * Aggregator.cpp:394-537) or no key (key_type = 0: a single group, without_key).
+ * arg_types[i] / arg_scales[i] describe the argument of agg i (ignored for COUNT_ALL). */
+int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds, const int *arg_types,
+                   const int *arg_scales, const tfg_agg_params *params, tfg_agg **out);
+int tfg_agg_destroy(tfg_agg *agg);
+/* Aggregator::executeOnBlock (Interpreters/Aggregator.cpp:1127-1246): folds n rows into the
+ * state.  `mask` (optional) is a UInt8 filter applied first (rows with 0 are skipped). */
+int tfg_agg_consume(tfg_agg *agg, const void *keys, const uint8_t *key_nullmap, const void *const *args,
+                    const uint8_t *const *arg_nullmaps, const uint8_t *mask, int64_t n);
+/* Fused Filter -> Aggregator: rows with pred_col Op scalar are aggregated (mask never built). */
+int tfg_agg_consume_filtered(tfg_agg *agg, int pred_type, const void *pred_col, const uint8_t *pred_nullmap, int op,
+                             int scalar_type, const void *scalar_host, const void *keys, const uint8_t *key_nullmap,
+                             const void *const *args, const uint8_t *const *arg_nullmaps, int64_t n);
+/* Merge partial states (mergeDataImpl / two-phase final agg, Aggregator.cpp:2338-2505):
+ * rows are (key, partial state) as produced by tfg_agg_result of the same agg signature. */
+int tfg_agg_consume_partial(tfg_agg *agg, const void *keys, const uint8_t *key_nullmap, const void *const *states,
+                            const uint8_t *const *state_nullmaps, int64_t n);
+int tfg_agg_merge(tfg_agg *dst, tfg_agg *src);
+/* Number of groups so far (syncs). */
+int tfg_agg_size(tfg_agg *agg, uint64_t *out_groups);
+/* convertToBlockImplFinal (Aggregator.cpp:1651-1780): writes every group.  out_keys: key type
+ * width per group; out_key_nullmap (optional, nullable keys); out_states[i]: result type
+ * width (8 B for Int64/UInt64/Float64 sums and counts, 16 B for Decimal sums);
+ * out_state_nullmaps[i] (optional): 1 when sum saw no non-NULL value (AggregateFunctionNull).
+ * Order is the table's (compare unordered, as the reference tests do). */
+int tfg_agg_result(tfg_agg *agg, void *out_keys, uint8_t *out_key_nullmap, void *const *out_states,
+                   uint8_t *const *out_state_nullmaps, uint64_t capacity, uint64_t *out_groups_host);
+/* Result type of agg i (tfg_type) and its width in bytes. */
+int tfg_agg_result_type(tfg_agg *agg, int i, int *out_type, int *out_width);
+
+/* ---------------------------------------------------------------- a18-a21 hash join */
+typedef struct tfg_join tfg_join;
+
+/* Join::insertFromBlock + finishOneBuild for one fixed-width key (Interpreters/Join.cpp:532-735,
+ * JoinPartition.cpp:584-728).  Rows with a NULL key are not inserted.  Build may be called
+ * repeatedly (blocks); build row ids continue across calls.  `expected_build_rows` sizes
+ * the partitioning (0 = size from the first block). */
+int tfg_join_create(tfg_ctx *ctx, int key_type, int64_t expected_build_rows, tfg_join **out);
+int tfg_join_build(tfg_join *join, const void *keys, const uint8_t *key_nullmap, int64_t n);
+int tfg_join_finalize(tfg_join *join);
+int tfg_join_destroy(tfg_join *join);
+/* Join::joinBlock (Join.cpp:1977 -> probeBlockImplTypeCase, JoinPartition.cpp:1465-1644):
+ * emits (probe row, build row) index pairs.  LEFT emits build = 0xFFFFFFFF for unmatched rows;
+ * SEMI/ANTI emit the probe row only (out_build_idx may be NULL).  If the result exceeds
+ * `capacity`, TFG_ERR_CAPACITY is returned and *out_count_host holds the needed size.
+ * Pair order: grouped by radix partition (compare unordered, like the reference's tests). */
+int tfg_join_probe(tfg_join *join, int kind, const void *keys, const uint8_t *key_nullmap, int64_t n,
+                   uint32_t *out_probe_idx, uint32_t *out_build_idx, uint64_t capacity, uint64_t *out_count_dev,
+                   uint64_t *out_count_host);
+/* Build-side statistics: rows inserted, distinct keys, partitions. */
+int tfg_join_stats(tfg_join *join, uint64_t *rows, uint64_t *partitions);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TIFLASH_AMD_H */

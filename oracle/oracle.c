@@ -1,0 +1,838 @@
+/*
+ * oracle.c — CPU restatement of the reference's hot path (xfworld/tiflash, dbms/src/...).
+ *
+ * TEST INFRASTRUCTURE ONLY (checker + timed CPU baseline).  Never linked by the product.
+ * Every function cites the reference lines it restates; paths are relative to
+ * /root/reference/dbms/src.  Written from scratch (the reference cannot be compiled here:
+ * SURVEY.md §8c); pinned by the hardware CRC32-C instruction and the reference gtests'
+ * known answers (tests/golden/).
+ */
+#define _GNU_SOURCE
+#include "oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef __SSE4_2__
+#include <nmmintrin.h>
+#endif
+
+#include "../include/tiflash_amd.h"
+
+/* ------------------------------------------------------------------ CRC32-C */
+/* intHashCRC32(x, seed) = _mm_crc32_u64(seed, x)  (Common/HashTable/Hash.h:70-95). */
+int orc_has_hw_crc(void)
+{
+#ifdef __SSE4_2__
+    return 1;
+#else
+    return 0;
+#endif
+}
+
+uint32_t orc_crc32c_u64_sw(uint32_t crc, uint64_t x)
+{
+    /* crc32q semantics: reflected CRC-32C (poly 0x1EDC6F41, reversed 0x82F63B78), no init/final
+     * inversion inside the instruction. */
+    for (int byte = 0; byte < 8; ++byte) {
+        crc ^= (uint32_t)(x & 0xFF);
+        x >>= 8;
+        for (int b = 0; b < 8; ++b)
+            crc = (crc >> 1) ^ (0x82F63B78u & (0u - (crc & 1u)));
+    }
+    return crc;
+}
+
+uint32_t orc_crc32c_u64(uint32_t crc, uint64_t x)
+{
+#ifdef __SSE4_2__
+    return (uint32_t)_mm_crc32_u64(crc, x);
+#else
+    return orc_crc32c_u64_sw(crc, x);
+#endif
+}
+
+static inline uint32_t int_hash_crc32(uint64_t x) { return orc_crc32c_u64(0xFFFFFFFFu, x); }
+
+/* ::updateWeakHash32(const UInt8 * pos, size_t size, UInt32) (Common/HashTable/Hash.h:148-214). */
+uint32_t orc_update_weak_hash32_bytes(const uint8_t *pos, size_t size, uint32_t h)
+{
+    if (size < 8) {
+        uint64_t value = 0;
+        memcpy(&value, pos, size);
+        ((unsigned char *)&value)[7] = (unsigned char)size;
+        return orc_crc32c_u64(h, value);
+    }
+    const uint8_t *end = pos + size;
+    while (pos + 8 <= end) {
+        uint64_t word;
+        memcpy(&word, pos, 8);
+        h = orc_crc32c_u64(h, word);
+        pos += 8;
+    }
+    if (pos < end) {
+        uint8_t tail = (uint8_t)(end - pos);
+        uint64_t word;
+        memcpy(&word, end - 8, 8);
+        word &= (~(uint64_t)0) << (8 * (8 - tail));
+        word |= tail;
+        h = orc_crc32c_u64(h, word);
+    }
+    return h;
+}
+
+/* ------------------------------------------------------------------ value access */
+static size_t type_width(int t)
+{
+    switch (t) {
+    case TFG_INT8: case TFG_UINT8: return 1;
+    case TFG_INT16: case TFG_UINT16: return 2;
+    case TFG_INT32: case TFG_UINT32: case TFG_FLOAT32: case TFG_DECIMAL32: return 4;
+    case TFG_INT64: case TFG_UINT64: case TFG_FLOAT64: case TFG_DECIMAL64: return 8;
+    case TFG_DECIMAL128: return 16;
+    default: return 0;
+    }
+}
+static int is_float(int t) { return t == TFG_FLOAT32 || t == TFG_FLOAT64; }
+static int is_unsigned(int t) { return t == TFG_UINT8 || t == TFG_UINT16 || t == TFG_UINT32 || t == TFG_UINT64; }
+
+static int64_t load_s(int t, const void *p, size_t i)
+{
+    switch (t) {
+    case TFG_INT8: return ((const int8_t *)p)[i];
+    case TFG_INT16: return ((const int16_t *)p)[i];
+    case TFG_INT32: case TFG_DECIMAL32: return ((const int32_t *)p)[i];
+    case TFG_INT64: case TFG_DECIMAL64: return ((const int64_t *)p)[i];
+    case TFG_UINT8: return ((const uint8_t *)p)[i];
+    case TFG_UINT16: return ((const uint16_t *)p)[i];
+    case TFG_UINT32: return ((const uint32_t *)p)[i];
+    case TFG_UINT64: return (int64_t)((const uint64_t *)p)[i];
+    default: return 0;
+    }
+}
+static double load_f(int t, const void *p, size_t i)
+{
+    return t == TFG_FLOAT32 ? (double)((const float *)p)[i] : ((const double *)p)[i];
+}
+static __int128 load_i128(int t, const void *p, size_t i)
+{
+    if (t == TFG_DECIMAL128) {
+        __int128 v;
+        memcpy(&v, (const char *)p + 16 * i, 16);
+        return v;
+    }
+    if (t == TFG_UINT64) return (__int128)((const uint64_t *)p)[i];
+    return (__int128)load_s(t, p, i);
+}
+/* Raw bits of a key zero-extended to UInt64 (HashMethodOneNumber reads the raw FieldType,
+ * Common/ColumnsHashing.h:43-90; key8..key64 methods). */
+static uint64_t load_key_bits(int t, const void *p, size_t i)
+{
+    switch (type_width(t)) {
+    case 1: return ((const uint8_t *)p)[i];
+    case 2: return ((const uint16_t *)p)[i];
+    case 4: return ((const uint32_t *)p)[i];
+    default: return ((const uint64_t *)p)[i];
+    }
+}
+
+/* ------------------------------------------------------------------ weak hash / partition */
+/* ColumnVector<T>::updateWeakHash32Impl (Columns/ColumnVector.cpp:499-535): h = crc(h, UInt64(v));
+ * ColumnDecimal (ColumnDecimal.cpp:658 -> wideIntHashCRC32, Hash.h:97-145);
+ * ColumnNullable keeps the old hash for NULL rows (ColumnNullable.cpp:131-173). */
+void orc_weak_hash_update(int type, const void *col, const uint8_t *nullmap, size_t n, uint32_t *h)
+{
+    for (size_t i = 0; i < n; ++i) {
+        if (nullmap && nullmap[i]) continue;
+        if (type == TFG_DECIMAL128) {
+            uint64_t limb[2];
+            memcpy(limb, (const char *)col + 16 * i, 16);
+            uint32_t x = orc_crc32c_u64(h[i], limb[0]);
+            h[i] = orc_crc32c_u64(x, limb[1]);
+        } else {
+            /* implicit conversion to UInt64: signed types sign-extend, unsigned zero-extend */
+            uint64_t v = is_unsigned(type) ? (uint64_t)load_s(type, col, i) : (uint64_t)load_s(type, col, i);
+            h[i] = orc_crc32c_u64(h[i], v);
+        }
+    }
+}
+
+/* ColumnString::updateWeakHash32 (Columns/ColumnString.cpp:1228-1327): hashes size-1 bytes (the
+ * trailing '\0' excluded) after the collator's sort key; BIN padding collators right-trim ' '
+ * (TiDB/Collation/CollatorCompare.h:49-95). */
+void orc_weak_hash_update_string(const uint8_t *chars, const uint64_t *offsets, const uint8_t *nullmap, size_t n,
+                                 int collator, uint32_t *h)
+{
+    for (size_t i = 0; i < n; ++i) {
+        if (nullmap && nullmap[i]) continue;
+        uint64_t prev = i ? offsets[i - 1] : 0;
+        size_t len = (size_t)(offsets[i] - prev - 1);
+        const uint8_t *s = chars + prev;
+        if (collator == TFG_COLLATOR_BIN_PADDING)
+            while (len > 0 && s[len - 1] == ' ') --len;
+        h[i] = orc_update_weak_hash32_bytes(s, len, h[i]);
+    }
+}
+
+/* fillSelector / fillSelectorForFineGrainedShuffle (Flash/Mpp/HashBaseWriterHelper.cpp:46-84). */
+void orc_fill_selector(const uint32_t *h, size_t n, uint32_t part_num, uint32_t fgs, uint32_t *sel)
+{
+    for (size_t i = 0; i < n; ++i) {
+        uint64_t s = h[i];
+        s *= part_num;
+        s >>= 32;
+        if (fgs) s = s * fgs + h[i] % fgs;
+        sel[i] = (uint32_t)s;
+    }
+}
+
+/* Stable partition behind IColumn::scatterImpl (Columns/IColumn.h:655-721): each destination
+ * receives rows in input order. */
+void orc_partition(const uint32_t *sel, size_t n, uint32_t parts, uint32_t *perm, uint64_t *offsets)
+{
+    memset(offsets, 0, sizeof(uint64_t) * (parts + 1));
+    for (size_t i = 0; i < n; ++i) offsets[sel[i] + 1]++;
+    for (uint32_t p = 0; p < parts; ++p) offsets[p + 1] += offsets[p];
+    uint64_t *cur = (uint64_t *)malloc(sizeof(uint64_t) * (parts ? parts : 1));
+    memcpy(cur, offsets, sizeof(uint64_t) * parts);
+    for (size_t i = 0; i < n; ++i) perm[cur[sel[i]]++] = (uint32_t)i;
+    free(cur);
+}
+
+/* ------------------------------------------------------------------ comparison */
+/* Exact comparison of two numbers of different classes; returns -1/0/1, or 2 if unordered (NaN).
+ * Restates accurate::lessOp / equalsOp (Core/AccurateComparison.h:33-159): same-signedness ints
+ * compare natively, mixed signedness exactly, int vs float exactly (DecomposedFloat for >32-bit
+ * ints, double cast otherwise — both exact), anything vs NaN is false. */
+typedef struct { int cls; int64_t s; uint64_t u; double d; } num; /* cls 0=signed 1=unsigned 2=float */
+
+static num load_num(int t, const void *p, size_t i)
+{
+    num r = {0, 0, 0, 0.0};
+    if (is_float(t)) { r.cls = 2; r.d = load_f(t, p, i); }
+    else if (is_unsigned(t)) { r.cls = 1; r.u = (uint64_t)load_s(t, p, i); }
+    else { r.cls = 0; r.s = load_s(t, p, i); }
+    return r;
+}
+
+static int cmp_s_d(int64_t a, double d)
+{
+    if (d >= 9223372036854775808.0) return -1;
+    if (d < -9223372036854775808.0) return 1;
+    int64_t t = (int64_t)d;
+    if (a < t) return -1;
+    if (a > t) return 1;
+    double frac = d - (double)t;
+    return frac > 0 ? -1 : (frac < 0 ? 1 : 0);
+}
+static int cmp_u_d(uint64_t a, double d)
+{
+    if (d >= 18446744073709551616.0) return -1;
+    if (d < 0) return 1;
+    uint64_t t = (uint64_t)d;
+    if (a < t) return -1;
+    if (a > t) return 1;
+    double frac = d - (double)t;
+    return frac > 0 ? -1 : 0;
+}
+static int cmp_num(num a, num b)
+{
+    if (a.cls == 2 && isnan(a.d)) return 2;
+    if (b.cls == 2 && isnan(b.d)) return 2;
+    if (a.cls == 2 && b.cls == 2) return a.d < b.d ? -1 : (a.d > b.d ? 1 : 0);
+    if (a.cls == 0 && b.cls == 0) return a.s < b.s ? -1 : (a.s > b.s ? 1 : 0);
+    if (a.cls == 1 && b.cls == 1) return a.u < b.u ? -1 : (a.u > b.u ? 1 : 0);
+    if (a.cls == 0 && b.cls == 1) return a.s < 0 ? -1 : ((uint64_t)a.s < b.u ? -1 : ((uint64_t)a.s > b.u ? 1 : 0));
+    if (a.cls == 1 && b.cls == 0) return -cmp_num(b, a);
+    if (a.cls == 0 && b.cls == 2) return cmp_s_d(a.s, b.d);
+    if (a.cls == 1 && b.cls == 2) return cmp_u_d(a.u, b.d);
+    /* a float, b int */
+    return -cmp_num(b, a);
+}
+
+static uint8_t apply_op(int op, int c)
+{
+    if (c == 2) return op == TFG_NE; /* NaN: only notEquals is true (notEqualsOp = !equalsOp) */
+    switch (op) {
+    case TFG_EQ: return c == 0;
+    case TFG_NE: return c != 0;
+    case TFG_LT: return c < 0;
+    case TFG_LE: return c <= 0;
+    case TFG_GT: return c > 0;
+    case TFG_GE: return c >= 0;
+    }
+    return 0;
+}
+
+/* NumComparisonImpl::vectorVector / vectorConstant / constantVector
+ * (Functions/FunctionsComparison.h:74-122).  NULL rows -> 0 (FilterDescription folding). */
+void orc_cmp(int a_type, const void *a, int a_const, int op, int b_type, const void *b, int b_const,
+             const uint8_t *a_null, const uint8_t *b_null, size_t n, uint8_t *out)
+{
+    for (size_t i = 0; i < n; ++i) {
+        if ((a_null && a_null[i]) || (b_null && b_null[i])) { out[i] = 0; continue; }
+        num x = load_num(a_type, a, a_const ? 0 : i);
+        num y = load_num(b_type, b, b_const ? 0 : i);
+        out[i] = apply_op(op, cmp_num(x, y));
+    }
+}
+
+/* countBytesInFilter / countBytesInFilterWithNull (Columns/countBytesInFilter.cpp:32-124). */
+size_t orc_count_bytes_in_filter(const uint8_t *f, const uint8_t *nullmap, size_t n)
+{
+    size_t c = 0;
+    for (size_t i = 0; i < n; ++i) c += (f[i] != 0) && !(nullmap && nullmap[i]);
+    return c;
+}
+
+/* filterImpl (Columns/filterColumn.cpp:174-305): per 64 rows ToBits64 -> prefix / suffix run
+ * or pop-bit loop; scalar tail.  Stable. */
+size_t orc_filter(int width, const void *col, const uint8_t *f, size_t n, void *out)
+{
+    const char *src = (const char *)col;
+    char *dst = (char *)out;
+    size_t k = 0, i = 0;
+    for (; i + 64 <= n; i += 64) {
+        uint64_t mask = 0;
+        for (int b = 0; b < 64; ++b) mask |= (uint64_t)(f[i + b] != 0) << b; /* ToBits64 */
+        while (mask) {
+            int idx = __builtin_ctzll(mask);
+            memcpy(dst + (size_t)width * k++, src + (size_t)width * (i + idx), (size_t)width);
+            mask &= mask - 1;
+        }
+    }
+    for (; i < n; ++i)
+        if (f[i]) memcpy(dst + (size_t)width * k++, src + (size_t)width * i, (size_t)width);
+    return k;
+}
+
+/* filterArraysImplGeneric for ColumnString (Columns/filterColumn.cpp:97-171). */
+size_t orc_filter_string(const uint8_t *chars, const uint64_t *offsets, const uint8_t *f, size_t n,
+                         uint8_t *out_chars, uint64_t *out_offsets, size_t *out_bytes)
+{
+    size_t rows = 0, bytes = 0;
+    for (size_t i = 0; i < n; ++i) {
+        if (!f[i]) continue;
+        uint64_t prev = i ? offsets[i - 1] : 0;
+        size_t len = (size_t)(offsets[i] - prev);
+        memcpy(out_chars + bytes, chars + prev, len);
+        bytes += len;
+        out_offsets[rows++] = bytes;
+    }
+    *out_bytes = bytes;
+    return rows;
+}
+
+/* ------------------------------------------------------------------ arithmetic */
+static __int128 pow10_i128(int e)
+{
+    __int128 r = 1;
+    while (e-- > 0) r *= 10;
+    return r;
+}
+static int is_decimal(int t) { return t == TFG_DECIMAL32 || t == TFG_DECIMAL64 || t == TFG_DECIMAL128; }
+
+/* BinaryOperationImplBase / DecimalBinaryOperation (Functions/FunctionBinaryArithmetic.h:72-215,
+ * 231-500): for +/- decimals are scaled to the result scale (applyScaled); * multiplies raw
+ * values (result scale = sa + sb).  Integer ops wrap (two's complement). */
+int orc_arith(int op, int a_type, const void *a, int a_const, int a_scale, int b_type, const void *b, int b_const,
+              int b_scale, int res_type, int res_scale, size_t n, void *out)
+{
+    int dec = is_decimal(res_type);
+    for (size_t i = 0; i < n; ++i) {
+        size_t ia = a_const ? 0 : i, ib = b_const ? 0 : i;
+        if (res_type == TFG_FLOAT64 || res_type == TFG_FLOAT32) {
+            double x = is_float(a_type) ? load_f(a_type, a, ia) : (double)load_s(a_type, a, ia);
+            double y = is_float(b_type) ? load_f(b_type, b, ib) : (double)load_s(b_type, b, ib);
+            double r = op == TFG_PLUS ? x + y : op == TFG_MINUS ? x - y : x * y;
+            if (res_type == TFG_FLOAT64) ((double *)out)[i] = r;
+            else ((float *)out)[i] = (float)r;
+            continue;
+        }
+        __int128 x = load_i128(a_type, a, ia), y = load_i128(b_type, b, ib), r;
+        if (dec && op != TFG_MULTIPLY) {
+            x *= pow10_i128(res_scale - (is_decimal(a_type) ? a_scale : 0));
+            y *= pow10_i128(res_scale - (is_decimal(b_type) ? b_scale : 0));
+        }
+        if (op == TFG_PLUS) r = (__int128)((unsigned __int128)x + (unsigned __int128)y);
+        else if (op == TFG_MINUS) r = (__int128)((unsigned __int128)x - (unsigned __int128)y);
+        else r = (__int128)((unsigned __int128)x * (unsigned __int128)y);
+        switch (type_width(res_type)) {
+        case 1: ((int8_t *)out)[i] = (int8_t)r; break;
+        case 2: ((int16_t *)out)[i] = (int16_t)r; break;
+        case 4: ((int32_t *)out)[i] = (int32_t)r; break;
+        case 8: ((int64_t *)out)[i] = (int64_t)r; break;
+        case 16: memcpy((char *)out + 16 * i, &r, 16); break;
+        default: return -1;
+        }
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------ HashMap (key64) */
+/* HashTable<UInt64, ..., HashCRC32<UInt64>, HashTableGrower<8>> restated:
+ * linear probing place = hash & mask, next = +1 (Common/HashTable/HashTable.h:437, 254-296);
+ * resize when size > maxFill = buf/2 (overflow), growing by 2 degrees below 2^23, then 1;
+ * key 0 lives outside the buffer (ZeroValueStorage, :325-360). */
+typedef struct {
+    uint64_t *keys;
+    int64_t *vals; /* mapped value: group / list index, -1 = empty */
+    int degree;
+    size_t size;
+    int has_zero;
+    int64_t zero_val;
+} hmap;
+
+static void hmap_init(hmap *m)
+{
+    m->degree = 8;
+    size_t cap = (size_t)1 << m->degree;
+    m->keys = (uint64_t *)calloc(cap, sizeof(uint64_t));
+    m->vals = (int64_t *)malloc(cap * sizeof(int64_t));
+    for (size_t i = 0; i < cap; ++i) m->vals[i] = -1;
+    m->size = 0;
+    m->has_zero = 0;
+    m->zero_val = -1;
+}
+static void hmap_free(hmap *m)
+{
+    free(m->keys);
+    free(m->vals);
+}
+static void hmap_resize(hmap *m)
+{
+    size_t old_cap = (size_t)1 << m->degree;
+    uint64_t *ok = m->keys;
+    int64_t *ov = m->vals;
+    m->degree += m->degree >= 23 ? 1 : 2;
+    size_t cap = (size_t)1 << m->degree, mask = cap - 1;
+    m->keys = (uint64_t *)calloc(cap, sizeof(uint64_t));
+    m->vals = (int64_t *)malloc(cap * sizeof(int64_t));
+    for (size_t i = 0; i < cap; ++i) m->vals[i] = -1;
+    for (size_t i = 0; i < old_cap; ++i) {
+        if (ov[i] < 0) continue;
+        size_t p = int_hash_crc32(ok[i]) & mask;
+        while (m->vals[p] >= 0) p = (p + 1) & mask;
+        m->keys[p] = ok[i];
+        m->vals[p] = ov[i];
+    }
+    free(ok);
+    free(ov);
+}
+/* emplace: returns pointer to mapped value; *inserted set when new. */
+static int64_t *hmap_emplace(hmap *m, uint64_t key, int *inserted)
+{
+    *inserted = 0;
+    if (key == 0) { /* emplaceIfZero */
+        if (!m->has_zero) { m->has_zero = 1; *inserted = 1; }
+        return &m->zero_val;
+    }
+    size_t mask = ((size_t)1 << m->degree) - 1;
+    size_t p = int_hash_crc32(key) & mask;
+    while (m->vals[p] >= 0 && m->keys[p] != key) p = (p + 1) & mask;
+    if (m->vals[p] >= 0) return &m->vals[p];
+    m->keys[p] = key;
+    m->vals[p] = 0;
+    m->size++;
+    *inserted = 1;
+    if (m->size > ((size_t)1 << (m->degree - 1))) { /* grower.overflow -> resize */
+        hmap_resize(m);
+        mask = ((size_t)1 << m->degree) - 1;
+        p = int_hash_crc32(key) & mask;
+        while (m->keys[p] != key || m->vals[p] < 0) p = (p + 1) & mask;
+    }
+    return &m->vals[p];
+}
+static const int64_t *hmap_find(const hmap *m, uint64_t key)
+{
+    if (key == 0) return m->has_zero ? &m->zero_val : NULL;
+    size_t mask = ((size_t)1 << m->degree) - 1;
+    size_t p = int_hash_crc32(key) & mask;
+    while (m->vals[p] >= 0) {
+        if (m->keys[p] == key) return &m->vals[p];
+        p = (p + 1) & mask;
+    }
+    return NULL;
+}
+
+/* ------------------------------------------------------------------ Aggregator */
+#define ORC_MAX_AGGS 8
+struct orc_agg {
+    int key_type; /* 0 = without_key */
+    int n_aggs;
+    int kinds[ORC_MAX_AGGS];
+    int arg_types[ORC_MAX_AGGS];
+    hmap map;
+    size_t n_groups, cap_groups;
+    uint64_t *gkeys;
+    uint8_t *gkey_null;
+    __int128 *acc_i[ORC_MAX_AGGS]; /* integer / decimal accumulators (wrap per result width) */
+    double *acc_f[ORC_MAX_AGGS];
+    uint64_t *cnt[ORC_MAX_AGGS]; /* non-NULL rows seen */
+    int64_t null_group;           /* group index of the NULL key, -1 */
+};
+
+orc_agg *orc_agg_create(int key_type, int n_aggs, const int *kinds, const int *arg_types)
+{
+    if (n_aggs > ORC_MAX_AGGS) return NULL;
+    orc_agg *a = (orc_agg *)calloc(1, sizeof(orc_agg));
+    a->key_type = key_type;
+    a->n_aggs = n_aggs;
+    for (int i = 0; i < n_aggs; ++i) {
+        a->kinds[i] = kinds[i];
+        a->arg_types[i] = arg_types ? arg_types[i] : 0;
+    }
+    hmap_init(&a->map);
+    a->null_group = -1;
+    return a;
+}
+
+void orc_agg_destroy(orc_agg *a)
+{
+    if (!a) return;
+    hmap_free(&a->map);
+    free(a->gkeys);
+    free(a->gkey_null);
+    for (int i = 0; i < a->n_aggs; ++i) {
+        free(a->acc_i[i]);
+        free(a->acc_f[i]);
+        free(a->cnt[i]);
+    }
+    free(a);
+}
+
+static int64_t agg_new_group(orc_agg *a, uint64_t key, uint8_t is_null)
+{
+    if (a->n_groups == a->cap_groups) {
+        size_t nc = a->cap_groups ? a->cap_groups * 2 : 1024;
+        a->gkeys = (uint64_t *)realloc(a->gkeys, nc * sizeof(uint64_t));
+        a->gkey_null = (uint8_t *)realloc(a->gkey_null, nc);
+        for (int i = 0; i < a->n_aggs; ++i) {
+            a->acc_i[i] = (__int128 *)realloc(a->acc_i[i], nc * sizeof(__int128));
+            a->acc_f[i] = (double *)realloc(a->acc_f[i], nc * sizeof(double));
+            a->cnt[i] = (uint64_t *)realloc(a->cnt[i], nc * sizeof(uint64_t));
+        }
+        a->cap_groups = nc;
+    }
+    size_t g = a->n_groups++;
+    a->gkeys[g] = key;
+    a->gkey_null[g] = is_null;
+    for (int i = 0; i < a->n_aggs; ++i) { /* createAggregateStates: zero-initialised sums */
+        a->acc_i[i][g] = 0;
+        a->acc_f[i][g] = 0.0;
+        a->cnt[i][g] = 0;
+    }
+    return (int64_t)g;
+}
+
+static int64_t agg_lookup(orc_agg *a, uint64_t key, int is_null)
+{
+    if (a->key_type == 0) { /* without_key: one group */
+        if (a->n_groups == 0) agg_new_group(a, 0, 0);
+        return 0;
+    }
+    if (is_null) { /* nullable key: NULL is its own group */
+        if (a->null_group < 0) a->null_group = agg_new_group(a, 0, 1);
+        return a->null_group;
+    }
+    int ins;
+    int64_t *slot = hmap_emplace(&a->map, key, &ins);
+    if (ins) *slot = agg_new_group(a, key, 0);
+    return *slot;
+}
+
+/* Aggregator::executeOnBlock -> handleOneBatch (Interpreters/Aggregator.cpp:852-1024):
+ * emplace key, then IAggregateFunction::addBatch in row order (IAggregateFunction.h:242-266);
+ * AggregateFunctionSumData::add (AggregateFunctionSum.h:64-80); count (AggregateFunctionCount.h:46);
+ * Nullable arguments skip NULL rows (AggregateFunctionNull.h:373). */
+void orc_agg_consume(orc_agg *a, const void *keys, const uint8_t *key_null, const void *const *args,
+                     const uint8_t *const *arg_nulls, const uint8_t *mask, size_t n)
+{
+    for (size_t r = 0; r < n; ++r) {
+        if (mask && !mask[r]) continue;
+        int kn = key_null && key_null[r];
+        uint64_t key = (a->key_type && !kn) ? load_key_bits(a->key_type, keys, r) : 0;
+        int64_t g = agg_lookup(a, key, kn);
+        for (int i = 0; i < a->n_aggs; ++i) {
+            if (a->kinds[i] == TFG_AGG_COUNT_ALL) { a->cnt[i][g]++; continue; }
+            if (arg_nulls && arg_nulls[i] && arg_nulls[i][r]) continue;
+            a->cnt[i][g]++;
+            if (a->kinds[i] == TFG_AGG_COUNT) continue;
+            int t = a->arg_types[i];
+            if (is_float(t)) a->acc_f[i][g] += load_f(t, args[i], r);
+            else a->acc_i[i][g] = (__int128)((unsigned __int128)a->acc_i[i][g] + (unsigned __int128)load_i128(t, args[i], r));
+        }
+    }
+}
+
+/* mergeDataImpl (Aggregator.cpp:2338-2363): add src states into dst, src groups in src order. */
+void orc_agg_merge(orc_agg *dst, const orc_agg *src)
+{
+    for (size_t g = 0; g < src->n_groups; ++g) {
+        int64_t d = agg_lookup(dst, src->gkeys[g], src->gkey_null[g]);
+        for (int i = 0; i < dst->n_aggs; ++i) {
+            dst->cnt[i][d] += src->cnt[i][g];
+            dst->acc_f[i][d] += src->acc_f[i][g];
+            dst->acc_i[i][d] = (__int128)((unsigned __int128)dst->acc_i[i][d] + (unsigned __int128)src->acc_i[i][g]);
+        }
+    }
+}
+
+size_t orc_agg_size(const orc_agg *a) { return a->n_groups; }
+
+static int sum_result_width(int arg_type)
+{
+    return (arg_type == TFG_DECIMAL32 || arg_type == TFG_DECIMAL64 || arg_type == TFG_DECIMAL128) ? 16 : 8;
+}
+
+/* insertAggregatesIntoColumns (Aggregator.cpp:1651-1780). Order: group creation order. */
+void orc_agg_result(const orc_agg *a, uint64_t *out_keys, uint8_t *out_key_null, void *const *out_states,
+                    uint8_t *const *out_state_null)
+{
+    for (size_t g = 0; g < a->n_groups; ++g) {
+        if (out_keys) out_keys[g] = a->gkeys[g];
+        if (out_key_null) out_key_null[g] = a->gkey_null[g];
+        for (int i = 0; i < a->n_aggs; ++i) {
+            if (out_state_null && out_state_null[i]) out_state_null[i][g] = a->cnt[i][g] == 0;
+            if (!out_states || !out_states[i]) continue;
+            if (a->kinds[i] != TFG_AGG_SUM) { ((uint64_t *)out_states[i])[g] = a->cnt[i][g]; continue; }
+            int t = a->arg_types[i];
+            if (is_float(t)) ((double *)out_states[i])[g] = a->acc_f[i][g];
+            else if (sum_result_width(t) == 16) memcpy((char *)out_states[i] + 16 * g, &a->acc_i[i][g], 16);
+            else ((int64_t *)out_states[i])[g] = (int64_t)a->acc_i[i][g];
+        }
+    }
+}
+
+/* ------------------------------------------------------------------ Join (hash join v1) */
+/* MapsAll = HashMap<UInt64, RowRefList, HashCRC32<UInt64>> (Interpreters/JoinHashMap.h:175-188).
+ * Inserter<All>::insert (JoinPartition.cpp:494-524): the first row of a key lives in the cell; every
+ * later row is inserted SECOND in the list (insertRowToList, :39-60), so iteration order is
+ * first, then newest ... oldest. */
+struct orc_join {
+    int key_type;
+    hmap map; /* key -> list id */
+    size_t n_lists, cap_lists;
+    int64_t *first, *after; /* per list: head row, most recent non-head row (-1) */
+    size_t n_rows, cap_rows;
+    int64_t *next; /* per build row: next row in list (-1) */
+};
+
+orc_join *orc_join_create(int key_type)
+{
+    orc_join *j = (orc_join *)calloc(1, sizeof(orc_join));
+    j->key_type = key_type;
+    hmap_init(&j->map);
+    return j;
+}
+
+void orc_join_destroy(orc_join *j)
+{
+    if (!j) return;
+    hmap_free(&j->map);
+    free(j->first);
+    free(j->after);
+    free(j->next);
+    free(j);
+}
+
+/* insertBlockIntoMapsTypeCase (JoinPartition.cpp:584-728); NULL keys are not inserted
+ * (extractNestedColumnsAndNullMap, Join.cpp:686). Row ids continue across calls. */
+void orc_join_build(orc_join *j, const void *keys, const uint8_t *key_null, size_t n)
+{
+    if (j->n_rows + n > j->cap_rows) {
+        size_t nc = (j->n_rows + n) * 2;
+        j->next = (int64_t *)realloc(j->next, nc * sizeof(int64_t));
+        j->cap_rows = nc;
+    }
+    for (size_t r = 0; r < n; ++r) {
+        int64_t row = (int64_t)(j->n_rows + r);
+        j->next[row] = -1;
+        if (key_null && key_null[r]) continue;
+        uint64_t key = load_key_bits(j->key_type, keys, r);
+        int ins;
+        int64_t *slot = hmap_emplace(&j->map, key, &ins);
+        if (ins) {
+            if (j->n_lists == j->cap_lists) {
+                size_t nc = j->cap_lists ? j->cap_lists * 2 : 1024;
+                j->first = (int64_t *)realloc(j->first, nc * sizeof(int64_t));
+                j->after = (int64_t *)realloc(j->after, nc * sizeof(int64_t));
+                j->cap_lists = nc;
+            }
+            *slot = (int64_t)j->n_lists;
+            j->first[j->n_lists] = row;
+            j->after[j->n_lists] = -1;
+            j->n_lists++;
+        } else {
+            j->next[row] = j->after[*slot];
+            j->after[*slot] = row;
+        }
+    }
+    j->n_rows += n;
+}
+
+/* probeBlockImplTypeCase + Adder<KIND, All> (JoinPartition.cpp:1290-1378, 1465-1644): probe rows in
+ * order; found -> every row of the list; not found -> inner: nothing, left: one default row
+ * (build index 0xFFFFFFFF); semi: probe row once if found; anti: probe row if not found. */
+size_t orc_join_probe(const orc_join *j, int kind, const void *keys, const uint8_t *key_null, size_t n,
+                      uint32_t *out_probe, uint32_t *out_build, size_t capacity)
+{
+    size_t k = 0;
+#define EMIT(p, b)                                                        \
+    do {                                                                  \
+        if (k < capacity) {                                               \
+            if (out_probe) out_probe[k] = (uint32_t)(p);                  \
+            if (out_build) out_build[k] = (uint32_t)(b);                  \
+        }                                                                 \
+        ++k;                                                              \
+    } while (0)
+    for (size_t r = 0; r < n; ++r) {
+        const int64_t *slot = NULL;
+        if (!(key_null && key_null[r])) slot = hmap_find(&j->map, load_key_bits(j->key_type, keys, r));
+        if (!slot) {
+            if (kind == TFG_JOIN_LEFT) EMIT(r, 0xFFFFFFFFu);
+            else if (kind == TFG_JOIN_ANTI) EMIT(r, 0xFFFFFFFFu);
+            continue;
+        }
+        if (kind == TFG_JOIN_ANTI) continue;
+        if (kind == TFG_JOIN_SEMI) { EMIT(r, j->first[*slot]); continue; }
+        EMIT(r, j->first[*slot]);
+        for (int64_t b = j->after[*slot]; b >= 0; b = j->next[b]) EMIT(r, b);
+    }
+#undef EMIT
+    return k;
+}
+
+/* ------------------------------------------------------------------ CPU baseline legs */
+typedef struct {
+    const int64_t *f, *k;
+    const double *v;
+    int64_t threshold;
+    size_t begin, end, block_rows;
+    orc_agg *agg;
+} fa_task;
+
+/* One source stream of the pipeline: per Block of block_rows (max_block_size, Core/Defines.h:65):
+ * FilterTransformAction::transform = compare -> countBytesInFilter -> filter each column
+ * (DataStreams/FilterTransformAction.cpp:72-173), then Aggregator::executeOnBlock. */
+static void *fa_worker(void *arg)
+{
+    fa_task *t = (fa_task *)arg;
+    size_t B = t->block_rows;
+    uint8_t *mask = (uint8_t *)malloc(B);
+    int64_t *fk = (int64_t *)malloc(B * 8);
+    double *fv = (double *)malloc(B * 8);
+    int64_t thr = t->threshold;
+    for (size_t s = t->begin; s < t->end; s += B) {
+        size_t m = t->end - s < B ? t->end - s : B;
+        orc_cmp(TFG_INT64, t->f + s, 0, TFG_LT, TFG_INT64, &thr, 1, NULL, NULL, m, mask);
+        size_t cnt = orc_count_bytes_in_filter(mask, NULL, m);
+        if (cnt == 0) continue;
+        const void *args[1];
+        if (cnt == m) {
+            args[0] = t->v + s;
+            orc_agg_consume(t->agg, t->k + s, NULL, args, NULL, NULL, m);
+        } else {
+            orc_filter(8, t->k + s, mask, m, fk);
+            orc_filter(8, t->v + s, mask, m, fv);
+            args[0] = fv;
+            orc_agg_consume(t->agg, fk, NULL, args, NULL, NULL, cnt);
+        }
+    }
+    free(mask);
+    free(fk);
+    free(fv);
+    return NULL;
+}
+
+size_t orc_bench_filter_agg(const int64_t *f, int64_t threshold, const int64_t *k, const double *v, size_t n,
+                            int nthreads, size_t block_rows, double *checksum)
+{
+    if (nthreads < 1) nthreads = 1;
+    int kinds[2] = {TFG_AGG_SUM, TFG_AGG_COUNT_ALL};
+    int types[2] = {TFG_FLOAT64, 0};
+    fa_task *tasks = (fa_task *)calloc((size_t)nthreads, sizeof(fa_task));
+    pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+    size_t per = (n + (size_t)nthreads - 1) / (size_t)nthreads;
+    for (int i = 0; i < nthreads; ++i) {
+        tasks[i].f = f;
+        tasks[i].k = k;
+        tasks[i].v = v;
+        tasks[i].threshold = threshold;
+        tasks[i].begin = per * (size_t)i < n ? per * (size_t)i : n;
+        tasks[i].end = per * (size_t)(i + 1) < n ? per * (size_t)(i + 1) : n;
+        tasks[i].block_rows = block_rows;
+        tasks[i].agg = orc_agg_create(TFG_INT64, 2, kinds, types);
+        pthread_create(&th[i], NULL, fa_worker, &tasks[i]);
+    }
+    for (int i = 0; i < nthreads; ++i) pthread_join(th[i], NULL);
+    /* merge per-thread tables after the barrier */
+    orc_agg *res = tasks[0].agg;
+    for (int i = 1; i < nthreads; ++i) {
+        orc_agg_merge(res, tasks[i].agg);
+        orc_agg_destroy(tasks[i].agg);
+    }
+    size_t groups = orc_agg_size(res);
+    double cs = 0;
+    for (size_t g = 0; g < groups; ++g) cs += res->acc_f[0][g] + (double)res->cnt[1][g];
+    if (checksum) *checksum = cs;
+    orc_agg_destroy(res);
+    free(tasks);
+    free(th);
+    return groups;
+}
+
+typedef struct {
+    const orc_join *j;
+    const int64_t *keys;
+    size_t begin, end;
+    size_t matches;
+    uint64_t checksum;
+} jp_task;
+
+static void *jp_worker(void *arg)
+{
+    jp_task *t = (jp_task *)arg;
+    const size_t B = 65536;
+    uint32_t *pi = (uint32_t *)malloc(B * 4 * 4), *bi = (uint32_t *)malloc(B * 4 * 4);
+    for (size_t s = t->begin; s < t->end; s += B) {
+        size_t m = t->end - s < B ? t->end - s : B;
+        size_t c = orc_join_probe(t->j, TFG_JOIN_INNER, t->keys + s, NULL, m, pi, bi, B * 4);
+        for (size_t i = 0; i < c && i < B * 4; ++i) t->checksum += (uint64_t)bi[i] + (uint64_t)(pi[i] + s);
+        t->matches += c;
+    }
+    free(pi);
+    free(bi);
+    return NULL;
+}
+
+size_t orc_bench_join(const int64_t *build_keys, size_t nb, const int64_t *probe_keys, size_t np, int nthreads,
+                      uint64_t *checksum)
+{
+    orc_join *j = orc_join_create(TFG_INT64);
+    orc_join_build(j, build_keys, NULL, nb);
+    if (nthreads < 1) nthreads = 1;
+    jp_task *tasks = (jp_task *)calloc((size_t)nthreads, sizeof(jp_task));
+    pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+    size_t per = (np + (size_t)nthreads - 1) / (size_t)nthreads;
+    for (int i = 0; i < nthreads; ++i) {
+        tasks[i].j = j;
+        tasks[i].keys = probe_keys;
+        tasks[i].begin = per * (size_t)i < np ? per * (size_t)i : np;
+        tasks[i].end = per * (size_t)(i + 1) < np ? per * (size_t)(i + 1) : np;
+        pthread_create(&th[i], NULL, jp_worker, &tasks[i]);
+    }
+    size_t total = 0;
+    uint64_t cs = 0;
+    for (int i = 0; i < nthreads; ++i) {
+        pthread_join(th[i], NULL);
+        total += tasks[i].matches;
+        cs += tasks[i].checksum;
+    }
+    if (checksum) *checksum = cs;
+    orc_join_destroy(j);
+    free(tasks);
+    free(th);
+    return total;
+}

@@ -1,0 +1,71 @@
+/*
+ * oracle.h — CPU restatement of the reference's hot-path algorithms.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this library, and only as the checker / the timed CPU baseline.
+ * The product path (tiflash_amd/) never links or calls it.
+ *
+ * The reference (xfworld/tiflash) cannot be compiled here (its contrib/ submodules incl. boost
+ * are empty — SURVEY.md §8c), so this is a from-scratch restatement of the cited reference
+ * functions.  It is pinned by: (1) the hardware CRC32-C instruction the reference itself uses
+ * (_mm_crc32_u64, Common/HashTable/Hash.h:70-95) on this host; (2) the known answers in the
+ * reference's own gtests, transcribed as fixtures in tests/golden/ (see tests/golden/README.md).
+ */
+#ifndef TFG_ORACLE_H
+#define TFG_ORACLE_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int orc_has_hw_crc(void);
+uint32_t orc_crc32c_u64(uint32_t crc, uint64_t x);    /* SSE4.2 crc32q when available */
+uint32_t orc_crc32c_u64_sw(uint32_t crc, uint64_t x); /* bitwise, reflected 0x82F63B78 */
+uint32_t orc_update_weak_hash32_bytes(const uint8_t *pos, size_t size, uint32_t h);
+
+void orc_weak_hash_update(int type, const void *col, const uint8_t *nullmap, size_t n, uint32_t *h);
+void orc_weak_hash_update_string(const uint8_t *chars, const uint64_t *offsets, const uint8_t *nullmap, size_t n,
+                                 int collator, uint32_t *h);
+void orc_fill_selector(const uint32_t *h, size_t n, uint32_t part_num, uint32_t fgs, uint32_t *sel);
+void orc_partition(const uint32_t *sel, size_t n, uint32_t parts, uint32_t *perm, uint64_t *offsets);
+
+void orc_cmp(int a_type, const void *a, int a_const, int op, int b_type, const void *b, int b_const,
+             const uint8_t *a_null, const uint8_t *b_null, size_t n, uint8_t *out);
+size_t orc_count_bytes_in_filter(const uint8_t *f, const uint8_t *nullmap, size_t n);
+size_t orc_filter(int width, const void *col, const uint8_t *f, size_t n, void *out);
+size_t orc_filter_string(const uint8_t *chars, const uint64_t *offsets, const uint8_t *f, size_t n,
+                         uint8_t *out_chars, uint64_t *out_offsets, size_t *out_bytes);
+int orc_arith(int op, int a_type, const void *a, int a_const, int a_scale, int b_type, const void *b, int b_const,
+              int b_scale, int res_type, int res_scale, size_t n, void *out);
+
+typedef struct orc_agg orc_agg;
+orc_agg *orc_agg_create(int key_type, int n_aggs, const int *kinds, const int *arg_types);
+void orc_agg_destroy(orc_agg *a);
+void orc_agg_consume(orc_agg *a, const void *keys, const uint8_t *key_null, const void *const *args,
+                     const uint8_t *const *arg_nulls, const uint8_t *mask, size_t n);
+void orc_agg_merge(orc_agg *dst, const orc_agg *src);
+size_t orc_agg_size(const orc_agg *a);
+/* out_keys: u64 key bits; out_key_null; out_states[i]: 8 or 16 B per group; out_state_null[i]. */
+void orc_agg_result(const orc_agg *a, uint64_t *out_keys, uint8_t *out_key_null, void *const *out_states,
+                    uint8_t *const *out_state_null);
+
+typedef struct orc_join orc_join;
+orc_join *orc_join_create(int key_type);
+void orc_join_build(orc_join *j, const void *keys, const uint8_t *key_null, size_t n);
+void orc_join_destroy(orc_join *j);
+size_t orc_join_probe(const orc_join *j, int kind, const void *keys, const uint8_t *key_null, size_t n,
+                      uint32_t *out_probe, uint32_t *out_build, size_t capacity);
+
+/* CPU baseline legs (threads = nthreads; per-thread tables merged after a barrier like
+ * ParallelAggregatingBlockInputStream.cpp:77-159).  Return the number of groups / matches. */
+size_t orc_bench_filter_agg(const int64_t *f, int64_t threshold, const int64_t *k, const double *v, size_t n,
+                            int nthreads, size_t block_rows, double *checksum);
+size_t orc_bench_join(const int64_t *build_keys, size_t nb, const int64_t *probe_keys, size_t np, int nthreads,
+                      uint64_t *checksum);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,238 @@
+"""ctypes wrapper of oracle/liboracle.so — the CPU restatement of the reference's hot path.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg as the checker / CPU baseline, never by the product (tiflash_amd/).
+Arrays are numpy arrays in host memory.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_PATH = os.path.join(_HERE, "liboracle.so")
+_L = None
+
+INT8, INT16, INT32, INT64, UINT8, UINT16, UINT32, UINT64, FLOAT32, FLOAT64 = range(1, 11)
+DECIMAL32, DECIMAL64, DECIMAL128 = 11, 12, 13
+NP_TYPE = {np.dtype(np.int8): INT8, np.dtype(np.int16): INT16, np.dtype(np.int32): INT32, np.dtype(np.int64): INT64,
+           np.dtype(np.uint8): UINT8, np.dtype(np.uint16): UINT16, np.dtype(np.uint32): UINT32,
+           np.dtype(np.uint64): UINT64, np.dtype(np.float32): FLOAT32, np.dtype(np.float64): FLOAT64}
+
+
+def build():
+    subprocess.run(["make", "-C", _HERE, "-s"], check=True)
+
+
+def lib():
+    global _L
+    if _L is None:
+        if not os.path.exists(_PATH):
+            build()
+        L = ctypes.CDLL(_PATH)
+        L.orc_crc32c_u64.restype = ctypes.c_uint32
+        L.orc_crc32c_u64.argtypes = [ctypes.c_uint32, ctypes.c_uint64]
+        L.orc_crc32c_u64_sw.restype = ctypes.c_uint32
+        L.orc_crc32c_u64_sw.argtypes = [ctypes.c_uint32, ctypes.c_uint64]
+        L.orc_update_weak_hash32_bytes.restype = ctypes.c_uint32
+        L.orc_update_weak_hash32_bytes.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32]
+        L.orc_count_bytes_in_filter.restype = ctypes.c_size_t
+        L.orc_filter.restype = ctypes.c_size_t
+        L.orc_filter_string.restype = ctypes.c_size_t
+        L.orc_agg_create.restype = ctypes.c_void_p
+        L.orc_agg_size.restype = ctypes.c_size_t
+        L.orc_agg_size.argtypes = [ctypes.c_void_p]
+        L.orc_agg_destroy.argtypes = [ctypes.c_void_p]
+        L.orc_join_create.restype = ctypes.c_void_p
+        L.orc_join_destroy.argtypes = [ctypes.c_void_p]
+        L.orc_join_probe.restype = ctypes.c_size_t
+        L.orc_bench_filter_agg.restype = ctypes.c_size_t
+        L.orc_bench_join.restype = ctypes.c_size_t
+        _L = L
+    return _L
+
+
+def _p(a):
+    return ctypes.c_void_p(0) if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _ptrs(arrs):
+    out = (ctypes.c_void_p * max(1, len(arrs)))()
+    for i, a in enumerate(arrs):
+        out[i] = 0 if a is None else a.ctypes.data
+    return out
+
+
+def type_of(a: np.ndarray) -> int:
+    return NP_TYPE[a.dtype]
+
+
+def crc32c_u64(crc: int, x: int) -> int:
+    return lib().orc_crc32c_u64(crc, x & 0xFFFFFFFFFFFFFFFF)
+
+
+def crc32c_u64_sw(crc: int, x: int) -> int:
+    return lib().orc_crc32c_u64_sw(crc, x & 0xFFFFFFFFFFFFFFFF)
+
+
+def weak_hash(cols, types=None, nullmaps=None, h=None) -> np.ndarray:
+    n = len(cols[0])
+    if h is None:
+        h = np.full(n, 0xFFFFFFFF, dtype=np.uint32)
+    for j, c in enumerate(cols):
+        c = np.ascontiguousarray(c)
+        t = types[j] if types else type_of(c)
+        nm = None if not nullmaps or nullmaps[j] is None else np.ascontiguousarray(nullmaps[j], dtype=np.uint8)
+        lib().orc_weak_hash_update(t, _p(c), _p(nm), ctypes.c_size_t(n), _p(h))
+    return h
+
+
+def weak_hash_string(chars: np.ndarray, offsets: np.ndarray, h: np.ndarray, nullmap=None, collator=0):
+    lib().orc_weak_hash_update_string(_p(chars), _p(offsets), _p(nullmap), ctypes.c_size_t(len(offsets)), collator,
+                                      _p(h))
+    return h
+
+
+def fill_selector(h: np.ndarray, part_num: int, fgs: int = 0) -> np.ndarray:
+    sel = np.empty(len(h), dtype=np.uint32)
+    lib().orc_fill_selector(_p(h), ctypes.c_size_t(len(h)), ctypes.c_uint32(part_num), ctypes.c_uint32(fgs), _p(sel))
+    return sel
+
+
+def partition(sel: np.ndarray, parts: int):
+    perm = np.empty(len(sel), dtype=np.uint32)
+    offs = np.empty(parts + 1, dtype=np.uint64)
+    lib().orc_partition(_p(sel), ctypes.c_size_t(len(sel)), ctypes.c_uint32(parts), _p(perm), _p(offs))
+    return perm, offs
+
+
+def cmp(a, op, b, a_type=None, b_type=None, a_const=False, b_const=False, a_null=None, b_null=None, n=None):
+    a = np.ascontiguousarray(a)
+    b = np.ascontiguousarray(b)
+    n = n if n is not None else (len(b) if a_const else len(a))
+    out = np.empty(n, dtype=np.uint8)
+    lib().orc_cmp(a_type or type_of(a), _p(a), int(a_const), op, b_type or type_of(b), _p(b), int(b_const),
+                  _p(a_null), _p(b_null), ctypes.c_size_t(n), _p(out))
+    return out
+
+
+def count_bytes_in_filter(f: np.ndarray, nullmap=None) -> int:
+    return lib().orc_count_bytes_in_filter(_p(f), _p(nullmap), ctypes.c_size_t(len(f)))
+
+
+def filter(col: np.ndarray, f: np.ndarray) -> np.ndarray:  # noqa: A001
+    col = np.ascontiguousarray(col)
+    out = np.empty_like(col)
+    width = col.dtype.itemsize * (col.shape[1] if col.ndim == 2 else 1)
+    k = lib().orc_filter(width, _p(col), _p(f), ctypes.c_size_t(len(f)), _p(out))
+    return out[:k]
+
+
+def filter_string(chars, offsets, f):
+    out_chars = np.empty(max(1, len(chars)), dtype=np.uint8)
+    out_offsets = np.empty(max(1, len(offsets)), dtype=np.uint64)
+    nbytes = ctypes.c_size_t()
+    rows = lib().orc_filter_string(_p(chars), _p(offsets), _p(f), ctypes.c_size_t(len(f)), _p(out_chars),
+                                   _p(out_offsets), ctypes.byref(nbytes))
+    return out_chars[:nbytes.value], out_offsets[:rows]
+
+
+def arith(op, a, b, res_type, a_type=None, b_type=None, a_const=False, b_const=False, a_scale=0, b_scale=0,
+          res_scale=0, n=None):
+    a = np.ascontiguousarray(a)
+    b = np.ascontiguousarray(b)
+    n = n if n is not None else (len(b) if a_const else len(a))
+    width = {1: 1, 2: 2, 3: 4, 4: 8, 5: 1, 6: 2, 7: 4, 8: 8, 9: 4, 10: 8, 11: 4, 12: 8, 13: 16}[res_type]
+    out = np.zeros(n * width, dtype=np.uint8)
+    rc = lib().orc_arith(op, a_type or type_of(a), _p(a), int(a_const), a_scale, b_type or type_of(b), _p(b),
+                         int(b_const), b_scale, res_type, res_scale, ctypes.c_size_t(n), _p(out))
+    assert rc == 0
+    return out
+
+
+class Agg:
+    """Reference-semantics Aggregator (HashMap key64 + sum/count states)."""
+
+    def __init__(self, key_type: int, aggs):
+        kinds = (ctypes.c_int * len(aggs))(*[k for k, _ in aggs])
+        types = (ctypes.c_int * len(aggs))(*[t & 0xFF for _, t in aggs])
+        self.aggs = list(aggs)
+        self.h = ctypes.c_void_p(lib().orc_agg_create(key_type, len(aggs), kinds, types))
+        self.key_type = key_type
+
+    def consume(self, keys, args, key_null=None, arg_nulls=None, mask=None, n=None):
+        n = n if n is not None else (len(keys) if keys is not None else len(next(a for a in args if a is not None)))
+        lib().orc_agg_consume(self.h, _p(keys), _p(key_null), _ptrs(args), _ptrs(arg_nulls) if arg_nulls else None,
+                              _p(mask), ctypes.c_size_t(n))
+
+    def merge(self, other: "Agg"):
+        lib().orc_agg_merge(self.h, other.h)
+
+    def size(self) -> int:
+        return lib().orc_agg_size(self.h)
+
+    def result(self):
+        g = self.size()
+        keys = np.empty(g, dtype=np.uint64)
+        key_null = np.empty(g, dtype=np.uint8)
+        states, snull = [], []
+        for kind, t in self.aggs:
+            wide = kind == 0 and (t & 0xFF) in (DECIMAL32, DECIMAL64, DECIMAL128)
+            if kind != 0:
+                states.append(np.empty(g, dtype=np.uint64))
+            elif (t & 0xFF) in (FLOAT32, FLOAT64):
+                states.append(np.empty(g, dtype=np.float64))
+            elif wide:
+                states.append(np.empty((g, 2), dtype=np.int64))
+            else:
+                states.append(np.empty(g, dtype=np.int64))
+            snull.append(np.empty(g, dtype=np.uint8))
+        lib().orc_agg_result(self.h, _p(keys), _p(key_null), _ptrs(states), _ptrs(snull))
+        return {"keys": keys, "key_null": key_null, "states": states, "state_null": snull}
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_agg_destroy(self.h)
+            self.h = None
+
+
+class JoinRef:
+    def __init__(self, key_type: int):
+        self.h = ctypes.c_void_p(lib().orc_join_create(key_type))
+
+    def build(self, keys, key_null=None):
+        keys = np.ascontiguousarray(keys)
+        lib().orc_join_build(self.h, _p(keys), _p(key_null), ctypes.c_size_t(len(keys)))
+
+    def probe(self, keys, kind=0, key_null=None):
+        keys = np.ascontiguousarray(keys)
+        n = len(keys)
+        total = lib().orc_join_probe(self.h, kind, _p(keys), _p(key_null), ctypes.c_size_t(n), None, None,
+                                     ctypes.c_size_t(0))
+        pi = np.empty(max(total, 1), dtype=np.uint32)
+        bi = np.empty(max(total, 1), dtype=np.uint32)
+        lib().orc_join_probe(self.h, kind, _p(keys), _p(key_null), ctypes.c_size_t(n), _p(pi), _p(bi),
+                             ctypes.c_size_t(total))
+        return pi[:total], bi[:total]
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_join_destroy(self.h)
+            self.h = None
+
+
+def bench_filter_agg(f, threshold, k, v, nthreads, block_rows=65536):
+    cs = ctypes.c_double()
+    g = lib().orc_bench_filter_agg(_p(f), ctypes.c_int64(threshold), _p(k), _p(v), ctypes.c_size_t(len(k)),
+                                   nthreads, ctypes.c_size_t(block_rows), ctypes.byref(cs))
+    return g, cs.value
+
+
+def bench_join(build_keys, probe_keys, nthreads):
+    cs = ctypes.c_uint64()
+    m = lib().orc_bench_join(_p(build_keys), ctypes.c_size_t(len(build_keys)), _p(probe_keys),
+                             ctypes.c_size_t(len(probe_keys)), nthreads, ctypes.byref(cs))
+    return m, cs.value

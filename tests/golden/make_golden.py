@@ -1,0 +1,85 @@
+"""Generates the committed golden fixtures in tests/golden/.
+
+reference_cases.json — known answers TRANSCRIBED (as data) from the reference's own gtests:
+  * groupby: dbms/src/Flash/tests/gtest_aggregation_executor.cpp:269-272 (columns) and :344-368
+    (expected GROUP BY key sets for tinyint_/smallint_/int_/bigint_);
+  * join: dbms/src/Flash/tests/gtest_join_executor.cpp:114-200 (SimpleJoin tables t1/t2 and the
+    expected inner / left / semi / anti results).  The reference keys are strings "1".."4"; join
+    equality is unchanged when they are written as the integers 1..4, which is how they are stored;
+  * exchange: dbms/src/Flash/Mpp/tests/gtest_mpp_exchange_writer.cpp:663-718 (64 blocks of keys
+    0..63, 4 partitions -> 1024 rows each).
+crc_vectors.json — CRC32-C / WeakHash32 vectors computed with the x86 SSE4.2 crc32q instruction,
+  the instruction the reference itself hashes with (Common/HashTable/Hash.h:70-95), via oracle.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+
+N = None
+T1 = {"a": [1, 2, N, 1, N], "b": [3, 4, 3, N, N]}
+T2 = {"a": [1, 3, N, 1, N], "b": [3, 4, 3, N, N]}
+
+
+def join_cases():
+    # (left, right, key) in the order of gtest_join_executor.cpp:126-131
+    combos = [("t1", "t2", "a"), ("t2", "t1", "a"), ("t1", "t2", "b"), ("t2", "t1", "b")]
+    inner = [
+        [[1, 1, 1, 1], [N, 3, N, 3], [1, 1, 1, 1], [3, 3, N, N]],
+        [[1, 1, 1, 1], [N, 3, N, 3], [1, 1, 1, 1], [3, 3, N, N]],
+        [[N, 1, 2, N, 1], [3, 3, 4, 3, 3], [1, 1, 3, N, N], [3, 3, 4, 3, 3]],
+        [[N, 1, 3, N, 1], [3, 3, 4, 3, 3], [1, 1, 2, N, N], [3, 3, 4, 3, 3]],
+    ]
+    left = [
+        [[1, 1, 2, N, 1, 1, N], [3, 3, 4, 3, N, N, N], [1, 1, N, N, 1, 1, N], [N, 3, N, N, N, 3, N]],
+        [[1, 1, 3, N, 1, 1, N], [3, 3, 4, 3, N, N, N], [1, 1, N, N, 1, 1, N], [N, 3, N, N, N, 3, N]],
+        [[1, 1, 2, N, N, 1, N], [3, 3, 4, 3, 3, N, N], [N, 1, 3, N, 1, N, N], [3, 3, 4, 3, 3, N, N]],
+        [[1, 1, 3, N, N, 1, N], [3, 3, 4, 3, 3, N, N], [N, 1, 2, N, 1, N, N], [3, 3, 4, 3, 3, N, N]],
+    ]
+    semi = [[[1, 1], [3, N]], [[1, 1], [3, N]], [[1, 2, N], [3, 4, 3]], [[1, 3, N], [3, 4, 3]]]
+    anti = [[[2, N, N], [4, 3, N]], [[3, N, N], [4, 3, N]], [[1, N], [N, N]], [[1, N], [N, N]]]
+    tables = {"t1": T1, "t2": T2}
+    out = []
+    for i, (l, r, key) in enumerate(combos):
+        for kind, exp in (("inner", inner[i]), ("left", left[i]), ("semi", semi[i]), ("anti", anti[i])):
+            out.append({"name": f"SimpleJoin {kind} {l} {r} on {key}", "kind": kind, "probe": tables[l],
+                        "build": tables[r], "key": key, "expected_columns": exp})
+    return out
+
+
+def groupby_cases():
+    cols = {  # gtest_aggregation_executor.cpp:269-272
+        "tinyint_": ([1, 2, 3, N, N, 0, 0, -1, -2], 1, "int8", [-1, 2, N, 0, 1, 3, -2]),
+        "smallint_": ([2, 3, N, N, 0, -1, -2, 4, 0], 2, "int16", [-1, 2, -2, N, 0, 4, 3]),
+        "int_": ([4, N, N, 0, 123, -1, -1, 123, 4], 3, "int32", [-1, N, 4, 0, 123]),
+        "bigint_": ([2, 2, N, 0, -1, N, -1, 0, 123], 4, "int64", [2, -1, 0, 123, N]),
+    }
+    return [{"name": k, "column": v[0], "type": v[1], "dtype": v[2], "expected": v[3]} for k, v in cols.items()]
+
+
+def crc_vectors():
+    from oracle import oracle as orc
+    rng = np.random.default_rng(2024)
+    xs = [0, 1, 2**63, 2**64 - 1, 0x0123456789ABCDEF] + [int(x) for x in rng.integers(0, 2**63, 27, dtype=np.int64)]
+    seeds = [0xFFFFFFFF, 0, 0x12345678]
+    vec = [{"crc": s, "x": x, "out": orc.crc32c_u64(s, x)} for s in seeds for x in xs]
+    keys = np.arange(64, dtype=np.int64)
+    h = orc.weak_hash([keys])
+    strs = [b"", b"a", b"abcdefg", b"abcdefgh", b"abcdefghi", b"k00000042", b"hello world  "]
+    sh = [orc.lib().orc_update_weak_hash32_bytes(s, len(s), 0xFFFFFFFF) for s in strs]
+    return {"crc32c_u64": vec, "weak_hash_int64_0_63": [int(x) for x in h],
+            "selector_0_63_p4": [int(x) for x in orc.fill_selector(h, 4)],
+            "weak_hash_bytes": [{"s": s.decode(), "h": int(v)} for s, v in zip(strs, sh)]}
+
+
+if __name__ == "__main__":
+    with open(os.path.join(HERE, "reference_cases.json"), "w") as f:
+        json.dump({"groupby": groupby_cases(), "join": join_cases(),
+                   "exchange": {"block_rows": 64, "blocks": 64, "parts": 4, "rows_per_part": 1024}}, f, indent=1)
+    with open(os.path.join(HERE, "crc_vectors.json"), "w") as f:
+        json.dump(crc_vectors(), f, indent=1)
+    print("wrote", os.listdir(HERE))

@@ -1,0 +1,153 @@
+"""CPU tests: pin the oracle (CPU restatement) against the reference's own known answers and the
+hardware CRC32-C instruction.  No GPU needed."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _load(name):
+    with open(os.path.join(GOLD, name)) as f:
+        return json.load(f)
+
+
+def test_crc_sw_matches_hw_instruction(orc):
+    assert orc.lib().orc_has_hw_crc() == 1, "oracle must be built with SSE4.2 (the reference's crc32q)"
+    rng = np.random.default_rng(0)
+    for _ in range(20000):
+        s, x = int(rng.integers(0, 2**32)), int(rng.integers(0, 2**63)) * 2 + int(rng.integers(0, 2))
+        assert orc.crc32c_u64(s, x) == orc.crc32c_u64_sw(s, x)
+
+
+def test_crc_golden_vectors(orc):
+    g = _load("crc_vectors.json")
+    for v in g["crc32c_u64"]:
+        assert orc.crc32c_u64(v["crc"], v["x"]) == v["out"]
+        assert orc.crc32c_u64_sw(v["crc"], v["x"]) == v["out"]
+    for v in g["weak_hash_bytes"]:
+        s = v["s"].encode()
+        assert orc.lib().orc_update_weak_hash32_bytes(s, len(s), 0xFFFFFFFF) == v["h"]
+
+
+def test_exchange_known_answer(orc):
+    """gtest_mpp_exchange_writer.cpp:663-718: 64 blocks x keys 0..63, 4 partitions -> 1024 rows each."""
+    case = _load("reference_cases.json")["exchange"]
+    keys = np.tile(np.arange(case["block_rows"], dtype=np.int64), case["blocks"])
+    sel = orc.fill_selector(orc.weak_hash([keys]), case["parts"])
+    counts = np.bincount(sel, minlength=case["parts"])
+    assert counts.tolist() == [case["rows_per_part"]] * case["parts"]
+    perm, offs = orc.partition(sel, case["parts"])
+    assert np.all(np.diff(perm[offs[0]:offs[1]].astype(np.int64)) > 0)  # stable within a partition
+
+
+def test_fine_grained_selector(orc):
+    h = np.array([0, 1, 0xFFFFFFFF, 0x80000000, 12345], dtype=np.uint32)
+    sel = orc.fill_selector(h, 4, 8)
+    exp = [((int(x) * 4) >> 32) * 8 + int(x) % 8 for x in h]
+    assert sel.tolist() == exp
+
+
+def test_accurate_comparison_semantics(orc):
+    # Int8(-1) != UInt8(255) (Core/AccurateComparison.h:27-29)
+    a = np.array([-1], dtype=np.int8)
+    b = np.array([255], dtype=np.uint8)
+    assert orc.cmp(a, 0, b)[0] == 0 and orc.cmp(a, 2, b)[0] == 1
+    # Int64 vs Float64 exactly (DecomposedFloat): 2^53+1 > 2^53
+    x = np.array([2**53 + 1], dtype=np.int64)
+    y = np.array([float(2**53)])
+    assert orc.cmp(x, 4, y)[0] == 1 and orc.cmp(x, 0, y)[0] == 0
+    # NaN: only != is true
+    nan = np.array([np.nan])
+    one = np.array([1], dtype=np.int64)
+    assert [orc.cmp(nan, op, one)[0] for op in range(6)] == [0, 1, 0, 0, 0, 0]
+    # UInt64 max vs Int64 -1
+    u = np.array([2**64 - 1], dtype=np.uint64)
+    assert orc.cmp(u, 4, np.array([-1], dtype=np.int64))[0] == 1
+
+
+def test_filter_stable_and_count(orc):
+    rng = np.random.default_rng(1)
+    for n in (0, 1, 63, 64, 65, 1000):
+        col = rng.integers(0, 1000, n, dtype=np.int64)
+        f = rng.integers(0, 3, n).astype(np.uint8)
+        out = orc.filter(col, f)
+        np.testing.assert_array_equal(out, col[f != 0])
+        assert orc.count_bytes_in_filter(f) == int((f != 0).sum())
+
+
+def test_groupby_reference_cases(orc):
+    for case in _load("reference_cases.json")["groupby"]:
+        vals = case["column"]
+        kn = np.array([v is None for v in vals], dtype=np.uint8)
+        k = np.array([0 if v is None else v for v in vals], dtype=case["dtype"])
+        a = orc.Agg(case["type"], [(2, 0)])
+        a.consume(k, [None], key_null=kn)
+        r = a.result()
+        width = k.itemsize
+        raw = r["keys"].astype({1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}[width]).view(case["dtype"])
+        got = [None if r["key_null"][i] else int(raw[i]) for i in range(a.size())]
+        assert sorted(got, key=repr) == sorted(case["expected"], key=repr), case["name"]
+
+
+def _join_rows(case, pi, bi):
+    p, b = case["probe"], case["build"]
+    rows = []
+    for i, j in zip(pi.tolist(), bi.tolist()):
+        row = [p["a"][i], p["b"][i]]
+        if case["kind"] in ("inner", "left"):
+            row += [None, None] if j == 0xFFFFFFFF else [b["a"][j], b["b"][j]]
+        rows.append(tuple(row))
+    return sorted(rows, key=repr)
+
+
+def test_join_reference_cases(orc):
+    kinds = {"inner": 0, "left": 1, "semi": 2, "anti": 3}
+    for case in _load("reference_cases.json")["join"]:
+        key = case["key"]
+        bcol, pcol = case["build"][key], case["probe"][key]
+        j = orc.JoinRef(orc.INT64)
+        j.build(np.array([0 if v is None else v for v in bcol], dtype=np.int64),
+                np.array([v is None for v in bcol], dtype=np.uint8))
+        pi, bi = j.probe(np.array([0 if v is None else v for v in pcol], dtype=np.int64), kinds[case["kind"]],
+                         np.array([v is None for v in pcol], dtype=np.uint8))
+        exp = sorted(zip(*case["expected_columns"]), key=repr)
+        assert _join_rows(case, pi, bi) == exp, case["name"]
+
+
+def test_join_rowreflist_order(orc):
+    """insertRowToList (JoinPartition.cpp:39-60): head first, then newest -> oldest."""
+    j = orc.JoinRef(orc.INT64)
+    j.build(np.array([7, 7, 7, 7], dtype=np.int64))
+    pi, bi = j.probe(np.array([7], dtype=np.int64))
+    assert bi.tolist() == [0, 3, 2, 1]
+
+
+def test_decimal_arith(orc):
+    # Decimal(10,2) 1.25 + Decimal(10,3) 0.125 -> scale 3: 1375 ; multiply -> scale 5
+    a = np.array([125, -1], dtype=np.int64)
+    b = np.array([125, 1000], dtype=np.int64)
+    out = orc.arith(0, a, b, orc.DECIMAL64, a_type=orc.DECIMAL64, b_type=orc.DECIMAL64, a_scale=2, b_scale=3,
+                    res_scale=3).view(np.int64)
+    assert out.tolist() == [1375, 990]
+    out = orc.arith(2, a, b, orc.DECIMAL128, a_type=orc.DECIMAL64, b_type=orc.DECIMAL64, a_scale=2, b_scale=3,
+                    res_scale=5).view(np.int64).reshape(-1, 2)
+    assert out[:, 0].tolist() == [15625, -1000] and out[:, 1].tolist() == [0, -1]
+
+
+def test_bench_legs_run(orc):
+    rng = np.random.default_rng(3)
+    n = 100_000
+    f = rng.integers(0, 100, n, dtype=np.int64)
+    k = rng.integers(0, 1000, n, dtype=np.int64)
+    v = rng.integers(0, 1 << 20, n).astype(np.float64) / 256
+    g, cs = orc.bench_filter_agg(f, 96, k, v, 2, 4096)
+    ref = orc.Agg(orc.INT64, [(0, orc.FLOAT64), (2, 0)])
+    ref.consume(k, [v, None], mask=(f < 96).astype(np.uint8))
+    r = ref.result()
+    assert g == ref.size()
+    assert cs == pytest.approx(float(r["states"][0].sum() + r["states"][1].sum()))
+    m, _ = orc.bench_join(np.arange(1000, dtype=np.int64), rng.integers(0, 2000, 5000, dtype=np.int64), 2)
+    assert 0 < m < 5000

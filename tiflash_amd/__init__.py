@@ -1,0 +1,464 @@
+"""tiflash_amd — MI355X (gfx950) execution layer for TiFlash's Block/Column hot path.
+
+This Python module is plumbing only: it loads ``libtiflash_amd.so`` (hand-written HIP kernels
+behind the C-ABI declared in ``include/tiflash_amd.h``) with ctypes and passes device pointers
+of torch tensors.  There is no CPU fallback: every entry point goes through the HIP library and
+raises if it is missing.  The C++ operator layer that mirrors the reference's
+FilterTransformAction / Aggregator / Join / HashPartitionWriter lives in ``tiflash_amd/host``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Sequence
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libtiflash_amd.so")
+
+# ---- constants mirrored from include/tiflash_amd.h --------------------------------------------
+TFG_OK = 0
+ERRORS = {
+    -1: "INVALID_ARG", -2: "HIP", -3: "OOM", -4: "NOT_IMPLEMENTED", -5: "SIZE_MISMATCH",
+    -6: "ILLEGAL_TYPE", -7: "LOGICAL", -8: "CAPACITY", -9: "NO_DEVICE", -10: "FAULT_INJECTED",
+}
+TFG_ERR_CAPACITY = -8
+TFG_ERR_NO_DEVICE = -9
+
+INT8, INT16, INT32, INT64, UINT8, UINT16, UINT32, UINT64, FLOAT32, FLOAT64 = range(1, 11)
+DECIMAL32, DECIMAL64, DECIMAL128 = 11, 12, 13
+NULLABLE = 0x100  # or-ed into an aggregate argument type: the argument may carry a null map
+
+EQ, NE, LT, LE, GT, GE = range(6)
+PLUS, MINUS, MULTIPLY = range(3)
+AND, OR, NOT = range(3)
+AGG_SUM, AGG_COUNT, AGG_COUNT_ALL = range(3)
+JOIN_INNER, JOIN_LEFT, JOIN_SEMI, JOIN_ANTI = range(4)
+COLLATOR_NONE, COLLATOR_BINARY, COLLATOR_BIN_PADDING = range(3)
+
+WIDTH = {INT8: 1, INT16: 2, INT32: 4, INT64: 8, UINT8: 1, UINT16: 2, UINT32: 4, UINT64: 8,
+         FLOAT32: 4, FLOAT64: 8, DECIMAL32: 4, DECIMAL64: 8, DECIMAL128: 16}
+_CTYPE = {INT8: ctypes.c_int8, INT16: ctypes.c_int16, INT32: ctypes.c_int32, INT64: ctypes.c_int64,
+          UINT8: ctypes.c_uint8, UINT16: ctypes.c_uint16, UINT32: ctypes.c_uint32, UINT64: ctypes.c_uint64,
+          FLOAT32: ctypes.c_float, FLOAT64: ctypes.c_double, DECIMAL32: ctypes.c_int32,
+          DECIMAL64: ctypes.c_int64}
+
+
+class TfgError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"tfg error {code} ({ERRORS.get(code, '?')}): {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """The HIP library.  Raises (never falls back) when it is not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = ctypes.CDLL(LIB_PATH)
+        L.tfg_last_error.restype = ctypes.c_char_p
+        L.tfg_version.restype = ctypes.c_char_p
+        L.tfg_type_width.restype = ctypes.c_size_t
+        L.tfg_type_width.argtypes = [ctypes.c_int]
+        _lib = L
+    return _lib
+
+
+def check(rc: int) -> int:
+    if rc != TFG_OK:
+        raise TfgError(rc, lib().tfg_last_error().decode(errors="replace"))
+    return rc
+
+
+def _p(t) -> ctypes.c_void_p:
+    """Device pointer of a torch tensor (None -> NULL)."""
+    if t is None:
+        return ctypes.c_void_p(0)
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _ptr_array(ts) -> ctypes.Array:
+    arr = (ctypes.c_void_p * max(1, len(ts)))()
+    for i, t in enumerate(ts):
+        arr[i] = t.data_ptr() if t is not None else 0
+    return arr
+
+
+def _int_array(xs) -> ctypes.Array:
+    arr = (ctypes.c_int * max(1, len(xs)))()
+    for i, x in enumerate(xs):
+        arr[i] = int(x)
+    return arr
+
+
+def _scalar(type_: int, value):
+    return _CTYPE[type_](value)
+
+
+def torch_type(t) -> int:
+    import torch
+    m = {torch.int8: INT8, torch.int16: INT16, torch.int32: INT32, torch.int64: INT64, torch.uint8: UINT8,
+         torch.float32: FLOAT32, torch.float64: FLOAT64}
+    if hasattr(torch, "uint16"):
+        m[torch.uint16] = UINT16
+        m[torch.uint32] = UINT32
+        m[torch.uint64] = UINT64
+    return m[t.dtype]
+
+
+def _empty(n, width, device):
+    import torch
+    dt = {1: torch.uint8, 2: torch.int16, 4: torch.int32, 8: torch.int64}.get(width)
+    if dt is None:  # 16-byte values (Decimal128) as (n, 2) int64
+        return torch.empty((max(n, 1), 2), dtype=torch.int64, device=device)[:n]
+    return torch.empty(max(n, 1), dtype=dt, device=device)[:n]
+
+
+class Context:
+    """tfg_ctx bound to a device and the current torch stream of that device."""
+
+    def __init__(self, device: int = 0, stream=None):
+        import torch
+        self.device = device
+        if stream is None:
+            stream = torch.cuda.current_stream(device)
+        self.stream = stream
+        h = ctypes.c_void_p()
+        check(lib().tfg_ctx_create(ctypes.c_int(device), ctypes.c_void_p(stream.cuda_stream), ctypes.byref(h)))
+        self.h = h
+
+    def sync(self):
+        check(lib().tfg_ctx_sync(self.h))
+
+    def reserve(self, nbytes: int):
+        check(lib().tfg_ctx_reserve(self.h, ctypes.c_size_t(nbytes)))
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().tfg_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+# ---- a1/a2 comparison -------------------------------------------------------------------------
+def cmp_const(ctx: Context, col, op: int, scalar, scalar_type: Optional[int] = None, nullmap=None,
+              col_type: Optional[int] = None, out=None):
+    import torch
+    ct = col_type or torch_type(col)
+    st = scalar_type or (FLOAT64 if isinstance(scalar, float) else INT64)
+    n = col.shape[0]
+    out = out if out is not None else torch.empty(n, dtype=torch.uint8, device=col.device)
+    s = _scalar(st, scalar)
+    check(lib().tfg_cmp_const(ctx.h, ct, _p(col), _p(nullmap), ctypes.c_int64(n), op, st, ctypes.byref(s), _p(out)))
+    return out
+
+
+def cmp_vector(ctx: Context, a, op: int, b, a_nullmap=None, b_nullmap=None, a_type=None, b_type=None):
+    import torch
+    n = a.shape[0]
+    out = torch.empty(n, dtype=torch.uint8, device=a.device)
+    check(lib().tfg_cmp_vector(ctx.h, a_type or torch_type(a), _p(a), _p(a_nullmap), op, b_type or torch_type(b),
+                               _p(b), _p(b_nullmap), ctypes.c_int64(n), _p(out)))
+    return out
+
+
+def mask_logic(ctx: Context, op: int, a, b=None):
+    import torch
+    out = torch.empty_like(a)
+    check(lib().tfg_mask_logic(ctx.h, op, _p(a), _p(b), ctypes.c_int64(a.shape[0]), _p(out)))
+    return out
+
+
+def count_mask(ctx: Context, mask, nullmap=None) -> int:
+    c = ctypes.c_uint64()
+    check(lib().tfg_count_mask(ctx.h, _p(mask), _p(nullmap), ctypes.c_int64(mask.shape[0]), ctypes.c_void_p(0),
+                               ctypes.byref(c)))
+    return c.value
+
+
+def _col_width(c) -> int:
+    return c.element_size() * (c.shape[1] if c.dim() == 2 else 1)
+
+
+def filter(ctx: Context, mask, cols: Sequence):  # noqa: A001 - mirrors IColumn::filter
+    """Stable compaction of every column by one UInt8 filter (ColumnVector<T>::filter)."""
+    n = mask.shape[0]
+    widths = [_col_width(c) for c in cols]
+    cnt = ctypes.c_uint64()
+    # count first so outputs are exactly sized (sync), then compact
+    check(lib().tfg_count_mask(ctx.h, _p(mask), ctypes.c_void_p(0), ctypes.c_int64(n), ctypes.c_void_p(0),
+                               ctypes.byref(cnt)))
+    outs = [_empty(cnt.value, w, mask.device).view(c.dtype) if w <= 8 else _empty(cnt.value, w, mask.device)
+            for c, w in zip(cols, widths)]
+    check(lib().tfg_filter(ctx.h, _p(mask), ctypes.c_int64(n), len(cols), _ptr_array(cols), _int_array(widths),
+                           _ptr_array(outs), ctypes.c_void_p(0), ctypes.byref(cnt)))
+    return outs
+
+
+def filter_cmp_const(ctx: Context, pred_col, op: int, scalar, cols: Sequence, scalar_type=None, pred_nullmap=None,
+                     pred_type=None, out_capacity: Optional[int] = None):
+    """Fused FilterTransformAction for `pred_col op scalar`; outputs sized to n unless given."""
+    import torch
+    n = pred_col.shape[0]
+    st = scalar_type or (FLOAT64 if isinstance(scalar, float) else INT64)
+    widths = [_col_width(c) for c in cols]
+    cap = n if out_capacity is None else out_capacity
+    outs = [_empty(cap, w, pred_col.device).view(c.dtype) if w <= 8 else _empty(cap, w, pred_col.device)
+            for c, w in zip(cols, widths)]
+    cnt = ctypes.c_uint64()
+    s = _scalar(st, scalar)
+    check(lib().tfg_filter_cmp_const(ctx.h, pred_type or torch_type(pred_col), _p(pred_col), _p(pred_nullmap), op, st,
+                                     ctypes.byref(s), ctypes.c_int64(n), len(cols), _ptr_array(cols),
+                                     _int_array(widths), _ptr_array(outs), ctypes.c_void_p(0), ctypes.byref(cnt)))
+    return [o[:cnt.value] for o in outs]
+
+
+def filter_string(ctx: Context, mask, chars, offsets):
+    import torch
+    n = mask.shape[0]
+    out_chars = torch.empty(max(1, chars.shape[0]), dtype=torch.uint8, device=mask.device)
+    out_offsets = torch.empty(max(1, n), dtype=torch.int64, device=mask.device)
+    rows, nbytes = ctypes.c_uint64(), ctypes.c_uint64()
+    check(lib().tfg_filter_string(ctx.h, _p(mask), ctypes.c_int64(n), _p(chars), _p(offsets), _p(out_chars),
+                                  _p(out_offsets), ctypes.byref(rows), ctypes.byref(nbytes)))
+    return out_chars[:nbytes.value], out_offsets[:rows.value]
+
+
+# ---- a3 arithmetic ----------------------------------------------------------------------------
+def arith(ctx: Context, op: int, a, b, res_type: int, a_type=None, b_type=None, a_scale=0, b_scale=0, res_scale=0,
+          n=None, device=None):
+    """a/b: tensors or Python scalars (constants); Decimal128 results are (n, 2) int64 tensors."""
+    import torch
+    a_const, b_const = not hasattr(a, "data_ptr"), not hasattr(b, "data_ptr")
+    if n is None:
+        n = (b if a_const else a).shape[0]
+    dev = device or (b if a_const else a).device
+    at = a_type or (torch_type(a) if not a_const else INT64)
+    bt = b_type or (torch_type(b) if not b_const else INT64)
+    out = _empty(n, WIDTH[res_type], dev)
+    ap = ctypes.byref(_scalar(at, a)) if a_const else _p(a)
+    bp = ctypes.byref(_scalar(bt, b)) if b_const else _p(b)
+    check(lib().tfg_arith(ctx.h, op, at, ap, int(a_const), a_scale, bt, bp, int(b_const), b_scale, res_type,
+                          res_scale, ctypes.c_int64(n), _p(out)))
+    if res_type == FLOAT64:
+        out = out.view(torch.float64)
+    elif res_type == FLOAT32:
+        out = out.view(torch.float32)
+    return out
+
+
+# ---- a22-a24 hash / partition -----------------------------------------------------------------
+def weak_hash(ctx: Context, cols: Sequence, types: Optional[Sequence[int]] = None, nullmaps=None, h=None):
+    """WeakHash32 over key columns (IColumn::updateWeakHash32); returns an int32 tensor of u32 bits."""
+    import torch
+    n = cols[0].shape[0]
+    if h is None:
+        h = torch.empty(n, dtype=torch.int32, device=cols[0].device)
+        check(lib().tfg_weak_hash_init(ctx.h, _p(h), ctypes.c_int64(n)))
+    for j, c in enumerate(cols):
+        t = types[j] if types else torch_type(c)
+        nm = nullmaps[j] if nullmaps else None
+        check(lib().tfg_weak_hash_update(ctx.h, t, _p(c), _p(nm), ctypes.c_int64(n), _p(h)))
+    return h
+
+
+def weak_hash_string(ctx: Context, chars, offsets, h, nullmap=None, collator=COLLATOR_NONE):
+    check(lib().tfg_weak_hash_update_string(ctx.h, _p(chars), _p(offsets), _p(nullmap),
+                                            ctypes.c_int64(offsets.shape[0]), collator, _p(h)))
+    return h
+
+
+def fill_selector(ctx: Context, h, part_num: int, fine_grained_stream_count: int = 0):
+    import torch
+    sel = torch.empty_like(h)
+    check(lib().tfg_fill_selector(ctx.h, _p(h), ctypes.c_int64(h.shape[0]), ctypes.c_uint32(part_num),
+                                  ctypes.c_uint32(fine_grained_stream_count), _p(sel)))
+    return sel
+
+
+def partition(ctx: Context, selector, num_parts: int):
+    """Stable partition permutation + offsets (the row order IColumn::scatter produces)."""
+    import torch
+    n = selector.shape[0]
+    perm = torch.empty(max(n, 1), dtype=torch.int32, device=selector.device)[:n]
+    offs = torch.empty(num_parts + 1, dtype=torch.int64, device=selector.device)
+    host = (ctypes.c_uint64 * (num_parts + 1))()
+    check(lib().tfg_partition(ctx.h, _p(selector), ctypes.c_int64(n), ctypes.c_uint32(num_parts), _p(perm), _p(offs),
+                              host))
+    return perm, list(host)
+
+
+def gather(ctx: Context, perm, cols: Sequence):
+    n = perm.shape[0]
+    widths = [_col_width(c) for c in cols]
+    outs = [_empty(n, w, perm.device).view(c.dtype) if w <= 8 else _empty(n, w, perm.device)
+            for c, w in zip(cols, widths)]
+    check(lib().tfg_gather(ctx.h, _p(perm), ctypes.c_int64(n), len(cols), _ptr_array(cols), _int_array(widths),
+                           _ptr_array(outs)))
+    return outs
+
+
+def hash_partition(ctx: Context, cols: Sequence, key_idx: Sequence[int], part_num: int, types=None, nullmaps=None):
+    """HashBaseWriterHelper::scatterColumns: returns (partition-major columns, host offsets[P+1])."""
+    n = cols[0].shape[0]
+    types = types or [torch_type(c) for c in cols]
+    outs = [_empty(n, WIDTH[t], c.device).view(c.dtype) if WIDTH[t] <= 8 else _empty(n, 16, c.device)
+            for c, t in zip(cols, types)]
+    import torch
+    offs = torch.empty(part_num + 1, dtype=torch.int64, device=cols[0].device)
+    host = (ctypes.c_uint64 * (part_num + 1))()
+    nm = _ptr_array(nullmaps) if nullmaps else ctypes.c_void_p(0)
+    check(lib().tfg_hash_partition(ctx.h, ctypes.c_int64(n), len(key_idx), _int_array(key_idx), len(cols),
+                                   _int_array(types), _ptr_array(cols), nm, ctypes.c_uint32(part_num),
+                                   _ptr_array(outs), _p(offs), host))
+    return outs, list(host)
+
+
+# ---- a9-a17 aggregation -----------------------------------------------------------------------
+class _AggParams(ctypes.Structure):
+    _fields_ = [("bucket_bits", ctypes.c_int), ("expected_groups", ctypes.c_int64)]
+
+
+class Aggregator:
+    """tfg_agg: hash GROUP BY with one fixed-width key (key_type=0: without key)."""
+
+    def __init__(self, ctx: Context, key_type: int, aggs: Sequence[tuple], bucket_bits: int = 0,
+                 expected_groups: int = 0):
+        """aggs: sequence of (kind, arg_type[|NULLABLE]) — arg_type ignored for AGG_COUNT_ALL."""
+        self.ctx = ctx
+        self.key_type = key_type
+        self.aggs = list(aggs)
+        kinds = _int_array([k for k, _ in aggs])
+        types = _int_array([t for _, t in aggs])
+        params = _AggParams(bucket_bits, expected_groups)
+        h = ctypes.c_void_p()
+        check(lib().tfg_agg_create(ctx.h, key_type, len(aggs), kinds, types, ctypes.c_void_p(0), ctypes.byref(params),
+                                   ctypes.byref(h)))
+        self.h = h
+
+    def consume(self, keys, args: Sequence, key_nullmap=None, arg_nullmaps=None, mask=None, n=None):
+        n = n if n is not None else (keys.shape[0] if keys is not None else next(a for a in args if a is not None).shape[0])
+        check(lib().tfg_agg_consume(self.h, _p(keys), _p(key_nullmap), _ptr_array(args),
+                                    _ptr_array(arg_nullmaps) if arg_nullmaps else ctypes.c_void_p(0), _p(mask),
+                                    ctypes.c_int64(n)))
+
+    def consume_filtered(self, pred_col, op: int, scalar, keys, args: Sequence, scalar_type=None, pred_nullmap=None,
+                         key_nullmap=None, arg_nullmaps=None, pred_type=None):
+        st = scalar_type or (FLOAT64 if isinstance(scalar, float) else INT64)
+        s = _scalar(st, scalar)
+        check(lib().tfg_agg_consume_filtered(self.h, pred_type or torch_type(pred_col), _p(pred_col), _p(pred_nullmap),
+                                             op, st, ctypes.byref(s), _p(keys), _p(key_nullmap), _ptr_array(args),
+                                             _ptr_array(arg_nullmaps) if arg_nullmaps else ctypes.c_void_p(0),
+                                             ctypes.c_int64(pred_col.shape[0])))
+
+    def consume_partial(self, keys, states: Sequence, key_nullmap=None, state_nullmaps=None):
+        n = keys.shape[0] if keys is not None else states[0].shape[0]
+        check(lib().tfg_agg_consume_partial(self.h, _p(keys), _p(key_nullmap), _ptr_array(states),
+                                            _ptr_array(state_nullmaps) if state_nullmaps else ctypes.c_void_p(0),
+                                            ctypes.c_int64(n)))
+
+    def merge(self, other: "Aggregator"):
+        check(lib().tfg_agg_merge(self.h, other.h))
+
+    def size(self) -> int:
+        g = ctypes.c_uint64()
+        check(lib().tfg_agg_size(self.h, ctypes.byref(g)))
+        return g.value
+
+    def result(self, device=None):
+        """-> dict(keys, key_null, states[i], state_null[i]) with exactly size() rows."""
+        import torch
+        dev = device or torch.device("cuda", self.ctx.device)
+        g = self.size()
+        kw = WIDTH.get(self.key_type, 8)
+        keys = _empty(g, kw, dev) if self.key_type else None
+        key_null = torch.empty(max(g, 1), dtype=torch.uint8, device=dev)[:g]
+        states, snulls = [], []
+        for i in range(len(self.aggs)):
+            t, w = ctypes.c_int(), ctypes.c_int()
+            check(lib().tfg_agg_result_type(self.h, i, ctypes.byref(t), ctypes.byref(w)))
+            s = _empty(g, w.value, dev)
+            if t.value == FLOAT64:
+                s = s.view(torch.float64)
+            states.append(s)
+            snulls.append(torch.empty(max(g, 1), dtype=torch.uint8, device=dev)[:g])
+        cnt = ctypes.c_uint64()
+        check(lib().tfg_agg_result(self.h, _p(keys), _p(key_null), _ptr_array(states), _ptr_array(snulls),
+                                   ctypes.c_uint64(g), ctypes.byref(cnt)))
+        return {"keys": keys, "key_null": key_null, "states": states, "state_null": snulls}
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().tfg_agg_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# ---- a18-a21 join -----------------------------------------------------------------------------
+class Join:
+    """tfg_join: hash join v1 semantics (strictness ALL) on one fixed-width key."""
+
+    def __init__(self, ctx: Context, key_type: int, expected_build_rows: int = 0):
+        self.ctx = ctx
+        h = ctypes.c_void_p()
+        check(lib().tfg_join_create(ctx.h, key_type, ctypes.c_int64(expected_build_rows), ctypes.byref(h)))
+        self.h = h
+
+    def build(self, keys, key_nullmap=None):
+        check(lib().tfg_join_build(self.h, _p(keys), _p(key_nullmap), ctypes.c_int64(keys.shape[0])))
+
+    def finalize(self):
+        check(lib().tfg_join_finalize(self.h))
+
+    def probe(self, keys, kind: int = JOIN_INNER, key_nullmap=None, capacity: Optional[int] = None,
+              out_probe=None, out_build=None):
+        """-> (probe_idx, build_idx) int32 tensors (u32 bits; build -1 = no match)."""
+        import torch
+        n = keys.shape[0]
+        cap = capacity if capacity is not None else max(n, 1)
+        while True:
+            pi = out_probe if out_probe is not None else torch.empty(max(cap, 1), dtype=torch.int32, device=keys.device)
+            bi = out_build if out_build is not None else torch.empty(max(cap, 1), dtype=torch.int32, device=keys.device)
+            cnt = ctypes.c_uint64()
+            rc = lib().tfg_join_probe(self.h, kind, _p(keys), _p(key_nullmap), ctypes.c_int64(n), _p(pi), _p(bi),
+                                      ctypes.c_uint64(cap), ctypes.c_void_p(0), ctypes.byref(cnt))
+            if rc == TFG_ERR_CAPACITY and out_probe is None:
+                cap = cnt.value
+                continue
+            check(rc)
+            return pi[:cnt.value], bi[:cnt.value]
+
+    def stats(self):
+        r, p = ctypes.c_uint64(), ctypes.c_uint64()
+        check(lib().tfg_join_stats(self.h, ctypes.byref(r), ctypes.byref(p)))
+        return r.value, p.value
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().tfg_join_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

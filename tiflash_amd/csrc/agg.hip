@@ -1,0 +1,922 @@
+// agg.hip — hash GROUP BY (Aggregator, a9-a17) for gfx950.
+//
+// Reference: Aggregator::executeOnBlock -> executeImplBatch -> handleOneBatch
+// (Interpreters/Aggregator.cpp:776-1024): per row HashTable::emplace (Common/HashTable/HashTable.h:875-1060,
+// HashCRC32 key64), then IAggregateFunction::addBatch (AggregateFunctions/IAggregateFunction.h:242-266,
+// AggregateFunctionSum.h:64-172, AggregateFunctionCount.h:46); mergeDataImpl / MergingBuckets
+// (Aggregator.cpp:2338-2505, 2940-3097); convertToBlockImplFinal (:1651-1780).
+//
+// GPU design (the radix-bucketed analogue of TwoLevelHashTable's 256 buckets):
+//   1. bucket pass — fused predicate + CRC32-C key hash + LDS-histogram partition of the
+//      (key, args) rows into B = 2^bucket_bits buckets (bucket = crc & (B-1));
+//   2. bucket kernel — one workgroup per bucket builds an open-addressing table in LDS
+//      (linear probing, 64-bit ds_cmpst for keys, ds_add_{u64,f64} for states, key 0 and the
+//      NULL key in side slots like ZeroValueStorage) seeded with the bucket's existing groups,
+//      aggregates the staged rows, and writes its groups out.  If a bucket holds more distinct
+//      keys than the LDS table, rows of keys not in the table are compacted in place and the
+//      bucket iterates (each pass finalises >= maxfill groups), so any distribution is correct;
+//   3. compaction — scan of per-bucket group counts -> groups stored bucket-major as the state.
+// Group state is columnar in HBM: key bits (u64), NULL-key flag, per aggregate an accumulator
+// (Int64/UInt64/Float64 or Int128) and a non-NULL row count.
+#include <algorithm>
+#include <vector>
+
+#include "common.h"
+#include "partition.h"
+
+namespace tfg {
+
+constexpr int AGG_MAX = 4;
+constexpr int BT = 512; // bucket kernel threads
+constexpr int LDS_TABLE_BYTES = 64 * 1024;
+
+enum AccKind { ACC_NONE = 0, ACC_I64 = 1, ACC_F64 = 2, ACC_I128 = 3 };
+enum RowMode { MODE_RAW = 0, MODE_PARTIAL = 1, MODE_STATE = 2 };
+
+struct AggSpec {
+    int key_width; // bytes of the key column (1,2,4,8); 0 = without key
+    int n_aggs;
+    int kind[AGG_MAX];
+    int acc[AGG_MAX];     // AccKind (SUM only)
+    int has_cnt[AGG_MAX]; // count slot present
+    int src_type[AGG_MAX];
+    // LDS layout (byte offsets into dynamic LDS)
+    int cap;      // table cells (power of two); slots cap (key 0) and cap+1 (NULL key) follow
+    int maxfill;  // sticky "full" threshold
+    int acc_off[AGG_MAX];
+    int cnt_off[AGG_MAX];
+    int ctrl_off;
+    int lds_bytes;
+};
+
+// Columnar row source staged by the bucket pass (bucket-major).
+struct RowsIO {
+    int key_width;                // bytes per key (raw key width, or 8 for STATE rows)
+    void *key;                    // key_width bytes per row
+    uint8_t *key_null;            // optional
+    void *val[AGG_MAX];           // RAW: arg type; PARTIAL: result type; STATE: acc
+    uint8_t *val_null[AGG_MAX];   // RAW / PARTIAL: optional null flags
+    uint64_t *val_cnt[AGG_MAX];   // STATE: counts
+};
+
+// Columnar groups (state / temp).
+struct GroupsIO {
+    uint64_t *key;
+    uint8_t *key_null;
+    void *acc[AGG_MAX];
+    uint64_t *cnt[AGG_MAX];
+};
+
+struct Ctrl {
+    unsigned used;
+    unsigned full;
+    unsigned zero_used;
+    unsigned null_used;
+    unsigned long long out_count;
+    unsigned long long spill_w;
+};
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) { // splitmix64 finaliser: slot hash inside a bucket
+    x ^= x >> 30;
+    x *= 0xbf58476d1ce4e5b9ull;
+    x ^= x >> 27;
+    x *= 0x94d049bb133111ebull;
+    x ^= x >> 31;
+    return x;
+}
+
+__device__ __forceinline__ uint64_t load_bits(const void *p, int width, int64_t i) {
+    switch (width) {
+    case 1: return ((const uint8_t *)p)[i];
+    case 2: return ((const uint16_t *)p)[i];
+    case 4: return ((const uint32_t *)p)[i];
+    default: return ((const uint64_t *)p)[i];
+    }
+}
+
+// value of a SUM argument widened to the accumulator
+__device__ __forceinline__ void load_sum_value(int type, const void *p, int64_t i, uint64_t &lo, uint64_t &hi, double &f) {
+    switch (type) {
+    case TFG_INT8: lo = (uint64_t)(int64_t)((const int8_t *)p)[i]; break;
+    case TFG_INT16: lo = (uint64_t)(int64_t)((const int16_t *)p)[i]; break;
+    case TFG_INT32: case TFG_DECIMAL32: lo = (uint64_t)(int64_t)((const int32_t *)p)[i]; break;
+    case TFG_INT64: case TFG_DECIMAL64: lo = ((const uint64_t *)p)[i]; break;
+    case TFG_UINT8: lo = ((const uint8_t *)p)[i]; hi = 0; return;
+    case TFG_UINT16: lo = ((const uint16_t *)p)[i]; hi = 0; return;
+    case TFG_UINT32: lo = ((const uint32_t *)p)[i]; hi = 0; return;
+    case TFG_UINT64: lo = ((const uint64_t *)p)[i]; hi = 0; return;
+    case TFG_FLOAT32: f = ((const float *)p)[i]; return;
+    case TFG_FLOAT64: f = ((const double *)p)[i]; return;
+    case TFG_DECIMAL128: lo = ((const uint64_t *)p)[2 * i]; hi = ((const uint64_t *)p)[2 * i + 1]; return;
+    default: lo = 0; break;
+    }
+    hi = (int64_t)lo < 0 ? ~0ull : 0ull; // sign extension into Int128
+}
+
+__device__ __forceinline__ void lds_add_i128(uint64_t *cell, uint64_t lo, uint64_t hi) {
+    const uint64_t old = atomicAdd((unsigned long long *)&cell[0], (unsigned long long)lo);
+    const uint64_t carry = (old + lo) < old ? 1ull : 0ull;
+    atomicAdd((unsigned long long *)&cell[1], (unsigned long long)(hi + carry));
+}
+
+struct Table {
+    uint64_t *keys;
+    char *base;
+    Ctrl *ctrl;
+    const AggSpec &S;
+    __device__ Table(char *lds, const AggSpec &s)
+        : keys(reinterpret_cast<uint64_t *>(lds)), base(lds), ctrl(reinterpret_cast<Ctrl *>(lds + s.ctrl_off)), S(s) {}
+
+    __device__ void clear() {
+        uint32_t *w = reinterpret_cast<uint32_t *>(base);
+        const int words = S.ctrl_off / 4;
+        for (int i = threadIdx.x; i < words; i += blockDim.x) w[i] = 0;
+        if (threadIdx.x == 0) {
+            ctrl->used = ctrl->full = ctrl->zero_used = ctrl->null_used = 0;
+            ctrl->spill_w = 0;
+        }
+    }
+
+    // returns the cell of `key`, inserting it when allowed; -1 = not in the table
+    __device__ __forceinline__ int find_or_insert(uint64_t key, bool is_null, bool may_insert, bool force) {
+        if (is_null) {
+            if (!ctrl->null_used) ctrl->null_used = 1;
+            return S.cap + 1;
+        }
+        if (key == 0) { // ZeroValueStorage
+            if (!ctrl->zero_used) ctrl->zero_used = 1;
+            return S.cap;
+        }
+        const unsigned mask = (unsigned)S.cap - 1;
+        unsigned pos = (unsigned)mix64(key) & mask;
+        for (int probe = 0; probe < S.cap; ++probe) {
+            const uint64_t k = __hip_atomic_load(&keys[pos], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (k == key) return (int)pos;
+            if (k == 0) {
+                if (!may_insert || (!force && __hip_atomic_load(&ctrl->full, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
+                    return -1;
+                const uint64_t old = atomicCAS((unsigned long long *)&keys[pos], 0ull, (unsigned long long)key);
+                if (old == 0) {
+                    const unsigned u = atomicAdd(&ctrl->used, 1u) + 1;
+                    if (u >= (unsigned)S.maxfill) ctrl->full = 1;
+                    return (int)pos;
+                }
+                if (old == key) return (int)pos;
+            }
+            pos = (pos + 1) & mask;
+        }
+        return -1;
+    }
+
+    __device__ __forceinline__ uint64_t *acc_cell(int i, int cell) const {
+        const int w = S.acc[i] == ACC_I128 ? 2 : 1;
+        return reinterpret_cast<uint64_t *>(base + S.acc_off[i]) + (int64_t)cell * w;
+    }
+    __device__ __forceinline__ uint64_t *cnt_cell(int i, int cell) const {
+        return reinterpret_cast<uint64_t *>(base + S.cnt_off[i]) + cell;
+    }
+
+    // fold row `r` of `rows` (mode) into cell
+    __device__ __forceinline__ void add_row(int cell, const RowsIO &rows, int64_t r, int mode) {
+        for (int i = 0; i < S.n_aggs; ++i) {
+            const int kind = S.kind[i];
+            if (mode == MODE_STATE) {
+                if (S.acc[i] == ACC_I128) {
+                    const uint64_t *v = (const uint64_t *)rows.val[i] + 2 * r;
+                    lds_add_i128(acc_cell(i, cell), v[0], v[1]);
+                } else if (S.acc[i] == ACC_F64) {
+                    atomicAdd((double *)acc_cell(i, cell), ((const double *)rows.val[i])[r]);
+                } else if (S.acc[i] == ACC_I64) {
+                    atomicAdd((unsigned long long *)acc_cell(i, cell), ((const unsigned long long *)rows.val[i])[r]);
+                }
+                if (S.has_cnt[i]) atomicAdd((unsigned long long *)cnt_cell(i, cell), rows.val_cnt[i][r]);
+                continue;
+            }
+            if (kind == TFG_AGG_COUNT_ALL && mode == MODE_RAW) {
+                atomicAdd((unsigned long long *)cnt_cell(i, cell), 1ull);
+                continue;
+            }
+            if (rows.val_null[i] && rows.val_null[i][r]) continue;
+            if (kind != TFG_AGG_SUM) { // COUNT (raw: +1) or partial count (+value)
+                const unsigned long long inc = mode == MODE_RAW ? 1ull : ((const unsigned long long *)rows.val[i])[r];
+                atomicAdd((unsigned long long *)cnt_cell(i, cell), inc);
+                continue;
+            }
+            uint64_t lo = 0, hi = 0;
+            double f = 0;
+            load_sum_value(S.src_type[i], rows.val[i], r, lo, hi, f);
+            if (S.acc[i] == ACC_F64) atomicAdd((double *)acc_cell(i, cell), f);
+            else if (S.acc[i] == ACC_I128) lds_add_i128(acc_cell(i, cell), lo, hi);
+            else atomicAdd((unsigned long long *)acc_cell(i, cell), (unsigned long long)lo);
+            if (S.has_cnt[i]) atomicAdd((unsigned long long *)cnt_cell(i, cell), 1ull);
+        }
+    }
+
+    // fold group g of `grp` (state) into cell
+    __device__ __forceinline__ void add_group(int cell, const GroupsIO &grp, int64_t g) {
+        for (int i = 0; i < S.n_aggs; ++i) {
+            if (S.acc[i] == ACC_I128) {
+                const uint64_t *v = (const uint64_t *)grp.acc[i] + 2 * g;
+                lds_add_i128(acc_cell(i, cell), v[0], v[1]);
+            } else if (S.acc[i] == ACC_F64) {
+                atomicAdd((double *)acc_cell(i, cell), ((const double *)grp.acc[i])[g]);
+            } else if (S.acc[i] == ACC_I64) {
+                atomicAdd((unsigned long long *)acc_cell(i, cell), ((const unsigned long long *)grp.acc[i])[g]);
+            }
+            if (S.has_cnt[i]) atomicAdd((unsigned long long *)cnt_cell(i, cell), grp.cnt[i][g]);
+        }
+    }
+
+    __device__ void flush(const GroupsIO &out, uint64_t out_base) {
+        for (int c = threadIdx.x; c < S.cap + 2; c += blockDim.x) {
+            bool occ;
+            uint64_t key = 0;
+            uint8_t isnull = 0;
+            if (c < S.cap) {
+                key = keys[c];
+                occ = key != 0;
+            } else if (c == S.cap) {
+                occ = ctrl->zero_used;
+            } else {
+                occ = ctrl->null_used;
+                isnull = 1;
+            }
+            if (!occ) continue;
+            const uint64_t pos = out_base + atomicAdd(&ctrl->out_count, 1ull);
+            out.key[pos] = key;
+            out.key_null[pos] = isnull;
+            for (int i = 0; i < S.n_aggs; ++i) {
+                if (S.acc[i] == ACC_I128) {
+                    const uint64_t *a = acc_cell(i, c);
+                    ((uint64_t *)out.acc[i])[2 * pos] = a[0];
+                    ((uint64_t *)out.acc[i])[2 * pos + 1] = a[1];
+                } else if (S.acc[i] != ACC_NONE) {
+                    ((uint64_t *)out.acc[i])[pos] = *acc_cell(i, c);
+                }
+                if (S.has_cnt[i]) out.cnt[i][pos] = *cnt_cell(i, c);
+            }
+        }
+    }
+};
+
+// copy row r of `rows` to slot w (in-place compaction of the bucket's pending rows)
+__device__ __forceinline__ void move_row(const AggSpec &S, const RowsIO &rows, int mode, int64_t r, int64_t w) {
+    if (r == w) return;
+    switch (rows.key_width) {
+    case 1: ((uint8_t *)rows.key)[w] = ((const uint8_t *)rows.key)[r]; break;
+    case 2: ((uint16_t *)rows.key)[w] = ((const uint16_t *)rows.key)[r]; break;
+    case 4: ((uint32_t *)rows.key)[w] = ((const uint32_t *)rows.key)[r]; break;
+    default: ((uint64_t *)rows.key)[w] = ((const uint64_t *)rows.key)[r]; break;
+    }
+    if (rows.key_null) rows.key_null[w] = rows.key_null[r];
+    for (int i = 0; i < S.n_aggs; ++i) {
+        if (rows.val[i]) {
+            int w8 = 8;
+            if (mode == MODE_RAW) w8 = (int)(S.src_type[i] == TFG_DECIMAL128 ? 16 : 0);
+            if (mode == MODE_RAW && w8 == 0) {
+                switch (S.src_type[i]) {
+                case TFG_INT8: case TFG_UINT8: ((uint8_t *)rows.val[i])[w] = ((const uint8_t *)rows.val[i])[r]; break;
+                case TFG_INT16: case TFG_UINT16: ((uint16_t *)rows.val[i])[w] = ((const uint16_t *)rows.val[i])[r]; break;
+                case TFG_INT32: case TFG_UINT32: case TFG_FLOAT32: case TFG_DECIMAL32:
+                    ((uint32_t *)rows.val[i])[w] = ((const uint32_t *)rows.val[i])[r]; break;
+                default: ((uint64_t *)rows.val[i])[w] = ((const uint64_t *)rows.val[i])[r]; break;
+                }
+            } else if (S.acc[i] == ACC_I128 || w8 == 16) {
+                ((uint4 *)rows.val[i])[w] = ((const uint4 *)rows.val[i])[r];
+            } else {
+                ((uint64_t *)rows.val[i])[w] = ((const uint64_t *)rows.val[i])[r];
+            }
+        }
+        if (rows.val_null[i]) rows.val_null[i][w] = rows.val_null[i][r];
+        if (rows.val_cnt[i]) rows.val_cnt[i][w] = rows.val_cnt[i][r];
+    }
+}
+
+__global__ void __launch_bounds__(BT) agg_bucket_kernel(AggSpec S, RowsIO rows, int mode, const uint64_t *stage_off,
+                                                        GroupsIO old, const uint64_t *old_off, GroupsIO out,
+                                                        uint64_t *out_cnt) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    Table T(lds, S);
+    const int b = blockIdx.x;
+    const int64_t rs = (int64_t)stage_off[b];
+    int64_t pending = (int64_t)stage_off[b + 1] - rs;
+    int64_t os = 0, oe = 0;
+    if (old_off) {
+        os = (int64_t)old_off[b];
+        oe = (int64_t)old_off[b + 1];
+    }
+    const uint64_t out_base = (uint64_t)os + (uint64_t)rs;
+    int64_t old_cursor = os;
+    if (threadIdx.x == 0) T.ctrl->out_count = 0;
+    while (pending > 0 || old_cursor < oe) {
+        T.clear();
+        __syncthreads();
+        // phase A: a chunk of existing groups (distinct keys)
+        int64_t take = oe - old_cursor;
+        if (take > S.maxfill) take = S.maxfill;
+        for (int64_t g = old_cursor + threadIdx.x; g < old_cursor + take; g += BT) {
+            const int cell = T.find_or_insert(old.key[g], old.key_null[g] != 0, true, true);
+            T.add_group(cell, old, g);
+        }
+        old_cursor += take;
+        const bool allow_insert = old_cursor >= oe;
+        __syncthreads();
+        // phase B: pending rows, misses compacted in place for the next pass
+        for (int64_t base = 0; base < pending; base += BT) {
+            const int64_t r = rs + base + threadIdx.x;
+            const bool valid = base + threadIdx.x < pending;
+            uint64_t key = 0;
+            bool knull = false;
+            if (valid) {
+                key = load_bits(rows.key, rows.key_width, r);
+                knull = rows.key_null && rows.key_null[r];
+            }
+            __syncthreads(); // every row of this step is in registers before any in-place write
+            int cell = -1;
+            if (valid) {
+                cell = T.find_or_insert(key, knull, allow_insert, false);
+                if (cell >= 0) T.add_row(cell, rows, r, mode);
+            }
+            __syncthreads(); // inserts of this step are complete: a retry sees the final key set
+            if (valid && cell < 0) {
+                cell = T.find_or_insert(key, knull, false, false);
+                if (cell >= 0) {
+                    T.add_row(cell, rows, r, mode);
+                } else {
+                    const int64_t w = rs + (int64_t)atomicAdd(&T.ctrl->spill_w, 1ull);
+                    move_row(S, rows, mode, r, w);
+                }
+            }
+        }
+        __syncthreads();
+        T.flush(out, out_base);
+        __syncthreads();
+        pending = (int64_t)T.ctrl->spill_w;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out_cnt[b] = T.ctrl->out_count;
+}
+
+// temp (bucket-strided) groups -> compact state
+__global__ void agg_compact_kernel(AggSpec S, GroupsIO tmp, const uint64_t *stage_off, const uint64_t *old_off,
+                                   const uint64_t *new_off, GroupsIO dst) {
+    const int b = blockIdx.x;
+    const uint64_t src0 = stage_off[b] + (old_off ? old_off[b] : 0);
+    const uint64_t d0 = new_off[b], cnt = new_off[b + 1] - d0;
+    for (uint64_t j = threadIdx.x; j < cnt; j += blockDim.x) {
+        const uint64_t s = src0 + j, d = d0 + j;
+        dst.key[d] = tmp.key[s];
+        dst.key_null[d] = tmp.key_null[s];
+        for (int i = 0; i < S.n_aggs; ++i) {
+            if (S.acc[i] == ACC_I128) ((uint4 *)dst.acc[i])[d] = ((const uint4 *)tmp.acc[i])[s];
+            else if (S.acc[i] != ACC_NONE) ((uint64_t *)dst.acc[i])[d] = ((const uint64_t *)tmp.acc[i])[s];
+            if (S.has_cnt[i]) dst.cnt[i][d] = tmp.cnt[i][s];
+        }
+    }
+}
+
+// ---------------------------------------------------------------- without key (single group)
+constexpr int NK_T = 256;
+struct NoKeyPartial {
+    uint64_t lo[AGG_MAX], hi[AGG_MAX], cnt[AGG_MAX];
+    double f[AGG_MAX];
+};
+
+__global__ void __launch_bounds__(NK_T) agg_nokey_kernel(AggSpec S, RowsIO rows, int mode, RowPred pred, int64_t n,
+                                                         NoKeyPartial *partials) {
+    NoKeyPartial p;
+    for (int i = 0; i < AGG_MAX; ++i) p.lo[i] = p.hi[i] = p.cnt[i] = 0, p.f[i] = 0;
+    for (int64_t r = (int64_t)blockIdx.x * NK_T + threadIdx.x; r < n; r += (int64_t)gridDim.x * NK_T) {
+        if (!pred(r)) continue;
+        for (int i = 0; i < S.n_aggs; ++i) {
+            if (mode == MODE_RAW && S.kind[i] == TFG_AGG_COUNT_ALL) { p.cnt[i]++; continue; }
+            if (rows.val_null[i] && rows.val_null[i][r]) continue;
+            if (S.kind[i] != TFG_AGG_SUM) {
+                p.cnt[i] += mode == MODE_RAW ? 1 : ((const uint64_t *)rows.val[i])[r];
+                continue;
+            }
+            uint64_t lo = 0, hi = 0;
+            double f = 0;
+            load_sum_value(S.src_type[i], rows.val[i], r, lo, hi, f);
+            if (S.acc[i] == ACC_F64) p.f[i] += f;
+            else {
+                const uint64_t o = p.lo[i];
+                p.lo[i] += lo;
+                p.hi[i] += hi + (p.lo[i] < o ? 1 : 0);
+            }
+            p.cnt[i]++;
+        }
+    }
+    // block reduction through LDS, in thread order
+    __shared__ NoKeyPartial red[NK_T];
+    red[threadIdx.x] = p;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        NoKeyPartial s = red[0];
+        for (int t = 1; t < NK_T; ++t)
+            for (int i = 0; i < S.n_aggs; ++i) {
+                const uint64_t o = s.lo[i];
+                s.lo[i] += red[t].lo[i];
+                s.hi[i] += red[t].hi[i] + (s.lo[i] < o ? 1 : 0);
+                s.f[i] += red[t].f[i];
+                s.cnt[i] += red[t].cnt[i];
+            }
+        partials[blockIdx.x] = s;
+    }
+}
+
+__global__ void agg_nokey_fold_kernel(AggSpec S, const NoKeyPartial *partials, int np, GroupsIO st) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    for (int b = 0; b < np; ++b)
+        for (int i = 0; i < S.n_aggs; ++i) {
+            const NoKeyPartial &p = partials[b];
+            if (S.acc[i] == ACC_F64) ((double *)st.acc[i])[0] += p.f[i];
+            else if (S.acc[i] == ACC_I128) {
+                uint64_t *a = (uint64_t *)st.acc[i];
+                const uint64_t o = a[0];
+                a[0] += p.lo[i];
+                a[1] += p.hi[i] + (a[0] < o ? 1 : 0);
+            } else if (S.acc[i] == ACC_I64) ((uint64_t *)st.acc[i])[0] += p.lo[i];
+            if (S.has_cnt[i]) st.cnt[i][0] += p.cnt[i];
+        }
+}
+
+// ---------------------------------------------------------------- result
+struct ResultPtrs {
+    void *state[AGG_MAX];
+    uint8_t *state_null[AGG_MAX];
+};
+
+__global__ void agg_result_kernel(AggSpec S, GroupsIO st, uint64_t n, int key_width, void *out_keys,
+                                  uint8_t *out_key_null, ResultPtrs res) {
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (uint64_t)gridDim.x * blockDim.x) {
+        if (out_keys) {
+            const uint64_t k = st.key[g];
+            switch (key_width) {
+            case 1: ((uint8_t *)out_keys)[g] = (uint8_t)k; break;
+            case 2: ((uint16_t *)out_keys)[g] = (uint16_t)k; break;
+            case 4: ((uint32_t *)out_keys)[g] = (uint32_t)k; break;
+            case 8: ((uint64_t *)out_keys)[g] = k; break;
+            default: break;
+            }
+        }
+        if (out_key_null) out_key_null[g] = st.key_null[g];
+        for (int i = 0; i < S.n_aggs; ++i) {
+            if (res.state[i]) {
+                if (S.kind[i] != TFG_AGG_SUM) ((uint64_t *)res.state[i])[g] = st.cnt[i][g];
+                else if (S.acc[i] == ACC_I128) ((uint4 *)res.state[i])[g] = ((const uint4 *)st.acc[i])[g];
+                else ((uint64_t *)res.state[i])[g] = ((const uint64_t *)st.acc[i])[g];
+            }
+            if (res.state_null[i])
+                res.state_null[i][g] = (S.kind[i] == TFG_AGG_SUM && S.has_cnt[i]) ? (st.cnt[i][g] == 0) : 0;
+        }
+    }
+}
+
+__global__ void agg_state_add_kernel(AggSpec S, GroupsIO dst, GroupsIO src) { // without-key merge
+    if (threadIdx.x || blockIdx.x) return;
+    for (int i = 0; i < S.n_aggs; ++i) {
+        if (S.acc[i] == ACC_F64) ((double *)dst.acc[i])[0] += ((const double *)src.acc[i])[0];
+        else if (S.acc[i] == ACC_I128) {
+            uint64_t *a = (uint64_t *)dst.acc[i];
+            const uint64_t *b = (const uint64_t *)src.acc[i];
+            const uint64_t o = a[0];
+            a[0] += b[0];
+            a[1] += b[1] + (a[0] < o ? 1 : 0);
+        } else if (S.acc[i] == ACC_I64) ((uint64_t *)dst.acc[i])[0] += ((const uint64_t *)src.acc[i])[0];
+        if (S.has_cnt[i]) dst.cnt[i][0] += src.cnt[i][0];
+    }
+}
+
+// bucket of a key: CRC32-C of the zero-extended key bits (HashCRC32 union form, Hash.h:282-292)
+struct SelBucket {
+    const void *key;
+    const uint8_t *key_null;
+    int width;
+    uint32_t mask;
+    static constexpr bool needs_crc = true;
+    __device__ __forceinline__ uint32_t operator()(const uint32_t (*t)[256], int64_t r) const {
+        if (key_null && key_null[r]) return 0;
+        return int_hash_crc32(t, load_bits(key, width, r)) & mask;
+    }
+};
+
+} // namespace tfg
+
+using namespace tfg;
+
+struct tfg_agg {
+    Ctx *ctx = nullptr;
+    AggSpec S{};
+    int key_type = 0;
+    bool nokey = false;
+    uint32_t B = 1;
+    int arg_types[AGG_MAX] = {};
+    int arg_nullable[AGG_MAX] = {};
+    int result_type[AGG_MAX] = {};
+    int result_width[AGG_MAX] = {};
+    uint64_t n_groups = 0;
+    // double-buffered state
+    void *blk[2] = {nullptr, nullptr};
+    size_t cap[2] = {0, 0};
+    GroupsIO st[2];
+    uint64_t *bucket_off[2] = {nullptr, nullptr};
+    int cur = 0;
+
+    size_t group_bytes() const {
+        size_t b = 8 + 1;
+        for (int i = 0; i < S.n_aggs; ++i) {
+            if (S.acc[i] == ACC_I128) b += 16;
+            else if (S.acc[i] != ACC_NONE) b += 8;
+            if (S.has_cnt[i]) b += 8;
+        }
+        return b;
+    }
+    // carve a GroupsIO of `n` groups out of `base` (returns bytes used)
+    size_t carve_groups(char *base, size_t n, GroupsIO &g) const {
+        Carver cv;
+        size_t ok = cv.take<uint64_t>(n), on = cv.take<uint8_t>(n);
+        size_t oa[AGG_MAX] = {}, oc[AGG_MAX] = {};
+        for (int i = 0; i < S.n_aggs; ++i) {
+            if (S.acc[i] == ACC_I128) oa[i] = cv.take<uint4>(n);
+            else if (S.acc[i] != ACC_NONE) oa[i] = cv.take<uint64_t>(n);
+            if (S.has_cnt[i]) oc[i] = cv.take<uint64_t>(n);
+        }
+        if (base) {
+            g.key = (uint64_t *)(base + ok);
+            g.key_null = (uint8_t *)(base + on);
+            for (int i = 0; i < AGG_MAX; ++i) {
+                g.acc[i] = (i < S.n_aggs && S.acc[i] != ACC_NONE) ? base + oa[i] : nullptr;
+                g.cnt[i] = (i < S.n_aggs && S.has_cnt[i]) ? (uint64_t *)(base + oc[i]) : nullptr;
+            }
+        }
+        return cv.off;
+    }
+    int ensure_state(int idx, size_t n) {
+        if (cap[idx] >= n && blk[idx]) return TFG_OK;
+        size_t nc = std::max<size_t>(n + n / 2, 1024);
+        size_t bytes = carve_groups(nullptr, nc, st[idx]);
+        if (blk[idx]) {
+            TFG_HIP(hipStreamSynchronize(ctx->stream));
+            TFG_HIP(hipFree(blk[idx]));
+            blk[idx] = nullptr;
+        }
+        TFG_HIP(hipMalloc(&blk[idx], bytes));
+        cap[idx] = nc;
+        carve_groups((char *)blk[idx], nc, st[idx]);
+        return TFG_OK;
+    }
+};
+
+namespace {
+
+int consume_keyed(tfg_agg *a, int mode, const RowPred &pred, const void *keys, int key_width, const uint8_t *key_null,
+                  const void *const *vals, const uint8_t *const *val_nulls, const uint64_t *const *val_cnts,
+                  const uint64_t *given_off, int64_t n) {
+    Ctx *ctx = a->ctx;
+    const AggSpec &S = a->S;
+    const uint32_t B = a->B;
+    const size_t n_old = a->n_groups;
+    // ---- scratch layout
+    Carver cv;
+    const size_t o_key = cv.take<uint64_t>(n), o_knull = cv.take<uint8_t>(n);
+    size_t o_val[AGG_MAX] = {}, o_vnull[AGG_MAX] = {}, o_vcnt[AGG_MAX] = {};
+    int vw[AGG_MAX] = {};
+    for (int i = 0; i < S.n_aggs; ++i) {
+        if (!vals[i]) continue;
+        if (mode == MODE_RAW) vw[i] = (int)type_width(S.src_type[i]);
+        else vw[i] = S.acc[i] == ACC_I128 ? 16 : 8;
+        o_val[i] = cv.take<uint4>((n * vw[i] + 15) / 16);
+        if (val_nulls && val_nulls[i]) o_vnull[i] = cv.take<uint8_t>(n);
+        if (val_cnts && val_cnts[i]) o_vcnt[i] = cv.take<uint64_t>(n);
+    }
+    const size_t o_stage_off = cv.take<uint64_t>(B + 1);
+    const size_t o_new_cnt = cv.take<uint64_t>(B), o_new_off = cv.take<uint64_t>(B + 1);
+    const size_t tmp_groups = n_old + (size_t)n;
+    const size_t o_tmpg = cv.take<uint8_t>(a->carve_groups(nullptr, tmp_groups, a->st[0]) + 256);
+    PartLayout L = make_layout(n, B);
+    const size_t o_part = cv.take<uint8_t>(std::max(part_tmp_bytes(L), scan_tmp_bytes(B + 1)));
+    void *sp;
+    if (int rc = scratch_get(ctx, cv.off, &sp)) return rc;
+    char *sb = (char *)sp;
+    // ---- stage rows (bucket-major)
+    RowsIO rows{};
+    rows.key_width = key_width;
+    rows.key = sb + o_key;
+    rows.key_null = key_null ? (uint8_t *)(sb + o_knull) : nullptr;
+    uint64_t *stage_off = (uint64_t *)(sb + o_stage_off);
+    if (given_off) {
+        // rows already bucket-major (merge of a state with the same bucket function): copy
+        TFG_HIP(hipMemcpyAsync(rows.key, keys, n * key_width, hipMemcpyDeviceToDevice, ctx->stream));
+        if (key_null) TFG_HIP(hipMemcpyAsync(rows.key_null, key_null, n, hipMemcpyDeviceToDevice, ctx->stream));
+        for (int i = 0; i < S.n_aggs; ++i) {
+            if (vals[i]) {
+                rows.val[i] = sb + o_val[i];
+                TFG_HIP(hipMemcpyAsync(rows.val[i], vals[i], n * vw[i], hipMemcpyDeviceToDevice, ctx->stream));
+            }
+            if (val_cnts && val_cnts[i]) {
+                rows.val_cnt[i] = (uint64_t *)(sb + o_vcnt[i]);
+                TFG_HIP(hipMemcpyAsync(rows.val_cnt[i], val_cnts[i], n * 8, hipMemcpyDeviceToDevice, ctx->stream));
+            }
+        }
+        TFG_HIP(hipMemcpyAsync(stage_off, given_off, (B + 1) * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    } else {
+        PCols pc{};
+        pc.in[pc.ncols] = keys;
+        pc.out[pc.ncols] = rows.key;
+        pc.width[pc.ncols++] = key_width;
+        if (key_null) {
+            pc.in[pc.ncols] = key_null;
+            pc.out[pc.ncols] = rows.key_null;
+            pc.width[pc.ncols++] = 1;
+        }
+        for (int i = 0; i < S.n_aggs; ++i) {
+            if (vals[i]) {
+                rows.val[i] = sb + o_val[i];
+                pc.in[pc.ncols] = vals[i];
+                pc.out[pc.ncols] = rows.val[i];
+                pc.width[pc.ncols++] = vw[i];
+            }
+            if (val_nulls && val_nulls[i]) {
+                rows.val_null[i] = (uint8_t *)(sb + o_vnull[i]);
+                pc.in[pc.ncols] = val_nulls[i];
+                pc.out[pc.ncols] = rows.val_null[i];
+                pc.width[pc.ncols++] = 1;
+            }
+        }
+        TFG_CHECK(pc.ncols <= PCOLS, TFG_ERR_NOT_IMPLEMENTED, "too many aggregate columns");
+        SelBucket sel{keys, key_null, key_width, B - 1};
+        if (int rc = run_partition<SelBucket, false>(ctx, sel, pred, L, pc, nullptr, nullptr, stage_off, sb + o_part))
+            return rc;
+    }
+    // ---- bucket kernel
+    GroupsIO tmp{};
+    a->carve_groups(sb + o_tmpg, tmp_groups, tmp);
+    uint64_t *new_cnt = (uint64_t *)(sb + o_new_cnt), *new_off = (uint64_t *)(sb + o_new_off);
+    const bool has_old = n_old > 0;
+    GroupsIO old = a->st[a->cur];
+    hipLaunchKernelGGL(agg_bucket_kernel, dim3(B), dim3(BT), S.lds_bytes, ctx->stream, S, rows, mode, stage_off, old,
+                       has_old ? a->bucket_off[a->cur] : (const uint64_t *)nullptr, tmp, new_cnt);
+    TFG_LAUNCH_CHECK();
+    if (int rc = exclusive_scan_u64(ctx, new_cnt, new_off, B, sb + o_part)) return rc;
+    uint64_t total = 0;
+    if (int rc = read_back_u64(ctx, new_off + B, &total, 1)) return rc;
+    const int nxt = a->cur ^ 1;
+    if (int rc = a->ensure_state(nxt, total)) return rc;
+    if (!a->bucket_off[nxt]) TFG_HIP(hipMalloc(&a->bucket_off[nxt], (B + 1) * 8));
+    hipLaunchKernelGGL(agg_compact_kernel, dim3(B), dim3(256), 0, ctx->stream, S, tmp, stage_off,
+                       has_old ? a->bucket_off[a->cur] : (const uint64_t *)nullptr, new_off, a->st[nxt]);
+    TFG_LAUNCH_CHECK();
+    TFG_HIP(hipMemcpyAsync(a->bucket_off[nxt], new_off, (B + 1) * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    a->cur = nxt;
+    a->n_groups = total;
+    return TFG_OK;
+}
+
+int consume_nokey(tfg_agg *a, int mode, const RowPred &pred, const void *const *vals, const uint8_t *const *val_nulls,
+                  int64_t n) {
+    Ctx *ctx = a->ctx;
+    RowsIO rows{};
+    for (int i = 0; i < a->S.n_aggs; ++i) {
+        rows.val[i] = (void *)vals[i];
+        rows.val_null[i] = val_nulls ? (uint8_t *)val_nulls[i] : nullptr;
+    }
+    const unsigned grid = stream_grid(n, NK_T * 16, 1024);
+    void *sp;
+    if (int rc = scratch_get(ctx, grid * sizeof(NoKeyPartial), &sp)) return rc;
+    hipLaunchKernelGGL(agg_nokey_kernel, dim3(grid), dim3(NK_T), 0, ctx->stream, a->S, rows, mode, pred, n,
+                       (NoKeyPartial *)sp);
+    hipLaunchKernelGGL(agg_nokey_fold_kernel, dim3(1), dim3(64), 0, ctx->stream, a->S, (const NoKeyPartial *)sp,
+                       (int)grid, a->st[a->cur]);
+    TFG_LAUNCH_CHECK();
+    return TFG_OK;
+}
+
+int sum_acc_kind(int t) {
+    if (t == TFG_FLOAT32 || t == TFG_FLOAT64) return ACC_F64;
+    if (is_decimal_type(t)) return ACC_I128;
+    return ACC_I64;
+}
+
+int consume_common(tfg_agg *a, int mode, const RowPred &pred, const void *keys, const uint8_t *key_nullmap,
+                   const void *const *args, const uint8_t *const *arg_nullmaps, int64_t n) {
+    TFG_CHECK(a, TFG_ERR_INVALID_ARG, "agg is null");
+    TFG_CHECK(n >= 0 && n < (int64_t)0xFFFFFFFFll, TFG_ERR_INVALID_ARG, "row count out of range");
+    if (failpoint("agg_consume")) return fail(TFG_ERR_FAULT_INJECTED, "failpoint agg_consume");
+    if (n == 0) return TFG_OK;
+    if (int rc = set_device(a->ctx)) return rc;
+    const void *vals[AGG_MAX] = {};
+    const uint8_t *vnull[AGG_MAX] = {};
+    for (int i = 0; i < a->S.n_aggs; ++i) {
+        if (mode == MODE_RAW && a->S.kind[i] == TFG_AGG_COUNT_ALL) continue;
+        TFG_CHECK(args && args[i], TFG_ERR_INVALID_ARG, "argument %d is null", i);
+        vals[i] = args[i];
+        vnull[i] = arg_nullmaps ? arg_nullmaps[i] : nullptr;
+        if (vnull[i] && mode == MODE_RAW && a->S.kind[i] == TFG_AGG_SUM && !a->S.has_cnt[i])
+            return fail(TFG_ERR_ILLEGAL_TYPE, "argument %d has a null map but was declared not nullable", i);
+    }
+    if (a->nokey) return consume_nokey(a, mode, pred, vals, vnull, n);
+    TFG_CHECK(keys, TFG_ERR_INVALID_ARG, "keys are null");
+    return consume_keyed(a, mode, pred, keys, (int)type_width(a->key_type), key_nullmap, vals, vnull, nullptr, nullptr,
+                         n);
+}
+
+} // namespace
+
+extern "C" {
+
+int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds, const int *arg_types,
+                   const int *arg_scales, const tfg_agg_params *params, tfg_agg **out) {
+    TFG_CHECK(ctx && out && agg_kinds, TFG_ERR_INVALID_ARG, "null argument");
+    TFG_CHECK(n_aggs >= 1 && n_aggs <= AGG_MAX, TFG_ERR_NOT_IMPLEMENTED, "n_aggs %d out of range [1,%d]", n_aggs, AGG_MAX);
+    TFG_CHECK(key_type == 0 || (type_width(key_type) > 0 && type_width(key_type) <= 8), TFG_ERR_ILLEGAL_TYPE,
+              "unsupported GROUP BY key type %d", key_type);
+    if (int rc = set_device(ctx)) return rc;
+    tfg_agg *a = new tfg_agg();
+    a->ctx = ctx;
+    a->key_type = key_type;
+    a->nokey = key_type == 0;
+    AggSpec &S = a->S;
+    S.key_width = (int)type_width(key_type);
+    S.n_aggs = n_aggs;
+    int cell = 8;
+    for (int i = 0; i < n_aggs; ++i) {
+        const int kind = agg_kinds[i];
+        const int at = arg_types ? (arg_types[i] & 0xFF) : 0;
+        const bool nullable = arg_types && (arg_types[i] & 0x100);
+        if (kind < TFG_AGG_SUM || kind > TFG_AGG_COUNT_ALL) {
+            delete a;
+            return fail(TFG_ERR_NOT_IMPLEMENTED, "aggregate kind %d not supported", kind);
+        }
+        S.kind[i] = kind;
+        S.src_type[i] = at;
+        a->arg_types[i] = at;
+        a->arg_nullable[i] = nullable;
+        if (kind == TFG_AGG_SUM) {
+            if (!(is_fixed_numeric(at) || is_decimal_type(at))) {
+                delete a;
+                return fail(TFG_ERR_ILLEGAL_TYPE, "sum over type %d not supported", at);
+            }
+            S.acc[i] = sum_acc_kind(at);
+            S.has_cnt[i] = nullable ? 1 : 0;
+            a->result_type[i] = S.acc[i] == ACC_F64 ? TFG_FLOAT64
+                                : S.acc[i] == ACC_I128 ? TFG_DECIMAL128
+                                : is_unsigned_type(at) ? TFG_UINT64 : TFG_INT64;
+            a->result_width[i] = S.acc[i] == ACC_I128 ? 16 : 8;
+            cell += S.acc[i] == ACC_I128 ? 16 : 8;
+        } else {
+            S.acc[i] = ACC_NONE;
+            S.has_cnt[i] = 1;
+            a->result_type[i] = TFG_UINT64;
+            a->result_width[i] = 8;
+        }
+        if (S.has_cnt[i]) cell += 8;
+        (void)arg_scales;
+    }
+    // LDS table geometry
+    int cap = 1;
+    while ((size_t)(cap * 2 + 2) * cell <= (size_t)LDS_TABLE_BYTES) cap *= 2;
+    S.cap = cap;
+    S.maxfill = std::max(1, std::min(cap * 5 / 8, cap - BT - 8));
+    int off = (cap + 2) * 8;
+    for (int i = 0; i < n_aggs; ++i) {
+        if (S.acc[i] != ACC_NONE) {
+            S.acc_off[i] = off;
+            off += (cap + 2) * (S.acc[i] == ACC_I128 ? 16 : 8);
+        }
+        if (S.has_cnt[i]) {
+            S.cnt_off[i] = off;
+            off += (cap + 2) * 8;
+        }
+    }
+    S.ctrl_off = off;
+    S.lds_bytes = off + (int)sizeof(Ctrl) + 16;
+    // buckets
+    int bbits = params ? params->bucket_bits : 0;
+    if (bbits <= 0) {
+        int64_t eg = (params && params->expected_groups > 0) ? params->expected_groups : (1 << 20);
+        int64_t want = eg / std::max(1, S.maxfill / 2);
+        bbits = 4;
+        while (bbits < 12 && ((int64_t)1 << bbits) < want) ++bbits;
+    }
+    if (bbits > 12) bbits = 12;
+    a->B = a->nokey ? 1 : (1u << bbits);
+    if (a->nokey) {
+        if (int rc = a->ensure_state(0, 1)) {
+            delete a;
+            return rc;
+        }
+        size_t bytes = a->carve_groups(nullptr, a->cap[0], a->st[0]);
+        TFG_HIP(hipMemsetAsync(a->blk[0], 0, bytes, ctx->stream));
+        a->n_groups = 1;
+    }
+    *out = a;
+    return TFG_OK;
+}
+
+int tfg_agg_destroy(tfg_agg *a) {
+    if (!a) return TFG_OK;
+    (void)hipSetDevice(a->ctx->device);
+    (void)hipStreamSynchronize(a->ctx->stream);
+    for (int i = 0; i < 2; ++i) {
+        if (a->blk[i]) (void)hipFree(a->blk[i]);
+        if (a->bucket_off[i]) (void)hipFree(a->bucket_off[i]);
+    }
+    delete a;
+    return TFG_OK;
+}
+
+int tfg_agg_consume(tfg_agg *a, const void *keys, const uint8_t *key_nullmap, const void *const *args,
+                    const uint8_t *const *arg_nullmaps, const uint8_t *mask, int64_t n) {
+    RowPred pred{};
+    if (mask) {
+        pred.kind = 1;
+        pred.col = mask;
+    }
+    return consume_common(a, MODE_RAW, pred, keys, key_nullmap, args, arg_nullmaps, n);
+}
+
+int tfg_agg_consume_filtered(tfg_agg *a, int pred_type, const void *pred_col, const uint8_t *pred_nullmap, int op,
+                             int scalar_type, const void *scalar_host, const void *keys, const uint8_t *key_nullmap,
+                             const void *const *args, const uint8_t *const *arg_nullmaps, int64_t n) {
+    TFG_CHECK(pred_col && scalar_host, TFG_ERR_INVALID_ARG, "null predicate");
+    TFG_CHECK(is_fixed_numeric(pred_type) && is_fixed_numeric(scalar_type), TFG_ERR_ILLEGAL_TYPE,
+              "unsupported predicate types %d / %d", pred_type, scalar_type);
+    TFG_CHECK(op >= TFG_EQ && op <= TFG_GE, TFG_ERR_INVALID_ARG, "bad comparison op %d", op);
+    RowPred pred{};
+    pred.kind = 2;
+    pred.type = pred_type;
+    pred.col = pred_col;
+    pred.nullmap = pred_nullmap;
+    pred.b = host_num(scalar_type, scalar_host);
+    pred.op = op;
+    return consume_common(a, MODE_RAW, pred, keys, key_nullmap, args, arg_nullmaps, n);
+}
+
+int tfg_agg_consume_partial(tfg_agg *a, const void *keys, const uint8_t *key_nullmap, const void *const *states,
+                            const uint8_t *const *state_nullmaps, int64_t n) {
+    RowPred pred{};
+    return consume_common(a, MODE_PARTIAL, pred, keys, key_nullmap, states, state_nullmaps, n);
+}
+
+int tfg_agg_merge(tfg_agg *dst, tfg_agg *src) {
+    TFG_CHECK(dst && src, TFG_ERR_INVALID_ARG, "null agg");
+    TFG_CHECK(dst->key_type == src->key_type && dst->S.n_aggs == src->S.n_aggs && dst->B == src->B,
+              TFG_ERR_LOGICAL, "merging aggregators of different signatures");
+    for (int i = 0; i < dst->S.n_aggs; ++i)
+        TFG_CHECK(dst->S.kind[i] == src->S.kind[i] && dst->S.acc[i] == src->S.acc[i] &&
+                      dst->S.has_cnt[i] == src->S.has_cnt[i],
+                  TFG_ERR_LOGICAL, "merging aggregators of different signatures");
+    TFG_HIP(hipStreamSynchronize(src->ctx->stream));
+    if (dst->nokey) {
+        hipLaunchKernelGGL(agg_state_add_kernel, dim3(1), dim3(64), 0, dst->ctx->stream, dst->S, dst->st[dst->cur],
+                           src->st[src->cur]);
+        TFG_LAUNCH_CHECK();
+        return TFG_OK;
+    }
+    if (src->n_groups == 0) return TFG_OK;
+    const GroupsIO &g = src->st[src->cur];
+    const void *vals[AGG_MAX] = {};
+    const uint64_t *cnts[AGG_MAX] = {};
+    for (int i = 0; i < src->S.n_aggs; ++i) {
+        vals[i] = g.acc[i];
+        cnts[i] = g.cnt[i];
+    }
+    RowPred pred{};
+    return consume_keyed(dst, MODE_STATE, pred, g.key, 8, g.key_null, vals, nullptr, cnts, src->bucket_off[src->cur],
+                         (int64_t)src->n_groups);
+}
+
+int tfg_agg_size(tfg_agg *a, uint64_t *out_groups) {
+    TFG_CHECK(a && out_groups, TFG_ERR_INVALID_ARG, "null argument");
+    *out_groups = a->n_groups;
+    return TFG_OK;
+}
+
+int tfg_agg_result_type(tfg_agg *a, int i, int *out_type, int *out_width) {
+    TFG_CHECK(a && i >= 0 && i < a->S.n_aggs, TFG_ERR_INVALID_ARG, "bad aggregate index");
+    if (out_type) *out_type = a->result_type[i];
+    if (out_width) *out_width = a->result_width[i];
+    return TFG_OK;
+}
+
+int tfg_agg_result(tfg_agg *a, void *out_keys, uint8_t *out_key_nullmap, void *const *out_states,
+                   uint8_t *const *out_state_nullmaps, uint64_t capacity, uint64_t *out_groups_host) {
+    TFG_CHECK(a, TFG_ERR_INVALID_ARG, "agg is null");
+    if (out_groups_host) *out_groups_host = a->n_groups;
+    if (a->n_groups > capacity) return fail(TFG_ERR_CAPACITY, "result needs %llu groups, capacity %llu",
+                                            (unsigned long long)a->n_groups, (unsigned long long)capacity);
+    if (a->n_groups == 0) return TFG_OK;
+    ResultPtrs rp{};
+    for (int i = 0; i < a->S.n_aggs; ++i) {
+        rp.state[i] = out_states ? out_states[i] : nullptr;
+        rp.state_null[i] = out_state_nullmaps ? out_state_nullmaps[i] : nullptr;
+    }
+    hipLaunchKernelGGL(agg_result_kernel, dim3(stream_grid((int64_t)a->n_groups, 256, 4096)), dim3(256), 0,
+                       a->ctx->stream, a->S, a->st[a->cur], a->n_groups, a->S.key_width,
+                       a->nokey ? nullptr : out_keys, out_key_nullmap, rp);
+    TFG_LAUNCH_CHECK();
+    return TFG_OK;
+}
+
+} // extern "C"

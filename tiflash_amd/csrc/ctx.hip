@@ -1,0 +1,323 @@
+// ctx.hip — context, memory, error state, and the device-wide scan used by every
+// count -> scan -> write pipeline (filter, partition, aggregation, join).
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+
+#include "common.h"
+
+namespace tfg {
+
+
+
+static thread_local std::string g_last_error;
+
+void set_error(const char *fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+}
+
+int fail(int code, const char *fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char *what) {
+    set_error("HIP error %d (%s) in %s", (int)e, hipGetErrorString(e), what);
+    return e == hipErrorOutOfMemory ? TFG_ERR_OOM : TFG_ERR_HIP;
+}
+
+bool failpoint(const char *name) {
+    const char *fp = getenv("TFG_FAILPOINT");
+    return fp && strcmp(fp, name) == 0;
+}
+
+size_t type_width(int t) {
+    switch (t) {
+    case TFG_INT8: case TFG_UINT8: return 1;
+    case TFG_INT16: case TFG_UINT16: return 2;
+    case TFG_INT32: case TFG_UINT32: case TFG_FLOAT32: case TFG_DECIMAL32: return 4;
+    case TFG_INT64: case TFG_UINT64: case TFG_FLOAT64: case TFG_DECIMAL64: return 8;
+    case TFG_DECIMAL128: return 16;
+    default: return 0;
+    }
+}
+
+Num host_num(int type, const void *p) {
+    Num r{0, 0, 0, 0.0};
+    switch (type) {
+    case TFG_INT8: r.s = *(const int8_t *)p; break;
+    case TFG_INT16: r.s = *(const int16_t *)p; break;
+    case TFG_INT32: case TFG_DECIMAL32: r.s = *(const int32_t *)p; break;
+    case TFG_INT64: case TFG_DECIMAL64: r.s = *(const int64_t *)p; break;
+    case TFG_UINT8: r.cls = 1; r.u = *(const uint8_t *)p; break;
+    case TFG_UINT16: r.cls = 1; r.u = *(const uint16_t *)p; break;
+    case TFG_UINT32: r.cls = 1; r.u = *(const uint32_t *)p; break;
+    case TFG_UINT64: r.cls = 1; r.u = *(const uint64_t *)p; break;
+    case TFG_FLOAT32: r.cls = 2; r.d = *(const float *)p; break;
+    case TFG_FLOAT64: r.cls = 2; r.d = *(const double *)p; break;
+    default: break;
+    }
+    return r;
+}
+
+int scratch_get(Ctx *ctx, size_t bytes, void **out) {
+    if (bytes == 0) bytes = 256;
+    if (bytes > ctx->scratch_bytes) {
+        if (ctx->scratch) {
+            TFG_HIP(hipStreamSynchronize(ctx->stream));
+            TFG_HIP(hipFree(ctx->scratch));
+            ctx->scratch = nullptr;
+            ctx->scratch_bytes = 0;
+        }
+        size_t sz = bytes + bytes / 4 + (1 << 20);
+        TFG_HIP(hipMalloc(&ctx->scratch, sz));
+        ctx->scratch_bytes = sz;
+    }
+    *out = ctx->scratch;
+    return TFG_OK;
+}
+
+int read_back_u64(Ctx *ctx, const uint64_t *dev, uint64_t *host, size_t count) {
+    TFG_CHECK(count <= 64, TFG_ERR_LOGICAL, "read_back_u64: count %zu > 64", count);
+    TFG_HIP(hipMemcpyAsync(ctx->host_pinned, dev, count * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream));
+    TFG_HIP(hipStreamSynchronize(ctx->stream));
+    memcpy(host, ctx->host_pinned, count * sizeof(uint64_t));
+    return TFG_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// exclusive scan: 1024 threads x 8 items per block (8192 entries), block sums scanned by one
+// block (<= 8192 blocks), then a fix-up pass.
+constexpr int SCAN_T = 1024, SCAN_I = 8, SCAN_TILE = SCAN_T * SCAN_I;
+
+template <typename T> __device__ __forceinline__ uint64_t block_scan_excl(uint64_t v, uint64_t *lds, uint64_t *total) {
+    // wave inclusive scan via shuffles, then wave totals in LDS
+    const unsigned lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint64_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint64_t y = __shfl_up(x, d, 64);
+        if (lane >= (unsigned)d) x += y;
+    }
+    if (lane == 63) lds[wave] = x;
+    __syncthreads();
+    if (wave == 0) {
+        const int nw = blockDim.x >> 6;
+        uint64_t w = lane < (unsigned)nw ? lds[lane] : 0;
+        uint64_t s = w;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            uint64_t y = __shfl_up(s, d, 64);
+            if (lane >= (unsigned)d) s += y;
+        }
+        if (lane < (unsigned)nw) lds[32 + lane] = s - w; // exclusive wave offsets
+        if (lane == (unsigned)nw - 1) lds[31] = s;
+    }
+    __syncthreads();
+    uint64_t r = x - v + lds[32 + wave];
+    if (total) *total = lds[31];
+    __syncthreads();
+    return r;
+}
+
+template <typename TIn>
+__global__ void __launch_bounds__(SCAN_T) scan_reduce_kernel(const TIn *in, int64_t n, uint64_t *block_sums) {
+    __shared__ uint64_t lds[64];
+    int64_t base = (int64_t)blockIdx.x * SCAN_TILE;
+    uint64_t s = 0;
+#pragma unroll
+    for (int i = 0; i < SCAN_I; ++i) {
+        int64_t idx = base + (int64_t)i * SCAN_T + threadIdx.x;
+        if (idx < n) s += (uint64_t)in[idx];
+    }
+    uint64_t tot;
+    block_scan_excl<uint64_t>(s, lds, &tot);
+    if (threadIdx.x == 0) block_sums[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(SCAN_T) scan_block_sums_kernel(uint64_t *block_sums, int64_t nb, uint64_t *total_out) {
+    __shared__ uint64_t lds[64];
+    // nb <= SCAN_TILE; each thread owns SCAN_I consecutive entries
+    uint64_t v[SCAN_I];
+    uint64_t s = 0;
+#pragma unroll
+    for (int i = 0; i < SCAN_I; ++i) {
+        int64_t idx = (int64_t)threadIdx.x * SCAN_I + i;
+        v[i] = idx < nb ? block_sums[idx] : 0;
+        s += v[i];
+    }
+    uint64_t tot;
+    uint64_t off = block_scan_excl<uint64_t>(s, lds, &tot);
+#pragma unroll
+    for (int i = 0; i < SCAN_I; ++i) {
+        int64_t idx = (int64_t)threadIdx.x * SCAN_I + i;
+        if (idx < nb) block_sums[idx] = off;
+        off += v[i];
+    }
+    if (threadIdx.x == 0 && total_out) *total_out = tot;
+}
+
+template <typename TIn>
+__global__ void __launch_bounds__(SCAN_T) scan_apply_kernel(const TIn *in, uint64_t *out, int64_t n, const uint64_t *block_offsets) {
+    __shared__ uint64_t lds[64];
+    int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_I;
+    uint64_t v[SCAN_I];
+    uint64_t s = 0;
+#pragma unroll
+    for (int i = 0; i < SCAN_I; ++i) {
+        int64_t idx = base + i;
+        v[i] = idx < n ? (uint64_t)in[idx] : 0;
+        s += v[i];
+    }
+    uint64_t off = block_scan_excl<uint64_t>(s, lds, nullptr) + block_offsets[blockIdx.x];
+#pragma unroll
+    for (int i = 0; i < SCAN_I; ++i) {
+        int64_t idx = base + i;
+        if (idx < n) out[idx] = off;
+        off += v[i];
+    }
+}
+
+size_t scan_tmp_bytes(int64_t n) {
+    int64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
+    return (size_t)(nb + 1) * sizeof(uint64_t) + 256;
+}
+
+template <typename TIn> static int scan_impl(Ctx *ctx, const TIn *in, uint64_t *out, int64_t n, void *tmp) {
+    TFG_CHECK(n >= 0 && n <= (int64_t)SCAN_TILE * SCAN_TILE, TFG_ERR_INVALID_ARG, "scan size %lld out of range",
+              (long long)n);
+    int64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
+    if (nb == 0) {
+        TFG_HIP(hipMemsetAsync(out, 0, sizeof(uint64_t), ctx->stream));
+        return TFG_OK;
+    }
+    uint64_t *bs = (uint64_t *)tmp;
+    // NB: the reduce pass reads the same elements as the apply pass; with the scan operating
+    // on the block sum layout (blocked vs striped) the sum per block is identical.
+    hipLaunchKernelGGL(scan_reduce_kernel<TIn>, dim3((unsigned)nb), dim3(SCAN_T), 0, ctx->stream, in, n, bs);
+    hipLaunchKernelGGL(scan_block_sums_kernel, dim3(1), dim3(SCAN_T), 0, ctx->stream, bs, nb, out + n);
+    hipLaunchKernelGGL(scan_apply_kernel<TIn>, dim3((unsigned)nb), dim3(SCAN_T), 0, ctx->stream, in, out, n, bs);
+    TFG_LAUNCH_CHECK();
+    return TFG_OK;
+}
+
+int exclusive_scan_u32(Ctx *ctx, const uint32_t *in, uint64_t *out, int64_t n, void *tmp) {
+    return scan_impl<uint32_t>(ctx, in, out, n, tmp);
+}
+int exclusive_scan_u64(Ctx *ctx, const uint64_t *in, uint64_t *out, int64_t n, void *tmp) {
+    return scan_impl<uint64_t>(ctx, in, out, n, tmp);
+}
+
+} // namespace tfg
+
+using namespace tfg;
+
+extern "C" {
+
+const char *tfg_last_error(void) { return g_last_error.c_str(); }
+const char *tfg_version(void) { return "tiflash_amd 0.1 (gfx950)"; }
+size_t tfg_type_width(int type) { return type_width(type); }
+
+int tfg_device_count(int *out) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) {
+        *out = 0;
+        return fail(TFG_ERR_NO_DEVICE, "hipGetDeviceCount failed: %s", hipGetErrorString(e));
+    }
+    *out = n;
+    return TFG_OK;
+}
+
+int tfg_ctx_create(int device, void *stream, tfg_ctx **out) {
+    TFG_CHECK(out, TFG_ERR_INVALID_ARG, "out is null");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(TFG_ERR_NO_DEVICE, "no HIP device visible");
+    TFG_CHECK(device >= 0 && device < n, TFG_ERR_INVALID_ARG, "device %d out of range (%d devices)", device, n);
+    TFG_HIP(hipSetDevice(device));
+    tfg_ctx *c = new tfg_ctx();
+    c->device = device;
+    c->stream = (hipStream_t)stream;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->cu_count = prop.multiProcessorCount;
+    if (hipMalloc(&c->dev_counter, 64 * sizeof(uint64_t)) != hipSuccess ||
+        hipHostMalloc(&c->host_pinned, 64 * sizeof(uint64_t), 0) != hipSuccess) {
+        delete c;
+        return fail(TFG_ERR_OOM, "context allocation failed");
+    }
+    *out = c;
+    return TFG_OK;
+}
+
+int tfg_ctx_destroy(tfg_ctx *ctx) {
+    if (!ctx) return TFG_OK;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    else (void)hipDeviceSynchronize();
+    if (ctx->scratch) (void)hipFree(ctx->scratch);
+    if (ctx->dev_counter) (void)hipFree(ctx->dev_counter);
+    if (ctx->host_pinned) (void)hipHostFree(ctx->host_pinned);
+    delete ctx;
+    return TFG_OK;
+}
+
+int tfg_ctx_set_stream(tfg_ctx *ctx, void *stream) {
+    TFG_CHECK(ctx, TFG_ERR_INVALID_ARG, "ctx is null");
+    ctx->stream = (hipStream_t)stream;
+    return TFG_OK;
+}
+
+int tfg_ctx_sync(tfg_ctx *ctx) {
+    TFG_CHECK(ctx, TFG_ERR_INVALID_ARG, "ctx is null");
+    TFG_HIP(hipStreamSynchronize(ctx->stream));
+    return TFG_OK;
+}
+
+int tfg_ctx_reserve(tfg_ctx *ctx, size_t bytes) {
+    TFG_CHECK(ctx, TFG_ERR_INVALID_ARG, "ctx is null");
+    void *p;
+    return scratch_get(ctx, bytes, &p);
+}
+
+int tfg_buf_alloc(tfg_ctx *ctx, size_t bytes, void **out_dev) {
+    TFG_CHECK(ctx && out_dev, TFG_ERR_INVALID_ARG, "null argument");
+    if (set_device(ctx)) return TFG_ERR_HIP;
+    TFG_HIP(hipMalloc(out_dev, bytes ? bytes : 1));
+    return TFG_OK;
+}
+
+int tfg_buf_free(tfg_ctx *ctx, void *dev) {
+    TFG_CHECK(ctx, TFG_ERR_INVALID_ARG, "ctx is null");
+    if (!dev) return TFG_OK;
+    TFG_HIP(hipStreamSynchronize(ctx->stream));
+    TFG_HIP(hipFree(dev));
+    return TFG_OK;
+}
+
+int tfg_upload(tfg_ctx *ctx, void *dst_dev, const void *src_host, size_t bytes) {
+    TFG_CHECK(ctx, TFG_ERR_INVALID_ARG, "ctx is null");
+    if (!bytes) return TFG_OK;
+    TFG_HIP(hipMemcpyAsync(dst_dev, src_host, bytes, hipMemcpyHostToDevice, ctx->stream));
+    TFG_HIP(hipStreamSynchronize(ctx->stream));
+    return TFG_OK;
+}
+
+int tfg_download(tfg_ctx *ctx, void *dst_host, const void *src_dev, size_t bytes) {
+    TFG_CHECK(ctx, TFG_ERR_INVALID_ARG, "ctx is null");
+    if (!bytes) return TFG_OK;
+    TFG_HIP(hipMemcpyAsync(dst_host, src_dev, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    TFG_HIP(hipStreamSynchronize(ctx->stream));
+    return TFG_OK;
+}
+
+} // extern "C"
