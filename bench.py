@@ -1,0 +1,296 @@
+#!/usr/bin/env python3
+"""bench.py — TPC-H Q1-shaped filter -> hash GROUP BY (BASELINE.json configs[1]) on MI355X.
+
+One "step" = one pass of the hot path over one batch of synthetic rows already resident in HBM:
+    Aggregator reset -> fused (f < 96) filter + GROUP BY k: sum(v), count(*) -> final Block (result
+    columns materialised on the device).
+With --gpus N (torchrun, one process per GPU) every rank aggregates its own 100M rows (weak
+scaling), the partial (key, sum, count) rows are hash-repartitioned with fillSelector and
+exchanged with RCCL all-to-all (the MPP ExchangeSender/Receiver of a two-phase aggregation),
+then merged by a final aggregation.  value = rows of all ranks / max-over-ranks time.
+
+Extras in the same JSON line: the hash-join probe (configs[2] shape, N=1), the per-kernel
+roofline of the dominant kernel from HIP events recorded on the library's stream, and the CPU
+baseline (oracle restatement, bounded sample) on the host cores.
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--rows", type=int, default=100_000_000)
+    ap.add_argument("--groups", type=int, default=1_000_000)
+    ap.add_argument("--threshold", type=int, default=96)
+    ap.add_argument("--join-build", type=int, default=10_000_000)
+    ap.add_argument("--join-probe", type=int, default=100_000_000)
+    ap.add_argument("--no-join", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--value-int64", action="store_true", help="Int64 value column instead of Float64")
+    return ap.parse_args()
+
+
+# algorithmic HBM bytes per row for each kernel of the pipeline:
+#   agg.part.hist    reads k, f                       16 B per input row
+#   agg.part.scatter reads k, v, f; writes k, v        24 B per input row + 16 B per kept row
+#   agg.bucket       reads the staged k, v            16 B per kept row
+def kernel_bytes(name, n_in, n_kept):
+    return {
+        "agg.part.hist": 16 * n_in,
+        "agg.part.scatter": 24 * n_in + 16 * n_kept,
+        "agg.bucket": 16 * n_kept,
+        "join.part.hist": 8 * n_in,
+        "join.part.scatter": 8 * n_in + 12 * n_in,
+        "join.probe": 12 * n_in,
+    }.get(name)
+
+
+def roofline_from_profile(prof, steps, n_in, n_kept):
+    if not prof:
+        return None
+    name, (ms, cnt) = max(prof.items(), key=lambda kv: kv[1][0])
+    per_launch_ms = ms / max(cnt, 1)
+    b = kernel_bytes(name, n_in, n_kept)
+    launches_per_step = cnt / max(steps, 1)
+    if b is None or per_launch_ms <= 0:
+        return {"kernel": name, "avg_ms": per_launch_ms}
+    b_launch = b / launches_per_step
+    ach = b_launch / (per_launch_ms * 1e-3) / 1e9
+    return {"bound": "hbm", "kernel": name, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "avg_ms": round(per_launch_ms, 4),
+            "algorithmic_bytes_per_launch": int(b_launch)}
+
+
+def load_pmc_traffic(kernel):
+    """HBM bytes per launch measured by the rocprofv3 PMC pass (profiles/pmc_traffic.json), if any."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(args):
+    import numpy as np
+    from oracle import oracle as orc
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    n = min(args.rows, 50_000_000)
+    rng = np.random.default_rng(1)
+    f = rng.integers(0, 100, n, dtype=np.int64)
+    k = rng.integers(0, args.groups, n, dtype=np.int64)
+    v = rng.integers(0, 1 << 20, n).astype(np.float64) / 256.0
+    times = []
+    t_end = time.time() + 20.0
+    while len(times) < 3 or (time.time() < t_end and len(times) < 5):
+        t0 = time.perf_counter()
+        orc.bench_filter_agg(f, args.threshold, k, v, threads, 65536)
+        times.append(time.perf_counter() - t0)
+        if time.time() > t_end and len(times) >= 1:
+            break
+    med = statistics.median(times)
+    out = {"value": round(n / med, 1), "unit": "rows/s", "cores": threads, "kind": "port",
+           "sample": f"{n} rows x {len(times)} runs (median), same distribution, 65536-row blocks, "
+                     f"per-thread HashMap + merge (reference-algorithm CPU restatement)"}
+    return out
+
+
+def cpu_join_baseline(args):
+    import numpy as np
+    from oracle import oracle as orc
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    nb, npr = min(args.join_build, 10_000_000), min(args.join_probe, 20_000_000)
+    rng = np.random.default_rng(7)
+    bk = rng.permutation(nb).astype(np.int64) * 4 + 1
+    pk = np.where(rng.random(npr) < 0.5, bk[rng.integers(0, nb, npr)], rng.integers(0, 1 << 40, npr) * 4 + 3)
+    t0 = time.perf_counter()
+    orc.bench_join(bk, pk, threads)
+    el = time.perf_counter() - t0
+    return {"value": round(npr / el, 1), "unit": "probe rows/s", "cores": threads, "kind": "port",
+            "sample": f"build {nb} (single-thread build included) + probe {npr}"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import tiflash_amd as tfa
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    N, G = args.rows, args.groups
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1 + rank)
+    f = torch.randint(0, 100, (N,), device=dev, generator=gen, dtype=torch.int64)
+    k = torch.randint(0, G, (N,), device=dev, generator=gen, dtype=torch.int64)
+    if args.value_int64:
+        v = torch.randint(0, 1 << 20, (N,), device=dev, generator=gen, dtype=torch.int64)
+        vtype = tfa.INT64
+    else:  # dyadic m * 2^-8, m < 2^20: partial sums exact, so any summation order is bit-exact
+        v = torch.randint(0, 1 << 20, (N,), device=dev, generator=gen, dtype=torch.int64).double() / 256.0
+        vtype = tfa.FLOAT64
+    n_kept = int((f < args.threshold).sum().item())
+
+    ctx = tfa.Context(local)
+    aggs = [(tfa.AGG_SUM, vtype), (tfa.AGG_COUNT_ALL, 0)]
+    agg = tfa.Aggregator(ctx, tfa.INT64, aggs, expected_groups=G)
+    final = tfa.Aggregator(ctx, tfa.INT64, aggs, expected_groups=G) if world > 1 else None
+
+    def step():
+        agg.reset()
+        agg.consume_filtered(f, tfa.LT, args.threshold, k, [v, None])
+        res = agg.result()  # final Block of this rank (or its partial states)
+        if world == 1:
+            return res
+        # ExchangeSender: hash-repartition partial rows by key, RCCL all-to-all, final merge
+        cols, offs = tfa.hash_partition(ctx, [res["keys"], res["states"][0], res["states"][1]], [0], world)
+        send = torch.tensor([offs[i + 1] - offs[i] for i in range(world)], dtype=torch.int64, device=dev)
+        recv = torch.empty_like(send)
+        dist.all_to_all_single(recv, send)
+        rs = recv.tolist()
+        ss = send.tolist()
+        outs = []
+        for c in cols:
+            o = torch.empty((sum(rs),) + tuple(c.shape[1:]), dtype=c.dtype, device=dev)
+            dist.all_to_all_single(o, c, rs, ss)
+            outs.append(o)
+        final.reset()
+        final.consume_partial(outs[0], [outs[1], outs[2]])
+        return final.result()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ctx.profile(True)
+    ctx.profile_reset()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    prof = ctx.profile_read()
+    ctx.profile(False)
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = t.item()
+    groups = agg.size() if world == 1 else final.size()
+    ms = el / args.steps * 1e3
+    value = N * world * args.steps / el
+
+    line = {
+        "metric": "rows/sec on filter->hash-agg (TPC-H Q1 shape: 100M rows, 1M-key GROUP BY)",
+        "value": round(value, 1), "unit": "rows/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "int64/f64" if vtype == tfa.FLOAT64 else "int64",
+        "data": "synthetic: f~U[0,100) (pred f<96), k~U[0,1e6), v dyadic f64; seed 1+rank",
+        "config": {"workload": "configs[1] filter + GROUP BY 1M keys" + (" two-phase + RCCL all-to-all" if world > 1 else ""),
+                   "rows_per_gpu": N, "groups": G, "kept_rows_per_gpu": n_kept, "groups_out": groups,
+                   "parallelism": f"dp{world}"},
+    }
+    if rank == 0:
+        rf = roofline_from_profile(prof, args.steps, N, n_kept)
+        if rf and "bound" in rf:
+            rf["traffic"] = load_pmc_traffic(rf["kernel"])
+        line["roofline"] = rf
+        line["pipeline_roofline"] = {"algorithmic_bytes_per_step": 24 * N, "achieved": round(24 * N / (ms * 1e-3) / 1e9, 1),
+                                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                     "frac": round(24 * N / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+        line["kernels_ms_per_step"] = {kname: round(v[0] / args.steps, 4) for kname, v in sorted(prof.items())}
+
+    # ---- hash join probe (configs[2] shape) at N=1
+    if world == 1 and not args.no_join:
+        nb, npr = args.join_build, args.join_probe
+        g2 = torch.Generator(device=dev)
+        g2.manual_seed(7)
+        bk = torch.randperm(nb, device=dev, generator=g2).to(torch.int64) * 4 + 1
+        bpay = torch.randint(0, 1 << 40, (nb,), device=dev, generator=g2, dtype=torch.int64)
+        hit = torch.rand(npr, device=dev, generator=g2) < 0.5
+        pk = torch.where(hit, bk[torch.randint(0, nb, (npr,), device=dev, generator=g2)],
+                         torch.randint(0, 1 << 40, (npr,), device=dev, generator=g2) * 4 + 3)
+        ppay = torch.randint(0, 1 << 40, (npr,), device=dev, generator=g2, dtype=torch.int64)
+        del hit
+        j = tfa.Join(ctx, tfa.INT64, expected_build_rows=nb)
+        tb0 = time.perf_counter()
+        j.build(bk)
+        j.finalize()
+        torch.cuda.synchronize()
+        build_s = time.perf_counter() - tb0
+        out_p = torch.empty(npr, dtype=torch.int32, device=dev)
+        out_b = torch.empty(npr, dtype=torch.int32, device=dev)
+
+        def jstep():
+            pi, bi = j.probe(pk, capacity=npr, out_probe=out_p, out_build=out_b)
+            # materialise the joined block: probe key + probe payload (replicated) + build payload
+            return tfa.gather(ctx, pi, [pk, ppay]) + tfa.gather(ctx, bi, [bpay])
+
+        for _ in range(args.warmup):
+            jstep()
+        torch.cuda.synchronize()
+        ctx.profile(True)
+        ctx.profile_reset()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            outj = jstep()
+        torch.cuda.synchronize()
+        jel = time.perf_counter() - t0
+        jprof = ctx.profile_read()
+        ctx.profile(False)
+        matches = outj[0].shape[0]
+        jms = jel / args.steps * 1e3
+        alg = 16 * npr + 24 * matches
+        line["join_probe"] = {
+            "metric": "probe rows/s (hash join 10M build x 100M probe, Int64 keys, ~50% hit, materialised)",
+            "value": round(npr / (jel / args.steps), 1), "unit": "rows/s", "ms_per_step": round(jms, 3),
+            "build_s": round(build_s, 4), "matches": matches,
+            "pipeline_roofline": {"algorithmic_bytes_per_step": alg, "achieved": round(alg / (jms * 1e-3) / 1e9, 1),
+                                  "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                  "frac": round(alg / (jms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+            "kernels_ms_per_step": {kname: round(vv[0] / args.steps, 4) for kname, vv in sorted(jprof.items())},
+        }
+
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cb = cpu_baseline(args)
+        line["cpu_baseline"] = cb
+        line["gpu_vs_cpu"] = round(value / cb["value"], 1)
+        if "join_probe" in line:
+            jb = cpu_join_baseline(args)
+            line["join_probe"]["cpu_baseline"] = jb
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    for o in (agg, final):
+        if o is not None:
+            o.close()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

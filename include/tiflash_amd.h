@@ -130,6 +130,15 @@ const char *tfg_last_error(void);
 const char *tfg_version(void);
 int tfg_device_count(int *out);
 
+/* Kernel profiler: when enabled, every kernel phase is bracketed by HIP events recorded on the
+ * context stream (the stream the kernels run on); totals accumulate per phase name
+ * (e.g. "agg.bucket", "part.scatter").  tfg_profile_read syncs the stream and returns phase
+ * `index` (TFG_ERR_INVALID_ARG past the last one).  Replaces the reference's per-operator
+ * stopwatches (DataStreams/BlockStreamProfileInfo.h:36-60, Operators/OperatorProfileInfo.h:27-59). */
+int tfg_profile_enable(tfg_ctx *ctx, int on);
+int tfg_profile_reset(tfg_ctx *ctx);
+int tfg_profile_read(tfg_ctx *ctx, int index, char *name, size_t name_len, double *total_ms, uint64_t *count);
+
 int tfg_buf_alloc(tfg_ctx *ctx, size_t bytes, void **out_dev);
 int tfg_buf_free(tfg_ctx *ctx, void *dev);
 int tfg_upload(tfg_ctx *ctx, void *dst_dev, const void *src_host, size_t bytes);
@@ -237,6 +246,8 @@ typedef struct tfg_agg_params {
 int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds, const int *arg_types,
                    const int *arg_scales, const tfg_agg_params *params, tfg_agg **out);
 int tfg_agg_destroy(tfg_agg *agg);
+/* Drops every group but keeps the device allocations (a new query on the same signature). */
+int tfg_agg_reset(tfg_agg *agg);
 /* Aggregator::executeOnBlock (Interpreters/Aggregator.cpp:1127-1246): folds n rows into the
  * state.  `mask` (optional) is a UInt8 filter applied first (rows with 0 are skipped). */
 int tfg_agg_consume(tfg_agg *agg, const void *keys, const uint8_t *key_nullmap, const void *const *args,

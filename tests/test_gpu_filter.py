@@ -27,8 +27,9 @@ def _t(x, dev):
 def _col(rng, dtype, n):
     if np.issubdtype(dtype, np.floating):
         x = rng.normal(0, 100, n).astype(dtype)
-        x[rng.integers(0, n, max(1, n // 50))] = np.nan
-        x[:4] = [0.0, -0.0, np.inf, -np.inf]
+        if n:
+            x[rng.integers(0, n, max(1, n // 50))] = np.nan
+        x[: min(n, 4)] = [0.0, -0.0, np.inf, -np.inf][: min(n, 4)]
         return x
     info = np.iinfo(dtype)
     x = rng.integers(info.min, info.max, n, dtype=dtype, endpoint=True)

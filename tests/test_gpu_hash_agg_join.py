@@ -252,7 +252,8 @@ def test_groupby_reference_gtest_groups(tfa, ctx, dev):
         g = tfa.Aggregator(ctx, case["type"], [(tfa.AGG_COUNT_ALL, 0)], bucket_bits=4)
         g.consume(torch.from_numpy(k).to(dev), [None], key_nullmap=torch.from_numpy(kn).to(dev), n=n)
         r = g.result()
-        got = sorted([None if r["key_null"][i] else int(r["keys"][i]) for i in range(g.size())], key=repr)
+        keys = r["keys"].cpu().numpy().view(case["dtype"])
+        got = sorted([None if r["key_null"][i] else int(keys[i]) for i in range(g.size())], key=repr)
         assert got == sorted(case["expected"], key=repr), case["name"]
 
 

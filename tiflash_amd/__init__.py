@@ -10,6 +10,8 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
+import weakref
 from typing import Optional, Sequence
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -117,6 +119,14 @@ def _empty(n, width, device):
     return torch.empty(max(n, 1), dtype=dt, device=device)[:n]
 
 
+def _alloc(n, width, device, dtype):
+    """n >= 1 elements of `width` bytes viewed as `dtype` (2-D (n, 2) int64 for 16-byte values)."""
+    import torch
+    if width == 16:
+        return torch.empty((n, 2), dtype=torch.int64, device=device)
+    return torch.empty(n, dtype=dtype, device=device)
+
+
 class Context:
     """tfg_ctx bound to a device and the current torch stream of that device."""
 
@@ -129,6 +139,7 @@ class Context:
         h = ctypes.c_void_p()
         check(lib().tfg_ctx_create(ctypes.c_int(device), ctypes.c_void_p(stream.cuda_stream), ctypes.byref(h)))
         self.h = h
+        self._children = weakref.WeakSet()  # aggregators / joins: destroyed before the context
 
     def sync(self):
         check(lib().tfg_ctx_sync(self.h))
@@ -136,10 +147,29 @@ class Context:
     def reserve(self, nbytes: int):
         check(lib().tfg_ctx_reserve(self.h, ctypes.c_size_t(nbytes)))
 
+    # kernel profiler (HIP events on this context's stream)
+    def profile(self, on: bool = True):
+        check(lib().tfg_profile_enable(self.h, int(on)))
+
+    def profile_reset(self):
+        check(lib().tfg_profile_reset(self.h))
+
+    def profile_read(self) -> dict:
+        """{phase name: (total_ms, launches)} accumulated since the last reset."""
+        out, i = {}, 0
+        name = ctypes.create_string_buffer(64)
+        ms, cnt = ctypes.c_double(), ctypes.c_uint64()
+        while lib().tfg_profile_read(self.h, i, name, 64, ctypes.byref(ms), ctypes.byref(cnt)) == TFG_OK:
+            out[name.value.decode()] = (ms.value, cnt.value)
+            i += 1
+        return out
+
     def close(self):
-        if getattr(self, "h", None):
+        if getattr(self, "h", None) and not sys.is_finalizing():
+            for c in list(self._children):
+                c.close()
             lib().tfg_ctx_destroy(self.h)
-            self.h = None
+        self.h = None
 
     def __del__(self):
         try:
@@ -202,11 +232,11 @@ def filter(ctx: Context, mask, cols: Sequence):  # noqa: A001 - mirrors IColumn:
     # count first so outputs are exactly sized (sync), then compact
     check(lib().tfg_count_mask(ctx.h, _p(mask), ctypes.c_void_p(0), ctypes.c_int64(n), ctypes.c_void_p(0),
                                ctypes.byref(cnt)))
-    outs = [_empty(cnt.value, w, mask.device).view(c.dtype) if w <= 8 else _empty(cnt.value, w, mask.device)
-            for c, w in zip(cols, widths)]
+    k = cnt.value
+    outs = [_alloc(max(k, 1), w, mask.device, c.dtype) for c, w in zip(cols, widths)]
     check(lib().tfg_filter(ctx.h, _p(mask), ctypes.c_int64(n), len(cols), _ptr_array(cols), _int_array(widths),
                            _ptr_array(outs), ctypes.c_void_p(0), ctypes.byref(cnt)))
-    return outs
+    return [o[:k] for o in outs]
 
 
 def filter_cmp_const(ctx: Context, pred_col, op: int, scalar, cols: Sequence, scalar_type=None, pred_nullmap=None,
@@ -217,8 +247,7 @@ def filter_cmp_const(ctx: Context, pred_col, op: int, scalar, cols: Sequence, sc
     st = scalar_type or (FLOAT64 if isinstance(scalar, float) else INT64)
     widths = [_col_width(c) for c in cols]
     cap = n if out_capacity is None else out_capacity
-    outs = [_empty(cap, w, pred_col.device).view(c.dtype) if w <= 8 else _empty(cap, w, pred_col.device)
-            for c, w in zip(cols, widths)]
+    outs = [_alloc(max(cap, 1), w, pred_col.device, c.dtype) for c, w in zip(cols, widths)]
     cnt = ctypes.c_uint64()
     s = _scalar(st, scalar)
     check(lib().tfg_filter_cmp_const(ctx.h, pred_type or torch_type(pred_col), _p(pred_col), _p(pred_nullmap), op, st,
@@ -305,19 +334,17 @@ def partition(ctx: Context, selector, num_parts: int):
 def gather(ctx: Context, perm, cols: Sequence):
     n = perm.shape[0]
     widths = [_col_width(c) for c in cols]
-    outs = [_empty(n, w, perm.device).view(c.dtype) if w <= 8 else _empty(n, w, perm.device)
-            for c, w in zip(cols, widths)]
+    outs = [_alloc(max(n, 1), w, perm.device, c.dtype) for c, w in zip(cols, widths)]
     check(lib().tfg_gather(ctx.h, _p(perm), ctypes.c_int64(n), len(cols), _ptr_array(cols), _int_array(widths),
                            _ptr_array(outs)))
-    return outs
+    return [o[:n] for o in outs]
 
 
 def hash_partition(ctx: Context, cols: Sequence, key_idx: Sequence[int], part_num: int, types=None, nullmaps=None):
     """HashBaseWriterHelper::scatterColumns: returns (partition-major columns, host offsets[P+1])."""
     n = cols[0].shape[0]
     types = types or [torch_type(c) for c in cols]
-    outs = [_empty(n, WIDTH[t], c.device).view(c.dtype) if WIDTH[t] <= 8 else _empty(n, 16, c.device)
-            for c, t in zip(cols, types)]
+    outs = [_alloc(max(n, 1), WIDTH[t], c.device, c.dtype) for c, t in zip(cols, types)]
     import torch
     offs = torch.empty(part_num + 1, dtype=torch.int64, device=cols[0].device)
     host = (ctypes.c_uint64 * (part_num + 1))()
@@ -325,7 +352,7 @@ def hash_partition(ctx: Context, cols: Sequence, key_idx: Sequence[int], part_nu
     check(lib().tfg_hash_partition(ctx.h, ctypes.c_int64(n), len(key_idx), _int_array(key_idx), len(cols),
                                    _int_array(types), _ptr_array(cols), nm, ctypes.c_uint32(part_num),
                                    _ptr_array(outs), _p(offs), host))
-    return outs, list(host)
+    return [o[:n] for o in outs], list(host)
 
 
 # ---- a9-a17 aggregation -----------------------------------------------------------------------
@@ -349,6 +376,7 @@ class Aggregator:
         check(lib().tfg_agg_create(ctx.h, key_type, len(aggs), kinds, types, ctypes.c_void_p(0), ctypes.byref(params),
                                    ctypes.byref(h)))
         self.h = h
+        ctx._children.add(self)
 
     def consume(self, keys, args: Sequence, key_nullmap=None, arg_nullmaps=None, mask=None, n=None):
         n = n if n is not None else (keys.shape[0] if keys is not None else next(a for a in args if a is not None).shape[0])
@@ -370,6 +398,9 @@ class Aggregator:
         check(lib().tfg_agg_consume_partial(self.h, _p(keys), _p(key_nullmap), _ptr_array(states),
                                             _ptr_array(state_nullmaps) if state_nullmaps else ctypes.c_void_p(0),
                                             ctypes.c_int64(n)))
+
+    def reset(self):
+        check(lib().tfg_agg_reset(self.h))
 
     def merge(self, other: "Aggregator"):
         check(lib().tfg_agg_merge(self.h, other.h))
@@ -402,9 +433,9 @@ class Aggregator:
         return {"keys": keys, "key_null": key_null, "states": states, "state_null": snulls}
 
     def close(self):
-        if getattr(self, "h", None):
+        if getattr(self, "h", None) and not sys.is_finalizing():
             lib().tfg_agg_destroy(self.h)
-            self.h = None
+        self.h = None
 
     def __del__(self):
         try:
@@ -422,6 +453,7 @@ class Join:
         h = ctypes.c_void_p()
         check(lib().tfg_join_create(ctx.h, key_type, ctypes.c_int64(expected_build_rows), ctypes.byref(h)))
         self.h = h
+        ctx._children.add(self)
 
     def build(self, keys, key_nullmap=None):
         check(lib().tfg_join_build(self.h, _p(keys), _p(key_nullmap), ctypes.c_int64(keys.shape[0])))
@@ -453,9 +485,9 @@ class Join:
         return r.value, p.value
 
     def close(self):
-        if getattr(self, "h", None):
+        if getattr(self, "h", None) and not sys.is_finalizing():
             lib().tfg_join_destroy(self.h)
-            self.h = None
+        self.h = None
 
     def __del__(self):
         try:

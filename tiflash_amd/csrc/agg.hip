@@ -119,6 +119,26 @@ __device__ __forceinline__ void lds_add_i128(uint64_t *cell, uint64_t lo, uint64
     atomicAdd((unsigned long long *)&cell[1], (unsigned long long)(hi + carry));
 }
 
+struct RowVal {
+    uint64_t key;
+    uint8_t knull;
+    uint8_t vnull[AGG_MAX];
+    uint64_t lo[AGG_MAX], hi[AGG_MAX], cnt[AGG_MAX];
+};
+
+// raw argument bits of a RAW row widened to the integer accumulator (sign / zero extension)
+__device__ __forceinline__ void widen_raw(int type, uint64_t &lo, uint64_t &hi) {
+    switch (type) {
+    case TFG_INT8: lo = (uint64_t)(int64_t)(int8_t)lo; break;
+    case TFG_INT16: lo = (uint64_t)(int64_t)(int16_t)lo; break;
+    case TFG_INT32: case TFG_DECIMAL32: lo = (uint64_t)(int64_t)(int32_t)lo; break;
+    case TFG_INT64: case TFG_DECIMAL64: break;
+    case TFG_DECIMAL128: return;
+    default: hi = 0; return; // unsigned: zero-extended already
+    }
+    hi = (int64_t)lo < 0 ? ~0ull : 0ull;
+}
+
 struct Table {
     uint64_t *keys;
     char *base;
@@ -139,13 +159,16 @@ struct Table {
 
     // returns the cell of `key`, inserting it when allowed; -1 = not in the table
     __device__ __forceinline__ int find_or_insert(uint64_t key, bool is_null, bool may_insert, bool force) {
-        if (is_null) {
-            if (!ctrl->null_used) ctrl->null_used = 1;
-            return S.cap + 1;
-        }
-        if (key == 0) { // ZeroValueStorage
-            if (!ctrl->zero_used) ctrl->zero_used = 1;
-            return S.cap;
+        // side slots (ZeroValueStorage for key 0, and the NULL key) obey the same insert rule as
+        // table cells: while older groups are pending (may_insert == false) a key that is not in
+        // the table yet must be deferred, or it would be emitted twice
+        if (is_null || key == 0) {
+            unsigned *used = is_null ? &ctrl->null_used : &ctrl->zero_used;
+            if (!__hip_atomic_load(used, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                if (!may_insert) return -1;
+                __hip_atomic_store(used, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            return is_null ? S.cap + 1 : S.cap;
         }
         const unsigned mask = (unsigned)S.cap - 1;
         unsigned pos = (unsigned)mix64(key) & mask;
@@ -176,38 +199,37 @@ struct Table {
         return reinterpret_cast<uint64_t *>(base + S.cnt_off[i]) + cell;
     }
 
-    // fold row `r` of `rows` (mode) into cell
-    __device__ __forceinline__ void add_row(int cell, const RowsIO &rows, int64_t r, int mode) {
+    // fold a register-resident row (mode) into cell
+    __device__ __forceinline__ void add_row(int cell, const RowVal &v, int mode) {
         for (int i = 0; i < S.n_aggs; ++i) {
             const int kind = S.kind[i];
             if (mode == MODE_STATE) {
-                if (S.acc[i] == ACC_I128) {
-                    const uint64_t *v = (const uint64_t *)rows.val[i] + 2 * r;
-                    lds_add_i128(acc_cell(i, cell), v[0], v[1]);
-                } else if (S.acc[i] == ACC_F64) {
-                    atomicAdd((double *)acc_cell(i, cell), ((const double *)rows.val[i])[r]);
-                } else if (S.acc[i] == ACC_I64) {
-                    atomicAdd((unsigned long long *)acc_cell(i, cell), ((const unsigned long long *)rows.val[i])[r]);
-                }
-                if (S.has_cnt[i]) atomicAdd((unsigned long long *)cnt_cell(i, cell), rows.val_cnt[i][r]);
+                if (S.acc[i] == ACC_I128) lds_add_i128(acc_cell(i, cell), v.lo[i], v.hi[i]);
+                else if (S.acc[i] == ACC_F64) atomicAdd((double *)acc_cell(i, cell), __longlong_as_double((long long)v.lo[i]));
+                else if (S.acc[i] == ACC_I64) atomicAdd((unsigned long long *)acc_cell(i, cell), (unsigned long long)v.lo[i]);
+                if (S.has_cnt[i]) atomicAdd((unsigned long long *)cnt_cell(i, cell), (unsigned long long)v.cnt[i]);
                 continue;
             }
             if (kind == TFG_AGG_COUNT_ALL && mode == MODE_RAW) {
                 atomicAdd((unsigned long long *)cnt_cell(i, cell), 1ull);
                 continue;
             }
-            if (rows.val_null[i] && rows.val_null[i][r]) continue;
+            if (v.vnull[i]) continue;
             if (kind != TFG_AGG_SUM) { // COUNT (raw: +1) or partial count (+value)
-                const unsigned long long inc = mode == MODE_RAW ? 1ull : ((const unsigned long long *)rows.val[i])[r];
-                atomicAdd((unsigned long long *)cnt_cell(i, cell), inc);
+                atomicAdd((unsigned long long *)cnt_cell(i, cell), mode == MODE_RAW ? 1ull : (unsigned long long)v.lo[i]);
                 continue;
             }
-            uint64_t lo = 0, hi = 0;
-            double f = 0;
-            load_sum_value(S.src_type[i], rows.val[i], r, lo, hi, f);
-            if (S.acc[i] == ACC_F64) atomicAdd((double *)acc_cell(i, cell), f);
-            else if (S.acc[i] == ACC_I128) lds_add_i128(acc_cell(i, cell), lo, hi);
-            else atomicAdd((unsigned long long *)acc_cell(i, cell), (unsigned long long)lo);
+            uint64_t lo = v.lo[i], hi = v.hi[i];
+            if (S.acc[i] == ACC_F64) {
+                const double f = (mode == MODE_RAW && S.src_type[i] == TFG_FLOAT32)
+                                     ? (double)__uint_as_float((unsigned)lo)
+                                     : __longlong_as_double((long long)lo);
+                atomicAdd((double *)acc_cell(i, cell), f);
+            } else {
+                if (mode == MODE_RAW) widen_raw(S.src_type[i], lo, hi);
+                if (S.acc[i] == ACC_I128) lds_add_i128(acc_cell(i, cell), lo, hi);
+                else atomicAdd((unsigned long long *)acc_cell(i, cell), (unsigned long long)lo);
+            }
             if (S.has_cnt[i]) atomicAdd((unsigned long long *)cnt_cell(i, cell), 1ull);
         }
     }
@@ -259,36 +281,64 @@ struct Table {
     }
 };
 
-// copy row r of `rows` to slot w (in-place compaction of the bucket's pending rows)
-__device__ __forceinline__ void move_row(const AggSpec &S, const RowsIO &rows, int mode, int64_t r, int64_t w) {
-    if (r == w) return;
-    switch (rows.key_width) {
-    case 1: ((uint8_t *)rows.key)[w] = ((const uint8_t *)rows.key)[r]; break;
-    case 2: ((uint16_t *)rows.key)[w] = ((const uint16_t *)rows.key)[r]; break;
-    case 4: ((uint32_t *)rows.key)[w] = ((const uint32_t *)rows.key)[r]; break;
-    default: ((uint64_t *)rows.key)[w] = ((const uint64_t *)rows.key)[r]; break;
+// width in bytes of value column i for a row mode
+__device__ __forceinline__ int val_width(const AggSpec &S, int mode, int i) {
+    if (mode != MODE_RAW) return S.acc[i] == ACC_I128 ? 16 : 8;
+    switch (S.src_type[i]) {
+    case TFG_INT8: case TFG_UINT8: return 1;
+    case TFG_INT16: case TFG_UINT16: return 2;
+    case TFG_INT32: case TFG_UINT32: case TFG_FLOAT32: case TFG_DECIMAL32: return 4;
+    case TFG_DECIMAL128: return 16;
+    default: return 8;
     }
-    if (rows.key_null) rows.key_null[w] = rows.key_null[r];
+}
+
+__device__ __forceinline__ void load_row(const AggSpec &S, const RowsIO &rows, int mode, int64_t r, RowVal &v) {
+    v.key = load_bits(rows.key, rows.key_width, r);
+    v.knull = rows.key_null ? rows.key_null[r] : 0;
     for (int i = 0; i < S.n_aggs; ++i) {
-        if (rows.val[i]) {
-            int w8 = 8;
-            if (mode == MODE_RAW) w8 = (int)(S.src_type[i] == TFG_DECIMAL128 ? 16 : 0);
-            if (mode == MODE_RAW && w8 == 0) {
-                switch (S.src_type[i]) {
-                case TFG_INT8: case TFG_UINT8: ((uint8_t *)rows.val[i])[w] = ((const uint8_t *)rows.val[i])[r]; break;
-                case TFG_INT16: case TFG_UINT16: ((uint16_t *)rows.val[i])[w] = ((const uint16_t *)rows.val[i])[r]; break;
-                case TFG_INT32: case TFG_UINT32: case TFG_FLOAT32: case TFG_DECIMAL32:
-                    ((uint32_t *)rows.val[i])[w] = ((const uint32_t *)rows.val[i])[r]; break;
-                default: ((uint64_t *)rows.val[i])[w] = ((const uint64_t *)rows.val[i])[r]; break;
-                }
-            } else if (S.acc[i] == ACC_I128 || w8 == 16) {
-                ((uint4 *)rows.val[i])[w] = ((const uint4 *)rows.val[i])[r];
-            } else {
-                ((uint64_t *)rows.val[i])[w] = ((const uint64_t *)rows.val[i])[r];
-            }
+        v.lo[i] = v.hi[i] = v.cnt[i] = 0;
+        v.vnull[i] = rows.val_null[i] ? rows.val_null[i][r] : 0;
+        if (rows.val_cnt[i]) v.cnt[i] = rows.val_cnt[i][r];
+        if (!rows.val[i]) continue;
+        const int w = val_width(S, mode, i);
+        if (w == 16) {
+            const uint4 q = ((const uint4 *)rows.val[i])[r];
+            v.lo[i] = ((uint64_t)q.y << 32) | q.x;
+            v.hi[i] = ((uint64_t)q.w << 32) | q.z;
+        } else {
+            v.lo[i] = load_bits(rows.val[i], w, r);
         }
-        if (rows.val_null[i]) rows.val_null[i][w] = rows.val_null[i][r];
-        if (rows.val_cnt[i]) rows.val_cnt[i][w] = rows.val_cnt[i][r];
+    }
+}
+
+// in-place compaction of the bucket's pending rows: write a register row to slot w
+__device__ __forceinline__ void store_row(const AggSpec &S, const RowsIO &rows, int mode, int64_t w, const RowVal &v) {
+    switch (rows.key_width) {
+    case 1: ((uint8_t *)rows.key)[w] = (uint8_t)v.key; break;
+    case 2: ((uint16_t *)rows.key)[w] = (uint16_t)v.key; break;
+    case 4: ((uint32_t *)rows.key)[w] = (uint32_t)v.key; break;
+    default: ((uint64_t *)rows.key)[w] = v.key; break;
+    }
+    if (rows.key_null) rows.key_null[w] = v.knull;
+    for (int i = 0; i < S.n_aggs; ++i) {
+        if (rows.val_null[i]) rows.val_null[i][w] = v.vnull[i];
+        if (rows.val_cnt[i]) rows.val_cnt[i][w] = v.cnt[i];
+        if (!rows.val[i]) continue;
+        switch (val_width(S, mode, i)) {
+        case 1: ((uint8_t *)rows.val[i])[w] = (uint8_t)v.lo[i]; break;
+        case 2: ((uint16_t *)rows.val[i])[w] = (uint16_t)v.lo[i]; break;
+        case 4: ((uint32_t *)rows.val[i])[w] = (uint32_t)v.lo[i]; break;
+        case 8: ((uint64_t *)rows.val[i])[w] = v.lo[i]; break;
+        default: {
+            uint4 q;
+            q.x = (unsigned)v.lo[i];
+            q.y = (unsigned)(v.lo[i] >> 32);
+            q.z = (unsigned)v.hi[i];
+            q.w = (unsigned)(v.hi[i] >> 32);
+            ((uint4 *)rows.val[i])[w] = q;
+        }
+        }
     }
 }
 
@@ -325,26 +375,22 @@ __global__ void __launch_bounds__(BT) agg_bucket_kernel(AggSpec S, RowsIO rows, 
         for (int64_t base = 0; base < pending; base += BT) {
             const int64_t r = rs + base + threadIdx.x;
             const bool valid = base + threadIdx.x < pending;
-            uint64_t key = 0;
-            bool knull = false;
-            if (valid) {
-                key = load_bits(rows.key, rows.key_width, r);
-                knull = rows.key_null && rows.key_null[r];
-            }
+            RowVal v;
+            if (valid) load_row(S, rows, mode, r, v);
             __syncthreads(); // every row of this step is in registers before any in-place write
             int cell = -1;
             if (valid) {
-                cell = T.find_or_insert(key, knull, allow_insert, false);
-                if (cell >= 0) T.add_row(cell, rows, r, mode);
+                cell = T.find_or_insert(v.key, v.knull != 0, allow_insert, false);
+                if (cell >= 0) T.add_row(cell, v, mode);
             }
             __syncthreads(); // inserts of this step are complete: a retry sees the final key set
             if (valid && cell < 0) {
-                cell = T.find_or_insert(key, knull, false, false);
+                cell = T.find_or_insert(v.key, v.knull != 0, false, false);
                 if (cell >= 0) {
-                    T.add_row(cell, rows, r, mode);
+                    T.add_row(cell, v, mode);
                 } else {
                     const int64_t w = rs + (int64_t)atomicAdd(&T.ctrl->spill_w, 1ull);
-                    move_row(S, rows, mode, r, w);
+                    store_row(S, rows, mode, w, v);
                 }
             }
         }
@@ -583,12 +629,12 @@ int consume_keyed(tfg_agg *a, int mode, const RowPred &pred, const void *keys, i
     size_t o_val[AGG_MAX] = {}, o_vnull[AGG_MAX] = {}, o_vcnt[AGG_MAX] = {};
     int vw[AGG_MAX] = {};
     for (int i = 0; i < S.n_aggs; ++i) {
+        if (val_nulls && val_nulls[i]) o_vnull[i] = cv.take<uint8_t>(n);
+        if (val_cnts && val_cnts[i]) o_vcnt[i] = cv.take<uint64_t>(n);
         if (!vals[i]) continue;
         if (mode == MODE_RAW) vw[i] = (int)type_width(S.src_type[i]);
         else vw[i] = S.acc[i] == ACC_I128 ? 16 : 8;
         o_val[i] = cv.take<uint4>((n * vw[i] + 15) / 16);
-        if (val_nulls && val_nulls[i]) o_vnull[i] = cv.take<uint8_t>(n);
-        if (val_cnts && val_cnts[i]) o_vcnt[i] = cv.take<uint64_t>(n);
     }
     const size_t o_stage_off = cv.take<uint64_t>(B + 1);
     const size_t o_new_cnt = cv.take<uint64_t>(B), o_new_off = cv.take<uint64_t>(B + 1);
@@ -646,7 +692,8 @@ int consume_keyed(tfg_agg *a, int mode, const RowPred &pred, const void *keys, i
         }
         TFG_CHECK(pc.ncols <= PCOLS, TFG_ERR_NOT_IMPLEMENTED, "too many aggregate columns");
         SelBucket sel{keys, key_null, key_width, B - 1};
-        if (int rc = run_partition<SelBucket, false>(ctx, sel, pred, L, pc, nullptr, nullptr, stage_off, sb + o_part))
+        if (int rc = run_partition<SelBucket, false>(ctx, sel, pred, L, pc, nullptr, nullptr, stage_off, sb + o_part,
+                                                      "agg.part.hist", "agg.part.scatter"))
             return rc;
     }
     // ---- bucket kernel
@@ -655,8 +702,10 @@ int consume_keyed(tfg_agg *a, int mode, const RowPred &pred, const void *keys, i
     uint64_t *new_cnt = (uint64_t *)(sb + o_new_cnt), *new_off = (uint64_t *)(sb + o_new_off);
     const bool has_old = n_old > 0;
     GroupsIO old = a->st[a->cur];
+    { ProfScope _ps(ctx, "agg.bucket");
     hipLaunchKernelGGL(agg_bucket_kernel, dim3(B), dim3(BT), S.lds_bytes, ctx->stream, S, rows, mode, stage_off, old,
                        has_old ? a->bucket_off[a->cur] : (const uint64_t *)nullptr, tmp, new_cnt);
+    }
     TFG_LAUNCH_CHECK();
     if (int rc = exclusive_scan_u64(ctx, new_cnt, new_off, B, sb + o_part)) return rc;
     uint64_t total = 0;
@@ -664,8 +713,10 @@ int consume_keyed(tfg_agg *a, int mode, const RowPred &pred, const void *keys, i
     const int nxt = a->cur ^ 1;
     if (int rc = a->ensure_state(nxt, total)) return rc;
     if (!a->bucket_off[nxt]) TFG_HIP(hipMalloc(&a->bucket_off[nxt], (B + 1) * 8));
+    { ProfScope _ps(ctx, "agg.compact");
     hipLaunchKernelGGL(agg_compact_kernel, dim3(B), dim3(256), 0, ctx->stream, S, tmp, stage_off,
                        has_old ? a->bucket_off[a->cur] : (const uint64_t *)nullptr, new_off, a->st[nxt]);
+    }
     TFG_LAUNCH_CHECK();
     TFG_HIP(hipMemcpyAsync(a->bucket_off[nxt], new_off, (B + 1) * 8, hipMemcpyDeviceToDevice, ctx->stream));
     a->cur = nxt;
@@ -684,8 +735,10 @@ int consume_nokey(tfg_agg *a, int mode, const RowPred &pred, const void *const *
     const unsigned grid = stream_grid(n, NK_T * 16, 1024);
     void *sp;
     if (int rc = scratch_get(ctx, grid * sizeof(NoKeyPartial), &sp)) return rc;
+    { ProfScope _ps(ctx, "agg.nokey");
     hipLaunchKernelGGL(agg_nokey_kernel, dim3(grid), dim3(NK_T), 0, ctx->stream, a->S, rows, mode, pred, n,
                        (NoKeyPartial *)sp);
+    }
     hipLaunchKernelGGL(agg_nokey_fold_kernel, dim3(1), dim3(64), 0, ctx->stream, a->S, (const NoKeyPartial *)sp,
                        (int)grid, a->st[a->cur]);
     TFG_LAUNCH_CHECK();
@@ -826,6 +879,19 @@ int tfg_agg_destroy(tfg_agg *a) {
     return TFG_OK;
 }
 
+int tfg_agg_reset(tfg_agg *a) {
+    TFG_CHECK(a, TFG_ERR_INVALID_ARG, "agg is null");
+    if (a->nokey) {
+        if (int rc = set_device(a->ctx)) return rc;
+        size_t bytes = a->carve_groups(nullptr, a->cap[a->cur], a->st[a->cur]);
+        TFG_HIP(hipMemsetAsync(a->blk[a->cur], 0, bytes, a->ctx->stream));
+        a->n_groups = 1;
+    } else {
+        a->n_groups = 0;
+    }
+    return TFG_OK;
+}
+
 int tfg_agg_consume(tfg_agg *a, const void *keys, const uint8_t *key_nullmap, const void *const *args,
                     const uint8_t *const *arg_nullmaps, const uint8_t *mask, int64_t n) {
     RowPred pred{};
@@ -912,9 +978,11 @@ int tfg_agg_result(tfg_agg *a, void *out_keys, uint8_t *out_key_nullmap, void *c
         rp.state[i] = out_states ? out_states[i] : nullptr;
         rp.state_null[i] = out_state_nullmaps ? out_state_nullmaps[i] : nullptr;
     }
+    { ProfScope _ps(a->ctx, "agg.result");
     hipLaunchKernelGGL(agg_result_kernel, dim3(stream_grid((int64_t)a->n_groups, 256, 4096)), dim3(256), 0,
                        a->ctx->stream, a->S, a->st[a->cur], a->n_groups, a->S.key_width,
                        a->nokey ? nullptr : out_keys, out_key_nullmap, rp);
+    }
     TFG_LAUNCH_CHECK();
     return TFG_OK;
 }

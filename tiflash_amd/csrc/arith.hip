@@ -129,8 +129,10 @@ extern "C" int tfg_arith(tfg_ctx *ctx, int op, int a_type, const void *a, int a_
     if (int rc = make_side(a_type, a, a_is_const, a_scale, res_type, res_scale, op, sa)) return rc;
     if (int rc = make_side(b_type, b, b_is_const, b_scale, res_type, res_scale, op, sb)) return rc;
     if (n <= 0) return TFG_OK;
+    { ProfScope _ps(ctx, "arith");
     hipLaunchKernelGGL(arith_kernel, dim3(stream_grid(n, 256, 8192)), dim3(256), 0, ctx->stream, op, sa, sb, res_type, n,
                        out);
+    }
     TFG_LAUNCH_CHECK();
     return TFG_OK;
 }

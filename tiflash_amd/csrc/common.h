@@ -11,6 +11,7 @@
 #include <cstdint>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/tiflash_amd.h"
 
@@ -36,6 +37,16 @@ bool failpoint(const char *name); // TFG_FAILPOINT=<name> injects TFG_ERR_FAULT_
 
 // ------------------------------------------------------------------------------------------
 // context + scratch arena
+struct ProfEvent {
+    const char *name;
+    hipEvent_t start, stop;
+};
+struct ProfTotal {
+    std::string name;
+    double ms = 0;
+    uint64_t count = 0;
+};
+
 struct Ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -44,7 +55,21 @@ struct Ctx {
     uint64_t *dev_counter = nullptr; // small device scratch for counts (64 x u64)
     uint64_t *host_pinned = nullptr; // pinned host words for count read-back
     int cu_count = 256;
+    // kernel profiler: HIP events recorded on `stream` around each launch (tfg_profile_*)
+    bool prof_on = false;
+    std::vector<ProfEvent> prof_pending;
+    std::vector<hipEvent_t> prof_pool;
+    std::vector<ProfTotal> prof_totals;
 };
+
+// RAII: brackets the kernel launches of one named phase with events on the context stream.
+struct ProfScope {
+    Ctx *ctx;
+    ProfEvent ev{};
+    ProfScope(Ctx *c, const char *name);
+    ~ProfScope();
+};
+int prof_resolve(Ctx *ctx);
 
 // Returns a device pointer to at least `bytes` of scratch (grows the arena; growth syncs the
 // stream).  The region is reused by the next call: callers carve it, never keep it.

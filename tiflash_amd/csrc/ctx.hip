@@ -87,6 +87,53 @@ int scratch_get(Ctx *ctx, size_t bytes, void **out) {
     return TFG_OK;
 }
 
+static hipEvent_t prof_take(Ctx *ctx) {
+    if (!ctx->prof_pool.empty()) {
+        hipEvent_t e = ctx->prof_pool.back();
+        ctx->prof_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+ProfScope::ProfScope(Ctx *c, const char *name) : ctx(c) {
+    if (!ctx->prof_on) return;
+    ev.name = name;
+    ev.start = prof_take(ctx);
+    ev.stop = prof_take(ctx);
+    if (ev.start) (void)hipEventRecord(ev.start, ctx->stream);
+}
+
+ProfScope::~ProfScope() {
+    if (!ctx->prof_on || !ev.start || !ev.stop) return;
+    (void)hipEventRecord(ev.stop, ctx->stream);
+    ctx->prof_pending.push_back(ev);
+}
+
+int prof_resolve(Ctx *ctx) {
+    if (ctx->prof_pending.empty()) return TFG_OK;
+    TFG_HIP(hipStreamSynchronize(ctx->stream));
+    for (auto &e : ctx->prof_pending) {
+        float ms = 0;
+        TFG_HIP(hipEventElapsedTime(&ms, e.start, e.stop));
+        ProfTotal *t = nullptr;
+        for (auto &x : ctx->prof_totals)
+            if (x.name == e.name) t = &x;
+        if (!t) {
+            ctx->prof_totals.push_back(ProfTotal{e.name, 0, 0});
+            t = &ctx->prof_totals.back();
+        }
+        t->ms += ms;
+        t->count++;
+        ctx->prof_pool.push_back(e.start);
+        ctx->prof_pool.push_back(e.stop);
+    }
+    ctx->prof_pending.clear();
+    return TFG_OK;
+}
+
 int read_back_u64(Ctx *ctx, const uint64_t *dev, uint64_t *host, size_t count) {
     TFG_CHECK(count <= 64, TFG_ERR_LOGICAL, "read_back_u64: count %zu > 64", count);
     TFG_HIP(hipMemcpyAsync(ctx->host_pinned, dev, count * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream));
@@ -204,9 +251,11 @@ template <typename TIn> static int scan_impl(Ctx *ctx, const TIn *in, uint64_t *
     uint64_t *bs = (uint64_t *)tmp;
     // NB: the reduce pass reads the same elements as the apply pass; with the scan operating
     // on the block sum layout (blocked vs striped) the sum per block is identical.
+    { ProfScope _ps(ctx, "scan");
     hipLaunchKernelGGL(scan_reduce_kernel<TIn>, dim3((unsigned)nb), dim3(SCAN_T), 0, ctx->stream, in, n, bs);
     hipLaunchKernelGGL(scan_block_sums_kernel, dim3(1), dim3(SCAN_T), 0, ctx->stream, bs, nb, out + n);
     hipLaunchKernelGGL(scan_apply_kernel<TIn>, dim3((unsigned)nb), dim3(SCAN_T), 0, ctx->stream, in, out, n, bs);
+    }
     TFG_LAUNCH_CHECK();
     return TFG_OK;
 }
@@ -265,6 +314,11 @@ int tfg_ctx_destroy(tfg_ctx *ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     else (void)hipDeviceSynchronize();
     if (ctx->scratch) (void)hipFree(ctx->scratch);
+    for (auto &e : ctx->prof_pending) {
+        (void)hipEventDestroy(e.start);
+        (void)hipEventDestroy(e.stop);
+    }
+    for (auto e : ctx->prof_pool) (void)hipEventDestroy(e);
     if (ctx->dev_counter) (void)hipFree(ctx->dev_counter);
     if (ctx->host_pinned) (void)hipHostFree(ctx->host_pinned);
     delete ctx;
@@ -287,6 +341,34 @@ int tfg_ctx_reserve(tfg_ctx *ctx, size_t bytes) {
     TFG_CHECK(ctx, TFG_ERR_INVALID_ARG, "ctx is null");
     void *p;
     return scratch_get(ctx, bytes, &p);
+}
+
+int tfg_profile_enable(tfg_ctx *ctx, int on) {
+    TFG_CHECK(ctx, TFG_ERR_INVALID_ARG, "ctx is null");
+    if (int rc = prof_resolve(ctx)) return rc;
+    ctx->prof_on = on != 0;
+    return TFG_OK;
+}
+
+int tfg_profile_reset(tfg_ctx *ctx) {
+    TFG_CHECK(ctx, TFG_ERR_INVALID_ARG, "ctx is null");
+    if (int rc = prof_resolve(ctx)) return rc;
+    ctx->prof_totals.clear();
+    return TFG_OK;
+}
+
+int tfg_profile_read(tfg_ctx *ctx, int index, char *name, size_t name_len, double *total_ms, uint64_t *count) {
+    TFG_CHECK(ctx, TFG_ERR_INVALID_ARG, "ctx is null");
+    if (int rc = prof_resolve(ctx)) return rc;
+    if (index < 0 || index >= (int)ctx->prof_totals.size()) return TFG_ERR_INVALID_ARG;
+    const ProfTotal &t = ctx->prof_totals[index];
+    if (name && name_len) {
+        strncpy(name, t.name.c_str(), name_len - 1);
+        name[name_len - 1] = 0;
+    }
+    if (total_ms) *total_ms = t.ms;
+    if (count) *count = t.count;
+    return TFG_OK;
 }
 
 int tfg_buf_alloc(tfg_ctx *ctx, size_t bytes, void **out_dev) {

@@ -273,12 +273,16 @@ static int run_filter(Ctx *ctx, const P &pred, int64_t n, const ColsArg &cols, u
     uint32_t *counts = (uint32_t *)(sb + o_counts);
     uint64_t *offs = (uint64_t *)(sb + o_offs);
     if (tiles > 0) {
+        { ProfScope _ps(ctx, "filter.count");
         hipLaunchKernelGGL(filter_count_kernel<P>, dim3((unsigned)tiles), dim3(FT), 0, ctx->stream, pred, n, counts);
+        }
         TFG_LAUNCH_CHECK();
     }
     if (int rc = exclusive_scan_u32(ctx, counts, offs, tiles, sb + o_tmp)) return rc;
     if (tiles > 0 && cols.ncols > 0) {
+        { ProfScope _ps(ctx, "filter.write");
         hipLaunchKernelGGL(filter_write_kernel<P>, dim3((unsigned)tiles), dim3(FT), 0, ctx->stream, pred, n, offs, cols);
+        }
         TFG_LAUNCH_CHECK();
     }
     if (out_count_dev)
@@ -299,6 +303,12 @@ static int make_cols(int ncols, const void *const *cols, const int *widths, void
         ca.width[j] = w;
         ca.aligned[j] = is_aligned16(cols[j]);
     }
+    return TFG_OK;
+}
+
+static int zero_count(Ctx *ctx, uint64_t *out_count_dev, uint64_t *out_count_host) {
+    if (out_count_dev) TFG_HIP(hipMemsetAsync(out_count_dev, 0, sizeof(uint64_t), ctx->stream));
+    if (out_count_host) *out_count_host = 0;
     return TFG_OK;
 }
 
@@ -331,8 +341,10 @@ int tfg_cmp_const(tfg_ctx *ctx, int col_type, const void *col, const uint8_t *co
     TFG_DISPATCH_NUMERIC(col_type, A, {
         constexpr int PER = 16 / sizeof(A);
         unsigned grid = stream_grid((n + PER - 1) / PER, 256, 8192);
+        { ProfScope _ps(ctx, "cmp.const");
         hipLaunchKernelGGL(cmp_const_kernel<A>, dim3(grid), dim3(256), 0, ctx->stream, (const A *)col, col_nullmap, n,
                            b, op, al, out_mask);
+        }
     });
     TFG_LAUNCH_CHECK();
     return TFG_OK;
@@ -391,6 +403,7 @@ int tfg_filter(tfg_ctx *ctx, const uint8_t *mask, int64_t n, int ncols, const vo
     TFG_CHECK(ctx && (n == 0 || mask), TFG_ERR_INVALID_ARG, "null argument");
     TFG_CHECK(n >= 0, TFG_ERR_INVALID_ARG, "negative row count");
     if (failpoint("filter")) return fail(TFG_ERR_FAULT_INJECTED, "failpoint filter");
+    if (n == 0) return zero_count(ctx, out_count_dev, out_count_host);
     ColsArg ca{};
     if (int rc = make_cols(ncols, cols, widths, outs, ca)) return rc;
     MaskPred p{mask, nullptr, is_aligned16(mask)};
@@ -404,6 +417,7 @@ int tfg_filter_cmp_const(tfg_ctx *ctx, int pred_type, const void *pred_col, cons
     TFG_CHECK(n >= 0, TFG_ERR_INVALID_ARG, "negative row count");
     TFG_CHECK(op >= TFG_EQ && op <= TFG_GE, TFG_ERR_INVALID_ARG, "bad comparison op %d", op);
     TFG_CHECK(is_fixed_numeric(scalar_type), TFG_ERR_ILLEGAL_TYPE, "unsupported constant type %d", scalar_type);
+    if (n == 0) return zero_count(ctx, out_count_dev, out_count_host);
     ColsArg ca{};
     if (int rc = make_cols(ncols, cols, widths, outs, ca)) return rc;
     Num b = host_num(scalar_type, scalar_host);

@@ -138,7 +138,9 @@ int tfg_weak_hash_update(tfg_ctx *ctx, int type, const void *col, const uint8_t 
     int types[1] = {type};
     if (int rc = make_keycols(1, nullptr, types, cols, nms, k)) return rc;
     if (n <= 0) return TFG_OK;
+    { ProfScope _ps(ctx, "hash.weak");
     hipLaunchKernelGGL(weak_hash_update_kernel, dim3(stream_grid(n, 256, 4096)), dim3(256), 0, ctx->stream, k, n, h);
+    }
     TFG_LAUNCH_CHECK();
     return TFG_OK;
 }
@@ -210,6 +212,11 @@ int tfg_hash_partition(tfg_ctx *ctx, int64_t n, int nkeys, const int *key_col_id
                        const void *const *cols, const uint8_t *const *nullmaps, uint32_t part_num, void *const *outs,
                        uint64_t *out_offsets, uint64_t *out_offsets_host) {
     TFG_CHECK(ctx && types && cols && outs && out_offsets && key_col_idx, TFG_ERR_INVALID_ARG, "null argument");
+    if (n == 0) { // every partition empty
+        TFG_HIP(hipMemsetAsync(out_offsets, 0, (part_num + 1) * sizeof(uint64_t), ctx->stream));
+        if (out_offsets_host) memset(out_offsets_host, 0, (part_num + 1) * sizeof(uint64_t));
+        return TFG_OK;
+    }
     TFG_CHECK(ncols >= 1 && ncols <= PCOLS, TFG_ERR_INVALID_ARG, "ncols %d out of range [1,%d]", ncols, PCOLS);
     TFG_CHECK(part_num >= 1 && part_num <= (uint32_t)PMAX, TFG_ERR_INVALID_ARG, "part_num %u out of range", part_num);
     TFG_CHECK(n >= 0 && n < (int64_t)0xFFFFFFFFll, TFG_ERR_INVALID_ARG, "row count out of range");

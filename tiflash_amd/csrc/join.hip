@@ -390,7 +390,9 @@ int tfg_join_finalize(tfg_join *j) {
     pc.width[0] = 8;
     SelJoin sel{j->keys, j->nulls, 8, P - 1};
     RowPred pred{};
-    if (int rc = run_partition<SelJoin, false>(ctx, sel, pred, L, pc, j->brows, nullptr, j->boff, tmp)) return rc;
+    if (int rc = run_partition<SelJoin, false>(ctx, sel, pred, L, pc, j->brows, nullptr, j->boff, tmp, "join.build.hist",
+                                               "join.build.scatter"))
+        return rc;
     uint64_t ins = 0;
     if (int rc = read_back_u64(ctx, j->boff + P, &ins, 1)) return rc;
     j->n_inserted = (int64_t)ins;
@@ -436,7 +438,8 @@ int tfg_join_probe(tfg_join *j, int kind, const void *keys, const uint8_t *key_n
         SelJoin sel{keys, key_nullmap, j->width, P - 1};
         RowPred pred{};
         uint64_t *poff = (uint64_t *)(sb + o_poff);
-        if (int rc = run_partition<SelJoin, false>(ctx, sel, pred, L, pc, (uint32_t *)(sb + o_pr), nullptr, poff, sb + o_tmp))
+        if (int rc = run_partition<SelJoin, false>(ctx, sel, pred, L, pc, (uint32_t *)(sb + o_pr), nullptr, poff, sb + o_tmp,
+                                                   "join.part.hist", "join.part.scatter"))
             return rc;
         TFG_HIP(hipMemsetAsync(sb + o_found, 0, n, ctx->stream));
         JoinArgs A{};
@@ -453,7 +456,9 @@ int tfg_join_probe(tfg_join *j, int kind, const void *keys, const uint8_t *key_n
         A.out_build = out_build_idx;
         A.capacity = capacity;
         A.cursor = cursor;
+        { ProfScope _ps(ctx, "join.probe");
         hipLaunchKernelGGL(join_probe_kernel, dim3(P), dim3(JT), sizeof(JLds), ctx->stream, A);
+        }
         TFG_LAUNCH_CHECK();
         if (key_nullmap && (kind == TFG_JOIN_LEFT || kind == TFG_JOIN_ANTI)) {
             hipLaunchKernelGGL(join_null_rows_kernel, dim3(stream_grid(n, 256, 4096)), dim3(256), 0, ctx->stream,

@@ -258,7 +258,8 @@ __global__ void gather_part_offsets_kernel(const uint64_t *offs, PartLayout L, u
 
 template <typename Sel, bool STABLE = true>
 int run_partition(Ctx *ctx, const Sel &sel, const RowPred &pred, const PartLayout &L, const PCols &cols,
-                  uint32_t *perm, uint32_t *part_out, uint64_t *offsets_out, void *tmp) {
+                  uint32_t *perm, uint32_t *part_out, uint64_t *offsets_out, void *tmp,
+                  const char *hist_name = "part.hist", const char *scatter_name = "part.scatter") {
     TFG_CHECK(L.P >= 1 && L.P <= (STABLE ? PMAX : PMAX_UNSTABLE), TFG_ERR_INVALID_ARG, "partition count %u out of range", L.P);
     const int64_t e = (int64_t)L.P * L.G;
     char *t = (char *)tmp;
@@ -268,17 +269,21 @@ int run_partition(Ctx *ctx, const Sel &sel, const RowPred &pred, const PartLayou
     t += ((size_t)(e + 1) * 8 + 255) / 256 * 256;
     void *scan_tmp = t;
     if (L.n > 0) {
+        { ProfScope _ps(ctx, hist_name);
         hipLaunchKernelGGL(part_hist_kernel<Sel>, dim3(L.G), dim3(PT), hist_lds_bytes(L.P, Sel::needs_crc), ctx->stream,
                            sel, pred, L, counts);
+        }
         TFG_LAUNCH_CHECK();
     } else {
         TFG_HIP(hipMemsetAsync(counts, 0, (size_t)e * 4, ctx->stream));
     }
     if (int rc = exclusive_scan_u32(ctx, counts, offs, e, scan_tmp)) return rc;
     if (L.n > 0 && (perm || part_out || cols.ncols > 0)) {
+        { ProfScope _ps(ctx, scatter_name);
         hipLaunchKernelGGL((part_scatter_kernel<Sel, STABLE>), dim3(L.G), dim3(PT),
                            scatter_lds_bytes(L.P, Sel::needs_crc, STABLE), ctx->stream, sel, pred, L, offs, cols, perm,
                            part_out);
+        }
         TFG_LAUNCH_CHECK();
     }
     if (offsets_out) {
