@@ -40,6 +40,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--value-int64", action="store_true", help="Int64 value column instead of Float64")
+    ap.add_argument("--bucket-bits", type=int, default=0, help="aggregation radix buckets (0 = from --groups)")
     return ap.parse_args()
 
 
@@ -154,8 +155,8 @@ def main():
 
     ctx = tfa.Context(local)
     aggs = [(tfa.AGG_SUM, vtype), (tfa.AGG_COUNT_ALL, 0)]
-    agg = tfa.Aggregator(ctx, tfa.INT64, aggs, expected_groups=G)
-    final = tfa.Aggregator(ctx, tfa.INT64, aggs, expected_groups=G) if world > 1 else None
+    agg = tfa.Aggregator(ctx, tfa.INT64, aggs, bucket_bits=args.bucket_bits, expected_groups=G)
+    final = tfa.Aggregator(ctx, tfa.INT64, aggs, bucket_bits=args.bucket_bits, expected_groups=G) if world > 1 else None
 
     def step():
         agg.reset()

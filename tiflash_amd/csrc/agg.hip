@@ -27,8 +27,8 @@
 namespace tfg {
 
 constexpr int AGG_MAX = 4;
-constexpr int BT = 512; // bucket kernel threads
-constexpr int LDS_TABLE_BYTES = 64 * 1024;
+constexpr int BT = 1024; // bucket kernel threads (one workgroup per CU)
+constexpr int LDS_TABLE_BYTES = 100 * 1024;
 
 enum AccKind { ACC_NONE = 0, ACC_I64 = 1, ACC_F64 = 2, ACC_I128 = 3 };
 enum RowMode { MODE_RAW = 0, MODE_PARTIAL = 1, MODE_STATE = 2 };
@@ -119,11 +119,12 @@ __device__ __forceinline__ void lds_add_i128(uint64_t *cell, uint64_t lo, uint64
     atomicAdd((unsigned long long *)&cell[1], (unsigned long long)(hi + carry));
 }
 
-struct RowVal {
+// one staged row held in registers; NA = number of aggregates (compile time, keeps VGPRs low)
+template <int NA> struct RowValT {
     uint64_t key;
     uint8_t knull;
-    uint8_t vnull[AGG_MAX];
-    uint64_t lo[AGG_MAX], hi[AGG_MAX], cnt[AGG_MAX];
+    uint8_t vnull[NA];
+    uint64_t lo[NA], hi[NA], cnt[NA];
 };
 
 // raw argument bits of a RAW row widened to the integer accumulator (sign / zero extension)
@@ -200,8 +201,9 @@ struct Table {
     }
 
     // fold a register-resident row (mode) into cell
-    __device__ __forceinline__ void add_row(int cell, const RowVal &v, int mode) {
-        for (int i = 0; i < S.n_aggs; ++i) {
+    template <int NA> __device__ __forceinline__ void add_row(int cell, const RowValT<NA> &v, int mode) {
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
             const int kind = S.kind[i];
             if (mode == MODE_STATE) {
                 if (S.acc[i] == ACC_I128) lds_add_i128(acc_cell(i, cell), v.lo[i], v.hi[i]);
@@ -293,10 +295,12 @@ __device__ __forceinline__ int val_width(const AggSpec &S, int mode, int i) {
     }
 }
 
-__device__ __forceinline__ void load_row(const AggSpec &S, const RowsIO &rows, int mode, int64_t r, RowVal &v) {
+template <int NA>
+__device__ __forceinline__ void load_row(const AggSpec &S, const RowsIO &rows, int mode, int64_t r, RowValT<NA> &v) {
     v.key = load_bits(rows.key, rows.key_width, r);
     v.knull = rows.key_null ? rows.key_null[r] : 0;
-    for (int i = 0; i < S.n_aggs; ++i) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
         v.lo[i] = v.hi[i] = v.cnt[i] = 0;
         v.vnull[i] = rows.val_null[i] ? rows.val_null[i][r] : 0;
         if (rows.val_cnt[i]) v.cnt[i] = rows.val_cnt[i][r];
@@ -313,7 +317,8 @@ __device__ __forceinline__ void load_row(const AggSpec &S, const RowsIO &rows, i
 }
 
 // in-place compaction of the bucket's pending rows: write a register row to slot w
-__device__ __forceinline__ void store_row(const AggSpec &S, const RowsIO &rows, int mode, int64_t w, const RowVal &v) {
+template <int NA>
+__device__ __forceinline__ void store_row(const AggSpec &S, const RowsIO &rows, int mode, int64_t w, const RowValT<NA> &v) {
     switch (rows.key_width) {
     case 1: ((uint8_t *)rows.key)[w] = (uint8_t)v.key; break;
     case 2: ((uint16_t *)rows.key)[w] = (uint16_t)v.key; break;
@@ -321,7 +326,8 @@ __device__ __forceinline__ void store_row(const AggSpec &S, const RowsIO &rows, 
     default: ((uint64_t *)rows.key)[w] = v.key; break;
     }
     if (rows.key_null) rows.key_null[w] = v.knull;
-    for (int i = 0; i < S.n_aggs; ++i) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
         if (rows.val_null[i]) rows.val_null[i][w] = v.vnull[i];
         if (rows.val_cnt[i]) rows.val_cnt[i][w] = v.cnt[i];
         if (!rows.val[i]) continue;
@@ -342,9 +348,15 @@ __device__ __forceinline__ void store_row(const AggSpec &S, const RowsIO &rows, 
     }
 }
 
-__global__ void __launch_bounds__(BT) agg_bucket_kernel(AggSpec S, RowsIO rows, int mode, const uint64_t *stage_off,
-                                                        GroupsIO old, const uint64_t *old_off, GroupsIO out,
-                                                        uint64_t *out_cnt) {
+// RPT rows per thread per step: several independent row loads in flight per thread, and one
+// barrier per step.  Misses (keys that do not fit the table, or whose older group is still
+// pending) are appended to the other row buffer (ping-pong), processed by the next pass.
+constexpr int RPT = 4;
+
+template <int NA>
+__global__ void __launch_bounds__(BT) agg_bucket_kernel(AggSpec S, RowsIO rows0, RowsIO rows1, int mode,
+                                                        const uint64_t *stage_off, GroupsIO old,
+                                                        const uint64_t *old_off, GroupsIO out, uint64_t *out_cnt) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     Table T(lds, S);
     const int b = blockIdx.x;
@@ -357,8 +369,12 @@ __global__ void __launch_bounds__(BT) agg_bucket_kernel(AggSpec S, RowsIO rows, 
     }
     const uint64_t out_base = (uint64_t)os + (uint64_t)rs;
     int64_t old_cursor = os;
+    int pass = 0;
     if (threadIdx.x == 0) T.ctrl->out_count = 0;
     while (pending > 0 || old_cursor < oe) {
+        const RowsIO &rows = (pass & 1) ? rows1 : rows0;
+        const RowsIO &spill = (pass & 1) ? rows0 : rows1;
+        ++pass;
         T.clear();
         __syncthreads();
         // phase A: a chunk of existing groups (distinct keys)
@@ -371,26 +387,36 @@ __global__ void __launch_bounds__(BT) agg_bucket_kernel(AggSpec S, RowsIO rows, 
         old_cursor += take;
         const bool allow_insert = old_cursor >= oe;
         __syncthreads();
-        // phase B: pending rows, misses compacted in place for the next pass
-        for (int64_t base = 0; base < pending; base += BT) {
-            const int64_t r = rs + base + threadIdx.x;
-            const bool valid = base + threadIdx.x < pending;
-            RowVal v;
-            if (valid) load_row(S, rows, mode, r, v);
-            __syncthreads(); // every row of this step is in registers before any in-place write
-            int cell = -1;
-            if (valid) {
-                cell = T.find_or_insert(v.key, v.knull != 0, allow_insert, false);
-                if (cell >= 0) T.add_row(cell, v, mode);
+        // phase B: pending rows; misses go to the other buffer for the next pass
+        for (int64_t base = 0; base < pending; base += BT * RPT) {
+            RowValT<NA> v[RPT];
+            bool miss[RPT];
+#pragma unroll
+            for (int u = 0; u < RPT; ++u) {
+                const int64_t i = base + u * BT + threadIdx.x;
+                if (i < pending) load_row<NA>(S, rows, mode, rs + i, v[u]);
             }
-            __syncthreads(); // inserts of this step are complete: a retry sees the final key set
-            if (valid && cell < 0) {
-                cell = T.find_or_insert(v.key, v.knull != 0, false, false);
+#pragma unroll
+            for (int u = 0; u < RPT; ++u) {
+                miss[u] = false;
+                if (base + u * BT + threadIdx.x >= pending) continue;
+                const int cell = T.find_or_insert(v[u].key, v[u].knull != 0, allow_insert, false);
+                if (cell >= 0) T.add_row<NA>(cell, v[u], mode);
+                else miss[u] = true;
+            }
+            // inserts of this step are complete before any retry: a retry sees the final key set
+            // (a miss means the table was full, or inserts are disabled, so no later step of this
+            // pass can insert the key either)
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < RPT; ++u) {
+                if (!miss[u]) continue;
+                const int cell = T.find_or_insert(v[u].key, v[u].knull != 0, false, false);
                 if (cell >= 0) {
-                    T.add_row(cell, v, mode);
+                    T.add_row<NA>(cell, v[u], mode);
                 } else {
                     const int64_t w = rs + (int64_t)atomicAdd(&T.ctrl->spill_w, 1ull);
-                    store_row(S, rows, mode, w, v);
+                    store_row<NA>(S, spill, mode, w, v[u]);
                 }
             }
         }
@@ -541,10 +567,13 @@ struct SelBucket {
     int width;
     uint32_t mask;
     static constexpr bool needs_crc = true;
-    __device__ __forceinline__ uint32_t operator()(const uint32_t (*t)[256], int64_t r) const {
-        if (key_null && key_null[r]) return 0;
-        return int_hash_crc32(t, load_bits(key, width, r)) & mask;
+    __device__ __forceinline__ Loaded load(int64_t r) const {
+        return Loaded{load_bits(key, width, r), key_null ? (uint32_t)key_null[r] : 0u};
     }
+    __device__ __forceinline__ uint32_t part(const uint32_t (*t)[256], const Loaded &l, int64_t) const {
+        return l.null ? 0u : (int_hash_crc32(t, l.bits) & mask);
+    }
+    __device__ __forceinline__ uint32_t operator()(const uint32_t (*t)[256], int64_t r) const { return part(t, load(r), r); }
 };
 
 } // namespace tfg
@@ -636,6 +665,8 @@ int consume_keyed(tfg_agg *a, int mode, const RowPred &pred, const void *keys, i
         else vw[i] = S.acc[i] == ACC_I128 ? 16 : 8;
         o_val[i] = cv.take<uint4>((n * vw[i] + 15) / 16);
     }
+    const size_t staging_bytes = cv.off; // key/value columns above; a second copy holds spills
+    const size_t o_spill = cv.take<uint8_t>(staging_bytes);
     const size_t o_stage_off = cv.take<uint64_t>(B + 1);
     const size_t o_new_cnt = cv.take<uint64_t>(B), o_new_off = cv.take<uint64_t>(B + 1);
     const size_t tmp_groups = n_old + (size_t)n;
@@ -702,9 +733,24 @@ int consume_keyed(tfg_agg *a, int mode, const RowPred &pred, const void *keys, i
     uint64_t *new_cnt = (uint64_t *)(sb + o_new_cnt), *new_off = (uint64_t *)(sb + o_new_off);
     const bool has_old = n_old > 0;
     GroupsIO old = a->st[a->cur];
-    { ProfScope _ps(ctx, "agg.bucket");
-    hipLaunchKernelGGL(agg_bucket_kernel, dim3(B), dim3(BT), S.lds_bytes, ctx->stream, S, rows, mode, stage_off, old,
-                       has_old ? a->bucket_off[a->cur] : (const uint64_t *)nullptr, tmp, new_cnt);
+    RowsIO rows1 = rows; // same layout, shifted into the spill copy
+    auto shift = [&](auto *p) { return p ? (decltype(p))((char *)p + o_spill) : p; };
+    rows1.key = shift(rows.key);
+    rows1.key_null = shift(rows.key_null);
+    for (int i = 0; i < AGG_MAX; ++i) {
+        rows1.val[i] = shift(rows.val[i]);
+        rows1.val_null[i] = shift(rows.val_null[i]);
+        rows1.val_cnt[i] = shift(rows.val_cnt[i]);
+    }
+    const uint64_t *ooff = has_old ? a->bucket_off[a->cur] : (const uint64_t *)nullptr;
+    {
+        ProfScope _ps(ctx, "agg.bucket");
+        switch (S.n_aggs) {
+        case 1: hipLaunchKernelGGL(agg_bucket_kernel<1>, dim3(B), dim3(BT), S.lds_bytes, ctx->stream, S, rows, rows1, mode, stage_off, old, ooff, tmp, new_cnt); break;
+        case 2: hipLaunchKernelGGL(agg_bucket_kernel<2>, dim3(B), dim3(BT), S.lds_bytes, ctx->stream, S, rows, rows1, mode, stage_off, old, ooff, tmp, new_cnt); break;
+        case 3: hipLaunchKernelGGL(agg_bucket_kernel<3>, dim3(B), dim3(BT), S.lds_bytes, ctx->stream, S, rows, rows1, mode, stage_off, old, ooff, tmp, new_cnt); break;
+        default: hipLaunchKernelGGL(agg_bucket_kernel<4>, dim3(B), dim3(BT), S.lds_bytes, ctx->stream, S, rows, rows1, mode, stage_off, old, ooff, tmp, new_cnt); break;
+        }
     }
     TFG_LAUNCH_CHECK();
     if (int rc = exclusive_scan_u64(ctx, new_cnt, new_off, B, sb + o_part)) return rc;
@@ -848,7 +894,7 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
     int bbits = params ? params->bucket_bits : 0;
     if (bbits <= 0) {
         int64_t eg = (params && params->expected_groups > 0) ? params->expected_groups : (1 << 20);
-        int64_t want = eg / std::max(1, S.maxfill / 2);
+        int64_t want = eg / std::max(1, S.maxfill * 4 / 5);
         bbits = 4;
         while (bbits < 12 && ((int64_t)1 << bbits) < want) ++bbits;
     }

@@ -51,10 +51,13 @@ struct SelJoin {
     int width;
     uint32_t mask;
     static constexpr bool needs_crc = true;
-    __device__ __forceinline__ uint32_t operator()(const uint32_t (*t)[256], int64_t r) const {
-        if (key_null && key_null[r]) return 0xFFFFFFFFu; // NULL keys never join
-        return int_hash_crc32(t, jload_bits(key, width, r)) & mask;
+    __device__ __forceinline__ Loaded load(int64_t r) const {
+        return Loaded{jload_bits(key, width, r), key_null ? (uint32_t)key_null[r] : 0u};
     }
+    __device__ __forceinline__ uint32_t part(const uint32_t (*t)[256], const Loaded &l, int64_t) const {
+        return l.null ? 0xFFFFFFFFu : (int_hash_crc32(t, l.bits) & mask); // NULL keys never join
+    }
+    __device__ __forceinline__ uint32_t operator()(const uint32_t (*t)[256], int64_t r) const { return part(t, load(r), r); }
 };
 
 struct JoinArgs {
