@@ -27,7 +27,7 @@
 namespace tfg {
 
 constexpr int AGG_MAX = 4;
-constexpr int BT = 1024; // bucket kernel threads (one workgroup per CU)
+constexpr int BT = 512; // bucket kernel threads (8 waves; 2-3 workgroups per CU)
 constexpr int LDS_TABLE_BYTES = 100 * 1024;
 
 enum AccKind { ACC_NONE = 0, ACC_I64 = 1, ACC_F64 = 2, ACC_I128 = 3 };
@@ -47,6 +47,7 @@ struct AggSpec {
     int cnt_off[AGG_MAX];
     int ctrl_off;
     int lds_bytes;
+    int dbg; // timing ablation knob (TFG_DBG_BUCKET), 0 in production
 };
 
 // Columnar row source staged by the bucket pass (bucket-major).
@@ -171,25 +172,105 @@ struct Table {
             }
             return is_null ? S.cap + 1 : S.cap;
         }
-        const unsigned mask = (unsigned)S.cap - 1;
-        unsigned pos = (unsigned)mix64(key) & mask;
-        for (int probe = 0; probe < S.cap; ++probe) {
-            const uint64_t k = __hip_atomic_load(&keys[pos], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (k == key) return (int)pos;
-            if (k == 0) {
-                if (!may_insert || (!force && __hip_atomic_load(&ctrl->full, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
-                    return -1;
-                const uint64_t old = atomicCAS((unsigned long long *)&keys[pos], 0ull, (unsigned long long)key);
-                if (old == 0) {
-                    const unsigned u = atomicAdd(&ctrl->used, 1u) + 1;
-                    if (u >= (unsigned)S.maxfill) ctrl->full = 1;
-                    return (int)pos;
-                }
-                if (old == key) return (int)pos;
-            }
-            pos = (pos + 1) & mask;
+        uint64_t k1[1] = {key};
+        bool n1[1] = {false}, v1[1] = {true};
+        int c1[1];
+        find_or_insert_multi<1>(k1, n1, v1, may_insert, c1, force);
+        return c1[0];
+    }
+
+    // One probe step reads a group of GS = 4 consecutive cells (two ds_read_b128) and compares
+    // them all: groups of 4 at fill <= 5/8 rarely overflow, so almost every lookup finishes in
+    // one step (single-cell linear probing had long worst-case chains, and a wave waits for its
+    // slowest lane).  Groups overflow linearly into the next group.
+    static constexpr int GS = 4;
+    __device__ __forceinline__ int try_claim(int cell, uint64_t key, bool force, bool &done) {
+        // returns the cell when `key` now owns it, -1 otherwise (done = a definitive miss)
+        if (!force && __hip_atomic_load(&ctrl->full, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+            done = true;
+            return -1;
         }
-        return -1;
+        const uint64_t old = atomicCAS((unsigned long long *)&keys[cell], 0ull, (unsigned long long)key);
+        if (old == 0) {
+            const unsigned n = atomicAdd(&ctrl->used, 1u) + 1;
+            if (n >= (unsigned)S.maxfill) ctrl->full = 1;
+            done = true;
+            return cell;
+        }
+        if (old == key) {
+            done = true;
+            return cell;
+        }
+        return -1; // lost the race to another key: re-read the group
+    }
+
+    // find_or_insert for R rows at once with their probe sequences interleaved: every round
+    // issues the LDS reads of all still-probing rows back to back, so R dependent LDS-latency
+    // chains overlap instead of running one after the other (a wave waits for its longest chain).
+    template <int R>
+    __device__ __forceinline__ void find_or_insert_multi(const uint64_t (&key)[R], const bool (&is_null)[R],
+                                                         const bool (&valid)[R], bool may_insert, int (&cell)[R],
+                                                         bool force = false) {
+        const unsigned gmask = (unsigned)S.cap / GS - 1;
+        unsigned grp[R];
+        bool live[R];
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            cell[u] = -1;
+            live[u] = false;
+            if (!valid[u]) continue;
+            if (is_null[u] || key[u] == 0) {
+                cell[u] = find_or_insert(key[u], is_null[u], may_insert, force);
+                continue;
+            }
+            grp[u] = (unsigned)mix64(key[u]) & gmask;
+            live[u] = true;
+        }
+        for (int step = 0; step <= (int)gmask; ++step) {
+            uint64_t k[R][GS];
+#pragma unroll
+            for (int u = 0; u < R; ++u) // every live row's group read before any compare
+                if (live[u]) {
+                    const uint4 a = *reinterpret_cast<const uint4 *>(&keys[grp[u] * GS]);
+                    const uint4 b = *reinterpret_cast<const uint4 *>(&keys[grp[u] * GS + 2]);
+                    k[u][0] = ((uint64_t)a.y << 32) | a.x;
+                    k[u][1] = ((uint64_t)a.w << 32) | a.z;
+                    k[u][2] = ((uint64_t)b.y << 32) | b.x;
+                    k[u][3] = ((uint64_t)b.w << 32) | b.z;
+                }
+            bool any = false;
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                if (!live[u]) continue;
+                int hit = -1, empty = -1;
+#pragma unroll
+                for (int s = 0; s < GS; ++s) {
+                    if (k[u][s] == key[u] && hit < 0) hit = s;
+                    if (k[u][s] == 0 && empty < 0) empty = s;
+                }
+                if (hit >= 0 && (empty < 0 || hit < empty)) { // found before the first empty cell
+                    cell[u] = (int)(grp[u] * GS + hit);
+                    live[u] = false;
+                } else if (empty >= 0) {
+                    if (!may_insert) {
+                        live[u] = false; // miss
+                        continue;
+                    }
+                    bool done = false;
+                    const int c = try_claim((int)(grp[u] * GS + empty), key[u], force, done);
+                    if (done) {
+                        cell[u] = c;
+                        live[u] = false;
+                    } else {
+                        any = true; // raced: re-read this group
+                    }
+                } else {
+                    grp[u] = (grp[u] + 1) & gmask; // full group: overflow into the next
+                    any = true;
+                }
+            }
+            if (!any) break;
+        }
     }
 
     __device__ __forceinline__ uint64_t *acc_cell(int i, int cell) const {
@@ -353,12 +434,65 @@ __device__ __forceinline__ void store_row(const AggSpec &S, const RowsIO &rows, 
 // pending) are appended to the other row buffer (ping-pong), processed by the next pass.
 constexpr int RPT = 4;
 
-template <int NA>
+// Row policies of the bucket kernel.  GenericOps handles every signature / mode / null map
+// through runtime switches; FastOps<A0,A1,A2> is the compile-time specialisation of the hot
+// signatures (8-byte key, no NULLs, RAW rows) — op codes: 0 absent, 1 count, 2 sum into Int64,
+// 3 sum Float64, 4 sum Decimal64 into Int128.  Without it the per-row switches cost ~350
+// wave-instructions per 64 rows (measured with SQ_INSTS_VALU / SQ_INSTS_SALU).
+template <int NA> struct GenericOps {
+    using Row = RowValT<NA>;
+    const AggSpec &S;
+    int mode;
+    __device__ __forceinline__ void load(const RowsIO &rows, int64_t r, Row &v) const { load_row<NA>(S, rows, mode, r, v); }
+    __device__ __forceinline__ uint64_t key(const Row &v) const { return v.key; }
+    __device__ __forceinline__ bool knull(const Row &v) const { return v.knull != 0; }
+    __device__ __forceinline__ void add(Table &T, int cell, const Row &v) const { T.add_row<NA>(cell, v, mode); }
+    __device__ __forceinline__ void store(const RowsIO &sp, int64_t w, const Row &v) const { store_row<NA>(S, sp, mode, w, v); }
+    __device__ __forceinline__ uint64_t probe_val(const Row &v) const { return v.lo[0]; }
+};
+
+template <int A0, int A1, int A2> struct FastOps {
+    static constexpr int NA = (A0 ? 1 : 0) + (A1 ? 1 : 0) + (A2 ? 1 : 0);
+    struct Row {
+        uint64_t key;
+        uint64_t v[3];
+    };
+    const AggSpec &S;
+    int mode;
+    static __device__ __forceinline__ constexpr int op(int i) { return i == 0 ? A0 : (i == 1 ? A1 : A2); }
+    __device__ __forceinline__ void load(const RowsIO &rows, int64_t r, Row &v) const {
+        v.key = ((const uint64_t *)rows.key)[r];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+            if (op(i) >= 2) v.v[i] = ((const uint64_t *)rows.val[i])[r];
+    }
+    __device__ __forceinline__ uint64_t key(const Row &v) const { return v.key; }
+    __device__ __forceinline__ bool knull(const Row &) const { return false; }
+    __device__ __forceinline__ void add(Table &T, int cell, const Row &v) const {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            if (op(i) == 1) atomicAdd((unsigned long long *)T.cnt_cell(i, cell), 1ull);
+            if (op(i) == 2) atomicAdd((unsigned long long *)T.acc_cell(i, cell), (unsigned long long)v.v[i]);
+            if (op(i) == 3) atomicAdd((double *)T.acc_cell(i, cell), __longlong_as_double((long long)v.v[i]));
+            if (op(i) == 4) lds_add_i128(T.acc_cell(i, cell), v.v[i], (int64_t)v.v[i] < 0 ? ~0ull : 0ull);
+        }
+    }
+    __device__ __forceinline__ void store(const RowsIO &sp, int64_t w, const Row &v) const {
+        ((uint64_t *)sp.key)[w] = v.key;
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+            if (op(i) >= 2) ((uint64_t *)sp.val[i])[w] = v.v[i];
+    }
+    __device__ __forceinline__ uint64_t probe_val(const Row &v) const { return v.v[0]; }
+};
+
+template <typename Ops>
 __global__ void __launch_bounds__(BT) agg_bucket_kernel(AggSpec S, RowsIO rows0, RowsIO rows1, int mode,
                                                         const uint64_t *stage_off, GroupsIO old,
                                                         const uint64_t *old_off, GroupsIO out, uint64_t *out_cnt) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     Table T(lds, S);
+    const Ops ops{S, mode};
     const int b = blockIdx.x;
     const int64_t rs = (int64_t)stage_off[b];
     int64_t pending = (int64_t)stage_off[b + 1] - rs;
@@ -388,20 +522,35 @@ __global__ void __launch_bounds__(BT) agg_bucket_kernel(AggSpec S, RowsIO rows0,
         const bool allow_insert = old_cursor >= oe;
         __syncthreads();
         // phase B: pending rows; misses go to the other buffer for the next pass
-        for (int64_t base = 0; base < pending; base += BT * RPT) {
-            RowValT<NA> v[RPT];
-            bool miss[RPT];
+        const uint32_t npend = (uint32_t)pending;
+        for (uint32_t base = 0; base < npend; base += BT * RPT) {
+            typename Ops::Row v[RPT];
+            uint64_t ku[RPT];
+            bool nu[RPT], vu[RPT], miss[RPT];
+            int cells[RPT];
 #pragma unroll
             for (int u = 0; u < RPT; ++u) {
-                const int64_t i = base + u * BT + threadIdx.x;
-                if (i < pending) load_row<NA>(S, rows, mode, rs + i, v[u]);
+                const uint32_t i = base + u * BT + threadIdx.x;
+                vu[u] = i < npend;
+                if (vu[u]) ops.load(rows, rs + i, v[u]);
             }
 #pragma unroll
             for (int u = 0; u < RPT; ++u) {
+                ku[u] = ops.key(v[u]);
+                nu[u] = ops.knull(v[u]);
+            }
+            if (S.dbg == 1) { // timing ablation: loads only
+#pragma unroll
+                for (int u = 0; u < RPT; ++u)
+                    if (vu[u] && ku[u] == 0x5555555555555555ull) T.ctrl->out_count += ops.probe_val(v[u]);
+                continue;
+            }
+            T.find_or_insert_multi<RPT>(ku, nu, vu, allow_insert, cells);
+#pragma unroll
+            for (int u = 0; u < RPT; ++u) {
                 miss[u] = false;
-                if (base + u * BT + threadIdx.x >= pending) continue;
-                const int cell = T.find_or_insert(v[u].key, v[u].knull != 0, allow_insert, false);
-                if (cell >= 0) T.add_row<NA>(cell, v[u], mode);
+                if (!vu[u] || S.dbg == 2) continue; // dbg 2: timing ablation, loads + probe/insert
+                if (cells[u] >= 0) ops.add(T, cells[u], v[u]);
                 else miss[u] = true;
             }
             // inserts of this step are complete before any retry: a retry sees the final key set
@@ -411,12 +560,12 @@ __global__ void __launch_bounds__(BT) agg_bucket_kernel(AggSpec S, RowsIO rows0,
 #pragma unroll
             for (int u = 0; u < RPT; ++u) {
                 if (!miss[u]) continue;
-                const int cell = T.find_or_insert(v[u].key, v[u].knull != 0, false, false);
+                const int cell = T.find_or_insert(ku[u], nu[u], false, false);
                 if (cell >= 0) {
-                    T.add_row<NA>(cell, v[u], mode);
+                    ops.add(T, cell, v[u]);
                 } else {
                     const int64_t w = rs + (int64_t)atomicAdd(&T.ctrl->spill_w, 1ull);
-                    store_row<NA>(S, spill, mode, w, v[u]);
+                    ops.store(spill, w, v[u]);
                 }
             }
         }
@@ -645,6 +794,35 @@ struct tfg_agg {
 
 namespace {
 
+template <typename Ops>
+void launch_bucket(int B, const AggSpec &S, hipStream_t st, const RowsIO &rows, const RowsIO &rows1, int mode,
+                   const uint64_t *stage_off, const GroupsIO &old, const uint64_t *ooff, const GroupsIO &tmp,
+                   uint64_t *new_cnt) {
+    hipLaunchKernelGGL(agg_bucket_kernel<Ops>, dim3(B), dim3(BT), S.lds_bytes, st, S, rows, rows1, mode, stage_off, old,
+                       ooff, tmp, new_cnt);
+}
+
+// op-code signature for the FastOps specialisations (0 = generic path)
+int fast_signature(const AggSpec &S, int mode, int key_width, const uint8_t *key_null, const uint8_t *const *val_nulls) {
+    if (mode != MODE_RAW || key_width != 8 || key_null || S.n_aggs > 3) return 0;
+    int code = 0;
+    for (int i = 0; i < 3; ++i) {
+        int op = 0;
+        if (i < S.n_aggs) {
+            if (val_nulls && val_nulls[i]) return 0;
+            const int k = S.kind[i], t = S.src_type[i];
+            if (k == TFG_AGG_COUNT_ALL || k == TFG_AGG_COUNT) op = 1;
+            else if (S.acc[i] == ACC_I64 && (t == TFG_INT64 || t == TFG_UINT64)) op = 2;
+            else if (S.acc[i] == ACC_F64 && t == TFG_FLOAT64) op = 3;
+            else if (S.acc[i] == ACC_I128 && t == TFG_DECIMAL64) op = 4;
+            else return 0;
+            if (S.has_cnt[i] && op != 1) return 0;
+        }
+        code = code * 10 + op;
+    }
+    return code;
+}
+
 int consume_keyed(tfg_agg *a, int mode, const RowPred &pred, const void *keys, int key_width, const uint8_t *key_null,
                   const void *const *vals, const uint8_t *const *val_nulls, const uint64_t *const *val_cnts,
                   const uint64_t *given_off, int64_t n) {
@@ -745,12 +923,29 @@ int consume_keyed(tfg_agg *a, int mode, const RowPred &pred, const void *keys, i
     const uint64_t *ooff = has_old ? a->bucket_off[a->cur] : (const uint64_t *)nullptr;
     {
         ProfScope _ps(ctx, "agg.bucket");
-        switch (S.n_aggs) {
-        case 1: hipLaunchKernelGGL(agg_bucket_kernel<1>, dim3(B), dim3(BT), S.lds_bytes, ctx->stream, S, rows, rows1, mode, stage_off, old, ooff, tmp, new_cnt); break;
-        case 2: hipLaunchKernelGGL(agg_bucket_kernel<2>, dim3(B), dim3(BT), S.lds_bytes, ctx->stream, S, rows, rows1, mode, stage_off, old, ooff, tmp, new_cnt); break;
-        case 3: hipLaunchKernelGGL(agg_bucket_kernel<3>, dim3(B), dim3(BT), S.lds_bytes, ctx->stream, S, rows, rows1, mode, stage_off, old, ooff, tmp, new_cnt); break;
-        default: hipLaunchKernelGGL(agg_bucket_kernel<4>, dim3(B), dim3(BT), S.lds_bytes, ctx->stream, S, rows, rows1, mode, stage_off, old, ooff, tmp, new_cnt); break;
+        const int fast = fast_signature(S, mode, key_width, key_null, val_nulls);
+#define TFG_BUCKET(...) launch_bucket<__VA_ARGS__>(B, S, ctx->stream, rows, rows1, mode, stage_off, old, ooff, tmp, new_cnt)
+        switch (fast) {
+        case 310: TFG_BUCKET(FastOps<3, 1, 0>); break;
+        case 210: TFG_BUCKET(FastOps<2, 1, 0>); break;
+        case 410: TFG_BUCKET(FastOps<4, 1, 0>); break;
+        case 300: TFG_BUCKET(FastOps<3, 0, 0>); break;
+        case 200: TFG_BUCKET(FastOps<2, 0, 0>); break;
+        case 400: TFG_BUCKET(FastOps<4, 0, 0>); break;
+        case 100: TFG_BUCKET(FastOps<1, 0, 0>); break;
+        case 231: TFG_BUCKET(FastOps<2, 3, 1>); break;
+        case 221: TFG_BUCKET(FastOps<2, 2, 1>); break;
+        case 331: TFG_BUCKET(FastOps<3, 3, 1>); break;
+        case 441: TFG_BUCKET(FastOps<4, 4, 1>); break;
+        default:
+            switch (S.n_aggs) {
+            case 1: TFG_BUCKET(GenericOps<1>); break;
+            case 2: TFG_BUCKET(GenericOps<2>); break;
+            case 3: TFG_BUCKET(GenericOps<3>); break;
+            default: TFG_BUCKET(GenericOps<4>); break;
+            }
         }
+#undef TFG_BUCKET
     }
     TFG_LAUNCH_CHECK();
     if (int rc = exclusive_scan_u64(ctx, new_cnt, new_off, B, sb + o_part)) return rc;
@@ -872,9 +1067,21 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
         if (S.has_cnt[i]) cell += 8;
         (void)arg_scales;
     }
-    // LDS table geometry
-    int cap = 1;
-    while ((size_t)(cap * 2 + 2) * cell <= (size_t)LDS_TABLE_BYTES) cap *= 2;
+    // buckets: about 1K expected groups per bucket (the TwoLevelHashTable analogue)
+    const int64_t eg = (params && params->expected_groups > 0) ? params->expected_groups : (1 << 20);
+    int bbits = params ? params->bucket_bits : 0;
+    if (bbits <= 0) {
+        bbits = 4;
+        while (bbits < 12 && ((int64_t)1 << bbits) * 1024 < eg) ++bbits;
+    }
+    if (bbits > 12) bbits = 12;
+    a->B = a->nokey ? 1 : (1u << bbits);
+    // LDS table geometry: room for a bucket's expected groups with 25% slack (fill <= 5/8 and
+    // headroom for one step of in-flight inserts); small tables let 2-3 workgroups share a CU
+    const int64_t per_bucket = eg / (int64_t)a->B + 1;
+    int cap = 256;
+    while (cap < (1 << 16) && std::min(cap * 5 / 8, cap - BT - 8) < per_bucket * 5 / 4) cap *= 2;
+    while (cap > 256 && (size_t)(cap + 2) * cell > (size_t)LDS_TABLE_BYTES) cap /= 2;
     S.cap = cap;
     S.maxfill = std::max(1, std::min(cap * 5 / 8, cap - BT - 8));
     int off = (cap + 2) * 8;
@@ -890,16 +1097,7 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
     }
     S.ctrl_off = off;
     S.lds_bytes = off + (int)sizeof(Ctrl) + 16;
-    // buckets
-    int bbits = params ? params->bucket_bits : 0;
-    if (bbits <= 0) {
-        int64_t eg = (params && params->expected_groups > 0) ? params->expected_groups : (1 << 20);
-        int64_t want = eg / std::max(1, S.maxfill * 4 / 5);
-        bbits = 4;
-        while (bbits < 12 && ((int64_t)1 << bbits) < want) ++bbits;
-    }
-    if (bbits > 12) bbits = 12;
-    a->B = a->nokey ? 1 : (1u << bbits);
+    S.dbg = getenv("TFG_DBG_BUCKET") ? atoi(getenv("TFG_DBG_BUCKET")) : 0;
     if (a->nokey) {
         if (int rc = a->ensure_state(0, 1)) {
             delete a;

@@ -145,6 +145,51 @@ struct RowPred {
     __device__ __forceinline__ bool operator()(int64_t r) const { return eval(load(r)); }
 };
 
+// Compile-time specialised predicates for the hot cases (no per-row type switch):
+// KIND 0 = none, 1 = UInt8 mask, 2 = `T col Op scalar`.
+template <int KIND, typename T = int64_t> struct PredT {
+    const void *col;
+    const uint8_t *nullmap;
+    Num b;
+    int op;
+    __device__ __forceinline__ Loaded load(int64_t r) const {
+        Loaded l{0, 0};
+        if constexpr (KIND == 1) l.bits = ((const uint8_t *)col)[r];
+        if constexpr (KIND == 2) {
+            T x = ((const T *)col)[r];
+            uint64_t bits = 0;
+            memcpy(&bits, &x, sizeof(T));
+            l.bits = bits;
+        }
+        if constexpr (KIND != 0)
+            if (nullmap) l.null = nullmap[r];
+        return l;
+    }
+    __device__ __forceinline__ bool eval(const Loaded &l) const {
+        if constexpr (KIND == 0) return true;
+        if (l.null) return false;
+        if constexpr (KIND == 1) return l.bits != 0;
+        else {
+            T x;
+            memcpy(&x, &l.bits, sizeof(T));
+            return cmp_value_num<T>(x, b, op);
+        }
+    }
+    __device__ __forceinline__ bool operator()(int64_t r) const { return eval(load(r)); }
+};
+
+// Calls f(pred) with the most specialised predicate type for `p`.
+template <typename F> int with_pred(const RowPred &p, F &&f) {
+    if (p.kind == 0) return f(PredT<0>{nullptr, nullptr, p.b, p.op});
+    if (p.kind == 1) return f(PredT<1>{p.col, p.nullmap, p.b, p.op});
+    switch (p.type) {
+    case TFG_INT64: return f(PredT<2, int64_t>{p.col, p.nullmap, p.b, p.op});
+    case TFG_INT32: return f(PredT<2, int32_t>{p.col, p.nullmap, p.b, p.op});
+    case TFG_FLOAT64: return f(PredT<2, double>{p.col, p.nullmap, p.b, p.op});
+    default: return f(p);
+    }
+}
+
 struct PartLayout {
     int64_t n;
     int64_t seg;   // rows per segment (multiple of PT)
@@ -171,8 +216,8 @@ inline PartLayout make_layout(int64_t n, uint32_t P) {
     return L;
 }
 
-template <typename Sel>
-__global__ void __launch_bounds__(PT) part_hist_kernel(Sel sel, RowPred pred, PartLayout L, uint32_t *counts) {
+template <typename Sel, typename Pred>
+__global__ void __launch_bounds__(PT) part_hist_kernel(Sel sel, Pred pred, PartLayout L, uint32_t *counts) {
     extern __shared__ __attribute__((aligned(16))) uint32_t hist[]; // P entries (+ crc tables)
     uint32_t(*crc)[256] = reinterpret_cast<uint32_t(*)[256]>(hist + ((L.P + 3) & ~3u));
     for (uint32_t p = threadIdx.x; p < L.P; p += PT) hist[p] = 0;
@@ -315,7 +360,7 @@ __global__ void gather_part_offsets_kernel(const uint64_t *offs, PartLayout L, u
 // tile of TR rows by destination in LDS first (LDS atomics give each row its rank inside its
 // destination), then streams the sorted tile out: consecutive lanes write consecutive
 // addresses of one destination run, so stores coalesce into runs of TR/P rows.
-constexpr int ST_T = 512;      // threads (8 waves; two workgroups per CU)
+constexpr int ST_T = 1024;     // threads (16 waves)
 constexpr int ST_MAXR = 8;     // rows per thread per tile (TR <= 4096)
 
 struct StagedGeom {
@@ -327,12 +372,21 @@ struct StagedGeom {
     int lds_bytes;
 };
 
+// LDS bytes a staged-scatter workgroup may use (TFG_STAGE_LDS overrides; tuning knob).
+inline size_t stage_lds_budget() {
+    static size_t v = [] {
+        const char *e = getenv("TFG_STAGE_LDS");
+        return e ? (size_t)atol(e) : (size_t)150 * 1024;
+    }();
+    return v;
+}
+
 inline bool make_staged_geom(uint32_t P, const PCols &cols, bool perm, bool crc, StagedGeom &g) {
     if (P > 4096) return false;
     size_t row_bytes = 2 + (perm ? 4 : 0);
     for (int j = 0; j < cols.ncols; ++j) row_bytes += cols.width[j];
     const size_t fixed = (size_t)P * 16 + (crc ? 8192 : 0) + 16 * (PCOLS + 2);
-    const size_t budget = 78 * 1024; // two workgroups per CU
+    const size_t budget = stage_lds_budget(); // LDS per workgroup (default: one workgroup per CU)
     if (fixed + row_bytes * ST_T * 4 > budget) return false;
     int tr = (int)((budget - fixed) / row_bytes) / ST_T * ST_T;
     if (tr > ST_T * ST_MAXR) tr = ST_T * ST_MAXR;
@@ -351,8 +405,10 @@ inline bool make_staged_geom(uint32_t P, const PCols &cols, bool perm, bool crc,
     return true;
 }
 
-template <typename Sel>
-__global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, RowPred pred, PartLayout L,
+// NC8 > 0: compile-time fast path for exactly NC8 columns of 8 bytes (keys, payloads); the
+// column loops unroll and no per-row width switch remains.  NC8 == 0: any widths.
+template <typename Sel, typename Pred, int NC8>
+__global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, Pred pred, PartLayout L,
                                                                    const uint64_t *offs, PCols cols, uint32_t *perm,
                                                                    StagedGeom g) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -366,11 +422,12 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, R
     uint32_t *red = reinterpret_cast<uint32_t *>(lds + g.red_off); // ST_T/64 + 1 words
     for (uint32_t p = threadIdx.x; p < P; p += ST_T) run[p] = offs[(int64_t)p * L.G + blockIdx.x];
     if constexpr (Sel::needs_crc) load_crc_lds(crc);
-    const int64_t begin = (int64_t)blockIdx.x * L.seg;
-    int64_t end = begin + L.seg;
-    if (end > L.n) end = L.n;
+    // row indices fit 32 bits (the ABI caps n below 2^32)
+    const uint32_t begin = (uint32_t)((int64_t)blockIdx.x * L.seg);
+    const uint32_t end = (uint32_t)std::min<int64_t>((int64_t)begin + L.seg, L.n);
     const int per = g.TR / ST_T;
-    for (int64_t tb = begin; tb < end; tb += g.TR) {
+    const int ncols = NC8 > 0 ? NC8 : cols.ncols;
+    for (uint32_t tb = begin; tb < end; tb += (uint32_t)g.TR) {
         for (uint32_t p = threadIdx.x; p < P; p += ST_T) hist[p] = 0;
         __syncthreads();
         // 1. destination + rank of every row of the tile
@@ -382,7 +439,7 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, R
 #pragma unroll
             for (int q = 0; q < HB; ++q) { // the half-batch's loads first ...
                 const int j = h * HB + q;
-                const int64_t r = tb + (int64_t)j * ST_T + threadIdx.x;
+                const uint32_t r = tb + (uint32_t)j * ST_T + threadIdx.x;
                 if (j < per && r < end) {
                     pl[q] = pred.load(r);
                     kl[q] = sel.load(r);
@@ -392,7 +449,7 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, R
             for (int q = 0; q < HB; ++q) { // ... then destinations and ranks
                 const int j = h * HB + q;
                 bq[j] = 0xFFFFFFFFu;
-                const int64_t r = tb + (int64_t)j * ST_T + threadIdx.x;
+                const uint32_t r = tb + (uint32_t)j * ST_T + threadIdx.x;
                 if (j < per && r < end && pred.eval(pl[q])) {
                     const uint32_t b = sel.part(crc, kl[q], r);
                     if (b < P) {
@@ -433,34 +490,48 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, R
 #pragma unroll
         for (int j = 0; j < ST_MAXR; ++j) {
             if (bq[j] == 0xFFFFFFFFu) continue;
-            const int64_t r = tb + (int64_t)j * ST_T + threadIdx.x;
             sl[j] = start[bq[j]] + rk[j];
             sb[sl[j]] = (uint16_t)bq[j];
-            if (perm) sperm[sl[j]] = (uint32_t)r;
+            if (perm) sperm[sl[j]] = tb + (uint32_t)j * ST_T + threadIdx.x;
         }
-        for (int c = 0; c < cols.ncols; ++c) { // per column: every row's load in flight, then LDS stores
-            char *st = lds + g.stage_off[c];
-            const int w = cols.width[c];
-            if (w <= 8) {
+        if constexpr (NC8 > 0) {
+#pragma unroll
+            for (int c = 0; c < NC8; ++c) { // per column: every row's load in flight, then LDS stores
+                uint64_t *st = reinterpret_cast<uint64_t *>(lds + g.stage_off[c]);
+                const uint64_t *src = reinterpret_cast<const uint64_t *>(cols.in[c]);
                 uint64_t v[ST_MAXR];
 #pragma unroll
                 for (int j = 0; j < ST_MAXR; ++j)
-                    if (bq[j] != 0xFFFFFFFFu) v[j] = load_width(cols.in[c], w, tb + (int64_t)j * ST_T + threadIdx.x);
-#pragma unroll
-                for (int j = 0; j < ST_MAXR; ++j) {
-                    if (bq[j] == 0xFFFFFFFFu) continue;
-                    switch (w) {
-                    case 1: ((uint8_t *)st)[sl[j]] = (uint8_t)v[j]; break;
-                    case 2: ((uint16_t *)st)[sl[j]] = (uint16_t)v[j]; break;
-                    case 4: ((uint32_t *)st)[sl[j]] = (uint32_t)v[j]; break;
-                    default: ((uint64_t *)st)[sl[j]] = v[j]; break;
-                    }
-                }
-            } else {
+                    if (bq[j] != 0xFFFFFFFFu) v[j] = src[tb + (uint32_t)j * ST_T + threadIdx.x];
 #pragma unroll
                 for (int j = 0; j < ST_MAXR; ++j)
-                    if (bq[j] != 0xFFFFFFFFu)
-                        ((uint4 *)st)[sl[j]] = ((const uint4 *)cols.in[c])[tb + (int64_t)j * ST_T + threadIdx.x];
+                    if (bq[j] != 0xFFFFFFFFu) st[sl[j]] = v[j];
+            }
+        } else {
+            for (int c = 0; c < ncols; ++c) {
+                char *st = lds + g.stage_off[c];
+                const int w = cols.width[c];
+                if (w <= 8) {
+                    uint64_t v[ST_MAXR];
+#pragma unroll
+                    for (int j = 0; j < ST_MAXR; ++j)
+                        if (bq[j] != 0xFFFFFFFFu) v[j] = load_width(cols.in[c], w, tb + (uint32_t)j * ST_T + threadIdx.x);
+#pragma unroll
+                    for (int j = 0; j < ST_MAXR; ++j) {
+                        if (bq[j] == 0xFFFFFFFFu) continue;
+                        switch (w) {
+                        case 1: ((uint8_t *)st)[sl[j]] = (uint8_t)v[j]; break;
+                        case 2: ((uint16_t *)st)[sl[j]] = (uint16_t)v[j]; break;
+                        case 4: ((uint32_t *)st)[sl[j]] = (uint32_t)v[j]; break;
+                        default: ((uint64_t *)st)[sl[j]] = v[j]; break;
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < ST_MAXR; ++j)
+                        if (bq[j] != 0xFFFFFFFFu)
+                            ((uint4 *)st)[sl[j]] = ((const uint4 *)cols.in[c])[tb + (uint32_t)j * ST_T + threadIdx.x];
+                }
             }
         }
         __syncthreads();
@@ -469,14 +540,20 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, R
             const uint32_t b = sb[s];
             const uint64_t gp = run[b] + (s - start[b]);
             if (perm) perm[gp] = sperm[s];
-            for (int c = 0; c < cols.ncols; ++c) {
-                const char *st = lds + g.stage_off[c];
-                switch (cols.width[c]) {
-                case 1: ((uint8_t *)cols.out[c])[gp] = ((const uint8_t *)st)[s]; break;
-                case 2: ((uint16_t *)cols.out[c])[gp] = ((const uint16_t *)st)[s]; break;
-                case 4: ((uint32_t *)cols.out[c])[gp] = ((const uint32_t *)st)[s]; break;
-                case 8: ((uint64_t *)cols.out[c])[gp] = ((const uint64_t *)st)[s]; break;
-                default: ((uint4 *)cols.out[c])[gp] = ((const uint4 *)st)[s]; break;
+            if constexpr (NC8 > 0) {
+#pragma unroll
+                for (int c = 0; c < NC8; ++c)
+                    ((uint64_t *)cols.out[c])[gp] = reinterpret_cast<const uint64_t *>(lds + g.stage_off[c])[s];
+            } else {
+                for (int c = 0; c < ncols; ++c) {
+                    const char *st = lds + g.stage_off[c];
+                    switch (cols.width[c]) {
+                    case 1: ((uint8_t *)cols.out[c])[gp] = ((const uint8_t *)st)[s]; break;
+                    case 2: ((uint16_t *)cols.out[c])[gp] = ((const uint16_t *)st)[s]; break;
+                    case 4: ((uint32_t *)cols.out[c])[gp] = ((const uint32_t *)st)[s]; break;
+                    case 8: ((uint64_t *)cols.out[c])[gp] = ((const uint64_t *)st)[s]; break;
+                    default: ((uint4 *)cols.out[c])[gp] = ((const uint4 *)st)[s]; break;
+                    }
                 }
             }
         }
@@ -499,22 +576,37 @@ int run_partition(Ctx *ctx, const Sel &sel, const RowPred &pred, const PartLayou
     t += ((size_t)(e + 1) * 8 + 255) / 256 * 256;
     void *scan_tmp = t;
     if (L.n > 0) {
-        { ProfScope _ps(ctx, hist_name);
-        hipLaunchKernelGGL(part_hist_kernel<Sel>, dim3(L.G), dim3(PT), hist_lds_bytes(L.P, Sel::needs_crc), ctx->stream,
-                           sel, pred, L, counts);
-        }
-        TFG_LAUNCH_CHECK();
+        ProfScope _ps(ctx, hist_name);
+        if (int rc = with_pred(pred, [&](auto pr) -> int {
+                hipLaunchKernelGGL((part_hist_kernel<Sel, decltype(pr)>), dim3(L.G), dim3(PT),
+                                   hist_lds_bytes(L.P, Sel::needs_crc), ctx->stream, sel, pr, L, counts);
+                TFG_LAUNCH_CHECK();
+                return TFG_OK;
+            }))
+            return rc;
     } else {
         TFG_HIP(hipMemsetAsync(counts, 0, (size_t)e * 4, ctx->stream));
     }
     if (int rc = exclusive_scan_u32(ctx, counts, offs, e, scan_tmp)) return rc;
     StagedGeom sg{};
     if (!STABLE && !part_out && L.n > 0 && make_staged_geom(L.P, cols, perm != nullptr, Sel::needs_crc, sg)) {
-        { ProfScope _ps(ctx, scatter_name);
-        hipLaunchKernelGGL(part_scatter_staged_kernel<Sel>, dim3(L.G), dim3(ST_T), sg.lds_bytes, ctx->stream, sel, pred,
-                           L, offs, cols, perm, sg);
-        }
-        TFG_LAUNCH_CHECK();
+        int nc8 = cols.ncols;
+        for (int c = 0; c < cols.ncols; ++c)
+            if (cols.width[c] != 8) nc8 = 0;
+        if (nc8 > 3) nc8 = 0;
+        ProfScope _ps(ctx, scatter_name);
+        if (int rc = with_pred(pred, [&](auto pr) -> int {
+                using PR = decltype(pr);
+                switch (nc8) {
+                case 1: hipLaunchKernelGGL((part_scatter_staged_kernel<Sel, PR, 1>), dim3(L.G), dim3(ST_T), sg.lds_bytes, ctx->stream, sel, pr, L, offs, cols, perm, sg); break;
+                case 2: hipLaunchKernelGGL((part_scatter_staged_kernel<Sel, PR, 2>), dim3(L.G), dim3(ST_T), sg.lds_bytes, ctx->stream, sel, pr, L, offs, cols, perm, sg); break;
+                case 3: hipLaunchKernelGGL((part_scatter_staged_kernel<Sel, PR, 3>), dim3(L.G), dim3(ST_T), sg.lds_bytes, ctx->stream, sel, pr, L, offs, cols, perm, sg); break;
+                default: hipLaunchKernelGGL((part_scatter_staged_kernel<Sel, PR, 0>), dim3(L.G), dim3(ST_T), sg.lds_bytes, ctx->stream, sel, pr, L, offs, cols, perm, sg); break;
+                }
+                TFG_LAUNCH_CHECK();
+                return TFG_OK;
+            }))
+            return rc;
     } else if (L.n > 0 && (perm || part_out || cols.ncols > 0)) {
         { ProfScope _ps(ctx, scatter_name);
         hipLaunchKernelGGL((part_scatter_kernel<Sel, STABLE>), dim3(L.G), dim3(PT),
