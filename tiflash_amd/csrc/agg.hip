@@ -7,8 +7,8 @@
 // (Aggregator.cpp:2338-2505, 2940-3097); convertToBlockImplFinal (:1651-1780).
 //
 // GPU design (the radix-bucketed analogue of TwoLevelHashTable's 256 buckets):
-//   1. bucket pass — fused predicate + CRC32-C key hash + LDS-histogram partition of the
-//      (key, args) rows into B = 2^bucket_bits buckets (bucket = crc & (B-1));
+//   1. bucket pass — fused predicate + key radix + LDS-histogram partition of the
+//      (key, args) rows into B = 2^bucket_bits buckets (bucket = Fibonacci radix of the key, fib_part);
 //   2. bucket kernel — one workgroup per bucket builds an open-addressing table in LDS
 //      (linear probing, 64-bit ds_cmpst for keys, ds_add_{u64,f64} for states, key 0 and the
 //      NULL key in side slots like ZeroValueStorage) seeded with the bucket's existing groups,
@@ -452,19 +452,31 @@ template <int NA> struct GenericOps {
 };
 
 template <int A0, int A1, int A2> struct FastOps {
-    static constexpr int NA = (A0 ? 1 : 0) + (A1 ? 1 : 0) + (A2 ? 1 : 0);
+    // rows are staged as interleaved records: key, then one word per summed argument
+    static constexpr int op(int i) { return i == 0 ? A0 : (i == 1 ? A1 : A2); }
+    static constexpr int NCOL = 1 + (A0 >= 2) + (A1 >= 2) + (A2 >= 2);
+    static constexpr int pos(int i) { return 1 + (i > 0 && A0 >= 2) + (i > 1 && A1 >= 2); }
     struct Row {
         uint64_t key;
         uint64_t v[3];
     };
     const AggSpec &S;
     int mode;
-    static __device__ __forceinline__ constexpr int op(int i) { return i == 0 ? A0 : (i == 1 ? A1 : A2); }
     __device__ __forceinline__ void load(const RowsIO &rows, int64_t r, Row &v) const {
-        v.key = ((const uint64_t *)rows.key)[r];
+        const uint64_t *rec = (const uint64_t *)rows.key + r * NCOL;
+        if constexpr (NCOL == 2) {
+            const uint4 q = *(const uint4 *)rec;
+            v.key = ((uint64_t)q.y << 32) | q.x;
+            const uint64_t w = ((uint64_t)q.w << 32) | q.z;
 #pragma unroll
-        for (int i = 0; i < 3; ++i)
-            if (op(i) >= 2) v.v[i] = ((const uint64_t *)rows.val[i])[r];
+            for (int i = 0; i < 3; ++i)
+                if (op(i) >= 2) v.v[i] = w;
+        } else {
+            v.key = rec[0];
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+                if (op(i) >= 2) v.v[i] = rec[pos(i)];
+        }
     }
     __device__ __forceinline__ uint64_t key(const Row &v) const { return v.key; }
     __device__ __forceinline__ bool knull(const Row &) const { return false; }
@@ -478,10 +490,11 @@ template <int A0, int A1, int A2> struct FastOps {
         }
     }
     __device__ __forceinline__ void store(const RowsIO &sp, int64_t w, const Row &v) const {
-        ((uint64_t *)sp.key)[w] = v.key;
+        uint64_t *rec = (uint64_t *)sp.key + w * NCOL;
+        rec[0] = v.key;
 #pragma unroll
         for (int i = 0; i < 3; ++i)
-            if (op(i) >= 2) ((uint64_t *)sp.val[i])[w] = v.v[i];
+            if (op(i) >= 2) rec[pos(i)] = v.v[i];
     }
     __device__ __forceinline__ uint64_t probe_val(const Row &v) const { return v.v[0]; }
 };
@@ -709,18 +722,18 @@ __global__ void agg_state_add_kernel(AggSpec S, GroupsIO dst, GroupsIO src) { //
     }
 }
 
-// bucket of a key: CRC32-C of the zero-extended key bits (HashCRC32 union form, Hash.h:282-292)
+// bucket of a key: Fibonacci radix of the zero-extended key bits (NULL key -> bucket 0)
 struct SelBucket {
     const void *key;
     const uint8_t *key_null;
     int width;
-    uint32_t mask;
-    static constexpr bool needs_crc = true;
+    uint32_t shift;
+    static constexpr bool needs_crc = false;
     __device__ __forceinline__ Loaded load(int64_t r) const {
         return Loaded{load_bits(key, width, r), key_null ? (uint32_t)key_null[r] : 0u};
     }
     __device__ __forceinline__ uint32_t part(const uint32_t (*t)[256], const Loaded &l, int64_t) const {
-        return l.null ? 0u : (int_hash_crc32(t, l.bits) & mask);
+        return l.null ? 0u : fib_part(l.bits, shift);
     }
     __device__ __forceinline__ uint32_t operator()(const uint32_t (*t)[256], int64_t r) const { return part(t, load(r), r); }
 };
@@ -830,12 +843,16 @@ int consume_keyed(tfg_agg *a, int mode, const RowPred &pred, const void *keys, i
     const AggSpec &S = a->S;
     const uint32_t B = a->B;
     const size_t n_old = a->n_groups;
+    // fast signature: rows staged as interleaved records (key + summed arguments, 8 B each)
+    const int fast = given_off ? 0 : fast_signature(S, mode, key_width, key_null, val_nulls);
+    int rec_words = 1;
+    for (int c = fast; c > 0; c /= 10) rec_words += (c % 10) >= 2;
     // ---- scratch layout
     Carver cv;
-    const size_t o_key = cv.take<uint64_t>(n), o_knull = cv.take<uint8_t>(n);
+    const size_t o_key = cv.take<uint64_t>(n * (fast ? rec_words : 1)), o_knull = cv.take<uint8_t>(n);
     size_t o_val[AGG_MAX] = {}, o_vnull[AGG_MAX] = {}, o_vcnt[AGG_MAX] = {};
     int vw[AGG_MAX] = {};
-    for (int i = 0; i < S.n_aggs; ++i) {
+    for (int i = 0; i < S.n_aggs && !fast; ++i) {
         if (val_nulls && val_nulls[i]) o_vnull[i] = cv.take<uint8_t>(n);
         if (val_cnts && val_cnts[i]) o_vcnt[i] = cv.take<uint64_t>(n);
         if (!vals[i]) continue;
@@ -875,11 +892,31 @@ int consume_keyed(tfg_agg *a, int mode, const RowPred &pred, const void *keys, i
             }
         }
         TFG_HIP(hipMemcpyAsync(stage_off, given_off, (B + 1) * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    } else if (fast) {
+        PCols pc{};
+        pc.in[0] = keys;
+        pc.out[0] = rows.key;
+        pc.width[0] = 8;
+        pc.ncols = 1;
+        pc.key0 = 1;
+        pc.aos = 1;
+        for (int i = 0, c = fast; i < S.n_aggs; ++i) {
+            const int op = (i == 0 ? c / 100 : i == 1 ? c / 10 : c) % 10;
+            if (op < 2) continue;
+            pc.in[pc.ncols] = vals[i];
+            pc.width[pc.ncols++] = 8;
+        }
+        TFG_CHECK(pc.ncols == rec_words, TFG_ERR_LOGICAL, "record layout mismatch");
+        SelBucket sel{keys, key_null, key_width, fib_shift(B)};
+        if (int rc = run_partition<SelBucket, false>(ctx, sel, pred, L, pc, nullptr, nullptr, stage_off, sb + o_part,
+                                                      "agg.part.hist", "agg.part.scatter"))
+            return rc;
     } else {
         PCols pc{};
         pc.in[pc.ncols] = keys;
         pc.out[pc.ncols] = rows.key;
         pc.width[pc.ncols++] = key_width;
+        pc.key0 = key_width == 8;
         if (key_null) {
             pc.in[pc.ncols] = key_null;
             pc.out[pc.ncols] = rows.key_null;
@@ -900,7 +937,7 @@ int consume_keyed(tfg_agg *a, int mode, const RowPred &pred, const void *keys, i
             }
         }
         TFG_CHECK(pc.ncols <= PCOLS, TFG_ERR_NOT_IMPLEMENTED, "too many aggregate columns");
-        SelBucket sel{keys, key_null, key_width, B - 1};
+        SelBucket sel{keys, key_null, key_width, fib_shift(B)};
         if (int rc = run_partition<SelBucket, false>(ctx, sel, pred, L, pc, nullptr, nullptr, stage_off, sb + o_part,
                                                       "agg.part.hist", "agg.part.scatter"))
             return rc;
@@ -923,7 +960,6 @@ int consume_keyed(tfg_agg *a, int mode, const RowPred &pred, const void *keys, i
     const uint64_t *ooff = has_old ? a->bucket_off[a->cur] : (const uint64_t *)nullptr;
     {
         ProfScope _ps(ctx, "agg.bucket");
-        const int fast = fast_signature(S, mode, key_width, key_null, val_nulls);
 #define TFG_BUCKET(...) launch_bucket<__VA_ARGS__>(B, S, ctx->stream, rows, rows1, mode, stage_off, old, ooff, tmp, new_cnt)
         switch (fast) {
         case 310: TFG_BUCKET(FastOps<3, 1, 0>); break;

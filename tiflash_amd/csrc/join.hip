@@ -6,8 +6,9 @@
 // (Join.cpp:1153-1358, 1977; JoinPartition.cpp:1290-1378, 1465-1644).
 //
 // GPU design (radix-partitioned, LDS-bucketed open addressing):
-//   finalize: the build keys are partitioned into P = 2^k partitions by CRC32-C(key) & (P-1)
-//             (hash seeded like HashCRC32<UInt64>), P sized so a partition fits the LDS table;
+//   finalize: the build keys are partitioned into P = 2^k partitions by the Fibonacci radix of
+//             the key bits (fib_part; internal, so not the CRC), P sized so a partition fits the
+//             LDS table;
 //   probe:    probe keys are partitioned by the same function, then one workgroup per partition
 //             loads the build partition into an LDS open-addressing table (u64 keys, 64-bit CAS,
 //             per-key chains of build rows = RowRefList), streams the probe partition, and emits
@@ -49,13 +50,13 @@ struct SelJoin {
     const void *key;
     const uint8_t *key_null;
     int width;
-    uint32_t mask;
-    static constexpr bool needs_crc = true;
+    uint32_t shift;
+    static constexpr bool needs_crc = false;
     __device__ __forceinline__ Loaded load(int64_t r) const {
         return Loaded{jload_bits(key, width, r), key_null ? (uint32_t)key_null[r] : 0u};
     }
     __device__ __forceinline__ uint32_t part(const uint32_t (*t)[256], const Loaded &l, int64_t) const {
-        return l.null ? 0xFFFFFFFFu : (int_hash_crc32(t, l.bits) & mask); // NULL keys never join
+        return l.null ? 0xFFFFFFFFu : fib_part(l.bits, shift); // NULL keys never join
     }
     __device__ __forceinline__ uint32_t operator()(const uint32_t (*t)[256], int64_t r) const { return part(t, load(r), r); }
 };
@@ -391,7 +392,8 @@ int tfg_join_finalize(tfg_join *j) {
     pc.in[0] = j->keys;
     pc.out[0] = j->bkeys;
     pc.width[0] = 8;
-    SelJoin sel{j->keys, j->nulls, 8, P - 1};
+    pc.key0 = 1;
+    SelJoin sel{j->keys, j->nulls, 8, fib_shift(P)};
     RowPred pred{};
     if (int rc = run_partition<SelJoin, false>(ctx, sel, pred, L, pc, j->brows, nullptr, j->boff, tmp, "join.build.hist",
                                                "join.build.scatter"))
@@ -438,7 +440,8 @@ int tfg_join_probe(tfg_join *j, int kind, const void *keys, const uint8_t *key_n
         pc.in[0] = keys;
         pc.out[0] = sb + o_pk;
         pc.width[0] = j->width;
-        SelJoin sel{keys, key_nullmap, j->width, P - 1};
+        pc.key0 = j->width == 8;
+        SelJoin sel{keys, key_nullmap, j->width, fib_shift(P)};
         RowPred pred{};
         uint64_t *poff = (uint64_t *)(sb + o_poff);
         if (int rc = run_partition<SelJoin, false>(ctx, sel, pred, L, pc, (uint32_t *)(sb + o_pr), nullptr, poff, sb + o_tmp,

@@ -26,6 +26,8 @@ struct PCols {
     void *out[PCOLS];
     int width[PCOLS];
     int ncols;
+    int key0; // column 0 holds the 8-byte key the selector loads (its staged copy reuses that load)
+    int aos;  // all columns 8 bytes, written as interleaved records of ncols words at out[0]
 };
 
 // Key columns hashed with IColumn::updateWeakHash32 semantics.
@@ -65,6 +67,19 @@ __device__ __forceinline__ uint32_t hash_key_row(const uint32_t (*t)[256], const
 // A selector maps a row to its partition (0xFFFFFFFF drops the row).  The work is split into
 // load(r) — the global loads — and part(crc, loaded, r), so kernels can issue the loads of
 // many rows before any of them is consumed (memory-level parallelism).
+// Internal radix of a key (aggregation buckets, join partitions): Fibonacci hashing, the top
+// `bits` bits of key * 2^64/phi.  These radices never leave the device (unlike the exchange
+// selector, which must reproduce fillSelector's CRC32-C routing), so a one-multiply hash
+// replaces the eight LDS table lookups of the CRC.
+__device__ __forceinline__ uint32_t fib_part(uint64_t key, uint32_t shift) {
+    return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 32 >> shift); // shift = 32 - bits (32 -> 0)
+}
+inline uint32_t fib_shift(uint32_t parts) { // parts is a power of two
+    uint32_t b = 0;
+    while ((1u << b) < parts) ++b;
+    return 32 - b;
+}
+
 struct Loaded {
     uint64_t bits;
     uint32_t null;
@@ -193,8 +208,10 @@ template <typename F> int with_pred(const RowPred &p, F &&f) {
 struct PartLayout {
     int64_t n;
     int64_t seg;   // rows per segment (multiple of PT)
-    unsigned G;    // segments = workgroups
+    unsigned G;    // segments = scatter workgroups
     uint32_t P;    // partitions
+    unsigned sub = 1;   // histogram workgroups per segment (> 1: counts accumulated atomically)
+    int64_t subseg = 0; // rows per histogram workgroup (multiple of PT)
 };
 
 inline PartLayout make_layout(int64_t n, uint32_t P) {
@@ -213,6 +230,36 @@ inline PartLayout make_layout(int64_t n, uint32_t P) {
     if (g < 1) g = 1;
     L.seg = seg;
     L.G = (unsigned)g;
+    L.sub = 1;
+    L.subseg = seg;
+    return L;
+}
+
+// Layout of the LDS-staged scatter: one long segment per CU (times TFG_STAGE_G, default 1), so
+// a destination's rows from one workgroup form a single long run (consecutive tiles continue
+// each other's partially written cache lines while they are still in L2) and the P x G count
+// table stays small; the histogram pass splits each segment over `sub` workgroups to keep the
+// chip full.
+inline PartLayout make_wide_layout(int64_t n, uint32_t P, int cu_count, unsigned gmax) {
+    static const int mult = [] {
+        const char *e = getenv("TFG_STAGE_G");
+        return e ? std::max(1, atoi(e)) : 1;
+    }();
+    PartLayout L;
+    L.n = n;
+    L.P = P;
+    int64_t g = std::min<int64_t>((int64_t)cu_count * mult, gmax);
+    if (g < 1) g = 1;
+    int64_t seg = (n + g - 1) / g;
+    seg = std::max<int64_t>((seg + PT - 1) / PT * PT, PT);
+    g = std::max<int64_t>((n + seg - 1) / seg, 1);
+    L.seg = seg;
+    L.G = (unsigned)g;
+    int64_t sub = std::max<int64_t>(1, 2048 / g);
+    int64_t subseg = (seg + sub - 1) / sub;
+    subseg = std::max<int64_t>((subseg + PT - 1) / PT * PT, (int64_t)8 * PT);
+    L.subseg = std::min(subseg, seg);
+    L.sub = (unsigned)((seg + L.subseg - 1) / L.subseg);
     return L;
 }
 
@@ -223,8 +270,9 @@ __global__ void __launch_bounds__(PT) part_hist_kernel(Sel sel, Pred pred, PartL
     for (uint32_t p = threadIdx.x; p < L.P; p += PT) hist[p] = 0;
     if constexpr (Sel::needs_crc) load_crc_lds(crc);
     __syncthreads();
-    const int64_t begin = (int64_t)blockIdx.x * L.seg;
-    int64_t end = begin + L.seg;
+    const unsigned g = blockIdx.x / L.sub, sg = blockIdx.x % L.sub;
+    const int64_t begin = (int64_t)g * L.seg + (int64_t)sg * L.subseg;
+    int64_t end = std::min<int64_t>(begin + L.subseg, (int64_t)g * L.seg + L.seg);
     if (end > L.n) end = L.n;
     int64_t r = begin + threadIdx.x;
     constexpr int U = 8;
@@ -247,10 +295,20 @@ __global__ void __launch_bounds__(PT) part_hist_kernel(Sel sel, Pred pred, PartL
         if (p < L.P) atomicAdd(&hist[p], 1u);
     }
     __syncthreads();
-    for (uint32_t p = threadIdx.x; p < L.P; p += PT) counts[(int64_t)p * L.G + blockIdx.x] = hist[p];
+    if (L.sub == 1) {
+        for (uint32_t p = threadIdx.x; p < L.P; p += PT) counts[(int64_t)p * L.G + g] = hist[p];
+    } else {
+        for (uint32_t p = threadIdx.x; p < L.P; p += PT)
+            if (hist[p]) atomicAdd(&counts[(int64_t)p * L.G + g], hist[p]);
+    }
 }
 
 __device__ __forceinline__ void scatter_row(const PCols &cols, int64_t r, uint64_t pos) {
+    if (cols.aos) {
+        for (int j = 0; j < cols.ncols; ++j)
+            ((uint64_t *)cols.out[0])[pos * cols.ncols + j] = ((const uint64_t *)cols.in[j])[r];
+        return;
+    }
     for (int j = 0; j < cols.ncols; ++j) {
         switch (cols.width[j]) {
         case 1: ((uint8_t *)cols.out[j])[pos] = ((const uint8_t *)cols.in[j])[r]; break;
@@ -370,6 +428,7 @@ struct StagedGeom {
     int crc_off;
     int red_off;
     int lds_bytes;
+    int dbg; // timing ablations (TFG_DBG_SCATTER): 1 no stream-out, 2 no placement / stream-out
 };
 
 // LDS bytes a staged-scatter workgroup may use (TFG_STAGE_LDS overrides; tuning knob).
@@ -402,12 +461,17 @@ inline bool make_staged_geom(uint32_t P, const PCols &cols, bool perm, bool crc,
     g.crc_off = (int)((off + 15) & ~size_t(15));
     g.red_off = g.crc_off + (crc ? 8192 : 0);
     g.lds_bytes = g.red_off + 64;
+    static const int dbg = [] {
+        const char *e = getenv("TFG_DBG_SCATTER");
+        return e ? atoi(e) : 0;
+    }();
+    g.dbg = dbg;
     return true;
 }
 
 // NC8 > 0: compile-time fast path for exactly NC8 columns of 8 bytes (keys, payloads); the
 // column loops unroll and no per-row width switch remains.  NC8 == 0: any widths.
-template <typename Sel, typename Pred, int NC8>
+template <typename Sel, typename Pred, int NC8, bool AOS = false>
 __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, Pred pred, PartLayout L,
                                                                    const uint64_t *offs, PCols cols, uint32_t *perm,
                                                                    StagedGeom g) {
@@ -487,6 +551,12 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
         const uint32_t kept = red[ST_T / 64];
         // 3. place rows in LDS in destination order
         uint32_t sl[ST_MAXR];
+        if (g.dbg == 2) {
+            __syncthreads();
+            for (uint32_t p = threadIdx.x; p < P; p += ST_T) run[p] += hist[p];
+            __syncthreads();
+            continue;
+        }
 #pragma unroll
         for (int j = 0; j < ST_MAXR; ++j) {
             if (bq[j] == 0xFFFFFFFFu) continue;
@@ -536,11 +606,20 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
         }
         __syncthreads();
         // 4. stream the sorted tile out: lanes of a run write consecutive addresses
-        for (uint32_t s = threadIdx.x; s < kept; s += ST_T) {
+        for (uint32_t s = threadIdx.x; s < (g.dbg ? 0u : kept); s += ST_T) {
             const uint32_t b = sb[s];
             const uint64_t gp = run[b] + (s - start[b]);
             if (perm) perm[gp] = sperm[s];
-            if constexpr (NC8 > 0) {
+            if constexpr (AOS && NC8 == 2) { // one 16-byte record store per row
+                const uint64_t a0 = reinterpret_cast<const uint64_t *>(lds + g.stage_off[0])[s];
+                const uint64_t a1 = reinterpret_cast<const uint64_t *>(lds + g.stage_off[1])[s];
+                reinterpret_cast<uint4 *>(cols.out[0])[gp] =
+                    make_uint4((uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)a1, (uint32_t)(a1 >> 32));
+            } else if constexpr (AOS) {
+#pragma unroll
+                for (int c = 0; c < NC8; ++c)
+                    ((uint64_t *)cols.out[0])[gp * NC8 + c] = reinterpret_cast<const uint64_t *>(lds + g.stage_off[c])[s];
+            } else if constexpr (NC8 > 0) {
 #pragma unroll
                 for (int c = 0; c < NC8; ++c)
                     ((uint64_t *)cols.out[c])[gp] = reinterpret_cast<const uint64_t *>(lds + g.stage_off[c])[s];
@@ -564,10 +643,14 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
 }
 
 template <typename Sel, bool STABLE = true>
-int run_partition(Ctx *ctx, const Sel &sel, const RowPred &pred, const PartLayout &L, const PCols &cols,
+int run_partition(Ctx *ctx, const Sel &sel, const RowPred &pred, const PartLayout &L0, const PCols &cols,
                   uint32_t *perm, uint32_t *part_out, uint64_t *offsets_out, void *tmp,
                   const char *hist_name = "part.hist", const char *scatter_name = "part.scatter") {
-    TFG_CHECK(L.P >= 1 && L.P <= (STABLE ? PMAX : PMAX_UNSTABLE), TFG_ERR_INVALID_ARG, "partition count %u out of range", L.P);
+    TFG_CHECK(L0.P >= 1 && L0.P <= (STABLE ? PMAX : PMAX_UNSTABLE), TFG_ERR_INVALID_ARG, "partition count %u out of range", L0.P);
+    StagedGeom sg{};
+    const bool staged = !STABLE && !part_out && L0.n > 0 && make_staged_geom(L0.P, cols, perm != nullptr, Sel::needs_crc, sg);
+    // the staged scatter uses fewer, longer segments (P x G <= P x L0.G: fits the caller's tmp)
+    const PartLayout L = staged ? make_wide_layout(L0.n, L0.P, ctx->cu_count, L0.G) : L0;
     const int64_t e = (int64_t)L.P * L.G;
     char *t = (char *)tmp;
     uint32_t *counts = (uint32_t *)t;
@@ -577,8 +660,9 @@ int run_partition(Ctx *ctx, const Sel &sel, const RowPred &pred, const PartLayou
     void *scan_tmp = t;
     if (L.n > 0) {
         ProfScope _ps(ctx, hist_name);
+        if (L.sub > 1) TFG_HIP(hipMemsetAsync(counts, 0, (size_t)e * 4, ctx->stream));
         if (int rc = with_pred(pred, [&](auto pr) -> int {
-                hipLaunchKernelGGL((part_hist_kernel<Sel, decltype(pr)>), dim3(L.G), dim3(PT),
+                hipLaunchKernelGGL((part_hist_kernel<Sel, decltype(pr)>), dim3(L.G * L.sub), dim3(PT),
                                    hist_lds_bytes(L.P, Sel::needs_crc), ctx->stream, sel, pr, L, counts);
                 TFG_LAUNCH_CHECK();
                 return TFG_OK;
@@ -588,15 +672,21 @@ int run_partition(Ctx *ctx, const Sel &sel, const RowPred &pred, const PartLayou
         TFG_HIP(hipMemsetAsync(counts, 0, (size_t)e * 4, ctx->stream));
     }
     if (int rc = exclusive_scan_u32(ctx, counts, offs, e, scan_tmp)) return rc;
-    StagedGeom sg{};
-    if (!STABLE && !part_out && L.n > 0 && make_staged_geom(L.P, cols, perm != nullptr, Sel::needs_crc, sg)) {
+    if (staged) {
         int nc8 = cols.ncols;
         for (int c = 0; c < cols.ncols; ++c)
             if (cols.width[c] != 8) nc8 = 0;
         if (nc8 > 3) nc8 = 0;
+        TFG_CHECK(!cols.aos || nc8 >= 2, TFG_ERR_INVALID_ARG, "record layout needs 2-3 columns of 8 bytes");
         ProfScope _ps(ctx, scatter_name);
         if (int rc = with_pred(pred, [&](auto pr) -> int {
                 using PR = decltype(pr);
+                if (cols.aos) {
+                    if (nc8 == 2) hipLaunchKernelGGL((part_scatter_staged_kernel<Sel, PR, 2, true>), dim3(L.G), dim3(ST_T), sg.lds_bytes, ctx->stream, sel, pr, L, offs, cols, perm, sg);
+                    else hipLaunchKernelGGL((part_scatter_staged_kernel<Sel, PR, 3, true>), dim3(L.G), dim3(ST_T), sg.lds_bytes, ctx->stream, sel, pr, L, offs, cols, perm, sg);
+                    TFG_LAUNCH_CHECK();
+                    return TFG_OK;
+                }
                 switch (nc8) {
                 case 1: hipLaunchKernelGGL((part_scatter_staged_kernel<Sel, PR, 1>), dim3(L.G), dim3(ST_T), sg.lds_bytes, ctx->stream, sel, pr, L, offs, cols, perm, sg); break;
                 case 2: hipLaunchKernelGGL((part_scatter_staged_kernel<Sel, PR, 2>), dim3(L.G), dim3(ST_T), sg.lds_bytes, ctx->stream, sel, pr, L, offs, cols, perm, sg); break;
