@@ -738,6 +738,18 @@ struct SelBucket {
     __device__ __forceinline__ uint32_t operator()(const uint32_t (*t)[256], int64_t r) const { return part(t, load(r), r); }
 };
 
+// the fast path's selector: 8-byte keys without a NULL map
+struct SelBucket8 {
+    const uint64_t *key;
+    uint32_t shift;
+    static constexpr bool needs_crc = false;
+    __device__ __forceinline__ Loaded load(int64_t r) const { return Loaded{key[r], 0u}; }
+    __device__ __forceinline__ uint32_t part(const uint32_t (*)[256], const Loaded &l, int64_t) const {
+        return fib_part(l.bits, shift);
+    }
+    __device__ __forceinline__ uint32_t operator()(const uint32_t (*t)[256], int64_t r) const { return part(t, load(r), r); }
+};
+
 } // namespace tfg
 
 using namespace tfg;
@@ -907,8 +919,8 @@ int consume_keyed(tfg_agg *a, int mode, const RowPred &pred, const void *keys, i
             pc.width[pc.ncols++] = 8;
         }
         TFG_CHECK(pc.ncols == rec_words, TFG_ERR_LOGICAL, "record layout mismatch");
-        SelBucket sel{keys, key_null, key_width, fib_shift(B)};
-        if (int rc = run_partition<SelBucket, false>(ctx, sel, pred, L, pc, nullptr, nullptr, stage_off, sb + o_part,
+        SelBucket8 sel{(const uint64_t *)keys, fib_shift(B)};
+        if (int rc = run_partition<SelBucket8, false>(ctx, sel, pred, L, pc, nullptr, nullptr, stage_off, sb + o_part,
                                                       "agg.part.hist", "agg.part.scatter"))
             return rc;
     } else {

@@ -162,7 +162,7 @@ struct RowPred {
 
 // Compile-time specialised predicates for the hot cases (no per-row type switch):
 // KIND 0 = none, 1 = UInt8 mask, 2 = `T col Op scalar`.
-template <int KIND, typename T = int64_t> struct PredT {
+template <int KIND, typename T = int64_t, bool NULLS = true> struct PredT {
     const void *col;
     const uint8_t *nullmap;
     Num b;
@@ -176,13 +176,14 @@ template <int KIND, typename T = int64_t> struct PredT {
             memcpy(&bits, &x, sizeof(T));
             l.bits = bits;
         }
-        if constexpr (KIND != 0)
+        if constexpr (KIND != 0 && NULLS)
             if (nullmap) l.null = nullmap[r];
         return l;
     }
     __device__ __forceinline__ bool eval(const Loaded &l) const {
         if constexpr (KIND == 0) return true;
-        if (l.null) return false;
+        if constexpr (NULLS)
+            if (l.null) return false;
         if constexpr (KIND == 1) return l.bits != 0;
         else {
             T x;
@@ -196,11 +197,12 @@ template <int KIND, typename T = int64_t> struct PredT {
 // Calls f(pred) with the most specialised predicate type for `p`.
 template <typename F> int with_pred(const RowPred &p, F &&f) {
     if (p.kind == 0) return f(PredT<0>{nullptr, nullptr, p.b, p.op});
-    if (p.kind == 1) return f(PredT<1>{p.col, p.nullmap, p.b, p.op});
+    if (p.nullmap) return f(p); // nullable predicate columns: the generic evaluator
+    if (p.kind == 1) return f(PredT<1, int64_t, false>{p.col, nullptr, p.b, p.op});
     switch (p.type) {
-    case TFG_INT64: return f(PredT<2, int64_t>{p.col, p.nullmap, p.b, p.op});
-    case TFG_INT32: return f(PredT<2, int32_t>{p.col, p.nullmap, p.b, p.op});
-    case TFG_FLOAT64: return f(PredT<2, double>{p.col, p.nullmap, p.b, p.op});
+    case TFG_INT64: return f(PredT<2, int64_t, false>{p.col, nullptr, p.b, p.op});
+    case TFG_INT32: return f(PredT<2, int32_t, false>{p.col, nullptr, p.b, p.op});
+    case TFG_FLOAT64: return f(PredT<2, double, false>{p.col, nullptr, p.b, p.op});
     default: return f(p);
     }
 }
@@ -419,7 +421,7 @@ __global__ void gather_part_offsets_kernel(const uint64_t *offs, PartLayout L, u
 // destination), then streams the sorted tile out: consecutive lanes write consecutive
 // addresses of one destination run, so stores coalesce into runs of TR/P rows.
 constexpr int ST_T = 1024;     // threads (16 waves)
-constexpr int ST_MAXR = 8;     // rows per thread per tile (TR <= 4096)
+constexpr int ST_MAXR = 8;     // rows per thread per tile (TR <= 8192 < 2^16: ranks pack in 16 bits)
 
 struct StagedGeom {
     int TR;          // rows per tile (multiple of ST_T)
@@ -495,7 +497,10 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
         for (uint32_t p = threadIdx.x; p < P; p += ST_T) hist[p] = 0;
         __syncthreads();
         // 1. destination + rank of every row of the tile
-        uint32_t bq[ST_MAXR], rk[ST_MAXR];
+        uint32_t bq[ST_MAXR]; // destination (low 16 bits) | rank inside the tile (high 16 bits)
+        constexpr int VC = NC8 > 0 ? NC8 : 1;
+        uint64_t v[VC][ST_MAXR]; // NC8 path: payload words, loaded before the ranks / scan
+        const int c0 = NC8 > 0 && cols.key0 ? 1 : 0;
         constexpr int HB = ST_MAXR / 2; // two half-batches keep the live loaded values small
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -510,18 +515,33 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
                 }
             }
 #pragma unroll
-            for (int q = 0; q < HB; ++q) { // ... then destinations and ranks
+            for (int q = 0; q < HB; ++q) { // ... then destinations
                 const int j = h * HB + q;
                 bq[j] = 0xFFFFFFFFu;
                 const uint32_t r = tb + (uint32_t)j * ST_T + threadIdx.x;
                 if (j < per && r < end && pred.eval(pl[q])) {
                     const uint32_t b = sel.part(crc, kl[q], r);
-                    if (b < P) {
-                        bq[j] = b;
-                        rk[j] = atomicAdd(&hist[b], 1u);
-                    }
+                    if (b < P) bq[j] = b;
+                }
+                if constexpr (NC8 > 0) v[0][j] = kl[q].bits;
+                if constexpr (NC8 == 0) {
+                    if (bq[j] != 0xFFFFFFFFu) bq[j] |= atomicAdd(&hist[bq[j]], 1u) << 16;
                 }
             }
+        }
+        if constexpr (NC8 > 0) {
+            // payload loads in flight across the LDS rank / scan phases
+#pragma unroll
+            for (int c = 0; c < NC8; ++c) {
+                if (c < c0) continue;
+                const uint64_t *src = reinterpret_cast<const uint64_t *>(cols.in[c]);
+#pragma unroll
+                for (int j = 0; j < ST_MAXR; ++j)
+                    if (bq[j] != 0xFFFFFFFFu) v[c][j] = src[tb + (uint32_t)j * ST_T + threadIdx.x];
+            }
+#pragma unroll
+            for (int j = 0; j < ST_MAXR; ++j)
+                if (bq[j] != 0xFFFFFFFFu) bq[j] |= atomicAdd(&hist[bq[j]], 1u) << 16;
         }
         __syncthreads();
         // 2. exclusive scan of the tile histogram -> start of each destination inside the tile
@@ -560,22 +580,17 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
 #pragma unroll
         for (int j = 0; j < ST_MAXR; ++j) {
             if (bq[j] == 0xFFFFFFFFu) continue;
-            sl[j] = start[bq[j]] + rk[j];
-            sb[sl[j]] = (uint16_t)bq[j];
+            sl[j] = start[bq[j] & 0xFFFFu] + (bq[j] >> 16);
+            sb[sl[j]] = (uint16_t)(bq[j] & 0xFFFFu);
             if (perm) sperm[sl[j]] = tb + (uint32_t)j * ST_T + threadIdx.x;
         }
         if constexpr (NC8 > 0) {
 #pragma unroll
-            for (int c = 0; c < NC8; ++c) { // per column: every row's load in flight, then LDS stores
+            for (int c = 0; c < NC8; ++c) {
                 uint64_t *st = reinterpret_cast<uint64_t *>(lds + g.stage_off[c]);
-                const uint64_t *src = reinterpret_cast<const uint64_t *>(cols.in[c]);
-                uint64_t v[ST_MAXR];
 #pragma unroll
                 for (int j = 0; j < ST_MAXR; ++j)
-                    if (bq[j] != 0xFFFFFFFFu) v[j] = src[tb + (uint32_t)j * ST_T + threadIdx.x];
-#pragma unroll
-                for (int j = 0; j < ST_MAXR; ++j)
-                    if (bq[j] != 0xFFFFFFFFu) st[sl[j]] = v[j];
+                    if (bq[j] != 0xFFFFFFFFu) st[sl[j]] = v[c][j];
             }
         } else {
             for (int c = 0; c < ncols; ++c) {
