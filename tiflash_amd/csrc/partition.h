@@ -430,7 +430,8 @@ struct StagedGeom {
     int crc_off;
     int red_off;
     int lds_bytes;
-    int dbg; // timing ablations (TFG_DBG_SCATTER): 1 no stream-out, 2 no placement / stream-out
+    int dbg; // timing ablations (TFG_DBG_SCATTER): 1 no stream-out, 2 no placement / stream-out,
+             // 3 stream-out to tile-contiguous addresses (wrong results; isolates the write pattern)
 };
 
 // LDS bytes a staged-scatter workgroup may use (TFG_STAGE_LDS overrides; tuning knob).
@@ -621,15 +622,18 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
         }
         __syncthreads();
         // 4. stream the sorted tile out: lanes of a run write consecutive addresses
-        for (uint32_t s = threadIdx.x; s < (g.dbg ? 0u : kept); s += ST_T) {
+        for (uint32_t s = threadIdx.x; s < (g.dbg == 1 || g.dbg == 2 ? 0u : kept); s += ST_T) {
             const uint32_t b = sb[s];
-            const uint64_t gp = run[b] + (s - start[b]);
+            const uint64_t gp = g.dbg == 3 ? (uint64_t)(tb + s) : run[b] + (s - start[b]);
             if (perm) perm[gp] = sperm[s];
             if constexpr (AOS && NC8 == 2) { // one 16-byte record store per row
                 const uint64_t a0 = reinterpret_cast<const uint64_t *>(lds + g.stage_off[0])[s];
                 const uint64_t a1 = reinterpret_cast<const uint64_t *>(lds + g.stage_off[1])[s];
-                reinterpret_cast<uint4 *>(cols.out[0])[gp] =
-                    make_uint4((uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)a1, (uint32_t)(a1 >> 32));
+                typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+                u64x2 rec;
+                rec.x = a0;
+                rec.y = a1;
+                reinterpret_cast<u64x2 *>(cols.out[0])[gp] = rec; // (nontemporal stores measured no different)
             } else if constexpr (AOS) {
 #pragma unroll
                 for (int c = 0; c < NC8; ++c)
