@@ -143,6 +143,8 @@ int tfg_buf_alloc(tfg_ctx *ctx, size_t bytes, void **out_dev);
 int tfg_buf_free(tfg_ctx *ctx, void *dev);
 int tfg_upload(tfg_ctx *ctx, void *dst_dev, const void *src_host, size_t bytes);
 int tfg_download(tfg_ctx *ctx, void *dst_host, const void *src_dev, size_t bytes);
+/* Device-to-device copy, asynchronous on the context's stream (column concatenation / COW copies). */
+int tfg_copy(tfg_ctx *ctx, void *dst_dev, const void *src_dev, size_t bytes);
 
 /* Size in bytes of one value of `type`, 0 if unknown. */
 size_t tfg_type_width(int type);
@@ -294,6 +296,24 @@ int tfg_join_probe(tfg_join *join, int kind, const void *keys, const uint8_t *ke
                    uint64_t *out_count_host);
 /* Build-side statistics: rows inserted, distinct keys, partitions. */
 int tfg_join_stats(tfg_join *join, uint64_t *rows, uint64_t *partitions);
+
+/* ---------------------------------------------------------------- (e) exchange over RCCL */
+/* MPP ExchangeSender -> ExchangeReceiver repartition inside one node (HashPartitionWriter::
+ * partitionAndWriteBlocks, Flash/Mpp/HashPartitionWriter.cpp:139-204 -> MPPTunnelSet::write ->
+ * ExchangeReceiver, Flash/Mpp/ExchangeReceiver.cpp:626-945): one process per GPU, one RCCL
+ * communicator, all-to-all of the partition-major buffers tfg_hash_partition produces.
+ * Rank 0 creates the id (tfg_comm_unique_id, 128 bytes) and distributes it out of band. */
+typedef struct tfg_comm tfg_comm;
+int tfg_comm_unique_id(uint8_t *out_id, size_t len);
+int tfg_comm_init(tfg_ctx *ctx, int nranks, int rank, const uint8_t *id, size_t len, tfg_comm **out);
+int tfg_comm_destroy(tfg_comm *comm);
+int tfg_comm_info(tfg_comm *comm, int *nranks, int *rank);
+/* recv_bytes_host[p] = send_bytes_host[this rank] of rank p (host arrays of nranks entries; syncs). */
+int tfg_alltoall_counts(tfg_comm *comm, const uint64_t *send_bytes_host, uint64_t *recv_bytes_host);
+/* Byte all-to-all on the context's stream: send slice p = [send_displs[p], +send_bytes[p]) to rank
+ * p; rank p's slice lands at recv + recv_displs[p].  Counts / displacements are host arrays. */
+int tfg_alltoallv(tfg_comm *comm, const void *send, const uint64_t *send_bytes, const uint64_t *send_displs,
+                  void *recv, const uint64_t *recv_bytes, const uint64_t *recv_displs);
 
 #ifdef __cplusplus
 }

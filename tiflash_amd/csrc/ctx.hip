@@ -394,6 +394,14 @@ int tfg_upload(tfg_ctx *ctx, void *dst_dev, const void *src_host, size_t bytes) 
     return TFG_OK;
 }
 
+int tfg_copy(tfg_ctx *ctx, void *dst_dev, const void *src_dev, size_t bytes) {
+    TFG_CHECK(ctx, TFG_ERR_INVALID_ARG, "ctx is null");
+    if (!bytes) return TFG_OK;
+    TFG_CHECK(dst_dev && src_dev, TFG_ERR_INVALID_ARG, "null buffer");
+    TFG_HIP(hipMemcpyAsync(dst_dev, src_dev, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+    return TFG_OK;
+}
+
 int tfg_download(tfg_ctx *ctx, void *dst_host, const void *src_dev, size_t bytes) {
     TFG_CHECK(ctx, TFG_ERR_INVALID_ARG, "ctx is null");
     if (!bytes) return TFG_OK;

@@ -1,0 +1,410 @@
+// operators.cpp — Aggregator, Join, HashPartitionWriter, MPPExchange and the block streams of the
+// host layer, each a thin C++ facade over the C-ABI (tfa_host.h lists the reference interfaces).
+#include <algorithm>
+#include <cstring>
+
+#include "tfa_host.h"
+
+namespace tfa {
+
+// ================================================================ Aggregator
+Aggregator::Aggregator(Context &ctx, const Params &params) : ctx_(ctx), params_(params) {
+    if (params_.keys.size() > 1)
+        throw Exception("GROUP BY over more than one key column", ErrorCodes::NOT_IMPLEMENTED);
+    int key_type = 0;
+    if (!params_.keys.empty()) {
+        key_type_ = params_.src_header.getByName(params_.keys[0]).type;
+        if (key_type_.isString()) throw Exception("String GROUP BY keys", ErrorCodes::NOT_IMPLEMENTED);
+        key_type = key_type_.type;
+    }
+    std::vector<int> arg_types, arg_scales;
+    for (const auto &d : params_.aggregates) {
+        int kind;
+        DataType at;
+        if (d.function == "sum") {
+            if (d.argument_names.size() != 1)
+                throw Exception("sum takes one argument", ErrorCodes::BAD_ARGUMENTS);
+            kind = TFG_AGG_SUM;
+            at = params_.src_header.getByName(d.argument_names[0]).type;
+        } else if (d.function == "count") {
+            if (d.argument_names.empty()) {
+                kind = TFG_AGG_COUNT_ALL;
+            } else {
+                kind = TFG_AGG_COUNT;
+                at = params_.src_header.getByName(d.argument_names[0]).type;
+            }
+        } else {
+            throw Exception("Unknown aggregate function " + d.function, ErrorCodes::NOT_IMPLEMENTED);
+        }
+        kinds_.push_back(kind);
+        arg_types_.push_back(at);
+        arg_types.push_back(kind == TFG_AGG_COUNT_ALL ? 0 : (at.type | (at.nullable ? 0x100 : 0)));
+        arg_scales.push_back(at.scale);
+    }
+    tfg_agg_params p{params_.bucket_bits, params_.expected_groups};
+    check(tfg_agg_create(ctx_.raw(), key_type, (int)kinds_.size(), kinds_.data(), arg_types.data(), arg_scales.data(),
+                         &p, &agg_),
+          "tfg_agg_create");
+}
+
+Aggregator::~Aggregator() {
+    if (agg_) tfg_agg_destroy(agg_);
+}
+
+void Aggregator::argPointers(const Block &b, std::vector<const void *> &args, std::vector<const uint8_t *> &nulls,
+                             std::vector<ColumnPtr> &hold) const {
+    for (size_t i = 0; i < params_.aggregates.size(); ++i) {
+        if (kinds_[i] == TFG_AGG_COUNT_ALL) {
+            args.push_back(nullptr);
+            nulls.push_back(nullptr);
+            continue;
+        }
+        ColumnPtr c = materialize(ctx_, b.getByName(params_.aggregates[i].argument_names[0]).column);
+        hold.push_back(c);
+        args.push_back(c->dataPtr());
+        nulls.push_back(c->nullPtr());
+    }
+}
+
+void Aggregator::executeOnBlock(const Block &block, const FilterPtr &filter) {
+    const size_t n = block.rows();
+    std::vector<const void *> args;
+    std::vector<const uint8_t *> nulls;
+    std::vector<ColumnPtr> hold;
+    argPointers(block, args, nulls, hold);
+    ColumnPtr key;
+    if (!params_.keys.empty()) key = materialize(ctx_, block.getByName(params_.keys[0]).column);
+    check(tfg_agg_consume(agg_, key ? key->dataPtr() : nullptr, key ? key->nullPtr() : nullptr, args.data(), nulls.data(),
+                          filter ? (const uint8_t *)filter->dataPtr() : nullptr, (int64_t)n),
+          "tfg_agg_consume");
+}
+
+void Aggregator::executeOnBlockFiltered(const Block &block, const std::string &pred, int op, Field constant) {
+    const size_t n = block.rows();
+    std::vector<const void *> args;
+    std::vector<const uint8_t *> nulls;
+    std::vector<ColumnPtr> hold;
+    argPointers(block, args, nulls, hold);
+    ColumnPtr key;
+    if (!params_.keys.empty()) key = materialize(ctx_, block.getByName(params_.keys[0]).column);
+    ColumnPtr p = materialize(ctx_, block.getByName(pred).column);
+    check(tfg_agg_consume_filtered(agg_, p->type.type, p->dataPtr(), p->nullPtr(), op, constant.type, &constant.bits,
+                                   key ? key->dataPtr() : nullptr, key ? key->nullPtr() : nullptr, args.data(),
+                                   nulls.data(), (int64_t)n),
+          "tfg_agg_consume_filtered");
+}
+
+void Aggregator::mergeOnBlock(const Block &partial) {
+    const size_t n = partial.rows();
+    std::vector<const void *> states;
+    std::vector<const uint8_t *> nulls;
+    std::vector<ColumnPtr> hold;
+    for (const auto &d : params_.aggregates) {
+        ColumnPtr c = materialize(ctx_, partial.getByName(d.column_name).column);
+        hold.push_back(c);
+        states.push_back(c->dataPtr());
+        nulls.push_back(c->nullPtr());
+    }
+    ColumnPtr key;
+    if (!params_.keys.empty()) key = materialize(ctx_, partial.getByName(params_.keys[0]).column);
+    check(tfg_agg_consume_partial(agg_, key ? key->dataPtr() : nullptr, key ? key->nullPtr() : nullptr, states.data(),
+                                  nulls.data(), (int64_t)n),
+          "tfg_agg_consume_partial");
+}
+
+void Aggregator::merge(Aggregator &other) { check(tfg_agg_merge(agg_, other.agg_), "tfg_agg_merge"); }
+
+size_t Aggregator::size() const {
+    uint64_t g = 0;
+    check(tfg_agg_size(agg_, &g), "tfg_agg_size");
+    return g;
+}
+
+void Aggregator::reset() { check(tfg_agg_reset(agg_), "tfg_agg_reset"); }
+
+Block Aggregator::convertToBlock(bool final) const {
+    (void)final; // partial and final blocks have the same layout: state = result value + NULL flag
+    const size_t g = size();
+    Block out;
+    std::shared_ptr<IColumn> key;
+    if (!params_.keys.empty()) {
+        key = std::make_shared<IColumn>();
+        key->type = key_type_;
+        key->rows = g;
+        key->data = std::make_shared<DeviceBuffer>(ctx_, g * key_type_.width());
+        if (key_type_.nullable) key->nullmap = std::make_shared<DeviceBuffer>(ctx_, g);
+    }
+    std::vector<std::shared_ptr<IColumn>> states;
+    std::vector<void *> sp;
+    std::vector<uint8_t *> snp;
+    for (size_t i = 0; i < params_.aggregates.size(); ++i) {
+        int t = 0, w = 0;
+        check(tfg_agg_result_type(agg_, (int)i, &t, &w), "tfg_agg_result_type");
+        auto c = std::make_shared<IColumn>();
+        c->type.type = t;
+        c->type.scale = kinds_[i] == TFG_AGG_SUM ? arg_types_[i].scale : 0;
+        // sum over a nullable argument is Nullable (AggregateFunctionNullUnary); count never is
+        c->type.nullable = kinds_[i] == TFG_AGG_SUM && arg_types_[i].nullable;
+        c->rows = g;
+        c->data = std::make_shared<DeviceBuffer>(ctx_, g * (size_t)w);
+        if (c->type.nullable) c->nullmap = std::make_shared<DeviceBuffer>(ctx_, g);
+        sp.push_back(c->data->data());
+        snp.push_back(c->nullmap ? (uint8_t *)c->nullmap->data() : nullptr);
+        states.push_back(c);
+    }
+    uint64_t got = 0;
+    check(tfg_agg_result(agg_, key ? key->data->data() : nullptr, key && key->nullmap ? (uint8_t *)key->nullmap->data() : nullptr,
+                         sp.data(), snp.data(), g, &got),
+          "tfg_agg_result");
+    ctx_.sync();
+    if (key) out.insert({key, key->type, params_.keys[0]});
+    for (size_t i = 0; i < states.size(); ++i)
+        out.insert({states[i], states[i]->type, params_.aggregates[i].column_name});
+    return out;
+}
+
+// ================================================================ Join
+Join::Join(Context &ctx, JoinKind kind, const std::string &probe_key, const std::string &build_key,
+           int64_t expected_build_rows)
+    : ctx_(ctx), kind_(kind), probe_key_(probe_key), build_key_(build_key), expected_(expected_build_rows) {}
+
+Join::~Join() {
+    if (join_) tfg_join_destroy(join_);
+}
+
+void Join::initBuild(const Block &sample_block) {
+    sample_ = sample_block.cloneEmpty();
+    const DataType kt = sample_.getByName(build_key_).type;
+    if (kt.isString() || kt.width() > 8 || kt.type == TFG_FLOAT32 || kt.type == TFG_FLOAT64)
+        throw Exception("join key type " + kt.getName(), ErrorCodes::NOT_IMPLEMENTED);
+    check(tfg_join_create(ctx_.raw(), kt.type, expected_, &join_), "tfg_join_create");
+}
+
+void Join::insertFromBlock(const Block &block) {
+    if (!join_) initBuild(block);
+    if (finished_) throw Exception("insertFromBlock after finishOneBuild", ErrorCodes::LOGICAL_ERROR);
+    ColumnPtr k = materialize(ctx_, block.getByName(build_key_).column);
+    check(tfg_join_build(join_, k->dataPtr(), k->nullPtr(), (int64_t)block.rows()), "tfg_join_build");
+    build_blocks_.push_back(block);
+}
+
+void Join::finishOneBuild() {
+    if (!join_) throw Exception("finishOneBuild before initBuild", ErrorCodes::LOGICAL_ERROR);
+    check(tfg_join_finalize(join_), "tfg_join_finalize");
+    build_ = concatenateBlocks(ctx_, build_blocks_);
+    build_blocks_.clear();
+    finished_ = true;
+}
+
+uint64_t Join::buildRows() const {
+    uint64_t rows = 0, parts = 0;
+    if (join_) check(tfg_join_stats(join_, &rows, &parts), "tfg_join_stats");
+    return rows;
+}
+
+Block Join::joinBlock(const Block &probe_block) {
+    if (!finished_) finishOneBuild();
+    const size_t n = probe_block.rows();
+    ColumnPtr k = materialize(ctx_, probe_block.getByName(probe_key_).column);
+    const bool pairs = kind_ == JoinKind::Inner || kind_ == JoinKind::Left;
+    uint64_t cap = std::max<uint64_t>(n, 1), count = 0;
+    std::shared_ptr<DeviceBuffer> pi, bi;
+    for (;;) {
+        pi = std::make_shared<DeviceBuffer>(ctx_, cap * 4);
+        bi = pairs ? std::make_shared<DeviceBuffer>(ctx_, cap * 4) : nullptr;
+        const int rc = tfg_join_probe(join_, (int)kind_, k->dataPtr(), k->nullPtr(), (int64_t)n, (uint32_t *)pi->data(),
+                                      bi ? (uint32_t *)bi->data() : nullptr, cap, nullptr, &count);
+        if (rc == TFG_ERR_CAPACITY) {
+            cap = count;
+            continue;
+        }
+        check(rc, "tfg_join_probe");
+        break;
+    }
+    Block out;
+    for (const auto &c : probe_block.getColumnsWithTypeAndName()) {
+        ColumnPtr g = gatherColumn(ctx_, *c.column, (const uint32_t *)pi->data(), count, false);
+        out.insert({g, g->type, c.name});
+    }
+    if (pairs) {
+        for (const auto &c : build_.getColumnsWithTypeAndName()) {
+            if (out.has(c.name)) continue; // same-named key columns appear once
+            ColumnPtr g = gatherColumn(ctx_, *c.column, (const uint32_t *)bi->data(), count, kind_ == JoinKind::Left);
+            out.insert({g, g->type, c.name});
+        }
+    }
+    ctx_.sync();
+    return out;
+}
+
+// ================================================================ partitioning / exchange
+std::vector<Block> hashPartitionBlock(Context &ctx, const Block &block, const std::vector<size_t> &key_ids,
+                                      uint32_t partition_num) {
+    const size_t n = block.rows();
+    std::vector<int> types, key_idx(key_ids.begin(), key_ids.end());
+    std::vector<const void *> cols;
+    std::vector<const uint8_t *> nulls;
+    std::vector<ColumnPtr> hold;
+    // the null maps travel as extra UInt8 columns (never hashed)
+    std::vector<int> null_col(block.columns(), -1);
+    for (size_t j = 0; j < block.columns(); ++j) {
+        ColumnPtr c = materialize(ctx, block.safeGetByPosition(j).column);
+        if (c->type.isString()) throw Exception("partitioning String columns", ErrorCodes::NOT_IMPLEMENTED);
+        hold.push_back(c);
+        types.push_back(c->type.type);
+        cols.push_back(c->dataPtr());
+        nulls.push_back(c->nullPtr());
+    }
+    for (size_t j = 0; j < block.columns(); ++j) {
+        if (!hold[j]->nullmap) continue;
+        null_col[j] = (int)types.size();
+        types.push_back(TFG_UINT8);
+        cols.push_back(hold[j]->nullPtr());
+        nulls.push_back(nullptr);
+    }
+    std::vector<DeviceBufferPtr> outs_buf;
+    std::vector<void *> outs;
+    for (size_t j = 0; j < types.size(); ++j) {
+        outs_buf.push_back(std::make_shared<DeviceBuffer>(ctx, n * tfg_type_width(types[j])));
+        outs.push_back(outs_buf.back()->data());
+    }
+    DeviceBuffer offs_dev(ctx, (partition_num + 1) * 8);
+    std::vector<uint64_t> offs(partition_num + 1, 0);
+    check(tfg_hash_partition(ctx.raw(), (int64_t)n, (int)key_idx.size(), key_idx.data(), (int)types.size(), types.data(),
+                             cols.data(), nulls.data(), partition_num, outs.data(), (uint64_t *)offs_dev.data(), offs.data()),
+          "tfg_hash_partition");
+    std::vector<Block> parts(partition_num);
+    for (uint32_t p = 0; p < partition_num; ++p) {
+        const size_t r0 = offs[p], rows = offs[p + 1] - offs[p];
+        for (size_t j = 0; j < block.columns(); ++j) {
+            auto c = std::make_shared<IColumn>();
+            c->type = hold[j]->type;
+            c->rows = rows;
+            const size_t w = c->type.width();
+            c->data = std::make_shared<DeviceBuffer>(ctx, rows * w);
+            check(tfg_copy(ctx.raw(), c->data->data(), (char *)outs[j] + r0 * w, rows * w), "tfg_copy");
+            if (null_col[j] >= 0) {
+                c->nullmap = std::make_shared<DeviceBuffer>(ctx, rows);
+                check(tfg_copy(ctx.raw(), c->nullmap->data(), (char *)outs[null_col[j]] + r0, rows), "tfg_copy");
+            }
+            parts[p].insert({c, c->type, block.safeGetByPosition(j).name});
+        }
+    }
+    ctx.sync();
+    return parts;
+}
+
+HashPartitionWriter::HashPartitionWriter(Context &ctx, std::vector<size_t> partition_col_ids, uint32_t partition_num,
+                                         Sink sink, int64_t batch_send_min_limit)
+    : ctx_(ctx), partition_col_ids_(std::move(partition_col_ids)), partition_num_(partition_num), sink_(std::move(sink)),
+      limit_(batch_send_min_limit < 0 ? (int64_t)8192 * partition_num : batch_send_min_limit) {
+    if (partition_num_ == 0) throw Exception("partition_num must be positive", ErrorCodes::BAD_ARGUMENTS);
+}
+
+void HashPartitionWriter::write(const Block &block) {
+    if (!block || block.rows() == 0) return;
+    pending_.push_back(block);
+    pending_rows_ += block.rows();
+    if ((int64_t)pending_rows_ >= limit_) flush();
+}
+
+void HashPartitionWriter::flush() {
+    if (pending_.empty()) return;
+    Block all = concatenateBlocks(ctx_, pending_);
+    pending_.clear();
+    pending_rows_ = 0;
+    std::vector<Block> parts = hashPartitionBlock(ctx_, all, partition_col_ids_, partition_num_);
+    for (uint32_t p = 0; p < partition_num_; ++p) sink_(p, std::move(parts[p]));
+}
+
+MPPExchange::MPPExchange(Context &ctx, int nranks, int rank, const uint8_t *unique_id, size_t id_len)
+    : ctx_(ctx), nranks_(nranks), rank_(rank) {
+    check(tfg_comm_init(ctx.raw(), nranks, rank, unique_id, id_len, &comm_), "tfg_comm_init");
+}
+
+MPPExchange::~MPPExchange() {
+    if (comm_) tfg_comm_destroy(comm_);
+}
+
+Block MPPExchange::exchange(const std::vector<Block> &partitions) {
+    if ((int)partitions.size() != nranks_)
+        throw Exception("exchange needs one block per rank", ErrorCodes::BAD_ARGUMENTS);
+    const Block &proto = partitions[0];
+    std::vector<uint64_t> send_rows(nranks_), recv_rows(nranks_);
+    for (int p = 0; p < nranks_; ++p) send_rows[p] = partitions[p].rows();
+    check(tfg_alltoall_counts(comm_, send_rows.data(), recv_rows.data()), "tfg_alltoall_counts");
+    uint64_t total_send = 0, total_recv = 0;
+    for (int p = 0; p < nranks_; ++p) {
+        total_send += send_rows[p];
+        total_recv += recv_rows[p];
+    }
+    Block out;
+    for (size_t j = 0; j < proto.columns(); ++j) {
+        const DataType t = proto.safeGetByPosition(j).column->type;
+        if (t.isString()) throw Exception("exchanging String columns", ErrorCodes::NOT_IMPLEMENTED);
+        bool nullable = false;
+        for (const auto &b : partitions) nullable |= b.safeGetByPosition(j).column->nullmap != nullptr;
+        auto c = std::make_shared<IColumn>();
+        c->type = t;
+        c->type.nullable = nullable;
+        c->rows = total_recv;
+        // one pass per byte plane: values, then the null map
+        for (int plane = 0; plane < (nullable ? 2 : 1); ++plane) {
+            const size_t w = plane == 0 ? t.width() : 1;
+            DeviceBuffer send(ctx_, total_send * w);
+            auto recv = std::make_shared<DeviceBuffer>(ctx_, total_recv * w);
+            std::vector<uint64_t> sb(nranks_), sd(nranks_), rb(nranks_), rd(nranks_);
+            uint64_t so = 0, ro = 0;
+            for (int p = 0; p < nranks_; ++p) {
+                ColumnPtr src = materialize(ctx_, partitions[p].safeGetByPosition(j).column);
+                const size_t bytes = send_rows[p] * w;
+                if (plane == 0) {
+                    check(tfg_copy(ctx_.raw(), (char *)send.data() + so, src->dataPtr(), bytes), "tfg_copy");
+                } else if (src->nullmap) {
+                    check(tfg_copy(ctx_.raw(), (char *)send.data() + so, src->nullPtr(), bytes), "tfg_copy");
+                } else if (bytes) {
+                    std::vector<uint8_t> z(bytes, 0);
+                    check(tfg_upload(ctx_.raw(), (char *)send.data() + so, z.data(), bytes), "tfg_upload");
+                }
+                sb[p] = bytes;
+                sd[p] = so;
+                so += bytes;
+                rb[p] = recv_rows[p] * w;
+                rd[p] = ro;
+                ro += rb[p];
+            }
+            check(tfg_alltoallv(comm_, send.data(), sb.data(), sd.data(), recv->data(), rb.data(), rd.data()),
+                  "tfg_alltoallv");
+            ctx_.sync();
+            if (plane == 0) c->data = recv;
+            else c->nullmap = recv;
+        }
+        out.insert({c, c->type, proto.safeGetByPosition(j).name});
+    }
+    return out;
+}
+
+// ================================================================ streams
+AggregatingBlockInputStream::AggregatingBlockInputStream(Context &ctx, BlockInputStreamPtr input,
+                                                         const Aggregator::Params &params, bool final)
+    : ctx_(ctx), input_(std::move(input)), aggregator_(ctx, params), final_(final) {}
+
+Block AggregatingBlockInputStream::getHeader() const { return Block(); }
+
+Block AggregatingBlockInputStream::read() {
+    if (done_) return Block();
+    done_ = true;
+    while (Block b = input_->read()) aggregator_.executeOnBlock(b);
+    return aggregator_.convertToBlock(final_);
+}
+
+Block HashJoinProbeBlockInputStream::read() {
+    for (;;) {
+        Block b = input_->read();
+        if (!b) return b;
+        Block out = join_->joinBlock(b);
+        if (out.rows() > 0) return out;
+    }
+}
+
+} // namespace tfa

@@ -1,0 +1,426 @@
+// tfa_host.h — C++ host operators above the C-ABI (include/tiflash_amd.h).
+//
+// The reference's drop-in surface for this path is C++: FilterTransformAction,
+// the Aggregator facade, the Join facade, HashPartitionWriter and the IBlockInputStream wrappers
+// that PhysicalPlan instantiates from tipb::Executor.  This layer restates those interfaces over
+// device-resident columns — same names, argument meaning and error behaviour — and calls only
+// the C-ABI (no HIP, no torch).  Differences from the reference are listed per class.
+//
+//   Block / ColumnWithTypeAndName      Core/Block.h:41, Core/ColumnWithTypeAndName.h
+//   IColumn (immutable, COW-shared)    Columns/IColumn.h:426 (filter returns a new column)
+//   DB::Exception + ErrorCodes         Common/Exception.h, Common/ErrorCodes.cpp:30-198
+//   ExpressionActions                  Interpreters/ExpressionActions.cpp:351-364,547
+//   FilterTransformAction              DataStreams/FilterTransformAction.cpp:32-173
+//   Aggregator (Params, executeOnBlock, merge, convertToBlocks)  Interpreters/Aggregator.h:855-1035
+//   Join (initBuild, insertFromBlock, finishOneBuild, joinBlock)  Interpreters/Join.h:191-283
+//   HashPartitionWriter (write, flush)  Flash/Mpp/HashPartitionWriter.cpp:76-204
+//   IBlockInputStream (getHeader, read) DataStreams/IBlockInputStream.h:60-201
+#pragma once
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <functional>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/tiflash_amd.h"
+
+namespace tfa {
+
+// ---------------------------------------------------------------- errors (Common/ErrorCodes.cpp)
+namespace ErrorCodes {
+constexpr int SIZES_OF_COLUMNS_DOESNT_MATCH = 9;
+constexpr int BAD_ARGUMENTS = 36;
+constexpr int ILLEGAL_TYPE_OF_ARGUMENT = 43;
+constexpr int NOT_IMPLEMENTED = 48;
+constexpr int LOGICAL_ERROR = 49;
+constexpr int ILLEGAL_TYPE_OF_COLUMN_FOR_FILTER = 59;
+constexpr int CANNOT_ALLOCATE_MEMORY = 173;
+constexpr int NOT_FOUND_COLUMN_IN_BLOCK = 10;
+} // namespace ErrorCodes
+
+class Exception : public std::runtime_error {
+public:
+    Exception(const std::string &msg, int code) : std::runtime_error(msg), code_(code) {}
+    int code() const { return code_; }
+
+private:
+    int code_;
+};
+
+// Maps a tfg status to the reference's error code and throws (no-op on TFG_OK).
+void check(int status, const char *what);
+
+// ---------------------------------------------------------------- device context
+class Context {
+public:
+    explicit Context(int device = 0);
+    ~Context();
+    Context(const Context &) = delete;
+    Context &operator=(const Context &) = delete;
+    tfg_ctx *raw() const { return ctx_; }
+    void sync() const;
+    int device() const { return device_; }
+
+private:
+    tfg_ctx *ctx_ = nullptr;
+    int device_ = 0;
+};
+
+// device allocation owned by a column (freed with the last reference)
+class DeviceBuffer {
+public:
+    DeviceBuffer(Context &ctx, size_t bytes);
+    ~DeviceBuffer();
+    DeviceBuffer(const DeviceBuffer &) = delete;
+    DeviceBuffer &operator=(const DeviceBuffer &) = delete;
+    void *data() const { return ptr_; }
+    size_t bytes() const { return bytes_; }
+
+private:
+    Context &ctx_;
+    void *ptr_ = nullptr;
+    size_t bytes_ = 0;
+};
+using DeviceBufferPtr = std::shared_ptr<DeviceBuffer>;
+
+// ---------------------------------------------------------------- types and columns
+struct DataType {
+    int type = TFG_INT64; // tfg_type, or TYPE_STRING
+    int scale = 0;        // Decimal scale
+    bool nullable = false;
+    static constexpr int TYPE_STRING = 100;
+    size_t width() const; // bytes per value (0 for String)
+    bool isString() const { return type == TYPE_STRING; }
+    std::string getName() const;
+    bool operator==(const DataType &o) const { return type == o.type && scale == o.scale && nullable == o.nullable; }
+};
+
+// Immutable device column: fixed-width values (`data`), or String chars + UInt64 end offsets
+// (ColumnString layout, each row '\0'-terminated); optional NULL map (ColumnNullable).  A
+// const column (ColumnConst) keeps one host value and a row count.
+struct IColumn {
+    DataType type;
+    size_t rows = 0;
+    DeviceBufferPtr data;    // values, or chars for String
+    DeviceBufferPtr offsets; // String only: rows x UInt64
+    DeviceBufferPtr nullmap; // rows x UInt8 (1 = NULL) or null
+    size_t chars = 0;        // String only: bytes in `data`
+    bool is_const = false;
+    uint64_t const_value = 0; // is_const: the bits of the one value
+
+    size_t size() const { return rows; }
+    bool isColumnConst() const { return is_const; }
+    const void *dataPtr() const { return data ? data->data() : nullptr; }
+    const uint8_t *nullPtr() const { return nullmap ? (const uint8_t *)nullmap->data() : nullptr; }
+};
+using ColumnPtr = std::shared_ptr<const IColumn>;
+
+struct ColumnWithTypeAndName {
+    ColumnPtr column;
+    DataType type;
+    std::string name;
+};
+
+class Block {
+public:
+    Block() = default;
+    Block(std::initializer_list<ColumnWithTypeAndName> cols) : data_(cols) {}
+    explicit Block(std::vector<ColumnWithTypeAndName> cols) : data_(std::move(cols)) {}
+    void insert(ColumnWithTypeAndName c) { data_.push_back(std::move(c)); }
+    void insert(size_t position, ColumnWithTypeAndName c);
+    void erase(size_t position);
+    size_t columns() const { return data_.size(); }
+    size_t rows() const; // checks every column has the same size
+    bool has(const std::string &name) const;
+    size_t getPositionByName(const std::string &name) const;
+    const ColumnWithTypeAndName &getByName(const std::string &name) const;
+    ColumnWithTypeAndName &safeGetByPosition(size_t i);
+    const ColumnWithTypeAndName &safeGetByPosition(size_t i) const;
+    Block cloneEmpty() const;
+    void clear() { data_.clear(); }
+    explicit operator bool() const { return !data_.empty(); }
+    const std::vector<ColumnWithTypeAndName> &getColumnsWithTypeAndName() const { return data_; }
+
+private:
+    std::vector<ColumnWithTypeAndName> data_;
+};
+
+// host <-> device helpers (tests, sources, sinks)
+ColumnPtr makeColumn(Context &ctx, DataType type, const void *values, size_t rows,
+                     const uint8_t *nullmap = nullptr);
+ColumnPtr makeStringColumn(Context &ctx, const std::vector<std::string> &values,
+                           const uint8_t *nullmap = nullptr);
+ColumnPtr makeConstColumn(DataType type, uint64_t bits, size_t rows);
+ColumnPtr materialize(Context &ctx, const ColumnPtr &c); // ColumnConst -> full column
+std::vector<uint8_t> toHostBytes(Context &ctx, const IColumn &c);
+std::vector<uint8_t> toHostNullMap(Context &ctx, const IColumn &c);
+std::vector<std::string> toHostStrings(Context &ctx, const IColumn &c);
+template <typename T> std::vector<T> toHost(Context &ctx, const IColumn &c) {
+    std::vector<uint8_t> b = toHostBytes(ctx, c);
+    std::vector<T> out(c.rows);
+    if (!b.empty()) memcpy(out.data(), b.data(), std::min(b.size(), out.size() * sizeof(T)));
+    return out;
+}
+// Concatenates blocks with the same structure (Join build side, partition buffers).
+Block concatenateBlocks(Context &ctx, const std::vector<Block> &blocks);
+// Rows of `src` at `perm` (0xFFFFFFFF -> default value and, when make_nullable, NULL).
+ColumnPtr gatherColumn(Context &ctx, const IColumn &src, const uint32_t *perm_dev, size_t n, bool make_nullable);
+
+// ---------------------------------------------------------------- expressions (a1-a4)
+// A literal (Field) for constant operands.
+struct Field {
+    int type = TFG_INT64;
+    uint64_t bits = 0;
+    static Field Int64(int64_t v);
+    static Field UInt64(uint64_t v);
+    static Field Float64(double v);
+    static Field Decimal64(int64_t raw, int scale);
+    int scale = 0;
+};
+
+// ExpressionActions restricted to the functions on the hot path: comparisons, and/or/not,
+// plus/minus/multiply.  execute(block) appends each action's result column like the
+// reference's ExpressionActions::execute (Interpreters/ExpressionActions.cpp:351-364).
+class ExpressionActions {
+public:
+    explicit ExpressionActions(Context &ctx) : ctx_(ctx) {}
+    // result = lhs Op constant   (equals/notEquals/less/greater/lessOrEquals/greaterOrEquals)
+    ExpressionActions &compare(const std::string &lhs, int op, Field constant, const std::string &result);
+    // result = lhs Op rhs (columns)
+    ExpressionActions &compareColumns(const std::string &lhs, int op, const std::string &rhs, const std::string &result);
+    // result = and/or(a, b) or not(a)
+    ExpressionActions &logical(int op, const std::string &a, const std::string &b, const std::string &result);
+    // result = a (+|-|*) b; b may be a constant; result type / scale as FunctionBinaryArithmetic infers
+    ExpressionActions &arithmetic(int op, const std::string &a, const std::string &b, const std::string &result);
+    ExpressionActions &arithmeticConst(int op, const std::string &a, Field b, const std::string &result);
+    void execute(Block &block) const;
+    // the fused form: a single `column Op constant` predicate feeding a filter / aggregation
+    bool singleCompare(std::string &column, int &op, Field &constant, std::string &result) const;
+
+private:
+    struct Action {
+        int kind; // 0 compare-const, 1 compare-cols, 2 logical, 3 arith, 4 arith-const
+        int op;
+        std::string a, b, result;
+        Field constant;
+    };
+    Context &ctx_;
+    std::vector<Action> actions_;
+};
+using ExpressionActionsPtr = std::shared_ptr<ExpressionActions>;
+
+// ---------------------------------------------------------------- filter (a5-a8)
+using FilterPtr = ColumnPtr; // UInt8 mask column
+
+class FilterTransformAction {
+public:
+    FilterTransformAction(Context &ctx, const Block &header, ExpressionActionsPtr expression,
+                          const std::string &filter_column_name);
+    // Same contract as the reference (:72-173): returns false if every row is filtered out
+    // (block untouched), true otherwise; with return_filter the mask is returned instead of
+    // filtering (nullptr when all rows pass).  The filter column becomes a constant 1.
+    bool transform(Block &block, FilterPtr &res_filter, bool return_filter);
+    Block getHeader() const { return header_; }
+
+private:
+    Context &ctx_;
+    Block header_;
+    ExpressionActionsPtr expression_;
+    std::string filter_column_name_;
+};
+
+// ---------------------------------------------------------------- aggregation (a9-a17)
+struct AggregateDescription {
+    std::string function;                    // "sum" | "count"
+    std::vector<std::string> argument_names; // count() has none
+    std::string column_name;
+};
+using AggregateDescriptions = std::vector<AggregateDescription>;
+
+class Aggregator {
+public:
+    struct Params {
+        Block src_header;
+        std::vector<std::string> keys; // 0 or 1 fixed-width key (method key8..key64 / nullable)
+        AggregateDescriptions aggregates;
+        int bucket_bits = 0;
+        int64_t expected_groups = 0;
+    };
+    Aggregator(Context &ctx, const Params &params);
+    ~Aggregator();
+    Aggregator(const Aggregator &) = delete;
+    Aggregator &operator=(const Aggregator &) = delete;
+    // executeOnBlock (Aggregator.cpp:1127-1246); `filter` (optional UInt8 mask) skips rows
+    void executeOnBlock(const Block &block, const FilterPtr &filter = nullptr);
+    // fused FilterTransformAction -> Aggregator for `pred Op constant`
+    void executeOnBlockFiltered(const Block &block, const std::string &pred, int op, Field constant);
+    // two-phase final aggregation: a Block of (key, partial states) from convertToBlock(false)
+    void mergeOnBlock(const Block &partial);
+    void merge(Aggregator &other); // mergeDataImpl of two variants with one signature
+    size_t size() const;
+    // final = true: result columns (sum of nullable args is NULL when it saw no value);
+    // final = false: partial states (key, sum / count state columns) for an exchange
+    Block convertToBlock(bool final = true) const;
+    void reset();
+    tfg_agg *raw() const { return agg_; }
+
+private:
+    Context &ctx_;
+    Params params_;
+    tfg_agg *agg_ = nullptr;
+    DataType key_type_;
+    std::vector<int> kinds_;
+    std::vector<DataType> arg_types_;
+    void argPointers(const Block &b, std::vector<const void *> &args, std::vector<const uint8_t *> &nulls,
+                     std::vector<ColumnPtr> &hold) const;
+};
+
+// ---------------------------------------------------------------- hash join (a18-a21)
+enum class JoinKind { Inner = TFG_JOIN_INNER, Left = TFG_JOIN_LEFT, Semi = TFG_JOIN_SEMI, Anti = TFG_JOIN_ANTI };
+
+class Join {
+public:
+    Join(Context &ctx, JoinKind kind, const std::string &probe_key, const std::string &build_key,
+         int64_t expected_build_rows = 0);
+    ~Join();
+    Join(const Join &) = delete;
+    Join &operator=(const Join &) = delete;
+    void initBuild(const Block &sample_block);
+    void insertFromBlock(const Block &block); // rows with a NULL key are not inserted
+    void finishOneBuild();
+    // probe columns replicated per match, then the build block's non-key columns (LEFT: NULL
+    // where unmatched).  SEMI / ANTI return the probe columns of the qualifying rows.
+    Block joinBlock(const Block &probe_block);
+    uint64_t buildRows() const;
+
+private:
+    Context &ctx_;
+    JoinKind kind_;
+    std::string probe_key_, build_key_;
+    int64_t expected_;
+    tfg_join *join_ = nullptr;
+    Block sample_;
+    std::vector<Block> build_blocks_;
+    Block build_; // concatenated at finishOneBuild
+    bool finished_ = false;
+};
+
+// ---------------------------------------------------------------- exchange (a22-a24, e)
+// HashPartitionWriter::write / flush (HashPartitionWriter.cpp:76-204): rows are buffered until
+// batch_send_min_limit, then weak-hashed on the partition key columns, routed with fillSelector
+// (part = (h * P) >> 32) and scattered stably; `sink(part, block)` receives each partition's
+// block (the ExchangeSender tunnel; with an MPPExchange it is an all-to-all).
+class HashPartitionWriter {
+public:
+    using Sink = std::function<void(uint32_t, Block &&)>;
+    HashPartitionWriter(Context &ctx, std::vector<size_t> partition_col_ids, uint32_t partition_num, Sink sink,
+                        int64_t batch_send_min_limit = -1);
+    void write(const Block &block);
+    void flush();
+
+private:
+    Context &ctx_;
+    std::vector<size_t> partition_col_ids_;
+    uint32_t partition_num_;
+    Sink sink_;
+    int64_t limit_;
+    std::vector<Block> pending_;
+    size_t pending_rows_ = 0;
+};
+
+// Partition a block into partition_num blocks (the scatterColumns step alone).
+std::vector<Block> hashPartitionBlock(Context &ctx, const Block &block, const std::vector<size_t> &key_ids,
+                                      uint32_t partition_num);
+
+// One-node exchange over RCCL: every rank contributes partition_num == nranks blocks and
+// receives the concatenation of its partition from every rank (ExchangeReceiver output).
+class MPPExchange {
+public:
+    MPPExchange(Context &ctx, int nranks, int rank, const uint8_t *unique_id, size_t id_len);
+    ~MPPExchange();
+    Block exchange(const std::vector<Block> &partitions);
+    int nranks() const { return nranks_; }
+    int rank() const { return rank_; }
+
+private:
+    Context &ctx_;
+    tfg_comm *comm_ = nullptr;
+    int nranks_, rank_;
+};
+
+// ---------------------------------------------------------------- streams (IBlockInputStream)
+class IBlockInputStream {
+public:
+    virtual ~IBlockInputStream() = default;
+    virtual std::string getName() const = 0;
+    virtual Block getHeader() const = 0;
+    virtual Block read() = 0; // empty Block = end of stream
+    virtual void readPrefix() {}
+    virtual void readSuffix() {}
+};
+using BlockInputStreamPtr = std::shared_ptr<IBlockInputStream>;
+
+class BlocksListBlockInputStream : public IBlockInputStream {
+public:
+    explicit BlocksListBlockInputStream(std::vector<Block> blocks) : blocks_(std::move(blocks)) {}
+    std::string getName() const override { return "BlocksList"; }
+    Block getHeader() const override { return blocks_.empty() ? Block() : blocks_[0].cloneEmpty(); }
+    Block read() override { return pos_ < blocks_.size() ? blocks_[pos_++] : Block(); }
+
+private:
+    std::vector<Block> blocks_;
+    size_t pos_ = 0;
+};
+
+// FilterBlockInputStream: skips blocks the filter empties (DataStreams/FilterBlockInputStream.cpp)
+class FilterBlockInputStream : public IBlockInputStream {
+public:
+    FilterBlockInputStream(Context &ctx, BlockInputStreamPtr input, ExpressionActionsPtr expression,
+                           const std::string &filter_column);
+    std::string getName() const override { return "Filter"; }
+    Block getHeader() const override { return action_.getHeader(); }
+    Block read() override;
+
+private:
+    BlockInputStreamPtr input_;
+    FilterTransformAction action_;
+};
+
+// AggregatingBlockInputStream: consumes the whole input, then returns the result block
+// (DataStreams/AggregatingBlockInputStream.cpp).  For the fused filter -> aggregation form
+// (no mask materialised) use Aggregator::executeOnBlockFiltered directly.
+class AggregatingBlockInputStream : public IBlockInputStream {
+public:
+    AggregatingBlockInputStream(Context &ctx, BlockInputStreamPtr input, const Aggregator::Params &params,
+                                bool final = true);
+    std::string getName() const override { return "Aggregating"; }
+    Block getHeader() const override;
+    Block read() override;
+
+private:
+    Context &ctx_;
+    BlockInputStreamPtr input_;
+    Aggregator aggregator_;
+    bool final_;
+    bool done_ = false;
+};
+
+// HashJoinProbeBlockInputStream: joinBlock per probe block (DataStreams/HashJoinProbeBlockInputStream.cpp)
+class HashJoinProbeBlockInputStream : public IBlockInputStream {
+public:
+    HashJoinProbeBlockInputStream(BlockInputStreamPtr input, std::shared_ptr<Join> join)
+        : input_(std::move(input)), join_(std::move(join)) {}
+    std::string getName() const override { return "HashJoinProbe"; }
+    Block getHeader() const override { return input_->getHeader(); }
+    Block read() override;
+
+private:
+    BlockInputStreamPtr input_;
+    std::shared_ptr<Join> join_;
+};
+
+} // namespace tfa
