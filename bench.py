@@ -41,6 +41,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--value-int64", action="store_true", help="Int64 value column instead of Float64")
     ap.add_argument("--bucket-bits", type=int, default=0, help="aggregation radix buckets (0 = from --groups)")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL, production) or gloo (rehearsal: all ranks may share one GPU)")
     return ap.parse_args()
 
 
@@ -131,14 +133,20 @@ def main():
     import torch.distributed as dist
 
     import tiflash_amd as tfa
+    from tiflash_amd.exchange import exchange_partitions
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dist_backend == "gloo":
+        local = local % max(torch.cuda.device_count(), 1)  # rehearsal: ranks may share a GPU
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
 
     N, G = args.rows, args.groups
     gen = torch.Generator(device=dev)
@@ -166,16 +174,7 @@ def main():
             return res
         # ExchangeSender: hash-repartition partial rows by key, RCCL all-to-all, final merge
         cols, offs = tfa.hash_partition(ctx, [res["keys"], res["states"][0], res["states"][1]], [0], world)
-        send = torch.tensor([offs[i + 1] - offs[i] for i in range(world)], dtype=torch.int64, device=dev)
-        recv = torch.empty_like(send)
-        dist.all_to_all_single(recv, send)
-        rs = recv.tolist()
-        ss = send.tolist()
-        outs = []
-        for c in cols:
-            o = torch.empty((sum(rs),) + tuple(c.shape[1:]), dtype=c.dtype, device=dev)
-            dist.all_to_all_single(o, c, rs, ss)
-            outs.append(o)
+        outs = exchange_partitions(cols, offs)
         final.reset()
         final.consume_partial(outs[0], [outs[1], outs[2]])
         return final.result()
@@ -197,10 +196,16 @@ def main():
     el = time.perf_counter() - t0
     prof = ctx.profile_read()
     ctx.profile(False)
+    # invariant of the last step's result: every kept row is counted exactly once over all ranks
+    red_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
+    inv = torch.tensor([float(res["states"][1].view(torch.int64).sum().item()), float(n_kept),
+                        float(res["keys"].shape[0])], dtype=torch.float64, device=red_dev)
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        t = torch.tensor([el], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = t.item()
+        dist.all_reduce(inv)
+    count_total, kept_total, groups_total = (int(x) for x in inv.tolist())
     groups = agg.size() if world == 1 else final.size()
     ms = el / args.steps * 1e3
     value = N * world * args.steps / el
@@ -214,6 +219,8 @@ def main():
         "config": {"workload": "configs[1] filter + GROUP BY 1M keys" + (" two-phase + RCCL all-to-all" if world > 1 else ""),
                    "rows_per_gpu": N, "groups": G, "kept_rows_per_gpu": n_kept, "groups_out": groups,
                    "parallelism": f"dp{world}"},
+        "check": {"count_total": count_total, "kept_total": kept_total, "groups_total": groups_total,
+                  "ok": count_total == kept_total and groups_total <= G},
     }
     if rank == 0:
         rf = roofline_from_profile(prof, args.steps, N, n_kept)
