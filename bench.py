@@ -101,14 +101,16 @@ def cpu_baseline(args):
     t_end = time.time() + 20.0
     while len(times) < 3 or (time.time() < t_end and len(times) < 5):
         t0 = time.perf_counter()
-        orc.bench_filter_agg(f, args.threshold, k, v, threads, 65536)
+        orc.bench_filter_agg_ref(f, args.threshold, k, v, threads, 65536)
         times.append(time.perf_counter() - t0)
         if time.time() > t_end and len(times) >= 1:
             break
     med = statistics.median(times)
     out = {"value": round(n / med, 1), "unit": "rows/s", "cores": threads, "kind": "port",
            "sample": f"{n} rows x {len(times)} runs (median), same distribution, 65536-row blocks, "
-                     f"per-thread HashMap + merge (reference-algorithm CPU restatement)"}
+                     f"per-thread key64 HashMap (CRC32-C, arena states, prefetch, two-level at 100k keys) + "
+                     f"bucket-parallel merge + result conversion (reference-algorithm CPU restatement, "
+                     f"oracle/cpu_baseline.c)"}
     return out
 
 

@@ -62,6 +62,11 @@ size_t orc_join_probe(const orc_join *j, int kind, const void *keys, const uint8
  * ParallelAggregatingBlockInputStream.cpp:77-159).  Return the number of groups / matches. */
 size_t orc_bench_filter_agg(const int64_t *f, int64_t threshold, const int64_t *k, const double *v, size_t n,
                             int nthreads, size_t block_rows, double *checksum);
+/* The C2 step with the reference's own data structures (cpu_baseline.c): per-thread key64 HashMap
+ * with arena states, prefetch, two-level conversion at 100k keys, bucket-parallel merge and
+ * result conversion.  bench.py's cpu_baseline leg. */
+size_t orc_bench_filter_agg_ref(const int64_t *f, int64_t threshold, const int64_t *k, const double *v, size_t n,
+                                int nthreads, size_t block_rows, double *checksum);
 size_t orc_bench_join(const int64_t *build_keys, size_t nb, const int64_t *probe_keys, size_t np, int nthreads,
                       uint64_t *checksum);
 

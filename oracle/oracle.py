@@ -51,6 +51,7 @@ def lib():
         L.orc_join_probe.restype = ctypes.c_size_t
         L.orc_bench_filter_agg.restype = ctypes.c_size_t
         L.orc_bench_join.restype = ctypes.c_size_t
+        L.orc_bench_filter_agg_ref.restype = ctypes.c_size_t
         _L = L
     return _L
 
@@ -228,6 +229,13 @@ def bench_filter_agg(f, threshold, k, v, nthreads, block_rows=65536):
     cs = ctypes.c_double()
     g = lib().orc_bench_filter_agg(_p(f), ctypes.c_int64(threshold), _p(k), _p(v), ctypes.c_size_t(len(k)),
                                    nthreads, ctypes.c_size_t(block_rows), ctypes.byref(cs))
+    return g, cs.value
+
+
+def bench_filter_agg_ref(f, threshold, k, v, nthreads, block_rows=65536):
+    cs = ctypes.c_double()
+    g = lib().orc_bench_filter_agg_ref(_p(f), ctypes.c_int64(threshold), _p(k), _p(v), ctypes.c_size_t(len(k)),
+                                       nthreads, ctypes.c_size_t(block_rows), ctypes.byref(cs))
     return g, cs.value
 
 

@@ -151,3 +151,21 @@ def test_bench_legs_run(orc):
     assert cs == pytest.approx(float(r["states"][0].sum() + r["states"][1].sum()))
     m, _ = orc.bench_join(np.arange(1000, dtype=np.int64), rng.integers(0, 2000, 5000, dtype=np.int64), 2)
     assert 0 < m < 5000
+
+
+@pytest.mark.parametrize("groups", [1000, 300_000])
+def test_bench_ref_leg_matches_oracle(orc, groups):
+    """cpu_baseline.c (the timed CPU leg) computes the same groups and sums as the restatement,
+    below and above the two-level threshold (100k keys), including key 0."""
+    rng = np.random.default_rng(4)
+    n = 600_000
+    f = rng.integers(0, 100, n, dtype=np.int64)
+    k = rng.integers(0, groups, n, dtype=np.int64)
+    v = rng.integers(0, 1 << 20, n).astype(np.float64) / 256
+    ref = orc.Agg(orc.INT64, [(0, orc.FLOAT64), (2, 0)])
+    ref.consume(k, [v, None], mask=(f < 96).astype(np.uint8))
+    r = ref.result()
+    for threads in (1, 3):
+        g, cs = orc.bench_filter_agg_ref(f, 96, k, v, threads, 4096)
+        assert g == ref.size()
+        assert cs == pytest.approx(float(r["states"][0].sum() + r["states"][1].sum()), rel=1e-12)
