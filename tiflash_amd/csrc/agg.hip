@@ -48,6 +48,8 @@ struct AggSpec {
     int ctrl_off;
     int lds_bytes;
     int dbg; // timing ablation knob (TFG_DBG_BUCKET), 0 in production
+    int slot_shift; // in-table group = bits [slot_shift, slot_shift + log2(cap/GS)) of key * 2^64/phi,
+                    // just below the bits that chose the bucket (one multiply instead of a mixer)
 };
 
 // Columnar row source staged by the bucket pass (bucket-major).
@@ -77,14 +79,6 @@ struct Ctrl {
     unsigned long long spill_w;
 };
 
-__device__ __forceinline__ uint64_t mix64(uint64_t x) { // splitmix64 finaliser: slot hash inside a bucket
-    x ^= x >> 30;
-    x *= 0xbf58476d1ce4e5b9ull;
-    x ^= x >> 27;
-    x *= 0x94d049bb133111ebull;
-    x ^= x >> 31;
-    return x;
-}
 
 __device__ __forceinline__ uint64_t load_bits(const void *p, int width, int64_t i) {
     switch (width) {
@@ -223,7 +217,7 @@ struct Table {
                 cell[u] = find_or_insert(key[u], is_null[u], may_insert, force);
                 continue;
             }
-            grp[u] = (unsigned)mix64(key[u]) & gmask;
+            grp[u] = (unsigned)((key[u] * 0x9E3779B97F4A7C15ull) >> S.slot_shift) & gmask;
             live[u] = true;
         }
         for (int step = 0; step <= (int)gmask; ++step) {
@@ -1132,6 +1126,11 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
     while (cap > 256 && (size_t)(cap + 2) * cell > (size_t)LDS_TABLE_BYTES) cap /= 2;
     S.cap = cap;
     S.maxfill = std::max(1, std::min(cap * 5 / 8, cap - BT - 8));
+    {
+        int gbits = 0;
+        while ((4 << gbits) < cap) ++gbits; // log2(cap / GS), GS = 4
+        S.slot_shift = 64 - (a->nokey ? 0 : bbits) - gbits;
+    }
     int off = (cap + 2) * 8;
     for (int i = 0; i < n_aggs; ++i) {
         if (S.acc[i] != ACC_NONE) {

@@ -1,6 +1,8 @@
 set -e
 mkdir -p gpurun_out
-timeout -k 10 200 python bench.py --no-cpu --no-join > gpurun_out/b1.log 2>&1 || { tail -20 gpurun_out/b1.log; exit 1; }
-tail -1 gpurun_out/b1.log | cut -c1-400
-timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --dist-backend gloo --rows 20000000 --steps 3 --warmup 1 --no-cpu --no-join > gpurun_out/b2.log 2>&1 || { tail -30 gpurun_out/b2.log; exit 1; }
-grep '^{' gpurun_out/b2.log | cut -c1-300; grep -o '"check": {[^}]*}' gpurun_out/b2.log
+timeout -k 10 300 python -m pytest tests -m gpu -x -q > gpurun_out/t.log 2>&1 || { tail -30 gpurun_out/t.log; exit 1; }
+tail -2 gpurun_out/t.log
+for cfg in "0 10" "0 11"; do set -- $cfg
+TFG_DBG_SCATTER=$1 timeout -k 10 120 python bench.py --no-cpu --no-join --bucket-bits $2 > gpurun_out/s_$1_$2.log 2>&1
+echo "dbg=$1 bb=$2 $(grep -o '"value": [0-9.]*' gpurun_out/s_$1_$2.log | head -1) $(grep -o '"kernels_ms_per_step": {[^}]*}' gpurun_out/s_$1_$2.log)"
+done
