@@ -27,7 +27,8 @@
 namespace tfg {
 
 constexpr int AGG_MAX = 4;
-constexpr int BT = 512; // bucket kernel threads (8 waves; 2-3 workgroups per CU)
+constexpr int BT = 512;      // bucket kernel threads (8 waves; 2-3 workgroups per CU)
+constexpr int BT_BIG = 1024; // for tables too large for two workgroups per CU (16 waves)
 constexpr int LDS_TABLE_BYTES = 100 * 1024;
 
 enum AccKind { ACC_NONE = 0, ACC_I64 = 1, ACC_F64 = 2, ACC_I128 = 3 };
@@ -48,6 +49,7 @@ struct AggSpec {
     int ctrl_off;
     int lds_bytes;
     int dbg; // timing ablation knob (TFG_DBG_BUCKET), 0 in production
+    int bt;         // bucket kernel workgroup size (BT or BT_BIG)
     int slot_shift; // in-table group = bits [slot_shift, slot_shift + log2(cap/GS)) of key * 2^64/phi,
                     // just below the bits that chose the bucket (one multiply instead of a mixer)
 };
@@ -493,7 +495,7 @@ template <int A0, int A1, int A2> struct FastOps {
     __device__ __forceinline__ uint64_t probe_val(const Row &v) const { return v.v[0]; }
 };
 
-template <typename Ops>
+template <typename Ops, int BT>
 __global__ void __launch_bounds__(BT) agg_bucket_kernel(AggSpec S, RowsIO rows0, RowsIO rows1, int mode,
                                                         const uint64_t *stage_off, GroupsIO old,
                                                         const uint64_t *old_off, GroupsIO out, uint64_t *out_cnt) {
@@ -817,8 +819,12 @@ template <typename Ops>
 void launch_bucket(int B, const AggSpec &S, hipStream_t st, const RowsIO &rows, const RowsIO &rows1, int mode,
                    const uint64_t *stage_off, const GroupsIO &old, const uint64_t *ooff, const GroupsIO &tmp,
                    uint64_t *new_cnt) {
-    hipLaunchKernelGGL(agg_bucket_kernel<Ops>, dim3(B), dim3(BT), S.lds_bytes, st, S, rows, rows1, mode, stage_off, old,
-                       ooff, tmp, new_cnt);
+    if (S.bt == BT_BIG)
+        hipLaunchKernelGGL((agg_bucket_kernel<Ops, BT_BIG>), dim3(B), dim3(BT_BIG), S.lds_bytes, st, S, rows, rows1, mode,
+                           stage_off, old, ooff, tmp, new_cnt);
+    else
+        hipLaunchKernelGGL((agg_bucket_kernel<Ops, BT>), dim3(B), dim3(BT), S.lds_bytes, st, S, rows, rows1, mode,
+                           stage_off, old, ooff, tmp, new_cnt);
 }
 
 // op-code signature for the FastOps specialisations (0 = generic path)
@@ -1109,12 +1115,13 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
         if (S.has_cnt[i]) cell += 8;
         (void)arg_scales;
     }
-    // buckets: about 1K expected groups per bucket (the TwoLevelHashTable analogue)
+    // buckets: about 2K expected groups per bucket (the TwoLevelHashTable analogue): fewer buckets
+    // give the radix scatter longer runs per destination; 2K-group tables run 16-wave workgroups
     const int64_t eg = (params && params->expected_groups > 0) ? params->expected_groups : (1 << 20);
     int bbits = params ? params->bucket_bits : 0;
     if (bbits <= 0) {
         bbits = 4;
-        while (bbits < 12 && ((int64_t)1 << bbits) * 1024 < eg) ++bbits;
+        while (bbits < 12 && ((int64_t)1 << bbits) * 2048 < eg) ++bbits;
     }
     if (bbits > 12) bbits = 12;
     a->B = a->nokey ? 1 : (1u << bbits);
@@ -1144,6 +1151,9 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
     }
     S.ctrl_off = off;
     S.lds_bytes = off + (int)sizeof(Ctrl) + 16;
+    // one workgroup per CU anyway (LDS): make it 16 waves, and keep the in-flight insert headroom
+    S.bt = S.lds_bytes > 80 * 1024 ? BT_BIG : BT;
+    S.maxfill = std::max(1, std::min(cap * 5 / 8, cap - S.bt - 8));
     S.dbg = getenv("TFG_DBG_BUCKET") ? atoi(getenv("TFG_DBG_BUCKET")) : 0;
     if (a->nokey) {
         if (int rc = a->ensure_state(0, 1)) {
