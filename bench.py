@@ -248,17 +248,17 @@ def main():
         del hit
         j = tfa.Join(ctx, tfa.INT64, expected_build_rows=nb)
         tb0 = time.perf_counter()
-        j.build(bk)
+        j.build(bk, payload=[bpay])
         j.finalize()
         torch.cuda.synchronize()
         build_s = time.perf_counter() - tb0
-        out_p = torch.empty(npr, dtype=torch.int32, device=dev)
-        out_b = torch.empty(npr, dtype=torch.int32, device=dev)
+        outs = ([torch.empty(npr, dtype=torch.int64, device=dev) for _ in range(2)],
+                [torch.empty(npr, dtype=torch.int64, device=dev)], torch.empty(npr, dtype=torch.uint8, device=dev))
 
         def jstep():
-            pi, bi = j.probe(pk, capacity=npr, out_probe=out_p, out_build=out_b)
-            # materialise the joined block: probe key + probe payload (replicated) + build payload
-            return tfa.gather(ctx, pi, [pk, ppay]) + tfa.gather(ctx, bi, [bpay])
+            # the joined block (probe key, probe payload, build payload), materialised by the probe
+            op, ob, _ = j.probe_rows(pk, [pk, ppay], 1, capacity=npr, outs=outs)
+            return op + ob
 
         for _ in range(args.warmup):
             jstep()

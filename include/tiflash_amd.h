@@ -294,6 +294,19 @@ int tfg_join_destroy(tfg_join *join);
 int tfg_join_probe(tfg_join *join, int kind, const void *keys, const uint8_t *key_nullmap, int64_t n,
                    uint32_t *out_probe_idx, uint32_t *out_build_idx, uint64_t capacity, uint64_t *out_count_dev,
                    uint64_t *out_count_host);
+/* Build rows that carry `npay` (1-2) payload columns of 8 bytes (the build block's columns the
+ * joined block needs).  A join is built either with tfg_join_build (index pairs) or with this
+ * call for every block (materialising probe). */
+int tfg_join_build_rows(tfg_join *join, const void *keys, const uint8_t *key_nullmap, int64_t n, int npay,
+                        const void *const *pay);
+/* Materialising probe (Join::joinBlock with Adder<KIND, All> + replicateRange, Join.cpp:1153-1358,
+ * ColumnVector.cpp:706-738): output row i carries the probe row's `npay` (1-2) payload columns of
+ * 8 bytes (out_probe[w]) and, for INNER / LEFT, the matched build row's payload columns
+ * (out_build[w]; LEFT rows without a match get 0 and out_build_null[i] = 1).  SEMI / ANTI output
+ * the probe payloads only.  Capacity handling as tfg_join_probe; row order grouped by partition. */
+int tfg_join_probe_rows(tfg_join *join, int kind, const void *keys, const uint8_t *key_nullmap, int64_t n, int npay,
+                        const void *const *probe_pay, void *const *out_probe, void *const *out_build,
+                        uint8_t *out_build_null, uint64_t capacity, uint64_t *out_count_host);
 /* Build-side statistics: rows inserted, distinct keys, partitions. */
 int tfg_join_stats(tfg_join *join, uint64_t *rows, uint64_t *partitions);
 

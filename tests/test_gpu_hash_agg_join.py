@@ -313,3 +313,98 @@ def test_join_capacity_retry(tfa, ctx, dev):
     assert e.value.code == tfa.TFG_ERR_CAPACITY
     pi, bi = j.probe(keys[:10])
     assert pi.shape[0] == 10_000
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", [0, 1, 2, 3])
+@pytest.mark.parametrize("key_as_payload", [True, False])
+@pytest.mark.parametrize("nb,np_,dup", [(0, 1000, 1), (3000, 50_000, 1), (20_000, 60_000, 30), (200_000, 300_000, 1),
+                                        (9000, 2000, 9000)])
+def test_join_probe_rows_materialised(tfa, ctx, dev, orc, kind, key_as_payload, nb, np_, dup):
+    """Materialising probe (tfg_join_probe_rows): every output row carries the probe payloads and
+    the matched build payload; compared as a multiset with the restatement's pairs."""
+    rng = np.random.default_rng(nb + np_ + kind + 17 * key_as_payload)
+    distinct = max(1, nb // dup)
+    bk = rng.integers(-distinct, distinct, nb, dtype=np.int64) if dup > 1 else rng.permutation(nb).astype(np.int64) * 4 + 1
+    bnull = (rng.random(nb) < 0.02).astype(np.uint8)
+    bpay = rng.integers(-2**62, 2**62, nb, dtype=np.int64)
+    pk = np.where(rng.random(np_) < 0.5, bk[rng.integers(0, max(nb, 1), np_)] if nb else 3,
+                  rng.integers(-2**40, 2**40, np_) * 4 + 3)
+    pk[:3] = [0, -1, 1]
+    pnull = (rng.random(np_) < 0.02).astype(np.uint8)
+    ppay = rng.integers(-2**62, 2**62, np_, dtype=np.int64)
+    j = tfa.Join(ctx, tfa.INT64, expected_build_rows=nb)
+    half = nb // 2
+    for lo, hi in ((0, half), (half, nb)):  # two build blocks
+        if hi > lo:
+            j.build(torch.from_numpy(bk[lo:hi]).to(dev), key_nullmap=torch.from_numpy(bnull[lo:hi]).to(dev),
+                    payload=[torch.from_numpy(bpay[lo:hi]).to(dev)])
+    if nb == 0:
+        j.build(torch.empty(0, dtype=torch.int64, device=dev), payload=[torch.empty(0, dtype=torch.int64, device=dev)])
+    pkd = torch.from_numpy(pk).to(dev)
+    pay = [pkd, torch.from_numpy(ppay).to(dev)] if key_as_payload else [torch.from_numpy(ppay).to(dev)]
+    op, ob, bnl = j.probe_rows(pkd, pay, 1, kind=kind, key_nullmap=torch.from_numpy(pnull).to(dev))
+    ref = orc.JoinRef(orc.INT64)
+    ref.build(bk, bnull if nb else None)
+    epi, ebi = ref.probe(pk, kind=kind, key_null=pnull)
+    want_p = ppay[epi]
+    got_p = op[-1].cpu().numpy()
+    if kind in (2, 3):
+        assert len(ob) == 0
+        assert sorted(got_p.tolist()) == sorted(want_p.tolist())
+        if key_as_payload:
+            assert sorted(op[0].cpu().numpy().tolist()) == sorted(pk[epi].tolist())
+        return
+    unmatched = ebi == 0xFFFFFFFF
+    bp = np.append(bpay, 0)
+    want_b = bp[np.where(unmatched, len(bpay), ebi)]
+    got_b = ob[0].cpu().numpy()
+    want = sorted(zip(want_p.tolist(), want_b.tolist(), unmatched.astype(int).tolist()))
+    gotn = bnl.cpu().numpy().astype(int) if kind == 1 else np.zeros(len(got_p), dtype=int)
+    got = sorted(zip(got_p.tolist(), got_b.tolist(), gotn.tolist()))
+    assert got == want
+    if key_as_payload:
+        assert sorted(op[0].cpu().numpy().tolist()) == sorted(pk[epi].tolist())
+
+
+@pytest.mark.parametrize("with_payload", [True, False])
+def test_join_two_pass_partitions(tfa, ctx, dev, orc, with_payload):
+    """Build sides above 1024 x 2560 rows partition in two radix passes (P = 4096): pairs and
+    payloads must match the restatement."""
+    rng = np.random.default_rng(55)
+    nb, np_ = 5_500_000, 400_000
+    bk = rng.permutation(nb).astype(np.int64) * 4 + 1
+    pk = np.where(rng.random(np_) < 0.5, bk[rng.integers(0, nb, np_)], rng.integers(0, 2**40, np_) * 4 + 3)
+    j = tfa.Join(ctx, tfa.INT64, expected_build_rows=nb)
+    bkd, pkd = torch.from_numpy(bk).to(dev), torch.from_numpy(pk).to(dev)
+    ref = orc.JoinRef(orc.INT64)
+    ref.build(bk)
+    epi, ebi = ref.probe(pk)
+    if with_payload:
+        j.build(bkd, payload=[bkd * 7])
+        op, ob, _ = j.probe_rows(pkd, [pkd], 1)
+        assert j.stats()[1] == 4096
+        got = sorted(zip(op[0].cpu().tolist(), ob[0].cpu().tolist()))
+        assert got == sorted(zip(pk[epi].tolist(), (bk[ebi] * 7).tolist()))
+    else:
+        j.build(bkd)
+        pi, bi = j.probe(pkd)
+        assert _pairs(pi.cpu().numpy().view(np.uint32), bi.cpu().numpy().view(np.uint32)) == _pairs(epi, ebi)
+
+
+def test_groupby_two_pass_buckets(tfa, ctx, dev, orc):
+    """4096 aggregation buckets (two-pass radix partition) vs the restatement."""
+    rng = np.random.default_rng(56)
+    n = 3_000_000
+    k = rng.integers(0, 8_000_000, n, dtype=np.int64)
+    v = rng.integers(-1000, 1000, n, dtype=np.int64)
+    g = tfa.Aggregator(ctx, tfa.INT64, [(tfa.AGG_SUM, tfa.INT64), (tfa.AGG_COUNT_ALL, 0)], expected_groups=8_000_000)
+    g.consume(torch.from_numpy(k).to(dev), [torch.from_numpy(v).to(dev), None])
+    r = g.result()
+    ref = orc.Agg(orc.INT64, [(0, orc.INT64), (2, 0)])
+    ref.consume(k, [v, None])
+    rr = ref.result()
+    got = sorted(zip(r["keys"].cpu().numpy().view(np.int64).tolist(), r["states"][0].cpu().tolist(),
+                     r["states"][1].cpu().tolist()))
+    want = sorted(zip(rr["keys"].view(np.int64).tolist(), rr["states"][0].tolist(), rr["states"][1].tolist()))
+    assert got == want

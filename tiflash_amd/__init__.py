@@ -455,8 +455,13 @@ class Join:
         self.h = h
         ctx._children.add(self)
 
-    def build(self, keys, key_nullmap=None):
-        check(lib().tfg_join_build(self.h, _p(keys), _p(key_nullmap), ctypes.c_int64(keys.shape[0])))
+    def build(self, keys, key_nullmap=None, payload: Optional[Sequence] = None):
+        """payload: 1-2 8-byte columns carried with the build rows (materialising probe_rows)."""
+        if payload:
+            check(lib().tfg_join_build_rows(self.h, _p(keys), _p(key_nullmap), ctypes.c_int64(keys.shape[0]),
+                                            len(payload), _ptr_array(payload)))
+        else:
+            check(lib().tfg_join_build(self.h, _p(keys), _p(key_nullmap), ctypes.c_int64(keys.shape[0])))
 
     def finalize(self):
         check(lib().tfg_join_finalize(self.h))
@@ -478,6 +483,35 @@ class Join:
                 continue
             check(rc)
             return pi[:cnt.value], bi[:cnt.value]
+
+    def probe_rows(self, keys, payload: Sequence, build_words: int, kind: int = JOIN_INNER, key_nullmap=None,
+                   capacity: Optional[int] = None, outs=None):
+        """Materialising probe -> (probe payload columns, build payload columns, build_null).
+        Columns are 8-byte tensors of the payload dtypes; build_null (LEFT) marks unmatched rows."""
+        import torch
+        n = keys.shape[0]
+        cap = capacity if capacity is not None else max(n, 1)
+        pairs = kind in (JOIN_INNER, JOIN_LEFT)
+        while True:
+            if outs is not None:
+                op, ob, bnull = outs
+            else:
+                op = [torch.empty(max(cap, 1), dtype=c.dtype, device=keys.device) for c in payload]
+                ob = [torch.empty(max(cap, 1), dtype=torch.int64, device=keys.device)
+                      for _ in range(build_words if pairs else 0)]
+                bnull = torch.empty(max(cap, 1), dtype=torch.uint8, device=keys.device)
+            cnt = ctypes.c_uint64()
+            rc = lib().tfg_join_probe_rows(self.h, kind, _p(keys), _p(key_nullmap), ctypes.c_int64(n), len(payload),
+                                           _ptr_array(payload), _ptr_array(op),
+                                           _ptr_array(ob) if ob else ctypes.c_void_p(0),
+                                           _p(bnull) if kind == JOIN_LEFT else ctypes.c_void_p(0),
+                                           ctypes.c_uint64(cap), ctypes.byref(cnt))
+            if rc == TFG_ERR_CAPACITY and outs is None:
+                cap = cnt.value
+                continue
+            check(rc)
+            m = cnt.value
+            return [o[:m] for o in op], [o[:m] for o in ob], bnull[:m]
 
     def stats(self):
         r, p = ctypes.c_uint64(), ctypes.c_uint64()

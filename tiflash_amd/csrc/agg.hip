@@ -725,6 +725,7 @@ struct SelBucket {
     int width;
     uint32_t shift;
     static constexpr bool needs_crc = false;
+    static constexpr bool fib_radix = false;
     __device__ __forceinline__ Loaded load(int64_t r) const {
         return Loaded{load_bits(key, width, r), key_null ? (uint32_t)key_null[r] : 0u};
     }
@@ -739,6 +740,7 @@ struct SelBucket8 {
     const uint64_t *key;
     uint32_t shift;
     static constexpr bool needs_crc = false;
+    static constexpr bool fib_radix = true;
     __device__ __forceinline__ Loaded load(int64_t r) const { return Loaded{key[r], 0u}; }
     __device__ __forceinline__ uint32_t part(const uint32_t (*)[256], const Loaded &l, int64_t) const {
         return fib_part(l.bits, shift);
@@ -879,7 +881,8 @@ int consume_keyed(tfg_agg *a, int mode, const RowPred &pred, const void *keys, i
     const size_t tmp_groups = n_old + (size_t)n;
     const size_t o_tmpg = cv.take<uint8_t>(a->carve_groups(nullptr, tmp_groups, a->st[0]) + 256);
     PartLayout L = make_layout(n, B);
-    const size_t o_part = cv.take<uint8_t>(std::max(part_tmp_bytes(L), scan_tmp_bytes(B + 1)));
+    const size_t o_part =
+        cv.take<uint8_t>(std::max(part_tmp_bytes(L, fast ? (size_t)rec_words * 8 : 0, false), scan_tmp_bytes(B + 1)));
     void *sp;
     if (int rc = scratch_get(ctx, cv.off, &sp)) return rc;
     char *sb = (char *)sp;
@@ -912,6 +915,7 @@ int consume_keyed(tfg_agg *a, int mode, const RowPred &pred, const void *keys, i
         pc.ncols = 1;
         pc.key0 = 1;
         pc.aos = 1;
+        pc.two_pass = 1;
         for (int i = 0, c = fast; i < S.n_aggs; ++i) {
             const int op = (i == 0 ? c / 100 : i == 1 ? c / 10 : c) % 10;
             if (op < 2) continue;

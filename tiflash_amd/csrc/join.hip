@@ -3,19 +3,24 @@
 // Reference: Join::insertFromBlock -> JoinPartition::insertBlockIntoMaps -> insertBlockIntoMapsTypeCase
 // (Interpreters/Join.cpp:532-735, JoinPartition.cpp:584-728; MapsAll = HashMap<UInt64, RowRefList,
 // HashCRC32>, JoinHashMap.h:175-188) and Join::joinBlock -> probeBlockImplTypeCase + Adder<KIND, All>
-// (Join.cpp:1153-1358, 1977; JoinPartition.cpp:1290-1378, 1465-1644).
+// (Join.cpp:1153-1358, 1977; JoinPartition.cpp:1290-1378, 1465-1644), replicateRange
+// (Columns/ColumnVector.cpp:706-738).
 //
-// GPU design (radix-partitioned, LDS-bucketed open addressing):
-//   finalize: the build keys are partitioned into P = 2^k partitions by the Fibonacci radix of
-//             the key bits (fib_part; internal, so not the CRC), P sized so a partition fits the
-//             LDS table;
-//   probe:    probe keys are partitioned by the same function, then one workgroup per partition
-//             loads the build partition into an LDS open-addressing table (u64 keys, 64-bit CAS,
-//             per-key chains of build rows = RowRefList), streams the probe partition, and emits
-//             (probe row, build row) pairs through an LDS output buffer flushed with one global
-//             atomic per 2K pairs.  Build partitions larger than one LDS chunk (duplicate-heavy
-//             keys) are processed chunk by chunk with a per-probe-row "found" flag, so LEFT / SEMI /
-//             ANTI stay exact.  Rows with a NULL key never match (not inserted / not probed).
+// GPU design (radix-partitioned, LDS-bucketed open addressing, materialising):
+//   finalize: build rows (key widened to u64, up to 2 payload words) are radix-partitioned by the
+//             Fibonacci radix of the key into P <= 4096 partitions of ~2.5K rows with the
+//             LDS-staged scatter, as interleaved records {key, payload...};
+//   probe:    probe rows are partitioned the same way (records {key, payload...}); one workgroup
+//             per partition loads the build partition into an LDS table (u64 keys, grouped
+//             probing of 4 cells per 32-byte read, 64-bit CAS; per key a chain of build rows and
+//             its length), streams the probe records, and emits matches through an LDS buffer of
+//             (probe record, build row) pairs flushed with one global atomic per flush.  The flush
+//             materialises the output rows itself — probe payload words from the probe record,
+//             build payload words from the build record — so the joined block needs no gathers.
+//             The index-pair API (tfg_join_probe) is the same kernel with row ids as the payload.
+//   Build partitions larger than one LDS chunk (duplicate-heavy keys) are processed chunk by
+//   chunk with a per-probe-row found flag so LEFT / SEMI / ANTI stay exact.  Rows with a NULL key
+//   never match (not inserted / not probed); LEFT and ANTI emit them as unmatched rows.
 #include <algorithm>
 
 #include "common.h"
@@ -23,19 +28,13 @@
 
 namespace tfg {
 
-constexpr int JT = 512;
-constexpr int JCAP = 4096;   // LDS table cells
-constexpr int JCHUNK = 2048; // build rows per LDS pass
-constexpr int JBUF = 2048;   // buffered output pairs
-
-__device__ __forceinline__ uint64_t jmix(uint64_t x) {
-    x ^= x >> 33;
-    x *= 0xff51afd7ed558ccdull;
-    x ^= x >> 33;
-    x *= 0xc4ceb9fe1a85ec53ull;
-    x ^= x >> 33;
-    return x;
-}
+constexpr int JT = 512;      // probe workgroup
+constexpr int JCAP = 4096;   // LDS table cells (power of two)
+constexpr int JGS = 4;       // cells per probe group (one 32-byte read)
+constexpr int JCHUNK = 4096; // build rows per LDS pass (row index fits 16 bits)
+constexpr int JBUF = 1024;   // buffered output pairs
+constexpr int JFILL = 2560;  // target build rows per partition (table load ~0.63)
+constexpr int JMAXW = 2;     // payload words per side
 
 __device__ __forceinline__ uint64_t jload_bits(const void *p, int width, int64_t i) {
     switch (width) {
@@ -46,12 +45,14 @@ __device__ __forceinline__ uint64_t jload_bits(const void *p, int width, int64_t
     }
 }
 
+// partition of a key: the Fibonacci radix (internal; NULL keys are dropped)
 struct SelJoin {
     const void *key;
     const uint8_t *key_null;
     int width;
     uint32_t shift;
     static constexpr bool needs_crc = false;
+    static constexpr bool fib_radix = true;
     __device__ __forceinline__ Loaded load(int64_t r) const {
         return Loaded{jload_bits(key, width, r), key_null ? (uint32_t)key_null[r] : 0u};
     }
@@ -61,60 +62,52 @@ struct SelJoin {
     __device__ __forceinline__ uint32_t operator()(const uint32_t (*t)[256], int64_t r) const { return part(t, load(r), r); }
 };
 
+// in-partition group of a key: the product bits below the partition radix
+__device__ __forceinline__ unsigned join_group(uint64_t key, int slot_shift) {
+    return (unsigned)((key * 0x9E3779B97F4A7C15ull) >> slot_shift) & (JCAP / JGS - 1);
+}
+
 struct JoinArgs {
-    const uint64_t *bkeys;   // build keys (u64 bits), partition-major
-    const uint32_t *brows;   // build row ids
-    const uint64_t *boff;    // P+1
-    const void *pkeys;       // probe keys (raw width), partition-major
-    const uint32_t *prows;   // probe row ids
-    const uint64_t *poff;    // P+1
-    int pwidth;
+    const uint64_t *brec;  // build records (key + bw words), partition-major
+    const uint32_t *brows; // build row ids (partition-major)
+    const uint64_t *boff;  // P+1
+    int bw;                // build payload words in a record
+    const uint64_t *prec;  // probe records (key + payload words), partition-major
+    const uint32_t *prows; // probe row ids (null when pw > 0)
+    const uint64_t *poff;  // P+1
+    int pw;                // probe payload words output
+    int prw;               // probe record words
+    int pw0;               // record word of payload 0 (0 when payload 0 is the key column itself)
     int kind;
-    uint8_t *found;          // per staged probe row (multi-chunk partitions), zeroed
-    uint32_t *out_probe;
-    uint32_t *out_build;
+    int slot_shift;
+    uint8_t *found; // per staged probe row (multi-chunk partitions), zeroed
+    // outputs: out_p[w] (pw > 0: u64 payload words; pw == 0: u32 probe row ids in out_p[0]),
+    // out_b[w] likewise for the build side; out_bnull: 1 for LEFT rows without a match
+    void *out_p[JMAXW];
+    void *out_b[JMAXW];
+    uint8_t *out_bnull;
     uint64_t capacity;
     unsigned long long *cursor;
 };
 
 struct JLds {
     uint64_t keys[JCAP];
-    uint32_t head[JCAP];
-    uint32_t next[JCHUNK];
-    uint32_t brow[JCHUNK];
-    uint32_t buf_p[JBUF];
-    uint32_t buf_b[JBUF];
-    uint32_t red[JT / 64];
+    uint32_t head[JCAP + 1]; // [JCAP] = chain of key 0 (ZeroValueStorage)
+    uint32_t cnt[JCAP + 1];
+    uint16_t next[JCHUNK];
+    uint32_t buf_p[JBUF]; // staged probe position
+    uint32_t buf_b[JBUF]; // build row within the chunk, 0xFFFFFFFF = none
+    uint32_t red[JT / 64 + 2];
     unsigned buf_n;
     unsigned long long base;
 };
-
-__device__ __forceinline__ void emit_pair(const JoinArgs &A, uint64_t pos, uint32_t p, uint32_t b) {
-    if (pos < A.capacity) {
-        A.out_probe[pos] = p;
-        if (A.out_build) A.out_build[pos] = b;
-    }
-}
-
-__device__ void flush_buf(const JoinArgs &A, JLds &L) {
-    // caller: all threads, after a barrier
-    const unsigned n = L.buf_n;
-    if (n == 0) return;
-    if (threadIdx.x == 0) L.base = atomicAdd(A.cursor, (unsigned long long)n);
-    __syncthreads();
-    const uint64_t base = L.base;
-    for (unsigned i = threadIdx.x; i < n; i += JT) emit_pair(A, base + i, L.buf_p[i], L.buf_b[i]);
-    __syncthreads();
-    if (threadIdx.x == 0) L.buf_n = 0;
-    __syncthreads();
-}
 
 __device__ __forceinline__ uint32_t jblock_scan(uint32_t v, uint32_t *red, uint32_t &total) {
     const unsigned lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t x = v;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-        uint32_t y = __shfl_up(x, d, 64);
+        const uint32_t y = __shfl_up(x, d, 64);
         if (lane >= (unsigned)d) x += y;
     }
     if (lane == 63) red[wave] = x;
@@ -131,6 +124,70 @@ __device__ __forceinline__ uint32_t jblock_scan(uint32_t v, uint32_t *red, uint3
     return off + x - v;
 }
 
+// writes buffered pairs as output rows (all threads; caller synchronised)
+__device__ void flush_pairs(const JoinArgs &A, JLds &L, int64_t ps, int64_t chunk_row0) {
+    const unsigned n = L.buf_n;
+    if (n == 0) return;
+    if (threadIdx.x == 0) L.base = atomicAdd(A.cursor, (unsigned long long)n);
+    __syncthreads();
+    const uint64_t base = L.base;
+    for (unsigned i = threadIdx.x; i < n; i += JT) {
+        const uint64_t pos = base + i;
+        if (pos >= A.capacity) continue;
+        const uint32_t p = L.buf_p[i], b = L.buf_b[i];
+        if (A.pw == 0) {
+            ((uint32_t *)A.out_p[0])[pos] = A.prows[ps + p];
+        } else {
+            const uint64_t *rec = A.prec + (ps + p) * A.prw;
+            for (int w = 0; w < A.pw; ++w) ((uint64_t *)A.out_p[w])[pos] = rec[A.pw0 + w];
+        }
+        if (A.out_bnull) A.out_bnull[pos] = b == 0xFFFFFFFFu;
+        if (A.bw == 0) {
+            if (A.out_b[0]) ((uint32_t *)A.out_b[0])[pos] = b == 0xFFFFFFFFu ? 0xFFFFFFFFu : A.brows[chunk_row0 + b];
+        } else if (A.out_b[0]) {
+            const uint64_t *rec = A.brec + (chunk_row0 + (b == 0xFFFFFFFFu ? 0 : b)) * (1 + A.bw);
+            for (int w = 0; w < A.bw; ++w) ((uint64_t *)A.out_b[w])[pos] = b == 0xFFFFFFFFu ? 0ull : rec[1 + w];
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) L.buf_n = 0;
+    __syncthreads();
+}
+
+__device__ __forceinline__ int jfind(const JLds &L, uint64_t key, int slot_shift) {
+    if (key == 0) return JCAP;
+    unsigned g = join_group(key, slot_shift);
+    for (int step = 0; step < JCAP / JGS; ++step) {
+        const uint4 a = *reinterpret_cast<const uint4 *>(&L.keys[g * JGS]);
+        const uint4 c = *reinterpret_cast<const uint4 *>(&L.keys[g * JGS + 2]);
+        const uint64_t k[JGS] = {((uint64_t)a.y << 32) | a.x, ((uint64_t)a.w << 32) | a.z, ((uint64_t)c.y << 32) | c.x,
+                                 ((uint64_t)c.w << 32) | c.z};
+#pragma unroll
+        for (int s = 0; s < JGS; ++s) {
+            if (k[s] == key) return (int)(g * JGS + s);
+            if (k[s] == 0) return -1;
+        }
+        g = (g + 1) & (JCAP / JGS - 1);
+    }
+    return -1;
+}
+
+__device__ __forceinline__ int jinsert(JLds &L, uint64_t key, int slot_shift) {
+    if (key == 0) return JCAP;
+    unsigned g = join_group(key, slot_shift);
+    for (;;) {
+        for (int s = 0; s < JGS; ++s) {
+            const int cell = (int)(g * JGS + s);
+            const uint64_t cur = L.keys[cell];
+            if (cur == key) return cell;
+            if (cur != 0) continue;
+            const uint64_t old = atomicCAS((unsigned long long *)&L.keys[cell], 0ull, (unsigned long long)key);
+            if (old == 0 || old == key) return cell;
+        }
+        g = (g + 1) & (JCAP / JGS - 1);
+    }
+}
+
 __global__ void __launch_bounds__(JT) join_probe_kernel(JoinArgs A) {
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
     JLds &L = *reinterpret_cast<JLds *>(lds_raw);
@@ -140,29 +197,23 @@ __global__ void __launch_bounds__(JT) join_probe_kernel(JoinArgs A) {
     if (pe == ps) return; // no probe rows in this partition
     const int64_t nb = be - bs;
     const int chunks = nb == 0 ? 1 : (int)((nb + JCHUNK - 1) / JCHUNK);
+    const int brw = 1 + A.bw, prw = A.prw;
     if (threadIdx.x == 0) L.buf_n = 0;
     for (int c = 0; c < chunks; ++c) {
-        for (int i = threadIdx.x; i < JCAP; i += JT) {
-            L.keys[i] = 0;
+        for (int i = threadIdx.x; i < JCAP + 1; i += JT) {
+            if (i < JCAP) L.keys[i] = 0;
             L.head[i] = 0xFFFFFFFFu;
+            L.cnt[i] = 0;
         }
         __syncthreads();
-        // ---- build the LDS table from this chunk (key 0 lives in cell JCAP-1's twin: use a sentinel
-        // remap — key 0 is stored as ~0 with an exact-compare guard below)
+        // ---- build the LDS table from this chunk: per key a chain (RowRefList) and its length
         const int64_t c0 = bs + (int64_t)c * JCHUNK;
         const int cn = (int)std::min<int64_t>(JCHUNK, be - c0);
-        for (int j = threadIdx.x; j < cn; j += JT) {
-            const uint64_t key = A.bkeys[c0 + j];
-            L.brow[j] = A.brows[c0 + j];
-            const uint64_t tag = key == 0 ? 0xFFFFFFFFFFFFFFFFull : key; // 0 is the empty marker
-            unsigned pos = (unsigned)jmix(key) & (JCAP - 1);
-            for (;;) {
-                const uint64_t old = atomicCAS((unsigned long long *)&L.keys[pos], 0ull, (unsigned long long)tag);
-                if (old == 0 || old == tag) break;
-                pos = (pos + 1) & (JCAP - 1);
-            }
-            // keys ~0 (real) and 0 (remapped) share a tag: keep them apart by the exact key in bkeys
-            L.next[j] = atomicExch(&L.head[pos], (uint32_t)j);
+        for (int jr = threadIdx.x; jr < cn; jr += JT) {
+            const uint64_t key = A.brec[(c0 + jr) * brw];
+            const int cell = jinsert(L, key, A.slot_shift);
+            L.next[jr] = (uint16_t)atomicExch(&L.head[cell], (uint32_t)jr);
+            atomicAdd(&L.cnt[cell], 1u);
         }
         __syncthreads();
         const bool last = c == chunks - 1;
@@ -170,25 +221,15 @@ __global__ void __launch_bounds__(JT) join_probe_kernel(JoinArgs A) {
         for (int64_t step = ps; step < pe; step += JT) {
             const int64_t r = step + threadIdx.x;
             const bool valid = r < pe;
-            uint64_t key = 0;
-            uint32_t prow = 0;
             unsigned head = 0xFFFFFFFFu;
             uint32_t cnt = 0;
             if (valid) {
-                key = jload_bits(A.pkeys, A.pwidth, r);
-                prow = A.prows[r];
-                const uint64_t tag = key == 0 ? 0xFFFFFFFFFFFFFFFFull : key;
-                unsigned pos = (unsigned)jmix(key) & (JCAP - 1);
-                for (;;) {
-                    const uint64_t k = L.keys[pos];
-                    if (k == tag) {
-                        head = L.head[pos];
-                        break;
-                    }
-                    if (k == 0) break;
-                    pos = (pos + 1) & (JCAP - 1);
+                const uint64_t key = A.prec[r * prw];
+                const int cell = jfind(L, key, A.slot_shift);
+                if (cell >= 0) {
+                    head = L.head[cell];
+                    cnt = L.cnt[cell];
                 }
-                for (unsigned j = head; j != 0xFFFFFFFFu; j = L.next[j]) cnt += (key + 1 > 1) || A.bkeys[c0 + j] == key; // exact check only for the shared tag of keys 0 and ~0
             }
             bool prev_found = false;
             if (valid && chunks > 1) {
@@ -204,58 +245,68 @@ __global__ void __launch_bounds__(JT) join_probe_kernel(JoinArgs A) {
                 default: e = (last && !cnt && !prev_found) ? 1 : 0; break;
                 }
             }
+            const bool pairs = A.kind <= TFG_JOIN_LEFT; // SEMI / ANTI emit the probe row alone
             uint32_t total;
             const uint32_t off = jblock_scan(e, L.red, total);
             if (total == 0) continue;
-            if (L.buf_n + total > (unsigned)JBUF) flush_buf(A, L);
+            if (L.buf_n + total > (unsigned)JBUF) flush_pairs(A, L, ps, c0);
             if (total > (unsigned)JBUF) {
-                // too many pairs for the buffer: reserve and write straight to HBM
-                if (threadIdx.x == 0) L.base = atomicAdd(A.cursor, (unsigned long long)total);
-                __syncthreads();
-                uint64_t pos = L.base + off;
-                if (A.kind == TFG_JOIN_INNER || A.kind == TFG_JOIN_LEFT) {
-                    for (unsigned j = head; j != 0xFFFFFFFFu; j = L.next[j])
-                        if ((key + 1 > 1) || A.bkeys[c0 + j] == key) emit_pair(A, pos++, prow, L.brow[j]);
-                    if (e > cnt) emit_pair(A, pos, prow, 0xFFFFFFFFu);
-                } else if (e) {
-                    emit_pair(A, pos, prow, 0xFFFFFFFFu);
+                // more pairs in this step than the buffer holds: emit it in buffer-sized rounds
+                for (uint32_t lo = 0; lo < total; lo += JBUF) {
+                    const uint32_t hi = std::min<uint32_t>(total, lo + JBUF);
+                    if (e && off + e > lo && off < hi) {
+                        unsigned jb = head;
+                        for (uint32_t q = 0; q < e; ++q) {
+                            const uint32_t slot = off + q;
+                            const bool pair = pairs && q < cnt;
+                            if (slot >= lo && slot < hi) {
+                                L.buf_p[slot - lo] = (uint32_t)(r - ps);
+                                L.buf_b[slot - lo] = pair ? jb : 0xFFFFFFFFu;
+                            }
+                            if (pair) jb = L.next[jb];
+                        }
+                    }
+                    __syncthreads();
+                    if (threadIdx.x == 0) L.buf_n = hi - lo;
+                    __syncthreads();
+                    flush_pairs(A, L, ps, c0);
                 }
-                __syncthreads();
                 continue;
             }
-            unsigned pos = L.buf_n + off;
-            if (A.kind == TFG_JOIN_INNER || A.kind == TFG_JOIN_LEFT) {
-                for (unsigned j = head; j != 0xFFFFFFFFu && cnt; j = L.next[j])
-                    if ((key + 1 > 1) || A.bkeys[c0 + j] == key) {
-                        L.buf_p[pos] = prow;
-                        L.buf_b[pos++] = L.brow[j];
-                    }
-                if (e > cnt) {
-                    L.buf_p[pos] = prow;
-                    L.buf_b[pos] = 0xFFFFFFFFu;
+            const unsigned pos0 = L.buf_n + off;
+            if (e) {
+                unsigned jb = head;
+                for (uint32_t q = 0; q < e; ++q) {
+                    const bool pair = pairs && q < cnt;
+                    L.buf_p[pos0 + q] = (uint32_t)(r - ps);
+                    L.buf_b[pos0 + q] = pair ? jb : 0xFFFFFFFFu;
+                    if (pair) jb = L.next[jb];
                 }
-            } else if (e) {
-                L.buf_p[pos] = prow;
-                L.buf_b[pos] = 0xFFFFFFFFu;
             }
             __syncthreads();
             if (threadIdx.x == 0) L.buf_n += total;
             __syncthreads();
         }
         __syncthreads();
+        flush_pairs(A, L, ps, c0); // pairs refer to this chunk's build rows
+        __syncthreads();
     }
-    flush_buf(A, L);
 }
 
 // LEFT / ANTI: probe rows with a NULL key are unmatched rows
-__global__ void join_null_rows_kernel(const uint8_t *key_null, int64_t n, uint32_t *out_probe, uint32_t *out_build,
-                                      uint64_t capacity, unsigned long long *cursor) {
+__global__ void join_null_rows_kernel(const uint8_t *key_null, int64_t n, JoinArgs A, const void *const *ppay_in,
+                                      int pw) {
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
         if (!key_null[r]) continue;
-        const uint64_t pos = atomicAdd(cursor, 1ull);
-        if (pos < capacity) {
-            out_probe[pos] = (uint32_t)r;
-            if (out_build) out_build[pos] = 0xFFFFFFFFu;
+        const uint64_t pos = atomicAdd(A.cursor, 1ull);
+        if (pos >= A.capacity) continue;
+        if (pw == 0) ((uint32_t *)A.out_p[0])[pos] = (uint32_t)r;
+        for (int w = 0; w < pw; ++w) ((uint64_t *)A.out_p[w])[pos] = ((const uint64_t *)ppay_in[w])[r];
+        if (A.out_bnull) A.out_bnull[pos] = 1;
+        if (A.bw == 0) {
+            if (A.out_b[0]) ((uint32_t *)A.out_b[0])[pos] = 0xFFFFFFFFu;
+        } else if (A.out_b[0]) {
+            for (int w = 0; w < A.bw; ++w) ((uint64_t *)A.out_b[w])[pos] = 0;
         }
     }
 }
@@ -264,7 +315,7 @@ __global__ void widen_keys_kernel(const void *in, int width, const uint8_t *key_
                                   uint8_t *out_null, int64_t row0) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         out[row0 + i] = jload_bits(in, width, i);
-        out_null[row0 + i] = key_null ? (key_null[i] != 0) : 0;
+        if (out_null) out_null[row0 + i] = key_null ? (key_null[i] != 0) : 0;
     }
 }
 
@@ -276,14 +327,17 @@ struct tfg_join {
     Ctx *ctx = nullptr;
     int key_type = 0;
     int width = 8;
-    // accumulated build keys (u64 bits) + null flags
+    // accumulated build side: keys widened to u64, null flags, payload words
     uint64_t *keys = nullptr;
     uint8_t *nulls = nullptr;
+    uint64_t *pay[JMAXW] = {};
+    int bw = -1; // payload words per build row (-1: not fixed yet)
     int64_t n_rows = 0, cap_rows = 0;
     // finalized partitioned build
     bool finalized = false;
     uint32_t P = 1;
-    uint64_t *bkeys = nullptr;
+    int slot_shift = 0;
+    uint64_t *brec = nullptr;
     uint32_t *brows = nullptr;
     uint64_t *boff = nullptr;
     int64_t n_inserted = 0;
@@ -295,30 +349,179 @@ int join_grow(tfg_join *j, int64_t need) {
     if (need <= j->cap_rows) return TFG_OK;
     int64_t nc = std::max<int64_t>(need, j->cap_rows * 2);
     nc = std::max<int64_t>(nc, 1 << 16);
+    const int words = std::max(j->bw, 0);
     uint64_t *k;
     uint8_t *z;
+    uint64_t *p[JMAXW] = {};
     TFG_HIP(hipMalloc(&k, nc * 8));
     TFG_HIP(hipMalloc(&z, nc));
+    for (int w = 0; w < words; ++w) TFG_HIP(hipMalloc(&p[w], nc * 8));
     if (j->n_rows) {
         TFG_HIP(hipMemcpyAsync(k, j->keys, j->n_rows * 8, hipMemcpyDeviceToDevice, j->ctx->stream));
         TFG_HIP(hipMemcpyAsync(z, j->nulls, j->n_rows, hipMemcpyDeviceToDevice, j->ctx->stream));
+        for (int w = 0; w < words; ++w)
+            TFG_HIP(hipMemcpyAsync(p[w], j->pay[w], j->n_rows * 8, hipMemcpyDeviceToDevice, j->ctx->stream));
     }
     TFG_HIP(hipStreamSynchronize(j->ctx->stream));
     if (j->keys) TFG_HIP(hipFree(j->keys));
     if (j->nulls) TFG_HIP(hipFree(j->nulls));
+    for (int w = 0; w < JMAXW; ++w)
+        if (j->pay[w]) TFG_HIP(hipFree(j->pay[w]));
     j->keys = k;
     j->nulls = z;
+    for (int w = 0; w < JMAXW; ++w) j->pay[w] = p[w];
     j->cap_rows = nc;
     return TFG_OK;
 }
 
 void free_build(tfg_join *j) {
-    if (j->bkeys) (void)hipFree(j->bkeys);
+    if (j->brec) (void)hipFree(j->brec);
     if (j->brows) (void)hipFree(j->brows);
     if (j->boff) (void)hipFree(j->boff);
-    j->bkeys = nullptr;
+    j->brec = nullptr;
     j->brows = nullptr;
     j->boff = nullptr;
+}
+
+uint32_t bits_of(uint32_t P) {
+    uint32_t b = 0;
+    while ((1u << b) < P) ++b;
+    return b;
+}
+
+int build_rows(tfg_join *j, const void *keys, const uint8_t *key_nullmap, int64_t n, int npay, const void *const *pay) {
+    TFG_CHECK(j && (n == 0 || keys), TFG_ERR_INVALID_ARG, "null argument");
+    TFG_CHECK(!j->finalized, TFG_ERR_LOGICAL, "build after finalize");
+    TFG_CHECK(npay >= 0 && npay <= JMAXW && (npay == 0 || pay), TFG_ERR_INVALID_ARG, "build payload words %d", npay);
+    TFG_CHECK(j->bw < 0 || j->bw == npay, TFG_ERR_LOGICAL, "every build block must carry the same payload columns");
+    TFG_CHECK(n >= 0 && j->n_rows + n < (int64_t)0xFFFFFFFFll, TFG_ERR_INVALID_ARG, "build row count out of range");
+    if (failpoint("join_build")) return fail(TFG_ERR_FAULT_INJECTED, "failpoint join_build");
+    if (int rc = set_device(j->ctx)) return rc;
+    if (j->bw < 0) {
+        j->bw = npay;
+        if (npay && j->cap_rows) { // capacity reserved at create: allocate the payload planes too
+            const int64_t cap = j->cap_rows;
+            if (j->keys) TFG_HIP(hipFree(j->keys));
+            if (j->nulls) TFG_HIP(hipFree(j->nulls));
+            j->keys = nullptr;
+            j->nulls = nullptr;
+            j->cap_rows = 0;
+            if (int rc = join_grow(j, cap)) return rc;
+        }
+    }
+    if (n == 0) return TFG_OK;
+    if (int rc = join_grow(j, j->n_rows + n)) return rc;
+    hipLaunchKernelGGL(widen_keys_kernel, dim3(stream_grid(n, 256, 4096)), dim3(256), 0, j->ctx->stream, keys, j->width,
+                       key_nullmap, n, j->keys, j->nulls, j->n_rows);
+    TFG_LAUNCH_CHECK();
+    for (int w = 0; w < npay; ++w)
+        TFG_HIP(hipMemcpyAsync(j->pay[w] + j->n_rows, pay[w], n * 8, hipMemcpyDeviceToDevice, j->ctx->stream));
+    j->n_rows += n;
+    return TFG_OK;
+}
+
+int probe_common(tfg_join *j, int kind, const void *keys, const uint8_t *key_nullmap, int64_t n, int npay,
+                 const void *const *ppay, void *const *out_p, void *const *out_b, uint8_t *out_bnull, uint64_t capacity,
+                 uint64_t *out_count_dev, uint64_t *out_count_host) {
+    TFG_CHECK(kind >= TFG_JOIN_INNER && kind <= TFG_JOIN_ANTI, TFG_ERR_NOT_IMPLEMENTED, "join kind %d", kind);
+    TFG_CHECK(n >= 0 && n < (int64_t)0xFFFFFFFFll, TFG_ERR_INVALID_ARG, "probe row count out of range");
+    TFG_CHECK(npay >= 0 && npay <= JMAXW && (npay == 0 || ppay), TFG_ERR_INVALID_ARG, "probe payload words %d", npay);
+    if (failpoint("join_probe")) return fail(TFG_ERR_FAULT_INJECTED, "failpoint join_probe");
+    if (!j->finalized)
+        if (int rc = tfg_join_finalize(j)) return rc;
+    if (int rc = set_device(j->ctx)) return rc;
+    Ctx *ctx = j->ctx;
+    const uint32_t P = j->P;
+    PartLayout L = make_layout(n, P);
+    // payload 0 may be the key column itself (the joined block's key): the record's key word
+    // then serves it instead of a second copy
+    const bool key_pay0 = npay >= 1 && ppay[0] == keys && j->width == 8;
+    const int prw = key_pay0 ? npay : 1 + npay;
+    Carver cv;
+    const size_t o_wide = cv.take<uint64_t>(j->width == 8 ? 0 : n);
+    const size_t o_prec = cv.take<uint64_t>(n * prw), o_pr = cv.take<uint32_t>(npay == 0 ? n : 0);
+    const size_t o_poff = cv.take<uint64_t>(P + 1), o_found = cv.take<uint8_t>(n), o_cur = cv.take<uint64_t>(1);
+    const size_t o_pin = cv.take<uint64_t>(JMAXW);
+    const size_t o_tmp = cv.take<uint8_t>(part_tmp_bytes(L, (size_t)prw * 8, npay == 0));
+    void *sp;
+    if (int rc = scratch_get(ctx, cv.off, &sp)) return rc;
+    char *sb = (char *)sp;
+    unsigned long long *cursor = (unsigned long long *)(sb + o_cur);
+    TFG_HIP(hipMemsetAsync(cursor, 0, 8, ctx->stream));
+    JoinArgs A{};
+    A.brec = j->brec;
+    A.brows = j->brows;
+    A.boff = j->boff;
+    A.bw = j->bw < 0 ? 0 : j->bw;
+    A.pw = npay;
+    A.prw = prw;
+    A.pw0 = key_pay0 ? 0 : 1;
+    A.kind = kind;
+    A.slot_shift = j->slot_shift;
+    for (int w = 0; w < JMAXW; ++w) {
+        A.out_p[w] = out_p ? out_p[w] : nullptr;
+        A.out_b[w] = out_b ? out_b[w] : nullptr;
+    }
+    A.out_bnull = out_bnull;
+    A.capacity = capacity;
+    A.cursor = cursor;
+    if (n > 0) {
+        // probe keys as u64 (narrower key types widened like the build side)
+        const void *pk = keys;
+        if (j->width != 8) {
+            hipLaunchKernelGGL(widen_keys_kernel, dim3(stream_grid(n, 256, 4096)), dim3(256), 0, ctx->stream, keys,
+                               j->width, nullptr, n, (uint64_t *)(sb + o_wide), nullptr, (int64_t)0);
+            TFG_LAUNCH_CHECK();
+            pk = sb + o_wide;
+        }
+        PCols pc{};
+        pc.ncols = prw;
+        pc.in[0] = pk;
+        pc.out[0] = sb + o_prec;
+        pc.width[0] = 8;
+        for (int w = key_pay0 ? 1 : 0; w < npay; ++w) {
+            pc.in[pc.ncols - npay + w] = ppay[w];
+            pc.width[pc.ncols - npay + w] = 8;
+        }
+        pc.key0 = 1;
+        pc.aos = prw >= 2;
+        pc.two_pass = 1;
+        SelJoin sel{pk, key_nullmap, 8, fib_shift(P)};
+        RowPred pred{};
+        uint64_t *poff = (uint64_t *)(sb + o_poff);
+        uint32_t *prows = npay == 0 ? (uint32_t *)(sb + o_pr) : nullptr;
+        if (int rc = run_partition<SelJoin, false>(ctx, sel, pred, L, pc, prows, nullptr, poff, sb + o_tmp,
+                                                   "join.part.hist", "join.part.scatter"))
+            return rc;
+        TFG_HIP(hipMemsetAsync(sb + o_found, 0, n, ctx->stream));
+        A.prec = (const uint64_t *)(sb + o_prec);
+        A.prows = prows;
+        A.poff = poff;
+        A.found = (uint8_t *)(sb + o_found);
+        {
+            ProfScope _ps(ctx, "join.probe");
+            hipLaunchKernelGGL(join_probe_kernel, dim3(P), dim3(JT), sizeof(JLds), ctx->stream, A);
+        }
+        TFG_LAUNCH_CHECK();
+        if (key_nullmap && (kind == TFG_JOIN_LEFT || kind == TFG_JOIN_ANTI)) {
+            const void **pin = nullptr;
+            if (npay) {
+                pin = (const void **)(sb + o_pin); // device array of the payload pointers
+                TFG_HIP(hipMemcpyAsync(pin, ppay, npay * sizeof(void *), hipMemcpyHostToDevice, ctx->stream));
+            }
+            hipLaunchKernelGGL(join_null_rows_kernel, dim3(stream_grid(n, 256, 4096)), dim3(256), 0, ctx->stream,
+                               key_nullmap, n, A, (const void *const *)pin, npay);
+            TFG_LAUNCH_CHECK();
+        }
+    }
+    if (out_count_dev) TFG_HIP(hipMemcpyAsync(out_count_dev, cursor, 8, hipMemcpyDeviceToDevice, ctx->stream));
+    uint64_t total = 0;
+    if (int rc = read_back_u64(ctx, (const uint64_t *)cursor, &total, 1)) return rc;
+    if (out_count_host) *out_count_host = total;
+    if (total > capacity)
+        return fail(TFG_ERR_CAPACITY, "join result needs %llu rows, capacity %llu", (unsigned long long)total,
+                    (unsigned long long)capacity);
+    return TFG_OK;
 }
 
 } // namespace
@@ -327,7 +530,7 @@ extern "C" {
 
 int tfg_join_create(tfg_ctx *ctx, int key_type, int64_t expected_build_rows, tfg_join **out) {
     TFG_CHECK(ctx && out, TFG_ERR_INVALID_ARG, "null argument");
-    TFG_CHECK(type_width(key_type) > 0 && type_width(key_type) <= 8, TFG_ERR_ILLEGAL_TYPE,
+    TFG_CHECK(type_width(key_type) > 0 && type_width(key_type) <= 8 && !is_float_type(key_type), TFG_ERR_ILLEGAL_TYPE,
               "unsupported join key type %d", key_type);
     if (int rc = set_device(ctx)) return rc;
     tfg_join *j = new tfg_join();
@@ -350,24 +553,20 @@ int tfg_join_destroy(tfg_join *j) {
     (void)hipStreamSynchronize(j->ctx->stream);
     if (j->keys) (void)hipFree(j->keys);
     if (j->nulls) (void)hipFree(j->nulls);
+    for (int w = 0; w < JMAXW; ++w)
+        if (j->pay[w]) (void)hipFree(j->pay[w]);
     free_build(j);
     delete j;
     return TFG_OK;
 }
 
 int tfg_join_build(tfg_join *j, const void *keys, const uint8_t *key_nullmap, int64_t n) {
-    TFG_CHECK(j && (n == 0 || keys), TFG_ERR_INVALID_ARG, "null argument");
-    TFG_CHECK(!j->finalized, TFG_ERR_LOGICAL, "build after finalize");
-    TFG_CHECK(n >= 0 && j->n_rows + n < (int64_t)0xFFFFFFFFll, TFG_ERR_INVALID_ARG, "build row count out of range");
-    if (failpoint("join_build")) return fail(TFG_ERR_FAULT_INJECTED, "failpoint join_build");
-    if (n == 0) return TFG_OK;
-    if (int rc = set_device(j->ctx)) return rc;
-    if (int rc = join_grow(j, j->n_rows + n)) return rc;
-    hipLaunchKernelGGL(widen_keys_kernel, dim3(stream_grid(n, 256, 4096)), dim3(256), 0, j->ctx->stream, keys, j->width,
-                       key_nullmap, n, j->keys, j->nulls, j->n_rows);
-    TFG_LAUNCH_CHECK();
-    j->n_rows += n;
-    return TFG_OK;
+    return build_rows(j, keys, key_nullmap, n, 0, nullptr);
+}
+
+int tfg_join_build_rows(tfg_join *j, const void *keys, const uint8_t *key_nullmap, int64_t n, int npay,
+                        const void *const *pay) {
+    return build_rows(j, keys, key_nullmap, n, npay, pay);
 }
 
 int tfg_join_finalize(tfg_join *j) {
@@ -375,24 +574,32 @@ int tfg_join_finalize(tfg_join *j) {
     if (j->finalized) return TFG_OK;
     if (int rc = set_device(j->ctx)) return rc;
     Ctx *ctx = j->ctx;
-    // partitions: keep the average build partition well under one LDS chunk
-    int64_t want = j->n_rows / (JCHUNK * 5 / 8);
+    if (j->bw < 0) j->bw = 0;
+    // partitions of ~JFILL build rows (table load ~0.63); the staged scatter takes P <= 4096
     uint32_t P = 1;
-    while ((int64_t)P < want && P < (uint32_t)PMAX_UNSTABLE) P <<= 1;
+    while ((int64_t)P * JFILL < j->n_rows && P < 4096u) P <<= 1;
     j->P = P;
+    j->slot_shift = 64 - (int)bits_of(P) - (int)bits_of(JCAP / JGS);
     const int64_t n = j->n_rows;
-    TFG_HIP(hipMalloc(&j->bkeys, std::max<int64_t>(n, 1) * 8));
+    const int brw = 1 + j->bw;
+    TFG_HIP(hipMalloc(&j->brec, std::max<int64_t>(n, 1) * 8 * brw));
     TFG_HIP(hipMalloc(&j->brows, std::max<int64_t>(n, 1) * 4));
     TFG_HIP(hipMalloc(&j->boff, (P + 1) * 8));
     PartLayout L = make_layout(n, P);
     void *tmp;
-    if (int rc = scratch_get(ctx, part_tmp_bytes(L), &tmp)) return rc;
+    if (int rc = scratch_get(ctx, part_tmp_bytes(L, (size_t)brw * 8, true), &tmp)) return rc;
     PCols pc{};
-    pc.ncols = 1;
+    pc.ncols = brw;
     pc.in[0] = j->keys;
-    pc.out[0] = j->bkeys;
+    pc.out[0] = j->brec;
     pc.width[0] = 8;
+    for (int w = 0; w < j->bw; ++w) {
+        pc.in[1 + w] = j->pay[w];
+        pc.width[1 + w] = 8;
+    }
     pc.key0 = 1;
+    pc.aos = brw >= 2;
+    pc.two_pass = 1;
     SelJoin sel{j->keys, j->nulls, 8, fib_shift(P)};
     RowPred pred{};
     if (int rc = run_partition<SelJoin, false>(ctx, sel, pred, L, pc, j->brows, nullptr, j->boff, tmp, "join.build.hist",
@@ -416,70 +623,32 @@ int tfg_join_probe(tfg_join *j, int kind, const void *keys, const uint8_t *key_n
                    uint32_t *out_probe_idx, uint32_t *out_build_idx, uint64_t capacity, uint64_t *out_count_dev,
                    uint64_t *out_count_host) {
     TFG_CHECK(j && (n == 0 || keys) && (capacity == 0 || out_probe_idx), TFG_ERR_INVALID_ARG, "null argument");
-    TFG_CHECK(kind >= TFG_JOIN_INNER && kind <= TFG_JOIN_ANTI, TFG_ERR_NOT_IMPLEMENTED, "join kind %d", kind);
-    TFG_CHECK(n >= 0 && n < (int64_t)0xFFFFFFFFll, TFG_ERR_INVALID_ARG, "probe row count out of range");
-    if (failpoint("join_probe")) return fail(TFG_ERR_FAULT_INJECTED, "failpoint join_probe");
+    TFG_CHECK(j->bw <= 0, TFG_ERR_LOGICAL, "index-pair probe of a join built with payload columns");
+    void *op[JMAXW] = {out_probe_idx, nullptr};
+    void *ob[JMAXW] = {out_build_idx, nullptr};
+    return probe_common(j, kind, keys, key_nullmap, n, 0, nullptr, op, ob, nullptr, capacity, out_count_dev,
+                        out_count_host);
+}
+
+int tfg_join_probe_rows(tfg_join *j, int kind, const void *keys, const uint8_t *key_nullmap, int64_t n, int npay,
+                        const void *const *probe_pay, void *const *out_probe, void *const *out_build,
+                        uint8_t *out_build_null, uint64_t capacity, uint64_t *out_count_host) {
+    TFG_CHECK(j && (n == 0 || keys) && (capacity == 0 || out_probe), TFG_ERR_INVALID_ARG, "null argument");
+    TFG_CHECK(npay >= 1 && npay <= JMAXW, TFG_ERR_INVALID_ARG, "materialising probe needs 1-%d probe payload columns",
+              JMAXW);
     if (!j->finalized)
         if (int rc = tfg_join_finalize(j)) return rc;
-    if (int rc = set_device(j->ctx)) return rc;
-    Ctx *ctx = j->ctx;
-    const uint32_t P = j->P;
-    PartLayout L = make_layout(n, P);
-    Carver cv;
-    const size_t o_pk = cv.take<uint64_t>(n), o_pr = cv.take<uint32_t>(n), o_poff = cv.take<uint64_t>(P + 1);
-    const size_t o_found = cv.take<uint8_t>(n), o_cur = cv.take<uint64_t>(1);
-    const size_t o_tmp = cv.take<uint8_t>(part_tmp_bytes(L));
-    void *sp;
-    if (int rc = scratch_get(ctx, cv.off, &sp)) return rc;
-    char *sb = (char *)sp;
-    unsigned long long *cursor = (unsigned long long *)(sb + o_cur);
-    TFG_HIP(hipMemsetAsync(cursor, 0, 8, ctx->stream));
-    if (n > 0) {
-        PCols pc{};
-        pc.ncols = 1;
-        pc.in[0] = keys;
-        pc.out[0] = sb + o_pk;
-        pc.width[0] = j->width;
-        pc.key0 = j->width == 8;
-        SelJoin sel{keys, key_nullmap, j->width, fib_shift(P)};
-        RowPred pred{};
-        uint64_t *poff = (uint64_t *)(sb + o_poff);
-        if (int rc = run_partition<SelJoin, false>(ctx, sel, pred, L, pc, (uint32_t *)(sb + o_pr), nullptr, poff, sb + o_tmp,
-                                                   "join.part.hist", "join.part.scatter"))
-            return rc;
-        TFG_HIP(hipMemsetAsync(sb + o_found, 0, n, ctx->stream));
-        JoinArgs A{};
-        A.bkeys = j->bkeys;
-        A.brows = j->brows;
-        A.boff = j->boff;
-        A.pkeys = sb + o_pk;
-        A.prows = (const uint32_t *)(sb + o_pr);
-        A.poff = poff;
-        A.pwidth = j->width;
-        A.kind = kind;
-        A.found = (uint8_t *)(sb + o_found);
-        A.out_probe = out_probe_idx;
-        A.out_build = out_build_idx;
-        A.capacity = capacity;
-        A.cursor = cursor;
-        { ProfScope _ps(ctx, "join.probe");
-        hipLaunchKernelGGL(join_probe_kernel, dim3(P), dim3(JT), sizeof(JLds), ctx->stream, A);
-        }
-        TFG_LAUNCH_CHECK();
-        if (key_nullmap && (kind == TFG_JOIN_LEFT || kind == TFG_JOIN_ANTI)) {
-            hipLaunchKernelGGL(join_null_rows_kernel, dim3(stream_grid(n, 256, 4096)), dim3(256), 0, ctx->stream,
-                               key_nullmap, n, out_probe_idx, out_build_idx, capacity, cursor);
-            TFG_LAUNCH_CHECK();
-        }
+    void *op[JMAXW] = {}, *ob[JMAXW] = {};
+    for (int w = 0; w < npay && capacity; ++w) {
+        TFG_CHECK(out_probe[w], TFG_ERR_INVALID_ARG, "null probe output column");
+        op[w] = out_probe[w];
     }
-    if (out_count_dev) TFG_HIP(hipMemcpyAsync(out_count_dev, cursor, 8, hipMemcpyDeviceToDevice, ctx->stream));
-    uint64_t total = 0;
-    if (int rc = read_back_u64(ctx, (const uint64_t *)cursor, &total, 1)) return rc;
-    if (out_count_host) *out_count_host = total;
-    if (total > capacity)
-        return fail(TFG_ERR_CAPACITY, "join result needs %llu pairs, capacity %llu", (unsigned long long)total,
-                    (unsigned long long)capacity);
-    return TFG_OK;
+    for (int w = 0; w < j->bw && kind <= TFG_JOIN_LEFT && capacity; ++w) {
+        TFG_CHECK(out_build && out_build[w], TFG_ERR_INVALID_ARG, "null build output column");
+        ob[w] = out_build[w];
+    }
+    return probe_common(j, kind, keys, key_nullmap, n, npay, probe_pay, op, ob,
+                        kind == TFG_JOIN_LEFT ? out_build_null : nullptr, capacity, nullptr, out_count_host);
 }
 
 } // extern "C"

@@ -28,6 +28,10 @@ struct PCols {
     int ncols;
     int key0; // column 0 holds the 8-byte key the selector loads (its staged copy reuses that load)
     int aos;  // all columns 8 bytes, written as interleaved records of ncols words at out[0]
+    int in_stride;            // > 1: the 8-byte input columns are words of records of this many words
+    const uint32_t *perm_in;  // staged path: perm output = perm_in[row] instead of row
+    int two_pass;             // the caller's tmp holds part_tmp_bytes(L, row_bytes, perm): large P may
+                              // run as two radix passes (64 wide, then the full radix)
 };
 
 // Key columns hashed with IColumn::updateWeakHash32 semantics.
@@ -67,6 +71,9 @@ __device__ __forceinline__ uint32_t hash_key_row(const uint32_t (*t)[256], const
 // A selector maps a row to its partition (0xFFFFFFFF drops the row).  The work is split into
 // load(r) — the global loads — and part(crc, loaded, r), so kernels can issue the loads of
 // many rows before any of them is consumed (memory-level parallelism).
+constexpr uint32_t TWO_PASS_MIN = 1024; // P above this partitions in two passes (see run_two_pass)
+constexpr uint32_t TWO_PASS_P1 = 64;
+
 // Internal radix of a key (aggregation buckets, join partitions): Fibonacci hashing, the top
 // `bits` bits of key * 2^64/phi.  These radices never leave the device (unlike the exchange
 // selector, which must reproduce fillSelector's CRC32-C routing), so a one-multiply hash
@@ -97,6 +104,7 @@ __device__ __forceinline__ uint64_t load_width(const void *p, int width, int64_t
 struct SelArray {
     const uint32_t *sel;
     static constexpr bool needs_crc = false;
+    static constexpr bool fib_radix = false;
     __device__ __forceinline__ Loaded load(int64_t r) const { return Loaded{sel[r], 0}; }
     __device__ __forceinline__ uint32_t part(const uint32_t (*)[256], const Loaded &l, int64_t) const {
         return (uint32_t)l.bits;
@@ -109,10 +117,25 @@ struct SelHashMul {
     KeyCols k;
     uint32_t parts;
     static constexpr bool needs_crc = true;
+    static constexpr bool fib_radix = false;
     __device__ __forceinline__ Loaded load(int64_t) const { return Loaded{0, 0}; }
     __device__ __forceinline__ uint32_t part(const uint32_t (*t)[256], const Loaded &, int64_t r) const {
         uint32_t h = hash_key_row(t, k, r, 0xFFFFFFFFu);
         return (uint32_t)(((uint64_t)h * parts) >> 32);
+    }
+    __device__ __forceinline__ uint32_t operator()(const uint32_t (*t)[256], int64_t r) const { return part(t, load(r), r); }
+};
+
+// second pass of a two-pass radix partition: the key is word 0 of the first pass's records
+struct SelRec8 {
+    const uint64_t *rec;
+    int stride; // record words
+    uint32_t shift;
+    static constexpr bool needs_crc = false;
+    static constexpr bool fib_radix = false; // already the second pass
+    __device__ __forceinline__ Loaded load(int64_t r) const { return Loaded{rec[r * stride], 0u}; }
+    __device__ __forceinline__ uint32_t part(const uint32_t (*)[256], const Loaded &l, int64_t) const {
+        return fib_part(l.bits, shift);
     }
     __device__ __forceinline__ uint32_t operator()(const uint32_t (*t)[256], int64_t r) const { return part(t, load(r), r); }
 };
@@ -306,9 +329,14 @@ __global__ void __launch_bounds__(PT) part_hist_kernel(Sel sel, Pred pred, PartL
 }
 
 __device__ __forceinline__ void scatter_row(const PCols &cols, int64_t r, uint64_t pos) {
+    const int64_t ri = cols.in_stride > 1 ? r * cols.in_stride : r; // 8-byte columns of records
     if (cols.aos) {
         for (int j = 0; j < cols.ncols; ++j)
-            ((uint64_t *)cols.out[0])[pos * cols.ncols + j] = ((const uint64_t *)cols.in[j])[r];
+            ((uint64_t *)cols.out[0])[pos * cols.ncols + j] = ((const uint64_t *)cols.in[j])[ri];
+        return;
+    }
+    if (cols.in_stride > 1) {
+        for (int j = 0; j < cols.ncols; ++j) ((uint64_t *)cols.out[j])[pos] = ((const uint64_t *)cols.in[j])[ri];
         return;
     }
     for (int j = 0; j < cols.ncols; ++j) {
@@ -352,7 +380,7 @@ __global__ void __launch_bounds__(PT) part_scatter_kernel(Sel sel, RowPred pred,
             const uint32_t p = sel(crc, r);
             if (p >= L.P) continue;
             const uint64_t pos = atomicAdd((unsigned long long *)&run[p], 1ull);
-            if (perm) perm[pos] = (uint32_t)r;
+            if (perm) perm[pos] = cols.perm_in ? cols.perm_in[r] : (uint32_t)r;
             if (part_out) part_out[pos] = p;
             scatter_row(cols, r, pos);
         }
@@ -391,7 +419,7 @@ __global__ void __launch_bounds__(PT) part_scatter_kernel(Sel sel, RowPred pred,
                 wcnt[wave * L.P + p] = 0;
             }
             if (valid) {
-                if (perm) perm[pos] = (uint32_t)r;
+                if (perm) perm[pos] = cols.perm_in ? cols.perm_in[r] : (uint32_t)r;
                 if (part_out) part_out[pos] = p;
                 scatter_row(cols, r, pos);
             }
@@ -410,6 +438,15 @@ inline size_t scatter_lds_bytes(uint32_t P, bool crc, bool stable) {
 inline size_t part_tmp_bytes(const PartLayout &L) {
     int64_t e = (int64_t)L.P * L.G;
     return ((size_t)e * 4 + 255) / 256 * 256 + ((size_t)(e + 1) * 8 + 255) / 256 * 256 + scan_tmp_bytes(e) + 256;
+}
+inline size_t align256(size_t b) { return (b + 255) / 256 * 256; }
+// ... plus, for callers that set PCols::two_pass, the first pass's records (row_bytes per row),
+// row ids and offsets
+inline size_t part_tmp_bytes(const PartLayout &L, size_t row_bytes, bool perm) {
+    size_t b = part_tmp_bytes(L);
+    if (L.P > TWO_PASS_MIN && row_bytes)
+        b += align256((size_t)L.n * row_bytes) + (perm ? align256((size_t)L.n * 4) : 0) + align256((TWO_PASS_P1 + 1) * 8);
+    return b;
 }
 
 __global__ void gather_part_offsets_kernel(const uint64_t *offs, PartLayout L, uint64_t *out);
@@ -449,7 +486,7 @@ inline bool make_staged_geom(uint32_t P, const PCols &cols, bool perm, bool crc,
     for (int j = 0; j < cols.ncols; ++j) row_bytes += cols.width[j];
     const size_t fixed = (size_t)P * 16 + (crc ? 8192 : 0) + 16 * (PCOLS + 2);
     const size_t budget = stage_lds_budget(); // LDS per workgroup (default: one workgroup per CU)
-    if (fixed + row_bytes * ST_T * 4 > budget) return false;
+    if (fixed + row_bytes * ST_T * 2 > budget) return false;
     int tr = (int)((budget - fixed) / row_bytes) / ST_T * ST_T;
     if (tr > ST_T * ST_MAXR) tr = ST_T * ST_MAXR;
     g.TR = tr;
@@ -463,7 +500,7 @@ inline bool make_staged_geom(uint32_t P, const PCols &cols, bool perm, bool crc,
     if (perm) off += (size_t)tr * 4;
     g.crc_off = (int)((off + 15) & ~size_t(15));
     g.red_off = g.crc_off + (crc ? 8192 : 0);
-    g.lds_bytes = g.red_off + 64;
+    g.lds_bytes = g.red_off + (ST_T / 64 + 2) * 4; // red[]: per-wave sums + the tile total
     static const int dbg = [] {
         const char *e = getenv("TFG_DBG_SCATTER");
         return e ? atoi(e) : 0;
@@ -532,13 +569,14 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
         }
         if constexpr (NC8 > 0) {
             // payload loads in flight across the LDS rank / scan phases
+            const uint32_t stride = cols.in_stride > 1 ? (uint32_t)cols.in_stride : 1u;
 #pragma unroll
             for (int c = 0; c < NC8; ++c) {
                 if (c < c0) continue;
                 const uint64_t *src = reinterpret_cast<const uint64_t *>(cols.in[c]);
 #pragma unroll
                 for (int j = 0; j < ST_MAXR; ++j)
-                    if (bq[j] != 0xFFFFFFFFu) v[c][j] = src[tb + (uint32_t)j * ST_T + threadIdx.x];
+                    if (bq[j] != 0xFFFFFFFFu) v[c][j] = src[(size_t)(tb + (uint32_t)j * ST_T + threadIdx.x) * stride];
             }
 #pragma unroll
             for (int j = 0; j < ST_MAXR; ++j)
@@ -583,7 +621,10 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
             if (bq[j] == 0xFFFFFFFFu) continue;
             sl[j] = start[bq[j] & 0xFFFFu] + (bq[j] >> 16);
             sb[sl[j]] = (uint16_t)(bq[j] & 0xFFFFu);
-            if (perm) sperm[sl[j]] = tb + (uint32_t)j * ST_T + threadIdx.x;
+            if (perm) {
+                const uint32_t row = tb + (uint32_t)j * ST_T + threadIdx.x;
+                sperm[sl[j]] = cols.perm_in ? cols.perm_in[row] : row;
+            }
         }
         if constexpr (NC8 > 0) {
 #pragma unroll
@@ -664,8 +705,59 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
 template <typename Sel, bool STABLE = true>
 int run_partition(Ctx *ctx, const Sel &sel, const RowPred &pred, const PartLayout &L0, const PCols &cols,
                   uint32_t *perm, uint32_t *part_out, uint64_t *offsets_out, void *tmp,
-                  const char *hist_name = "part.hist", const char *scatter_name = "part.scatter") {
+                  const char *hist_name = "part.hist", const char *scatter_name = "part.scatter");
+
+// Radix partition into P > TWO_PASS_MIN destinations in two passes: the staged scatter's runs
+// per destination shrink with P (a tile of ~8K rows into 4096 destinations writes ~2-row runs),
+// so pass 1 scatters into 64 radix groups (long runs), and pass 2 partitions those records by
+// the full radix — every pass-2 tile then holds rows of one or two groups, so its rows go to
+// at most ~128 destinations.  Bytes: 2x the scatter traffic, at full write efficiency.
+template <typename Sel>
+int run_two_pass(Ctx *ctx, const Sel &sel, const RowPred &pred, const PartLayout &L0, const PCols &cols,
+                 uint32_t *perm, uint64_t *offsets_out, void *tmp, const char *hist_name, const char *scatter_name) {
+    const int nc = cols.ncols;
+    char *x = (char *)tmp + part_tmp_bytes(L0);
+    uint64_t *inter = (uint64_t *)x;
+    x += align256((size_t)L0.n * nc * 8);
+    uint32_t *perm1 = nullptr;
+    if (perm) {
+        perm1 = (uint32_t *)x;
+        x += align256((size_t)L0.n * 4);
+    }
+    uint64_t *offs1 = (uint64_t *)x;
+    Sel s1 = sel;
+    s1.shift = fib_shift(TWO_PASS_P1);
+    PCols c1 = cols;
+    c1.out[0] = inter;
+    c1.two_pass = 0;
+    if (int rc = run_partition<Sel, false>(ctx, s1, pred, make_layout(L0.n, TWO_PASS_P1), c1, perm1, nullptr, offs1,
+                                           tmp, hist_name, scatter_name))
+        return rc;
+    uint64_t kept = 0;
+    if (int rc = read_back_u64(ctx, offs1 + TWO_PASS_P1, &kept, 1)) return rc;
+    SelRec8 s2{inter, nc, fib_shift(L0.P)};
+    PCols c2 = cols;
+    for (int c = 0; c < nc; ++c) c2.in[c] = inter + c;
+    c2.in_stride = nc;
+    c2.perm_in = perm1;
+    c2.key0 = 1;
+    c2.two_pass = 0;
+    RowPred all{};
+    return run_partition<SelRec8, false>(ctx, s2, all, make_layout((int64_t)kept, L0.P), c2, perm, nullptr, offsets_out,
+                                         tmp, hist_name, scatter_name);
+}
+
+template <typename Sel, bool STABLE>
+int run_partition(Ctx *ctx, const Sel &sel, const RowPred &pred, const PartLayout &L0, const PCols &cols,
+                  uint32_t *perm, uint32_t *part_out, uint64_t *offsets_out, void *tmp,
+                  const char *hist_name, const char *scatter_name) {
     TFG_CHECK(L0.P >= 1 && L0.P <= (STABLE ? PMAX : PMAX_UNSTABLE), TFG_ERR_INVALID_ARG, "partition count %u out of range", L0.P);
+    if constexpr (!STABLE && Sel::fib_radix) {
+        bool all8 = cols.ncols >= 1 && cols.ncols <= 3 && (cols.aos || cols.ncols == 1);
+        for (int c = 0; c < cols.ncols; ++c) all8 = all8 && cols.width[c] == 8;
+        if (cols.two_pass && all8 && !part_out && L0.n > 0 && L0.P > TWO_PASS_MIN)
+            return run_two_pass(ctx, sel, pred, L0, cols, perm, offsets_out, tmp, hist_name, scatter_name);
+    }
     StagedGeom sg{};
     const bool staged = !STABLE && !part_out && L0.n > 0 && make_staged_geom(L0.P, cols, perm != nullptr, Sel::needs_crc, sg);
     // the staged scatter uses fewer, longer segments (P x G <= P x L0.G: fits the caller's tmp)
