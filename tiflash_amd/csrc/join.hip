@@ -32,7 +32,8 @@ constexpr int JT = 512;      // probe workgroup
 constexpr int JCAP = 4096;   // LDS table cells (power of two)
 constexpr int JGS = 4;       // cells per probe group (one 32-byte read)
 constexpr int JCHUNK = 4096; // build rows per LDS pass (row index fits 16 bits)
-constexpr int JBUF = 1024;   // buffered output pairs
+constexpr int JBUF = 992;    // buffered output pairs (JLds stays under 80 KB: two workgroups per CU)
+constexpr int JRPT = 4;      // probe rows per thread per step
 constexpr int JFILL = 2560;  // target build rows per partition (table load ~0.63)
 constexpr int JMAXW = 2;     // payload words per side
 
@@ -101,6 +102,8 @@ struct JLds {
     unsigned buf_n;
     unsigned long long base;
 };
+
+static_assert(2 * sizeof(JLds) <= 160 * 1024, "two probe workgroups per CU");
 
 __device__ __forceinline__ uint32_t jblock_scan(uint32_t v, uint32_t *red, uint32_t &total) {
     const unsigned lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -217,48 +220,60 @@ __global__ void __launch_bounds__(JT) join_probe_kernel(JoinArgs A) {
         }
         __syncthreads();
         const bool last = c == chunks - 1;
-        // ---- stream the probe partition
-        for (int64_t step = ps; step < pe; step += JT) {
-            const int64_t r = step + threadIdx.x;
-            const bool valid = r < pe;
-            unsigned head = 0xFFFFFFFFu;
-            uint32_t cnt = 0;
-            if (valid) {
-                const uint64_t key = A.prec[r * prw];
-                const int cell = jfind(L, key, A.slot_shift);
+        // ---- stream the probe partition, JRPT rows per thread per step (their record loads in
+        // flight together; one block scan and one barrier pair per JT * JRPT rows)
+        const bool pairs = A.kind <= TFG_JOIN_LEFT; // SEMI / ANTI emit the probe row alone
+        for (int64_t step = ps; step < pe; step += (int64_t)JT * JRPT) {
+            uint64_t key[JRPT];
+            unsigned head[JRPT];
+            uint32_t cnt[JRPT], e[JRPT];
+#pragma unroll
+            for (int u = 0; u < JRPT; ++u) {
+                const int64_t r = step + u * JT + threadIdx.x;
+                if (r < pe) key[u] = A.prec[r * prw];
+            }
+            uint32_t esum = 0;
+#pragma unroll
+            for (int u = 0; u < JRPT; ++u) {
+                const int64_t r = step + u * JT + threadIdx.x;
+                const bool valid = r < pe;
+                head[u] = 0xFFFFFFFFu;
+                cnt[u] = 0;
+                e[u] = 0;
+                if (!valid) continue;
+                const int cell = jfind(L, key[u], A.slot_shift);
                 if (cell >= 0) {
-                    head = L.head[cell];
-                    cnt = L.cnt[cell];
+                    head[u] = L.head[cell];
+                    cnt[u] = L.cnt[cell];
                 }
-            }
-            bool prev_found = false;
-            if (valid && chunks > 1) {
-                prev_found = A.found[r] != 0;
-                if (cnt && !last) A.found[r] = 1;
-            }
-            uint32_t e = 0;
-            if (valid) {
+                bool prev_found = false;
+                if (chunks > 1) {
+                    prev_found = A.found[r] != 0;
+                    if (cnt[u] && !last) A.found[r] = 1;
+                }
                 switch (A.kind) {
-                case TFG_JOIN_INNER: e = cnt; break;
-                case TFG_JOIN_LEFT: e = cnt + ((last && cnt == 0 && !prev_found) ? 1 : 0); break;
-                case TFG_JOIN_SEMI: e = (last && (cnt || prev_found)) ? 1 : 0; break;
-                default: e = (last && !cnt && !prev_found) ? 1 : 0; break;
+                case TFG_JOIN_INNER: e[u] = cnt[u]; break;
+                case TFG_JOIN_LEFT: e[u] = cnt[u] + ((last && cnt[u] == 0 && !prev_found) ? 1 : 0); break;
+                case TFG_JOIN_SEMI: e[u] = (last && (cnt[u] || prev_found)) ? 1 : 0; break;
+                default: e[u] = (last && !cnt[u] && !prev_found) ? 1 : 0; break;
                 }
+                esum += e[u];
             }
-            const bool pairs = A.kind <= TFG_JOIN_LEFT; // SEMI / ANTI emit the probe row alone
             uint32_t total;
-            const uint32_t off = jblock_scan(e, L.red, total);
+            const uint32_t off = jblock_scan(esum, L.red, total);
             if (total == 0) continue;
             if (L.buf_n + total > (unsigned)JBUF) flush_pairs(A, L, ps, c0);
             if (total > (unsigned)JBUF) {
                 // more pairs in this step than the buffer holds: emit it in buffer-sized rounds
                 for (uint32_t lo = 0; lo < total; lo += JBUF) {
                     const uint32_t hi = std::min<uint32_t>(total, lo + JBUF);
-                    if (e && off + e > lo && off < hi) {
-                        unsigned jb = head;
-                        for (uint32_t q = 0; q < e; ++q) {
-                            const uint32_t slot = off + q;
-                            const bool pair = pairs && q < cnt;
+                    uint32_t slot = off;
+#pragma unroll
+                    for (int u = 0; u < JRPT; ++u) {
+                        const int64_t r = step + u * JT + threadIdx.x;
+                        unsigned jb = head[u];
+                        for (uint32_t q = 0; q < e[u]; ++q, ++slot) {
+                            const bool pair = pairs && q < cnt[u];
                             if (slot >= lo && slot < hi) {
                                 L.buf_p[slot - lo] = (uint32_t)(r - ps);
                                 L.buf_b[slot - lo] = pair ? jb : 0xFFFFFFFFu;
@@ -273,13 +288,15 @@ __global__ void __launch_bounds__(JT) join_probe_kernel(JoinArgs A) {
                 }
                 continue;
             }
-            const unsigned pos0 = L.buf_n + off;
-            if (e) {
-                unsigned jb = head;
-                for (uint32_t q = 0; q < e; ++q) {
-                    const bool pair = pairs && q < cnt;
-                    L.buf_p[pos0 + q] = (uint32_t)(r - ps);
-                    L.buf_b[pos0 + q] = pair ? jb : 0xFFFFFFFFu;
+            unsigned pos = L.buf_n + off;
+#pragma unroll
+            for (int u = 0; u < JRPT; ++u) {
+                const int64_t r = step + u * JT + threadIdx.x;
+                unsigned jb = head[u];
+                for (uint32_t q = 0; q < e[u]; ++q, ++pos) {
+                    const bool pair = pairs && q < cnt[u];
+                    L.buf_p[pos] = (uint32_t)(r - ps);
+                    L.buf_b[pos] = pair ? jb : 0xFFFFFFFFu;
                     if (pair) jb = L.next[jb];
                 }
             }
