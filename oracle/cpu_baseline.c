@@ -418,3 +418,277 @@ size_t orc_bench_filter_agg_ref(const int64_t *f, int64_t threshold, const int64
     free(th);
     return groups;
 }
+
+/* ------------------------------------------------------------------ C3 join leg
+ * Join with the reference's structures (Interpreters/Join.cpp:532-735, JoinPartition.cpp:584-728,
+ * 1290-1644; JoinHashMap.h:24-60,175-188): build_concurrency = nthreads segment maps
+ * HashMap<UInt64, RowRefList, HashCRC32> (32-byte cells: key + RowRefList{block, row,
+ * list_length, next}), segment = hash % build_concurrency; a later row of a key goes into the
+ * list at position 2 (insertRowToList).  Probe: each thread takes 65536-row probe blocks
+ * (max_block_size), finds each key in its segment's map and appends the matched rows to the
+ * output block columns (probe key, probe payload replicated; build payload inserted) —
+ * Adder<Inner, All> + replicateRange.  Only the probe is timed by the caller's leg. */
+typedef struct {
+    uint64_t key;
+    uint32_t row;
+    uint32_t list_length;
+    int64_t next; /* extra RowRefList node, -1 = end */
+    uint64_t block; /* the RowRef's Block pointer (kept for the cell size) */
+} jcell;
+
+typedef struct {
+    jcell *cells;
+    int degree;
+    size_t size;
+    int has_zero;
+    jcell zero;
+    /* extra list nodes (RowRefList allocated in the pool) */
+    uint32_t *node_row;
+    int64_t *node_next;
+    size_t nodes, node_cap;
+} jmap;
+
+static void jm_init(jmap *m)
+{
+    memset(m, 0, sizeof(*m));
+    m->degree = 8;
+    m->cells = (jcell *)calloc((size_t)1 << m->degree, sizeof(jcell));
+}
+
+static void jm_resize(jmap *m)
+{
+    const size_t old_cap = (size_t)1 << m->degree;
+    jcell *old = m->cells;
+    m->degree += m->degree >= 23 ? 1 : 2;
+    const size_t mask = ((size_t)1 << m->degree) - 1;
+    m->cells = (jcell *)calloc(mask + 1, sizeof(jcell));
+    for (size_t i = 0; i < old_cap; ++i) {
+        if (!old[i].list_length) continue;
+        size_t p = crc_key(old[i].key) & mask;
+        while (m->cells[p].list_length) p = (p + 1) & mask;
+        m->cells[p] = old[i];
+    }
+    free(old);
+}
+
+static void jm_insert(jmap *m, uint64_t key, uint32_t h, uint32_t row)
+{
+    jcell *c;
+    if (key == 0) {
+        c = &m->zero;
+        m->has_zero = 1;
+    } else {
+        const size_t mask = ((size_t)1 << m->degree) - 1;
+        size_t p = h & mask;
+        while (m->cells[p].list_length && m->cells[p].key != key) p = (p + 1) & mask;
+        c = &m->cells[p];
+        if (!c->list_length) {
+            c->key = key;
+            c->row = row;
+            c->list_length = 1;
+            c->next = -1;
+            if (++m->size > ((size_t)1 << (m->degree - 1))) jm_resize(m);
+            return;
+        }
+    }
+    if (!c->list_length) {
+        c->key = key;
+        c->row = row;
+        c->list_length = 1;
+        c->next = -1;
+        return;
+    }
+    if (m->nodes == m->node_cap) {
+        m->node_cap = m->node_cap ? m->node_cap * 2 : 1024;
+        m->node_row = (uint32_t *)realloc(m->node_row, m->node_cap * 4);
+        m->node_next = (int64_t *)realloc(m->node_next, m->node_cap * 8);
+    }
+    m->node_row[m->nodes] = row; /* insertRowToList: new node right after the head */
+    m->node_next[m->nodes] = c->next;
+    c->next = (int64_t)m->nodes++;
+    c->list_length++;
+}
+
+static const jcell *jm_find(const jmap *m, uint64_t key, uint32_t h)
+{
+    if (key == 0) return m->has_zero ? &m->zero : NULL;
+    const size_t mask = ((size_t)1 << m->degree) - 1;
+    size_t p = h & mask;
+    while (m->cells[p].list_length) {
+        if (m->cells[p].key == key) return &m->cells[p];
+        p = (p + 1) & mask;
+    }
+    return NULL;
+}
+
+typedef struct orc_join_ref {
+    int segs;
+    jmap *maps;
+    const int64_t *bpay;
+} orc_join_ref;
+
+typedef struct {
+    orc_join_ref *j;
+    const int64_t *bk;
+    size_t nb;
+    int seg;
+    uint32_t **seg_rows; /* [thread][seg] lists (filled by the dispatch step) */
+    size_t **seg_cnt;
+    int nthreads;
+    size_t begin, end;
+} jb_task;
+
+static void *jb_dispatch(void *arg)
+{
+    jb_task *t = (jb_task *)arg;
+    const int S = t->j->segs;
+    size_t *cnt = t->seg_cnt[t->seg];
+    for (size_t r = t->begin; r < t->end; ++r) cnt[crc_key((uint64_t)t->bk[r]) % (uint32_t)S]++;
+    size_t *off = (size_t *)calloc((size_t)S + 1, sizeof(size_t));
+    for (int s = 0; s < S; ++s) off[s + 1] = off[s] + cnt[s];
+    uint32_t *rows = (uint32_t *)malloc((t->end - t->begin + 1) * 4);
+    size_t *pos = (size_t *)malloc((size_t)S * sizeof(size_t));
+    memcpy(pos, off, (size_t)S * sizeof(size_t));
+    for (size_t r = t->begin; r < t->end; ++r) rows[pos[crc_key((uint64_t)t->bk[r]) % (uint32_t)S]++] = (uint32_t)r;
+    t->seg_rows[t->seg] = rows;
+    memcpy(cnt, off, (size_t)(S + 1) * sizeof(size_t)); /* becomes the offsets */
+    free(off);
+    free(pos);
+    return NULL;
+}
+
+static void *jb_build(void *arg)
+{
+    jb_task *t = (jb_task *)arg;
+    jmap *m = &t->j->maps[t->seg];
+    for (int th = 0; th < t->nthreads; ++th) {
+        const size_t *off = t->seg_cnt[th];
+        const uint32_t *rows = t->seg_rows[th];
+        for (size_t i = off[t->seg]; i < off[t->seg + 1]; ++i) {
+            const uint32_t r = rows[i];
+            const uint64_t key = (uint64_t)t->bk[r];
+            jm_insert(m, key, crc_key(key), r);
+        }
+    }
+    return NULL;
+}
+
+orc_join_ref *orc_join_ref_build(const int64_t *bk, const int64_t *bpay, size_t nb, int nthreads)
+{
+    if (nthreads < 1) nthreads = 1;
+    orc_join_ref *j = (orc_join_ref *)calloc(1, sizeof(orc_join_ref));
+    j->segs = nthreads;
+    j->bpay = bpay;
+    j->maps = (jmap *)calloc((size_t)nthreads, sizeof(jmap));
+    for (int s = 0; s < nthreads; ++s) jm_init(&j->maps[s]);
+    jb_task *tasks = (jb_task *)calloc((size_t)nthreads, sizeof(jb_task));
+    uint32_t **seg_rows = (uint32_t **)calloc((size_t)nthreads, sizeof(uint32_t *));
+    size_t **seg_cnt = (size_t **)calloc((size_t)nthreads, sizeof(size_t *));
+    pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+    const size_t per = (nb + (size_t)nthreads - 1) / (size_t)nthreads;
+    for (int i = 0; i < nthreads; ++i) {
+        seg_cnt[i] = (size_t *)calloc((size_t)nthreads + 1, sizeof(size_t));
+        tasks[i] = (jb_task){j, bk, nb, i, seg_rows, seg_cnt, nthreads, per * (size_t)i < nb ? per * (size_t)i : nb,
+                             per * (size_t)(i + 1) < nb ? per * (size_t)(i + 1) : nb};
+        pthread_create(&th[i], NULL, jb_dispatch, &tasks[i]);
+    }
+    for (int i = 0; i < nthreads; ++i) pthread_join(th[i], NULL);
+    for (int i = 0; i < nthreads; ++i) pthread_create(&th[i], NULL, jb_build, &tasks[i]);
+    for (int i = 0; i < nthreads; ++i) pthread_join(th[i], NULL);
+    for (int i = 0; i < nthreads; ++i) {
+        free(seg_rows[i]);
+        free(seg_cnt[i]);
+    }
+    free(seg_rows);
+    free(seg_cnt);
+    free(tasks);
+    free(th);
+    return j;
+}
+
+void orc_join_ref_destroy(orc_join_ref *j)
+{
+    for (int s = 0; s < j->segs; ++s) {
+        free(j->maps[s].cells);
+        free(j->maps[s].node_row);
+        free(j->maps[s].node_next);
+    }
+    free(j->maps);
+    free(j);
+}
+
+typedef struct {
+    const orc_join_ref *j;
+    const int64_t *pk, *ppay;
+    size_t begin, end;
+    size_t matches;
+    uint64_t checksum;
+} jp_ref_task;
+
+static void *jp_ref_worker(void *arg)
+{
+    jp_ref_task *t = (jp_ref_task *)arg;
+    const orc_join_ref *j = t->j;
+    const size_t B = 65536;
+    size_t cap = B * 2;
+    int64_t *ok = (int64_t *)malloc(cap * 8), *op = (int64_t *)malloc(cap * 8), *ob = (int64_t *)malloc(cap * 8);
+    for (size_t s = t->begin; s < t->end; s += B) {
+        const size_t m = t->end - s < B ? t->end - s : B;
+        size_t k = 0;
+        for (size_t i = 0; i < m; ++i) {
+            const uint64_t key = (uint64_t)t->pk[s + i];
+            const uint32_t h = crc_key(key);
+            const jcell *c = jm_find(&j->maps[h % (uint32_t)j->segs], key, h);
+            if (!c) continue;
+            if (k + c->list_length > cap) {
+                cap = (k + c->list_length) * 2;
+                ok = (int64_t *)realloc(ok, cap * 8);
+                op = (int64_t *)realloc(op, cap * 8);
+                ob = (int64_t *)realloc(ob, cap * 8);
+            }
+            const jmap *mm = &j->maps[h % (uint32_t)j->segs];
+            ok[k] = (int64_t)key;
+            op[k] = t->ppay[s + i];
+            ob[k++] = j->bpay[c->row];
+            for (int64_t nd = c->next; nd >= 0; nd = mm->node_next[nd]) {
+                ok[k] = (int64_t)key;
+                op[k] = t->ppay[s + i];
+                ob[k++] = j->bpay[mm->node_row[nd]];
+            }
+        }
+        for (size_t q = 0; q < k; q += 97) t->checksum += (uint64_t)ob[q] ^ (uint64_t)op[q]; /* consume the block */
+        t->matches += k;
+    }
+    free(ok);
+    free(op);
+    free(ob);
+    return NULL;
+}
+
+size_t orc_join_ref_probe(const orc_join_ref *j, const int64_t *pk, const int64_t *ppay, size_t np, int nthreads,
+                          uint64_t *checksum)
+{
+    if (nthreads < 1) nthreads = 1;
+    jp_ref_task *tasks = (jp_ref_task *)calloc((size_t)nthreads, sizeof(jp_ref_task));
+    pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+    const size_t per = (np + (size_t)nthreads - 1) / (size_t)nthreads;
+    for (int i = 0; i < nthreads; ++i) {
+        tasks[i].j = j;
+        tasks[i].pk = pk;
+        tasks[i].ppay = ppay;
+        tasks[i].begin = per * (size_t)i < np ? per * (size_t)i : np;
+        tasks[i].end = per * (size_t)(i + 1) < np ? per * (size_t)(i + 1) : np;
+        pthread_create(&th[i], NULL, jp_ref_worker, &tasks[i]);
+    }
+    size_t total = 0;
+    uint64_t cs = 0;
+    for (int i = 0; i < nthreads; ++i) {
+        pthread_join(th[i], NULL);
+        total += tasks[i].matches;
+        cs += tasks[i].checksum;
+    }
+    if (checksum) *checksum = cs;
+    free(tasks);
+    free(th);
+    return total;
+}

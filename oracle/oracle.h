@@ -67,6 +67,12 @@ size_t orc_bench_filter_agg(const int64_t *f, int64_t threshold, const int64_t *
  * result conversion.  bench.py's cpu_baseline leg. */
 size_t orc_bench_filter_agg_ref(const int64_t *f, int64_t threshold, const int64_t *k, const double *v, size_t n,
                                 int nthreads, size_t block_rows, double *checksum);
+/* C3 join leg with the reference's structures (cpu_baseline.c): segment maps of RowRefList cells. */
+typedef struct orc_join_ref orc_join_ref;
+orc_join_ref *orc_join_ref_build(const int64_t *build_keys, const int64_t *build_pay, size_t nb, int nthreads);
+size_t orc_join_ref_probe(const orc_join_ref *j, const int64_t *probe_keys, const int64_t *probe_pay, size_t np,
+                          int nthreads, uint64_t *checksum);
+void orc_join_ref_destroy(orc_join_ref *j);
 size_t orc_bench_join(const int64_t *build_keys, size_t nb, const int64_t *probe_keys, size_t np, int nthreads,
                       uint64_t *checksum);
 

@@ -52,6 +52,11 @@ def lib():
         L.orc_bench_filter_agg.restype = ctypes.c_size_t
         L.orc_bench_join.restype = ctypes.c_size_t
         L.orc_bench_filter_agg_ref.restype = ctypes.c_size_t
+        L.orc_join_ref_build.restype = ctypes.c_void_p
+        L.orc_join_ref_probe.restype = ctypes.c_size_t
+        L.orc_join_ref_probe.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                         ctypes.c_int, ctypes.c_void_p]
+        L.orc_join_ref_destroy.argtypes = [ctypes.c_void_p]
         _L = L
     return _L
 
@@ -237,6 +242,27 @@ def bench_filter_agg_ref(f, threshold, k, v, nthreads, block_rows=65536):
     g = lib().orc_bench_filter_agg_ref(_p(f), ctypes.c_int64(threshold), _p(k), _p(v), ctypes.c_size_t(len(k)),
                                        nthreads, ctypes.c_size_t(block_rows), ctypes.byref(cs))
     return g, cs.value
+
+
+class JoinBench:
+    """C3 CPU leg: build once (timed separately), probe + materialise timed by the caller."""
+
+    def __init__(self, build_keys, build_pay, nthreads):
+        self.bk, self.bp = np.ascontiguousarray(build_keys), np.ascontiguousarray(build_pay)
+        self.threads = nthreads
+        self.h = ctypes.c_void_p(lib().orc_join_ref_build(_p(self.bk), _p(self.bp), ctypes.c_size_t(len(self.bk)),
+                                                          nthreads))
+
+    def probe(self, probe_keys, probe_pay):
+        cs = ctypes.c_uint64()
+        m = lib().orc_join_ref_probe(self.h, _p(probe_keys), _p(probe_pay), ctypes.c_size_t(len(probe_keys)),
+                                     self.threads, ctypes.byref(cs))
+        return m, cs.value
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_join_ref_destroy(self.h)
+            self.h = None
 
 
 def bench_join(build_keys, probe_keys, nthreads):

@@ -169,3 +169,17 @@ def test_bench_ref_leg_matches_oracle(orc, groups):
         g, cs = orc.bench_filter_agg_ref(f, 96, k, v, threads, 4096)
         assert g == ref.size()
         assert cs == pytest.approx(float(r["states"][0].sum() + r["states"][1].sum()), rel=1e-12)
+
+
+def test_bench_join_ref_leg_matches_oracle(orc):
+    """cpu_baseline.c's join leg finds the same matches as the restatement (duplicates, key 0)."""
+    rng = np.random.default_rng(9)
+    bk = rng.integers(0, 5000, 20_000, dtype=np.int64)
+    bk[:5] = 0
+    pk = rng.integers(0, 8000, 50_000, dtype=np.int64)
+    jb = orc.JoinBench(bk, bk * 3, 3)
+    m, _ = jb.probe(pk, pk)
+    ref = orc.JoinRef(orc.INT64)
+    ref.build(bk)
+    pi, _ = ref.probe(pk)
+    assert m == len(pi)
