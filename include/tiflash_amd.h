@@ -62,6 +62,11 @@ typedef enum tfg_type {
     TFG_DECIMAL32 = 11,  /* Int32 payload  (precision <= 9)  */
     TFG_DECIMAL64 = 12,  /* Int64 payload  (precision <= 18) */
     TFG_DECIMAL128 = 13, /* Int128 payload (precision <= 38), little-endian two's complement */
+    TFG_STRING = 20,     /* ColumnString: chars (every row ends with '\0') + UInt64 end offsets
+                          * (Columns/ColumnString.h:50-54); GROUP BY keys only */
+    TFG_KEYS128 = 21,    /* a packed 16-byte GROUP BY key (see tfg_agg_create_keys): the device
+                          * form the keys128 / key_string methods aggregate on, and the form
+                          * partial results travel in between the two phases of an aggregation */
 } tfg_type;
 
 /* Comparison ops (dbms/src/Functions/FunctionsComparison.h, accurate:: semantics of
@@ -272,6 +277,33 @@ int tfg_agg_size(tfg_agg *agg, uint64_t *out_groups);
  * Order is the table's (compare unordered, as the reference tests do). */
 int tfg_agg_result(tfg_agg *agg, void *out_keys, uint8_t *out_key_nullmap, void *const *out_states,
                    uint8_t *const *out_state_nullmaps, uint64_t capacity, uint64_t *out_groups_host);
+/* Several GROUP BY keys or one String key (Aggregator::chooseAggregationMethod, Interpreters/
+ * Aggregator.cpp:394-537): fixed-width keys whose widths sum to <= 16 bytes take the keys128 /
+ * nullable_keys128 method (packFixed, Common/ColumnsHashing.h:324-480; nullable keys need
+ * widths summing to <= 15: byte 15 holds their NULL bits); one String key takes key_string
+ * (HashMethodString, ColumnsHashing.h:179-241): rows group by the collator's sort key
+ * (key_collators[0]: tfg_collator; BIN_PADDING right-trims spaces), which must be <= 15 bytes
+ * (longer keys fail with TFG_ERR_NOT_IMPLEMENTED).  Both aggregate on a packed 16-byte key
+ * (TFG_KEYS128).  One non-String key falls back to tfg_agg_create.  key_collators may be NULL. */
+int tfg_agg_create_keys(tfg_ctx *ctx, int nkeys, const int *key_types, const int *key_collators, int n_aggs,
+                        const int *agg_kinds, const int *arg_types, const int *arg_scales, const tfg_agg_params *params,
+                        tfg_agg **out);
+/* executeOnBlock over the key columns of tfg_agg_create_keys: key_cols[j] is the data (String:
+ * chars) of key j, key_offsets[j] the String key's end offsets (NULL for fixed keys),
+ * key_nullmaps (optional) their null maps. */
+int tfg_agg_consume_keys(tfg_agg *agg, const void *const *key_cols, const uint64_t *const *key_offsets,
+                         const uint8_t *const *key_nullmaps, const void *const *args, const uint8_t *const *arg_nullmaps,
+                         const uint8_t *mask, int64_t n);
+/* Two-phase final aggregation over partial (key columns, states) rows (mergeOnBlock). */
+int tfg_agg_consume_partial_keys(tfg_agg *agg, const void *const *key_cols, const uint64_t *const *key_offsets,
+                                 const uint8_t *const *key_nullmaps, const void *const *states,
+                                 const uint8_t *const *state_nullmaps, int64_t n);
+/* convertToBlockImplFinal with the key columns restored (String: chars + end offsets; chars
+ * need *out_chars_host bytes, TFG_ERR_CAPACITY past chars_capacity).  tfg_agg_result on the same
+ * agg writes the packed TFG_KEYS128 keys instead, which tfg_agg_consume_partial accepts. */
+int tfg_agg_result_keys(tfg_agg *agg, void *const *out_key_cols, uint64_t *const *out_key_offsets,
+                        uint8_t *const *out_key_nullmaps, void *const *out_states, uint8_t *const *out_state_nullmaps,
+                        uint64_t capacity, uint64_t chars_capacity, uint64_t *out_groups_host, uint64_t *out_chars_host);
 /* Result type of agg i (tfg_type) and its width in bytes. */
 int tfg_agg_result_type(tfg_agg *agg, int i, int *out_type, int *out_width);
 

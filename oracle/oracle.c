@@ -605,6 +605,189 @@ void orc_agg_result(const orc_agg *a, uint64_t *out_keys, uint8_t *out_key_null,
     }
 }
 
+/* ------------------------------------------------------------------ Aggregator, several keys / String key */
+/* Methods keys128 / nullable_keys128 / key_string / serialized (Interpreters/Aggregator.cpp:394-537,
+ * Common/ColumnsHashing.h:179-629): every method groups rows by the tuple of key values, a NULL
+ * key value being its own value, and a String key by its collator sort key
+ * (HashMethodString::getKeyHolder, ColumnsHashing.h:224-236; BIN padding = right-trim ' ').  The
+ * restatement serialises each row's tuple like the serialized method (serializeValueIntoArena):
+ * per key one NULL byte, then the fixed value's bytes or an 8-byte length + the sort-key bytes;
+ * the bytes map to a dense group id (first-seen order) through a byte-string hash map, and the
+ * states live in an inner orc_agg keyed by that id. */
+struct orc_aggk {
+    int nkeys;
+    int key_types[4];
+    int collators[4];
+    /* byte-string map: open addressing over (hash, id) cells; keys in one arena */
+    uint64_t *cells; /* (crc << 32) | (id + 1), 0 = empty */
+    size_t cap, size;
+    uint8_t *arena;
+    size_t arena_len, arena_cap;
+    uint64_t *key_off; /* id -> arena offset, id + 1 -> end */
+    size_t key_cap;
+    orc_agg *inner;
+    uint32_t *ids;
+    size_t ids_cap;
+};
+
+static uint32_t bytes_hash(const uint8_t *p, size_t n) { return orc_update_weak_hash32_bytes(p, n, 0xFFFFFFFFu); }
+
+orc_aggk *orc_aggk_create(int nkeys, const int *key_types, const int *collators, int n_aggs, const int *kinds,
+                          const int *arg_types)
+{
+    if (nkeys < 1 || nkeys > 4) return NULL;
+    orc_aggk *a = (orc_aggk *)calloc(1, sizeof(orc_aggk));
+    a->nkeys = nkeys;
+    for (int j = 0; j < nkeys; ++j) {
+        a->key_types[j] = key_types[j];
+        a->collators[j] = collators ? collators[j] : 0;
+    }
+    a->cap = 1024;
+    a->cells = (uint64_t *)calloc(a->cap, 8);
+    a->key_cap = 1024;
+    a->key_off = (uint64_t *)malloc(a->key_cap * 8);
+    a->key_off[0] = 0;
+    a->inner = orc_agg_create(TFG_UINT32, n_aggs, kinds, arg_types);
+    return a;
+}
+
+void orc_aggk_destroy(orc_aggk *a)
+{
+    if (!a) return;
+    free(a->cells);
+    free(a->arena);
+    free(a->key_off);
+    free(a->ids);
+    orc_agg_destroy(a->inner);
+    free(a);
+}
+
+static void aggk_grow(orc_aggk *a)
+{
+    size_t nc = a->cap * 2;
+    uint64_t *c = (uint64_t *)calloc(nc, 8);
+    for (size_t i = 0; i < a->cap; ++i) {
+        if (!a->cells[i]) continue;
+        size_t p = (a->cells[i] >> 32) & (nc - 1);
+        while (c[p]) p = (p + 1) & (nc - 1);
+        c[p] = a->cells[i];
+    }
+    free(a->cells);
+    a->cells = c;
+    a->cap = nc;
+}
+
+static uint32_t aggk_id(orc_aggk *a, const uint8_t *k, size_t len)
+{
+    const uint32_t h = bytes_hash(k, len);
+    size_t p = h & (a->cap - 1);
+    for (;; p = (p + 1) & (a->cap - 1)) {
+        const uint64_t c = a->cells[p];
+        if (!c) break;
+        if ((uint32_t)(c >> 32) != h) continue;
+        const uint32_t id = (uint32_t)c - 1;
+        if (a->key_off[id + 1] - a->key_off[id] == len && !memcmp(a->arena + a->key_off[id], k, len)) return id;
+    }
+    const uint32_t id = (uint32_t)a->size++;
+    a->cells[p] = ((uint64_t)h << 32) | (id + 1);
+    if (a->arena_len + len > a->arena_cap) {
+        a->arena_cap = (a->arena_len + len) * 2 + 4096;
+        a->arena = (uint8_t *)realloc(a->arena, a->arena_cap);
+    }
+    memcpy(a->arena + a->arena_len, k, len);
+    a->arena_len += len;
+    if (id + 2 > a->key_cap) {
+        a->key_cap *= 2;
+        a->key_off = (uint64_t *)realloc(a->key_off, a->key_cap * 8);
+    }
+    a->key_off[id + 1] = a->arena_len;
+    if (a->size * 2 > a->cap) aggk_grow(a);
+    return id;
+}
+
+/* serialise row r's key tuple into buf (<= 4 keys x (1 + 16) bytes, or 9 + string length) */
+static size_t aggk_serialize(const orc_aggk *a, const void *const *cols, const uint64_t *const *offs,
+                             const uint8_t *const *nulls, size_t r, uint8_t **buf, size_t *bcap)
+{
+    size_t need = 0;
+    for (int j = 0; j < a->nkeys; ++j) {
+        if (a->key_types[j] == TFG_STRING) need += 9 + (offs[j][r] - (r ? offs[j][r - 1] : 0));
+        else need += 17;
+    }
+    if (need > *bcap) {
+        *bcap = need * 2;
+        *buf = (uint8_t *)realloc(*buf, *bcap);
+    }
+    uint8_t *o = *buf;
+    for (int j = 0; j < a->nkeys; ++j) {
+        const int isnull = nulls && nulls[j] && nulls[j][r];
+        *o++ = (uint8_t)isnull;
+        if (isnull) continue;
+        if (a->key_types[j] == TFG_STRING) {
+            const uint64_t s = r ? offs[j][r - 1] : 0;
+            uint64_t len = offs[j][r] - s - 1;
+            const uint8_t *c = (const uint8_t *)cols[j] + s;
+            if (a->collators[j] == TFG_COLLATOR_BIN_PADDING)
+                while (len > 0 && c[len - 1] == ' ') --len;
+            memcpy(o, &len, 8);
+            memcpy(o + 8, c, len);
+            o += 8 + len;
+        } else {
+            const size_t w = type_width(a->key_types[j]);
+            memcpy(o, (const uint8_t *)cols[j] + w * r, w);
+            o += w;
+        }
+    }
+    return (size_t)(o - *buf);
+}
+
+static uint32_t *aggk_ids(orc_aggk *a, const void *const *key_cols, const uint64_t *const *key_offsets,
+                          const uint8_t *const *key_nulls, const uint8_t *mask, size_t n)
+{
+    if (n > a->ids_cap) {
+        a->ids_cap = n;
+        a->ids = (uint32_t *)realloc(a->ids, n * 4);
+    }
+    uint8_t *buf = NULL;
+    size_t bcap = 0;
+    for (size_t r = 0; r < n; ++r) {
+        if (mask && !mask[r]) { a->ids[r] = 0; continue; }
+        size_t len = aggk_serialize(a, key_cols, key_offsets, key_nulls, r, &buf, &bcap);
+        a->ids[r] = aggk_id(a, buf, len);
+    }
+    free(buf);
+    return a->ids;
+}
+
+void orc_aggk_consume(orc_aggk *a, const void *const *key_cols, const uint64_t *const *key_offsets,
+                      const uint8_t *const *key_nulls, const void *const *args, const uint8_t *const *arg_nulls,
+                      const uint8_t *mask, size_t n)
+{
+    uint32_t *ids = aggk_ids(a, key_cols, key_offsets, key_nulls, mask, n);
+    orc_agg_consume(a->inner, ids, NULL, args, arg_nulls, mask, n);
+}
+
+size_t orc_aggk_size(const orc_aggk *a) { return orc_agg_size(a->inner); }
+
+/* groups in creation order: serialized keys (out_keys: arena bytes, out_key_offsets: end offsets,
+ * pass NULL to get the byte count first) and states as orc_agg_result. */
+size_t orc_aggk_result(const orc_aggk *a, uint8_t *out_keys, uint64_t *out_key_offsets, void *const *out_states,
+                       uint8_t *const *out_state_null)
+{
+    const size_t g = orc_agg_size(a->inner);
+    uint64_t *ids = (uint64_t *)malloc((g ? g : 1) * 8);
+    orc_agg_result(a->inner, ids, NULL, out_states, out_state_null);
+    size_t total = 0;
+    for (size_t i = 0; i < g; ++i) {
+        const uint64_t id = ids[i], s = a->key_off[id], e = a->key_off[id + 1];
+        if (out_keys) memcpy(out_keys + total, a->arena + s, e - s);
+        total += e - s;
+        if (out_key_offsets) out_key_offsets[i] = total;
+    }
+    free(ids);
+    return total;
+}
+
 /* ------------------------------------------------------------------ Join (hash join v1) */
 /* MapsAll = HashMap<UInt64, RowRefList, HashCRC32<UInt64>> (Interpreters/JoinHashMap.h:175-188).
  * Inserter<All>::insert (JoinPartition.cpp:494-524): the first row of a key lives in the cell; every

@@ -51,6 +51,18 @@ size_t orc_agg_size(const orc_agg *a);
 void orc_agg_result(const orc_agg *a, uint64_t *out_keys, uint8_t *out_key_null, void *const *out_states,
                     uint8_t *const *out_state_null);
 
+/* Several keys / one String key (Aggregator methods keys128, key_string, serialized). */
+typedef struct orc_aggk orc_aggk;
+orc_aggk *orc_aggk_create(int nkeys, const int *key_types, const int *collators, int n_aggs, const int *kinds,
+                          const int *arg_types);
+void orc_aggk_destroy(orc_aggk *a);
+void orc_aggk_consume(orc_aggk *a, const void *const *key_cols, const uint64_t *const *key_offsets,
+                      const uint8_t *const *key_nulls, const void *const *args, const uint8_t *const *arg_nulls,
+                      const uint8_t *mask, size_t n);
+size_t orc_aggk_size(const orc_aggk *a);
+size_t orc_aggk_result(const orc_aggk *a, uint8_t *out_keys, uint64_t *out_key_offsets, void *const *out_states,
+                       uint8_t *const *out_state_null);
+
 typedef struct orc_join orc_join;
 orc_join *orc_join_create(int key_type);
 void orc_join_build(orc_join *j, const void *keys, const uint8_t *key_null, size_t n);

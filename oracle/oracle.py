@@ -18,6 +18,7 @@ _L = None
 
 INT8, INT16, INT32, INT64, UINT8, UINT16, UINT32, UINT64, FLOAT32, FLOAT64 = range(1, 11)
 DECIMAL32, DECIMAL64, DECIMAL128 = 11, 12, 13
+STRING = 20
 NP_TYPE = {np.dtype(np.int8): INT8, np.dtype(np.int16): INT16, np.dtype(np.int32): INT32, np.dtype(np.int64): INT64,
            np.dtype(np.uint8): UINT8, np.dtype(np.uint16): UINT16, np.dtype(np.uint32): UINT32,
            np.dtype(np.uint64): UINT64, np.dtype(np.float32): FLOAT32, np.dtype(np.float64): FLOAT64}
@@ -46,6 +47,11 @@ def lib():
         L.orc_agg_size.restype = ctypes.c_size_t
         L.orc_agg_size.argtypes = [ctypes.c_void_p]
         L.orc_agg_destroy.argtypes = [ctypes.c_void_p]
+        L.orc_aggk_create.restype = ctypes.c_void_p
+        L.orc_aggk_destroy.argtypes = [ctypes.c_void_p]
+        L.orc_aggk_size.restype = ctypes.c_size_t
+        L.orc_aggk_size.argtypes = [ctypes.c_void_p]
+        L.orc_aggk_result.restype = ctypes.c_size_t
         L.orc_join_create.restype = ctypes.c_void_p
         L.orc_join_destroy.argtypes = [ctypes.c_void_p]
         L.orc_join_probe.restype = ctypes.c_size_t
@@ -203,6 +209,99 @@ class Agg:
         if getattr(self, "h", None):
             lib().orc_agg_destroy(self.h)
             self.h = None
+
+
+_SIGNED = {INT8, INT16, INT32, INT64, DECIMAL32, DECIMAL64, DECIMAL128}
+_KW = {INT8: 1, INT16: 2, INT32: 4, INT64: 8, UINT8: 1, UINT16: 2, UINT32: 4, UINT64: 8, FLOAT32: 4, FLOAT64: 8,
+       DECIMAL32: 4, DECIMAL64: 8, DECIMAL128: 16}
+
+
+class AggKeys:
+    """orc_aggk: GROUP BY several keys or one String key (keys128 / key_string / serialized).
+    A String key column is a (chars uint8, offsets uint64) pair.  result() returns the groups as
+    (key tuple, [state_i]) with key values int / bytes / None (NULL)."""
+
+    def __init__(self, key_types, aggs, collators=None):
+        self.key_types = list(key_types)
+        self.aggs = list(aggs)
+        kt = (ctypes.c_int * len(key_types))(*key_types)
+        co = (ctypes.c_int * len(key_types))(*(collators or [0] * len(key_types)))
+        kinds = (ctypes.c_int * len(aggs))(*[k for k, _ in aggs])
+        types = (ctypes.c_int * len(aggs))(*[t & 0xFF for _, t in aggs])
+        self.h = ctypes.c_void_p(lib().orc_aggk_create(len(key_types), kt, co, len(aggs), kinds, types))
+
+    def consume(self, keys, args, key_nulls=None, arg_nulls=None, mask=None):
+        cols, offs = [], []
+        for t, k in zip(self.key_types, keys):
+            if t == STRING:
+                cols.append(np.ascontiguousarray(k[0]))
+                offs.append(np.ascontiguousarray(k[1], dtype=np.uint64))
+            else:
+                cols.append(np.ascontiguousarray(k))
+                offs.append(None)
+        n = len(offs[0]) if self.key_types[0] == STRING else len(cols[0])
+        self._keep = (cols, offs, args, key_nulls, arg_nulls, mask)
+        lib().orc_aggk_consume(self.h, _ptrs(cols), _ptrs(offs), _ptrs(key_nulls) if key_nulls else None, _ptrs(args),
+                               _ptrs(arg_nulls) if arg_nulls else None, _p(mask), ctypes.c_size_t(n))
+
+    def size(self) -> int:
+        return lib().orc_aggk_size(self.h)
+
+    def _decode(self, b: bytes):
+        out, o = [], 0
+        for t in self.key_types:
+            isnull = b[o]
+            o += 1
+            if isnull:
+                out.append(None)
+                continue
+            if t == STRING:
+                ln = int.from_bytes(b[o:o + 8], "little")
+                out.append(bytes(b[o + 8:o + 8 + ln]))
+                o += 8 + ln
+            else:
+                w = _KW[t]
+                if t in (FLOAT32, FLOAT64):
+                    out.append(float(np.frombuffer(b[o:o + w], np.float32 if t == FLOAT32 else np.float64)[0]))
+                else:
+                    out.append(int.from_bytes(b[o:o + w], "little", signed=t in _SIGNED))
+                o += w
+        return tuple(out)
+
+    def result(self):
+        g = self.size()
+        total = lib().orc_aggk_result(self.h, None, None, None, None)
+        kb = np.zeros(max(total, 1), np.uint8)
+        ko = np.zeros(max(g, 1), np.uint64)
+        states, snull = [], []
+        for kind, t in self.aggs:
+            t &= 0xFF
+            if kind == 0 and t in (DECIMAL32, DECIMAL64, DECIMAL128):
+                states.append(np.zeros((max(g, 1), 2), np.int64))
+            elif kind == 0 and t in (FLOAT32, FLOAT64):
+                states.append(np.zeros(max(g, 1), np.float64))
+            else:
+                states.append(np.zeros(max(g, 1), np.int64))
+            snull.append(np.zeros(max(g, 1), np.uint8))
+        lib().orc_aggk_result(self.h, _p(kb), _p(ko), _ptrs(states), _ptrs(snull))
+        groups = []
+        s = 0
+        for i in range(g):
+            e = int(ko[i])
+            key = self._decode(kb[s:e].tobytes())
+            s = e
+            vals = []
+            for st in states:
+                v = st[i]
+                vals.append(int(v[0]) & ((1 << 64) - 1) | (int(v[1]) << 64) if st.ndim == 2 else v.item())
+            groups.append((key, vals))
+        return groups
+
+    def __del__(self):
+        try:
+            lib().orc_aggk_destroy(self.h)
+        except Exception:
+            pass
 
 
 class JoinRef:

@@ -3,6 +3,9 @@
 reference_cases.json — known answers TRANSCRIBED (as data) from the reference's own gtests:
   * groupby: dbms/src/Flash/tests/gtest_aggregation_executor.cpp:269-272 (columns) and :344-368
     (expected GROUP BY key sets for tinyint_/smallint_/int_/bigint_);
+  * groupby_keys: the same file, :261-270 (columns incl. float_, double_, date_, datetime_ (MyDate /
+    MyDateTime are packed UInt64), string_) with the expected key sets of GROUP BY string_
+    (:408-415) and of the two-column GROUP BYs (:433-482);
   * join: dbms/src/Flash/tests/gtest_join_executor.cpp:114-200 (SimpleJoin tables t1/t2 and the
     expected inner / left / semi / anti results).  The reference keys are strings "1".."4"; join
     equality is unchanged when they are written as the integers 1..4, which is how they are stored;
@@ -61,6 +64,35 @@ def groupby_cases():
     return [{"name": k, "column": v[0], "type": v[1], "dtype": v[2], "expected": v[3]} for k, v in cols.items()]
 
 
+def groupby_keys_cases():
+    # gtest_aggregation_executor.cpp:261-270; type codes of include/tiflash_amd.h (MyDate /
+    # MyDateTime = UInt64 8, Float32 9, Float64 10, String 20)
+    cols = {
+        "tinyint_": (1, [1, 2, 3, N, N, 0, 0, -1, -2]),
+        "smallint_": (2, [2, 3, N, N, 0, -1, -2, 4, 0]),
+        "int_": (3, [4, N, N, 0, 123, -1, -1, 123, 4]),
+        "bigint_": (4, [2, 2, N, 0, -1, N, -1, 0, 123]),
+        "float_": (9, [3.3, N, 0, 4.0, 3.3, 5.6, -0.1, -0.1, N]),
+        "double_": (10, [0.1, 0, 1.1, 1.1, 1.2, N, N, -1.2, -1.2]),
+        "date_": (8, [1000000, 2000000, N, 300000, 1000000, N, 0, 2000000, N]),
+        "datetime_": (8, [2000000, 0, N, 3000000, 1000000, N, 0, 2000000, 1000000]),
+        "string_": (20, [N, "pingcap", "PingCAP", N, "PINGCAP", "PingCAP", N, "Shanghai", "Shanghai"]),
+    }
+    expected = [  # (group by columns, expected columns) :408-415, :433-482
+        (["string_"], [[N, "pingcap", "PingCAP", "PINGCAP", "Shanghai"]]),
+        (["tinyint_", "float_"], [[1, 2, N, 3, 0, 0, -1, N, -2], [3.3, N, 4, 0, -0.1, 5.6, -0.1, 3.3, N]]),
+        (["smallint_", "datetime_"], [[2, 3, N, N, 0, -1, -2, 4], [2000000, 0, N, 3000000, 1000000, N, 0, 2000000]]),
+        (["int_", "double_"], [[N, 123, -1, 0, N, 4, 4, 123], [0, -1.2, N, 1.1, 1.1, -1.2, 0.1, 1.2]]),
+        (["bigint_", "string_"], [[-1, 0, 0, 123, 2, N, -1, 2], [N, N, "Shanghai", "Shanghai", N, "PingCAP", "PINGCAP", "pingcap"]]),
+        (["date_", "datetime_"], [[1000000, 2000000, N, 300000, 1000000, 0, 2000000, N],
+                                  [2000000, 0, N, 3000000, 1000000, 0, 2000000, 1000000]]),
+        (["datetime_", "string_"], [[2000000, 0, N, 3000000, 1000000, 0, 2000000, 1000000],
+                                    [N, "pingcap", "PingCAP", N, "PINGCAP", N, "Shanghai", "Shanghai"]]),
+    ]
+    return {"columns": {k: {"type": t, "values": v} for k, (t, v) in cols.items()},
+            "cases": [{"group_by": g, "expected": e} for g, e in expected]}
+
+
 def crc_vectors():
     from oracle import oracle as orc
     rng = np.random.default_rng(2024)
@@ -78,7 +110,7 @@ def crc_vectors():
 
 if __name__ == "__main__":
     with open(os.path.join(HERE, "reference_cases.json"), "w") as f:
-        json.dump({"groupby": groupby_cases(), "join": join_cases(),
+        json.dump({"groupby": groupby_cases(), "groupby_keys": groupby_keys_cases(), "join": join_cases(),
                    "exchange": {"block_rows": 64, "blocks": 64, "parts": 4, "rows_per_part": 1024}}, f, indent=1)
     with open(os.path.join(HERE, "crc_vectors.json"), "w") as f:
         json.dump(crc_vectors(), f, indent=1)

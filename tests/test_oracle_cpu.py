@@ -92,6 +92,47 @@ def test_groupby_reference_cases(orc):
         assert sorted(got, key=repr) == sorted(case["expected"], key=repr), case["name"]
 
 
+def golden_key_columns(case, cols):
+    """numpy key columns (String: (chars, offsets)) + null maps of one groupby_keys case."""
+    np_t = {1: np.int8, 2: np.int16, 3: np.int32, 4: np.int64, 8: np.uint64, 9: np.float32, 10: np.float64}
+    keys, nulls, types = [], [], []
+    for name in case["group_by"]:
+        t, vals = cols[name]["type"], cols[name]["values"]
+        nulls.append(np.array([v is None for v in vals], dtype=np.uint8))
+        if t == 20:
+            strs = [b"" if v is None else v.encode() for v in vals]
+            keys.append((np.frombuffer(b"".join(x + b"\0" for x in strs), np.uint8).copy(),
+                         np.cumsum([len(x) + 1 for x in strs]).astype(np.uint64)))
+        else:
+            keys.append(np.array([0 if v is None else v for v in vals], dtype=np_t[t]))
+        types.append(t)
+    exp = []
+    for row in zip(*case["expected"]):
+        k = []
+        for t, v in zip(types, row):
+            if v is None:
+                k.append(None)
+            elif t == 20:
+                k.append(v.encode())
+            elif t in (9, 10):
+                k.append(float((np.float32 if t == 9 else np.float64)(v)))
+            else:
+                k.append(int(v))
+        exp.append(tuple(k))
+    return types, keys, nulls, exp
+
+
+def test_groupby_keys_reference_cases(orc):
+    """GroupBy string_ and two-column GROUP BYs (gtest_aggregation_executor.cpp:408-482)."""
+    g = _load("reference_cases.json")["groupby_keys"]
+    for case in g["cases"]:
+        types, keys, nulls, exp = golden_key_columns(case, g["columns"])
+        a = orc.AggKeys(types, [(2, 0)])
+        a.consume(keys, [None], key_nulls=nulls)
+        got = [k for k, _ in a.result()]
+        assert sorted(got, key=repr) == sorted(exp, key=repr), case["group_by"]
+
+
 def _join_rows(case, pi, bi):
     p, b = case["probe"], case["build"]
     rows = []

@@ -28,6 +28,7 @@ TFG_ERR_NO_DEVICE = -9
 
 INT8, INT16, INT32, INT64, UINT8, UINT16, UINT32, UINT64, FLOAT32, FLOAT64 = range(1, 11)
 DECIMAL32, DECIMAL64, DECIMAL128 = 11, 12, 13
+STRING, KEYS128 = 20, 21  # String GROUP BY keys (chars, offsets); packed 16-byte key (tfg_agg_create_keys)
 NULLABLE = 0x100  # or-ed into an aggregate argument type: the argument may carry a null map
 
 EQ, NE, LT, LE, GT, GE = range(6)
@@ -38,7 +39,7 @@ JOIN_INNER, JOIN_LEFT, JOIN_SEMI, JOIN_ANTI = range(4)
 COLLATOR_NONE, COLLATOR_BINARY, COLLATOR_BIN_PADDING = range(3)
 
 WIDTH = {INT8: 1, INT16: 2, INT32: 4, INT64: 8, UINT8: 1, UINT16: 2, UINT32: 4, UINT64: 8,
-         FLOAT32: 4, FLOAT64: 8, DECIMAL32: 4, DECIMAL64: 8, DECIMAL128: 16}
+         FLOAT32: 4, FLOAT64: 8, DECIMAL32: 4, DECIMAL64: 8, DECIMAL128: 16, KEYS128: 16}
 _CTYPE = {INT8: ctypes.c_int8, INT16: ctypes.c_int16, INT32: ctypes.c_int32, INT64: ctypes.c_int64,
           UINT8: ctypes.c_uint8, UINT16: ctypes.c_uint16, UINT32: ctypes.c_uint32, UINT64: ctypes.c_uint64,
           FLOAT32: ctypes.c_float, FLOAT64: ctypes.c_double, DECIMAL32: ctypes.c_int32,
@@ -442,6 +443,91 @@ class Aggregator:
             self.close()
         except Exception:
             pass
+
+
+class KeysAggregator(Aggregator):
+    """tfg_agg_create_keys: GROUP BY several fixed-width keys (keys128) or one String key
+    (key_string; a String column is a (chars uint8, offsets int64/uint64) pair of device tensors).
+    result() restores the key columns; result_packed() / consume_partial_packed() carry the packed
+    16-byte keys between the phases of a two-phase aggregation."""
+
+    def __init__(self, ctx: Context, key_types: Sequence[int], aggs: Sequence[tuple], collators=None,
+                 bucket_bits: int = 0, expected_groups: int = 0):
+        self.ctx = ctx
+        self.key_types = list(key_types)
+        self.key_type = KEYS128 if (len(key_types) > 1 or key_types[0] == STRING) else key_types[0]
+        self.aggs = list(aggs)
+        params = _AggParams(bucket_bits, expected_groups)
+        h = ctypes.c_void_p()
+        check(lib().tfg_agg_create_keys(ctx.h, len(key_types), _int_array(key_types),
+                                        _int_array(collators) if collators else ctypes.c_void_p(0), len(aggs),
+                                        _int_array([k for k, _ in aggs]), _int_array([t for _, t in aggs]),
+                                        ctypes.c_void_p(0), ctypes.byref(params), ctypes.byref(h)))
+        self.h = h
+        ctx._children.add(self)
+
+    def _key_arrays(self, keys):
+        cols, offs = [], []
+        for t, k in zip(self.key_types, keys):
+            if t == STRING:
+                cols.append(k[0])
+                offs.append(k[1])
+            else:
+                cols.append(k)
+                offs.append(None)
+        n = offs[0].shape[0] if self.key_types[0] == STRING else cols[0].shape[0]
+        return _ptr_array(cols), _ptr_array(offs), n
+
+    def consume(self, keys, args: Sequence, key_nullmaps=None, arg_nullmaps=None, mask=None):
+        kc, ko, n = self._key_arrays(keys)
+        check(lib().tfg_agg_consume_keys(self.h, kc, ko, _ptr_array(key_nullmaps) if key_nullmaps else ctypes.c_void_p(0),
+                                         _ptr_array(args), _ptr_array(arg_nullmaps) if arg_nullmaps else ctypes.c_void_p(0),
+                                         _p(mask), ctypes.c_int64(n)))
+
+    def consume_partial(self, keys, states: Sequence, key_nullmaps=None, state_nullmaps=None):
+        kc, ko, n = self._key_arrays(keys)
+        check(lib().tfg_agg_consume_partial_keys(
+            self.h, kc, ko, _ptr_array(key_nullmaps) if key_nullmaps else ctypes.c_void_p(0), _ptr_array(states),
+            _ptr_array(state_nullmaps) if state_nullmaps else ctypes.c_void_p(0), ctypes.c_int64(n)))
+
+    def consume_partial_packed(self, keys16, states: Sequence, state_nullmaps=None):
+        Aggregator.consume_partial(self, keys16, states, None, state_nullmaps)
+
+    def result_packed(self, device=None):
+        """-> dict as Aggregator.result() with keys = (G, 2) int64 packed keys."""
+        return Aggregator.result(self, device)
+
+    def result(self, device=None):
+        """-> dict(keys=[col or (chars, offsets)], key_null=[uint8], states=[...], state_null=[...])."""
+        import torch
+        dev = device or torch.device("cuda", self.ctx.device)
+        g = self.size()
+        cols, offs, nulls = [], [], []
+        for t in self.key_types:
+            if t == STRING:
+                cols.append(torch.empty(max(16 * g, 1), dtype=torch.uint8, device=dev))
+                offs.append(torch.empty(max(g, 1), dtype=torch.int64, device=dev))
+            else:
+                cols.append(_empty(g, WIDTH[t], dev))
+                offs.append(None)
+            nulls.append(torch.empty(max(g, 1), dtype=torch.uint8, device=dev))
+        states, snulls = [], []
+        for i in range(len(self.aggs)):
+            t, w = ctypes.c_int(), ctypes.c_int()
+            check(lib().tfg_agg_result_type(self.h, i, ctypes.byref(t), ctypes.byref(w)))
+            s = _empty(g, w.value, dev)
+            if t.value == FLOAT64:
+                s = s.view(torch.float64)
+            states.append(s)
+            snulls.append(torch.empty(max(g, 1), dtype=torch.uint8, device=dev)[:g])
+        cnt, chars = ctypes.c_uint64(), ctypes.c_uint64()
+        check(lib().tfg_agg_result_keys(self.h, _ptr_array(cols), _ptr_array(offs), _ptr_array(nulls), _ptr_array(states),
+                                        _ptr_array(snulls), ctypes.c_uint64(g), ctypes.c_uint64(16 * g),
+                                        ctypes.byref(cnt), ctypes.byref(chars)))
+        keys = []
+        for t, c, o in zip(self.key_types, cols, offs):
+            keys.append((c[:chars.value], o[:g]) if t == STRING else c[:g])
+        return {"keys": keys, "key_null": [x[:g] for x in nulls], "states": states, "state_null": snulls}
 
 
 # ---- a18-a21 join -----------------------------------------------------------------------------

@@ -50,6 +50,8 @@ struct AggSpec {
     int lds_bytes;
     int dbg; // timing ablation knob (TFG_DBG_BUCKET), 0 in production
     int bt;         // bucket kernel workgroup size (BT or BT_BIG)
+    int wkey_off;   // wide keys (key_width 16): LDS byte offset of the 16-byte keys (cells' tags sit in
+                    // the u64 key array); 0 for keys of <= 8 bytes
     int slot_shift; // in-table group = bits [slot_shift, slot_shift + log2(cap/GS)) of key * 2^64/phi,
                     // just below the bits that chose the bucket (one multiply instead of a mixer)
 };
@@ -66,7 +68,7 @@ struct RowsIO {
 
 // Columnar groups (state / temp).
 struct GroupsIO {
-    uint64_t *key;
+    uint64_t *key; // key bits; wide keys: two words (lo, hi) per group
     uint8_t *key_null;
     void *acc[AGG_MAX];
     uint64_t *cnt[AGG_MAX];
@@ -114,6 +116,17 @@ __device__ __forceinline__ void lds_add_i128(uint64_t *cell, uint64_t lo, uint64
     const uint64_t old = atomicAdd((unsigned long long *)&cell[0], (unsigned long long)lo);
     const uint64_t carry = (old + lo) < old ? 1ull : 0ull;
     atomicAdd((unsigned long long *)&cell[1], (unsigned long long)(hi + carry));
+}
+
+// Tag of a wide (16-byte packed) key: a 64-bit mix of both halves with bit 1 set (never 0) and
+// bit 0 clear.  The bucket radix and the in-table slot group come from tag * 2^64/phi exactly
+// as they come from the key itself for 8-byte keys; bit 0 of a stored tag marks "key published".
+__host__ __device__ __forceinline__ uint64_t wide_tag(uint64_t lo, uint64_t hi) {
+    uint64_t x = lo * 0x9E3779B97F4A7C15ull ^ hi;
+    x ^= x >> 29;
+    x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 32;
+    return (x | 2ull) & ~1ull;
 }
 
 // one staged row held in registers; NA = number of aggregates (compile time, keeps VGPRs low)
@@ -269,6 +282,103 @@ struct Table {
         }
     }
 
+    // Wide keys (keys128 / packed String keys).  A cell is claimed by a 64-bit CAS of the key's
+    // tag into keys[cell]; the claimant then writes the 16-byte key to wkeys[cell] and
+    // republishes the tag with bit 0 set.  A reader whose tag equals a cell's unpublished tag
+    // re-reads the group (the claimant never waits on anything, so the wait is short); equal
+    // published tags are confirmed by comparing the full key, so tag collisions only cost a
+    // probe step.  Every key has exactly one cell: a key cannot be claimed behind an unresolved
+    // cell of the same tag.
+    template <int R>
+    __device__ __forceinline__ void find_wide_multi(const uint64_t (&lo)[R], const uint64_t (&hi)[R],
+                                                    const uint64_t (&tag)[R], const bool (&valid)[R], bool may_insert,
+                                                    int (&cell)[R], bool force = false) {
+        const unsigned gmask = (unsigned)S.cap / GS - 1;
+        uint4 *wk = reinterpret_cast<uint4 *>(base + S.wkey_off);
+        unsigned grp[R];
+        bool live[R];
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            cell[u] = -1;
+            live[u] = valid[u];
+            grp[u] = (unsigned)((tag[u] * 0x9E3779B97F4A7C15ull) >> S.slot_shift) & gmask;
+        }
+        for (;;) {
+            uint64_t k[R][GS];
+            asm volatile("" ::: "memory"); // re-read the cells every round (other waves publish)
+#pragma unroll
+            for (int u = 0; u < R; ++u)
+                if (live[u]) {
+                    const uint4 a = *reinterpret_cast<const uint4 *>(&keys[grp[u] * GS]);
+                    const uint4 b = *reinterpret_cast<const uint4 *>(&keys[grp[u] * GS + 2]);
+                    k[u][0] = ((uint64_t)a.y << 32) | a.x;
+                    k[u][1] = ((uint64_t)a.w << 32) | a.z;
+                    k[u][2] = ((uint64_t)b.y << 32) | b.x;
+                    k[u][3] = ((uint64_t)b.w << 32) | b.z;
+                }
+            bool any = false;
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                if (!live[u]) continue;
+                int hit = -1, empty = -1;
+                bool pend = false;
+#pragma unroll
+                for (int s = 0; s < GS; ++s) {
+                    if (empty >= 0 || hit >= 0 || pend) continue;
+                    const uint64_t st = k[u][s];
+                    if (st == 0) {
+                        empty = s;
+                    } else if ((st | 1ull) == (tag[u] | 1ull)) {
+                        if (!(st & 1ull)) {
+                            pend = true;
+                        } else {
+                            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                            const uint4 q = wk[grp[u] * GS + s];
+                            if ((((uint64_t)q.y << 32) | q.x) == lo[u] && (((uint64_t)q.w << 32) | q.z) == hi[u]) hit = s;
+                        }
+                    }
+                }
+                if (hit >= 0) {
+                    cell[u] = (int)(grp[u] * GS + hit);
+                    live[u] = false;
+                } else if (pend) {
+                    any = true; // a same-tag key is being published: re-read this group
+                } else if (empty >= 0) {
+                    if (!may_insert) {
+                        live[u] = false;
+                        continue;
+                    }
+                    if (!force && __hip_atomic_load(&ctrl->full, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                        live[u] = false;
+                        continue;
+                    }
+                    const int c = (int)(grp[u] * GS + empty);
+                    const uint64_t old = atomicCAS((unsigned long long *)&keys[c], 0ull, (unsigned long long)tag[u]);
+                    if (old == 0) {
+                        uint4 q;
+                        q.x = (unsigned)lo[u];
+                        q.y = (unsigned)(lo[u] >> 32);
+                        q.z = (unsigned)hi[u];
+                        q.w = (unsigned)(hi[u] >> 32);
+                        wk[c] = q;
+                        __hip_atomic_store((unsigned long long *)&keys[c], (unsigned long long)(tag[u] | 1ull),
+                                           __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        const unsigned n = atomicAdd(&ctrl->used, 1u) + 1;
+                        if (n >= (unsigned)S.maxfill) ctrl->full = 1;
+                        cell[u] = c;
+                        live[u] = false;
+                    } else {
+                        any = true; // raced: re-read the group
+                    }
+                } else {
+                    grp[u] = (grp[u] + 1) & gmask;
+                    any = true;
+                }
+            }
+            if (!any) break;
+        }
+    }
+
     __device__ __forceinline__ uint64_t *acc_cell(int i, int cell) const {
         const int w = S.acc[i] == ACC_I128 ? 2 : 1;
         return reinterpret_cast<uint64_t *>(base + S.acc_off[i]) + (int64_t)cell * w;
@@ -344,7 +454,11 @@ struct Table {
             }
             if (!occ) continue;
             const uint64_t pos = out_base + atomicAdd(&ctrl->out_count, 1ull);
-            out.key[pos] = key;
+            if (S.wkey_off) { // wide: the cell's 16-byte key (tags never take the side slots)
+                reinterpret_cast<uint4 *>(out.key)[pos] = reinterpret_cast<const uint4 *>(base + S.wkey_off)[c];
+            } else {
+                out.key[pos] = key;
+            }
             out.key_null[pos] = isnull;
             for (int i = 0; i < S.n_aggs; ++i) {
                 if (S.acc[i] == ACC_I128) {
@@ -374,7 +488,7 @@ __device__ __forceinline__ int val_width(const AggSpec &S, int mode, int i) {
 
 template <int NA>
 __device__ __forceinline__ void load_row(const AggSpec &S, const RowsIO &rows, int mode, int64_t r, RowValT<NA> &v) {
-    v.key = load_bits(rows.key, rows.key_width, r);
+    if (rows.key_width != 16) v.key = load_bits(rows.key, rows.key_width, r); // wide keys: WideOps
     v.knull = rows.key_null ? rows.key_null[r] : 0;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
@@ -400,6 +514,7 @@ __device__ __forceinline__ void store_row(const AggSpec &S, const RowsIO &rows, 
     case 1: ((uint8_t *)rows.key)[w] = (uint8_t)v.key; break;
     case 2: ((uint16_t *)rows.key)[w] = (uint16_t)v.key; break;
     case 4: ((uint32_t *)rows.key)[w] = (uint32_t)v.key; break;
+    case 16: break; // wide keys: WideOps
     default: ((uint64_t *)rows.key)[w] = v.key; break;
     }
     if (rows.key_null) rows.key_null[w] = v.knull;
@@ -437,6 +552,8 @@ constexpr int RPT = 4;
 // wave-instructions per 64 rows (measured with SQ_INSTS_VALU / SQ_INSTS_SALU).
 template <int NA> struct GenericOps {
     using Row = RowValT<NA>;
+    static constexpr bool WIDE = false;
+    __device__ __forceinline__ uint64_t hi(const Row &) const { return 0; }
     const AggSpec &S;
     int mode;
     __device__ __forceinline__ void load(const RowsIO &rows, int64_t r, Row &v) const { load_row<NA>(S, rows, mode, r, v); }
@@ -451,6 +568,7 @@ template <int A0, int A1, int A2> struct FastOps {
     // rows are staged as interleaved records: key, then one word per summed argument
     static constexpr int op(int i) { return i == 0 ? A0 : (i == 1 ? A1 : A2); }
     static constexpr int NCOL = 1 + (A0 >= 2) + (A1 >= 2) + (A2 >= 2);
+    static constexpr bool WIDE = false;
     static constexpr int pos(int i) { return 1 + (i > 0 && A0 >= 2) + (i > 1 && A1 >= 2); }
     struct Row {
         uint64_t key;
@@ -476,6 +594,7 @@ template <int A0, int A1, int A2> struct FastOps {
     }
     __device__ __forceinline__ uint64_t key(const Row &v) const { return v.key; }
     __device__ __forceinline__ bool knull(const Row &) const { return false; }
+    __device__ __forceinline__ uint64_t hi(const Row &) const { return 0; }
     __device__ __forceinline__ void add(Table &T, int cell, const Row &v) const {
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
@@ -493,6 +612,37 @@ template <int A0, int A1, int A2> struct FastOps {
             if (op(i) >= 2) rec[pos(i)] = v.v[i];
     }
     __device__ __forceinline__ uint64_t probe_val(const Row &v) const { return v.v[0]; }
+};
+
+// Wide keys (16-byte packed keys128 / String keys, staged as one uint4 per row): generic
+// value handling, the key's two words travel in Row::key and Row::hi.
+template <int NA> struct WideOps {
+    struct Row : RowValT<NA> {
+        uint64_t khi;
+    };
+    static constexpr bool WIDE = true;
+    const AggSpec &S;
+    int mode;
+    __device__ __forceinline__ void load(const RowsIO &rows, int64_t r, Row &v) const {
+        load_row<NA>(S, rows, mode, r, v);
+        const uint4 q = reinterpret_cast<const uint4 *>(rows.key)[r];
+        v.key = ((uint64_t)q.y << 32) | q.x;
+        v.khi = ((uint64_t)q.w << 32) | q.z;
+    }
+    __device__ __forceinline__ uint64_t key(const Row &v) const { return v.key; }
+    __device__ __forceinline__ uint64_t hi(const Row &v) const { return v.khi; }
+    __device__ __forceinline__ bool knull(const Row &) const { return false; }
+    __device__ __forceinline__ void add(Table &T, int cell, const Row &v) const { T.add_row<NA>(cell, v, mode); }
+    __device__ __forceinline__ void store(const RowsIO &sp, int64_t w, const Row &v) const {
+        store_row<NA>(S, sp, mode, w, v);
+        uint4 q;
+        q.x = (unsigned)v.key;
+        q.y = (unsigned)(v.key >> 32);
+        q.z = (unsigned)v.khi;
+        q.w = (unsigned)(v.khi >> 32);
+        reinterpret_cast<uint4 *>(sp.key)[w] = q;
+    }
+    __device__ __forceinline__ uint64_t probe_val(const Row &v) const { return v.lo[0]; }
 };
 
 template <typename Ops, int BT>
@@ -524,7 +674,17 @@ __global__ void __launch_bounds__(BT) agg_bucket_kernel(AggSpec S, RowsIO rows0,
         int64_t take = oe - old_cursor;
         if (take > S.maxfill) take = S.maxfill;
         for (int64_t g = old_cursor + threadIdx.x; g < old_cursor + take; g += BT) {
-            const int cell = T.find_or_insert(old.key[g], old.key_null[g] != 0, true, true);
+            int cell;
+            if constexpr (Ops::WIDE) {
+                const uint64_t lo[1] = {old.key[2 * g]}, hi[1] = {old.key[2 * g + 1]};
+                const uint64_t tg[1] = {wide_tag(lo[0], hi[0])};
+                const bool ok[1] = {true};
+                int c1[1];
+                T.find_wide_multi<1>(lo, hi, tg, ok, true, c1, true);
+                cell = c1[0];
+            } else {
+                cell = T.find_or_insert(old.key[g], old.key_null[g] != 0, true, true);
+            }
             T.add_group(cell, old, g);
         }
         old_cursor += take;
@@ -554,7 +714,17 @@ __global__ void __launch_bounds__(BT) agg_bucket_kernel(AggSpec S, RowsIO rows0,
                     if (vu[u] && ku[u] == 0x5555555555555555ull) T.ctrl->out_count += ops.probe_val(v[u]);
                 continue;
             }
-            T.find_or_insert_multi<RPT>(ku, nu, vu, allow_insert, cells);
+            uint64_t kh[RPT], tg[RPT];
+            if constexpr (Ops::WIDE) {
+#pragma unroll
+                for (int u = 0; u < RPT; ++u) {
+                    kh[u] = ops.hi(v[u]);
+                    tg[u] = wide_tag(ku[u], kh[u]);
+                }
+                T.find_wide_multi<RPT>(ku, kh, tg, vu, allow_insert, cells);
+            } else {
+                T.find_or_insert_multi<RPT>(ku, nu, vu, allow_insert, cells);
+            }
 #pragma unroll
             for (int u = 0; u < RPT; ++u) {
                 miss[u] = false;
@@ -569,7 +739,16 @@ __global__ void __launch_bounds__(BT) agg_bucket_kernel(AggSpec S, RowsIO rows0,
 #pragma unroll
             for (int u = 0; u < RPT; ++u) {
                 if (!miss[u]) continue;
-                const int cell = T.find_or_insert(ku[u], nu[u], false, false);
+                int cell;
+                if constexpr (Ops::WIDE) {
+                    const uint64_t lo[1] = {ku[u]}, hi[1] = {kh[u]}, t1[1] = {tg[u]};
+                    const bool ok[1] = {true};
+                    int c1[1];
+                    T.find_wide_multi<1>(lo, hi, t1, ok, false, c1);
+                    cell = c1[0];
+                } else {
+                    cell = T.find_or_insert(ku[u], nu[u], false, false);
+                }
                 if (cell >= 0) {
                     ops.add(T, cell, v[u]);
                 } else {
@@ -595,7 +774,8 @@ __global__ void agg_compact_kernel(AggSpec S, GroupsIO tmp, const uint64_t *stag
     const uint64_t d0 = new_off[b], cnt = new_off[b + 1] - d0;
     for (uint64_t j = threadIdx.x; j < cnt; j += blockDim.x) {
         const uint64_t s = src0 + j, d = d0 + j;
-        dst.key[d] = tmp.key[s];
+        if (S.key_width == 16) reinterpret_cast<uint4 *>(dst.key)[d] = reinterpret_cast<const uint4 *>(tmp.key)[s];
+        else dst.key[d] = tmp.key[s];
         dst.key_null[d] = tmp.key_null[s];
         for (int i = 0; i < S.n_aggs; ++i) {
             if (S.acc[i] == ACC_I128) ((uint4 *)dst.acc[i])[d] = ((const uint4 *)tmp.acc[i])[s];
@@ -681,12 +861,13 @@ __global__ void agg_result_kernel(AggSpec S, GroupsIO st, uint64_t n, int key_wi
                                   uint8_t *out_key_null, ResultPtrs res) {
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (uint64_t)gridDim.x * blockDim.x) {
         if (out_keys) {
-            const uint64_t k = st.key[g];
+            const uint64_t k = key_width == 16 ? 0 : st.key[g];
             switch (key_width) {
             case 1: ((uint8_t *)out_keys)[g] = (uint8_t)k; break;
             case 2: ((uint16_t *)out_keys)[g] = (uint16_t)k; break;
             case 4: ((uint32_t *)out_keys)[g] = (uint32_t)k; break;
             case 8: ((uint64_t *)out_keys)[g] = k; break;
+            case 16: ((uint4 *)out_keys)[g] = reinterpret_cast<const uint4 *>(st.key)[g]; break;
             default: break;
             }
         }
@@ -748,6 +929,142 @@ struct SelBucket8 {
     __device__ __forceinline__ uint32_t operator()(const uint32_t (*t)[256], int64_t r) const { return part(t, load(r), r); }
 };
 
+// wide keys: the radix of the key's tag (the bucket kernel derives the slot from the same product)
+struct SelWide {
+    const uint4 *key;
+    uint32_t shift;
+    static constexpr bool needs_crc = false;
+    static constexpr bool fib_radix = false;
+    __device__ __forceinline__ Loaded load(int64_t r) const {
+        const uint4 q = key[r];
+        return Loaded{wide_tag(((uint64_t)q.y << 32) | q.x, ((uint64_t)q.w << 32) | q.z), 0u};
+    }
+    __device__ __forceinline__ uint32_t part(const uint32_t (*)[256], const Loaded &l, int64_t) const {
+        return fib_part(l.bits, shift);
+    }
+    __device__ __forceinline__ uint32_t operator()(const uint32_t (*t)[256], int64_t r) const { return part(t, load(r), r); }
+};
+
+// ---------------------------------------------------------------- wide-key packing
+// keys128 (Aggregator.cpp:394-537 chooses keys128 / nullable_keys128 for several fixed keys of
+// <= 16 bytes, packing them with packFixed, Common/ColumnsHashing.h:324-480) and key_string
+// (HashMethodString, ColumnsHashing.h:179-241: the key is the collator's sort key of the row)
+// become one 16-byte key:
+//   fixed keys: the columns' little-endian bytes at consecutive offsets; when the sum of the
+//               widths is <= 15, byte 15 holds the NULL bit of each nullable key (its value
+//               bytes are then zero), like nullable_keys128's bitmap;
+//   String:     the sort-key bytes (<= 15), zero padded, with byte 15 = length; NULL = 0x80.
+constexpr int WK_FIXED = 1, WK_STRING = 2;
+struct KeyPack {
+    int kind;
+    int nkeys;
+    int width[4];
+    int off[4];
+    const void *col[4];
+    const uint8_t *nullmap[4];
+    const uint64_t *offsets; // String
+    int collator;
+};
+
+__global__ void pack_keys_kernel(KeyPack kp, int64_t n, uint4 *out, unsigned *err) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t w[2] = {0, 0};
+        if (kp.kind == WK_STRING) {
+            if (kp.nullmap[0] && kp.nullmap[0][r]) {
+                w[1] = 0x80ull << 56;
+            } else {
+                const uint64_t s = r ? kp.offsets[r - 1] : 0, e = kp.offsets[r];
+                const uint8_t *c = (const uint8_t *)kp.col[0] + s;
+                int64_t len = (int64_t)(e - s) - 1; // ColumnString rows end with '\0'
+                if (kp.collator == TFG_COLLATOR_BIN_PADDING)
+                    while (len > 0 && c[len - 1] == ' ') --len; // BinCollatorSortKey<true>: right-trim
+                if (len > 15) {
+                    atomicOr(err, 1u);
+                    len = 15;
+                }
+                for (int i = 0; i < (int)len; ++i) w[i >> 3] |= (uint64_t)c[i] << ((i & 7) * 8);
+                w[1] |= (uint64_t)len << 56;
+            }
+        } else {
+            uint64_t nb = 0;
+            for (int j = 0; j < kp.nkeys; ++j) {
+                if (kp.nullmap[j] && kp.nullmap[j][r]) {
+                    nb |= 1ull << j;
+                    continue;
+                }
+                const int wd = kp.width[j], o = kp.off[j];
+                uint64_t lo = 0, hi = 0;
+                if (wd == 16) {
+                    lo = ((const uint64_t *)kp.col[j])[2 * r];
+                    hi = ((const uint64_t *)kp.col[j])[2 * r + 1];
+                } else {
+                    lo = load_bits(kp.col[j], wd, r);
+                }
+                // place wd bytes at byte offset o
+                if (o < 8) {
+                    w[0] |= lo << (o * 8);
+                    if (o > 0) w[1] |= lo >> ((8 - o) * 8);
+                    if (wd == 16) w[1] |= hi << (o * 8);
+                } else {
+                    w[1] |= lo << ((o - 8) * 8);
+                }
+            }
+            if (nb) w[1] |= nb << 56;
+        }
+        uint4 q;
+        q.x = (unsigned)w[0];
+        q.y = (unsigned)(w[0] >> 32);
+        q.z = (unsigned)w[1];
+        q.w = (unsigned)(w[1] >> 32);
+        out[r] = q;
+    }
+}
+
+// packed String keys -> lengths + 1 (the '\0' each ColumnString row ends with)
+__global__ void wide_str_len_kernel(const uint4 *keys, uint64_t n, uint64_t *len1) {
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (uint64_t)gridDim.x * blockDim.x)
+        len1[g] = ((keys[g].w >> 24) & 0x7Fu) + 1;
+}
+
+// packed keys -> the key columns of the result Block (convertToBlockImplFinal's insertKeyIntoColumns)
+struct KeyOut {
+    void *col[4];
+    uint64_t *offsets;        // String: end offsets
+    uint8_t *nullmap[4];
+};
+__global__ void unpack_keys_kernel(KeyPack kp, const uint4 *keys, const uint64_t *start, uint64_t n, KeyOut ko) {
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 q = keys[g];
+        const uint64_t w[2] = {((uint64_t)q.y << 32) | q.x, ((uint64_t)q.w << 32) | q.z};
+        if (kp.kind == WK_STRING) {
+            const int len = (int)((w[1] >> 56) & 0x7F);
+            const uint64_t s = start[g];
+            uint8_t *c = (uint8_t *)ko.col[0] + s;
+            for (int i = 0; i < len; ++i) c[i] = (uint8_t)(w[i >> 3] >> ((i & 7) * 8));
+            c[len] = 0;
+            ko.offsets[g] = s + len + 1;
+            if (ko.nullmap[0]) ko.nullmap[0][g] = (w[1] >> 63) ? 1 : 0;
+            continue;
+        }
+        const uint64_t nb = kp.off[kp.nkeys - 1] + kp.width[kp.nkeys - 1] <= 15 ? (w[1] >> 56) : 0;
+        for (int j = 0; j < kp.nkeys; ++j) {
+            const int wd = kp.width[j], o = kp.off[j];
+            if (ko.nullmap[j]) ko.nullmap[j][g] = (nb >> j) & 1;
+            if (!ko.col[j]) continue;
+            uint64_t lo = o < 8 ? (w[0] >> (o * 8)) | (o > 0 ? w[1] << ((8 - o) * 8) : 0) : w[1] >> ((o - 8) * 8);
+            switch (wd) {
+            case 1: ((uint8_t *)ko.col[j])[g] = (uint8_t)lo; break;
+            case 2: ((uint16_t *)ko.col[j])[g] = (uint16_t)lo; break;
+            case 4: ((uint32_t *)ko.col[j])[g] = (uint32_t)lo; break;
+            case 8: ((uint64_t *)ko.col[j])[g] = lo; break;
+            default: // 16: a single Decimal128 / Int128 key at offset 0
+                ((uint64_t *)ko.col[j])[2 * g] = w[0];
+                ((uint64_t *)ko.col[j])[2 * g + 1] = w[1];
+            }
+        }
+    }
+}
+
 } // namespace tfg
 
 using namespace tfg;
@@ -769,9 +1086,28 @@ struct tfg_agg {
     GroupsIO st[2];
     uint64_t *bucket_off[2] = {nullptr, nullptr};
     int cur = 0;
+    // wide keys (keys128 / key_string): key_type == TFG_KEYS_WIDE, packing spec, and a device
+    // buffer holding the packed keys of the block being consumed / the result being written
+    KeyPack kp{};
+    int key_types[4] = {};
+    void *pack_buf = nullptr;
+    size_t pack_cap = 0;
+    unsigned *pack_err = nullptr;
+    int ensure_pack(size_t rows) {
+        if (pack_cap >= rows && pack_buf) return TFG_OK;
+        if (pack_buf) {
+            TFG_HIP(hipStreamSynchronize(ctx->stream));
+            TFG_HIP(hipFree(pack_buf));
+            pack_buf = nullptr;
+        }
+        const size_t nc = std::max<size_t>(rows + rows / 4, 4096);
+        TFG_HIP(hipMalloc(&pack_buf, nc * 16));
+        pack_cap = nc;
+        return TFG_OK;
+    }
 
     size_t group_bytes() const {
-        size_t b = 8 + 1;
+        size_t b = (S.key_width == 16 ? 16 : 8) + 1;
         for (int i = 0; i < S.n_aggs; ++i) {
             if (S.acc[i] == ACC_I128) b += 16;
             else if (S.acc[i] != ACC_NONE) b += 8;
@@ -782,7 +1118,7 @@ struct tfg_agg {
     // carve a GroupsIO of `n` groups out of `base` (returns bytes used)
     size_t carve_groups(char *base, size_t n, GroupsIO &g) const {
         Carver cv;
-        size_t ok = cv.take<uint64_t>(n), on = cv.take<uint8_t>(n);
+        size_t ok = cv.take<uint64_t>(S.key_width == 16 ? 2 * n : n), on = cv.take<uint8_t>(n);
         size_t oa[AGG_MAX] = {}, oc[AGG_MAX] = {};
         for (int i = 0; i < S.n_aggs; ++i) {
             if (S.acc[i] == ACC_I128) oa[i] = cv.take<uint4>(n);
@@ -863,7 +1199,7 @@ int consume_keyed(tfg_agg *a, int mode, const RowPred &pred, const void *keys, i
     for (int c = fast; c > 0; c /= 10) rec_words += (c % 10) >= 2;
     // ---- scratch layout
     Carver cv;
-    const size_t o_key = cv.take<uint64_t>(n * (fast ? rec_words : 1)), o_knull = cv.take<uint8_t>(n);
+    const size_t o_key = cv.take<uint64_t>(n * (fast ? rec_words : key_width == 16 ? 2 : 1)), o_knull = cv.take<uint8_t>(n);
     size_t o_val[AGG_MAX] = {}, o_vnull[AGG_MAX] = {}, o_vcnt[AGG_MAX] = {};
     int vw[AGG_MAX] = {};
     for (int i = 0; i < S.n_aggs && !fast; ++i) {
@@ -953,10 +1289,17 @@ int consume_keyed(tfg_agg *a, int mode, const RowPred &pred, const void *keys, i
             }
         }
         TFG_CHECK(pc.ncols <= PCOLS, TFG_ERR_NOT_IMPLEMENTED, "too many aggregate columns");
-        SelBucket sel{keys, key_null, key_width, fib_shift(B)};
-        if (int rc = run_partition<SelBucket, false>(ctx, sel, pred, L, pc, nullptr, nullptr, stage_off, sb + o_part,
-                                                      "agg.part.hist", "agg.part.scatter"))
-            return rc;
+        if (key_width == 16) {
+            SelWide sel{(const uint4 *)keys, fib_shift(B)};
+            if (int rc = run_partition<SelWide, false>(ctx, sel, pred, L, pc, nullptr, nullptr, stage_off, sb + o_part,
+                                                        "agg.part.hist", "agg.part.scatter"))
+                return rc;
+        } else {
+            SelBucket sel{keys, key_null, key_width, fib_shift(B)};
+            if (int rc = run_partition<SelBucket, false>(ctx, sel, pred, L, pc, nullptr, nullptr, stage_off,
+                                                          sb + o_part, "agg.part.hist", "agg.part.scatter"))
+                return rc;
+        }
     }
     // ---- bucket kernel
     GroupsIO tmp{};
@@ -990,6 +1333,15 @@ int consume_keyed(tfg_agg *a, int mode, const RowPred &pred, const void *keys, i
         case 331: TFG_BUCKET(FastOps<3, 3, 1>); break;
         case 441: TFG_BUCKET(FastOps<4, 4, 1>); break;
         default:
+            if (key_width == 16) {
+                switch (S.n_aggs) {
+                case 1: TFG_BUCKET(WideOps<1>); break;
+                case 2: TFG_BUCKET(WideOps<2>); break;
+                case 3: TFG_BUCKET(WideOps<3>); break;
+                default: TFG_BUCKET(WideOps<4>); break;
+                }
+                break;
+            }
             switch (S.n_aggs) {
             case 1: TFG_BUCKET(GenericOps<1>); break;
             case 2: TFG_BUCKET(GenericOps<2>); break;
@@ -1063,8 +1415,8 @@ int consume_common(tfg_agg *a, int mode, const RowPred &pred, const void *keys, 
     }
     if (a->nokey) return consume_nokey(a, mode, pred, vals, vnull, n);
     TFG_CHECK(keys, TFG_ERR_INVALID_ARG, "keys are null");
-    return consume_keyed(a, mode, pred, keys, (int)type_width(a->key_type), key_nullmap, vals, vnull, nullptr, nullptr,
-                         n);
+    if (a->S.key_width == 16) TFG_CHECK(!key_nullmap, TFG_ERR_INVALID_ARG, "packed keys carry their NULL bits");
+    return consume_keyed(a, mode, pred, keys, a->S.key_width, key_nullmap, vals, vnull, nullptr, nullptr, n);
 }
 
 } // namespace
@@ -1075,17 +1427,18 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
                    const int *arg_scales, const tfg_agg_params *params, tfg_agg **out) {
     TFG_CHECK(ctx && out && agg_kinds, TFG_ERR_INVALID_ARG, "null argument");
     TFG_CHECK(n_aggs >= 1 && n_aggs <= AGG_MAX, TFG_ERR_NOT_IMPLEMENTED, "n_aggs %d out of range [1,%d]", n_aggs, AGG_MAX);
-    TFG_CHECK(key_type == 0 || (type_width(key_type) > 0 && type_width(key_type) <= 8), TFG_ERR_ILLEGAL_TYPE,
-              "unsupported GROUP BY key type %d", key_type);
+    TFG_CHECK(key_type == 0 || key_type == TFG_KEYS128 || (type_width(key_type) > 0 && type_width(key_type) <= 8),
+              TFG_ERR_ILLEGAL_TYPE, "unsupported GROUP BY key type %d", key_type);
     if (int rc = set_device(ctx)) return rc;
     tfg_agg *a = new tfg_agg();
     a->ctx = ctx;
     a->key_type = key_type;
     a->nokey = key_type == 0;
     AggSpec &S = a->S;
-    S.key_width = (int)type_width(key_type);
+    const bool wide = key_type == TFG_KEYS128;
+    S.key_width = wide ? 16 : (int)type_width(key_type);
     S.n_aggs = n_aggs;
-    int cell = 8;
+    int cell = wide ? 24 : 8; // key (wide: tag + 16-byte key)
     for (int i = 0; i < n_aggs; ++i) {
         const int kind = agg_kinds[i];
         const int at = arg_types ? (arg_types[i] & 0xFF) : 0;
@@ -1143,6 +1496,10 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
         S.slot_shift = 64 - (a->nokey ? 0 : bbits) - gbits;
     }
     int off = (cap + 2) * 8;
+    if (wide) {
+        S.wkey_off = off;
+        off += cap * 16;
+    }
     for (int i = 0; i < n_aggs; ++i) {
         if (S.acc[i] != ACC_NONE) {
             S.acc_off[i] = off;
@@ -1180,6 +1537,8 @@ int tfg_agg_destroy(tfg_agg *a) {
         if (a->blk[i]) (void)hipFree(a->blk[i]);
         if (a->bucket_off[i]) (void)hipFree(a->bucket_off[i]);
     }
+    if (a->pack_buf) (void)hipFree(a->pack_buf);
+    if (a->pack_err) (void)hipFree(a->pack_err);
     delete a;
     return TFG_OK;
 }
@@ -1254,7 +1613,8 @@ int tfg_agg_merge(tfg_agg *dst, tfg_agg *src) {
         cnts[i] = g.cnt[i];
     }
     RowPred pred{};
-    return consume_keyed(dst, MODE_STATE, pred, g.key, 8, g.key_null, vals, nullptr, cnts, src->bucket_off[src->cur],
+    return consume_keyed(dst, MODE_STATE, pred, g.key, dst->S.key_width == 16 ? 16 : 8, g.key_null, vals, nullptr, cnts,
+                         src->bucket_off[src->cur],
                          (int64_t)src->n_groups);
 }
 
@@ -1287,6 +1647,162 @@ int tfg_agg_result(tfg_agg *a, void *out_keys, uint8_t *out_key_nullmap, void *c
     hipLaunchKernelGGL(agg_result_kernel, dim3(stream_grid((int64_t)a->n_groups, 256, 4096)), dim3(256), 0,
                        a->ctx->stream, a->S, a->st[a->cur], a->n_groups, a->S.key_width,
                        a->nokey ? nullptr : out_keys, out_key_nullmap, rp);
+    }
+    TFG_LAUNCH_CHECK();
+    return TFG_OK;
+}
+
+
+// ---------------------------------------------------------------- wide keys: keys128 / key_string
+static int pack_keys(tfg_agg *a, const void *const *key_cols, const uint64_t *const *key_offsets,
+                     const uint8_t *const *key_nullmaps, int64_t n) {
+    TFG_CHECK(key_cols, TFG_ERR_INVALID_ARG, "key columns are null");
+    KeyPack kp = a->kp;
+    for (int j = 0; j < kp.nkeys; ++j) {
+        TFG_CHECK(key_cols[j], TFG_ERR_INVALID_ARG, "key column %d is null", j);
+        kp.col[j] = key_cols[j];
+        kp.nullmap[j] = key_nullmaps ? key_nullmaps[j] : nullptr;
+        if (kp.nullmap[j] && kp.kind == WK_FIXED)
+            TFG_CHECK(kp.off[kp.nkeys - 1] + kp.width[kp.nkeys - 1] <= 15, TFG_ERR_NOT_IMPLEMENTED,
+                      "nullable keys need a spare byte of the 16-byte packed key (nullable_keys256 not supported)");
+    }
+    if (kp.kind == WK_STRING) {
+        TFG_CHECK(key_offsets && key_offsets[0], TFG_ERR_INVALID_ARG, "String key needs its offsets");
+        kp.offsets = key_offsets[0];
+    }
+    if (int rc = a->ensure_pack((size_t)n)) return rc;
+    if (!a->pack_err) TFG_HIP(hipMalloc(&a->pack_err, sizeof(unsigned)));
+    TFG_HIP(hipMemsetAsync(a->pack_err, 0, sizeof(unsigned), a->ctx->stream));
+    {
+        ProfScope _ps(a->ctx, "agg.pack_keys");
+        hipLaunchKernelGGL(pack_keys_kernel, dim3(stream_grid(n, 256 * 4, 8192)), dim3(256), 0, a->ctx->stream, kp, n,
+                           (uint4 *)a->pack_buf, a->pack_err);
+    }
+    TFG_LAUNCH_CHECK();
+    if (kp.kind == WK_STRING) {
+        unsigned err = 0;
+        TFG_HIP(hipMemcpyAsync(&err, a->pack_err, sizeof(unsigned), hipMemcpyDeviceToHost, a->ctx->stream));
+        TFG_HIP(hipStreamSynchronize(a->ctx->stream));
+        TFG_CHECK(!err, TFG_ERR_NOT_IMPLEMENTED,
+                  "String GROUP BY key longer than 15 bytes (after the collator's sort key): not supported");
+    }
+    return TFG_OK;
+}
+
+int tfg_agg_create_keys(tfg_ctx *ctx, int nkeys, const int *key_types, const int *key_collators, int n_aggs,
+                        const int *agg_kinds, const int *arg_types, const int *arg_scales, const tfg_agg_params *params,
+                        tfg_agg **out) {
+    TFG_CHECK(ctx && out && key_types, TFG_ERR_INVALID_ARG, "null argument");
+    TFG_CHECK(nkeys >= 1 && nkeys <= 4, TFG_ERR_NOT_IMPLEMENTED, "%d GROUP BY keys: 1-4 supported", nkeys);
+    KeyPack kp{};
+    kp.nkeys = nkeys;
+    if (nkeys == 1 && key_types[0] != TFG_STRING)
+        return tfg_agg_create(ctx, key_types[0], n_aggs, agg_kinds, arg_types, arg_scales, params, out);
+    if (key_types[0] == TFG_STRING) {
+        TFG_CHECK(nkeys == 1, TFG_ERR_NOT_IMPLEMENTED, "String keys combined with other keys (serialized method)");
+        kp.kind = WK_STRING;
+        kp.collator = key_collators ? key_collators[0] : TFG_COLLATOR_NONE;
+        TFG_CHECK(kp.collator >= TFG_COLLATOR_NONE && kp.collator <= TFG_COLLATOR_BIN_PADDING, TFG_ERR_NOT_IMPLEMENTED,
+                  "collator %d not supported", kp.collator);
+    } else {
+        kp.kind = WK_FIXED;
+        int off = 0;
+        for (int j = 0; j < nkeys; ++j) {
+            const int t = key_types[j];
+            TFG_CHECK(t != TFG_STRING && type_width(t) > 0, TFG_ERR_ILLEGAL_TYPE,
+                      "GROUP BY key %d of type %d cannot be packed", j, t); // floats: raw bits, like packFixed
+            kp.width[j] = (int)type_width(t);
+            kp.off[j] = off;
+            off += kp.width[j];
+        }
+        TFG_CHECK(off <= 16, TFG_ERR_NOT_IMPLEMENTED, "fixed keys of %d bytes exceed keys128", off);
+        TFG_CHECK(kp.width[0] == 16 ? nkeys == 1 : true, TFG_ERR_NOT_IMPLEMENTED, "Decimal128 key with other keys");
+    }
+    tfg_agg_params p{};
+    if (params) p = *params;
+    if (int rc = tfg_agg_create(ctx, TFG_KEYS128, n_aggs, agg_kinds, arg_types, arg_scales, &p, out)) return rc;
+    (*out)->kp = kp;
+    for (int j = 0; j < nkeys; ++j) (*out)->key_types[j] = key_types[j];
+    return TFG_OK;
+}
+
+int tfg_agg_consume_keys(tfg_agg *a, const void *const *key_cols, const uint64_t *const *key_offsets,
+                         const uint8_t *const *key_nullmaps, const void *const *args, const uint8_t *const *arg_nullmaps,
+                         const uint8_t *mask, int64_t n) {
+    TFG_CHECK(a, TFG_ERR_INVALID_ARG, "agg is null");
+    if (!a->kp.kind)
+        return tfg_agg_consume(a, key_cols ? key_cols[0] : nullptr, key_nullmaps ? key_nullmaps[0] : nullptr, args,
+                               arg_nullmaps, mask, n);
+    if (n <= 0) return n == 0 ? TFG_OK : fail(TFG_ERR_INVALID_ARG, "negative row count");
+    if (int rc = set_device(a->ctx)) return rc;
+    if (int rc = pack_keys(a, key_cols, key_offsets, key_nullmaps, n)) return rc;
+    return tfg_agg_consume(a, a->pack_buf, nullptr, args, arg_nullmaps, mask, n);
+}
+
+int tfg_agg_consume_partial_keys(tfg_agg *a, const void *const *key_cols, const uint64_t *const *key_offsets,
+                                 const uint8_t *const *key_nullmaps, const void *const *states,
+                                 const uint8_t *const *state_nullmaps, int64_t n) {
+    TFG_CHECK(a, TFG_ERR_INVALID_ARG, "agg is null");
+    if (!a->kp.kind)
+        return tfg_agg_consume_partial(a, key_cols ? key_cols[0] : nullptr, key_nullmaps ? key_nullmaps[0] : nullptr,
+                                       states, state_nullmaps, n);
+    if (n <= 0) return n == 0 ? TFG_OK : fail(TFG_ERR_INVALID_ARG, "negative row count");
+    if (int rc = set_device(a->ctx)) return rc;
+    if (int rc = pack_keys(a, key_cols, key_offsets, key_nullmaps, n)) return rc;
+    return tfg_agg_consume_partial(a, a->pack_buf, nullptr, states, state_nullmaps, n);
+}
+
+int tfg_agg_result_keys(tfg_agg *a, void *const *out_key_cols, uint64_t *const *out_key_offsets,
+                        uint8_t *const *out_key_nullmaps, void *const *out_states, uint8_t *const *out_state_nullmaps,
+                        uint64_t capacity, uint64_t chars_capacity, uint64_t *out_groups_host, uint64_t *out_chars_host) {
+    TFG_CHECK(a, TFG_ERR_INVALID_ARG, "agg is null");
+    if (!a->kp.kind) {
+        if (out_chars_host) *out_chars_host = 0;
+        return tfg_agg_result(a, out_key_cols ? out_key_cols[0] : nullptr, out_key_nullmaps ? out_key_nullmaps[0] : nullptr,
+                              out_states, out_state_nullmaps, capacity, out_groups_host);
+    }
+    const uint64_t G = a->n_groups;
+    if (out_groups_host) *out_groups_host = G;
+    if (out_chars_host) *out_chars_host = 0;
+    if (G > capacity)
+        return fail(TFG_ERR_CAPACITY, "result needs %llu groups, capacity %llu", (unsigned long long)G,
+                    (unsigned long long)capacity);
+    if (G == 0) return TFG_OK;
+    if (int rc = set_device(a->ctx)) return rc;
+    if (int rc = a->ensure_pack(G)) return rc;
+    if (int rc = tfg_agg_result(a, a->pack_buf, nullptr, out_states, out_state_nullmaps, capacity, nullptr)) return rc;
+    Ctx *ctx = a->ctx;
+    KeyOut ko{};
+    uint64_t *start = nullptr;
+    const unsigned grid = stream_grid((int64_t)G, 256, 4096);
+    if (a->kp.kind == WK_STRING) {
+        TFG_CHECK(out_key_cols && out_key_cols[0] && out_key_offsets && out_key_offsets[0], TFG_ERR_INVALID_ARG,
+                  "String result needs chars and offsets");
+        Carver cv;
+        const size_t o_len = cv.take<uint64_t>(G), o_start = cv.take<uint64_t>(G + 1), o_tmp = cv.take<uint8_t>(scan_tmp_bytes(G));
+        void *sp;
+        if (int rc = scratch_get(ctx, cv.off, &sp)) return rc;
+        uint64_t *len1 = (uint64_t *)((char *)sp + o_len);
+        start = (uint64_t *)((char *)sp + o_start);
+        hipLaunchKernelGGL(wide_str_len_kernel, dim3(grid), dim3(256), 0, ctx->stream, (const uint4 *)a->pack_buf, G, len1);
+        TFG_LAUNCH_CHECK();
+        if (int rc = exclusive_scan_u64(ctx, len1, start, (int64_t)G, (char *)sp + o_tmp)) return rc;
+        uint64_t chars = 0;
+        if (int rc = read_back_u64(ctx, start + G, &chars, 1)) return rc;
+        if (out_chars_host) *out_chars_host = chars;
+        if (chars > chars_capacity)
+            return fail(TFG_ERR_CAPACITY, "String keys need %llu bytes, capacity %llu", (unsigned long long)chars,
+                        (unsigned long long)chars_capacity);
+        ko.offsets = out_key_offsets[0];
+    }
+    for (int j = 0; j < a->kp.nkeys; ++j) {
+        ko.col[j] = out_key_cols ? out_key_cols[j] : nullptr;
+        ko.nullmap[j] = out_key_nullmaps ? out_key_nullmaps[j] : nullptr;
+    }
+    {
+        ProfScope _ps(ctx, "agg.unpack_keys");
+        hipLaunchKernelGGL(unpack_keys_kernel, dim3(grid), dim3(256), 0, ctx->stream, a->kp,
+                           (const uint4 *)a->pack_buf, (const uint64_t *)start, G, ko);
     }
     TFG_LAUNCH_CHECK();
     return TFG_OK;
