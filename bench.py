@@ -37,6 +37,9 @@ def parse():
     ap.add_argument("--join-build", type=int, default=10_000_000)
     ap.add_argument("--join-probe", type=int, default=100_000_000)
     ap.add_argument("--no-join", action="store_true")
+    ap.add_argument("--c5-rows", type=int, default=100_000_000, help="C5 String-key GROUP BY rows per GPU (0 = skip)")
+    ap.add_argument("--c5-groups", type=int, default=10_000_000)
+    ap.add_argument("--c4", type=int, default=-1, help="repartitioned join leg (configs[3]): 1 on, 0 off, -1 = on when N > 1")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--value-int64", action="store_true", help="Int64 value column instead of Float64")
@@ -139,6 +142,199 @@ def cpu_join_baseline(args):
             "sample": f"build {nb} rows into {threads} segment HashMaps of RowRefList cells (not timed), "
                       f"probe {npr} rows x 3 runs (median) with materialised output blocks "
                       f"(reference-algorithm CPU restatement, oracle/cpu_baseline.c)"}
+
+
+def cpu_string_baseline(args):
+    import numpy as np
+    from oracle import oracle as orc
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    n = min(args.c5_rows, 20_000_000)
+    rng = np.random.default_rng(11)
+    ids = rng.integers(0, args.c5_groups, n)
+    chars = np.empty((n, 10), np.uint8)
+    chars[:, 0] = ord("k")
+    x = ids.copy()
+    for j in range(8, 0, -1):
+        chars[:, j] = 48 + x % 10
+        x //= 10
+    chars[:, 9] = 0
+    chars = chars.reshape(-1)
+    offs = (np.arange(1, n + 1, dtype=np.uint64) * 10)
+    v = rng.integers(0, 10**9, n, dtype=np.int64)
+    times = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        orc.bench_string_agg(chars, offs, v, threads)
+        times.append(time.perf_counter() - t0)
+    med = statistics.median(times)
+    return {"value": round(n / med, 1), "unit": "rows/s", "cores": threads, "kind": "port",
+            "sample": f"{n} rows x 3 runs (median), k%08d keys over {args.c5_groups} ids, per-thread StringHashMap "
+                      f"StringKey16 sub-maps (CRC32-C, arena Decimal128+count states, prefetch, two-level at 100k keys) "
+                      f"+ bucket-parallel merge + result conversion (reference-algorithm CPU restatement, "
+                      f"oracle/cpu_baseline_str.c)"}
+
+
+def c4_leg(args, ctx, dev, world, rank):
+    """configs[3]: hash-repartitioned join.  Every rank holds join_build build rows and join_probe
+    probe rows (C3 distributions over the global key space); a step repartitions both sides by the
+    reference's weak hash + fillSelector (ExchangeSender, HashPartitionWriter) with an RCCL
+    all-to-all, builds the local hash table and runs the materialising probe.  value = probe rows
+    of all ranks / max-over-ranks step time (weak scaling)."""
+    import torch
+    import torch.distributed as dist
+
+    import tiflash_amd as tfa
+    from tiflash_amd.exchange import exchange_partitions
+    nb, npr = args.join_build, args.join_probe
+    g = torch.Generator(device=dev)
+    g.manual_seed(7 + 1000 * rank)
+    bk = (torch.randperm(nb, device=dev, generator=g).to(torch.int64) + rank * nb) * 4 + 1
+    bpay = torch.randint(0, 1 << 40, (nb,), device=dev, generator=g, dtype=torch.int64)
+    hit = torch.rand(npr, device=dev, generator=g) < 0.5
+    pk = torch.where(hit, torch.randint(0, nb * world, (npr,), device=dev, generator=g) * 4 + 1,
+                     torch.randint(0, 1 << 40, (npr,), device=dev, generator=g) * 4 + 3)
+    ppay = torch.randint(0, 1 << 40, (npr,), device=dev, generator=g, dtype=torch.int64)
+    del hit
+    cap = npr * 3 // 4 + (1 << 20)
+    outs = ([torch.empty(cap, dtype=torch.int64, device=dev) for _ in range(2)],
+            [torch.empty(cap, dtype=torch.int64, device=dev)], torch.empty(cap, dtype=torch.uint8, device=dev))
+    state = {}
+
+    def step():
+        if world > 1:
+            bcols, boffs = tfa.hash_partition(ctx, [bk, bpay], [0], world)
+            lb = exchange_partitions(bcols, boffs)
+            pcols, poffs = tfa.hash_partition(ctx, [pk, ppay], [0], world)
+            lp = exchange_partitions(pcols, poffs)
+        else:
+            lb, lp = [bk, bpay], [pk, ppay]
+        j = tfa.Join(ctx, tfa.INT64, expected_build_rows=lb[0].shape[0])
+        j.build(lb[0], payload=[lb[1]])
+        j.finalize()
+        n_out = lp[0].shape[0] * 3 // 4 + (1 << 20)
+        o = outs if n_out <= cap else None
+        op, ob, _ = j.probe_rows(lp[0], [lp[0], lp[1]], 1, capacity=cap if o else None, outs=o)
+        state["matches"] = op[0].shape[0]
+        state["probe_rows"] = lp[0].shape[0]
+        state["join"] = j  # freed at the next step (after its kernels are done)
+        return op
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ctx.profile(True)
+    ctx.profile_reset()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    prof = ctx.profile_read()
+    ctx.profile(False)
+    red_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
+    inv = torch.tensor([float(state["matches"]), float(state["probe_rows"])], dtype=torch.float64, device=red_dev)
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = t.item()
+        dist.all_reduce(inv)
+    matches, probe_total = (int(z) for z in inv.tolist())
+    ms = el / args.steps * 1e3
+    state.clear()
+    return {"metric": "probe rows/s on the hash-repartitioned join (C3 per GPU: 10M build x 100M probe, "
+                      "weak hash + fillSelector + RCCL all-to-all of both sides, local build + materialising probe)",
+            "value": round(npr * world * args.steps / el, 1), "unit": "rows/s", "ms_per_step": round(ms, 3),
+            "scaling": "weak", "config": {"workload": "configs[3] repartitioned join", "build_rows_per_gpu": nb,
+                                          "probe_rows_per_gpu": npr, "parallelism": f"dp{world}"},
+            "check": {"probe_rows_total": probe_total, "expected_probe_rows": npr * world, "matches": matches,
+                      "ok": probe_total == npr * world},
+            "kernels_ms_per_step": {kname: round(vv[0] / args.steps, 4) for kname, vv in sorted(prof.items())}}
+
+
+def c5_leg(args, ctx, dev, world, rank):
+    """configs[4]: GROUP BY a String key ("k%08d", c5_groups distinct) with sum(Decimal(15,2)) ->
+    Decimal(37,2) and count(*); N>1: partial -> packed-key RCCL exchange -> final (two-phase)."""
+    import torch
+    import torch.distributed as dist
+
+    import tiflash_amd as tfa
+    from tiflash_amd.exchange import two_phase_merge_keys
+    n, G = args.c5_rows, args.c5_groups
+    g = torch.Generator(device=dev)
+    g.manual_seed(11 + rank)
+    ids = torch.randint(0, G, (n,), device=dev, generator=g, dtype=torch.int64)
+    chars = torch.empty((n, 10), dtype=torch.uint8, device=dev)
+    chars[:, 0] = ord("k")
+    x = ids.clone()
+    for j in range(8, 0, -1):
+        chars[:, j] = (48 + x % 10).to(torch.uint8)
+        x //= 10
+    chars[:, 9] = 0
+    del x, ids
+    chars = chars.reshape(-1)
+    offs = torch.arange(1, n + 1, device=dev, dtype=torch.int64) * 10
+    v = torch.randint(0, 10**9, (n,), device=dev, generator=g, dtype=torch.int64)
+    aggs = [(tfa.AGG_SUM, tfa.DECIMAL64), (tfa.AGG_COUNT_ALL, 0)]
+    part = tfa.KeysAggregator(ctx, [tfa.STRING], aggs, expected_groups=G)
+    fin = tfa.KeysAggregator(ctx, [tfa.STRING], aggs, expected_groups=G) if world > 1 else None
+
+    def step():
+        part.reset()
+        part.consume([(chars, offs)], [v, None])
+        if world == 1:
+            return part.result()
+        fin.reset()
+        two_phase_merge_keys(ctx, part, fin)
+        return fin.result()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ctx.profile(True)
+    ctx.profile_reset()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    prof = ctx.profile_read()
+    ctx.profile(False)
+    red_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
+    inv = torch.tensor([float(res["states"][1].view(torch.int64).sum().item()), float(res["states"][1].shape[0])],
+                       dtype=torch.float64, device=red_dev)
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = t.item()
+        dist.all_reduce(inv)
+    cnt_total, groups_total = (int(z) for z in inv.tolist())
+    ms = el / args.steps * 1e3
+    alg = n * (8 + 10 + 8)  # offsets + chars + value per row
+    out = {"metric": "rows/s on GROUP BY String key (k%08d) sum(Decimal64)->Decimal128 + count" +
+                     (" two-phase + RCCL all-to-all" if world > 1 else ""),
+           "value": round(n * world * args.steps / el, 1), "unit": "rows/s", "ms_per_step": round(ms, 3),
+           "config": {"workload": "configs[4] String + Decimal GROUP BY", "rows_per_gpu": n, "groups": G},
+           "check": {"count_total": cnt_total, "rows_total": n * world, "groups_total": groups_total,
+                     "ok": cnt_total == n * world and groups_total <= G},
+           "pipeline_roofline": {"algorithmic_bytes_per_step": alg, "achieved": round(alg / (ms * 1e-3) / 1e9, 1),
+                                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+           "kernels_ms_per_step": {kname: round(vv[0] / args.steps, 4) for kname, vv in sorted(prof.items())}}
+    for o in (part, fin):
+        if o is not None:
+            o.close()
+    del chars, offs, v
+    return out
 
 
 def main():
@@ -297,7 +493,18 @@ def main():
             "kernels_ms_per_step": {kname: round(vv[0] / args.steps, 4) for kname, vv in sorted(jprof.items())},
         }
 
+    if args.c4 == 1 or (args.c4 == -1 and world > 1):
+        c4 = c4_leg(args, ctx, dev, world, rank)
+        if rank == 0:
+            line["repartitioned_join"] = c4
+    if args.c5_rows > 0:
+        c5 = c5_leg(args, ctx, dev, world, rank)
+        if rank == 0:
+            line["string_agg"] = c5
+
     if rank == 0 and world == 1 and not args.no_cpu:
+        if "string_agg" in line:
+            line["string_agg"]["cpu_baseline"] = cpu_string_baseline(args)
         cb = cpu_baseline(args)
         line["cpu_baseline"] = cb
         line["gpu_vs_cpu"] = round(value / cb["value"], 1)

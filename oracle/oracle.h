@@ -85,6 +85,10 @@ orc_join_ref *orc_join_ref_build(const int64_t *build_keys, const int64_t *build
 size_t orc_join_ref_probe(const orc_join_ref *j, const int64_t *probe_keys, const int64_t *probe_pay, size_t np,
                           int nthreads, uint64_t *checksum);
 void orc_join_ref_destroy(orc_join_ref *j);
+/* C5 partial aggregation leg (cpu_baseline_str.c): StringHashMap StringKey16 sub-maps, arena
+ * Decimal128 + count states, two-level at 100k keys, bucket-parallel merge + result conversion. */
+size_t orc_bench_string_agg(const uint8_t *chars, const uint64_t *offsets, const int64_t *v, size_t n, int nthreads,
+                            size_t block_rows, uint64_t *checksum);
 size_t orc_bench_join(const int64_t *build_keys, size_t nb, const int64_t *probe_keys, size_t np, int nthreads,
                       uint64_t *checksum);
 

@@ -58,6 +58,7 @@ def lib():
         L.orc_bench_filter_agg.restype = ctypes.c_size_t
         L.orc_bench_join.restype = ctypes.c_size_t
         L.orc_bench_filter_agg_ref.restype = ctypes.c_size_t
+        L.orc_bench_string_agg.restype = ctypes.c_size_t
         L.orc_join_ref_build.restype = ctypes.c_void_p
         L.orc_join_ref_probe.restype = ctypes.c_size_t
         L.orc_join_ref_probe.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
@@ -362,6 +363,14 @@ class JoinBench:
         if getattr(self, "h", None):
             lib().orc_join_ref_destroy(self.h)
             self.h = None
+
+
+def bench_string_agg(chars, offsets, v, nthreads, block_rows=65536):
+    """C5 partial aggregation on the CPU (cpu_baseline_str.c) -> (groups, sum of counts)."""
+    cs = ctypes.c_uint64()
+    g = lib().orc_bench_string_agg(_p(chars), _p(offsets), _p(v), ctypes.c_size_t(len(v)), nthreads,
+                                   ctypes.c_size_t(block_rows), ctypes.byref(cs))
+    return g, cs.value
 
 
 def bench_join(build_keys, probe_keys, nthreads):

@@ -171,3 +171,102 @@ def test_repartitioned_join_gloo():
     want = sorted(zip(pk[pi].tolist(), ppay[pi].tolist(), bpay[bi].tolist()))
     assert len(want) > 1000
     assert got == want
+
+
+# ---- C5: two-phase GROUP BY a String key, partial rows exchanged as packed 16-byte keys ----------
+def _str_data(rank, n=20000, groups=5000):
+    rng = np.random.default_rng(300 + rank)
+    ids = rng.integers(0, groups, n)
+    strs = [b"k%08d" % i for i in ids]
+    d = rng.integers(0, 10**9, n, dtype=np.int64)
+    return strs, d
+
+
+def _str_col(strs):
+    chars = np.frombuffer(b"".join(s + b"\0" for s in strs), dtype=np.uint8).copy()
+    return chars, np.cumsum([len(s) + 1 for s in strs]).astype(np.uint64)
+
+
+def _pack(strs):
+    """The packed key form partial rows travel in (tfg_agg_create_keys, key_string): bytes, zero
+    padded, byte 15 = length."""
+    out = np.zeros((len(strs), 16), dtype=np.uint8)
+    for i, s in enumerate(strs):
+        out[i, :len(s)] = np.frombuffer(s, np.uint8)
+        out[i, 15] = len(s)
+    return out
+
+
+def _unpack(a):
+    return [bytes(r[:r[15]]) for r in a]
+
+
+def _two_phase_string_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import sys
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as orc
+    from tiflash_amd.exchange import exchange_partitions
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        strs, d = _str_data(rank)
+        part = orc.AggKeys([orc.STRING], [(0, orc.DECIMAL64), (2, 0)])
+        part.consume([_str_col(strs)], [d, None])
+        groups = part.result()
+        keys = [k[0] for k, _ in groups]
+        sums = np.array([[s & (2**64 - 1), s >> 64] for (_, (s, _c)) in groups], dtype=np.uint64).view(np.int64)
+        cnts = np.array([c for (_, (_s, c)) in groups], dtype=np.int64)
+        # ExchangeSender: route by ColumnString::updateWeakHash32 of the key -> fillSelector
+        chars, offs = _str_col(keys)
+        h = orc.weak_hash_string(chars, offs, np.full(len(keys), 0xFFFFFFFF, dtype=np.uint32))
+        sel = orc.fill_selector(h, world)
+        perm, poffs = orc.partition(sel, world)
+        packed = _pack(keys)[perm].view(np.int64)
+        rk, rs, rc = [x.numpy() for x in exchange_partitions(
+            [torch.from_numpy(np.ascontiguousarray(packed)), torch.from_numpy(np.ascontiguousarray(sums[perm])),
+             torch.from_numpy(np.ascontiguousarray(cnts[perm]))], [int(x) for x in poffs])]
+        rstr = _unpack(rk.view(np.uint8).reshape(-1, 16))
+        if rstr:
+            c2, o2 = _str_col(rstr)
+            h2 = orc.weak_hash_string(c2, o2, np.full(len(rstr), 0xFFFFFFFF, dtype=np.uint32))
+            assert (orc.fill_selector(h2, world) == rank).all()
+        # final: merge partial states (sum of Decimal128 partial sums, sum of counts)
+        fin = orc.AggKeys([orc.STRING], [(0, orc.DECIMAL128), (0, orc.INT64)])
+        if rstr:
+            fin.consume([_str_col(rstr)], [np.ascontiguousarray(rs), np.ascontiguousarray(rc)])
+        res = {k[0]: (s, c) for k, (s, c) in fin.result()}
+        allres = [None] * world
+        dist.all_gather_object(allres, res)
+        if rank == 0:
+            merged = {}
+            for r in allres:
+                assert not (set(r) & set(merged)), "a key was finalised on two ranks"
+                merged.update(r)
+            q.put(merged)
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put(repr(e))
+        raise
+
+
+def test_two_phase_string_aggregation_gloo():
+    from oracle import oracle as orc
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_two_phase_string_worker, args=(r, WORLD, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    assert isinstance(got, dict), got
+    ref = orc.AggKeys([orc.STRING], [(0, orc.DECIMAL64), (2, 0)])
+    for r in range(WORLD):
+        strs, d = _str_data(r)
+        ref.consume([_str_col(strs)], [d, None])
+    want = {k[0]: (s, c) for k, (s, c) in ref.result()}
+    assert len(want) > 1000
+    assert got == want

@@ -29,7 +29,8 @@ namespace tfg {
 constexpr int AGG_MAX = 4;
 constexpr int BT = 512;      // bucket kernel threads (8 waves; 2-3 workgroups per CU)
 constexpr int BT_BIG = 1024; // for tables too large for two workgroups per CU (16 waves)
-constexpr int LDS_TABLE_BYTES = 100 * 1024;
+constexpr int LDS_TABLE_BYTES = 100 * 1024;  // preferred table size (two workgroups per CU)
+constexpr int LDS_TABLE_MAX = 150 * 1024;    // largest table (one 16-wave workgroup per CU)
 
 enum AccKind { ACC_NONE = 0, ACC_I64 = 1, ACC_F64 = 2, ACC_I128 = 3 };
 enum RowMode { MODE_RAW = 0, MODE_PARTIAL = 1, MODE_STATE = 2 };
@@ -52,8 +53,9 @@ struct AggSpec {
     int bt;         // bucket kernel workgroup size (BT or BT_BIG)
     int wkey_off;   // wide keys (key_width 16): LDS byte offset of the 16-byte keys (cells' tags sit in
                     // the u64 key array); 0 for keys of <= 8 bytes
-    int slot_shift; // in-table group = bits [slot_shift, slot_shift + log2(cap/GS)) of key * 2^64/phi,
-                    // just below the bits that chose the bucket (one multiply instead of a mixer)
+    int bbits;          // bucket radix bits: the in-table slot group comes from the 32 bits of
+                        // key * 2^64/phi just below them (one multiply instead of a mixer) ...
+    unsigned ngroups;   // ... scaled to the table's cap / GS groups (any count: LDS-sized tables)
 };
 
 // Columnar row source staged by the bucket pass (bucket-major).
@@ -193,6 +195,10 @@ struct Table {
     // one step (single-cell linear probing had long worst-case chains, and a wave waits for its
     // slowest lane).  Groups overflow linearly into the next group.
     static constexpr int GS = 4;
+    __device__ __forceinline__ unsigned slot_group(uint64_t key) const {
+        const uint32_t below = (uint32_t)(((key * 0x9E3779B97F4A7C15ull) << S.bbits) >> 32);
+        return (unsigned)(((uint64_t)below * S.ngroups) >> 32);
+    }
     __device__ __forceinline__ int try_claim(int cell, uint64_t key, bool force, bool &done) {
         // returns the cell when `key` now owns it, -1 otherwise (done = a definitive miss)
         if (!force && __hip_atomic_load(&ctrl->full, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
@@ -220,7 +226,7 @@ struct Table {
     __device__ __forceinline__ void find_or_insert_multi(const uint64_t (&key)[R], const bool (&is_null)[R],
                                                          const bool (&valid)[R], bool may_insert, int (&cell)[R],
                                                          bool force = false) {
-        const unsigned gmask = (unsigned)S.cap / GS - 1;
+        const unsigned ng = S.ngroups;
         unsigned grp[R];
         bool live[R];
 #pragma unroll
@@ -232,10 +238,10 @@ struct Table {
                 cell[u] = find_or_insert(key[u], is_null[u], may_insert, force);
                 continue;
             }
-            grp[u] = (unsigned)((key[u] * 0x9E3779B97F4A7C15ull) >> S.slot_shift) & gmask;
+            grp[u] = slot_group(key[u]);
             live[u] = true;
         }
-        for (int step = 0; step <= (int)gmask; ++step) {
+        for (int step = 0; step < (int)ng; ++step) {
             uint64_t k[R][GS];
 #pragma unroll
             for (int u = 0; u < R; ++u) // every live row's group read before any compare
@@ -274,7 +280,7 @@ struct Table {
                         any = true; // raced: re-read this group
                     }
                 } else {
-                    grp[u] = (grp[u] + 1) & gmask; // full group: overflow into the next
+                    grp[u] = grp[u] + 1 == ng ? 0 : grp[u] + 1; // full group: overflow into the next
                     any = true;
                 }
             }
@@ -293,7 +299,7 @@ struct Table {
     __device__ __forceinline__ void find_wide_multi(const uint64_t (&lo)[R], const uint64_t (&hi)[R],
                                                     const uint64_t (&tag)[R], const bool (&valid)[R], bool may_insert,
                                                     int (&cell)[R], bool force = false) {
-        const unsigned gmask = (unsigned)S.cap / GS - 1;
+        const unsigned ng = S.ngroups;
         uint4 *wk = reinterpret_cast<uint4 *>(base + S.wkey_off);
         unsigned grp[R];
         bool live[R];
@@ -301,7 +307,7 @@ struct Table {
         for (int u = 0; u < R; ++u) {
             cell[u] = -1;
             live[u] = valid[u];
-            grp[u] = (unsigned)((tag[u] * 0x9E3779B97F4A7C15ull) >> S.slot_shift) & gmask;
+            grp[u] = slot_group(tag[u]);
         }
         for (;;) {
             uint64_t k[R][GS];
@@ -371,7 +377,7 @@ struct Table {
                         any = true; // raced: re-read the group
                     }
                 } else {
-                    grp[u] = (grp[u] + 1) & gmask;
+                    grp[u] = grp[u] + 1 == ng ? 0 : grp[u] + 1;
                     any = true;
                 }
             }
@@ -1472,29 +1478,39 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
         if (S.has_cnt[i]) cell += 8;
         (void)arg_scales;
     }
-    // buckets: about 2K expected groups per bucket (the TwoLevelHashTable analogue): fewer buckets
-    // give the radix scatter longer runs per destination; 2K-group tables run 16-wave workgroups
+    // buckets: as many groups per bucket as the largest LDS table holds with slack (~4K for
+    // 8-byte keys with sum + count, the TwoLevelHashTable analogue): fewer buckets give the radix
+    // scatter longer runs per destination (measured: 256 buckets with 6K-cell tables 53.6G rows/s
+    // against 512 with 4K-cell tables 48.5G on C2); at least 256 buckets, one per CU
     const int64_t eg = (params && params->expected_groups > 0) ? params->expected_groups : (1 << 20);
     int bbits = params ? params->bucket_bits : 0;
     if (bbits <= 0) {
-        bbits = 4;
-        while (bbits < 12 && ((int64_t)1 << bbits) * 2048 < eg) ++bbits;
+        const int64_t cells_max = LDS_TABLE_MAX / cell;
+        const int64_t fit = std::min<int64_t>(cells_max * 6 / 8, cells_max - BT_BIG - 8) * 5 / 6;
+        bbits = 8;
+        while (bbits < 12 && ((int64_t)1 << bbits) * fit < eg) ++bbits;
     }
     if (bbits > 12) bbits = 12;
     a->B = a->nokey ? 1 : (1u << bbits);
-    // LDS table geometry: room for a bucket's expected groups with 25% slack (fill <= 5/8 and
-    // headroom for one step of in-flight inserts); small tables let 2-3 workgroups share a CU
+    // LDS table geometry: room for a bucket's expected groups with 25% slack and headroom for one
+    // step of in-flight inserts.  Power-of-two tables up to LDS_TABLE_BYTES (fill <= 5/8; 2-3
+    // workgroups share a CU); a bucket too large for that gets the largest table one workgroup per
+    // CU can hold (any multiple of 256 cells, fill <= 3/4)
     const int64_t per_bucket = eg / (int64_t)a->B + 1;
+    const int64_t need = per_bucket * 5 / 4;
     int cap = 256;
-    while (cap < (1 << 16) && std::min(cap * 5 / 8, cap - BT - 8) < per_bucket * 5 / 4) cap *= 2;
-    while (cap > 256 && (size_t)(cap + 2) * cell > (size_t)LDS_TABLE_BYTES) cap /= 2;
-    S.cap = cap;
-    S.maxfill = std::max(1, std::min(cap * 5 / 8, cap - BT - 8));
-    {
-        int gbits = 0;
-        while ((4 << gbits) < cap) ++gbits; // log2(cap / GS), GS = 4
-        S.slot_shift = 64 - (a->nokey ? 0 : bbits) - gbits;
+    while (cap < (1 << 16) && std::min(cap * 5 / 8, cap - BT - 8) < need) cap *= 2;
+    int fill_num = 5;
+    if ((size_t)(cap + 2) * cell > (size_t)LDS_TABLE_BYTES) {
+        int c2 = 256;
+        while ((size_t)(c2 + 256 + 2) * cell <= (size_t)LDS_TABLE_MAX && std::min(c2 * 6 / 8, c2 - BT_BIG - 8) < need)
+            c2 += 256;
+        cap = c2;
+        fill_num = 6;
     }
+    S.cap = cap;
+    S.bbits = a->nokey ? 0 : bbits;
+    S.ngroups = (unsigned)(cap / 4); // GS = 4
     int off = (cap + 2) * 8;
     if (wide) {
         S.wkey_off = off;
@@ -1514,7 +1530,7 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
     S.lds_bytes = off + (int)sizeof(Ctrl) + 16;
     // one workgroup per CU anyway (LDS): make it 16 waves, and keep the in-flight insert headroom
     S.bt = S.lds_bytes > 80 * 1024 ? BT_BIG : BT;
-    S.maxfill = std::max(1, std::min(cap * 5 / 8, cap - S.bt - 8));
+    S.maxfill = std::max(1, std::min(cap * fill_num / 8, cap - S.bt - 8));
     S.dbg = getenv("TFG_DBG_BUCKET") ? atoi(getenv("TFG_DBG_BUCKET")) : 0;
     if (a->nokey) {
         if (int rc = a->ensure_state(0, 1)) {

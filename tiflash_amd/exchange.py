@@ -38,3 +38,28 @@ def exchange_partitions(cols: Sequence[torch.Tensor], offsets: Sequence[int], gr
         dist.all_to_all_single(o, c.contiguous(), recv_counts, send_counts, group=group)
         outs.append(o)
     return outs
+
+
+def two_phase_merge_keys(ctx, partial, final, group=None, collators=None):
+    """ExchangeSender -> ExchangeReceiver of a two-phase GROUP BY over String / several keys
+    (C5): the partial aggregation's rows are routed by the reference's hash of the key columns
+    (IColumn::updateWeakHash32 -> fillSelector, HashBaseWriterHelper.cpp:46-84), travel as packed
+    16-byte keys plus states, and the final aggregation merges them (mergeOnBlock).  `partial` and
+    `final` are tiflash_amd.KeysAggregator objects of the same signature."""
+    import tiflash_amd as tfa
+    world = dist.get_world_size(group)
+    packed = partial.result_packed()
+    cols = partial.result()
+    n = packed["keys"].shape[0]
+    h = torch.empty(n, dtype=torch.int32, device=packed["keys"].device)
+    tfa.check(tfa.lib().tfg_weak_hash_init(ctx.h, tfa._p(h), tfa.ctypes.c_int64(n)))
+    for j, (t, k, kn) in enumerate(zip(partial.key_types, cols["keys"], cols["key_null"])):
+        if t == tfa.STRING:
+            tfa.weak_hash_string(ctx, k[0], k[1], h, nullmap=kn, collator=(collators or [0] * 4)[j])
+        else:
+            tfa.weak_hash(ctx, [k], types=[t], nullmaps=[kn], h=h)
+    sel = tfa.fill_selector(ctx, h, world)
+    perm, offs = tfa.partition(ctx, sel, world)
+    send = tfa.gather(ctx, perm, [packed["keys"]] + list(packed["states"]))
+    recv = exchange_partitions(send, offs, group)
+    final.consume_partial_packed(recv[0], recv[1:])

@@ -25,6 +25,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 # demangled kernel name -> pipeline scope name used by bench.py / the library profiler
 NAME_MAP = [
+    (r"part_hist_kernel<tfg::SelWide", "agg.wide.part.hist"),
+    (r"part_scatter.*<tfg::SelWide", "agg.wide.part.scatter"),
+    (r"agg_bucket_kernel<tfg::WideOps", "agg.wide.bucket"),
+    (r"pack_keys_kernel", "agg.pack_keys"),
     (r"part_hist_kernel<tfg::SelBucket", "agg.part.hist"),
     (r"part_scatter_staged_kernel<tfg::SelBucket", "agg.part.scatter"),
     (r"part_scatter_kernel<tfg::SelBucket", "agg.part.scatter"),
