@@ -772,11 +772,180 @@ __global__ void __launch_bounds__(BT) agg_bucket_kernel(AggSpec S, RowsIO rows0,
     if (threadIdx.x == 0) out_cnt[b] = T.ctrl->out_count;
 }
 
+// Bucket kernel over a tile-sorted partition (run_partition_tiled): bucket b's rows are runs
+// in every tile, tile_hist[b * T + t] = start | count << 16.  Pass 0 walks the runs chunk by
+// chunk (runs average kept / B rows, ~30 for C2).  Rows that miss (table full / older groups pending) go to
+// the bucket's spill regions, reserved once per workgroup from a global cursor, and later passes
+// ping-pong between them as in agg_bucket_kernel.  Temp groups go to a region reserved the same
+// way; tmp_base[b] tells the compaction where.
+struct TiledIn {
+    const uint64_t *rec;       // records of the tiled partition (Ops::NCOL words each)
+    const uint32_t *tile_hist; // [B][T]
+    int T;
+    int TR;
+    uint64_t *spill[2];        // two spill arenas of >= kept rows (records)
+    unsigned long long *cursor; // [0] spill rows, [1] temp groups
+};
+
+template <typename Ops, int BT>
+__global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn tin, int mode, GroupsIO old,
+                                                              const uint64_t *old_off, GroupsIO out, uint64_t *out_cnt,
+                                                              uint64_t *tmp_base) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    __shared__ unsigned long long s_red[BT / 64];
+    __shared__ unsigned long long s_base[2];
+    constexpr int CH = 128; // tiles per pass-0 chunk
+    __shared__ uint32_t s_ent[CH];
+    __shared__ uint32_t s_pref[CH + 1];
+    Table T(lds, S);
+    const Ops ops{S, mode};
+    const int b = blockIdx.x;
+    const uint32_t *col = tin.tile_hist + (size_t)b * tin.T;
+    // rows of this bucket
+    unsigned long long tot = 0;
+    for (int t = threadIdx.x; t < tin.T; t += BT) tot += col[t] >> 16;
+    for (int d = 32; d > 0; d >>= 1) tot += __shfl_down(tot, d, 64);
+    if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = tot;
+    __syncthreads();
+    int64_t os = 0, oe = 0;
+    if (old_off) {
+        os = (int64_t)old_off[b];
+        oe = (int64_t)old_off[b + 1];
+    }
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int w = 0; w < BT / 64; ++w) t += s_red[w];
+        s_base[0] = atomicAdd(&tin.cursor[0], t);
+        s_base[1] = atomicAdd(&tin.cursor[1], t + (unsigned long long)(oe - os));
+        T.ctrl->out_count = 0;
+    }
+    __syncthreads();
+    const uint64_t sbase = s_base[0], out_base = s_base[1];
+    RowsIO src{}, reg[2]{};
+    src.key = (void *)tin.rec;
+    for (int r = 0; r < 2; ++r) reg[r].key = tin.spill[r] + sbase * Ops::NCOL;
+    int64_t old_cursor = os;
+    int64_t pending = -1; // pass 0: the tile runs
+    int pass = 0;
+    while (pending != 0 || old_cursor < oe) {
+        const RowsIO &rows = reg[(pass + 1) & 1]; // pass p >= 1 reads region (p - 1) & 1
+        const RowsIO &spill = reg[pass & 1];      // ... and spills into region p & 1
+        T.clear();
+        __syncthreads();
+        if (threadIdx.x == 0) T.ctrl->spill_w = 0;
+        int64_t take = oe - old_cursor;
+        if (take > S.maxfill) take = S.maxfill;
+        for (int64_t g = old_cursor + threadIdx.x; g < old_cursor + take; g += BT) {
+            const int cell = T.find_or_insert(old.key[g], old.key_null[g] != 0, true, true);
+            T.add_group(cell, old, g);
+        }
+        old_cursor += take;
+        const bool allow_insert = old_cursor >= oe;
+        __syncthreads();
+        // one step: up to RPT rows per thread (v / ok), lookup, add, retry misses after a barrier
+        auto step = [&](typename Ops::Row (&v)[RPT], bool (&ok)[RPT]) {
+            uint64_t ku[RPT];
+            bool nu[RPT];
+            int cells[RPT];
+            bool miss[RPT];
+#pragma unroll
+            for (int u = 0; u < RPT; ++u) {
+                ku[u] = ops.key(v[u]);
+                nu[u] = false;
+            }
+            T.find_or_insert_multi<RPT>(ku, nu, ok, allow_insert, cells);
+#pragma unroll
+            for (int u = 0; u < RPT; ++u) {
+                miss[u] = false;
+                if (!ok[u]) continue;
+                if (cells[u] >= 0) ops.add(T, cells[u], v[u]);
+                else miss[u] = true;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < RPT; ++u) {
+                if (!miss[u]) continue;
+                const int cell = T.find_or_insert(ku[u], false, false, false);
+                if (cell >= 0) {
+                    ops.add(T, cell, v[u]);
+                } else {
+                    const int64_t w = (int64_t)atomicAdd(&T.ctrl->spill_w, 1ull);
+                    ops.store(spill, w, v[u]);
+                }
+            }
+        };
+        if (pass == 0) {
+            // chunks of CH tiles: their runs are concatenated (prefix of the counts in LDS) and
+            // row i of the chunk finds its tile by a 7-step binary search, so every thread
+            // takes RPT rows per step whatever the run lengths
+            for (int t0 = 0; t0 < tin.T; t0 += CH) {
+                if (threadIdx.x < CH) s_ent[threadIdx.x] = t0 + (int)threadIdx.x < tin.T ? col[t0 + threadIdx.x] : 0u;
+                __syncthreads();
+                if (threadIdx.x < 64) {
+                    const uint32_t c0 = s_ent[2 * threadIdx.x] >> 16, c1 = s_ent[2 * threadIdx.x + 1] >> 16;
+                    uint32_t x = c0 + c1;
+#pragma unroll
+                    for (int d = 1; d < 64; d <<= 1) {
+                        const uint32_t y = __shfl_up(x, d, 64);
+                        if ((int)threadIdx.x >= d) x += y;
+                    }
+                    s_pref[2 * threadIdx.x] = x - c0 - c1;
+                    s_pref[2 * threadIdx.x + 1] = x - c1;
+                    if (threadIdx.x == 63) s_pref[CH] = x;
+                }
+                __syncthreads();
+                const uint32_t tot = s_pref[CH];
+                for (uint32_t base = 0; base < tot; base += BT * RPT) {
+                    typename Ops::Row v[RPT];
+                    bool ok[RPT];
+#pragma unroll
+                    for (int u = 0; u < RPT; ++u) {
+                        const uint32_t i = base + u * BT + threadIdx.x;
+                        ok[u] = i < tot;
+                        if (!ok[u]) continue;
+                        uint32_t lo = 0;
+#pragma unroll
+                        for (uint32_t st = CH / 2; st > 0; st >>= 1)
+                            if (s_pref[lo + st] <= i) lo += st;
+                        const int64_t r = (int64_t)(t0 + (int)lo) * tin.TR + (s_ent[lo] & 0xFFFFu) + (i - s_pref[lo]);
+                        ops.load(src, r, v[u]);
+                    }
+                    step(v, ok);
+                }
+                __syncthreads();
+            }
+        } else {
+            const uint32_t npend = (uint32_t)pending;
+            for (uint32_t base = 0; base < npend; base += BT * RPT) {
+                typename Ops::Row v[RPT];
+                bool ok[RPT];
+#pragma unroll
+                for (int u = 0; u < RPT; ++u) {
+                    const uint32_t i = base + u * BT + threadIdx.x;
+                    ok[u] = i < npend;
+                    if (ok[u]) ops.load(rows, i, v[u]);
+                }
+                step(v, ok);
+            }
+        }
+        ++pass;
+        __syncthreads();
+        T.flush(out, out_base);
+        __syncthreads();
+        pending = (int64_t)T.ctrl->spill_w;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        out_cnt[b] = T.ctrl->out_count;
+        tmp_base[b] = out_base;
+    }
+}
+
 // temp (bucket-strided) groups -> compact state
 __global__ void agg_compact_kernel(AggSpec S, GroupsIO tmp, const uint64_t *stage_off, const uint64_t *old_off,
-                                   const uint64_t *new_off, GroupsIO dst) {
+                                   const uint64_t *new_off, GroupsIO dst, const uint64_t *tmp_base) {
     const int b = blockIdx.x;
-    const uint64_t src0 = stage_off[b] + (old_off ? old_off[b] : 0);
+    const uint64_t src0 = tmp_base ? tmp_base[b] : stage_off[b] + (old_off ? old_off[b] : 0);
     const uint64_t d0 = new_off[b], cnt = new_off[b + 1] - d0;
     for (uint64_t j = threadIdx.x; j < cnt; j += blockDim.x) {
         const uint64_t s = src0 + j, d = d0 + j;
@@ -1192,6 +1361,121 @@ int fast_signature(const AggSpec &S, int mode, int key_width, const uint8_t *key
     return code;
 }
 
+// The fast signatures over a tile-sorted partition (TFG_AGG_TILED=0 falls back to the
+// histogram + scatter partition): partition -> agg_bucket_tiled_kernel -> scan -> compaction.
+bool agg_tiled_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("TFG_AGG_TILED");
+        return !e || atoi(e) != 0;
+    }();
+    return on;
+}
+
+template <typename Ops>
+void launch_bucket_tiled(int B, const AggSpec &S, hipStream_t st, const TiledIn &tin, int mode, const GroupsIO &old,
+                         const uint64_t *ooff, const GroupsIO &tmp, uint64_t *new_cnt, uint64_t *tmp_base) {
+    if (S.bt == BT_BIG)
+        hipLaunchKernelGGL((agg_bucket_tiled_kernel<Ops, BT_BIG>), dim3(B), dim3(BT_BIG), S.lds_bytes, st, S, tin, mode,
+                           old, ooff, tmp, new_cnt, tmp_base);
+    else
+        hipLaunchKernelGGL((agg_bucket_tiled_kernel<Ops, BT>), dim3(B), dim3(BT), S.lds_bytes, st, S, tin, mode, old,
+                           ooff, tmp, new_cnt, tmp_base);
+}
+
+int consume_fast_tiled(tfg_agg *a, int fast, const RowPred &pred, const void *keys, const void *const *vals,
+                       int64_t n, bool &done) {
+    done = false;
+    Ctx *ctx = a->ctx;
+    const AggSpec &S = a->S;
+    const uint32_t B = a->B;
+    const size_t n_old = a->n_groups;
+    int rec_words = 1;
+    for (int c = fast; c > 0; c /= 10) rec_words += (c % 10) >= 2;
+    PCols pc{};
+    pc.in[0] = keys;
+    pc.width[0] = 8;
+    pc.ncols = 1;
+    pc.key0 = 1;
+    pc.aos = 1;
+    for (int i = 0, c = fast; i < S.n_aggs; ++i) {
+        const int op = (i == 0 ? c / 100 : i == 1 ? c / 10 : c) % 10;
+        if (op < 2) continue;
+        pc.in[pc.ncols] = vals[i];
+        pc.width[pc.ncols++] = 8;
+    }
+    TFG_CHECK(pc.ncols == rec_words, TFG_ERR_LOGICAL, "record layout mismatch");
+    TiledGeom tg{};
+    if (!make_tiled_geom(ctx, n, B, pc, tg)) return TFG_OK; // not applicable: caller takes the general path
+    Carver cv;
+    const size_t o_rec = cv.take<uint64_t>((size_t)tg.out_rows * rec_words);
+    const size_t o_sp0 = cv.take<uint64_t>((size_t)n * rec_words), o_sp1 = cv.take<uint64_t>((size_t)n * rec_words);
+    const size_t o_hist = cv.take<uint32_t>((size_t)B * tg.sg.T);
+    const size_t o_cur = cv.take<unsigned long long>(2);
+    const size_t o_new_cnt = cv.take<uint64_t>(B), o_new_off = cv.take<uint64_t>(B + 1), o_tbase = cv.take<uint64_t>(B);
+    const size_t tmp_groups = n_old + (size_t)n;
+    const size_t o_tmpg = cv.take<uint8_t>(a->carve_groups(nullptr, tmp_groups, a->st[0]) + 256);
+    const size_t o_scan = cv.take<uint8_t>(scan_tmp_bytes(B + 1));
+    void *sp;
+    if (int rc = scratch_get(ctx, cv.off, &sp)) return rc;
+    char *sb = (char *)sp;
+    pc.out[0] = sb + o_rec;
+    SelBucket8 sel{(const uint64_t *)keys, fib_shift(B)};
+    if (int rc = run_partition_tiled(ctx, sel, pred, tg, pc, (uint32_t *)(sb + o_hist), "agg.part.tiled")) return rc;
+    TiledIn tin{};
+    tin.rec = (const uint64_t *)(sb + o_rec);
+    tin.tile_hist = (const uint32_t *)(sb + o_hist);
+    tin.T = tg.sg.T;
+    tin.TR = tg.sg.TR;
+    tin.spill[0] = (uint64_t *)(sb + o_sp0);
+    tin.spill[1] = (uint64_t *)(sb + o_sp1);
+    tin.cursor = (unsigned long long *)(sb + o_cur);
+    TFG_HIP(hipMemsetAsync(tin.cursor, 0, 16, ctx->stream));
+    GroupsIO tmp{};
+    a->carve_groups(sb + o_tmpg, tmp_groups, tmp);
+    uint64_t *new_cnt = (uint64_t *)(sb + o_new_cnt), *new_off = (uint64_t *)(sb + o_new_off);
+    uint64_t *tbase = (uint64_t *)(sb + o_tbase);
+    const bool has_old = n_old > 0;
+    const GroupsIO old = a->st[a->cur];
+    const uint64_t *ooff = has_old ? a->bucket_off[a->cur] : (const uint64_t *)nullptr;
+    {
+        ProfScope _ps(ctx, "agg.bucket");
+#define TFG_TBUCKET(...) launch_bucket_tiled<__VA_ARGS__>(B, S, ctx->stream, tin, MODE_RAW, old, ooff, tmp, new_cnt, tbase)
+        switch (fast) {
+        case 310: TFG_TBUCKET(FastOps<3, 1, 0>); break;
+        case 210: TFG_TBUCKET(FastOps<2, 1, 0>); break;
+        case 410: TFG_TBUCKET(FastOps<4, 1, 0>); break;
+        case 300: TFG_TBUCKET(FastOps<3, 0, 0>); break;
+        case 200: TFG_TBUCKET(FastOps<2, 0, 0>); break;
+        case 400: TFG_TBUCKET(FastOps<4, 0, 0>); break;
+        case 100: TFG_TBUCKET(FastOps<1, 0, 0>); break;
+        case 231: TFG_TBUCKET(FastOps<2, 3, 1>); break;
+        case 221: TFG_TBUCKET(FastOps<2, 2, 1>); break;
+        case 331: TFG_TBUCKET(FastOps<3, 3, 1>); break;
+        case 441: TFG_TBUCKET(FastOps<4, 4, 1>); break;
+        default: return TFG_OK; // not reached: fast_signature returns these codes only
+        }
+#undef TFG_TBUCKET
+    }
+    TFG_LAUNCH_CHECK();
+    if (int rc = exclusive_scan_u64(ctx, new_cnt, new_off, B, sb + o_scan)) return rc;
+    uint64_t total = 0;
+    if (int rc = read_back_u64(ctx, new_off + B, &total, 1)) return rc;
+    const int nxt = a->cur ^ 1;
+    if (int rc = a->ensure_state(nxt, total)) return rc;
+    if (!a->bucket_off[nxt]) TFG_HIP(hipMalloc(&a->bucket_off[nxt], (B + 1) * 8));
+    {
+        ProfScope _ps(ctx, "agg.compact");
+        hipLaunchKernelGGL(agg_compact_kernel, dim3(B), dim3(256), 0, ctx->stream, S, tmp, (const uint64_t *)nullptr,
+                           (const uint64_t *)nullptr, new_off, a->st[nxt], (const uint64_t *)tbase);
+    }
+    TFG_LAUNCH_CHECK();
+    TFG_HIP(hipMemcpyAsync(a->bucket_off[nxt], new_off, (B + 1) * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    a->cur = nxt;
+    a->n_groups = total;
+    done = true;
+    return TFG_OK;
+}
+
 int consume_keyed(tfg_agg *a, int mode, const RowPred &pred, const void *keys, int key_width, const uint8_t *key_null,
                   const void *const *vals, const uint8_t *const *val_nulls, const uint64_t *const *val_cnts,
                   const uint64_t *given_off, int64_t n) {
@@ -1201,6 +1485,11 @@ int consume_keyed(tfg_agg *a, int mode, const RowPred &pred, const void *keys, i
     const size_t n_old = a->n_groups;
     // fast signature: rows staged as interleaved records (key + summed arguments, 8 B each)
     const int fast = given_off ? 0 : fast_signature(S, mode, key_width, key_null, val_nulls);
+    if (fast && agg_tiled_enabled()) {
+        bool done = false;
+        if (int rc = consume_fast_tiled(a, fast, pred, keys, vals, n, done)) return rc;
+        if (done) return TFG_OK;
+    }
     int rec_words = 1;
     for (int c = fast; c > 0; c /= 10) rec_words += (c % 10) >= 2;
     // ---- scratch layout
@@ -1366,7 +1655,8 @@ int consume_keyed(tfg_agg *a, int mode, const RowPred &pred, const void *keys, i
     if (!a->bucket_off[nxt]) TFG_HIP(hipMalloc(&a->bucket_off[nxt], (B + 1) * 8));
     { ProfScope _ps(ctx, "agg.compact");
     hipLaunchKernelGGL(agg_compact_kernel, dim3(B), dim3(256), 0, ctx->stream, S, tmp, stage_off,
-                       has_old ? a->bucket_off[a->cur] : (const uint64_t *)nullptr, new_off, a->st[nxt]);
+                       has_old ? a->bucket_off[a->cur] : (const uint64_t *)nullptr, new_off, a->st[nxt],
+                       (const uint64_t *)nullptr);
     }
     TFG_LAUNCH_CHECK();
     TFG_HIP(hipMemcpyAsync(a->bucket_off[nxt], new_off, (B + 1) * 8, hipMemcpyDeviceToDevice, ctx->stream));

@@ -469,6 +469,12 @@ struct StagedGeom {
     int lds_bytes;
     int dbg; // timing ablations (TFG_DBG_SCATTER): 1 no stream-out, 2 no placement / stream-out,
              // 3 stream-out to tile-contiguous addresses (wrong results; isolates the write pattern)
+    // tile-sorted mode (TILED kernels): tile k of segment g is written, sorted by destination, to
+    // rows [(g * tps + k) * TR, + kept) of the output, and tile_hist[p * T + tile] receives the
+    // destination's start inside the tile | its row count << 16
+    uint32_t *tile_hist;
+    int tps; // tiles per segment
+    int T;   // tiles
 };
 
 // LDS bytes a staged-scatter workgroup may use (TFG_STAGE_LDS overrides; tuning knob).
@@ -511,7 +517,7 @@ inline bool make_staged_geom(uint32_t P, const PCols &cols, bool perm, bool crc,
 
 // NC8 > 0: compile-time fast path for exactly NC8 columns of 8 bytes (keys, payloads); the
 // column loops unroll and no per-row width switch remains.  NC8 == 0: any widths.
-template <typename Sel, typename Pred, int NC8, bool AOS = false>
+template <typename Sel, typename Pred, int NC8, bool AOS = false, bool TILED = false>
 __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, Pred pred, PartLayout L,
                                                                    const uint64_t *offs, PCols cols, uint32_t *perm,
                                                                    StagedGeom g) {
@@ -524,7 +530,8 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
     uint32_t *sperm = reinterpret_cast<uint32_t *>(lds + g.perm_off);
     uint32_t(*crc)[256] = reinterpret_cast<uint32_t(*)[256]>(lds + g.crc_off);
     uint32_t *red = reinterpret_cast<uint32_t *>(lds + g.red_off); // ST_T/64 + 1 words
-    for (uint32_t p = threadIdx.x; p < P; p += ST_T) run[p] = offs[(int64_t)p * L.G + blockIdx.x];
+    if constexpr (!TILED)
+        for (uint32_t p = threadIdx.x; p < P; p += ST_T) run[p] = offs[(int64_t)p * L.G + blockIdx.x];
     if constexpr (Sel::needs_crc) load_crc_lds(crc);
     // row indices fit 32 bits (the ABI caps n below 2^32)
     const uint32_t begin = (uint32_t)((int64_t)blockIdx.x * L.seg);
@@ -608,6 +615,9 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
         }
         __syncthreads();
         const uint32_t kept = red[ST_T / 64];
+        const uint32_t tile = blockIdx.x * (uint32_t)g.tps + (tb - begin) / (uint32_t)g.TR;
+        if constexpr (TILED)
+            for (uint32_t p = threadIdx.x; p < P; p += ST_T) g.tile_hist[(size_t)p * g.T + tile] = start[p] | (hist[p] << 16);
         // 3. place rows in LDS in destination order
         uint32_t sl[ST_MAXR];
         if (g.dbg == 2) {
@@ -665,7 +675,9 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
         // 4. stream the sorted tile out: lanes of a run write consecutive addresses
         for (uint32_t s = threadIdx.x; s < (g.dbg == 1 || g.dbg == 2 ? 0u : kept); s += ST_T) {
             const uint32_t b = sb[s];
-            const uint64_t gp = g.dbg == 3 ? (uint64_t)(tb + s) : run[b] + (s - start[b]);
+            uint64_t gp;
+            if constexpr (TILED) gp = (uint64_t)tile * (uint32_t)g.TR + s;
+            else gp = g.dbg == 3 ? (uint64_t)(tb + s) : run[b] + (s - start[b]);
             if (perm) perm[gp] = sperm[s];
             if constexpr (AOS && NC8 == 2) { // one 16-byte record store per row
                 const uint64_t a0 = reinterpret_cast<const uint64_t *>(lds + g.stage_off[0])[s];
@@ -697,7 +709,8 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
             }
         }
         __syncthreads();
-        for (uint32_t p = threadIdx.x; p < P; p += ST_T) run[p] += hist[p];
+        if constexpr (!TILED)
+            for (uint32_t p = threadIdx.x; p < P; p += ST_T) run[p] += hist[p];
         __syncthreads();
     }
 }
@@ -822,6 +835,50 @@ int run_partition(Ctx *ctx, const Sel &sel, const RowPred &pred, const PartLayou
         TFG_LAUNCH_CHECK();
     }
     return TFG_OK;
+}
+
+// Tile-sorted partition (no histogram pass, no scattered stores): every tile of TR rows is
+// counting-sorted by destination in LDS and written back contiguously to its own slot; the
+// per-(destination, tile) start | count table tells a destination's consumer where its runs are.
+// Used where the consumer reads a destination's rows once (the aggregation bucket kernel):
+// it replaces the histogram pass (16 B / row) and the scatter's ~P-way store pattern.
+struct TiledGeom {
+    StagedGeom sg;
+    PartLayout L;
+    int64_t out_rows; // T * TR
+};
+
+inline bool make_tiled_geom(Ctx *ctx, int64_t n, uint32_t P, const PCols &cols, TiledGeom &tg) {
+    if (n <= 0 || !make_staged_geom(P, cols, false, false, tg.sg)) return false;
+    tg.L = make_wide_layout(n, P, ctx->cu_count, 1u << 30);
+    tg.sg.tps = (int)((tg.L.seg + tg.sg.TR - 1) / tg.sg.TR);
+    tg.sg.T = (int)tg.L.G * tg.sg.tps;
+    tg.out_rows = (int64_t)tg.sg.T * tg.sg.TR;
+    return true;
+}
+
+template <typename Sel>
+int run_partition_tiled(Ctx *ctx, const Sel &sel, const RowPred &pred, TiledGeom tg, const PCols &cols,
+                        uint32_t *tile_hist, const char *name) {
+    tg.sg.tile_hist = tile_hist;
+    int nc8 = cols.ncols;
+    for (int c = 0; c < cols.ncols; ++c)
+        if (cols.width[c] != 8) nc8 = 0;
+    TFG_CHECK(cols.aos && (nc8 == 2 || nc8 == 3), TFG_ERR_INVALID_ARG, "tiled partition needs 2-3 word records");
+    ProfScope _ps(ctx, name);
+    return with_pred(pred, [&](auto pr) -> int {
+        using PR = decltype(pr);
+        if (nc8 == 2)
+            hipLaunchKernelGGL((part_scatter_staged_kernel<Sel, PR, 2, true, true>), dim3(tg.L.G), dim3(ST_T),
+                               tg.sg.lds_bytes, ctx->stream, sel, pr, tg.L, (const uint64_t *)nullptr, cols,
+                               (uint32_t *)nullptr, tg.sg);
+        else
+            hipLaunchKernelGGL((part_scatter_staged_kernel<Sel, PR, 3, true, true>), dim3(tg.L.G), dim3(ST_T),
+                               tg.sg.lds_bytes, ctx->stream, sel, pr, tg.L, (const uint64_t *)nullptr, cols,
+                               (uint32_t *)nullptr, tg.sg);
+        TFG_LAUNCH_CHECK();
+        return TFG_OK;
+    });
 }
 
 } // namespace tfg
