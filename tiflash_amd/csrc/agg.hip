@@ -794,9 +794,10 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
     extern __shared__ __attribute__((aligned(16))) char lds[];
     __shared__ unsigned long long s_red[BT / 64];
     __shared__ unsigned long long s_base[2];
-    constexpr int CH = 128; // tiles per pass-0 chunk
+    constexpr int CH = BT; // tiles per pass-0 chunk: one per thread
     __shared__ uint32_t s_ent[CH];
     __shared__ uint32_t s_pref[CH + 1];
+    __shared__ uint32_t s_wsum[BT / 64];
     Table T(lds, S);
     const Ops ops{S, mode};
     const int b = blockIdx.x;
@@ -876,22 +877,25 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
         };
         if (pass == 0) {
             // chunks of CH tiles: their runs are concatenated (prefix of the counts in LDS) and
-            // row i of the chunk finds its tile by a 7-step binary search, so every thread
+            // row i of the chunk finds its tile by a log2(CH)-step binary search, so every thread
             // takes RPT rows per step whatever the run lengths
             for (int t0 = 0; t0 < tin.T; t0 += CH) {
-                if (threadIdx.x < CH) s_ent[threadIdx.x] = t0 + (int)threadIdx.x < tin.T ? col[t0 + threadIdx.x] : 0u;
-                __syncthreads();
-                if (threadIdx.x < 64) {
-                    const uint32_t c0 = s_ent[2 * threadIdx.x] >> 16, c1 = s_ent[2 * threadIdx.x + 1] >> 16;
-                    uint32_t x = c0 + c1;
+                const uint32_t e = t0 + (int)threadIdx.x < tin.T ? col[t0 + threadIdx.x] : 0u;
+                s_ent[threadIdx.x] = e;
+                { // block-wide exclusive scan of the run lengths
+                    const uint32_t c = e >> 16;
+                    uint32_t x = c;
 #pragma unroll
                     for (int d = 1; d < 64; d <<= 1) {
                         const uint32_t y = __shfl_up(x, d, 64);
-                        if ((int)threadIdx.x >= d) x += y;
+                        if ((int)(threadIdx.x & 63) >= d) x += y;
                     }
-                    s_pref[2 * threadIdx.x] = x - c0 - c1;
-                    s_pref[2 * threadIdx.x + 1] = x - c1;
-                    if (threadIdx.x == 63) s_pref[CH] = x;
+                    if ((threadIdx.x & 63) == 63) s_wsum[threadIdx.x >> 6] = x;
+                    __syncthreads();
+                    uint32_t off = 0;
+                    for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) off += s_wsum[w];
+                    s_pref[threadIdx.x] = off + x - c;
+                    if (threadIdx.x == CH - 1) s_pref[CH] = off + x;
                 }
                 __syncthreads();
                 const uint32_t tot = s_pref[CH];

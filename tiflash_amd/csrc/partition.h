@@ -265,11 +265,12 @@ inline PartLayout make_layout(int64_t n, uint32_t P) {
 // each other's partially written cache lines while they are still in L2) and the P x G count
 // table stays small; the histogram pass splits each segment over `sub` workgroups to keep the
 // chip full.
-inline PartLayout make_wide_layout(int64_t n, uint32_t P, int cu_count, unsigned gmax) {
-    static const int mult = [] {
+inline PartLayout make_wide_layout(int64_t n, uint32_t P, int cu_count, unsigned gmax, int mult_default = 1) {
+    static const int env_mult = [] {
         const char *e = getenv("TFG_STAGE_G");
-        return e ? std::max(1, atoi(e)) : 1;
+        return e ? std::max(1, atoi(e)) : 0;
     }();
+    const int mult = env_mult ? env_mult : mult_default;
     PartLayout L;
     L.n = n;
     L.P = P;
@@ -850,7 +851,7 @@ struct TiledGeom {
 
 inline bool make_tiled_geom(Ctx *ctx, int64_t n, uint32_t P, const PCols &cols, TiledGeom &tg) {
     if (n <= 0 || !make_staged_geom(P, cols, false, false, tg.sg)) return false;
-    tg.L = make_wide_layout(n, P, ctx->cu_count, 1u << 30);
+    tg.L = make_wide_layout(n, P, ctx->cu_count, 1u << 30, 3); // 3 segments per CU: measured 0.77 vs 0.83 ms at 1
     tg.sg.tps = (int)((tg.L.seg + tg.sg.TR - 1) / tg.sg.TR);
     tg.sg.T = (int)tg.L.G * tg.sg.tps;
     tg.out_rows = (int64_t)tg.sg.T * tg.sg.TR;
