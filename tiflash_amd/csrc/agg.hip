@@ -911,7 +911,9 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
 #pragma unroll
                         for (uint32_t st = CH / 2; st > 0; st >>= 1)
                             if (s_pref[lo + st] <= i) lo += st;
-                        const int64_t r = (int64_t)(t0 + (int)lo) * tin.TR + (s_ent[lo] & 0xFFFFu) + (i - s_pref[lo]);
+                        int64_t r = (int64_t)(t0 + (int)lo) * tin.TR + (s_ent[lo] & 0xFFFFu) + (i - s_pref[lo]);
+                        if (S.dbg == 5) r = (int64_t)b * 390000 + (int64_t)t0 * 30 + i; // ablation: contiguous reads
+                        if (S.dbg == 6) r = (int64_t)t0 * tin.TR + i;                    // ablation: no search dependency
                         ops.load(src, r, v[u]);
                     }
                     step(v, ok);
