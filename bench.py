@@ -52,11 +52,13 @@ def parse():
 # algorithmic HBM bytes per row for each kernel of the pipeline:
 #   agg.part.hist    reads k, f                       16 B per input row
 #   agg.part.scatter reads k, v, f; writes k, v        24 B per input row + 16 B per kept row
+#   agg.part.tiled   same bytes as agg.part.scatter (tile-sorted partition, no histogram pass)
 #   agg.bucket       reads the staged k, v            16 B per kept row
 def kernel_bytes(name, n_in, n_kept):
     return {
         "agg.part.hist": 16 * n_in,
         "agg.part.scatter": 24 * n_in + 16 * n_kept,
+        "agg.part.tiled": 24 * n_in + 16 * n_kept,
         "agg.bucket": 16 * n_kept,
         "join.part.hist": 8 * n_in,
         "join.part.scatter": 8 * n_in + 12 * n_in,

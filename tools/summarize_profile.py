@@ -7,11 +7,11 @@ Outputs
   profiles/pmc_traffic.json         HBM bytes per launch per pipeline kernel (bench.py's roofline.traffic)
 
 HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_SIZE come from separate --pmc passes.
-FETCH_SIZE is exact only after a calibration for the access width (the guide: ½ for 16-B/lane
-streaming reads; other widths uncalibrated), so the factor is measured here on a kernel with a
-known byte count in the same run: agg.part.hist reads exactly the predicate and key columns
-(16 B per input row, 8-B/lane loads) — factor = 16 * rows / FETCH_SIZE(hist).  WRITE_SIZE is used
-as reported (exact for the 16-B/lane record stores of the scatter).
+FETCH_SIZE reports exactly half the bytes of wide coalesced streaming reads on gfx950 (the guide's
+HBM/rocprofv3 section), so it is doubled.  The factor was cross-checked on a kernel with a known
+byte count (agg.part.hist, 16 B per input row: measured 2.000, r01); when that kernel is in the
+run it is re-measured and reported next to the guide's factor.  WRITE_SIZE is used as reported
+(exact for 16-B/lane streaming stores, the record stores of the partition).
 """
 import argparse
 import collections
@@ -30,9 +30,11 @@ NAME_MAP = [
     (r"agg_bucket_kernel<tfg::WideOps", "agg.wide.bucket"),
     (r"pack_keys_kernel", "agg.pack_keys"),
     (r"part_hist_kernel<tfg::SelBucket", "agg.part.hist"),
+    (r"part_scatter_staged_kernel<tfg::SelBucket.*true, true>", "agg.part.tiled"),
     (r"part_scatter_staged_kernel<tfg::SelBucket", "agg.part.scatter"),
     (r"part_scatter_kernel<tfg::SelBucket", "agg.part.scatter"),
     (r"agg_bucket_kernel", "agg.bucket"),
+    (r"agg_bucket_tiled_kernel", "agg.bucket"),
     (r"agg_compact_kernel", "agg.compact"),
     (r"agg_result_kernel", "agg.result"),
     (r"scan_", "scan"),
@@ -92,11 +94,12 @@ def main():
     # FETCH_SIZE / WRITE_SIZE are in KB (rocprofv3 derived counters)
     fetch = {k: v * 1024 for k, v in fetch.items()}
     write = {k: v * 1024 for k, v in write.items()}
-    known = 16 * a.rows
-    factor = known / fetch["agg.part.hist"] if fetch.get("agg.part.hist") else 1.0
-    alg = {"agg.part.hist": 16 * a.rows, "agg.part.scatter": 24 * a.rows + 16 * kept, "agg.bucket": 16 * kept}
-    traffic = {"_calibration": {"fetch_factor": round(factor, 4),
-                                "basis": "agg.part.hist reads 16 B/row (f, k) with 8-B/lane loads",
+    factor = 2.0  # MI355X_MICROARCH.md: FETCH_SIZE = 1/2 of the bytes of wide streaming reads
+    measured = 16 * a.rows / fetch["agg.part.hist"] if fetch.get("agg.part.hist") else None
+    alg = {"agg.part.hist": 16 * a.rows, "agg.part.scatter": 24 * a.rows + 16 * kept,
+           "agg.part.tiled": 24 * a.rows + 16 * kept, "agg.bucket": 16 * kept}
+    traffic = {"_calibration": {"fetch_factor": factor, "basis": "MI355X_MICROARCH.md HBM section (x2 on gfx950)",
+                                "measured_on_agg_part_hist": round(measured, 4) if measured else None,
                                 "rows": a.rows, "kept": kept}}
     for k in sorted(set(fetch) | set(write)):
         fb = fetch.get(k, 0.0) * factor
@@ -122,7 +125,7 @@ def main():
         f.write("| kernel | calls | avg ms | total ms | % |\n|---|---|---|---|---|\n")
         for name, calls, avg, tot, pct in sorted(rows, key=lambda x: -x[3])[:20]:
             f.write(f"| {name} | {calls} | {avg:.4f} | {tot:.3f} | {pct:.1f} |\n")
-        f.write(f"\nFETCH calibration factor (known 16 B/row of agg.part.hist): {factor:.3f}\n\n")
+        f.write(f"\nFETCH_SIZE factor {factor} (guide); re-measured on agg.part.hist: {measured}\n\n")
         f.write("| kernel | fetch B/launch (corrected) | write B/launch | HBM B/launch | algorithmic B |\n|---|---|---|---|---|\n")
         for k, v in sorted(traffic.items()):
             if k.startswith("_"):
