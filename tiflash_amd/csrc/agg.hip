@@ -899,9 +899,10 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
                 }
                 __syncthreads();
                 const uint32_t tot = s_pref[CH];
-                for (uint32_t base = 0; base < tot; base += BT * RPT) {
-                    typename Ops::Row v[RPT];
-                    bool ok[RPT];
+                // software pipeline: the next step's rows are loaded (address search + global
+                // loads issued) before this step's LDS probe / atomics, so HBM latency overlaps
+                // the table work instead of following it after every step barrier
+                auto load_step = [&](uint32_t base, typename Ops::Row (&v)[RPT], bool (&ok)[RPT]) {
 #pragma unroll
                     for (int u = 0; u < RPT; ++u) {
                         const uint32_t i = base + u * BT + threadIdx.x;
@@ -915,6 +916,25 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
                         if (S.dbg == 5) r = (int64_t)b * 390000 + (int64_t)t0 * 30 + i; // ablation: contiguous reads
                         if (S.dbg == 6) r = (int64_t)t0 * tin.TR + i;                    // ablation: no search dependency
                         ops.load(src, r, v[u]);
+                    }
+                };
+                typename Ops::Row vn[RPT];
+                bool okn[RPT];
+                if (tot > 0) load_step(0, vn, okn);
+                for (uint32_t base = 0; base < tot; base += BT * RPT) {
+                    typename Ops::Row v[RPT];
+                    bool ok[RPT];
+#pragma unroll
+                    for (int u = 0; u < RPT; ++u) {
+                        v[u] = vn[u];
+                        ok[u] = okn[u];
+                    }
+                    if (base + BT * RPT < tot) load_step(base + BT * RPT, vn, okn);
+                    if (S.dbg == 1) { // timing ablation: search + loads only
+#pragma unroll
+                        for (int u = 0; u < RPT; ++u)
+                            if (ok[u] && ops.key(v[u]) == 0x5555555555555555ull) T.ctrl->out_count += ops.probe_val(v[u]);
+                        continue;
                     }
                     step(v, ok);
                 }
