@@ -360,6 +360,45 @@ int tfg_alltoall_counts(tfg_comm *comm, const uint64_t *send_bytes_host, uint64_
 int tfg_alltoallv(tfg_comm *comm, const void *send, const uint64_t *send_bytes, const uint64_t *send_displs,
                   void *recv, const uint64_t *recv_bytes, const uint64_t *recv_displs);
 
+/* ---------------------------------------------------------------- (f1) MPP packet codec */
+/* The Block wire format of MPP packets, encoded from / decoded into device columns; the packet
+ * itself is a device buffer (the tunnel moves its bytes).
+ *   TFG_CODEC_CHBLOCK: CHBlockChunkCodecStream::encode / CHBlockChunkCodec::decode
+ *                      (Flash/Coprocessor/CHBlockChunkCodec.cpp:134-258).
+ *   TFG_CODEC_V1:      CHBlockChunkCodecV1::encode / decode with CompressionMethod::NONE
+ *                      (Flash/Coprocessor/CHBlockChunkCodecV1.cpp:370-432, 567-583); decode accepts
+ *                      packets of several parts (decodeColumnsByBlock, :97-142).  LZ4 / ZSTD
+ *                      packets return TFG_ERR_NOT_IMPLEMENTED.
+ * Type names as on the wire (IDataType::getName): Int8..Int64, UInt8..UInt64, Float32, Float64,
+ * Decimal(P,S) with P <= 38, MyDate, MyDateTime(n), MyDuration(n), String (size-prefixed rows),
+ * StringV2 (sizes, then chars), and Nullable(...) of each.  Column data follows the tfg_type
+ * payloads above; String columns pass chars in `data` and end offsets in `offsets`. */
+#define TFG_CODEC_CHBLOCK 0
+#define TFG_CODEC_V1 1
+typedef struct tfg_codec_column {
+    const char *name;       /* host string */
+    const char *type_name;  /* host string, e.g. "Nullable(Decimal(15,2))" */
+    const void *data;       /* device: values, or String chars */
+    const uint64_t *offsets; /* device: String end offsets */
+    const uint8_t *nullmap; /* device: Nullable null map */
+} tfg_codec_column;
+/* Encodes n rows of ncols columns into `out` (device, `capacity` bytes).  out == NULL: returns
+ * the exact packet size in *out_bytes_host only.  Synchronises the context stream. */
+int tfg_codec_encode(tfg_ctx *ctx, int version, int ncols, const tfg_codec_column *cols, int64_t n, uint8_t *out,
+                     size_t capacity, size_t *out_bytes_host);
+/* Decoding: tfg_codec_decode parses the header and locates every column's data (String rows are
+ * found on the device); then tfg_codec_column_info gives each column's name, type name, tfg_type,
+ * nullability and decoded String chars bytes (terminators included), and tfg_codec_column_read
+ * writes the column (values / chars + offsets / null map) into caller-provided device buffers.
+ * The packet buffer must stay alive until the packet is destroyed. */
+typedef struct tfg_codec_packet tfg_codec_packet;
+int tfg_codec_decode(tfg_ctx *ctx, int version, const uint8_t *packet, size_t bytes, tfg_codec_packet **out);
+int tfg_codec_packet_info(tfg_codec_packet *p, int *out_cols, int64_t *out_rows);
+int tfg_codec_column_info(tfg_codec_packet *p, int i, char *name, size_t name_len, char *type_name, size_t type_len,
+                          int *out_type, int *out_nullable, uint64_t *out_chars_bytes);
+int tfg_codec_column_read(tfg_codec_packet *p, int i, void *out_data, uint64_t *out_offsets, uint8_t *out_nullmap);
+int tfg_codec_packet_destroy(tfg_codec_packet *p);
+
 #ifdef __cplusplus
 }
 #endif

@@ -64,6 +64,8 @@ def lib():
         L.orc_join_ref_probe.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                          ctypes.c_int, ctypes.c_void_p]
         L.orc_join_ref_destroy.argtypes = [ctypes.c_void_p]
+        L.orc_codec_encode.restype = ctypes.c_size_t
+        L.orc_codec_decode_strings.restype = ctypes.c_size_t
         _L = L
     return _L
 
@@ -378,3 +380,40 @@ def bench_join(build_keys, probe_keys, nthreads):
     m = lib().orc_bench_join(_p(build_keys), ctypes.c_size_t(len(build_keys)), _p(probe_keys),
                              ctypes.c_size_t(len(probe_keys)), nthreads, ctypes.byref(cs))
     return m, cs.value
+
+
+# ---- (f1) MPP packet codec (oracle/codec.c) --------------------------------------------------
+CODEC_CHBLOCK, CODEC_V1 = 0, 1
+
+
+def codec_encode(columns, n, version=CODEC_V1, part_rows=None) -> bytes:
+    """CHBlockChunkCodec(V1) encode of host columns: (name, type_name, data, offsets, nullmap)."""
+    nc = len(columns)
+    names = (ctypes.c_char_p * max(nc, 1))(*[c[0].encode() for c in columns])
+    types = (ctypes.c_char_p * max(nc, 1))(*[c[1].encode() for c in columns])
+    keep = [np.ascontiguousarray(x) if x is not None else None for c in columns for x in c[2:5]]
+    data = _ptrs([keep[3 * i] for i in range(nc)])
+    offs = _ptrs([keep[3 * i + 1] for i in range(nc)])
+    nms = _ptrs([keep[3 * i + 2] for i in range(nc)])
+    np_ = len(part_rows) if part_rows else 0
+    pr = (ctypes.c_int64 * max(np_, 1))(*(part_rows or [0]))
+    L = lib()
+    size = L.orc_codec_encode(version, nc, names, types, data, offs, nms, ctypes.c_int64(n), np_, pr, None,
+                              ctypes.c_size_t(0))
+    assert size != ctypes.c_size_t(-1).value, "unsupported type"
+    out = np.zeros(max(size, 1), np.uint8)
+    got = L.orc_codec_encode(version, nc, names, types, data, offs, nms, ctypes.c_int64(n), np_, pr, _p(out),
+                             ctypes.c_size_t(out.size))
+    assert got == size
+    return out[:size].tobytes()
+
+
+def codec_decode_strings(buf: bytes, rows: int, chars_cap: int):
+    """Legacy String bulk decode -> (chars with terminators, end offsets, bytes consumed)."""
+    src = np.frombuffer(buf, np.uint8)
+    chars = np.zeros(max(chars_cap, 1), np.uint8)
+    offs = np.zeros(max(rows, 1), np.uint64)
+    used = lib().orc_codec_decode_strings(_p(src), ctypes.c_size_t(src.size), ctypes.c_int64(rows), _p(chars),
+                                          _p(offs))
+    assert used != ctypes.c_size_t(-1).value, "truncated"
+    return chars[:int(offs[rows - 1]) if rows else 0], offs[:rows], used

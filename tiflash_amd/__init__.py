@@ -61,6 +61,9 @@ def lib() -> ctypes.CDLL:
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+        # torch first: the library then binds to the HIP runtime torch already loaded (one
+        # runtime per process; loading ours first made torch see no device)
+        import torch  # noqa: F401
         L = ctypes.CDLL(LIB_PATH)
         L.tfg_last_error.restype = ctypes.c_char_p
         L.tfg_version.restype = ctypes.c_char_p
@@ -614,3 +617,72 @@ class Join:
             self.close()
         except Exception:
             pass
+
+
+# ---- (f1) MPP packet codec: CHBlockChunkCodec / CHBlockChunkCodecV1 --------------------------
+CODEC_CHBLOCK, CODEC_V1 = 0, 1
+
+
+class _CodecColumn(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char_p), ("type_name", ctypes.c_char_p), ("data", ctypes.c_void_p),
+                ("offsets", ctypes.c_void_p), ("nullmap", ctypes.c_void_p)]
+
+
+def codec_encode(ctx: Context, columns: Sequence, n: int, version: int = CODEC_V1):
+    """CHBlockChunkCodec(V1)::encode of a Block held on the device.
+
+    columns: sequence of (name, type_name, data, offsets, nullmap) — data / offsets / nullmap are
+    device tensors (offsets and nullmap may be None).  Returns the packet as a uint8 device tensor.
+    """
+    import torch
+    arr = (_CodecColumn * max(len(columns), 1))()
+    for i, (name, tname, data, offs, nm) in enumerate(columns):
+        arr[i] = _CodecColumn(name.encode(), tname.encode(), _p(data).value, _p(offs).value, _p(nm).value)
+    size = ctypes.c_size_t()
+    check(lib().tfg_codec_encode(ctx.h, version, len(columns), arr, ctypes.c_int64(n), None, ctypes.c_size_t(0),
+                                 ctypes.byref(size)))
+    dev = columns[0][2].device if columns and columns[0][2] is not None else torch.device("cuda", ctx.device)
+    out = torch.empty(max(size.value, 1), dtype=torch.uint8, device=dev)
+    check(lib().tfg_codec_encode(ctx.h, version, len(columns), arr, ctypes.c_int64(n), _p(out),
+                                 ctypes.c_size_t(out.numel()), ctypes.byref(size)))
+    return out[:size.value]
+
+
+def codec_decode(ctx: Context, packet, version: int = CODEC_V1):
+    """CHBlockChunkCodec(V1)::decode of a device packet -> (rows, [column dicts]).
+
+    Each column: {"name", "type_name", "type", "data", "offsets" (String), "nullmap" (Nullable)}."""
+    import torch
+    h = ctypes.c_void_p()
+    check(lib().tfg_codec_decode(ctx.h, version, _p(packet), ctypes.c_size_t(packet.numel()), ctypes.byref(h)))
+    try:
+        nc, rows = ctypes.c_int(), ctypes.c_int64()
+        check(lib().tfg_codec_packet_info(h, ctypes.byref(nc), ctypes.byref(rows)))
+        n = rows.value
+        cols = []
+        name, tname = ctypes.create_string_buffer(256), ctypes.create_string_buffer(256)
+        for i in range(nc.value):
+            t, nl, cb = ctypes.c_int(), ctypes.c_int(), ctypes.c_uint64()
+            check(lib().tfg_codec_column_info(h, i, name, 256, tname, 256, ctypes.byref(t), ctypes.byref(nl),
+                                              ctypes.byref(cb)))
+            dev = packet.device
+            if t.value == STRING:
+                data = torch.empty(max(cb.value, 1), dtype=torch.uint8, device=dev)
+                offs = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+            else:
+                dt = {INT8: torch.int8, INT16: torch.int16, INT32: torch.int32, INT64: torch.int64,
+                      UINT8: torch.uint8, UINT16: torch.int16, UINT32: torch.int32, UINT64: torch.int64,
+                      FLOAT32: torch.float32, FLOAT64: torch.float64, DECIMAL32: torch.int32,
+                      DECIMAL64: torch.int64}.get(t.value, torch.int64)
+                data = _alloc(max(n, 1), WIDTH[t.value], dev, dt)
+                offs = None
+            nm = torch.empty(max(n, 1), dtype=torch.uint8, device=dev) if nl.value else None
+            check(lib().tfg_codec_column_read(h, i, _p(data), _p(offs), _p(nm)))
+            cols.append({"name": name.value.decode(), "type_name": tname.value.decode(), "type": t.value,
+                         "data": data[:cb.value] if t.value == STRING else data[:n],
+                         "offsets": offs[:n] if offs is not None else None,
+                         "nullmap": nm[:n] if nm is not None else None})
+        torch.cuda.synchronize(packet.device)
+        return n, cols
+    finally:
+        lib().tfg_codec_packet_destroy(h)
