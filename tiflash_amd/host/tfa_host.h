@@ -352,6 +352,47 @@ private:
     int nranks_, rank_;
 };
 
+// ---------------------------------------------------------------- packet codec (f1)
+// CHBlockChunkCodec / CHBlockChunkCodecV1 (Flash/Coprocessor/CHBlockChunkCodec.cpp:134-258,
+// CHBlockChunkCodecV1.cpp:370-583) over tfg_codec_*: the packet is a device buffer.  Const
+// columns are materialised first (WriteColumnData).  Differences: compression NONE only (LZ4 /
+// ZSTD packets throw NOT_IMPLEMENTED); encode(vector<Block>) writes one part of the concatenated
+// rows (the reference writes one part per block; decode accepts both).
+struct DevicePacket {
+    DeviceBufferPtr buf;
+    size_t bytes = 0;
+    bool empty() const { return bytes == 0; }
+};
+
+class CHBlockChunkCodecV1 {
+public:
+    CHBlockChunkCodecV1(Context &ctx, Block header) : ctx_(ctx), header_(std::move(header)) {}
+    DevicePacket encode(const Block &block); // nothing (empty packet) when the block has no rows
+    DevicePacket encode(const std::vector<Block> &blocks);
+    static Block decode(Context &ctx, const Block &header, const DevicePacket &packet);
+    size_t encoded_rows = 0;
+    size_t original_size = 0;
+
+private:
+    Context &ctx_;
+    Block header_;
+};
+
+class CHBlockChunkCodec {
+public:
+    explicit CHBlockChunkCodec(Context &ctx, Block header = Block()) : ctx_(ctx), header_(std::move(header)) {}
+    DevicePacket encode(const Block &block); // CHBlockChunkCodecStream::encode
+    Block decode(const DevicePacket &packet) const;
+
+private:
+    Context &ctx_;
+    Block header_;
+};
+
+// shared by both codecs: version = TFG_CODEC_CHBLOCK / TFG_CODEC_V1
+DevicePacket encodeBlockPacket(Context &ctx, const Block &block, int version);
+Block decodeBlockPacket(Context &ctx, const Block &header, const uint8_t *packet, size_t bytes, int version);
+
 // ---------------------------------------------------------------- streams (IBlockInputStream)
 class IBlockInputStream {
 public:
