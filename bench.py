@@ -39,6 +39,7 @@ def parse():
     ap.add_argument("--no-join", action="store_true")
     ap.add_argument("--c5-rows", type=int, default=100_000_000, help="C5 String-key GROUP BY rows per GPU (0 = skip)")
     ap.add_argument("--c5-groups", type=int, default=10_000_000)
+    ap.add_argument("--codec-rows", type=int, default=20_000_000, help="packet codec leg rows (0 = skip)")
     ap.add_argument("--c4", type=int, default=-1, help="repartitioned join leg (configs[3]): 1 on, 0 off, -1 = on when N > 1")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -339,6 +340,73 @@ def c5_leg(args, ctx, dev, world, rank):
     return out
 
 
+def codec_leg(args, ctx, dev):
+    """§8 f1: CHBlockChunkCodecV1 (NONE) encode + decode of a C5-shaped block on the device:
+    String "k%08d" key (legacy size-prefixed String, the pre-V2 MPP packet form), Decimal(15,2)
+    value, Int64 row id.  value = rows / (encode + decode time); packet bytes per second beside it."""
+    import numpy as np
+    import torch
+
+    import tiflash_amd as tfa
+    n = args.codec_rows
+    g = torch.Generator(device=dev)
+    g.manual_seed(13)
+    ids = torch.randint(0, args.c5_groups, (n,), device=dev, generator=g, dtype=torch.int64)
+    chars = torch.empty((n, 10), dtype=torch.uint8, device=dev)
+    chars[:, 0] = ord("k")
+    x = ids.clone()
+    for j in range(8, 0, -1):
+        chars[:, j] = (48 + x % 10).to(torch.uint8)
+        x //= 10
+    chars[:, 9] = 0
+    chars = chars.reshape(-1)
+    offs = torch.arange(1, n + 1, device=dev, dtype=torch.int64) * 10
+    v = torch.randint(0, 10**9, (n,), device=dev, generator=g, dtype=torch.int64)
+    cols = [("k", "String", chars, offs, None), ("v", "Decimal(15,2)", v, None, None), ("id", "Int64", ids, None, None)]
+    res = {}
+    for label, tn in (("string", "String"), ("string_v2", "StringV2")):
+        cols[0] = ("k", tn, chars, offs, None)
+        for _ in range(2):
+            pkt = tfa.codec_encode(ctx, cols, n)
+            tfa.codec_decode(ctx, pkt)
+        te, td = [], []
+        for _ in range(max(args.steps, 3)):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            pkt = tfa.codec_encode(ctx, cols, n)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            rows, dec = tfa.codec_decode(ctx, pkt)
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            te.append(t1 - t0)
+            td.append(t2 - t1)
+        assert rows == n and torch.equal(dec[0]["offsets"], offs) and torch.equal(dec[2]["data"], ids)
+        e, d = statistics.median(te), statistics.median(td)
+        res[label] = {"encode_ms": round(e * 1e3, 3), "decode_ms": round(d * 1e3, 3),
+                      "packet_bytes": int(pkt.numel()), "rows_per_s": round(n / (e + d), 1),
+                      "packet_GBps": round(2 * pkt.numel() / (e + d) / 1e9, 1)}
+        del pkt, dec
+    out = {"metric": "rows/s CHBlockChunkCodecV1 encode + decode (String k%08d, Decimal(15,2), Int64)",
+           "value": res["string"]["rows_per_s"], "unit": "rows/s", "rows": n, "legs": res}
+    if not args.no_cpu:  # oracle/codec.c: the reference's serialisation restated, one host thread
+        from oracle import oracle as orc
+        m = min(n, 5_000_000)
+        hc = [("k", "String", chars[:m * 10].cpu().numpy(), offs[:m].cpu().numpy().astype(np.uint64), None),
+              ("v", "Decimal(15,2)", v[:m].cpu().numpy(), None, None), ("id", "Int64", ids[:m].cpu().numpy(), None, None)]
+        t0 = time.perf_counter()
+        pk = orc.codec_encode(hc, m)
+        t1 = time.perf_counter()
+        hdr = len(pk) - (m * 10 + 16 * m)  # fixed part of the packet before the String rows
+        orc.codec_decode_strings(pk[hdr:], m, m * 10)
+        t2 = time.perf_counter()
+        out["cpu_baseline"] = {"value": round(m / (t2 - t0), 1), "unit": "rows/s", "cores": 1, "kind": "port",
+                               "sample": f"{m} rows: oracle/codec.c encode of the 3 columns + legacy String decode "
+                                         f"(deserializeBinarySSE2 restated), one host thread"}
+    del chars, offs, v, ids
+    return out
+
+
 def main():
     args = parse()
     import torch
@@ -499,6 +567,8 @@ def main():
         c4 = c4_leg(args, ctx, dev, world, rank)
         if rank == 0:
             line["repartitioned_join"] = c4
+    if world == 1 and args.codec_rows > 0:
+        line["packet_codec"] = codec_leg(args, ctx, dev)
     if args.c5_rows > 0:
         c5 = c5_leg(args, ctx, dev, world, rank)
         if rank == 0:

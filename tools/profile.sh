@@ -9,7 +9,7 @@ TAG=${1:-r01}
 OUT=gpurun_out/prof_${TAG}
 export TMPDIR=/tmp
 mkdir -p "$OUT"
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run -f csv -- python3 bench.py --no-cpu --c5-rows 0 --c4 0 --steps 5 --warmup 2 > "$OUT/kt_bench.log" 2>&1
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/fetch" -o run -f csv -- python3 bench.py --no-cpu --no-join --c5-rows 0 --c4 0 --steps 2 --warmup 1 > "$OUT/fetch_bench.log" 2>&1
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/write" -o run -f csv -- python3 bench.py --no-cpu --no-join --c5-rows 0 --c4 0 --steps 2 --warmup 1 > "$OUT/write_bench.log" 2>&1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run -f csv -- python3 bench.py --no-cpu --c5-rows 0 --c4 0 --codec-rows 0 --steps 5 --warmup 2 > "$OUT/kt_bench.log" 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/fetch" -o run -f csv -- python3 bench.py --no-cpu --no-join --c5-rows 0 --c4 0 --codec-rows 0 --steps 2 --warmup 1 > "$OUT/fetch_bench.log" 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/write" -o run -f csv -- python3 bench.py --no-cpu --no-join --c5-rows 0 --c4 0 --codec-rows 0 --steps 2 --warmup 1 > "$OUT/write_bench.log" 2>&1
 echo PROFILE_DONE
