@@ -339,6 +339,11 @@ int tfg_join_build_rows(tfg_join *join, const void *keys, const uint8_t *key_nul
 int tfg_join_probe_rows(tfg_join *join, int kind, const void *keys, const uint8_t *key_nullmap, int64_t n, int npay,
                         const void *const *probe_pay, void *const *out_probe, void *const *out_build,
                         uint8_t *out_build_null, uint64_t capacity, uint64_t *out_count_host);
+/* Other conditions (Join::handleOtherConditions, Interpreters/Join.cpp:798-1150): after an
+ * INNER probe and the condition evaluated over the joined pairs, flags[probe_idx[i]] = 1 for
+ * every pair i with pass[i] != 0 (pass == NULL: every pair).  `flags` (one byte per probe row)
+ * is zeroed by the caller; the LEFT / SEMI / ANTI / left-outer-semi results follow from it. */
+int tfg_join_mark(tfg_ctx *ctx, const uint32_t *probe_idx, const uint8_t *pass, int64_t n_pairs, uint8_t *flags);
 /* Build-side statistics: rows inserted, distinct keys, partitions. */
 int tfg_join_stats(tfg_join *join, uint64_t *rows, uint64_t *partitions);
 

@@ -7,6 +7,8 @@
 // usage: test_host <repo_root> [test-name-substring]     (run by tests/test_gpu_host_cpp.py)
 #include <cmath>
 #include <cstdio>
+#include <optional>
+#include <random>
 #include <cstdlib>
 #include <fstream>
 #include <map>
@@ -667,6 +669,111 @@ TEST(ChunkCodecRoundTrip) {
     w.write(bn);
     w.flush();
     EXPECT(rows == 5);
+}
+
+// Join with other conditions: the reference's SemiJoin known answers for `t.a = s.a and
+// t.c < s.c` (gtest_join_executor.cpp:4400-4470: semi / anti / left-outer-semi /
+// anti-left-outer-semi), and INNER / LEFT with the condition against a nested-loop restatement
+// of Join::handleOtherConditions (NULL condition = no match).
+static ColumnPtr i32col(Context &ctx, const std::vector<std::optional<int32_t>> &v) {
+    std::vector<int32_t> x(v.size());
+    std::vector<uint8_t> nm(v.size());
+    for (size_t i = 0; i < v.size(); ++i) {
+        x[i] = v[i].value_or(0);
+        nm[i] = !v[i].has_value();
+    }
+    DataType t;
+    t.type = TFG_INT32;
+    return makeColumn(ctx, t, x.data(), v.size(), nm.data());
+}
+
+TEST(JoinOtherConditionKnownAnswers) {
+    using V = std::vector<std::optional<int32_t>>;
+    struct Case {
+        V la, lc, ra, rc;
+        std::vector<int> res;
+    };
+    const std::optional<int32_t> N;
+    const std::vector<Case> cases = {
+        {{1, 2, 3, 4, 5}, {1, 1, 1, 1, 1}, {1, 2, 3, 4, 5}, {2, 2, 2, 2, 2}, {1, 1, 1, 1, 1}},
+        {{1, 2, 3, 4, 5}, {1, 1, 1, 1, 1}, {6, 7, 8, 9, 10}, {2, 2, 2, 2, 2}, {0, 0, 0, 0, 0}},
+        {{1, 2, 3, 4, 5}, {1, 1, 1, 1, 1}, {}, {}, {0, 0, 0, 0, 0}},
+        {{1, 1, 2, 2}, {1, N, 2, N}, {1, 1, 1, 2, 2, 2}, {N, 1, 2, 2, N, 3}, {1, 0, 1, 0}},
+    };
+    DataType i32;
+    i32.type = TFG_INT32;
+    for (const Case &cs : cases) {
+        for (JoinKind kind : {JoinKind::Semi, JoinKind::Anti, JoinKind::LeftOuterSemi, JoinKind::AntiLeftOuterSemi}) {
+            Block left{{i32col(ctx, cs.la), i32, "a"}, {i32col(ctx, cs.lc), i32, "c"}};
+            Block right{{i32col(ctx, cs.ra), i32, "s_a"}, {i32col(ctx, cs.rc), i32, "s_c"}};
+            Join j(ctx, kind, "a", "s_a");
+            auto cond = std::make_shared<ExpressionActions>(ctx);
+            cond->compareColumns("c", TFG_LT, "s_c", "other_cond");
+            j.setOtherCondition(cond, "other_cond");
+            j.insertFromBlock(right);
+            j.finishOneBuild();
+            Block r = j.joinBlock(left);
+            std::vector<std::string> want_a;
+            std::vector<std::string> want_match;
+            for (size_t i = 0; i < cs.la.size(); ++i) {
+                const bool m = cs.res[i] == 1;
+                if (kind == JoinKind::Semi && m) want_a.push_back(std::to_string(*cs.la[i]));
+                if (kind == JoinKind::Anti && !m) want_a.push_back(std::to_string(*cs.la[i]));
+                if (kind == JoinKind::LeftOuterSemi) want_match.push_back(m ? "1" : "0");
+                if (kind == JoinKind::AntiLeftOuterSemi) want_match.push_back(m ? "0" : "1");
+            }
+            if (kind == JoinKind::Semi || kind == JoinKind::Anti) {
+                std::vector<std::string> got = cellStrings(ctx, *r.getByName("a").column);
+                std::sort(got.begin(), got.end());
+                std::sort(want_a.begin(), want_a.end());
+                EXPECT(got == want_a);
+            } else {
+                EXPECT(r.rows() == cs.la.size());
+                EXPECT(cellStrings(ctx, *r.getByName("match_helper").column) == want_match);
+            }
+        }
+    }
+}
+
+TEST(JoinOtherConditionMatchesNestedLoop) {
+    std::mt19937_64 rng(9);
+    const size_t np = 300, nb = 120;
+    std::vector<std::optional<int32_t>> pa(np), pc(np), ba(nb), bc(nb);
+    for (auto &x : pa) x = (int32_t)(rng() % 25);
+    for (auto &x : pc) x = rng() % 5 == 0 ? std::optional<int32_t>() : std::optional<int32_t>((int32_t)(rng() % 50));
+    for (auto &x : ba) x = (int32_t)(rng() % 25);
+    for (auto &x : bc) x = rng() % 5 == 0 ? std::optional<int32_t>() : std::optional<int32_t>((int32_t)(rng() % 50));
+    pa[3] = std::nullopt; // a NULL probe key: never matched (LEFT keeps it with a NULL build side)
+    DataType i32;
+    i32.type = TFG_INT32;
+    for (JoinKind kind : {JoinKind::Inner, JoinKind::Left}) {
+        Block left{{i32col(ctx, pa), i32, "a"}, {i32col(ctx, pc), i32, "c"}};
+        Block right{{i32col(ctx, ba), i32, "s_a"}, {i32col(ctx, bc), i32, "s_c"}};
+        Join j(ctx, kind, "a", "s_a");
+        auto cond = std::make_shared<ExpressionActions>(ctx);
+        cond->compareColumns("c", TFG_LT, "s_c", "other_cond");
+        j.setOtherCondition(cond, "other_cond");
+        j.insertFromBlock(right);
+        j.finishOneBuild();
+        Block r = j.joinBlock(left);
+        auto str = [](const std::optional<int32_t> &x) { return x ? std::to_string(*x) : std::string("N"); };
+        std::multiset<std::vector<std::string>> want, got;
+        for (size_t i = 0; i < np; ++i) {
+            bool any = false;
+            for (size_t b = 0; b < nb; ++b)
+                if (pa[i] && ba[b] && *pa[i] == *ba[b] && pc[i] && bc[b] && *pc[i] < *bc[b]) {
+                    want.insert({str(pa[i]), str(pc[i]), str(ba[b]), str(bc[b])});
+                    any = true;
+                }
+            if (!any && kind == JoinKind::Left) want.insert({str(pa[i]), str(pc[i]), "N", "N"});
+        }
+        auto ca = cellStrings(ctx, *materialize(ctx, r.getByName("a").column));
+        auto cc = cellStrings(ctx, *materialize(ctx, r.getByName("c").column));
+        auto sa = cellStrings(ctx, *materialize(ctx, r.getByName("s_a").column));
+        auto sc = cellStrings(ctx, *materialize(ctx, r.getByName("s_c").column));
+        for (size_t i = 0; i < r.rows(); ++i) got.insert({ca[i], cc[i], sa[i], sc[i]});
+        EXPECT(got == want);
+    }
 }
 
 int main(int argc, char **argv) {

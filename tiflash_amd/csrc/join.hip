@@ -336,6 +336,13 @@ __global__ void widen_keys_kernel(const void *in, int width, const uint8_t *key_
     }
 }
 
+// other conditions (Join::handleOtherConditions, Interpreters/Join.cpp:798-1150): a probe row
+// is matched when at least one of its key-equal pairs passes the condition
+__global__ void join_mark_kernel(const uint32_t *probe_idx, const uint8_t *pass, int64_t n, uint8_t *flags) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        if (!pass || pass[i]) flags[probe_idx[i]] = 1; // benign race: every writer stores 1
+}
+
 } // namespace tfg
 
 using namespace tfg;
@@ -633,6 +640,15 @@ int tfg_join_stats(tfg_join *j, uint64_t *rows, uint64_t *partitions) {
     TFG_CHECK(j, TFG_ERR_INVALID_ARG, "join is null");
     if (rows) *rows = (uint64_t)j->n_inserted;
     if (partitions) *partitions = j->P;
+    return TFG_OK;
+}
+
+int tfg_join_mark(tfg_ctx *ctx, const uint32_t *probe_idx, const uint8_t *pass, int64_t n_pairs, uint8_t *flags) {
+    TFG_CHECK(ctx && (n_pairs == 0 || (probe_idx && flags)), TFG_ERR_INVALID_ARG, "null argument");
+    if (n_pairs <= 0) return TFG_OK;
+    hipLaunchKernelGGL(join_mark_kernel, dim3(stream_grid(n_pairs, 256)), dim3(256), 0, ctx->stream, probe_idx, pass,
+                       n_pairs, flags);
+    TFG_LAUNCH_CHECK();
     return TFG_OK;
 }
 

@@ -202,8 +202,172 @@ uint64_t Join::buildRows() const {
     return rows;
 }
 
+void Join::setOtherCondition(ExpressionActionsPtr expr, std::string filter_column) {
+    other_cond_ = std::move(expr);
+    other_filter_ = std::move(filter_column);
+}
+
+// Rows of `block` where the device mask (UInt8, n rows) is set, in order (FilterTransformAction).
+static Block filterByMask(Context &ctx, const Block &block, DeviceBufferPtr mask, size_t n) {
+    static const std::string tmp = "__join_mark";
+    Block b = block;
+    DataType u8;
+    u8.type = TFG_UINT8;
+    auto m = std::make_shared<IColumn>();
+    m->type = u8;
+    m->rows = n;
+    m->data = std::move(mask);
+    b.insert({m, u8, tmp});
+    FilterTransformAction f(ctx, b.cloneEmpty(), nullptr, tmp);
+    FilterPtr none;
+    if (!f.transform(b, none, false)) { // nothing qualifies: zero-row columns of the same types
+        Block e;
+        for (const auto &c : block.getColumnsWithTypeAndName()) {
+            ColumnPtr g = gatherColumn(ctx, *c.column, nullptr, 0, false);
+            e.insert({g, g->type, c.name});
+        }
+        return e;
+    }
+    b.erase(b.getPositionByName(tmp));
+    return b;
+}
+
+// Join::handleOtherConditions (Interpreters/Join.cpp:798-1150), restated over device pairs: INNER
+// probe -> joined pairs -> condition (NULL = false) -> per probe row "some pair passed" flags
+// (tfg_join_mark) -> the kind's result.  Output order: passing pairs, then (LEFT) the unmatched
+// probe rows; compare unordered, as the reference's join tests do.
+Block Join::joinBlockWithCondition(const Block &probe_block) {
+    const size_t n = probe_block.rows();
+    ColumnPtr k = materialize(ctx_, probe_block.getByName(probe_key_).column);
+    uint64_t cap = std::max<uint64_t>(n, 1), count = 0;
+    DeviceBufferPtr pi, bi;
+    for (;;) {
+        pi = std::make_shared<DeviceBuffer>(ctx_, cap * 4);
+        bi = std::make_shared<DeviceBuffer>(ctx_, cap * 4);
+        const int rc = tfg_join_probe(join_, TFG_JOIN_INNER, k->dataPtr(), k->nullPtr(), (int64_t)n,
+                                      (uint32_t *)pi->data(), (uint32_t *)bi->data(), cap, nullptr, &count);
+        if (rc == TFG_ERR_CAPACITY) {
+            cap = count;
+            continue;
+        }
+        check(rc, "tfg_join_probe");
+        break;
+    }
+    // pairs joined, condition evaluated -> pass mask over the pairs (null = all pass)
+    DeviceBufferPtr pass;
+    Block joined;
+    for (const auto &c : probe_block.getColumnsWithTypeAndName()) {
+        ColumnPtr g = gatherColumn(ctx_, *c.column, (const uint32_t *)pi->data(), count, false);
+        joined.insert({g, g->type, c.name});
+    }
+    for (const auto &c : build_.getColumnsWithTypeAndName()) {
+        if (joined.has(c.name)) continue;
+        ColumnPtr g = gatherColumn(ctx_, *c.column, (const uint32_t *)bi->data(), count, false);
+        joined.insert({g, g->type, c.name});
+    }
+    if (other_cond_ && count) {
+        FilterTransformAction f(ctx_, joined.cloneEmpty(), other_cond_, other_filter_);
+        Block tmp = joined;
+        FilterPtr mask;
+        f.transform(tmp, mask, /*return_filter=*/true); // Nullable(UInt8) folded: v && !null
+        if (!tmp) { // constant false: no pair passes
+            pass = std::make_shared<DeviceBuffer>(ctx_, count);
+            std::vector<uint8_t> z(count, 0);
+            check(tfg_upload(ctx_.raw(), pass->data(), z.data(), count), "tfg_upload");
+        } else if (mask) {
+            pass = mask->data;
+        }
+    }
+    if (kind_ == JoinKind::Inner) {
+        if (!pass) return joined;
+        return filterByMask(ctx_, joined, pass, count);
+    }
+    auto flags = std::make_shared<DeviceBuffer>(ctx_, std::max<size_t>(n, 1));
+    std::vector<uint8_t> zeros(std::max<size_t>(n, 1), 0);
+    check(tfg_upload(ctx_.raw(), flags->data(), zeros.data(), zeros.size()), "tfg_upload");
+    check(tfg_join_mark(ctx_.raw(), (const uint32_t *)pi->data(), pass ? (const uint8_t *)pass->data() : nullptr,
+                        (int64_t)count, (uint8_t *)flags->data()),
+          "tfg_join_mark");
+    auto notflags = std::make_shared<DeviceBuffer>(ctx_, std::max<size_t>(n, 1));
+    if (n)
+        check(tfg_mask_logic(ctx_.raw(), TFG_NOT, (const uint8_t *)flags->data(), nullptr, (int64_t)n,
+                             (uint8_t *)notflags->data()),
+              "tfg_mask_logic");
+    ctx_.sync();
+    switch (kind_) {
+    case JoinKind::Semi: return filterByMask(ctx_, probe_block, flags, n);
+    case JoinKind::Anti: return filterByMask(ctx_, probe_block, notflags, n);
+    case JoinKind::LeftOuterSemi:
+    case JoinKind::AntiLeftOuterSemi: {
+        Block out = probe_block;
+        DataType i8;
+        i8.type = TFG_INT8;
+        i8.nullable = true;
+        auto m = std::make_shared<IColumn>();
+        m->type = i8;
+        m->rows = n;
+        m->data = kind_ == JoinKind::LeftOuterSemi ? flags : notflags;
+        m->nullmap = std::make_shared<DeviceBuffer>(ctx_, std::max<size_t>(n, 1));
+        check(tfg_upload(ctx_.raw(), m->nullmap->data(), zeros.data(), zeros.size()), "tfg_upload");
+        out.insert({m, i8, match_helper_});
+        ctx_.sync();
+        return out;
+    }
+    default: break;
+    }
+    // LEFT: passing pairs, then every probe row without one (build side NULL)
+    uint64_t kept = count;
+    DeviceBufferPtr pk = pi, bk = bi;
+    if (pass) {
+        pk = std::make_shared<DeviceBuffer>(ctx_, std::max<uint64_t>(count, 1) * 4);
+        bk = std::make_shared<DeviceBuffer>(ctx_, std::max<uint64_t>(count, 1) * 4);
+        const void *ins[2] = {pi->data(), bi->data()};
+        void *outs[2] = {pk->data(), bk->data()};
+        const int w[2] = {4, 4};
+        check(tfg_filter(ctx_.raw(), (const uint8_t *)pass->data(), (int64_t)count, 2, ins, w, outs, nullptr, &kept),
+              "tfg_filter");
+    }
+    std::vector<uint32_t> iota(std::max<size_t>(n, 1));
+    for (size_t i = 0; i < n; ++i) iota[i] = (uint32_t)i;
+    DeviceBuffer rows_dev(ctx_, iota.size() * 4);
+    check(tfg_upload(ctx_.raw(), rows_dev.data(), iota.data(), iota.size() * 4), "tfg_upload");
+    uint64_t unmatched = 0;
+    const uint64_t total_cap = kept + n;
+    auto pall = std::make_shared<DeviceBuffer>(ctx_, std::max<uint64_t>(total_cap, 1) * 4);
+    auto ball = std::make_shared<DeviceBuffer>(ctx_, std::max<uint64_t>(total_cap, 1) * 4);
+    if (kept) check(tfg_copy(ctx_.raw(), pall->data(), pk->data(), kept * 4), "tfg_copy");
+    if (kept) check(tfg_copy(ctx_.raw(), ball->data(), bk->data(), kept * 4), "tfg_copy");
+    {
+        const void *ins[1] = {rows_dev.data()};
+        void *outs[1] = {(uint8_t *)pall->data() + kept * 4};
+        const int w[1] = {4};
+        if (n)
+            check(tfg_filter(ctx_.raw(), (const uint8_t *)notflags->data(), (int64_t)n, 1, ins, w, outs, nullptr,
+                             &unmatched),
+                  "tfg_filter");
+    }
+    std::vector<uint32_t> none(std::max<uint64_t>(unmatched, 1), 0xFFFFFFFFu);
+    if (unmatched)
+        check(tfg_upload(ctx_.raw(), (uint8_t *)ball->data() + kept * 4, none.data(), unmatched * 4), "tfg_upload");
+    const uint64_t total = kept + unmatched;
+    Block out;
+    for (const auto &c : probe_block.getColumnsWithTypeAndName()) {
+        ColumnPtr g = gatherColumn(ctx_, *c.column, (const uint32_t *)pall->data(), total, false);
+        out.insert({g, g->type, c.name});
+    }
+    for (const auto &c : build_.getColumnsWithTypeAndName()) {
+        if (out.has(c.name)) continue;
+        ColumnPtr g = gatherColumn(ctx_, *c.column, (const uint32_t *)ball->data(), total, true);
+        out.insert({g, g->type, c.name});
+    }
+    ctx_.sync();
+    return out;
+}
+
 Block Join::joinBlock(const Block &probe_block) {
     if (!finished_) finishOneBuild();
+    if (other_cond_ || kind_ == JoinKind::LeftOuterSemi || kind_ == JoinKind::AntiLeftOuterSemi)
+        return joinBlockWithCondition(probe_block);
     const size_t n = probe_block.rows();
     ColumnPtr k = materialize(ctx_, probe_block.getByName(probe_key_).column);
     const bool pairs = kind_ == JoinKind::Inner || kind_ == JoinKind::Left;

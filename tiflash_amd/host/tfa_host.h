@@ -280,7 +280,17 @@ private:
 };
 
 // ---------------------------------------------------------------- hash join (a18-a21)
-enum class JoinKind { Inner = TFG_JOIN_INNER, Left = TFG_JOIN_LEFT, Semi = TFG_JOIN_SEMI, Anti = TFG_JOIN_ANTI };
+// Inner / Left / Semi / Anti map onto tfg_join_kind; LeftOuterSemi / AntiLeftOuterSemi (tipb
+// TypeLeftOuterSemiJoin / TypeAntiLeftOuterSemiJoin) return every probe row plus a Nullable(Int8)
+// match column and are derived on the host from an INNER probe + tfg_join_mark.
+enum class JoinKind {
+    Inner = TFG_JOIN_INNER,
+    Left = TFG_JOIN_LEFT,
+    Semi = TFG_JOIN_SEMI,
+    Anti = TFG_JOIN_ANTI,
+    LeftOuterSemi = 100,
+    AntiLeftOuterSemi = 101
+};
 
 class Join {
 public:
@@ -296,6 +306,11 @@ public:
     // where unmatched).  SEMI / ANTI return the probe columns of the qualifying rows.
     Block joinBlock(const Block &probe_block);
     uint64_t buildRows() const;
+    // JoinNonEqualConditions::other_cond_expr / other_cond_name (Interpreters/Join.cpp:798-1150):
+    // evaluated over the joined (probe + build) columns of every key-equal pair; NULL = false.
+    void setOtherCondition(ExpressionActionsPtr expr, std::string filter_column);
+    // LeftOuterSemi / AntiLeftOuterSemi: name of the match column (default "match_helper")
+    void setMatchHelperName(std::string name) { match_helper_ = std::move(name); }
 
 private:
     Context &ctx_;
@@ -307,6 +322,10 @@ private:
     std::vector<Block> build_blocks_;
     Block build_; // concatenated at finishOneBuild
     bool finished_ = false;
+    ExpressionActionsPtr other_cond_;
+    std::string other_filter_;
+    std::string match_helper_ = "match_helper";
+    Block joinBlockWithCondition(const Block &probe_block);
 };
 
 // ---------------------------------------------------------------- exchange (a22-a24, e)
