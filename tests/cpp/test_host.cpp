@@ -776,6 +776,82 @@ TEST(JoinOtherConditionMatchesNestedLoop) {
     }
 }
 
+// AutoPassThroughHashAggContext: the reference's state machine driven by three key
+// distributions (all-new keys -> PassThrough, few keys -> stays Init, half-known keys ->
+// Selective); pass-through blocks + the hash map's block, merged as the second stage would,
+// must equal a direct aggregation of the input.
+TEST(AutoPassThroughHashAgg) {
+    DataType i64, i32n;
+    i32n.type = TFG_INT32;
+    i32n.nullable = true;
+    Aggregator::Params p;
+    p.keys = {"k"};
+    p.aggregates = {{"sum", {"v"}, "sum_v"}, {"count", {"v"}, "cnt_v"}, {"count", {}, "cnt"}};
+    p.src_header = Block{{nullptr, i64, "k"}, {nullptr, i32n, "v"}};
+    const size_t B = 8192;
+    auto run = [&](int scenario, size_t blocks, size_t &pass_rows, std::set<int> &states) {
+        AutoPassThroughHashAggContext apt(ctx, p, /*row_limit_unit=*/B);
+        std::mt19937_64 rng(77 + scenario);
+        std::map<int64_t, std::tuple<int64_t, uint64_t, uint64_t, bool>> want; // sum, cnt_v, cnt, any non-null
+        std::vector<Block> out;
+        int64_t next_new = 0;
+        for (size_t bi = 0; bi < blocks; ++bi) {
+            std::vector<int64_t> k(B);
+            std::vector<int32_t> v(B);
+            std::vector<uint8_t> vn(B);
+            for (size_t i = 0; i < B; ++i) {
+                if (scenario == 0) k[i] = next_new++;                            // every key new
+                else if (scenario == 1) k[i] = (int64_t)(rng() % 1000);          // few keys
+                else k[i] = bi < 9 || rng() % 2 ? (bi < 9 ? next_new++ : (int64_t)(rng() % 70000)) : 1000000 + next_new++;
+                v[i] = (int32_t)(rng() % 1000) - 500;
+                vn[i] = rng() % 7 == 0;
+                auto &w = want[k[i]];
+                if (!vn[i]) {
+                    std::get<0>(w) += v[i];
+                    std::get<1>(w) += 1;
+                    std::get<3>(w) = true;
+                }
+                std::get<2>(w) += 1;
+            }
+            Block b{{makeColumn(ctx, i64, k.data(), B), i64, "k"}, {makeColumn(ctx, i32n, v.data(), B, vn.data()), i32n, "v"}};
+            apt.onBlock(b);
+            states.insert((int)apt.state());
+            while (Block r = apt.tryGetDataInAdvance()) out.push_back(r);
+        }
+        if (Block h = apt.getDataFromHashTable()) out.push_back(h);
+        pass_rows = apt.passThroughRows();
+        std::map<int64_t, std::tuple<int64_t, uint64_t, uint64_t, bool>> got;
+        for (const Block &b : out) {
+            auto kk = toHost<int64_t>(ctx, *materialize(ctx, b.getByName("k").column));
+            auto sc = b.getByName("sum_v").column;
+            auto ss = toHost<int64_t>(ctx, *sc);
+            auto sn = toHostNullMap(ctx, *sc);
+            auto c1 = toHost<uint64_t>(ctx, *materialize(ctx, b.getByName("cnt_v").column));
+            auto c2 = toHost<uint64_t>(ctx, *materialize(ctx, b.getByName("cnt").column));
+            for (size_t i = 0; i < kk.size(); ++i) {
+                auto &g = got[kk[i]];
+                if (!sn[i]) {
+                    std::get<0>(g) += ss[i];
+                    std::get<3>(g) = true;
+                }
+                std::get<1>(g) += c1[i];
+                std::get<2>(g) += c2[i];
+            }
+        }
+        EXPECT(got == want);
+    };
+    size_t pass = 0;
+    std::set<int> st;
+    run(0, 30, pass, st);
+    EXPECT(pass > 0 && st.count((int)AutoPassThroughHashAggContext::State::PassThrough));
+    st.clear();
+    run(1, 10, pass, st);
+    EXPECT(pass == 0 && st == std::set<int>{(int)AutoPassThroughHashAggContext::State::Init});
+    st.clear();
+    run(2, 30, pass, st);
+    EXPECT(pass > 0 && st.count((int)AutoPassThroughHashAggContext::State::Selective));
+}
+
 int main(int argc, char **argv) {
     g_root = argc > 1 ? argv[1] : ".";
     const char *filter = argc > 2 ? argv[2] : nullptr;

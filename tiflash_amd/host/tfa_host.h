@@ -371,6 +371,59 @@ private:
     int nranks_, rank_;
 };
 
+// ---------------------------------------------------------------- auto pass-through (f4)
+// AutoPassThroughHashAggContext (Operators/AutoPassThroughHashAggContext.{h,cpp}, design doc
+// docs/design/2024-08-07-auto-pass-through-hashagg.md): the first stage of a two-stage
+// aggregation decides at run time whether pre-aggregating pays.  Same states, thresholds and
+// switching rules: Init (until the hash map passes 2 MB) -> Adjust (insert, measure the hit
+// rate over normal_row_limit rows) -> PreHashAgg (hit rate >= 0.9) / PassThrough (<= 0.2) /
+// Selective (between: rows whose key is in the map are aggregated, the others pass through)
+// -> back to Adjust after normal / dynamic row limits (dynamic doubles up to 100 units).
+// Pass-through blocks carry the final-form columns of one row per group
+// (AutoPassThroughHashAggHelper.cpp): keys copied, sum(x) widened to the sum type (NULL kept),
+// count(x) = 0/1, count() = 1.  Differences: the hash-map byte size is restated from the group
+// count (16-byte cells at <= 50% load, as HashMap<UInt64, AggregateDataPtr>); Selective rows
+// are materialised (filtered) instead of flagged in Block::info.selective.
+class AutoPassThroughHashAggContext {
+public:
+    enum class State { Init, Adjust, PreHashAgg, PassThrough, Selective };
+    static constexpr size_t INIT_STATE_HASHMAP_THRESHOLD = 2 * 1024 * 1024;
+    static constexpr size_t MAX_DYNAMIC_UNIT_LIMIT = 100;
+    static constexpr double PassThroughRateLimit = 0.2;
+    static constexpr double PreHashAggRateLimit = 0.9;
+
+    AutoPassThroughHashAggContext(Context &ctx, const Aggregator::Params &params, uint64_t row_limit_unit,
+                                  uint64_t normal_unit_num = 1, uint64_t dynamic_unit_num = 5);
+    void onBlock(const Block &block, bool force_streaming = false);
+    Block tryGetDataInAdvance();  // the next pass-through block, or an empty Block
+    Block getDataFromHashTable(); // the hash map's final block (once; the map is then closed)
+    Block getHeader() const { return header_; }
+    State state() const { return state_; }
+    size_t hashMapBytes() const;
+    size_t passThroughRows() const { return pass_through_rows_; }
+    size_t aggregatedRows() const { return aggregated_rows_; }
+
+private:
+    Context &ctx_;
+    Aggregator::Params params_;
+    Aggregator agg_;
+    Block header_;
+    State state_ = State::Init;
+    size_t normal_row_limit_, dynamic_row_limit_, row_limit_unit_, max_dynamic_row_limit_;
+    size_t adjust_processed_rows_ = 0, adjust_hit_rows_ = 0, state_processed_rows_ = 0;
+    size_t pass_through_rows_ = 0, aggregated_rows_ = 0;
+    bool already_get_data_from_hash_table_ = false;
+    std::vector<Block> buffer_;
+    size_t buffer_head_ = 0;
+    std::unique_ptr<Join> lookup_; // Selective: the map's keys (LeftOuterSemi probe = "is in the map")
+    bool lookup_has_null_ = false;
+    void trySwitchFromInitState();
+    void trySwitchFromAdjustState(size_t total_rows, size_t hit_rows);
+    void trySwitchBackAdjustState(size_t block_rows);
+    Block getPassThroughBlock(const Block &block) const;
+    void buildLookup();
+};
+
 // ---------------------------------------------------------------- packet codec (f1)
 // CHBlockChunkCodec / CHBlockChunkCodecV1 (Flash/Coprocessor/CHBlockChunkCodec.cpp:134-258,
 // CHBlockChunkCodecV1.cpp:370-583) over tfg_codec_*: the packet is a device buffer.  Const
