@@ -228,6 +228,13 @@ int tfg_partition(tfg_ctx *ctx, const uint32_t *selector, int64_t n, uint32_t nu
  * materialise join results.  perm entries of 0xFFFFFFFF (-1) write a zero / default value. */
 int tfg_gather(tfg_ctx *ctx, const uint32_t *perm, int64_t n, int ncols, const void *const *cols, const int *widths,
                void *const *outs);
+/* String gather (ColumnString::insertFrom per joined row, Interpreters/JoinPartition.cpp:1290-1378;
+ * replicate of a String probe column): row r of the output is row perm[r] of (chars, offsets);
+ * perm 0xFFFFFFFF writes the default (empty) String.  Writes the n end offsets, then the chars
+ * when out_chars is non-NULL and they fit in chars_capacity (else TFG_ERR_CAPACITY);
+ * *out_chars_host = the output chars bytes (terminators included).  Synchronises. */
+int tfg_gather_string(tfg_ctx *ctx, const uint32_t *perm, int64_t n, const uint8_t *chars, const uint64_t *offsets,
+                      uint64_t *out_offsets, uint8_t *out_chars, uint64_t chars_capacity, uint64_t *out_chars_host);
 /* One-call HashBaseWriterHelper::scatterColumns (HashBaseWriterHelper.cpp:144-172) for
  * fixed-width key columns: weak hash over key_cols -> fillSelector(part_num) -> stable
  * partition -> gather of all `ncols` columns into outs (partition-major).  */
@@ -346,6 +353,24 @@ int tfg_join_probe_rows(tfg_join *join, int kind, const void *keys, const uint8_
 int tfg_join_mark(tfg_ctx *ctx, const uint32_t *probe_idx, const uint8_t *pass, int64_t n_pairs, uint8_t *flags);
 /* Build-side statistics: rows inserted, distinct keys, partitions. */
 int tfg_join_stats(tfg_join *join, uint64_t *rows, uint64_t *partitions);
+/* General join keys (chooseJoinMapMethod, Interpreters/JoinHashMap.cpp:33-116: keys128 / keys256
+ * for several fixed keys, key_strbin / key_strbinpadding for one String key by collator,
+ * serialized otherwise; HashMethodKeysFixed / HashMethodString / HashMethodSerialized,
+ * Common/ColumnsHashing.h:179-629).  tfg_join_key_hash folds each row's key tuple (fixed keys of
+ * 1-16 bytes as stored; String keys as the collator's sort key, any length) into a UInt64
+ * fingerprint; out_nullmap[i] = 1 when any key column is NULL (the row is then a NULL key, as
+ * extractNestedColumnsAndNullMap ORs the key null maps).  A join built and probed on the
+ * fingerprints yields candidate pairs; tfg_join_keys_equal writes out_pass[i] = pass_in[i] (1
+ * when pass_in is NULL) && the full key tuples of probe row probe_idx[i] and build row
+ * build_idx[i] are equal, so the verified pairs are exactly the reference's key-equal pairs.
+ * key_offsets[j] are String end offsets (NULL for fixed keys); out_pass may alias pass_in. */
+int tfg_join_key_hash(tfg_ctx *ctx, int nkeys, const int *key_types, const int *key_collators,
+                      const void *const *key_cols, const uint64_t *const *key_offsets,
+                      const uint8_t *const *key_nullmaps, int64_t n, uint64_t *out_keys, uint8_t *out_nullmap);
+int tfg_join_keys_equal(tfg_ctx *ctx, int nkeys, const int *key_types, const int *key_collators,
+                        const void *const *probe_cols, const uint64_t *const *probe_offsets,
+                        const void *const *build_cols, const uint64_t *const *build_offsets, const uint32_t *probe_idx,
+                        const uint32_t *build_idx, const uint8_t *pass_in, int64_t n_pairs, uint8_t *out_pass);
 
 /* ---------------------------------------------------------------- (e) exchange over RCCL */
 /* MPP ExchangeSender -> ExchangeReceiver repartition inside one node (HashPartitionWriter::

@@ -776,6 +776,116 @@ TEST(JoinOtherConditionMatchesNestedLoop) {
     }
 }
 
+// General join keys (§8 f2, chooseJoinMapMethod keys128 / key_strbinpadding / serialized,
+// JoinHashMap.cpp:33-116): two key columns (Int32, Nullable Int64) and one String key under the
+// binary and the padding collator (strings longer than 16 bytes, trailing spaces, empty), each
+// kind against a nested loop over the same rows.  A NULL in any key column never matches.
+TEST(JoinGeneralKeysMatchNestedLoop) {
+    std::mt19937_64 rng(21);
+    const size_t np = 400, nb = 150;
+    DataType i32, i64n, str{DataType::TYPE_STRING}, u8;
+    i32.type = TFG_INT32;
+    i64n.type = TFG_INT64;
+    i64n.nullable = true;
+    u8.type = TFG_UINT8;
+    std::vector<std::string> words = {"", "a", "a ", "a  ", "b", "k00000001", "k00000001 ",
+                                      "a fairly long join key over 16 bytes", "a fairly long join key over 16 bytez",
+                                      " a", "z"};
+    for (int collator : {-1 /* two fixed keys */, (int)TFG_COLLATOR_BINARY, (int)TFG_COLLATOR_BIN_PADDING}) {
+        const bool fixed = collator < 0;
+        std::vector<int32_t> pa(np), ba(nb);
+        std::vector<int64_t> pb(np), bb(nb);
+        std::vector<uint8_t> pbn(np), bbn(nb), ptag(np), btag(nb);
+        std::vector<std::string> ps(np), bs(nb);
+        for (size_t i = 0; i < np; ++i) {
+            pa[i] = (int32_t)(rng() % 6);
+            pb[i] = (int64_t)(rng() % 4) - 2;
+            pbn[i] = rng() % 10 == 0;
+            ps[i] = words[rng() % words.size()];
+            ptag[i] = (uint8_t)(i % 251);
+        }
+        for (size_t i = 0; i < nb; ++i) {
+            ba[i] = (int32_t)(rng() % 6);
+            bb[i] = (int64_t)(rng() % 4) - 2;
+            bbn[i] = rng() % 10 == 0;
+            bs[i] = words[rng() % words.size()];
+            btag[i] = (uint8_t)(i % 251);
+        }
+        auto trim = [&](std::string s) {
+            if (collator == TFG_COLLATOR_BIN_PADDING)
+                while (!s.empty() && s.back() == ' ') s.pop_back();
+            return s;
+        };
+        auto eq = [&](size_t i, size_t b) {
+            if (fixed) return !pbn[i] && !bbn[b] && pa[i] == ba[b] && pb[i] == bb[b];
+            return trim(ps[i]) == trim(bs[b]);
+        };
+        for (JoinKind kind : {JoinKind::Inner, JoinKind::Left, JoinKind::Semi, JoinKind::Anti}) {
+            Block left, right;
+            if (fixed) {
+                left = Block{{makeColumn(ctx, i32, pa.data(), np), i32, "a"},
+                             {makeColumn(ctx, i64n, pb.data(), np, pbn.data()), i64n, "b"},
+                             {makeColumn(ctx, u8, ptag.data(), np), u8, "ptag"}};
+                right = Block{{makeColumn(ctx, i32, ba.data(), nb), i32, "s_a"},
+                              {makeColumn(ctx, i64n, bb.data(), nb, bbn.data()), i64n, "s_b"},
+                              {makeColumn(ctx, u8, btag.data(), nb), u8, "btag"}};
+            } else {
+                left = Block{{makeStringColumn(ctx, ps), str, "s"}, {makeColumn(ctx, u8, ptag.data(), np), u8, "ptag"}};
+                right = Block{{makeStringColumn(ctx, bs), str, "s_s"},
+                              {makeColumn(ctx, u8, btag.data(), nb), u8, "btag"}};
+            }
+            std::unique_ptr<Join> j;
+            if (fixed)
+                j = std::make_unique<Join>(ctx, kind, std::vector<std::string>{"a", "b"},
+                                           std::vector<std::string>{"s_a", "s_b"});
+            else
+                j = std::make_unique<Join>(ctx, kind, std::vector<std::string>{"s"}, std::vector<std::string>{"s_s"},
+                                           0, std::vector<int>{collator});
+            j->insertFromBlock(right);
+            j->finishOneBuild();
+            Block r = j->joinBlock(left);
+            std::multiset<std::pair<std::string, std::string>> want, got;
+            for (size_t i = 0; i < np; ++i) {
+                bool any = false;
+                for (size_t b = 0; b < nb; ++b)
+                    if (eq(i, b)) {
+                        any = true;
+                        if (kind == JoinKind::Inner || kind == JoinKind::Left)
+                            want.insert({std::to_string(ptag[i]) + "/" + std::to_string(i), std::to_string(btag[b])});
+                    }
+                if (!any && kind == JoinKind::Left) want.insert({std::to_string(ptag[i]) + "/" + std::to_string(i), "N"});
+                if ((any && kind == JoinKind::Semi) || (!any && kind == JoinKind::Anti))
+                    want.insert({std::to_string(ptag[i]) + "/" + std::to_string(i), ""});
+            }
+            // probe row identity: ptag plus the row's key text (rows are unique by construction
+            // only through the tag and keys; compare (tag, keys) multisets instead of row ids)
+            std::vector<std::string> tags = cellStrings(ctx, *materialize(ctx, r.getByName("ptag").column));
+            std::vector<std::string> keys;
+            if (fixed) {
+                auto a = cellStrings(ctx, *materialize(ctx, r.getByName("a").column));
+                auto b = cellStrings(ctx, *materialize(ctx, r.getByName("b").column));
+                for (size_t i = 0; i < r.rows(); ++i) keys.push_back(a[i] + "," + b[i]);
+            } else {
+                keys = toHostStrings(ctx, *r.getByName("s").column);
+            }
+            std::vector<std::string> bt;
+            if (kind == JoinKind::Inner || kind == JoinKind::Left)
+                bt = cellStrings(ctx, *materialize(ctx, r.getByName("btag").column));
+            for (size_t i = 0; i < r.rows(); ++i)
+                got.insert({tags[i] + "|" + keys[i], bt.empty() ? "" : bt[i]});
+            // expected in the same (tag | keys) form
+            std::multiset<std::pair<std::string, std::string>> want2;
+            for (const auto &w : want) {
+                const size_t i = std::stoul(w.first.substr(w.first.find('/') + 1));
+                const std::string k = fixed ? std::to_string(pa[i]) + "," + (pbn[i] ? std::string("N") : std::to_string(pb[i]))
+                                            : ps[i];
+                want2.insert({std::to_string(ptag[i]) + "|" + k, w.second});
+            }
+            EXPECT(got == want2);
+        }
+    }
+}
+
 // AutoPassThroughHashAggContext: the reference's state machine driven by three key
 // distributions (all-new keys -> PassThrough, few keys -> stays Init, half-known keys ->
 // Selective); pass-through blocks + the hash map's block, merged as the second stage would,

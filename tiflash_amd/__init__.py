@@ -619,6 +619,52 @@ class Join:
             pass
 
 
+def join_key_hash(ctx: Context, cols: Sequence, types: Sequence[int], offsets: Optional[Sequence] = None,
+                  nullmaps: Optional[Sequence] = None, collators: Optional[Sequence[int]] = None):
+    """tfg_join_key_hash: UInt64 fingerprints of the key tuples + the OR of the key null maps
+    (general join keys: several columns, String, 16-byte; JoinHashMap.cpp:33-116)."""
+    import torch
+    n = int(offsets[0].shape[0]) if types[0] == STRING else int(cols[0].shape[0])
+    dev = cols[0].device
+    out = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    onull = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+    k = len(cols)
+    check(lib().tfg_join_key_hash(ctx.h, k, _int_array(types), _int_array(collators or [0] * k), _ptr_array(cols),
+                                  _ptr_array(offsets or [None] * k), _ptr_array(nullmaps or [None] * k),
+                                  ctypes.c_int64(n), _p(out), _p(onull)))
+    return out[:n], onull[:n]
+
+
+def join_keys_equal(ctx: Context, types: Sequence[int], probe_cols: Sequence, build_cols: Sequence, probe_idx,
+                    build_idx, probe_offsets: Optional[Sequence] = None, build_offsets: Optional[Sequence] = None,
+                    collators: Optional[Sequence[int]] = None, pass_in=None):
+    """tfg_join_keys_equal: 1 where pass_in (default 1) and the pair's full key tuples are equal."""
+    import torch
+    n = int(probe_idx.shape[0])
+    out = torch.empty(max(n, 1), dtype=torch.uint8, device=probe_idx.device)
+    k = len(types)
+    check(lib().tfg_join_keys_equal(ctx.h, k, _int_array(types), _int_array(collators or [0] * k),
+                                    _ptr_array(probe_cols), _ptr_array(probe_offsets or [None] * k),
+                                    _ptr_array(build_cols), _ptr_array(build_offsets or [None] * k), _p(probe_idx),
+                                    _p(build_idx), _p(pass_in), ctypes.c_int64(n), _p(out)))
+    return out[:n]
+
+
+def gather_string(ctx: Context, perm, chars, offsets):
+    """tfg_gather_string -> (chars, end offsets) of rows perm (-1 -> the empty String)."""
+    import torch
+    n = int(perm.shape[0])
+    dev = perm.device
+    oo = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    nbytes = ctypes.c_uint64()
+    check(lib().tfg_gather_string(ctx.h, _p(perm), ctypes.c_int64(n), _p(chars), _p(offsets), _p(oo),
+                                  ctypes.c_void_p(0), ctypes.c_uint64(0), ctypes.byref(nbytes)))
+    oc = torch.empty(max(nbytes.value, 1), dtype=torch.uint8, device=dev)
+    check(lib().tfg_gather_string(ctx.h, _p(perm), ctypes.c_int64(n), _p(chars), _p(offsets), _p(oo), _p(oc),
+                                  ctypes.c_uint64(nbytes.value), ctypes.byref(nbytes)))
+    return oc[:nbytes.value], oo[:n]
+
+
 # ---- (f1) MPP packet codec: CHBlockChunkCodec / CHBlockChunkCodecV1 --------------------------
 CODEC_CHBLOCK, CODEC_V1 = 0, 1
 

@@ -258,6 +258,39 @@ __global__ void string_copy_kernel(const uint8_t *mask, const uint8_t *chars, co
     }
 }
 
+// String gather: row lengths through perm (0xFFFFFFFF -> the empty String, 1 byte '\0')
+__global__ void string_gather_lengths_kernel(const uint32_t *perm, const uint64_t *offsets, int64_t n,
+                                             uint64_t *lens) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t p = perm[i];
+        lens[i] = p == 0xFFFFFFFFu ? 1 : offsets[p] - (p ? offsets[p - 1] : 0);
+    }
+}
+
+__global__ void string_gather_offsets_kernel(const uint64_t *starts, const uint64_t *lens, int64_t n,
+                                             uint64_t *out_offsets) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out_offsets[i] = starts[i] + lens[i];
+}
+
+// one wave per row: lanes copy the row's bytes
+__global__ void string_gather_copy_kernel(const uint32_t *perm, const uint8_t *chars, const uint64_t *offsets,
+                                          int64_t n, const uint64_t *starts, uint8_t *out_chars) {
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const unsigned lane = threadIdx.x & 63;
+    for (int64_t i = wave; i < n; i += nwaves) {
+        const uint32_t p = perm[i];
+        const uint64_t s = starts[i];
+        if (p == 0xFFFFFFFFu) {
+            if (lane == 0) out_chars[s] = 0;
+            continue;
+        }
+        const uint64_t prev = p ? offsets[p - 1] : 0, len = offsets[p] - prev;
+        for (uint64_t b = lane; b < len; b += 64) out_chars[s + b] = chars[prev + b];
+    }
+}
+
 // ---------------------------------------------------------------- host drivers
 template <typename P>
 static int run_filter(Ctx *ctx, const P &pred, int64_t n, const ColsArg &cols, uint64_t *out_count_dev,
@@ -465,6 +498,44 @@ int tfg_filter_string(tfg_ctx *ctx, const uint8_t *mask, int64_t n, const uint8_
             if (out_rows_host) *out_rows_host = rows;
             if (!rc && out_bytes_host) rc = read_back_u64(ctx, starts + n, out_bytes_host, 1);
         }
+    }
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipFree(mine);
+    return rc;
+}
+
+int tfg_gather_string(tfg_ctx *ctx, const uint32_t *perm, int64_t n, const uint8_t *chars, const uint64_t *offsets,
+                      uint64_t *out_offsets, uint8_t *out_chars, uint64_t chars_capacity, uint64_t *out_chars_host) {
+    TFG_CHECK(ctx && (n == 0 || (perm && offsets && out_offsets)), TFG_ERR_INVALID_ARG, "null argument");
+    TFG_CHECK(!out_chars || chars, TFG_ERR_INVALID_ARG, "null chars");
+    if (n <= 0) {
+        if (out_chars_host) *out_chars_host = 0;
+        return TFG_OK;
+    }
+    Carver cv;
+    size_t o_lens = cv.take<uint64_t>(n), o_starts = cv.take<uint64_t>(n + 1);
+    size_t o_tmp = cv.take<uint8_t>(scan_tmp_bytes(n));
+    uint64_t *mine;
+    if (int rc = tfg_buf_alloc(ctx, cv.off, (void **)&mine)) return rc;
+    char *sb = (char *)mine;
+    uint64_t *lens = (uint64_t *)(sb + o_lens), *starts = (uint64_t *)(sb + o_starts);
+    const unsigned grid = stream_grid(n, 256, 8192);
+    hipLaunchKernelGGL(string_gather_lengths_kernel, dim3(grid), dim3(256), 0, ctx->stream, perm, offsets, n, lens);
+    int rc = exclusive_scan_u64(ctx, lens, starts, n, sb + o_tmp);
+    uint64_t total = 0;
+    if (!rc) {
+        hipLaunchKernelGGL(string_gather_offsets_kernel, dim3(grid), dim3(256), 0, ctx->stream, starts, lens, n,
+                           out_offsets);
+        rc = read_back_u64(ctx, starts + n, &total, 1);
+    }
+    if (!rc && out_chars_host) *out_chars_host = total;
+    if (!rc && out_chars) {
+        if (total > chars_capacity)
+            rc = fail(TFG_ERR_CAPACITY, "String gather needs %llu chars bytes, capacity %llu",
+                      (unsigned long long)total, (unsigned long long)chars_capacity);
+        else
+            hipLaunchKernelGGL(string_gather_copy_kernel, dim3(stream_grid(n * 64, 256, 8192)), dim3(256), 0,
+                               ctx->stream, perm, chars, offsets, n, starts, out_chars);
     }
     (void)hipStreamSynchronize(ctx->stream);
     (void)hipFree(mine);

@@ -548,9 +548,164 @@ int probe_common(tfg_join *j, int kind, const void *keys, const uint8_t *key_nul
     return TFG_OK;
 }
 
+// ---------------------------------------------------------------- general join keys (§8 f2)
+// chooseJoinMapMethod (Interpreters/JoinHashMap.cpp:33-116) picks keys128 / keys256 for several
+// fixed keys, key_strbin / key_strbinpadding for one String key (by collator) and serialized
+// otherwise.  Here every such key set joins through the one fixed-width table: each row's key
+// tuple is folded into a 64-bit fingerprint (tfg_join_key_hash), the u64 join produces the
+// candidate pairs, and tfg_join_keys_equal keeps the pairs whose full key tuples are equal, so
+// a fingerprint collision costs a rejected pair, never a wrong one.  A row with a NULL in any
+// key column is a NULL key (extractNestedColumnsAndNullMap ORs the key null maps).
+constexpr int JKMAX = 8;
+struct JoinKeyCols {
+    int nkeys;
+    int width[JKMAX]; // bytes; 0 = String
+    int collator[JKMAX];
+    const void *col[JKMAX];
+    const uint64_t *offsets[JKMAX];
+    const uint8_t *nullmap[JKMAX];
+};
+
+__device__ __forceinline__ uint64_t jk_mix(uint64_t h, uint64_t w) {
+    h = (h ^ w) * 0xbf58476d1ce4e5b9ull;
+    return h ^ (h >> 31);
+}
+
+// the collator's sort key of String row r: [s, s + len)  (BinCollatorSortKey<true> right-trims)
+__device__ __forceinline__ const uint8_t *jk_sort_key(const JoinKeyCols &k, int j, int64_t r, int64_t &len) {
+    const uint64_t s = r ? k.offsets[j][r - 1] : 0, e = k.offsets[j][r];
+    const uint8_t *c = (const uint8_t *)k.col[j] + s;
+    len = (int64_t)(e - s) - 1; // rows end with '\0'
+    if (k.collator[j] == TFG_COLLATOR_BIN_PADDING)
+        while (len > 0 && c[len - 1] == ' ') --len;
+    return c;
+}
+
+__global__ void join_key_hash_kernel(JoinKeyCols k, int64_t n, uint64_t *out, uint8_t *out_null) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t h = 0x2545F4914F6CDD1Dull;
+        uint8_t isnull = 0;
+        for (int j = 0; j < k.nkeys; ++j) {
+            if (k.nullmap[j] && k.nullmap[j][r]) {
+                isnull = 1;
+                break;
+            }
+            const int wd = k.width[j];
+            if (wd == 0) {
+                int64_t len;
+                const uint8_t *c = jk_sort_key(k, j, r, len);
+                uint64_t w = 0;
+                for (int64_t i = 0; i < len; ++i) {
+                    w |= (uint64_t)c[i] << ((i & 7) * 8);
+                    if ((i & 7) == 7) {
+                        h = jk_mix(h, w);
+                        w = 0;
+                    }
+                }
+                h = jk_mix(h, w ^ ((uint64_t)len << 56)); // tail word tagged with the length
+            } else if (wd <= 8) {
+                h = jk_mix(h, jload_bits(k.col[j], wd, r));
+            } else {
+                const uint64_t *p = (const uint64_t *)k.col[j] + (int64_t)(wd / 8) * r;
+                for (int i = 0; i < wd / 8; ++i) h = jk_mix(h, p[i]);
+            }
+        }
+        // fmix64 so the partition radix (the product's high bits) sees every input bit
+        h ^= h >> 33;
+        h *= 0xff51afd7ed558ccdull;
+        h ^= h >> 33;
+        h *= 0xc4ceb9aa6b8f5d35ull;
+        h ^= h >> 33;
+        out[r] = isnull ? 0 : h;
+        if (out_null) out_null[r] = isnull;
+    }
+}
+
+__global__ void join_keys_equal_kernel(JoinKeyCols pk, JoinKeyCols bk, const uint32_t *pidx, const uint32_t *bidx,
+                                       const uint8_t *pass_in, int64_t n, uint8_t *pass_out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        bool eq = pass_in ? pass_in[i] != 0 : true;
+        const int64_t p = pidx[i], b = bidx[i];
+        for (int j = 0; j < pk.nkeys && eq; ++j) {
+            const int wd = pk.width[j];
+            if (wd == 0) {
+                int64_t lp, lb;
+                const uint8_t *cp = jk_sort_key(pk, j, p, lp);
+                const uint8_t *cb = jk_sort_key(bk, j, b, lb);
+                eq = lp == lb;
+                for (int64_t t = 0; t < lp && eq; ++t) eq = cp[t] == cb[t];
+            } else if (wd <= 8) {
+                eq = jload_bits(pk.col[j], wd, p) == jload_bits(bk.col[j], wd, b);
+            } else {
+                const uint64_t *a = (const uint64_t *)pk.col[j] + (int64_t)(wd / 8) * p;
+                const uint64_t *c = (const uint64_t *)bk.col[j] + (int64_t)(wd / 8) * b;
+                for (int t = 0; t < wd / 8 && eq; ++t) eq = a[t] == c[t];
+            }
+        }
+        pass_out[i] = eq ? 1 : 0;
+    }
+}
+
+int join_key_cols(int nkeys, const int *types, const int *collators, const void *const *cols,
+                  const uint64_t *const *offsets, const uint8_t *const *nullmaps, JoinKeyCols &k) {
+    TFG_CHECK(nkeys >= 1 && nkeys <= JKMAX && types && cols, TFG_ERR_INVALID_ARG, "join keys: need 1-%d key columns",
+              JKMAX);
+    k = JoinKeyCols{};
+    k.nkeys = nkeys;
+    for (int j = 0; j < nkeys; ++j) {
+        k.col[j] = cols[j];
+        k.nullmap[j] = nullmaps ? nullmaps[j] : nullptr;
+        k.collator[j] = collators ? collators[j] : TFG_COLLATOR_NONE;
+        TFG_CHECK(k.collator[j] >= TFG_COLLATOR_NONE && k.collator[j] <= TFG_COLLATOR_BIN_PADDING,
+                  TFG_ERR_NOT_IMPLEMENTED, "join key collator %d not supported", k.collator[j]);
+        if (types[j] == TFG_STRING) {
+            TFG_CHECK(offsets && offsets[j], TFG_ERR_INVALID_ARG, "String join key %d without offsets", j);
+            k.offsets[j] = offsets[j];
+            k.width[j] = 0;
+        } else {
+            const size_t w = type_width(types[j]);
+            TFG_CHECK(w == 1 || w == 2 || w == 4 || w == 8 || w == 16, TFG_ERR_ILLEGAL_TYPE,
+                      "unsupported join key type %d", types[j]);
+            k.width[j] = (int)w;
+        }
+    }
+    return TFG_OK;
+}
+
 } // namespace
 
 extern "C" {
+
+int tfg_join_key_hash(tfg_ctx *ctx, int nkeys, const int *key_types, const int *key_collators,
+                      const void *const *key_cols, const uint64_t *const *key_offsets,
+                      const uint8_t *const *key_nullmaps, int64_t n, uint64_t *out_keys, uint8_t *out_nullmap) {
+    TFG_CHECK(ctx && (n == 0 || out_keys), TFG_ERR_INVALID_ARG, "null argument");
+    JoinKeyCols k;
+    if (int rc = join_key_cols(nkeys, key_types, key_collators, key_cols, key_offsets, key_nullmaps, k)) return rc;
+    if (n <= 0) return TFG_OK;
+    for (int j = 0; j < nkeys; ++j) TFG_CHECK(key_cols[j], TFG_ERR_INVALID_ARG, "null key column %d", j);
+    if (int rc = set_device(ctx)) return rc;
+    hipLaunchKernelGGL(join_key_hash_kernel, dim3(stream_grid(n, 256)), dim3(256), 0, ctx->stream, k, n, out_keys,
+                       out_nullmap);
+    TFG_LAUNCH_CHECK();
+    return TFG_OK;
+}
+
+int tfg_join_keys_equal(tfg_ctx *ctx, int nkeys, const int *key_types, const int *key_collators,
+                        const void *const *probe_cols, const uint64_t *const *probe_offsets,
+                        const void *const *build_cols, const uint64_t *const *build_offsets, const uint32_t *probe_idx,
+                        const uint32_t *build_idx, const uint8_t *pass_in, int64_t n_pairs, uint8_t *out_pass) {
+    TFG_CHECK(ctx && (n_pairs == 0 || (probe_idx && build_idx && out_pass)), TFG_ERR_INVALID_ARG, "null argument");
+    JoinKeyCols pk, bk;
+    if (int rc = join_key_cols(nkeys, key_types, key_collators, probe_cols, probe_offsets, nullptr, pk)) return rc;
+    if (int rc = join_key_cols(nkeys, key_types, key_collators, build_cols, build_offsets, nullptr, bk)) return rc;
+    if (n_pairs <= 0) return TFG_OK;
+    if (int rc = set_device(ctx)) return rc;
+    hipLaunchKernelGGL(join_keys_equal_kernel, dim3(stream_grid(n_pairs, 256)), dim3(256), 0, ctx->stream, pk, bk,
+                       probe_idx, build_idx, pass_in, n_pairs, out_pass);
+    TFG_LAUNCH_CHECK();
+    return TFG_OK;
+}
 
 int tfg_join_create(tfg_ctx *ctx, int key_type, int64_t expected_build_rows, tfg_join **out) {
     TFG_CHECK(ctx && out, TFG_ERR_INVALID_ARG, "null argument");

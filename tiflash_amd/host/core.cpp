@@ -278,7 +278,6 @@ Block concatenateBlocks(Context &ctx, const std::vector<Block> &blocks) {
 }
 
 ColumnPtr gatherColumn(Context &ctx, const IColumn &src, const uint32_t *perm_dev, size_t n, bool make_nullable) {
-    if (src.type.isString()) throw Exception("gather of String columns", ErrorCodes::NOT_IMPLEMENTED);
     auto col = std::make_shared<IColumn>();
     col->type = src.type;
     col->rows = n;
@@ -288,10 +287,26 @@ ColumnPtr gatherColumn(Context &ctx, const IColumn &src, const uint32_t *perm_de
         col->const_value = src.const_value;
         return col;
     }
-    col->data = std::make_shared<DeviceBuffer>(ctx, n * w);
-    const void *in[1] = {src.dataPtr()};
-    void *out[1] = {col->data->data()};
-    if (n) check(tfg_gather(ctx.raw(), perm_dev, (int64_t)n, 1, in, &w, out), "tfg_gather");
+    if (src.type.isString()) { // offsets, then the chars they need
+        col->offsets = std::make_shared<DeviceBuffer>(ctx, std::max<size_t>(n, 1) * 8);
+        uint64_t chars = 0;
+        check(tfg_gather_string(ctx.raw(), perm_dev, (int64_t)n, (const uint8_t *)src.dataPtr(),
+                                (const uint64_t *)src.offsets->data(), (uint64_t *)col->offsets->data(), nullptr, 0,
+                                &chars),
+              "tfg_gather_string");
+        col->chars = chars;
+        col->data = std::make_shared<DeviceBuffer>(ctx, std::max<uint64_t>(chars, 1));
+        if (n)
+            check(tfg_gather_string(ctx.raw(), perm_dev, (int64_t)n, (const uint8_t *)src.dataPtr(),
+                                    (const uint64_t *)src.offsets->data(), (uint64_t *)col->offsets->data(),
+                                    (uint8_t *)col->data->data(), chars, &chars),
+                  "tfg_gather_string");
+    } else {
+        col->data = std::make_shared<DeviceBuffer>(ctx, n * w);
+        const void *in[1] = {src.dataPtr()};
+        void *out[1] = {col->data->data()};
+        if (n) check(tfg_gather(ctx.raw(), perm_dev, (int64_t)n, 1, in, &w, out), "tfg_gather");
+    }
     if (src.nullmap || make_nullable) {
         col->type.nullable = true;
         col->nullmap = std::make_shared<DeviceBuffer>(ctx, n);

@@ -166,7 +166,16 @@ Block Aggregator::convertToBlock(bool final) const {
 // ================================================================ Join
 Join::Join(Context &ctx, JoinKind kind, const std::string &probe_key, const std::string &build_key,
            int64_t expected_build_rows)
-    : ctx_(ctx), kind_(kind), probe_key_(probe_key), build_key_(build_key), expected_(expected_build_rows) {}
+    : Join(ctx, kind, std::vector<std::string>{probe_key}, std::vector<std::string>{build_key}, expected_build_rows) {}
+
+Join::Join(Context &ctx, JoinKind kind, std::vector<std::string> probe_keys, std::vector<std::string> build_keys,
+           int64_t expected_build_rows, std::vector<int> collators)
+    : ctx_(ctx), kind_(kind), probe_keys_(std::move(probe_keys)), build_keys_(std::move(build_keys)),
+      collators_(std::move(collators)), expected_(expected_build_rows) {
+    if (probe_keys_.empty() || probe_keys_.size() != build_keys_.size())
+        throw Exception("join needs the same number (>= 1) of probe and build keys", ErrorCodes::BAD_ARGUMENTS);
+    collators_.resize(build_keys_.size(), TFG_COLLATOR_NONE);
+}
 
 Join::~Join() {
     if (join_) tfg_join_destroy(join_);
@@ -174,16 +183,80 @@ Join::~Join() {
 
 void Join::initBuild(const Block &sample_block) {
     sample_ = sample_block.cloneEmpty();
-    const DataType kt = sample_.getByName(build_key_).type;
-    if (kt.isString() || kt.width() > 8 || kt.type == TFG_FLOAT32 || kt.type == TFG_FLOAT64)
-        throw Exception("join key type " + kt.getName(), ErrorCodes::NOT_IMPLEMENTED);
-    check(tfg_join_create(ctx_.raw(), kt.type, expected_, &join_), "tfg_join_create");
+    // chooseJoinMapMethod (JoinHashMap.cpp:33-116): one integer key of <= 8 bytes joins on its
+    // value (key8..key64); anything else on the key tuple's fingerprint, verified per pair
+    const DataType kt = sample_.getByName(build_keys_[0]).type;
+    general_keys_ = build_keys_.size() > 1 || kt.isString() || kt.width() > 8 || kt.type == TFG_FLOAT32 ||
+                    kt.type == TFG_FLOAT64;
+    check(tfg_join_create(ctx_.raw(), general_keys_ ? (int)TFG_UINT64 : kt.type, expected_, &join_),
+          "tfg_join_create");
+}
+
+// The column the table is keyed on: the key itself, or (general keys) the UInt64 fingerprint
+// of the tuple with the OR of the key null maps.
+ColumnPtr Join::joinKey(const Block &block, const std::vector<std::string> &names) const {
+    if (!general_keys_) return materialize(ctx_, block.getByName(names[0]).column);
+    const size_t n = block.rows(), nk = names.size();
+    std::vector<ColumnPtr> hold(nk);
+    std::vector<int> types(nk);
+    std::vector<const void *> cols(nk);
+    std::vector<const uint64_t *> offs(nk);
+    std::vector<const uint8_t *> nulls(nk);
+    for (size_t j = 0; j < nk; ++j) {
+        hold[j] = materialize(ctx_, block.getByName(names[j]).column);
+        types[j] = hold[j]->type.isString() ? (int)TFG_STRING : hold[j]->type.type;
+        cols[j] = hold[j]->dataPtr();
+        offs[j] = hold[j]->offsets ? (const uint64_t *)hold[j]->offsets->data() : nullptr;
+        nulls[j] = hold[j]->nullPtr();
+    }
+    auto c = std::make_shared<IColumn>();
+    c->type.type = TFG_UINT64;
+    c->type.nullable = true;
+    c->rows = n;
+    c->data = std::make_shared<DeviceBuffer>(ctx_, std::max<size_t>(n, 1) * 8);
+    c->nullmap = std::make_shared<DeviceBuffer>(ctx_, std::max<size_t>(n, 1));
+    check(tfg_join_key_hash(ctx_.raw(), (int)nk, types.data(), collators_.data(), cols.data(), offs.data(),
+                            nulls.data(), (int64_t)n, (uint64_t *)c->data->data(), (uint8_t *)c->nullmap->data()),
+          "tfg_join_key_hash");
+    ctx_.sync();
+    return c;
+}
+
+// pass[i] && the full key tuples of pair i are equal (general keys only)
+DeviceBufferPtr Join::verifyKeys(const Block &probe_block, const uint32_t *pi, const uint32_t *bi, uint64_t count,
+                                 DeviceBufferPtr pass) const {
+    const size_t nk = probe_keys_.size();
+    std::vector<ColumnPtr> hold;
+    std::vector<int> types(nk);
+    std::vector<const void *> pc(nk), bc(nk);
+    std::vector<const uint64_t *> po(nk), bo(nk);
+    for (size_t j = 0; j < nk; ++j) {
+        ColumnPtr p = materialize(ctx_, probe_block.getByName(probe_keys_[j]).column);
+        ColumnPtr b = materialize(ctx_, build_.getByName(build_keys_[j]).column);
+        if (p->type.type != b->type.type)
+            throw Exception("join key " + probe_keys_[j] + ": probe and build types differ",
+                            ErrorCodes::ILLEGAL_TYPE_OF_ARGUMENT);
+        types[j] = p->type.isString() ? (int)TFG_STRING : p->type.type;
+        pc[j] = p->dataPtr();
+        bc[j] = b->dataPtr();
+        po[j] = p->offsets ? (const uint64_t *)p->offsets->data() : nullptr;
+        bo[j] = b->offsets ? (const uint64_t *)b->offsets->data() : nullptr;
+        hold.push_back(p);
+        hold.push_back(b);
+    }
+    auto out = std::make_shared<DeviceBuffer>(ctx_, std::max<uint64_t>(count, 1));
+    check(tfg_join_keys_equal(ctx_.raw(), (int)nk, types.data(), collators_.data(), pc.data(), po.data(), bc.data(),
+                              bo.data(), pi, bi, pass ? (const uint8_t *)pass->data() : nullptr, (int64_t)count,
+                              (uint8_t *)out->data()),
+          "tfg_join_keys_equal");
+    ctx_.sync();
+    return out;
 }
 
 void Join::insertFromBlock(const Block &block) {
     if (!join_) initBuild(block);
     if (finished_) throw Exception("insertFromBlock after finishOneBuild", ErrorCodes::LOGICAL_ERROR);
-    ColumnPtr k = materialize(ctx_, block.getByName(build_key_).column);
+    ColumnPtr k = joinKey(block, build_keys_);
     check(tfg_join_build(join_, k->dataPtr(), k->nullPtr(), (int64_t)block.rows()), "tfg_join_build");
     build_blocks_.push_back(block);
 }
@@ -238,7 +311,7 @@ static Block filterByMask(Context &ctx, const Block &block, DeviceBufferPtr mask
 // probe rows; compare unordered, as the reference's join tests do.
 Block Join::joinBlockWithCondition(const Block &probe_block) {
     const size_t n = probe_block.rows();
-    ColumnPtr k = materialize(ctx_, probe_block.getByName(probe_key_).column);
+    ColumnPtr k = joinKey(probe_block, probe_keys_);
     uint64_t cap = std::max<uint64_t>(n, 1), count = 0;
     DeviceBufferPtr pi, bi;
     for (;;) {
@@ -278,6 +351,8 @@ Block Join::joinBlockWithCondition(const Block &probe_block) {
             pass = mask->data;
         }
     }
+    if (general_keys_ && count) // candidate pairs of equal fingerprints -> key-equal pairs
+        pass = verifyKeys(probe_block, (const uint32_t *)pi->data(), (const uint32_t *)bi->data(), count, pass);
     if (kind_ == JoinKind::Inner) {
         if (!pass) return joined;
         return filterByMask(ctx_, joined, pass, count);
@@ -366,10 +441,10 @@ Block Join::joinBlockWithCondition(const Block &probe_block) {
 
 Block Join::joinBlock(const Block &probe_block) {
     if (!finished_) finishOneBuild();
-    if (other_cond_ || kind_ == JoinKind::LeftOuterSemi || kind_ == JoinKind::AntiLeftOuterSemi)
+    if (other_cond_ || general_keys_ || kind_ == JoinKind::LeftOuterSemi || kind_ == JoinKind::AntiLeftOuterSemi)
         return joinBlockWithCondition(probe_block);
     const size_t n = probe_block.rows();
-    ColumnPtr k = materialize(ctx_, probe_block.getByName(probe_key_).column);
+    ColumnPtr k = joinKey(probe_block, probe_keys_);
     const bool pairs = kind_ == JoinKind::Inner || kind_ == JoinKind::Left;
     uint64_t cap = std::max<uint64_t>(n, 1), count = 0;
     std::shared_ptr<DeviceBuffer> pi, bi;

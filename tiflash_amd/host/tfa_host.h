@@ -296,6 +296,12 @@ class Join {
 public:
     Join(Context &ctx, JoinKind kind, const std::string &probe_key, const std::string &build_key,
          int64_t expected_build_rows = 0);
+    // Several key columns, or String / 16-byte / float keys (chooseJoinMapMethod keys128 /
+    // keys256 / key_strbin / key_strbinpadding / serialized, JoinHashMap.cpp:33-116): joined on
+    // device fingerprints of the key tuples, every candidate pair verified on the full keys.
+    // collators[j] (tfg_collator) applies to String key j; empty = binary.
+    Join(Context &ctx, JoinKind kind, std::vector<std::string> probe_keys, std::vector<std::string> build_keys,
+         int64_t expected_build_rows = 0, std::vector<int> collators = {});
     ~Join();
     Join(const Join &) = delete;
     Join &operator=(const Join &) = delete;
@@ -315,7 +321,9 @@ public:
 private:
     Context &ctx_;
     JoinKind kind_;
-    std::string probe_key_, build_key_;
+    std::vector<std::string> probe_keys_, build_keys_;
+    std::vector<int> collators_;
+    bool general_keys_ = false; // fingerprint + verify (several / String / wide keys)
     int64_t expected_;
     tfg_join *join_ = nullptr;
     Block sample_;
@@ -326,6 +334,9 @@ private:
     std::string other_filter_;
     std::string match_helper_ = "match_helper";
     Block joinBlockWithCondition(const Block &probe_block);
+    ColumnPtr joinKey(const Block &block, const std::vector<std::string> &names) const;
+    DeviceBufferPtr verifyKeys(const Block &probe_block, const uint32_t *pi, const uint32_t *bi, uint64_t count,
+                               DeviceBufferPtr pass) const;
 };
 
 // ---------------------------------------------------------------- exchange (a22-a24, e)
