@@ -886,6 +886,93 @@ TEST(JoinGeneralKeysMatchNestedLoop) {
     }
 }
 
+// Aggregator with several fixed keys (keys128 / nullable_keys128) and with one String key
+// (key_string under the padding collator): executeOnBlock, the fused filter, two-phase
+// convertToBlock(false) -> mergeOnBlock, against std::map over the same rows.
+TEST(AggregatorPackedKeysMatchMap) {
+    std::mt19937_64 rng(31);
+    const size_t n = 20000;
+    DataType i32, i16n, i64, str{DataType::TYPE_STRING};
+    i32.type = TFG_INT32;
+    i16n.type = TFG_INT16;
+    i16n.nullable = true;
+    std::vector<int32_t> a(n);
+    std::vector<int16_t> b(n);
+    std::vector<uint8_t> bn(n);
+    std::vector<int64_t> v(n), f(n);
+    std::vector<std::string> s(n);
+    const std::vector<std::string> words = {"", "x", "x ", "k00000001", "k00000001  ", "abcdefghijklmno", " y"};
+    for (size_t i = 0; i < n; ++i) {
+        a[i] = (int32_t)(rng() % 50) - 25;
+        b[i] = (int16_t)(rng() % 7);
+        bn[i] = rng() % 9 == 0;
+        v[i] = (int64_t)(rng() % 1000) - 500;
+        f[i] = (int64_t)(rng() % 10);
+        s[i] = words[rng() % words.size()];
+    }
+    Block blk{{makeColumn(ctx, i32, a.data(), n), i32, "a"},
+              {makeColumn(ctx, i16n, b.data(), n, bn.data()), i16n, "b"},
+              {makeStringColumn(ctx, s), str, "s"},
+              {makeColumn(ctx, i64, v.data(), n), i64, "v"},
+              {makeColumn(ctx, i64, f.data(), n), i64, "f"}};
+    for (int mode = 0; mode < 2; ++mode) { // 0: (a, b) keys, 1: String key s
+        Aggregator::Params p;
+        p.keys = mode == 0 ? std::vector<std::string>{"a", "b"} : std::vector<std::string>{"s"};
+        if (mode == 1) p.collators = {TFG_COLLATOR_BIN_PADDING};
+        p.aggregates = {{"sum", {"v"}, "sum_v"}, {"count", {}, "cnt"}};
+        p.src_header = blk.cloneEmpty();
+        auto keyOf = [&](size_t i) {
+            if (mode == 0) return std::to_string(a[i]) + "," + (bn[i] ? std::string("N") : std::to_string(b[i]));
+            std::string t = s[i];
+            while (!t.empty() && t.back() == ' ') t.pop_back();
+            return t;
+        };
+        for (int filtered = 0; filtered < 2; ++filtered) {
+            std::map<std::string, std::pair<int64_t, uint64_t>> want;
+            for (size_t i = 0; i < n; ++i) {
+                if (filtered && !(f[i] < 7)) continue;
+                auto &w = want[keyOf(i)];
+                w.first += v[i];
+                w.second += 1;
+            }
+            // phase 1 over two halves (two partial aggregators), phase 2 merges their blocks
+            Aggregator final_agg(ctx, p);
+            for (int half = 0; half < 2; ++half) {
+                Aggregator part(ctx, p);
+                std::vector<uint32_t> rows;
+                for (size_t i = half; i < n; i += 2) rows.push_back((uint32_t)i);
+                DeviceBuffer perm(ctx, rows.size() * 4);
+                check(tfg_upload(ctx.raw(), perm.data(), rows.data(), rows.size() * 4), "tfg_upload");
+                Block hb;
+                for (const auto &c : blk.getColumnsWithTypeAndName()) {
+                    ColumnPtr g = gatherColumn(ctx, *c.column, (const uint32_t *)perm.data(), rows.size(), false);
+                    hb.insert({g, g->type, c.name});
+                }
+                if (filtered)
+                    part.executeOnBlockFiltered(hb, "f", TFG_LT, Field::Int64(7));
+                else
+                    part.executeOnBlock(hb);
+                final_agg.mergeOnBlock(part.convertToBlock(false));
+            }
+            Block r = final_agg.convertToBlock(true);
+            std::map<std::string, std::pair<int64_t, uint64_t>> got;
+            std::vector<std::string> keys;
+            if (mode == 0) {
+                auto ka = cellStrings(ctx, *r.getByName("a").column);
+                auto kb = cellStrings(ctx, *r.getByName("b").column);
+                for (size_t i = 0; i < r.rows(); ++i) keys.push_back(ka[i] + "," + kb[i]);
+            } else {
+                keys = toHostStrings(ctx, *r.getByName("s").column);
+            }
+            auto sums = toHost<int64_t>(ctx, *r.getByName("sum_v").column);
+            auto cnts = toHost<uint64_t>(ctx, *r.getByName("cnt").column);
+            for (size_t i = 0; i < r.rows(); ++i) got[keys[i]] = {sums[i], cnts[i]};
+            EXPECT(r.rows() == want.size());
+            EXPECT(got == want);
+        }
+    }
+}
+
 // AutoPassThroughHashAggContext: the reference's state machine driven by three key
 // distributions (all-new keys -> PassThrough, few keys -> stays Init, half-known keys ->
 // Selective); pass-through blocks + the hash map's block, merged as the second stage would,

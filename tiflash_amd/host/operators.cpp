@@ -9,14 +9,19 @@ namespace tfa {
 
 // ================================================================ Aggregator
 Aggregator::Aggregator(Context &ctx, const Params &params) : ctx_(ctx), params_(params) {
-    if (params_.keys.size() > 1)
-        throw Exception("GROUP BY over more than one key column", ErrorCodes::NOT_IMPLEMENTED);
+    // chooseAggregationMethod (Aggregator.cpp:394-537): one fixed key -> key8..key64; several
+    // fixed keys or one String key -> the packed 16-byte methods (keys128 / key_string)
     int key_type = 0;
+    std::vector<int> packed_types;
+    for (const auto &k : params_.keys) {
+        key_types_.push_back(params_.src_header.getByName(k).type);
+        packed_types.push_back(key_types_.back().isString() ? (int)TFG_STRING : key_types_.back().type);
+    }
     if (!params_.keys.empty()) {
-        key_type_ = params_.src_header.getByName(params_.keys[0]).type;
-        if (key_type_.isString()) throw Exception("String GROUP BY keys", ErrorCodes::NOT_IMPLEMENTED);
+        key_type_ = key_types_[0];
         key_type = key_type_.type;
     }
+    packed_ = params_.keys.size() > 1 || (!params_.keys.empty() && key_type_.isString());
     std::vector<int> arg_types, arg_scales;
     for (const auto &d : params_.aggregates) {
         int kind;
@@ -42,9 +47,28 @@ Aggregator::Aggregator(Context &ctx, const Params &params) : ctx_(ctx), params_(
         arg_scales.push_back(at.scale);
     }
     tfg_agg_params p{params_.bucket_bits, params_.expected_groups};
+    if (packed_) {
+        std::vector<int> coll = params_.collators;
+        coll.resize(params_.keys.size(), TFG_COLLATOR_NONE);
+        check(tfg_agg_create_keys(ctx_.raw(), (int)packed_types.size(), packed_types.data(), coll.data(),
+                                  (int)kinds_.size(), kinds_.data(), arg_types.data(), arg_scales.data(), &p, &agg_),
+              "tfg_agg_create_keys");
+        return;
+    }
     check(tfg_agg_create(ctx_.raw(), key_type, (int)kinds_.size(), kinds_.data(), arg_types.data(), arg_scales.data(),
                          &p, &agg_),
           "tfg_agg_create");
+}
+
+void Aggregator::keyPointers(const Block &b, std::vector<const void *> &cols, std::vector<const uint64_t *> &offs,
+                             std::vector<const uint8_t *> &nulls, std::vector<ColumnPtr> &hold) const {
+    for (const auto &k : params_.keys) {
+        ColumnPtr c = materialize(ctx_, b.getByName(k).column);
+        hold.push_back(c);
+        cols.push_back(c->dataPtr());
+        offs.push_back(c->offsets ? (const uint64_t *)c->offsets->data() : nullptr);
+        nulls.push_back(c->nullPtr());
+    }
 }
 
 Aggregator::~Aggregator() {
@@ -72,6 +96,16 @@ void Aggregator::executeOnBlock(const Block &block, const FilterPtr &filter) {
     std::vector<const uint8_t *> nulls;
     std::vector<ColumnPtr> hold;
     argPointers(block, args, nulls, hold);
+    if (packed_) {
+        std::vector<const void *> kc;
+        std::vector<const uint64_t *> ko;
+        std::vector<const uint8_t *> kn;
+        keyPointers(block, kc, ko, kn, hold);
+        check(tfg_agg_consume_keys(agg_, kc.data(), ko.data(), kn.data(), args.data(), nulls.data(),
+                                   filter ? (const uint8_t *)filter->dataPtr() : nullptr, (int64_t)n),
+              "tfg_agg_consume_keys");
+        return;
+    }
     ColumnPtr key;
     if (!params_.keys.empty()) key = materialize(ctx_, block.getByName(params_.keys[0]).column);
     check(tfg_agg_consume(agg_, key ? key->dataPtr() : nullptr, key ? key->nullPtr() : nullptr, args.data(), nulls.data(),
@@ -81,6 +115,19 @@ void Aggregator::executeOnBlock(const Block &block, const FilterPtr &filter) {
 
 void Aggregator::executeOnBlockFiltered(const Block &block, const std::string &pred, int op, Field constant) {
     const size_t n = block.rows();
+    if (packed_) { // the predicate's mask, then the packed-key consume
+        ColumnPtr p = materialize(ctx_, block.getByName(pred).column);
+        auto m = std::make_shared<IColumn>();
+        m->type.type = TFG_UINT8;
+        m->rows = n;
+        m->data = std::make_shared<DeviceBuffer>(ctx_, std::max<size_t>(n, 1));
+        if (n)
+            check(tfg_cmp_const(ctx_.raw(), p->type.type, p->dataPtr(), p->nullPtr(), (int64_t)n, op, constant.type,
+                                &constant.bits, (uint8_t *)m->data->data()),
+                  "tfg_cmp_const");
+        executeOnBlock(block, m);
+        return;
+    }
     std::vector<const void *> args;
     std::vector<const uint8_t *> nulls;
     std::vector<ColumnPtr> hold;
@@ -105,6 +152,16 @@ void Aggregator::mergeOnBlock(const Block &partial) {
         states.push_back(c->dataPtr());
         nulls.push_back(c->nullPtr());
     }
+    if (packed_) {
+        std::vector<const void *> kc;
+        std::vector<const uint64_t *> ko;
+        std::vector<const uint8_t *> kn;
+        keyPointers(partial, kc, ko, kn, hold);
+        check(tfg_agg_consume_partial_keys(agg_, kc.data(), ko.data(), kn.data(), states.data(), nulls.data(),
+                                           (int64_t)n),
+              "tfg_agg_consume_partial_keys");
+        return;
+    }
     ColumnPtr key;
     if (!params_.keys.empty()) key = materialize(ctx_, partial.getByName(params_.keys[0]).column);
     check(tfg_agg_consume_partial(agg_, key ? key->dataPtr() : nullptr, key ? key->nullPtr() : nullptr, states.data(),
@@ -127,7 +184,7 @@ Block Aggregator::convertToBlock(bool final) const {
     const size_t g = size();
     Block out;
     std::shared_ptr<IColumn> key;
-    if (!params_.keys.empty()) {
+    if (!params_.keys.empty() && !packed_) {
         key = std::make_shared<IColumn>();
         key->type = key_type_;
         key->rows = g;
@@ -153,6 +210,49 @@ Block Aggregator::convertToBlock(bool final) const {
         states.push_back(c);
     }
     uint64_t got = 0;
+    if (packed_) { // convertToBlockImplFinal with the packed keys unpacked into their columns
+        std::vector<std::shared_ptr<IColumn>> kcols;
+        std::vector<void *> kp;
+        std::vector<uint64_t *> ko;
+        std::vector<uint8_t *> kn;
+        for (const DataType &t : key_types_) {
+            auto c = std::make_shared<IColumn>();
+            c->type = t;
+            c->rows = g;
+            if (t.isString()) {
+                c->offsets = std::make_shared<DeviceBuffer>(ctx_, std::max<size_t>(g, 1) * 8);
+            } else {
+                c->data = std::make_shared<DeviceBuffer>(ctx_, std::max<size_t>(g, 1) * t.width());
+            }
+            if (t.nullable) c->nullmap = std::make_shared<DeviceBuffer>(ctx_, std::max<size_t>(g, 1));
+            kcols.push_back(c);
+        }
+        uint64_t chars = 0;
+        if (key_types_[0].isString()) { // chars size first (TFG_ERR_CAPACITY reports it)
+            std::shared_ptr<IColumn> &c = kcols[0];
+            DeviceBuffer probe(ctx_, 1);
+            void *pk[1] = {probe.data()};
+            uint64_t *po[1] = {(uint64_t *)c->offsets->data()};
+            uint8_t *pn[1] = {c->nullmap ? (uint8_t *)c->nullmap->data() : nullptr};
+            const int rc = tfg_agg_result_keys(agg_, pk, po, pn, sp.data(), snp.data(), g, 0, &got, &chars);
+            if (rc != TFG_ERR_CAPACITY) check(rc, "tfg_agg_result_keys");
+            c->chars = chars;
+            c->data = std::make_shared<DeviceBuffer>(ctx_, std::max<uint64_t>(chars, 1));
+        }
+        for (auto &c : kcols) {
+            kp.push_back(c->data->data());
+            ko.push_back(c->offsets ? (uint64_t *)c->offsets->data() : nullptr);
+            kn.push_back(c->nullmap ? (uint8_t *)c->nullmap->data() : nullptr);
+        }
+        check(tfg_agg_result_keys(agg_, kp.data(), ko.data(), kn.data(), sp.data(), snp.data(), g, chars, &got,
+                                  &chars),
+              "tfg_agg_result_keys");
+        ctx_.sync();
+        for (size_t j = 0; j < kcols.size(); ++j) out.insert({kcols[j], kcols[j]->type, params_.keys[j]});
+        for (size_t i = 0; i < states.size(); ++i)
+            out.insert({states[i], states[i]->type, params_.aggregates[i].column_name});
+        return out;
+    }
     check(tfg_agg_result(agg_, key ? key->data->data() : nullptr, key && key->nullmap ? (uint8_t *)key->nullmap->data() : nullptr,
                          sp.data(), snp.data(), g, &got),
           "tfg_agg_result");

@@ -245,8 +245,11 @@ class Aggregator {
 public:
     struct Params {
         Block src_header;
-        std::vector<std::string> keys; // 0 or 1 fixed-width key (method key8..key64 / nullable)
+        // 0 or 1 fixed-width key (key8..key64 / nullable), or several fixed keys of <= 16 bytes
+        // (keys128 / nullable_keys128) or one String key (key_string, sort key <= 15 bytes)
+        std::vector<std::string> keys;
         AggregateDescriptions aggregates;
+        std::vector<int> collators; // tfg_collator of a String key (empty = binary)
         int bucket_bits = 0;
         int64_t expected_groups = 0;
     };
@@ -273,10 +276,14 @@ private:
     Params params_;
     tfg_agg *agg_ = nullptr;
     DataType key_type_;
+    std::vector<DataType> key_types_; // every key (packed methods)
+    bool packed_ = false;             // keys128 / key_string through tfg_agg_*_keys
     std::vector<int> kinds_;
     std::vector<DataType> arg_types_;
     void argPointers(const Block &b, std::vector<const void *> &args, std::vector<const uint8_t *> &nulls,
                      std::vector<ColumnPtr> &hold) const;
+    void keyPointers(const Block &b, std::vector<const void *> &cols, std::vector<const uint64_t *> &offs,
+                     std::vector<const uint8_t *> &nulls, std::vector<ColumnPtr> &hold) const;
 };
 
 // ---------------------------------------------------------------- hash join (a18-a21)
