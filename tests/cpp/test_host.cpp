@@ -973,6 +973,68 @@ TEST(AggregatorPackedKeysMatchMap) {
     }
 }
 
+// HashPartitionWriter over a block with String columns (partition keys: a String under the
+// padding collator, then a Nullable Int64): the rows of every partition, in order, equal the
+// oracle's weak hash -> fillSelector -> stable partition of the same rows.
+TEST(HashPartitionStringColumnsMatchOracle) {
+    std::mt19937_64 rng(41);
+    const size_t n = 5000;
+    const uint32_t P = 5;
+    DataType i64n, str{DataType::TYPE_STRING};
+    i64n.nullable = true;
+    std::vector<std::string> s(n);
+    std::vector<int64_t> k(n), tag(n);
+    std::vector<uint8_t> kn(n), sn(n);
+    for (size_t i = 0; i < n; ++i) {
+        s[i] = "k" + std::to_string(rng() % 300) + std::string(rng() % 3, ' ');
+        k[i] = (int64_t)(rng() % 40) - 20;
+        kn[i] = rng() % 8 == 0;
+        sn[i] = rng() % 11 == 0;
+        tag[i] = (int64_t)i;
+    }
+    DataType str_n = str;
+    str_n.nullable = true;
+    Block blk{{makeStringColumn(ctx, s, sn.data()), str_n, "s"},
+              {makeColumn(ctx, i64n, k.data(), n, kn.data()), i64n, "k"},
+              {makeColumn(ctx, DataType{}, tag.data(), n), DataType{}, "tag"}};
+    std::vector<Block> got(P);
+    HashPartitionWriter w(ctx, {0, 1}, P, [&](uint32_t p, Block &&b) { got[p] = std::move(b); }, 1);
+    w.setCollators({TFG_COLLATOR_BIN_PADDING, TFG_COLLATOR_NONE});
+    w.write(blk);
+    w.flush();
+    // oracle: same hash chain over host copies
+    std::string chars;
+    std::vector<uint64_t> offs(n);
+    for (size_t i = 0; i < n; ++i) {
+        chars += s[i];
+        chars.push_back('\0');
+        offs[i] = chars.size();
+    }
+    std::vector<uint32_t> h(n, 0xFFFFFFFFu), sel(n), perm(n);
+    std::vector<uint64_t> po(P + 1);
+    orc_weak_hash_update_string((const uint8_t *)chars.data(), offs.data(), sn.data(), n, TFG_COLLATOR_BIN_PADDING,
+                                h.data());
+    orc_weak_hash_update(TFG_INT64, k.data(), kn.data(), n, h.data());
+    orc_fill_selector(h.data(), n, P, 0, sel.data());
+    orc_partition(sel.data(), n, P, perm.data(), po.data());
+    (void)w;
+    for (uint32_t p = 0; p < P; ++p) {
+        std::vector<std::string> want_tag, want_s;
+        for (uint64_t r = po[p]; r < po[p + 1]; ++r) {
+            want_tag.push_back(std::to_string(perm[r]));
+            want_s.push_back(sn[perm[r]] ? "N" : s[perm[r]]);
+        }
+        EXPECT(got[p].rows() == want_tag.size());
+        if (!got[p].rows()) continue;
+        EXPECT(cellStrings(ctx, *got[p].getByName("tag").column) == want_tag);
+        auto gs = toHostStrings(ctx, *got[p].getByName("s").column);
+        auto gn = toHostNullMap(ctx, *got[p].getByName("s").column);
+        for (size_t i = 0; i < gs.size(); ++i)
+            if (gn[i]) gs[i] = "N";
+        EXPECT(gs == want_s);
+    }
+}
+
 // AutoPassThroughHashAggContext: the reference's state machine driven by three key
 // distributions (all-new keys -> PassThrough, few keys -> stays Init, half-known keys ->
 // Selective); pass-through blocks + the hash map's block, merged as the second stage would,

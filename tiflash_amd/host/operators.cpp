@@ -577,8 +577,53 @@ Block Join::joinBlock(const Block &probe_block) {
 }
 
 // ================================================================ partitioning / exchange
+// Blocks with String columns: weak hash column by column, fillSelector, the stable partition
+// permutation (IColumn::scatter's order), then every column gathered per partition.
+static std::vector<Block> hashPartitionBlockGather(Context &ctx, const Block &block, const std::vector<size_t> &key_ids,
+                                                   uint32_t partition_num, const std::vector<int> &collators) {
+    const size_t n = block.rows();
+    DeviceBuffer h(ctx, std::max<size_t>(n, 1) * 4), sel(ctx, std::max<size_t>(n, 1) * 4),
+        perm(ctx, std::max<size_t>(n, 1) * 4), offs_dev(ctx, (partition_num + 1) * 8);
+    std::vector<uint64_t> offs(partition_num + 1, 0);
+    if (n) {
+        check(tfg_weak_hash_init(ctx.raw(), (uint32_t *)h.data(), (int64_t)n), "tfg_weak_hash_init");
+        for (size_t k = 0; k < key_ids.size(); ++k) {
+            ColumnPtr c = materialize(ctx, block.safeGetByPosition(key_ids[k]).column);
+            if (c->type.isString())
+                check(tfg_weak_hash_update_string(ctx.raw(), (const uint8_t *)c->dataPtr(),
+                                                  (const uint64_t *)c->offsets->data(), c->nullPtr(), (int64_t)n,
+                                                  k < collators.size() ? collators[k] : TFG_COLLATOR_NONE,
+                                                  (uint32_t *)h.data()),
+                      "tfg_weak_hash_update_string");
+            else
+                check(tfg_weak_hash_update(ctx.raw(), c->type.type, c->dataPtr(), c->nullPtr(), (int64_t)n,
+                                           (uint32_t *)h.data()),
+                      "tfg_weak_hash_update");
+        }
+        check(tfg_fill_selector(ctx.raw(), (const uint32_t *)h.data(), (int64_t)n, partition_num, 0,
+                                (uint32_t *)sel.data()),
+              "tfg_fill_selector");
+    }
+    check(tfg_partition(ctx.raw(), (const uint32_t *)sel.data(), (int64_t)n, partition_num, (uint32_t *)perm.data(),
+                        (uint64_t *)offs_dev.data(), offs.data()),
+          "tfg_partition");
+    std::vector<Block> parts(partition_num);
+    for (uint32_t p = 0; p < partition_num; ++p) {
+        const uint32_t *pp = (const uint32_t *)perm.data() + offs[p];
+        const size_t rows = offs[p + 1] - offs[p];
+        for (const auto &c : block.getColumnsWithTypeAndName()) {
+            ColumnPtr g = gatherColumn(ctx, *materialize(ctx, c.column), pp, rows, false);
+            parts[p].insert({g, g->type, c.name});
+        }
+    }
+    ctx.sync();
+    return parts;
+}
+
 std::vector<Block> hashPartitionBlock(Context &ctx, const Block &block, const std::vector<size_t> &key_ids,
-                                      uint32_t partition_num) {
+                                      uint32_t partition_num, const std::vector<int> &collators) {
+    for (const auto &c : block.getColumnsWithTypeAndName())
+        if (c.type.isString()) return hashPartitionBlockGather(ctx, block, key_ids, partition_num, collators);
     const size_t n = block.rows();
     std::vector<int> types, key_idx(key_ids.begin(), key_ids.end());
     std::vector<const void *> cols;
@@ -652,7 +697,7 @@ void HashPartitionWriter::flush() {
     Block all = concatenateBlocks(ctx_, pending_);
     pending_.clear();
     pending_rows_ = 0;
-    std::vector<Block> parts = hashPartitionBlock(ctx_, all, partition_col_ids_, partition_num_);
+    std::vector<Block> parts = hashPartitionBlock(ctx_, all, partition_col_ids_, partition_num_, collators_);
     for (uint32_t p = 0; p < partition_num_; ++p) sink_(p, std::move(parts[p]));
 }
 

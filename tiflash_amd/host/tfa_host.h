@@ -358,6 +358,8 @@ public:
                         int64_t batch_send_min_limit = -1);
     void write(const Block &block);
     void flush();
+    // collators of the partition key columns (String keys; TiDB::TiDBCollators in the reference)
+    void setCollators(std::vector<int> collators) { collators_ = std::move(collators); }
 
 private:
     Context &ctx_;
@@ -367,11 +369,14 @@ private:
     int64_t limit_;
     std::vector<Block> pending_;
     size_t pending_rows_ = 0;
+    std::vector<int> collators_;
 };
 
 // Partition a block into partition_num blocks (the scatterColumns step alone).
+// String columns (keys hashed by ColumnString::updateWeakHash32 under collators[k], the k-th
+// key's collator) are scattered through the stable partition permutation.
 std::vector<Block> hashPartitionBlock(Context &ctx, const Block &block, const std::vector<size_t> &key_ids,
-                                      uint32_t partition_num);
+                                      uint32_t partition_num, const std::vector<int> &collators = {});
 
 // One-node exchange over RCCL: every rank contributes partition_num == nranks blocks and
 // receives the concatenation of its partition from every rank (ExchangeReceiver output).
