@@ -620,6 +620,16 @@ TEST(MPPExchangeSingleRank) {
     Block b{{makeColumn(ctx, i64n, k.data(), 4, kn.data()), i64n, "k"}};
     Block r = ex.exchange({b});
     EXPECT(cellStrings(ctx, *r.getByName("k").column) == (std::vector<std::string>{"5", "N", "7", "8"}));
+    // a block with a String column travels as a CHBlockChunkCodecV1 packet
+    DataType str{DataType::TYPE_STRING};
+    Block bs{{makeColumn(ctx, i64n, k.data(), 4, kn.data()), i64n, "k"},
+             {makeStringColumn(ctx, {"a", "", std::string(70, 'q'), "k00000001"}), str, "s"}};
+    Block rs = ex.exchange({bs});
+    EXPECT(cellStrings(ctx, *rs.getByName("k").column) == (std::vector<std::string>{"5", "N", "7", "8"}));
+    EXPECT(toHostStrings(ctx, *rs.getByName("s").column) ==
+           (std::vector<std::string>{"a", "", std::string(70, 'q'), "k00000001"}));
+    Block es = ex.exchange({bs.cloneEmpty()}); // nothing sent, nothing received
+    EXPECT(es.rows() == 0 && es.columns() == 2);
 }
 
 // CHBlockChunkCodecV1 / CHBlockChunkCodec round trips through device packets (the reference's

@@ -710,10 +710,50 @@ MPPExchange::~MPPExchange() {
     if (comm_) tfg_comm_destroy(comm_);
 }
 
+Block MPPExchange::exchangePackets(const std::vector<Block> &partitions) {
+    const Block header = partitions[0].cloneEmpty();
+    std::vector<DevicePacket> pk(nranks_);
+    std::vector<uint64_t> sb(nranks_), sd(nranks_), rb(nranks_), rd(nranks_);
+    uint64_t so = 0, ro = 0;
+    for (int p = 0; p < nranks_; ++p) {
+        CHBlockChunkCodecV1 codec(ctx_, header);
+        pk[p] = codec.encode(partitions[p]);
+        sb[p] = pk[p].bytes;
+        sd[p] = so;
+        so += sb[p];
+    }
+    check(tfg_alltoall_counts(comm_, sb.data(), rb.data()), "tfg_alltoall_counts");
+    for (int p = 0; p < nranks_; ++p) {
+        rd[p] = ro;
+        ro += rb[p];
+    }
+    DeviceBuffer send(ctx_, std::max<uint64_t>(so, 1)), recv(ctx_, std::max<uint64_t>(ro, 1));
+    for (int p = 0; p < nranks_; ++p)
+        if (sb[p]) check(tfg_copy(ctx_.raw(), (char *)send.data() + sd[p], pk[p].buf->data(), sb[p]), "tfg_copy");
+    check(tfg_alltoallv(comm_, send.data(), sb.data(), sd.data(), recv.data(), rb.data(), rd.data()), "tfg_alltoallv");
+    ctx_.sync();
+    std::vector<Block> got;
+    for (int p = 0; p < nranks_; ++p)
+        if (rb[p]) got.push_back(decodeBlockPacket(ctx_, header, (const uint8_t *)recv.data() + rd[p], rb[p], TFG_CODEC_V1));
+    if (!got.empty()) return concatenateBlocks(ctx_, got);
+    Block empty; // no rows arrived: zero-row columns of the header's types
+    for (const auto &c : header.getColumnsWithTypeAndName()) {
+        auto z = std::make_shared<IColumn>();
+        z->type = c.type;
+        z->data = std::make_shared<DeviceBuffer>(ctx_, 1);
+        if (c.type.isString()) z->offsets = std::make_shared<DeviceBuffer>(ctx_, 8);
+        if (c.type.nullable) z->nullmap = std::make_shared<DeviceBuffer>(ctx_, 1);
+        empty.insert({z, z->type, c.name});
+    }
+    return empty;
+}
+
 Block MPPExchange::exchange(const std::vector<Block> &partitions) {
     if ((int)partitions.size() != nranks_)
         throw Exception("exchange needs one block per rank", ErrorCodes::BAD_ARGUMENTS);
     const Block &proto = partitions[0];
+    for (const auto &c : proto.getColumnsWithTypeAndName())
+        if (c.type.isString()) return exchangePackets(partitions);
     std::vector<uint64_t> send_rows(nranks_), recv_rows(nranks_);
     for (int p = 0; p < nranks_; ++p) send_rows[p] = partitions[p].rows();
     check(tfg_alltoall_counts(comm_, send_rows.data(), recv_rows.data()), "tfg_alltoall_counts");

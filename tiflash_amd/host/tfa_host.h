@@ -392,6 +392,9 @@ private:
     Context &ctx_;
     tfg_comm *comm_ = nullptr;
     int nranks_, rank_;
+    // blocks with String columns travel as CHBlockChunkCodecV1 packets (ExchangeSender ->
+    // ExchangeReceiver): encoded on the device, packet bytes all-to-all, decoded on arrival
+    Block exchangePackets(const std::vector<Block> &partitions);
 };
 
 // ---------------------------------------------------------------- auto pass-through (f4)
