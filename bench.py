@@ -4,19 +4,23 @@
 One "step" = one pass of the hot path over one batch of synthetic rows already resident in HBM:
     Aggregator reset -> fused (f < 96) filter + GROUP BY k: sum(v), count(*) -> final Block (result
     columns materialised on the device).
-With --gpus N (torchrun, one process per GPU) every rank aggregates its own 100M rows (weak
-scaling), the partial (key, sum, count) rows are hash-repartitioned with fillSelector and
-exchanged with RCCL all-to-all (the MPP ExchangeSender/Receiver of a two-phase aggregation),
-then merged by a final aggregation.  value = rows of all ranks / max-over-ranks time.
+`--gpus N` (N > 1) without a torchrun environment starts N ranks itself (torch.distributed.run
+as a child process, before this process touches the GPU).  Every rank aggregates its own 100M
+rows (weak scaling), the partial (key, sum, count) rows are hash-repartitioned with fillSelector
+and exchanged with an RCCL all-to-all (the MPP ExchangeSender/Receiver of a two-phase
+aggregation), then merged by a final aggregation.  value = rows of all ranks / max-over-ranks time.
 
-Extras in the same JSON line: the hash-join probe (configs[2] shape, N=1), the per-kernel
-roofline of the dominant kernel from HIP events recorded on the library's stream, and the CPU
-baseline (oracle restatement, bounded sample) on the host cores.
+Extras in the same JSON line: the §8(d) variants (selectivity sweep 0/1/10/50/100 %, Int64 value
+column), the hash-join probe (configs[2] shape, N=1), the repartitioned join (configs[3], N>1),
+the String + Decimal GROUP BY (configs[4]), the packet codec, the per-kernel roofline of the
+dominant kernel from HIP events recorded on the library's stream, and the CPU baseline (oracle
+restatement of the reference's algorithm) on the host cores.
 """
 import argparse
 import json
 import os
 import statistics
+import subprocess
 import sys
 import time
 
@@ -37,54 +41,82 @@ def parse():
     ap.add_argument("--join-build", type=int, default=10_000_000)
     ap.add_argument("--join-probe", type=int, default=100_000_000)
     ap.add_argument("--no-join", action="store_true")
+    ap.add_argument("--no-variants", action="store_true", help="skip the selectivity sweep / Int64-value legs")
     ap.add_argument("--c5-rows", type=int, default=100_000_000, help="C5 String-key GROUP BY rows per GPU (0 = skip)")
     ap.add_argument("--c5-groups", type=int, default=10_000_000)
     ap.add_argument("--codec-rows", type=int, default=20_000_000, help="packet codec leg rows (0 = skip)")
     ap.add_argument("--c4", type=int, default=-1, help="repartitioned join leg (configs[3]): 1 on, 0 off, -1 = on when N > 1")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
-    ap.add_argument("--value-int64", action="store_true", help="Int64 value column instead of Float64")
+    ap.add_argument("--value-int64", action="store_true", help="Int64 value column instead of Float64 (headline leg)")
     ap.add_argument("--bucket-bits", type=int, default=0, help="aggregation radix buckets (0 = from --groups)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, production) or gloo (rehearsal: all ranks may share one GPU)")
     return ap.parse_args()
 
 
-# algorithmic HBM bytes per row for each kernel of the pipeline:
-#   agg.part.hist    reads k, f                       16 B per input row
-#   agg.part.scatter reads k, v, f; writes k, v        24 B per input row + 16 B per kept row
-#   agg.part.tiled   same bytes as agg.part.scatter (tile-sorted partition, no histogram pass)
-#   agg.bucket       reads the staged k, v            16 B per kept row
-def kernel_bytes(name, n_in, n_kept):
-    return {
+def launch_ranks(args) -> int:
+    """--gpus N > 1 outside torchrun: start N ranks (one process per GPU) with torch.distributed.run
+    as a CHILD process and return its exit code.  Nothing here touches the GPU."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+# Algorithmic HBM bytes of each kernel (SURVEY §8(d)): the bytes a perfect implementation must
+# move — every input byte once (f, k, v = 24 B per input row for C2) plus the output.  Staging
+# records a kernel writes and a later kernel re-reads are the implementation's cost, reported
+# separately as moved_bytes (and measured by the PMC passes as traffic).
+def kernel_bytes(name, n_in, n_kept, n_groups):
+    alg = {
+        "agg.fused": 24 * n_in + 24 * n_groups,
+        "agg.part.tiled": 24 * n_in,
+        "agg.part.hist": 16 * n_in,
+        "agg.part.scatter": 24 * n_in,
+        "agg.bucket": 24 * n_groups,
+        "join.part.hist": 8 * n_in,
+        "join.part.scatter": 16 * n_in,
+        "join.probe": 0,
+    }.get(name)
+    moved = {
+        "agg.fused": 24 * n_in + 24 * n_groups,
+        "agg.part.tiled": 24 * n_in + 16 * n_kept,
         "agg.part.hist": 16 * n_in,
         "agg.part.scatter": 24 * n_in + 16 * n_kept,
-        "agg.part.tiled": 24 * n_in + 16 * n_kept,
-        "agg.bucket": 16 * n_kept,
-        "join.part.hist": 8 * n_in,
-        "join.part.scatter": 8 * n_in + 12 * n_in,
-        "join.probe": 12 * n_in,
+        "agg.bucket": 16 * n_kept + 24 * n_groups,
     }.get(name)
+    return alg, moved
 
 
-def roofline_from_profile(prof, steps, n_in, n_kept):
+def roofline_from_profile(prof, steps, n_in, n_kept, n_groups):
     if not prof:
         return None
     name, (ms, cnt) = max(prof.items(), key=lambda kv: kv[1][0])
     per_launch_ms = ms / max(cnt, 1)
-    b = kernel_bytes(name, n_in, n_kept)
+    alg, moved = kernel_bytes(name, n_in, n_kept, n_groups)
     launches_per_step = cnt / max(steps, 1)
-    if b is None or per_launch_ms <= 0:
+    if not alg or per_launch_ms <= 0:
         return {"kernel": name, "avg_ms": per_launch_ms}
-    b_launch = b / launches_per_step
+    b_launch = alg / launches_per_step
     ach = b_launch / (per_launch_ms * 1e-3) / 1e9
-    return {"bound": "hbm", "kernel": name, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "avg_ms": round(per_launch_ms, 4),
-            "algorithmic_bytes_per_launch": int(b_launch)}
+    out = {"bound": "hbm", "kernel": name, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "avg_ms": round(per_launch_ms, 4),
+           "algorithmic_bytes_per_launch": int(b_launch),
+           "algorithmic_basis": "SURVEY 8(d): 24 B per input row (f, k, v) read once (+ 24 B per group out)"}
+    if moved:
+        out["moved_bytes_per_launch"] = int(moved / launches_per_step)
+        out["moved_GBps"] = round(moved / launches_per_step / (per_launch_ms * 1e-3) / 1e9, 1)
+    return out
 
 
 def load_pmc_traffic(kernel):
-    """HBM bytes per launch measured by the rocprofv3 PMC pass (profiles/pmc_traffic.json), if any."""
+    """HBM bytes per launch measured by the rocprofv3 PMC passes (profiles/pmc_traffic.json), if any."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
@@ -94,11 +126,31 @@ def load_pmc_traffic(kernel):
         return None
 
 
+def host_cores():
+    """Host CPUs this process may use: affinity mask, capped by a cgroup CPU quota and by the
+    OMP_NUM_THREADS the GPU box sets to its per-GPU CPU share."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = int(q) / int(per)
+    except Exception:
+        pass
+    cores = aff if quota is None else max(1, min(aff, int(quota)))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        cores = min(cores, int(omp))
+    return cores, {"os_cpu_count": os.cpu_count(), "affinity_cpus": aff, "cgroup_cpu_quota": quota,
+                   "omp_num_threads": omp}
+
+
 def cpu_baseline(args):
     import numpy as np
     from oracle import oracle as orc
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-    n = min(args.rows, 50_000_000)
+    cores, host = host_cores()
+    threads = args.cpu_threads or cores
+    n = args.rows  # the full C2 batch
     rng = np.random.default_rng(1)
     f = rng.integers(0, 100, n, dtype=np.int64)
     k = rng.integers(0, args.groups, n, dtype=np.int64)
@@ -112,8 +164,8 @@ def cpu_baseline(args):
         if time.time() > t_end and len(times) >= 1:
             break
     med = statistics.median(times)
-    out = {"value": round(n / med, 1), "unit": "rows/s", "cores": threads, "kind": "port",
-           "sample": f"{n} rows x {len(times)} runs (median), same distribution, 65536-row blocks, "
+    out = {"value": round(n / med, 1), "unit": "rows/s", "cores": threads, "kind": "port", "host": host,
+           "sample": f"{n} rows (the full C2 batch) x {len(times)} runs (median), same distribution, 65536-row blocks, "
                      f"per-thread key64 HashMap (CRC32-C, arena states, prefetch, two-level at 100k keys) + "
                      f"bucket-parallel merge + result conversion (reference-algorithm CPU restatement, "
                      f"oracle/cpu_baseline.c)"}
@@ -123,8 +175,9 @@ def cpu_baseline(args):
 def cpu_join_baseline(args):
     import numpy as np
     from oracle import oracle as orc
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-    nb, npr = min(args.join_build, 10_000_000), min(args.join_probe, 50_000_000)
+    cores, host = host_cores()
+    threads = args.cpu_threads or cores
+    nb, npr = args.join_build, args.join_probe  # the full C3 sizes
     rng = np.random.default_rng(7)
     bk = rng.permutation(nb).astype(np.int64) * 4 + 1
     bpay = rng.integers(0, 1 << 40, nb, dtype=np.int64)
@@ -140,7 +193,7 @@ def cpu_join_baseline(args):
         jb.probe(pk, ppay)
         times.append(time.perf_counter() - t0)
     med = statistics.median(times)
-    return {"value": round(npr / med, 1), "unit": "probe rows/s", "cores": threads, "kind": "port",
+    return {"value": round(npr / med, 1), "unit": "probe rows/s", "cores": threads, "kind": "port", "host": host,
             "build_s": round(build_s, 3),
             "sample": f"build {nb} rows into {threads} segment HashMaps of RowRefList cells (not timed), "
                       f"probe {npr} rows x 3 runs (median) with materialised output blocks "
@@ -150,8 +203,9 @@ def cpu_join_baseline(args):
 def cpu_string_baseline(args):
     import numpy as np
     from oracle import oracle as orc
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-    n = min(args.c5_rows, 20_000_000)
+    cores, host = host_cores()
+    threads = args.cpu_threads or cores
+    n = min(args.c5_rows, 20_000_000)  # bounded: the CPU restatement runs ~10M rows/s
     rng = np.random.default_rng(11)
     ids = rng.integers(0, args.c5_groups, n)
     chars = np.empty((n, 10), np.uint8)
@@ -170,7 +224,7 @@ def cpu_string_baseline(args):
         orc.bench_string_agg(chars, offs, v, threads)
         times.append(time.perf_counter() - t0)
     med = statistics.median(times)
-    return {"value": round(n / med, 1), "unit": "rows/s", "cores": threads, "kind": "port",
+    return {"value": round(n / med, 1), "unit": "rows/s", "cores": threads, "kind": "port", "host": host,
             "sample": f"{n} rows x 3 runs (median), k%08d keys over {args.c5_groups} ids, per-thread StringHashMap "
                       f"StringKey16 sub-maps (CRC32-C, arena Decimal128+count states, prefetch, two-level at 100k keys) "
                       f"+ bucket-parallel merge + result conversion (reference-algorithm CPU restatement, "
@@ -407,8 +461,83 @@ def codec_leg(args, ctx, dev):
     return out
 
 
+def timed(step, args, ctx, world):
+    """W warmup steps, then exactly K timed steps bracketed by barrier + synchronize; returns
+    (elapsed seconds of this rank, last result, {kernel phase: (ms, launches)})."""
+    import torch
+    import torch.distributed as dist
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ctx.profile(True)
+    ctx.profile_reset()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = None
+    for _ in range(args.steps):
+        res = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    prof = ctx.profile_read()
+    ctx.profile(False)
+    return el, res, prof
+
+
+def variants_leg(args, ctx, dev, f, k, v):
+    """SURVEY 8(d) extras of C2 at N=1: the selectivity sweep f < t for t in 0/1/10/50/100 %
+    (bench_column_filter.cpp:251-290) and the Int64 value column, each a separate timed run."""
+    import torch
+
+    import tiflash_amd as tfa
+    out = {}
+    N, G = args.rows, args.groups
+    sweep = {}
+    agg = tfa.Aggregator(ctx, tfa.INT64, [(tfa.AGG_SUM, tfa.FLOAT64), (tfa.AGG_COUNT_ALL, 0)],
+                         bucket_bits=args.bucket_bits, expected_groups=G)
+    for t in (0, 1, 10, 50, 100):
+        def step():
+            agg.reset()
+            agg.consume_filtered(f, tfa.LT, t, k, [v, None])
+            return agg.result()
+        el, res, _ = timed(step, args, ctx, 1)
+        ms = el / args.steps * 1e3
+        kept = int((f < t).sum().item())
+        cnt = int(res["states"][1].view(torch.int64).sum().item()) if res["keys"] is not None else 0
+        sweep[f"{t}%"] = {"value": round(N * args.steps / el, 1), "ms_per_step": round(ms, 3), "kept_rows": kept,
+                          "check_ok": cnt == kept, "pipeline_frac": round(24 * N / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    agg.close()
+    out["selectivity_sweep"] = sweep
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(2)
+    vi = torch.randint(0, 1 << 20, (N,), device=dev, generator=gen, dtype=torch.int64)
+    agg = tfa.Aggregator(ctx, tfa.INT64, [(tfa.AGG_SUM, tfa.INT64), (tfa.AGG_COUNT_ALL, 0)],
+                         bucket_bits=args.bucket_bits, expected_groups=G)
+
+    def istep():
+        agg.reset()
+        agg.consume_filtered(f, tfa.LT, args.threshold, k, [vi, None])
+        return agg.result()
+    el, res, _ = timed(istep, args, ctx, 1)
+    ms = el / args.steps * 1e3
+    kept = int((f < args.threshold).sum().item())
+    exact = int(vi[f < args.threshold].sum().item()) == int(res["states"][0].sum().item())
+    out["int64_value"] = {"metric": "rows/s filter + GROUP BY, sum(Int64) + count (exact)",
+                          "value": round(N * args.steps / el, 1), "ms_per_step": round(ms, 3),
+                          "check_ok": exact and int(res["states"][1].sum().item()) == kept,
+                          "pipeline_frac": round(24 * N / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    agg.close()
+    del vi
+    return out
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     import torch
     import torch.distributed as dist
 
@@ -459,23 +588,7 @@ def main():
         final.consume_partial(outs[0], [outs[1], outs[2]])
         return final.result()
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    ctx.profile(True)
-    ctx.profile_reset()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        res = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    prof = ctx.profile_read()
-    ctx.profile(False)
+    el, res, prof = timed(step, args, ctx, world)
     # invariant of the last step's result: every kept row is counted exactly once over all ranks
     red_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
     inv = torch.tensor([float(res["states"][1].view(torch.int64).sum().item()), float(n_kept),
@@ -498,19 +611,24 @@ def main():
         "data": "synthetic: f~U[0,100) (pred f<96), k~U[0,1e6), v dyadic f64; seed 1+rank",
         "config": {"workload": "configs[1] filter + GROUP BY 1M keys" + (" two-phase + RCCL all-to-all" if world > 1 else ""),
                    "rows_per_gpu": N, "groups": G, "kept_rows_per_gpu": n_kept, "groups_out": groups,
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}", "dist_backend": args.dist_backend if world > 1 else None},
         "check": {"count_total": count_total, "kept_total": kept_total, "groups_total": groups_total,
                   "ok": count_total == kept_total and groups_total <= G},
     }
     if rank == 0:
-        rf = roofline_from_profile(prof, args.steps, N, n_kept)
+        rf = roofline_from_profile(prof, args.steps, N, n_kept, agg.size())
         if rf and "bound" in rf:
             rf["traffic"] = load_pmc_traffic(rf["kernel"])
+            if rf["traffic"]:
+                rf["traffic_over_algorithmic"] = round(rf["traffic"] / rf["algorithmic_bytes_per_launch"], 3)
         line["roofline"] = rf
         line["pipeline_roofline"] = {"algorithmic_bytes_per_step": 24 * N, "achieved": round(24 * N / (ms * 1e-3) / 1e9, 1),
                                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                      "frac": round(24 * N / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
         line["kernels_ms_per_step"] = {kname: round(v[0] / args.steps, 4) for kname, v in sorted(prof.items())}
+
+    if world == 1 and not args.no_variants:
+        line["c2_variants"] = variants_leg(args, ctx, dev, f, k, v)
 
     # ---- hash join probe (configs[2] shape) at N=1
     if world == 1 and not args.no_join:

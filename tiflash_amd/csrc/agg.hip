@@ -49,7 +49,6 @@ struct AggSpec {
     int cnt_off[AGG_MAX];
     int ctrl_off;
     int lds_bytes;
-    int dbg; // timing ablation knob (TFG_DBG_BUCKET), 0 in production
     int bt;         // bucket kernel workgroup size (BT or BT_BIG)
     int wkey_off;   // wide keys (key_width 16): LDS byte offset of the 16-byte keys (cells' tags sit in
                     // the u64 key array); 0 for keys of <= 8 bytes
@@ -567,7 +566,6 @@ template <int NA> struct GenericOps {
     __device__ __forceinline__ bool knull(const Row &v) const { return v.knull != 0; }
     __device__ __forceinline__ void add(Table &T, int cell, const Row &v) const { T.add_row<NA>(cell, v, mode); }
     __device__ __forceinline__ void store(const RowsIO &sp, int64_t w, const Row &v) const { store_row<NA>(S, sp, mode, w, v); }
-    __device__ __forceinline__ uint64_t probe_val(const Row &v) const { return v.lo[0]; }
 };
 
 template <int A0, int A1, int A2> struct FastOps {
@@ -617,7 +615,6 @@ template <int A0, int A1, int A2> struct FastOps {
         for (int i = 0; i < 3; ++i)
             if (op(i) >= 2) rec[pos(i)] = v.v[i];
     }
-    __device__ __forceinline__ uint64_t probe_val(const Row &v) const { return v.v[0]; }
 };
 
 // Wide keys (16-byte packed keys128 / String keys, staged as one uint4 per row): generic
@@ -648,7 +645,6 @@ template <int NA> struct WideOps {
         q.w = (unsigned)(v.khi >> 32);
         reinterpret_cast<uint4 *>(sp.key)[w] = q;
     }
-    __device__ __forceinline__ uint64_t probe_val(const Row &v) const { return v.lo[0]; }
 };
 
 template <typename Ops, int BT>
@@ -714,12 +710,6 @@ __global__ void __launch_bounds__(BT) agg_bucket_kernel(AggSpec S, RowsIO rows0,
                 ku[u] = ops.key(v[u]);
                 nu[u] = ops.knull(v[u]);
             }
-            if (S.dbg == 1) { // timing ablation: loads only
-#pragma unroll
-                for (int u = 0; u < RPT; ++u)
-                    if (vu[u] && ku[u] == 0x5555555555555555ull) T.ctrl->out_count += ops.probe_val(v[u]);
-                continue;
-            }
             uint64_t kh[RPT], tg[RPT];
             if constexpr (Ops::WIDE) {
 #pragma unroll
@@ -734,7 +724,7 @@ __global__ void __launch_bounds__(BT) agg_bucket_kernel(AggSpec S, RowsIO rows0,
 #pragma unroll
             for (int u = 0; u < RPT; ++u) {
                 miss[u] = false;
-                if (!vu[u] || S.dbg == 2) continue; // dbg 2: timing ablation, loads + probe/insert
+                if (!vu[u]) continue;
                 if (cells[u] >= 0) ops.add(T, cells[u], v[u]);
                 else miss[u] = true;
             }
@@ -913,8 +903,6 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
                         for (uint32_t st = CH / 2; st > 0; st >>= 1)
                             if (s_pref[lo + st] <= i) lo += st;
                         int64_t r = (int64_t)(t0 + (int)lo) * tin.TR + (s_ent[lo] & 0xFFFFu) + (i - s_pref[lo]);
-                        if (S.dbg == 5) r = (int64_t)b * 390000 + (int64_t)t0 * 30 + i; // ablation: contiguous reads
-                        if (S.dbg == 6) r = (int64_t)t0 * tin.TR + i;                    // ablation: no search dependency
                         ops.load(src, r, v[u]);
                     }
                 };
@@ -930,12 +918,6 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
                         ok[u] = okn[u];
                     }
                     if (base + BT * RPT < tot) load_step(base + BT * RPT, vn, okn);
-                    if (S.dbg == 1) { // timing ablation: search + loads only
-#pragma unroll
-                        for (int u = 0; u < RPT; ++u)
-                            if (ok[u] && ops.key(v[u]) == 0x5555555555555555ull) T.ctrl->out_count += ops.probe_val(v[u]);
-                        continue;
-                    }
                     step(v, ok);
                 }
                 __syncthreads();
@@ -1387,15 +1369,8 @@ int fast_signature(const AggSpec &S, int mode, int key_width, const uint8_t *key
     return code;
 }
 
-// The fast signatures over a tile-sorted partition (TFG_AGG_TILED=0 falls back to the
-// histogram + scatter partition): partition -> agg_bucket_tiled_kernel -> scan -> compaction.
-bool agg_tiled_enabled() {
-    static const bool on = [] {
-        const char *e = getenv("TFG_AGG_TILED");
-        return !e || atoi(e) != 0;
-    }();
-    return on;
-}
+// The fast signatures run over a tile-sorted partition: partition -> agg_bucket_tiled_kernel ->
+// scan -> compaction (the histogram + scatter partition serves the other signatures).
 
 template <typename Ops>
 void launch_bucket_tiled(int B, const AggSpec &S, hipStream_t st, const TiledIn &tin, int mode, const GroupsIO &old,
@@ -1511,7 +1486,7 @@ int consume_keyed(tfg_agg *a, int mode, const RowPred &pred, const void *keys, i
     const size_t n_old = a->n_groups;
     // fast signature: rows staged as interleaved records (key + summed arguments, 8 B each)
     const int fast = given_off ? 0 : fast_signature(S, mode, key_width, key_null, val_nulls);
-    if (fast && agg_tiled_enabled()) {
+    if (fast) {
         bool done = false;
         if (int rc = consume_fast_tiled(a, fast, pred, keys, vals, n, done)) return rc;
         if (done) return TFG_OK;
@@ -1847,7 +1822,6 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
     // one workgroup per CU anyway (LDS): make it 16 waves, and keep the in-flight insert headroom
     S.bt = S.lds_bytes > 80 * 1024 ? BT_BIG : BT;
     S.maxfill = std::max(1, std::min(cap * fill_num / 8, cap - S.bt - 8));
-    S.dbg = getenv("TFG_DBG_BUCKET") ? atoi(getenv("TFG_DBG_BUCKET")) : 0;
     if (a->nokey) {
         if (int rc = a->ensure_state(0, 1)) {
             delete a;

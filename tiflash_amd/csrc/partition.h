@@ -260,17 +260,12 @@ inline PartLayout make_layout(int64_t n, uint32_t P) {
     return L;
 }
 
-// Layout of the LDS-staged scatter: one long segment per CU (times TFG_STAGE_G, default 1), so
+// Layout of the LDS-staged scatter: `mult` long segments per CU (default 1), so
 // a destination's rows from one workgroup form a single long run (consecutive tiles continue
 // each other's partially written cache lines while they are still in L2) and the P x G count
 // table stays small; the histogram pass splits each segment over `sub` workgroups to keep the
 // chip full.
-inline PartLayout make_wide_layout(int64_t n, uint32_t P, int cu_count, unsigned gmax, int mult_default = 1) {
-    static const int env_mult = [] {
-        const char *e = getenv("TFG_STAGE_G");
-        return e ? std::max(1, atoi(e)) : 0;
-    }();
-    const int mult = env_mult ? env_mult : mult_default;
+inline PartLayout make_wide_layout(int64_t n, uint32_t P, int cu_count, unsigned gmax, int mult = 1) {
     PartLayout L;
     L.n = n;
     L.P = P;
@@ -468,8 +463,6 @@ struct StagedGeom {
     int crc_off;
     int red_off;
     int lds_bytes;
-    int dbg; // timing ablations (TFG_DBG_SCATTER): 1 no stream-out, 2 no placement / stream-out,
-             // 3 stream-out to tile-contiguous addresses (wrong results; isolates the write pattern)
     // tile-sorted mode (TILED kernels): tile k of segment g is written, sorted by destination, to
     // rows [(g * tps + k) * TR, + kept) of the output, and tile_hist[p * T + tile] receives the
     // destination's start inside the tile | its row count << 16
@@ -478,21 +471,15 @@ struct StagedGeom {
     int T;   // tiles
 };
 
-// LDS bytes a staged-scatter workgroup may use (TFG_STAGE_LDS overrides; tuning knob).
-inline size_t stage_lds_budget() {
-    static size_t v = [] {
-        const char *e = getenv("TFG_STAGE_LDS");
-        return e ? (size_t)atol(e) : (size_t)150 * 1024;
-    }();
-    return v;
-}
+// LDS bytes a staged-scatter workgroup uses: one workgroup per CU.
+constexpr size_t STAGE_LDS_BUDGET = (size_t)150 * 1024;
 
 inline bool make_staged_geom(uint32_t P, const PCols &cols, bool perm, bool crc, StagedGeom &g) {
     if (P > 4096) return false;
     size_t row_bytes = 2 + (perm ? 4 : 0);
     for (int j = 0; j < cols.ncols; ++j) row_bytes += cols.width[j];
     const size_t fixed = (size_t)P * 16 + (crc ? 8192 : 0) + 16 * (PCOLS + 2);
-    const size_t budget = stage_lds_budget(); // LDS per workgroup (default: one workgroup per CU)
+    const size_t budget = STAGE_LDS_BUDGET; // LDS per workgroup (default: one workgroup per CU)
     if (fixed + row_bytes * ST_T * 2 > budget) return false;
     int tr = (int)((budget - fixed) / row_bytes) / ST_T * ST_T;
     if (tr > ST_T * ST_MAXR) tr = ST_T * ST_MAXR;
@@ -508,11 +495,6 @@ inline bool make_staged_geom(uint32_t P, const PCols &cols, bool perm, bool crc,
     g.crc_off = (int)((off + 15) & ~size_t(15));
     g.red_off = g.crc_off + (crc ? 8192 : 0);
     g.lds_bytes = g.red_off + (ST_T / 64 + 2) * 4; // red[]: per-wave sums + the tile total
-    static const int dbg = [] {
-        const char *e = getenv("TFG_DBG_SCATTER");
-        return e ? atoi(e) : 0;
-    }();
-    g.dbg = dbg;
     return true;
 }
 
@@ -621,12 +603,6 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
             for (uint32_t p = threadIdx.x; p < P; p += ST_T) g.tile_hist[(size_t)p * g.T + tile] = start[p] | (hist[p] << 16);
         // 3. place rows in LDS in destination order
         uint32_t sl[ST_MAXR];
-        if (g.dbg == 2) {
-            __syncthreads();
-            for (uint32_t p = threadIdx.x; p < P; p += ST_T) run[p] += hist[p];
-            __syncthreads();
-            continue;
-        }
 #pragma unroll
         for (int j = 0; j < ST_MAXR; ++j) {
             if (bq[j] == 0xFFFFFFFFu) continue;
@@ -674,11 +650,11 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
         }
         __syncthreads();
         // 4. stream the sorted tile out: lanes of a run write consecutive addresses
-        for (uint32_t s = threadIdx.x; s < (g.dbg == 1 || g.dbg == 2 ? 0u : kept); s += ST_T) {
+        for (uint32_t s = threadIdx.x; s < kept; s += ST_T) {
             const uint32_t b = sb[s];
             uint64_t gp;
             if constexpr (TILED) gp = (uint64_t)tile * (uint32_t)g.TR + s;
-            else gp = g.dbg == 3 ? (uint64_t)(tb + s) : run[b] + (s - start[b]);
+            else gp = run[b] + (s - start[b]);
             if (perm) perm[gp] = sperm[s];
             if constexpr (AOS && NC8 == 2) { // one 16-byte record store per row
                 const uint64_t a0 = reinterpret_cast<const uint64_t *>(lds + g.stage_off[0])[s];
