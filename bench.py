@@ -336,7 +336,7 @@ def c5_leg(args, ctx, dev, world, rank):
     chars = chars.reshape(-1)
     offs = torch.arange(1, n + 1, device=dev, dtype=torch.int64) * 10
     v = torch.randint(0, 10**9, (n,), device=dev, generator=g, dtype=torch.int64)
-    aggs = [(tfa.AGG_SUM, tfa.DECIMAL64), (tfa.AGG_COUNT_ALL, 0)]
+    aggs = [(tfa.AGG_SUM, tfa.prec(tfa.DECIMAL64, 15)), (tfa.AGG_COUNT_ALL, 0)]
     part = tfa.KeysAggregator(ctx, [tfa.STRING], aggs, expected_groups=G)
     fin = tfa.KeysAggregator(ctx, [tfa.STRING], aggs, expected_groups=G) if world > 1 else None
 

@@ -62,6 +62,10 @@ typedef enum tfg_type {
     TFG_DECIMAL32 = 11,  /* Int32 payload  (precision <= 9)  */
     TFG_DECIMAL64 = 12,  /* Int64 payload  (precision <= 18) */
     TFG_DECIMAL128 = 13, /* Int128 payload (precision <= 38), little-endian two's complement */
+    TFG_DECIMAL256 = 14, /* 256-bit payload (precision <= 65), four little-endian 64-bit limbs, two's
+                          * complement: the reference's Decimal256 (boost checked_int256_t,
+                          * libs/libcommon/include/common/types.h:35) as a fixed-width value; sum
+                          * results and sum arguments only */
     TFG_STRING = 20,     /* ColumnString: chars (every row ends with '\0') + UInt64 end offsets
                           * (Columns/ColumnString.h:50-54); GROUP BY keys only */
     TFG_KEYS128 = 21,    /* a packed 16-byte GROUP BY key (see tfg_agg_create_keys): the device
@@ -97,8 +101,20 @@ typedef enum tfg_logic_op {
 /* Aggregate functions on the path (dbms/src/AggregateFunctions/AggregateFunctionSum.h,
  * AggregateFunctionCount.h).  Result types follow the reference factory
  * (AggregateFunctionSum.cpp:31-120): sum(Int*) -> Int64, sum(UInt*) -> UInt64,
- * sum(Float*) -> Float64, sum(Decimal(p,s)) -> Decimal(min(p+22,65), s) held as Int128;
- * count -> UInt64. */
+ * sum(Float*) -> Float64, sum(Decimal(p,s)) -> Decimal(min(p+22,65), s) (SumDecimalInferer,
+ * Common/Decimal.h:156-163): Decimal128 when p+22 <= 38 (Decimal32 / Decimal64 with p <= 16),
+ * else Decimal256 (Decimal64 with p >= 17, every Decimal128 / Decimal256 argument);
+ * count -> UInt64.
+ *
+ * An aggregate argument type word is the tfg_type, optionally or-ed with TFG_ARG_NULLABLE (the
+ * argument carries a null map) and, for Decimal arguments, TFG_ARG_PREC(p): the column's
+ * DataTypeDecimal precision (0 = the type's maximum, 9 / 18 / 38 / 65).  Decimal256 sums are
+ * exact: a Decimal(<=65) value is below 10^65 < 2^216, so fewer than 2^39 rows cannot reach the
+ * 2^255 bound where checked_int256_t would throw. */
+#define TFG_ARG_NULLABLE 0x100
+#define TFG_ARG_PREC(p) ((int)(p) << 16)
+#define TFG_ARG_TYPE(w) ((w) & 0xFF)
+#define TFG_ARG_PREC_OF(w) (((w) >> 16) & 0xFF)
 typedef enum tfg_agg_kind {
     TFG_AGG_SUM = 0,
     TFG_AGG_COUNT = 1,     /* count(arg): non-NULL rows of arg */
@@ -279,7 +295,8 @@ int tfg_agg_merge(tfg_agg *dst, tfg_agg *src);
 int tfg_agg_size(tfg_agg *agg, uint64_t *out_groups);
 /* convertToBlockImplFinal (Aggregator.cpp:1651-1780): writes every group.  out_keys: key type
  * width per group; out_key_nullmap (optional, nullable keys); out_states[i]: result type
- * width (8 B for Int64/UInt64/Float64 sums and counts, 16 B for Decimal sums);
+ * width (8 B for Int64/UInt64/Float64 sums and counts, 16 B for Decimal128 sums, 32 B for
+ * Decimal256 sums);
  * out_state_nullmaps[i] (optional): 1 when sum saw no non-NULL value (AggregateFunctionNull).
  * Order is the table's (compare unordered, as the reference tests do). */
 int tfg_agg_result(tfg_agg *agg, void *out_keys, uint8_t *out_key_nullmap, void *const *out_states,

@@ -91,6 +91,7 @@ static size_t type_width(int t)
     case TFG_INT32: case TFG_UINT32: case TFG_FLOAT32: case TFG_DECIMAL32: return 4;
     case TFG_INT64: case TFG_UINT64: case TFG_FLOAT64: case TFG_DECIMAL64: return 8;
     case TFG_DECIMAL128: return 16;
+    case TFG_DECIMAL256: return 32;
     default: return 0;
     }
 }
@@ -467,11 +468,55 @@ struct orc_agg {
     size_t n_groups, cap_groups;
     uint64_t *gkeys;
     uint8_t *gkey_null;
+    int prec[ORC_MAX_AGGS];       /* Decimal argument precision (0: the type's maximum) */
+    int wide[ORC_MAX_AGGS];       /* sum result is Decimal256 (SumDecimalInferer: p + 22 > 38) */
     __int128 *acc_i[ORC_MAX_AGGS]; /* integer / decimal accumulators (wrap per result width) */
+    uint64_t *acc_w[ORC_MAX_AGGS]; /* Decimal256 accumulators: 4 little-endian limbs per group */
     double *acc_f[ORC_MAX_AGGS];
     uint64_t *cnt[ORC_MAX_AGGS]; /* non-NULL rows seen */
     int64_t null_group;           /* group index of the NULL key, -1 */
 };
+
+/* Result precision of sum(Decimal(p, s)): SumDecimalInferer::infer (Common/Decimal.h:156-163),
+ * min(p + 22, 65); the result is Decimal256 above 38 digits (createDecimal, DataTypes/DataTypeDecimal.h). */
+static int decimal_max_prec(int t)
+{
+    return t == TFG_DECIMAL32 ? 9 : t == TFG_DECIMAL64 ? 18 : t == TFG_DECIMAL128 ? 38 : 65;
+}
+static int is_decimal_t(int t)
+{
+    return t == TFG_DECIMAL32 || t == TFG_DECIMAL64 || t == TFG_DECIMAL128 || t == TFG_DECIMAL256;
+}
+int orc_sum_result_prec(int arg_type_word)
+{
+    const int t = arg_type_word & 0xFF;
+    int p = (arg_type_word >> 16) & 0xFF;
+    if (!is_decimal_t(t)) return 0;
+    if (p == 0) p = decimal_max_prec(t);
+    return p + 22 < 65 ? p + 22 : 65;
+}
+
+/* 256-bit two's complement add (boost checked_int256_t sums: exact below 2^255) */
+static void add256(uint64_t *acc, const uint64_t *x)
+{
+    unsigned __int128 c = 0;
+    for (int k = 0; k < 4; ++k) {
+        c += (unsigned __int128)acc[k] + x[k];
+        acc[k] = (uint64_t)c;
+        c >>= 64;
+    }
+}
+static void load_i256(int t, const void *p, size_t i, uint64_t *x)
+{
+    if (t == TFG_DECIMAL256) {
+        memcpy(x, (const char *)p + 32 * i, 32);
+        return;
+    }
+    __int128 v = load_i128(t, p, i);
+    x[0] = (uint64_t)v;
+    x[1] = (uint64_t)((unsigned __int128)v >> 64);
+    x[2] = x[3] = v < 0 ? ~0ull : 0ull;
+}
 
 orc_agg *orc_agg_create(int key_type, int n_aggs, const int *kinds, const int *arg_types)
 {
@@ -480,8 +525,11 @@ orc_agg *orc_agg_create(int key_type, int n_aggs, const int *kinds, const int *a
     a->key_type = key_type;
     a->n_aggs = n_aggs;
     for (int i = 0; i < n_aggs; ++i) {
+        const int w = arg_types ? arg_types[i] : 0;
         a->kinds[i] = kinds[i];
-        a->arg_types[i] = arg_types ? arg_types[i] : 0;
+        a->arg_types[i] = w & 0xFF;
+        a->prec[i] = (w >> 16) & 0xFF;
+        a->wide[i] = kinds[i] == TFG_AGG_SUM && orc_sum_result_prec(w) > 38;
     }
     hmap_init(&a->map);
     a->null_group = -1;
@@ -496,6 +544,7 @@ void orc_agg_destroy(orc_agg *a)
     free(a->gkey_null);
     for (int i = 0; i < a->n_aggs; ++i) {
         free(a->acc_i[i]);
+        free(a->acc_w[i]);
         free(a->acc_f[i]);
         free(a->cnt[i]);
     }
@@ -510,6 +559,7 @@ static int64_t agg_new_group(orc_agg *a, uint64_t key, uint8_t is_null)
         a->gkey_null = (uint8_t *)realloc(a->gkey_null, nc);
         for (int i = 0; i < a->n_aggs; ++i) {
             a->acc_i[i] = (__int128 *)realloc(a->acc_i[i], nc * sizeof(__int128));
+            a->acc_w[i] = (uint64_t *)realloc(a->acc_w[i], nc * 4 * sizeof(uint64_t));
             a->acc_f[i] = (double *)realloc(a->acc_f[i], nc * sizeof(double));
             a->cnt[i] = (uint64_t *)realloc(a->cnt[i], nc * sizeof(uint64_t));
         }
@@ -520,6 +570,7 @@ static int64_t agg_new_group(orc_agg *a, uint64_t key, uint8_t is_null)
     a->gkey_null[g] = is_null;
     for (int i = 0; i < a->n_aggs; ++i) { /* createAggregateStates: zero-initialised sums */
         a->acc_i[i][g] = 0;
+        memset(a->acc_w[i] + 4 * g, 0, 32);
         a->acc_f[i][g] = 0.0;
         a->cnt[i][g] = 0;
     }
@@ -561,7 +612,11 @@ void orc_agg_consume(orc_agg *a, const void *keys, const uint8_t *key_null, cons
             if (a->kinds[i] == TFG_AGG_COUNT) continue;
             int t = a->arg_types[i];
             if (is_float(t)) a->acc_f[i][g] += load_f(t, args[i], r);
-            else a->acc_i[i][g] = (__int128)((unsigned __int128)a->acc_i[i][g] + (unsigned __int128)load_i128(t, args[i], r));
+            else if (a->wide[i]) {
+                uint64_t x[4];
+                load_i256(t, args[i], r, x);
+                add256(a->acc_w[i] + 4 * g, x);
+            } else a->acc_i[i][g] = (__int128)((unsigned __int128)a->acc_i[i][g] + (unsigned __int128)load_i128(t, args[i], r));
         }
     }
 }
@@ -575,15 +630,16 @@ void orc_agg_merge(orc_agg *dst, const orc_agg *src)
             dst->cnt[i][d] += src->cnt[i][g];
             dst->acc_f[i][d] += src->acc_f[i][g];
             dst->acc_i[i][d] = (__int128)((unsigned __int128)dst->acc_i[i][d] + (unsigned __int128)src->acc_i[i][g]);
+            add256(dst->acc_w[i] + 4 * d, src->acc_w[i] + 4 * g);
         }
     }
 }
 
 size_t orc_agg_size(const orc_agg *a) { return a->n_groups; }
 
-static int sum_result_width(int arg_type)
+static int sum_result_width(const orc_agg *a, int i)
 {
-    return (arg_type == TFG_DECIMAL32 || arg_type == TFG_DECIMAL64 || arg_type == TFG_DECIMAL128) ? 16 : 8;
+    return a->wide[i] ? 32 : is_decimal_t(a->arg_types[i]) ? 16 : 8;
 }
 
 /* insertAggregatesIntoColumns (Aggregator.cpp:1651-1780). Order: group creation order. */
@@ -599,7 +655,8 @@ void orc_agg_result(const orc_agg *a, uint64_t *out_keys, uint8_t *out_key_null,
             if (a->kinds[i] != TFG_AGG_SUM) { ((uint64_t *)out_states[i])[g] = a->cnt[i][g]; continue; }
             int t = a->arg_types[i];
             if (is_float(t)) ((double *)out_states[i])[g] = a->acc_f[i][g];
-            else if (sum_result_width(t) == 16) memcpy((char *)out_states[i] + 16 * g, &a->acc_i[i][g], 16);
+            else if (sum_result_width(a, i) == 32) memcpy((char *)out_states[i] + 32 * g, a->acc_w[i] + 4 * g, 32);
+            else if (sum_result_width(a, i) == 16) memcpy((char *)out_states[i] + 16 * g, &a->acc_i[i][g], 16);
             else ((int64_t *)out_states[i])[g] = (int64_t)a->acc_i[i][g];
         }
     }

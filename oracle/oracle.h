@@ -41,13 +41,16 @@ int orc_arith(int op, int a_type, const void *a, int a_const, int a_scale, int b
               int b_scale, int res_type, int res_scale, size_t n, void *out);
 
 typedef struct orc_agg orc_agg;
+/* arg_types[i]: tfg_type | TFG_ARG_PREC(p) (include/tiflash_amd.h); sum(Decimal(p,s)) keeps a
+ * Decimal256 state when min(p + 22, 65) > 38 (SumDecimalInferer). */
+int orc_sum_result_prec(int arg_type_word);
 orc_agg *orc_agg_create(int key_type, int n_aggs, const int *kinds, const int *arg_types);
 void orc_agg_destroy(orc_agg *a);
 void orc_agg_consume(orc_agg *a, const void *keys, const uint8_t *key_null, const void *const *args,
                      const uint8_t *const *arg_nulls, const uint8_t *mask, size_t n);
 void orc_agg_merge(orc_agg *dst, const orc_agg *src);
 size_t orc_agg_size(const orc_agg *a);
-/* out_keys: u64 key bits; out_key_null; out_states[i]: 8 or 16 B per group; out_state_null[i]. */
+/* out_keys: u64 key bits; out_key_null; out_states[i]: 8, 16 or 32 B per group; out_state_null[i]. */
 void orc_agg_result(const orc_agg *a, uint64_t *out_keys, uint8_t *out_key_null, void *const *out_states,
                     uint8_t *const *out_state_null);
 
@@ -91,6 +94,11 @@ size_t orc_bench_string_agg(const uint8_t *chars, const uint64_t *offsets, const
                             size_t block_rows, uint64_t *checksum);
 size_t orc_bench_join(const int64_t *build_keys, size_t nb, const int64_t *probe_keys, size_t np, int nthreads,
                       uint64_t *checksum);
+
+/* CHBlockChunkCodec / V1 (NONE) restated (codec.c): packet bytes of n rows (see codec.c). */
+size_t orc_codec_encode(int version, int ncols, const char *const *names, const char *const *types,
+                        const void *const *data, const uint64_t *const *offsets, const uint8_t *const *nullmaps,
+                        int64_t n, int nparts, const int64_t *part_rows, uint8_t *out, size_t cap);
 
 #ifdef __cplusplus
 }

@@ -17,8 +17,41 @@ _PATH = os.path.join(_HERE, "liboracle.so")
 _L = None
 
 INT8, INT16, INT32, INT64, UINT8, UINT16, UINT32, UINT64, FLOAT32, FLOAT64 = range(1, 11)
-DECIMAL32, DECIMAL64, DECIMAL128 = 11, 12, 13
+DECIMAL32, DECIMAL64, DECIMAL128, DECIMAL256 = 11, 12, 13, 14
 STRING = 20
+NULLABLE = 0x100
+
+
+def prec(t: int, p: int) -> int:
+    """Aggregate argument type word of a Decimal column with precision p (TFG_ARG_PREC)."""
+    return t | (p << 16)
+
+
+def sum_result_prec(t: int) -> int:
+    """SumDecimalInferer (Common/Decimal.h:156-163): min(p + 22, 65); 0 for non-decimal args."""
+    return lib().orc_sum_result_prec(int(t) & ~NULLABLE)
+
+
+def sum_limbs(kind: int, t: int) -> int:
+    """Words of a sum result: 1 (Int64 / UInt64 / Float64), 2 (Decimal128) or 4 (Decimal256)."""
+    base = t & 0xFF
+    if kind != 0 or base not in (DECIMAL32, DECIMAL64, DECIMAL128, DECIMAL256):
+        return 1
+    return 4 if sum_result_prec(t) > 38 else 2
+
+
+def limbs_to_int(row) -> int:
+    """Little-endian two's complement 64-bit limbs -> Python int."""
+    v = 0
+    for i, w in enumerate(row):
+        v |= (int(w) & ((1 << 64) - 1)) << (64 * i)
+    bits = 64 * len(row)
+    return v - (1 << bits) if v >> (bits - 1) else v
+
+
+def int_to_limbs(v: int, n: int) -> np.ndarray:
+    m = v & ((1 << (64 * n)) - 1)
+    return np.array([(m >> (64 * i)) & ((1 << 64) - 1) for i in range(n)], dtype=np.uint64).view(np.int64)
 NP_TYPE = {np.dtype(np.int8): INT8, np.dtype(np.int16): INT16, np.dtype(np.int32): INT32, np.dtype(np.int64): INT64,
            np.dtype(np.uint8): UINT8, np.dtype(np.uint16): UINT16, np.dtype(np.uint32): UINT32,
            np.dtype(np.uint64): UINT64, np.dtype(np.float32): FLOAT32, np.dtype(np.float64): FLOAT64}
@@ -173,7 +206,7 @@ class Agg:
 
     def __init__(self, key_type: int, aggs):
         kinds = (ctypes.c_int * len(aggs))(*[k for k, _ in aggs])
-        types = (ctypes.c_int * len(aggs))(*[t & 0xFF for _, t in aggs])
+        types = (ctypes.c_int * len(aggs))(*[t & ~NULLABLE for _, t in aggs])
         self.aggs = list(aggs)
         self.h = ctypes.c_void_p(lib().orc_agg_create(key_type, len(aggs), kinds, types))
         self.key_type = key_type
@@ -195,13 +228,13 @@ class Agg:
         key_null = np.empty(g, dtype=np.uint8)
         states, snull = [], []
         for kind, t in self.aggs:
-            wide = kind == 0 and (t & 0xFF) in (DECIMAL32, DECIMAL64, DECIMAL128)
+            limbs = sum_limbs(kind, t)
             if kind != 0:
                 states.append(np.empty(g, dtype=np.uint64))
             elif (t & 0xFF) in (FLOAT32, FLOAT64):
                 states.append(np.empty(g, dtype=np.float64))
-            elif wide:
-                states.append(np.empty((g, 2), dtype=np.int64))
+            elif limbs > 1:
+                states.append(np.empty((g, limbs), dtype=np.int64))
             else:
                 states.append(np.empty(g, dtype=np.int64))
             snull.append(np.empty(g, dtype=np.uint8))
@@ -214,9 +247,9 @@ class Agg:
             self.h = None
 
 
-_SIGNED = {INT8, INT16, INT32, INT64, DECIMAL32, DECIMAL64, DECIMAL128}
+_SIGNED = {INT8, INT16, INT32, INT64, DECIMAL32, DECIMAL64, DECIMAL128, DECIMAL256}
 _KW = {INT8: 1, INT16: 2, INT32: 4, INT64: 8, UINT8: 1, UINT16: 2, UINT32: 4, UINT64: 8, FLOAT32: 4, FLOAT64: 8,
-       DECIMAL32: 4, DECIMAL64: 8, DECIMAL128: 16}
+       DECIMAL32: 4, DECIMAL64: 8, DECIMAL128: 16, DECIMAL256: 32}
 
 
 class AggKeys:
@@ -230,7 +263,7 @@ class AggKeys:
         kt = (ctypes.c_int * len(key_types))(*key_types)
         co = (ctypes.c_int * len(key_types))(*(collators or [0] * len(key_types)))
         kinds = (ctypes.c_int * len(aggs))(*[k for k, _ in aggs])
-        types = (ctypes.c_int * len(aggs))(*[t & 0xFF for _, t in aggs])
+        types = (ctypes.c_int * len(aggs))(*[t & ~NULLABLE for _, t in aggs])
         self.h = ctypes.c_void_p(lib().orc_aggk_create(len(key_types), kt, co, len(aggs), kinds, types))
 
     def consume(self, keys, args, key_nulls=None, arg_nulls=None, mask=None):
@@ -278,9 +311,10 @@ class AggKeys:
         ko = np.zeros(max(g, 1), np.uint64)
         states, snull = [], []
         for kind, t in self.aggs:
+            limbs = sum_limbs(kind, t)
             t &= 0xFF
-            if kind == 0 and t in (DECIMAL32, DECIMAL64, DECIMAL128):
-                states.append(np.zeros((max(g, 1), 2), np.int64))
+            if limbs > 1:
+                states.append(np.zeros((max(g, 1), limbs), np.int64))
             elif kind == 0 and t in (FLOAT32, FLOAT64):
                 states.append(np.zeros(max(g, 1), np.float64))
             else:
@@ -296,7 +330,7 @@ class AggKeys:
             vals = []
             for st in states:
                 v = st[i]
-                vals.append(int(v[0]) & ((1 << 64) - 1) | (int(v[1]) << 64) if st.ndim == 2 else v.item())
+                vals.append(limbs_to_int(v) if st.ndim == 2 else v.item())
             groups.append((key, vals))
         return groups
 

@@ -1121,6 +1121,129 @@ TEST(AutoPassThroughHashAgg) {
     EXPECT(pass > 0 && st.count((int)AutoPassThroughHashAggContext::State::Selective));
 }
 
+// Decimal precision (DataTypeDecimal(prec, scale)) through the operators: sum(Decimal(p, s)) ->
+// Decimal(min(p + 22, 65), s) (SumDecimalInferer, Common/Decimal.h:156-163): Decimal(15,2) keeps an
+// Int128 state, Decimal(18,2) and Decimal(38,4) a Decimal256 one (exact past Int128); and the
+// packet header names the column's real precision, so the V1 packet of a Decimal(15,2) column is
+// byte-identical to the oracle's (CodecUtils::checkDataTypeName on the receiver compares names).
+static void add256(uint64_t *a, __int128 v) {
+    const uint64_t x[4] = {(uint64_t)v, (uint64_t)((unsigned __int128)v >> 64), v < 0 ? ~0ull : 0ull, v < 0 ? ~0ull : 0ull};
+    unsigned __int128 c = 0;
+    for (int k = 0; k < 4; ++k) {
+        c += (unsigned __int128)a[k] + x[k];
+        a[k] = (uint64_t)c;
+        c >>= 64;
+    }
+}
+
+TEST(DecimalPrecisionSumAndCodec) {
+    const size_t n = 50000;
+    std::mt19937_64 rng(77);
+    std::vector<int64_t> k(n), d15(n), d18(n);
+    std::vector<__int128> d38(n);
+    for (size_t i = 0; i < n; ++i) {
+        k[i] = (int64_t)(rng() % 300);
+        d15[i] = (int64_t)(rng() % 1999999999999999ull) - 999999999999999ll;
+        d18[i] = (int64_t)(rng() % 1999999999999999999ull) - 999999999999999999ll;
+        const __int128 hi = (__int128)((rng() % (1ull << 61)) + (1ull << 61)) * ((rng() % 5) ? 1 : -1);
+        d38[i] = (hi << 64) + (__int128)rng();
+    }
+    DataType i64;
+    DataType t15 = DataType::decimal(15, 2), t18 = DataType::decimal(18, 2), t38 = DataType::decimal(38, 4);
+    EXPECT(t15.type == TFG_DECIMAL64 && t18.type == TFG_DECIMAL64 && t38.type == TFG_DECIMAL128);
+    EXPECT(t15.getName() == "Decimal(15,2)" && t38.getName() == "Decimal(38,4)");
+    EXPECT(!(t15 == t18));
+    Block b{{makeColumn(ctx, i64, k.data(), n), i64, "k"},
+            {makeColumn(ctx, t15, d15.data(), n), t15, "d15"},
+            {makeColumn(ctx, t18, d18.data(), n), t18, "d18"},
+            {makeColumn(ctx, t38, d38.data(), n), t38, "d38"}};
+    Aggregator::Params p;
+    p.src_header = b;
+    p.keys = {"k"};
+    p.aggregates = {{"sum", {"d15"}, "s15"}, {"sum", {"d18"}, "s18"}, {"sum", {"d38"}, "s38"}};
+    Aggregator agg(ctx, p);
+    agg.executeOnBlock(b);
+    Block r = agg.convertToBlock();
+    const IColumn &s15 = *r.getByName("s15").column, &s18 = *r.getByName("s18").column, &s38 = *r.getByName("s38").column;
+    EXPECT(s15.type.type == TFG_DECIMAL128 && s15.type.getName() == "Decimal(37,2)");
+    EXPECT(s18.type.type == TFG_DECIMAL256 && s18.type.getName() == "Decimal(40,2)" && s18.type.width() == 32);
+    EXPECT(s38.type.type == TFG_DECIMAL256 && s38.type.getName() == "Decimal(60,4)");
+    std::map<int64_t, std::vector<uint64_t>> want; // key -> 3 x 4 limbs
+    for (size_t i = 0; i < n; ++i) {
+        auto &w = want[k[i]];
+        w.resize(12);
+        add256(&w[0], d15[i]);
+        add256(&w[4], d18[i]);
+        add256(&w[8], d38[i]);
+    }
+    auto rk = toHost<int64_t>(ctx, *r.getByName("k").column);
+    auto b15 = toHostBytes(ctx, s15), b18 = toHostBytes(ctx, s18), b38 = toHostBytes(ctx, s38);
+    EXPECT(rk.size() == want.size());
+    bool past128 = false;
+    for (size_t g = 0; g < rk.size(); ++g) {
+        const auto &w = want[rk[g]];
+        __int128 v15;
+        memcpy(&v15, b15.data() + 16 * g, 16);
+        uint64_t lo15[4] = {0, 0, 0, 0};
+        add256(lo15, v15);
+        EXPECT(memcmp(lo15, &w[0], 32) == 0);
+        EXPECT(memcmp(b18.data() + 32 * g, &w[4], 32) == 0);
+        EXPECT(memcmp(b38.data() + 32 * g, &w[8], 32) == 0);
+        past128 = past128 || (w[10] != 0 && w[10] != ~0ull) || ((w[9] >> 63) != (w[10] & 1));
+    }
+    EXPECT(past128); // some Decimal(38,4) sums leave Int128
+    // codec: the Decimal(15,2) header and bytes equal the oracle's packet
+    Block cb{{b.getByName("d15").column, t15, "d15"}};
+    CHBlockChunkCodecV1 codec(ctx, cb.cloneEmpty());
+    DevicePacket pk = codec.encode(cb);
+    std::vector<uint8_t> got(pk.bytes);
+    check(tfg_download(ctx.raw(), got.data(), pk.buf->data(), pk.bytes), "download");
+    const char *names[1] = {"d15"}, *types[1] = {"Decimal(15,2)"};
+    const void *data[1] = {d15.data()};
+    const uint64_t *offs[1] = {nullptr};
+    const uint8_t *nms[1] = {nullptr};
+    const size_t want_bytes = orc_codec_encode(TFG_CODEC_V1, 1, names, types, data, offs, nms, (int64_t)n, 0, nullptr,
+                                               nullptr, 0);
+    std::vector<uint8_t> exp(want_bytes);
+    orc_codec_encode(TFG_CODEC_V1, 1, names, types, data, offs, nms, (int64_t)n, 0, nullptr, exp.data(), exp.size());
+    EXPECT(got == exp);
+    Block back = CHBlockChunkCodecV1::decode(ctx, cb.cloneEmpty(), pk);
+    EXPECT(back.getByName("d15").column->type == t15);
+}
+
+// DataTypeDecimal_test A (gtest_funtions_decimal_arith.cpp:47-77): Decimal(10,4) (+|-) Decimal(10,6)
+// has scale max(4, 6) = 6 and Decimal(10,4) * Decimal(10,6) scale 4 + 6 = 10; precision per
+// PlusDecimalInferer / MulDecimalInferer (Common/Decimal.h:109-163), values vs Int128 arithmetic.
+TEST(DecimalArithInferers) {
+    const size_t n = 1000;
+    std::mt19937_64 rng(5);
+    std::vector<int64_t> a(n), b(n);
+    for (size_t i = 0; i < n; ++i) {
+        a[i] = (int64_t)(rng() % 19999999999ull) - 9999999999ll; // |a| < 10^10: Decimal(10,4)
+        b[i] = (int64_t)(rng() % 19999999999ull) - 9999999999ll;
+    }
+    DataType ta = DataType::decimal(10, 4), tb = DataType::decimal(10, 6);
+    Block blk{{makeColumn(ctx, ta, a.data(), n), ta, "a"}, {makeColumn(ctx, tb, b.data(), n), tb, "b"}};
+    auto e = std::make_shared<ExpressionActions>(ctx);
+    e->arithmetic(TFG_PLUS, "a", "b", "p");
+    e->arithmetic(TFG_MINUS, "a", "b", "m");
+    e->arithmetic(TFG_MULTIPLY, "a", "b", "x");
+    e->execute(blk);
+    const IColumn &p = *blk.getByName("p").column, &m = *blk.getByName("m").column, &x = *blk.getByName("x").column;
+    EXPECT(p.type.scale == 6 && m.type.scale == 6 && x.type.scale == 10);
+    EXPECT(p.type.getName() == "Decimal(13,6)" && p.type.type == TFG_DECIMAL64);
+    EXPECT(x.type.getName() == "Decimal(20,10)" && x.type.type == TFG_DECIMAL128);
+    auto hp = toHost<int64_t>(ctx, p), hm = toHost<int64_t>(ctx, m);
+    auto hx = toHost<__int128>(ctx, x);
+    size_t bad = 0;
+    for (size_t i = 0; i < n; ++i) {
+        bad += hp[i] != a[i] * 100 + b[i];
+        bad += hm[i] != a[i] * 100 - b[i];
+        bad += hx[i] != (__int128)a[i] * b[i];
+    }
+    EXPECT(bad == 0);
+}
+
 int main(int argc, char **argv) {
     g_root = argc > 1 ? argv[1] : ".";
     const char *filter = argc > 2 ? argv[2] : nullptr;

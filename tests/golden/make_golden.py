@@ -10,7 +10,14 @@ reference_cases.json — known answers TRANSCRIBED (as data) from the reference'
     expected inner / left / semi / anti results).  The reference keys are strings "1".."4"; join
     equality is unchanged when they are written as the integers 1..4, which is how they are stored;
   * exchange: dbms/src/Flash/Mpp/tests/gtest_mpp_exchange_writer.cpp:663-718 (64 blocks of keys
-    0..63, 4 partitions -> 1024 rows each).
+    0..63, 4 partitions -> 1024 rows each);
+  * aggregates: aggregate VALUES the reference's tests pin — the clerk table
+    (gtest_aggregation_executor.cpp:272-290) with AggregationCount's expected count columns
+    (:562-585), test_table (:102-106) with RepeatedAggregateFunction's sum(s2) = 6 (:755-757);
+  * sum_types: result types of sum — integer inputs per gtest_sum_int_agg_func.cpp:88-99
+    (ReturnTypeForIntegerInputs), Decimal inputs per SumDecimalInferer (Common/Decimal.h:156-163,
+    Decimal(min(p+22, 65), s)), the Decimal256 bound of 65 digits (gtest_decimal_type.cpp:52-62) and
+    the +/-/* result scales of DataTypeDecimal_test A (gtest_funtions_decimal_arith.cpp:47-77).
 crc_vectors.json — CRC32-C / WeakHash32 vectors computed with the x86 SSE4.2 crc32q instruction,
   the instruction the reference itself hashes with (Common/HashTable/Hash.h:70-95), via oracle.
 """
@@ -93,6 +100,37 @@ def groupby_keys_cases():
             "cases": [{"group_by": g, "expected": e} for g, e in expected]}
 
 
+def aggregate_cases():
+    clerk = {  # gtest_aggregation_executor.cpp:272-290
+        "age": [30, N, 27, 32, 25, 36, N, 22, 34],
+        "gender": ["male", "female", "female", "male", "female", "female", "male", "female", "male"],
+        "country": ["russia", "korea", "usa", "usa", "usa", "china", "china", "china", "china"],
+        "salary": [1000.1, 1300.2, 0.3, N, -200.4, 900.5, -999.6, 2000.7, -300.8],
+        "pr": [1, 2, 0, 3290124, 968933, 3125, 31236, 4327, 80000],
+    }
+    counts = [  # AggregationCount (:562-585): expected count columns, in unspecified group order
+        {"func": "count(age)", "group_by": ["country"], "expected": [3, 3, 1, 0]},
+        {"func": "count(gender)", "group_by": ["country", "gender"], "expected": [2, 2, 2, 1, 1, 1]},
+        {"func": "count(1)", "group_by": [], "expected": [9]},
+        {"func": "count(1)", "group_by": ["country"], "expected": [4, 3, 1, 1]},
+        {"func": "count(pr)", "group_by": ["country"], "expected": [4, 3, 1, 1]},
+    ]
+    test_table = {"s1": [1, 2, 3], "s2": [1, 2, 3]}  # :102-106
+    return {"clerk": clerk, "counts": counts, "test_table": test_table,
+            "sums": [{"func": "sum(s2)", "group_by": [], "expected": [6]}]}  # :755-757
+
+
+def sum_type_cases():
+    ints = [  # gtest_sum_int_agg_func.cpp:88-99 (tfg type codes of include/tiflash_amd.h)
+        (1, "Int64"), (2, "Int64"), (3, "Int64"), (4, "Int64"),
+        (5, "UInt64"), (6, "UInt64"), (7, "UInt64"), (8, "UInt64"),
+    ]
+    decimals = [{"arg_prec": p, "result_prec": min(p + 22, 65)} for p in (1, 9, 10, 15, 16, 17, 18, 19, 38, 43, 65)]
+    return {"int": [{"arg_type": t, "result": r} for t, r in ints], "decimal": decimals,
+            "decimal256_max_digits": 65,  # gtest_decimal_type.cpp:52-62: 65 nines parse, 66 digits do not
+            "arith_scales": {"lhs": [10, 4], "rhs": [10, 6], "plus": 6, "minus": 6, "multiply": 10}}
+
+
 def crc_vectors():
     from oracle import oracle as orc
     rng = np.random.default_rng(2024)
@@ -111,7 +149,8 @@ def crc_vectors():
 if __name__ == "__main__":
     with open(os.path.join(HERE, "reference_cases.json"), "w") as f:
         json.dump({"groupby": groupby_cases(), "groupby_keys": groupby_keys_cases(), "join": join_cases(),
-                   "exchange": {"block_rows": 64, "blocks": 64, "parts": 4, "rows_per_part": 1024}}, f, indent=1)
+                   "exchange": {"block_rows": 64, "blocks": 64, "parts": 4, "rows_per_part": 1024},
+                   "aggregates": aggregate_cases(), "sum_types": sum_type_cases()}, f, indent=1)
     with open(os.path.join(HERE, "crc_vectors.json"), "w") as f:
         json.dump(crc_vectors(), f, indent=1)
     print("wrote", os.listdir(HERE))

@@ -104,7 +104,7 @@ def main():
 
         # ---- C5: two-phase GROUP BY String key, sum(Decimal(15,2)) + count(*)
         chars, offs, nulls, v = agg_data(rank)
-        aggs = [(tfa.AGG_SUM, tfa.DECIMAL64), (tfa.AGG_COUNT_ALL, 0)]
+        aggs = [(tfa.AGG_SUM, tfa.prec(tfa.DECIMAL64, 15)), (tfa.AGG_COUNT_ALL, 0)]
         part = tfa.KeysAggregator(ctx, [tfa.STRING], aggs, expected_groups=10_000)
         fin = tfa.KeysAggregator(ctx, [tfa.STRING], aggs, expected_groups=10_000)
         part.consume([(T(chars), T(offs.astype(np.int64)))], [T(v), None], key_nullmaps=[T(nulls)])

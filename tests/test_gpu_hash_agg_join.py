@@ -164,19 +164,106 @@ def test_groupby_nullable_keys_and_args(tfa, ctx, dev, orc, key_dtype, kt):
     assert _gpu_rows(g.result(), key_dtype, True) == _ref_rows(ref.result(), key_dtype, True)
 
 
+def _limbs_to_ints(a):
+    """(n, L) int64 limbs (little-endian two's complement) -> Python ints."""
+    from oracle.oracle import limbs_to_int
+    return [limbs_to_int(r) for r in a]
+
+
+def _exact_group_sums(k, vals):
+    """Python big-int sums per key: the exact value boost checked_int256_t holds (no overflow)."""
+    out = {}
+    for key, v in zip(k.tolist(), vals):
+        out[key] = out.get(key, 0) + v
+    return out
+
+
+def test_groupby_decimal_sum_result_types(tfa, ctx):
+    """SumDecimalInferer (Common/Decimal.h:156-163) -> Decimal(min(p+22,65)): Decimal128 up to 38
+    digits, Decimal256 above (AggregateFunctionSum.cpp:57-85); integer sums per
+    gtest_sum_int_agg_func.cpp ReturnTypeForIntegerInputs."""
+    import ctypes
+    cases = [(tfa.prec(tfa.DECIMAL32, 9), tfa.DECIMAL128, 16), (tfa.prec(tfa.DECIMAL64, 15), tfa.DECIMAL128, 16),
+             (tfa.prec(tfa.DECIMAL64, 16), tfa.DECIMAL128, 16), (tfa.prec(tfa.DECIMAL64, 17), tfa.DECIMAL256, 32),
+             (tfa.DECIMAL64, tfa.DECIMAL256, 32), (tfa.prec(tfa.DECIMAL128, 19), tfa.DECIMAL256, 32),
+             (tfa.DECIMAL128, tfa.DECIMAL256, 32), (tfa.prec(tfa.DECIMAL256, 65), tfa.DECIMAL256, 32),
+             (tfa.INT8, tfa.INT64, 8), (tfa.INT32, tfa.INT64, 8), (tfa.UINT16, tfa.UINT64, 8),
+             (tfa.UINT64, tfa.UINT64, 8), (tfa.FLOAT32, tfa.FLOAT64, 8)]
+    for arg, want_t, want_w in cases:
+        g = tfa.Aggregator(ctx, tfa.INT64, [(tfa.AGG_SUM, arg)])
+        t, w = ctypes.c_int(), ctypes.c_int()
+        tfa.check(tfa.lib().tfg_agg_result_type(g.h, 0, ctypes.byref(t), ctypes.byref(w)))
+        assert (t.value, w.value) == (want_t, want_w), (hex(arg), t.value, w.value)
+        g.close()
+
+
 def test_groupby_decimal_sum_exact(tfa, ctx, dev, orc):
-    """sum(Decimal64) -> Decimal128 (SumDecimalInferer prec+22): bit-exact incl. carries."""
+    """sum(Decimal(15,2)) -> Decimal(37,2) (Int128); sum(Decimal(18,s)) and sum(Decimal128) ->
+    Decimal256, exact where Int128 would overflow: Decimal128 values near 2^126, ~60 per group,
+    sum past 2^127.  Checked against Python big-int sums and the oracle."""
     rng = np.random.default_rng(12)
     n = 300_000
     k = rng.integers(0, 5000, n, dtype=np.int64)
-    d = rng.integers(-10**18 + 1, 10**18 - 1, n, dtype=np.int64)
-    d128 = rng.integers(-2**62, 2**62, (n, 2), dtype=np.int64)
-    aggs = [(tfa.AGG_SUM, tfa.DECIMAL64), (tfa.AGG_SUM, tfa.DECIMAL128)]
+    d15 = rng.integers(-10**15 + 1, 10**15 - 1, n, dtype=np.int64)
+    d18 = rng.integers(-10**18 + 1, 10**18 - 1, n, dtype=np.int64)
+    hi = rng.integers(2**61, 2**62, n, dtype=np.int64) * np.where(rng.random(n) < 0.8, 1, -1)
+    d128 = np.stack([rng.integers(-2**63, 2**63 - 1, n, dtype=np.int64), hi], axis=1)
+    aggs = [(tfa.AGG_SUM, tfa.prec(tfa.DECIMAL64, 15)), (tfa.AGG_SUM, tfa.prec(tfa.DECIMAL64, 18)),
+            (tfa.AGG_SUM, tfa.DECIMAL128), (tfa.AGG_COUNT_ALL, 0)]
     g = tfa.Aggregator(ctx, tfa.INT64, aggs)
-    g.consume(torch.from_numpy(k).to(dev), [torch.from_numpy(d).to(dev), torch.from_numpy(d128).to(dev)])
-    ref = orc.Agg(orc.INT64, [(0, orc.DECIMAL64), (0, orc.DECIMAL128)])
-    ref.consume(k, [d, d128])
-    assert _gpu_rows(g.result(), np.int64, False) == _ref_rows(ref.result(), np.int64, False)
+    g.consume(torch.from_numpy(k).to(dev), [torch.from_numpy(x).to(dev) for x in (d15, d18, d128)] + [None])
+    r = g.result()
+    assert r["states"][0].shape[1] == 2 and r["states"][1].shape[1] == 4 and r["states"][2].shape[1] == 4
+    keys = r["keys"].cpu().numpy().tolist()
+    got = [dict(zip(keys, _limbs_to_ints(r["states"][i].cpu().numpy()))) for i in range(3)]
+    v128 = [(int(b) << 64) | (int(a) & (2**64 - 1)) for a, b in d128]
+    exp = [_exact_group_sums(k, d15.tolist()), _exact_group_sums(k, d18.tolist()), _exact_group_sums(k, v128)]
+    assert got == exp
+    assert max(abs(v) for v in exp[2].values()) >= 2**127, "the Decimal128 sums must leave Int128"
+    ref = orc.Agg(orc.INT64, [(0, orc.prec(orc.DECIMAL64, 15)), (0, orc.prec(orc.DECIMAL64, 18)), (0, orc.DECIMAL128)])
+    ref.consume(k, [d15, d18, d128])
+    rr = ref.result()
+    for i in range(3):
+        assert dict(zip(rr["keys"].view(np.int64).tolist(), _limbs_to_ints(rr["states"][i]))) == exp[i]
+
+
+def test_groupby_decimal256_args_and_two_phase(tfa, ctx, dev, orc):
+    """sum(Decimal(65,s)) over Decimal256 arguments (|x| < 10^65) with a nullable argument;
+    partial (32-byte states) -> hash repartition -> final (sumOnPartialResult keeps the type)."""
+    rng = np.random.default_rng(13)
+    n = 80_000
+    k = rng.integers(0, 3000, n, dtype=np.int64)
+    vals = [int(x) * 10**48 + int(y) for x, y in zip(rng.integers(-10**16, 10**16, n), rng.integers(0, 10**15, n))]
+    from oracle.oracle import int_to_limbs
+    d256 = np.stack([int_to_limbs(v, 4) for v in vals])
+    vn = (rng.random(n) < 0.1).astype(np.uint8)
+    word = tfa.prec(tfa.DECIMAL256, 65) | tfa.NULLABLE
+    aggs = [(tfa.AGG_SUM, word), (tfa.AGG_COUNT_ALL, 0)]
+    exp = {}
+    for key, v, isnull in zip(k.tolist(), vals, vn.tolist()):
+        s = exp.setdefault(key, [0, 0])
+        if not isnull:
+            s[0] += v
+        s[1] += 1
+    halves = []
+    for lo, hi in ((0, n // 2), (n // 2, n)):
+        p = tfa.Aggregator(ctx, tfa.INT64, aggs, bucket_bits=5)
+        p.consume(torch.from_numpy(k[lo:hi]).to(dev), [torch.from_numpy(d256[lo:hi]).to(dev), None],
+                  arg_nullmaps=[torch.from_numpy(vn[lo:hi]).to(dev), None])
+        halves.append(p.result())
+    fin = tfa.Aggregator(ctx, tfa.INT64, aggs, bucket_bits=4)
+    for r in halves:
+        cols, offs = tfa.hash_partition(ctx, [r["keys"], r["states"][0], r["states"][1], r["state_null"][0]], [0], 2,
+                                        types=[tfa.INT64, tfa.DECIMAL256, tfa.INT64, tfa.UINT8])
+        fin.consume_partial(cols[0], [cols[1], cols[2]], state_nullmaps=[cols[3], None])
+    fr = fin.result()
+    got = dict(zip(fr["keys"].cpu().numpy().tolist(),
+                   [[a, int(c)] for a, c in zip(_limbs_to_ints(fr["states"][0].cpu().numpy()), fr["states"][1].cpu().numpy())]))
+    assert got == exp
+    ref = orc.Agg(orc.INT64, [(0, orc.prec(orc.DECIMAL256, 65)), (2, 0)])
+    ref.consume(k, [d256, None], arg_nulls=[vn, None])
+    rr = ref.result()
+    assert dict(zip(rr["keys"].view(np.int64).tolist(), _limbs_to_ints(rr["states"][0]))) == {a: b[0] for a, b in exp.items()}
 
 
 def test_groupby_multi_block_and_overflowing_buckets(tfa, ctx, dev, orc):
@@ -227,17 +314,19 @@ def test_groupby_without_key(tfa, ctx, dev, orc):
     rng = np.random.default_rng(8)
     n = 1_000_000
     a = rng.integers(0, 2**31, n, dtype=np.int64)
-    aggs = [(tfa.AGG_SUM, tfa.INT64), (tfa.AGG_COUNT_ALL, 0), (tfa.AGG_SUM, tfa.DECIMAL64)]
+    aggs = [(tfa.AGG_SUM, tfa.INT64), (tfa.AGG_COUNT_ALL, 0), (tfa.AGG_SUM, tfa.prec(tfa.DECIMAL64, 12)),
+            (tfa.AGG_SUM, tfa.DECIMAL64)]
     g = tfa.Aggregator(ctx, 0, aggs)
     ad = torch.from_numpy(a).to(dev)
-    g.consume_filtered(ad, tfa.LT, 2**30, None, [ad, None, ad])
+    g.consume_filtered(ad, tfa.LT, 2**30, None, [ad, None, ad, ad])
     r = g.result()
     m = a < 2**30
     assert g.size() == 1
     assert int(r["states"][0].item()) == int(a[m].sum())
     assert int(r["states"][1].item()) == int(m.sum())
-    lo, hi = r["states"][2].cpu().numpy()[0]
-    assert (int(hi) << 64) + (int(lo) & (2**64 - 1)) == int(a[m].sum())
+    assert r["states"][2].shape[1] == 2 and r["states"][3].shape[1] == 4  # Decimal(34,s) / Decimal(40,s)
+    assert _limbs_to_ints(r["states"][2].cpu().numpy()) == [int(a[m].sum())]
+    assert _limbs_to_ints(r["states"][3].cpu().numpy()) == [int(a[m].sum())]
 
 
 def test_groupby_reference_gtest_groups(tfa, ctx, dev):

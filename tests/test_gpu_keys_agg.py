@@ -62,8 +62,9 @@ def gpu_groups(res, key_types):
     sts = []
     for s in res["states"]:
         a = s.cpu().numpy()
-        if a.ndim == 2:
-            sts.append([(int(x[0]) & ((1 << 64) - 1)) | (int(x[1]) << 64) for x in a])
+        if a.ndim == 2:  # Decimal128 / Decimal256 limbs
+            from oracle.oracle import limbs_to_int
+            sts.append([limbs_to_int(x) for x in a])
         else:
             sts.append(a.tolist())
     return [(tuple(c[i] for c in cols), [st[i] for st in sts]) for i in range(g)]
@@ -105,7 +106,7 @@ def test_string_key_sum_count(tfa, ctx, dev, orc, collator, nullable):
     d = rng.integers(-10**9, 10**9, n, dtype=np.int64)  # Decimal(15,2) payload
     iv = rng.integers(-2**40, 2**40, n, dtype=np.int64)
     ivn = (rng.random(n) < 0.1).astype(np.uint8)
-    aggs = [(tfa.AGG_SUM, tfa.DECIMAL64), (tfa.AGG_COUNT_ALL, 0), (tfa.AGG_SUM, tfa.INT64 | tfa.NULLABLE)]
+    aggs = [(tfa.AGG_SUM, tfa.prec(tfa.DECIMAL64, 15)), (tfa.AGG_COUNT_ALL, 0), (tfa.AGG_SUM, tfa.INT64 | tfa.NULLABLE)]
     agg = tfa.KeysAggregator(ctx, [tfa.STRING], aggs, collators=[collator])
     half = n // 2
     for lo, hi in ((0, half), (half, n)):  # two blocks: the second seeds the first's groups
@@ -114,7 +115,7 @@ def test_string_key_sum_count(tfa, ctx, dev, orc, collator, nullable):
                     key_nullmaps=[to_dev(knull[lo:hi], dev)] if nullable else None,
                     arg_nullmaps=[None, None, to_dev(ivn[lo:hi], dev)])
     got = gpu_groups(agg.result(), [20])
-    ref = orc.AggKeys([orc.STRING], [(0, orc.DECIMAL64), (2, 0), (0, orc.INT64)], collators=[collator])
+    ref = orc.AggKeys([orc.STRING], [(0, orc.prec(orc.DECIMAL64, 15)), (2, 0), (0, orc.INT64)], collators=[collator])
     ref.consume([(chars, offs)], [d, None, iv], key_nulls=[knull] if nullable else None, arg_nulls=[None, None, ivn])
     check_same(got, ref.result())
 
@@ -127,11 +128,11 @@ def test_string_key_c5_shape_spills(tfa, ctx, dev, orc):
     strs = [b"k%08d" % i for i in ids]
     chars, offs = str_col(strs)
     d = rng.integers(0, 10**9, n, dtype=np.int64)
-    aggs = [(tfa.AGG_SUM, tfa.DECIMAL64), (tfa.AGG_COUNT_ALL, 0)]
+    aggs = [(tfa.AGG_SUM, tfa.prec(tfa.DECIMAL64, 15)), (tfa.AGG_COUNT_ALL, 0)]
     agg = tfa.KeysAggregator(ctx, [tfa.STRING], aggs, bucket_bits=4, expected_groups=4096)
     agg.consume([to_dev((chars, offs), dev)], [to_dev(d, dev), None])
     got = gpu_groups(agg.result(), [20])
-    ref = orc.AggKeys([orc.STRING], [(0, orc.DECIMAL64), (2, 0)])
+    ref = orc.AggKeys([orc.STRING], [(0, orc.prec(orc.DECIMAL64, 15)), (2, 0)])
     ref.consume([(chars, offs)], [d, None])
     check_same(got, ref.result())
 
@@ -190,10 +191,10 @@ def test_two_phase_string_packed_and_unpacked(tfa, ctx, dev, orc):
     rng = np.random.default_rng(12)
     vocab = [b"k%08d" % i for i in range(20_000)]
     n = 100_000
-    aggs = [(tfa.AGG_SUM, tfa.DECIMAL64), (tfa.AGG_COUNT_ALL, 0)]
+    aggs = [(tfa.AGG_SUM, tfa.prec(tfa.DECIMAL64, 15)), (tfa.AGG_COUNT_ALL, 0)]
     fin_p = tfa.KeysAggregator(ctx, [tfa.STRING], aggs)
     fin_u = tfa.KeysAggregator(ctx, [tfa.STRING], aggs)
-    ref = orc.AggKeys([orc.STRING], [(0, orc.DECIMAL64), (2, 0)])
+    ref = orc.AggKeys([orc.STRING], [(0, orc.prec(orc.DECIMAL64, 15)), (2, 0)])
     for part in range(3):
         strs = rand_strings(rng, n, vocab)
         chars, offs = str_col(strs)
@@ -247,3 +248,41 @@ def test_groupby_keys_reference_cases(tfa, ctx, dev):
         assert sorted(got, key=repr) == sorted(exp, key=repr), case["group_by"]
         ran += 1
     assert ran == 4
+
+
+def test_reference_aggregate_values(tfa, ctx, dev, orc):
+    """The aggregate VALUES the reference's tests pin (tests/golden/reference_cases.json
+    "aggregates"): AggregationCount over the clerk table, gtest_aggregation_executor.cpp:562-585
+    (count(x) skips NULL x), and sum(s2) = 6 (:755-757), on the device."""
+    import json
+    import os
+    case = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "reference_cases.json")))["aggregates"]
+    clerk = case["clerk"]
+    age = np.array([0 if a is None else a for a in clerk["age"]], dtype=np.int32)
+    age_null = np.array([a is None for a in clerk["age"]], dtype=np.uint8)
+    pr = np.array(clerk["pr"], dtype=np.uint64)
+    country = str_col([s.encode() for s in clerk["country"]])
+    gender = str_col([s.encode() for s in clerk["gender"]])
+    for c in case["counts"]:
+        kind, arg, atype, nulls = {"count(age)": (tfa.AGG_COUNT, age, tfa.INT32, age_null),
+                                   "count(gender)": (tfa.AGG_COUNT_ALL, None, 0, None),
+                                   "count(1)": (tfa.AGG_COUNT_ALL, None, 0, None),
+                                   "count(pr)": (tfa.AGG_COUNT, pr, tfa.UINT64, None)}[c["func"]]
+        word = atype | (tfa.NULLABLE if nulls is not None else 0)
+        if not c["group_by"]:
+            g = tfa.Aggregator(ctx, 0, [(kind, word)])
+            g.consume(None, [to_dev(arg, dev) if arg is not None else None], n=len(age))
+            got = [int(x) for x in g.result()["states"][0].cpu().numpy()]
+        else:
+            cols = {"country": country, "gender": gender}
+            if len(c["group_by"]) > 1 and not hasattr(tfa, "SERIALIZED_KEYS"):
+                continue  # two String keys: the serialized method
+            g = tfa.KeysAggregator(ctx, [tfa.STRING] * len(c["group_by"]), [(kind, word)])
+            g.consume([to_dev(cols[k], dev) for k in c["group_by"]], [to_dev(arg, dev) if arg is not None else None],
+                      arg_nullmaps=[to_dev(nulls, dev)] if nulls is not None else None)
+            got = sorted(int(x) for x in g.result()["states"][0].cpu().numpy())
+        assert got == sorted(c["expected"]), c
+    s2 = np.array(case["test_table"]["s2"], dtype=np.int64)
+    g = tfa.Aggregator(ctx, 0, [(tfa.AGG_SUM, tfa.INT64)])
+    g.consume(None, [to_dev(s2, dev)], n=3)
+    assert int(g.result()["states"][0].item()) == case["sums"][0]["expected"][0]

@@ -97,7 +97,7 @@ def test_repartitioned_join_matches_oracle(ranks, orc):
 
 @pytest.mark.gpu
 def test_two_phase_string_decimal_groupby_matches_oracle(ranks, orc):
-    ref = orc.AggKeys([orc.STRING], [(0, orc.DECIMAL64), (2, 0)])
+    ref = orc.AggKeys([orc.STRING], [(0, orc.prec(orc.DECIMAL64, 15)), (2, 0)])
     for r in range(WORLD):
         chars, offs, nulls, v = W.agg_data(r)
         ref.consume([(chars, offs)], [v, None], key_nulls=[nulls])

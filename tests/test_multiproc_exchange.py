@@ -211,7 +211,7 @@ def _two_phase_string_worker(rank, world, port, q):
     try:
         dist.init_process_group("gloo", rank=rank, world_size=world)
         strs, d = _str_data(rank)
-        part = orc.AggKeys([orc.STRING], [(0, orc.DECIMAL64), (2, 0)])
+        part = orc.AggKeys([orc.STRING], [(0, orc.prec(orc.DECIMAL64, 15)), (2, 0)])
         part.consume([_str_col(strs)], [d, None])
         groups = part.result()
         keys = [k[0] for k, _ in groups]
@@ -263,7 +263,7 @@ def test_two_phase_string_aggregation_gloo():
         p.join(timeout=60)
     assert all(p.exitcode == 0 for p in procs)
     assert isinstance(got, dict), got
-    ref = orc.AggKeys([orc.STRING], [(0, orc.DECIMAL64), (2, 0)])
+    ref = orc.AggKeys([orc.STRING], [(0, orc.prec(orc.DECIMAL64, 15)), (2, 0)])
     for r in range(WORLD):
         strs, d = _str_data(r)
         ref.consume([_str_col(strs)], [d, None])

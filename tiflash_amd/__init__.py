@@ -27,9 +27,16 @@ TFG_ERR_CAPACITY = -8
 TFG_ERR_NO_DEVICE = -9
 
 INT8, INT16, INT32, INT64, UINT8, UINT16, UINT32, UINT64, FLOAT32, FLOAT64 = range(1, 11)
-DECIMAL32, DECIMAL64, DECIMAL128 = 11, 12, 13
+DECIMAL32, DECIMAL64, DECIMAL128, DECIMAL256 = 11, 12, 13, 14
 STRING, KEYS128 = 20, 21  # String GROUP BY keys (chars, offsets); packed 16-byte key (tfg_agg_create_keys)
 NULLABLE = 0x100  # or-ed into an aggregate argument type: the argument may carry a null map
+
+
+def prec(t: int, p: int) -> int:
+    """Aggregate argument type word of a Decimal column of precision p (TFG_ARG_PREC): sum over
+    Decimal(p, s) returns Decimal(min(p + 22, 65), s) — Decimal128 up to 38 digits, else
+    Decimal256 (4 int64 limbs per value).  Without it the type's maximum precision is assumed."""
+    return t | (int(p) << 16)
 
 EQ, NE, LT, LE, GT, GE = range(6)
 PLUS, MINUS, MULTIPLY = range(3)
@@ -39,7 +46,7 @@ JOIN_INNER, JOIN_LEFT, JOIN_SEMI, JOIN_ANTI = range(4)
 COLLATOR_NONE, COLLATOR_BINARY, COLLATOR_BIN_PADDING = range(3)
 
 WIDTH = {INT8: 1, INT16: 2, INT32: 4, INT64: 8, UINT8: 1, UINT16: 2, UINT32: 4, UINT64: 8,
-         FLOAT32: 4, FLOAT64: 8, DECIMAL32: 4, DECIMAL64: 8, DECIMAL128: 16, KEYS128: 16}
+         FLOAT32: 4, FLOAT64: 8, DECIMAL32: 4, DECIMAL64: 8, DECIMAL128: 16, DECIMAL256: 32, KEYS128: 16}
 _CTYPE = {INT8: ctypes.c_int8, INT16: ctypes.c_int16, INT32: ctypes.c_int32, INT64: ctypes.c_int64,
           UINT8: ctypes.c_uint8, UINT16: ctypes.c_uint16, UINT32: ctypes.c_uint32, UINT64: ctypes.c_uint64,
           FLOAT32: ctypes.c_float, FLOAT64: ctypes.c_double, DECIMAL32: ctypes.c_int32,
@@ -118,16 +125,16 @@ def torch_type(t) -> int:
 def _empty(n, width, device):
     import torch
     dt = {1: torch.uint8, 2: torch.int16, 4: torch.int32, 8: torch.int64}.get(width)
-    if dt is None:  # 16-byte values (Decimal128) as (n, 2) int64
-        return torch.empty((max(n, 1), 2), dtype=torch.int64, device=device)[:n]
+    if dt is None:  # 16- / 32-byte values (Decimal128 / Decimal256) as (n, 2) / (n, 4) int64
+        return torch.empty((max(n, 1), width // 8), dtype=torch.int64, device=device)[:n]
     return torch.empty(max(n, 1), dtype=dt, device=device)[:n]
 
 
 def _alloc(n, width, device, dtype):
-    """n >= 1 elements of `width` bytes viewed as `dtype` (2-D (n, 2) int64 for 16-byte values)."""
+    """n >= 1 elements of `width` bytes viewed as `dtype` (2-D (n, 2) / (n, 4) int64 for 16- / 32-byte values)."""
     import torch
-    if width == 16:
-        return torch.empty((n, 2), dtype=torch.int64, device=device)
+    if width in (16, 32):
+        return torch.empty((n, width // 8), dtype=torch.int64, device=device)
     return torch.empty(n, dtype=dtype, device=device)
 
 

@@ -32,7 +32,9 @@ constexpr int BT_BIG = 1024; // for tables too large for two workgroups per CU (
 constexpr int LDS_TABLE_BYTES = 100 * 1024;  // preferred table size (two workgroups per CU)
 constexpr int LDS_TABLE_MAX = 150 * 1024;    // largest table (one 16-wave workgroup per CU)
 
-enum AccKind { ACC_NONE = 0, ACC_I64 = 1, ACC_F64 = 2, ACC_I128 = 3 };
+enum AccKind { ACC_NONE = 0, ACC_I64 = 1, ACC_F64 = 2, ACC_I128 = 3, ACC_I256 = 4 };
+// 64-bit words of an accumulator of kind k
+__host__ __device__ constexpr int acc_words(int k) { return k == ACC_I256 ? 4 : k == ACC_I128 ? 2 : k == ACC_NONE ? 0 : 1; }
 enum RowMode { MODE_RAW = 0, MODE_PARTIAL = 1, MODE_STATE = 2 };
 
 struct AggSpec {
@@ -119,6 +121,36 @@ __device__ __forceinline__ void lds_add_i128(uint64_t *cell, uint64_t lo, uint64
     atomicAdd((unsigned long long *)&cell[1], (unsigned long long)(hi + carry));
 }
 
+// Decimal256 sum state (AggregateFunctionSumData<Decimal256>, boost checked_int256_t): four
+// 64-bit limbs added limb by limb with LDS atomics.  Every adder carries its own carry-outs into
+// the next limb (a carry from x_k + c_k itself, or from the atomic add), so the cell ends at the
+// exact two's complement sum mod 2^256 whatever the interleaving of concurrent adders.
+__device__ __forceinline__ void lds_add_i256(uint64_t *cell, uint64_t x0, uint64_t x1, uint64_t x2, uint64_t x3) {
+    uint64_t old = atomicAdd((unsigned long long *)&cell[0], (unsigned long long)x0);
+    uint64_t c = (old + x0) < old ? 1ull : 0ull;
+    uint64_t t = x1 + c;
+    uint64_t ca = t < c ? 1ull : 0ull;
+    old = atomicAdd((unsigned long long *)&cell[1], (unsigned long long)t);
+    c = ((old + t) < old ? 1ull : 0ull) + ca;
+    t = x2 + c;
+    ca = t < c ? 1ull : 0ull;
+    old = atomicAdd((unsigned long long *)&cell[2], (unsigned long long)t);
+    c = ((old + t) < old ? 1ull : 0ull) + ca;
+    atomicAdd((unsigned long long *)&cell[3], (unsigned long long)(x3 + c));
+}
+
+// register form: a += x (mod 2^256)
+__host__ __device__ __forceinline__ void add_i256(uint64_t *a, const uint64_t *x) {
+    uint64_t c = 0;
+    for (int k = 0; k < 4; ++k) {
+        const uint64_t t = x[k] + c;
+        const uint64_t c1 = t < c ? 1ull : 0ull;
+        const uint64_t s = a[k] + t;
+        c = (s < t ? 1ull : 0ull) + c1;
+        a[k] = s;
+    }
+}
+
 // Tag of a wide (16-byte packed) key: a 64-bit mix of both halves with bit 1 set (never 0) and
 // bit 0 clear.  The bucket radix and the in-table slot group come from tag * 2^64/phi exactly
 // as they come from the key itself for 8-byte keys; bit 0 of a stored tag marks "key published".
@@ -130,8 +162,13 @@ __host__ __device__ __forceinline__ uint64_t wide_tag(uint64_t lo, uint64_t hi) 
     return (x | 2ull) & ~1ull;
 }
 
-// one staged row held in registers; NA = number of aggregates (compile time, keeps VGPRs low)
-template <int NA> struct RowValT {
+// one staged row held in registers; NA = number of aggregates (compile time, keeps VGPRs low);
+// W: the signature has a Decimal256 sum, whose values carry two more limbs (x2, x3)
+template <int NA, bool W> struct RowHi {
+    uint64_t x2[NA], x3[NA];
+};
+template <int NA> struct RowHi<NA, false> {};
+template <int NA, bool W = false> struct RowValT : RowHi<NA, W> {
     uint64_t key;
     uint8_t knull;
     uint8_t vnull[NA];
@@ -385,19 +422,20 @@ struct Table {
     }
 
     __device__ __forceinline__ uint64_t *acc_cell(int i, int cell) const {
-        const int w = S.acc[i] == ACC_I128 ? 2 : 1;
-        return reinterpret_cast<uint64_t *>(base + S.acc_off[i]) + (int64_t)cell * w;
+        return reinterpret_cast<uint64_t *>(base + S.acc_off[i]) + (int64_t)cell * acc_words(S.acc[i]);
     }
     __device__ __forceinline__ uint64_t *cnt_cell(int i, int cell) const {
         return reinterpret_cast<uint64_t *>(base + S.cnt_off[i]) + cell;
     }
 
     // fold a register-resident row (mode) into cell
-    template <int NA> __device__ __forceinline__ void add_row(int cell, const RowValT<NA> &v, int mode) {
+    template <int NA, bool W> __device__ __forceinline__ void add_row(int cell, const RowValT<NA, W> &v, int mode) {
 #pragma unroll
         for (int i = 0; i < NA; ++i) {
             const int kind = S.kind[i];
             if (mode == MODE_STATE) {
+                if constexpr (W)
+                    if (S.acc[i] == ACC_I256) lds_add_i256(acc_cell(i, cell), v.lo[i], v.hi[i], v.x2[i], v.x3[i]);
                 if (S.acc[i] == ACC_I128) lds_add_i128(acc_cell(i, cell), v.lo[i], v.hi[i]);
                 else if (S.acc[i] == ACC_F64) atomicAdd((double *)acc_cell(i, cell), __longlong_as_double((long long)v.lo[i]));
                 else if (S.acc[i] == ACC_I64) atomicAdd((unsigned long long *)acc_cell(i, cell), (unsigned long long)v.lo[i]);
@@ -419,6 +457,15 @@ struct Table {
                                      ? (double)__uint_as_float((unsigned)lo)
                                      : __longlong_as_double((long long)lo);
                 atomicAdd((double *)acc_cell(i, cell), f);
+            } else if (S.acc[i] == ACC_I256) {
+                if constexpr (W) {
+                    uint64_t x2 = v.x2[i], x3 = v.x3[i];
+                    if (mode == MODE_RAW && S.src_type[i] != TFG_DECIMAL256) { // widen to 256 bits
+                        widen_raw(S.src_type[i], lo, hi);
+                        x2 = x3 = (int64_t)hi < 0 ? ~0ull : 0ull;
+                    }
+                    lds_add_i256(acc_cell(i, cell), lo, hi, x2, x3);
+                }
             } else {
                 if (mode == MODE_RAW) widen_raw(S.src_type[i], lo, hi);
                 if (S.acc[i] == ACC_I128) lds_add_i128(acc_cell(i, cell), lo, hi);
@@ -431,7 +478,10 @@ struct Table {
     // fold group g of `grp` (state) into cell
     __device__ __forceinline__ void add_group(int cell, const GroupsIO &grp, int64_t g) {
         for (int i = 0; i < S.n_aggs; ++i) {
-            if (S.acc[i] == ACC_I128) {
+            if (S.acc[i] == ACC_I256) {
+                const uint64_t *v = (const uint64_t *)grp.acc[i] + 4 * g;
+                lds_add_i256(acc_cell(i, cell), v[0], v[1], v[2], v[3]);
+            } else if (S.acc[i] == ACC_I128) {
                 const uint64_t *v = (const uint64_t *)grp.acc[i] + 2 * g;
                 lds_add_i128(acc_cell(i, cell), v[0], v[1]);
             } else if (S.acc[i] == ACC_F64) {
@@ -466,10 +516,10 @@ struct Table {
             }
             out.key_null[pos] = isnull;
             for (int i = 0; i < S.n_aggs; ++i) {
-                if (S.acc[i] == ACC_I128) {
+                if (S.acc[i] == ACC_I128 || S.acc[i] == ACC_I256) {
+                    const int nw = acc_words(S.acc[i]);
                     const uint64_t *a = acc_cell(i, c);
-                    ((uint64_t *)out.acc[i])[2 * pos] = a[0];
-                    ((uint64_t *)out.acc[i])[2 * pos + 1] = a[1];
+                    for (int k = 0; k < nw; ++k) ((uint64_t *)out.acc[i])[nw * pos + k] = a[k];
                 } else if (S.acc[i] != ACC_NONE) {
                     ((uint64_t *)out.acc[i])[pos] = *acc_cell(i, c);
                 }
@@ -481,8 +531,9 @@ struct Table {
 
 // width in bytes of value column i for a row mode
 __device__ __forceinline__ int val_width(const AggSpec &S, int mode, int i) {
-    if (mode != MODE_RAW) return S.acc[i] == ACC_I128 ? 16 : 8;
+    if (mode != MODE_RAW) return S.acc[i] == ACC_I256 ? 32 : S.acc[i] == ACC_I128 ? 16 : 8;
     switch (S.src_type[i]) {
+    case TFG_DECIMAL256: return 32;
     case TFG_INT8: case TFG_UINT8: return 1;
     case TFG_INT16: case TFG_UINT16: return 2;
     case TFG_INT32: case TFG_UINT32: case TFG_FLOAT32: case TFG_DECIMAL32: return 4;
@@ -491,8 +542,8 @@ __device__ __forceinline__ int val_width(const AggSpec &S, int mode, int i) {
     }
 }
 
-template <int NA>
-__device__ __forceinline__ void load_row(const AggSpec &S, const RowsIO &rows, int mode, int64_t r, RowValT<NA> &v) {
+template <int NA, bool W>
+__device__ __forceinline__ void load_row(const AggSpec &S, const RowsIO &rows, int mode, int64_t r, RowValT<NA, W> &v) {
     if (rows.key_width != 16) v.key = load_bits(rows.key, rows.key_width, r); // wide keys: WideOps
     v.knull = rows.key_null ? rows.key_null[r] : 0;
 #pragma unroll
@@ -500,9 +551,18 @@ __device__ __forceinline__ void load_row(const AggSpec &S, const RowsIO &rows, i
         v.lo[i] = v.hi[i] = v.cnt[i] = 0;
         v.vnull[i] = rows.val_null[i] ? rows.val_null[i][r] : 0;
         if (rows.val_cnt[i]) v.cnt[i] = rows.val_cnt[i][r];
+        if constexpr (W) v.x2[i] = v.x3[i] = 0;
         if (!rows.val[i]) continue;
         const int w = val_width(S, mode, i);
-        if (w == 16) {
+        if (w == 32) {
+            if constexpr (W) {
+                const uint4 q = ((const uint4 *)rows.val[i])[2 * r], q2 = ((const uint4 *)rows.val[i])[2 * r + 1];
+                v.lo[i] = ((uint64_t)q.y << 32) | q.x;
+                v.hi[i] = ((uint64_t)q.w << 32) | q.z;
+                v.x2[i] = ((uint64_t)q2.y << 32) | q2.x;
+                v.x3[i] = ((uint64_t)q2.w << 32) | q2.z;
+            }
+        } else if (w == 16) {
             const uint4 q = ((const uint4 *)rows.val[i])[r];
             v.lo[i] = ((uint64_t)q.y << 32) | q.x;
             v.hi[i] = ((uint64_t)q.w << 32) | q.z;
@@ -513,8 +573,8 @@ __device__ __forceinline__ void load_row(const AggSpec &S, const RowsIO &rows, i
 }
 
 // in-place compaction of the bucket's pending rows: write a register row to slot w
-template <int NA>
-__device__ __forceinline__ void store_row(const AggSpec &S, const RowsIO &rows, int mode, int64_t w, const RowValT<NA> &v) {
+template <int NA, bool W>
+__device__ __forceinline__ void store_row(const AggSpec &S, const RowsIO &rows, int mode, int64_t w, const RowValT<NA, W> &v) {
     switch (rows.key_width) {
     case 1: ((uint8_t *)rows.key)[w] = (uint8_t)v.key; break;
     case 2: ((uint16_t *)rows.key)[w] = (uint16_t)v.key; break;
@@ -533,6 +593,15 @@ __device__ __forceinline__ void store_row(const AggSpec &S, const RowsIO &rows, 
         case 2: ((uint16_t *)rows.val[i])[w] = (uint16_t)v.lo[i]; break;
         case 4: ((uint32_t *)rows.val[i])[w] = (uint32_t)v.lo[i]; break;
         case 8: ((uint64_t *)rows.val[i])[w] = v.lo[i]; break;
+        case 32:
+            if constexpr (W) {
+                uint64_t *o = (uint64_t *)rows.val[i] + 4 * w;
+                o[0] = v.lo[i];
+                o[1] = v.hi[i];
+                o[2] = v.x2[i];
+                o[3] = v.x3[i];
+            }
+            break;
         default: {
             uint4 q;
             q.x = (unsigned)v.lo[i];
@@ -555,17 +624,17 @@ constexpr int RPT = 4;
 // signatures (8-byte key, no NULLs, RAW rows) — op codes: 0 absent, 1 count, 2 sum into Int64,
 // 3 sum Float64, 4 sum Decimal64 into Int128.  Without it the per-row switches cost ~350
 // wave-instructions per 64 rows (measured with SQ_INSTS_VALU / SQ_INSTS_SALU).
-template <int NA> struct GenericOps {
-    using Row = RowValT<NA>;
+template <int NA, bool W = false> struct GenericOps {
+    using Row = RowValT<NA, W>;
     static constexpr bool WIDE = false;
     __device__ __forceinline__ uint64_t hi(const Row &) const { return 0; }
     const AggSpec &S;
     int mode;
-    __device__ __forceinline__ void load(const RowsIO &rows, int64_t r, Row &v) const { load_row<NA>(S, rows, mode, r, v); }
+    __device__ __forceinline__ void load(const RowsIO &rows, int64_t r, Row &v) const { load_row<NA, W>(S, rows, mode, r, v); }
     __device__ __forceinline__ uint64_t key(const Row &v) const { return v.key; }
     __device__ __forceinline__ bool knull(const Row &v) const { return v.knull != 0; }
-    __device__ __forceinline__ void add(Table &T, int cell, const Row &v) const { T.add_row<NA>(cell, v, mode); }
-    __device__ __forceinline__ void store(const RowsIO &sp, int64_t w, const Row &v) const { store_row<NA>(S, sp, mode, w, v); }
+    __device__ __forceinline__ void add(Table &T, int cell, const Row &v) const { T.add_row<NA, W>(cell, v, mode); }
+    __device__ __forceinline__ void store(const RowsIO &sp, int64_t w, const Row &v) const { store_row<NA, W>(S, sp, mode, w, v); }
 };
 
 template <int A0, int A1, int A2> struct FastOps {
@@ -619,15 +688,15 @@ template <int A0, int A1, int A2> struct FastOps {
 
 // Wide keys (16-byte packed keys128 / String keys, staged as one uint4 per row): generic
 // value handling, the key's two words travel in Row::key and Row::hi.
-template <int NA> struct WideOps {
-    struct Row : RowValT<NA> {
+template <int NA, bool W = false> struct WideOps {
+    struct Row : RowValT<NA, W> {
         uint64_t khi;
     };
     static constexpr bool WIDE = true;
     const AggSpec &S;
     int mode;
     __device__ __forceinline__ void load(const RowsIO &rows, int64_t r, Row &v) const {
-        load_row<NA>(S, rows, mode, r, v);
+        load_row<NA, W>(S, rows, mode, r, v);
         const uint4 q = reinterpret_cast<const uint4 *>(rows.key)[r];
         v.key = ((uint64_t)q.y << 32) | q.x;
         v.khi = ((uint64_t)q.w << 32) | q.z;
@@ -635,9 +704,9 @@ template <int NA> struct WideOps {
     __device__ __forceinline__ uint64_t key(const Row &v) const { return v.key; }
     __device__ __forceinline__ uint64_t hi(const Row &v) const { return v.khi; }
     __device__ __forceinline__ bool knull(const Row &) const { return false; }
-    __device__ __forceinline__ void add(Table &T, int cell, const Row &v) const { T.add_row<NA>(cell, v, mode); }
+    __device__ __forceinline__ void add(Table &T, int cell, const Row &v) const { T.add_row<NA, W>(cell, v, mode); }
     __device__ __forceinline__ void store(const RowsIO &sp, int64_t w, const Row &v) const {
-        store_row<NA>(S, sp, mode, w, v);
+        store_row<NA, W>(S, sp, mode, w, v);
         uint4 q;
         q.x = (unsigned)v.key;
         q.y = (unsigned)(v.key >> 32);
@@ -961,7 +1030,10 @@ __global__ void agg_compact_kernel(AggSpec S, GroupsIO tmp, const uint64_t *stag
         else dst.key[d] = tmp.key[s];
         dst.key_null[d] = tmp.key_null[s];
         for (int i = 0; i < S.n_aggs; ++i) {
-            if (S.acc[i] == ACC_I128) ((uint4 *)dst.acc[i])[d] = ((const uint4 *)tmp.acc[i])[s];
+            if (S.acc[i] == ACC_I256) {
+                ((uint4 *)dst.acc[i])[2 * d] = ((const uint4 *)tmp.acc[i])[2 * s];
+                ((uint4 *)dst.acc[i])[2 * d + 1] = ((const uint4 *)tmp.acc[i])[2 * s + 1];
+            } else if (S.acc[i] == ACC_I128) ((uint4 *)dst.acc[i])[d] = ((const uint4 *)tmp.acc[i])[s];
             else if (S.acc[i] != ACC_NONE) ((uint64_t *)dst.acc[i])[d] = ((const uint64_t *)tmp.acc[i])[s];
             if (S.has_cnt[i]) dst.cnt[i][d] = tmp.cnt[i][s];
         }
@@ -971,14 +1043,23 @@ __global__ void agg_compact_kernel(AggSpec S, GroupsIO tmp, const uint64_t *stag
 // ---------------------------------------------------------------- without key (single group)
 constexpr int NK_T = 256;
 struct NoKeyPartial {
-    uint64_t lo[AGG_MAX], hi[AGG_MAX], cnt[AGG_MAX];
+    uint64_t lo[AGG_MAX], hi[AGG_MAX], x2[AGG_MAX], x3[AGG_MAX], cnt[AGG_MAX];
     double f[AGG_MAX];
 };
+// p (4 limbs at lo/hi/x2/x3[i]) += q
+__device__ __forceinline__ void nk_add(NoKeyPartial &p, int i, const uint64_t *q) {
+    uint64_t a[4] = {p.lo[i], p.hi[i], p.x2[i], p.x3[i]};
+    add_i256(a, q);
+    p.lo[i] = a[0];
+    p.hi[i] = a[1];
+    p.x2[i] = a[2];
+    p.x3[i] = a[3];
+}
 
 __global__ void __launch_bounds__(NK_T) agg_nokey_kernel(AggSpec S, RowsIO rows, int mode, RowPred pred, int64_t n,
                                                          NoKeyPartial *partials) {
     NoKeyPartial p;
-    for (int i = 0; i < AGG_MAX; ++i) p.lo[i] = p.hi[i] = p.cnt[i] = 0, p.f[i] = 0;
+    for (int i = 0; i < AGG_MAX; ++i) p.lo[i] = p.hi[i] = p.x2[i] = p.x3[i] = p.cnt[i] = 0, p.f[i] = 0;
     for (int64_t r = (int64_t)blockIdx.x * NK_T + threadIdx.x; r < n; r += (int64_t)gridDim.x * NK_T) {
         if (!pred(r)) continue;
         for (int i = 0; i < S.n_aggs; ++i) {
@@ -990,9 +1071,18 @@ __global__ void __launch_bounds__(NK_T) agg_nokey_kernel(AggSpec S, RowsIO rows,
             }
             uint64_t lo = 0, hi = 0;
             double f = 0;
+            if (S.src_type[i] == TFG_DECIMAL256) {
+                nk_add(p, i, (const uint64_t *)rows.val[i] + 4 * r);
+                p.cnt[i]++;
+                continue;
+            }
             load_sum_value(S.src_type[i], rows.val[i], r, lo, hi, f);
             if (S.acc[i] == ACC_F64) p.f[i] += f;
-            else {
+            else if (S.acc[i] == ACC_I256) {
+                const uint64_t ext = (int64_t)hi < 0 ? ~0ull : 0ull;
+                const uint64_t q[4] = {lo, hi, ext, ext};
+                nk_add(p, i, q);
+            } else {
                 const uint64_t o = p.lo[i];
                 p.lo[i] += lo;
                 p.hi[i] += hi + (p.lo[i] < o ? 1 : 0);
@@ -1008,9 +1098,14 @@ __global__ void __launch_bounds__(NK_T) agg_nokey_kernel(AggSpec S, RowsIO rows,
         NoKeyPartial s = red[0];
         for (int t = 1; t < NK_T; ++t)
             for (int i = 0; i < S.n_aggs; ++i) {
-                const uint64_t o = s.lo[i];
-                s.lo[i] += red[t].lo[i];
-                s.hi[i] += red[t].hi[i] + (s.lo[i] < o ? 1 : 0);
+                if (S.acc[i] == ACC_I256) {
+                    const uint64_t q[4] = {red[t].lo[i], red[t].hi[i], red[t].x2[i], red[t].x3[i]};
+                    nk_add(s, i, q);
+                } else {
+                    const uint64_t o = s.lo[i];
+                    s.lo[i] += red[t].lo[i];
+                    s.hi[i] += red[t].hi[i] + (s.lo[i] < o ? 1 : 0);
+                }
                 s.f[i] += red[t].f[i];
                 s.cnt[i] += red[t].cnt[i];
             }
@@ -1024,7 +1119,10 @@ __global__ void agg_nokey_fold_kernel(AggSpec S, const NoKeyPartial *partials, i
         for (int i = 0; i < S.n_aggs; ++i) {
             const NoKeyPartial &p = partials[b];
             if (S.acc[i] == ACC_F64) ((double *)st.acc[i])[0] += p.f[i];
-            else if (S.acc[i] == ACC_I128) {
+            else if (S.acc[i] == ACC_I256) {
+                const uint64_t q[4] = {p.lo[i], p.hi[i], p.x2[i], p.x3[i]};
+                add_i256((uint64_t *)st.acc[i], q);
+            } else if (S.acc[i] == ACC_I128) {
                 uint64_t *a = (uint64_t *)st.acc[i];
                 const uint64_t o = a[0];
                 a[0] += p.lo[i];
@@ -1058,7 +1156,10 @@ __global__ void agg_result_kernel(AggSpec S, GroupsIO st, uint64_t n, int key_wi
         for (int i = 0; i < S.n_aggs; ++i) {
             if (res.state[i]) {
                 if (S.kind[i] != TFG_AGG_SUM) ((uint64_t *)res.state[i])[g] = st.cnt[i][g];
-                else if (S.acc[i] == ACC_I128) ((uint4 *)res.state[i])[g] = ((const uint4 *)st.acc[i])[g];
+                else if (S.acc[i] == ACC_I256) {
+                    ((uint4 *)res.state[i])[2 * g] = ((const uint4 *)st.acc[i])[2 * g];
+                    ((uint4 *)res.state[i])[2 * g + 1] = ((const uint4 *)st.acc[i])[2 * g + 1];
+                } else if (S.acc[i] == ACC_I128) ((uint4 *)res.state[i])[g] = ((const uint4 *)st.acc[i])[g];
                 else ((uint64_t *)res.state[i])[g] = ((const uint64_t *)st.acc[i])[g];
             }
             if (res.state_null[i])
@@ -1071,6 +1172,7 @@ __global__ void agg_state_add_kernel(AggSpec S, GroupsIO dst, GroupsIO src) { //
     if (threadIdx.x || blockIdx.x) return;
     for (int i = 0; i < S.n_aggs; ++i) {
         if (S.acc[i] == ACC_F64) ((double *)dst.acc[i])[0] += ((const double *)src.acc[i])[0];
+        else if (S.acc[i] == ACC_I256) add_i256((uint64_t *)dst.acc[i], (const uint64_t *)src.acc[i]);
         else if (S.acc[i] == ACC_I128) {
             uint64_t *a = (uint64_t *)dst.acc[i];
             const uint64_t *b = (const uint64_t *)src.acc[i];
@@ -1292,8 +1394,7 @@ struct tfg_agg {
     size_t group_bytes() const {
         size_t b = (S.key_width == 16 ? 16 : 8) + 1;
         for (int i = 0; i < S.n_aggs; ++i) {
-            if (S.acc[i] == ACC_I128) b += 16;
-            else if (S.acc[i] != ACC_NONE) b += 8;
+            b += 8 * acc_words(S.acc[i]);
             if (S.has_cnt[i]) b += 8;
         }
         return b;
@@ -1304,7 +1405,8 @@ struct tfg_agg {
         size_t ok = cv.take<uint64_t>(S.key_width == 16 ? 2 * n : n), on = cv.take<uint8_t>(n);
         size_t oa[AGG_MAX] = {}, oc[AGG_MAX] = {};
         for (int i = 0; i < S.n_aggs; ++i) {
-            if (S.acc[i] == ACC_I128) oa[i] = cv.take<uint4>(n);
+            if (S.acc[i] == ACC_I256) oa[i] = cv.take<uint4>(2 * n);
+            else if (S.acc[i] == ACC_I128) oa[i] = cv.take<uint4>(n);
             else if (S.acc[i] != ACC_NONE) oa[i] = cv.take<uint64_t>(n);
             if (S.has_cnt[i]) oc[i] = cv.take<uint64_t>(n);
         }
@@ -1503,7 +1605,7 @@ int consume_keyed(tfg_agg *a, int mode, const RowPred &pred, const void *keys, i
         if (val_cnts && val_cnts[i]) o_vcnt[i] = cv.take<uint64_t>(n);
         if (!vals[i]) continue;
         if (mode == MODE_RAW) vw[i] = (int)type_width(S.src_type[i]);
-        else vw[i] = S.acc[i] == ACC_I128 ? 16 : 8;
+        else vw[i] = 8 * std::max(1, acc_words(S.acc[i]));
         o_val[i] = cv.take<uint4>((n * vw[i] + 15) / 16);
     }
     const size_t staging_bytes = cv.off; // key/value columns above; a second copy holds spills
@@ -1628,22 +1730,37 @@ int consume_keyed(tfg_agg *a, int mode, const RowPred &pred, const void *keys, i
         case 221: TFG_BUCKET(FastOps<2, 2, 1>); break;
         case 331: TFG_BUCKET(FastOps<3, 3, 1>); break;
         case 441: TFG_BUCKET(FastOps<4, 4, 1>); break;
-        default:
+        default: {
+            bool w256 = false; // a Decimal256 sum: rows carry 4-limb values
+            for (int i = 0; i < S.n_aggs; ++i) w256 = w256 || S.acc[i] == ACC_I256;
             if (key_width == 16) {
-                switch (S.n_aggs) {
-                case 1: TFG_BUCKET(WideOps<1>); break;
-                case 2: TFG_BUCKET(WideOps<2>); break;
-                case 3: TFG_BUCKET(WideOps<3>); break;
-                default: TFG_BUCKET(WideOps<4>); break;
-                }
+                if (w256) switch (S.n_aggs) {
+                    case 1: TFG_BUCKET(WideOps<1, true>); break;
+                    case 2: TFG_BUCKET(WideOps<2, true>); break;
+                    case 3: TFG_BUCKET(WideOps<3, true>); break;
+                    default: TFG_BUCKET(WideOps<4, true>); break;
+                    }
+                else switch (S.n_aggs) {
+                    case 1: TFG_BUCKET(WideOps<1>); break;
+                    case 2: TFG_BUCKET(WideOps<2>); break;
+                    case 3: TFG_BUCKET(WideOps<3>); break;
+                    default: TFG_BUCKET(WideOps<4>); break;
+                    }
                 break;
             }
-            switch (S.n_aggs) {
-            case 1: TFG_BUCKET(GenericOps<1>); break;
-            case 2: TFG_BUCKET(GenericOps<2>); break;
-            case 3: TFG_BUCKET(GenericOps<3>); break;
-            default: TFG_BUCKET(GenericOps<4>); break;
-            }
+            if (w256) switch (S.n_aggs) {
+                case 1: TFG_BUCKET(GenericOps<1, true>); break;
+                case 2: TFG_BUCKET(GenericOps<2, true>); break;
+                case 3: TFG_BUCKET(GenericOps<3, true>); break;
+                default: TFG_BUCKET(GenericOps<4, true>); break;
+                }
+            else switch (S.n_aggs) {
+                case 1: TFG_BUCKET(GenericOps<1>); break;
+                case 2: TFG_BUCKET(GenericOps<2>); break;
+                case 3: TFG_BUCKET(GenericOps<3>); break;
+                default: TFG_BUCKET(GenericOps<4>); break;
+                }
+        }
         }
 #undef TFG_BUCKET
     }
@@ -1687,9 +1804,17 @@ int consume_nokey(tfg_agg *a, int mode, const RowPred &pred, const void *const *
     return TFG_OK;
 }
 
-int sum_acc_kind(int t) {
+// sum state of an argument type word (tfg_type | TFG_ARG_PREC(p)): Float64, Int64 / UInt64, or the
+// Decimal result of SumDecimalInferer (Common/Decimal.h:156-163), Decimal(min(p + 22, 65), s):
+// Decimal128 up to 38 digits, Decimal256 above (AggregateFunctionSum.cpp:57-85)
+int sum_acc_kind(int word) {
+    const int t = TFG_ARG_TYPE(word);
     if (t == TFG_FLOAT32 || t == TFG_FLOAT64) return ACC_F64;
-    if (is_decimal_type(t)) return ACC_I128;
+    if (is_decimal_type(t) || t == TFG_DECIMAL256) {
+        int p = TFG_ARG_PREC_OF(word);
+        if (p == 0) p = t == TFG_DECIMAL32 ? 9 : t == TFG_DECIMAL64 ? 18 : t == TFG_DECIMAL128 ? 38 : 65;
+        return std::min(p + 22, 65) > 38 ? ACC_I256 : ACC_I128;
+    }
     return ACC_I64;
 }
 
@@ -1738,8 +1863,12 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
     int cell = wide ? 24 : 8; // key (wide: tag + 16-byte key)
     for (int i = 0; i < n_aggs; ++i) {
         const int kind = agg_kinds[i];
-        const int at = arg_types ? (arg_types[i] & 0xFF) : 0;
-        const bool nullable = arg_types && (arg_types[i] & 0x100);
+        const int at = arg_types ? TFG_ARG_TYPE(arg_types[i]) : 0;
+        const bool nullable = arg_types && (arg_types[i] & TFG_ARG_NULLABLE);
+        if (arg_types && TFG_ARG_PREC_OF(arg_types[i]) > 65) {
+            delete a;
+            return fail(TFG_ERR_ILLEGAL_TYPE, "decimal precision %d of argument %d exceeds 65", TFG_ARG_PREC_OF(arg_types[i]), i);
+        }
         if (kind < TFG_AGG_SUM || kind > TFG_AGG_COUNT_ALL) {
             delete a;
             return fail(TFG_ERR_NOT_IMPLEMENTED, "aggregate kind %d not supported", kind);
@@ -1749,17 +1878,18 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
         a->arg_types[i] = at;
         a->arg_nullable[i] = nullable;
         if (kind == TFG_AGG_SUM) {
-            if (!(is_fixed_numeric(at) || is_decimal_type(at))) {
+            if (!(is_fixed_numeric(at) || is_decimal_type(at) || at == TFG_DECIMAL256)) {
                 delete a;
                 return fail(TFG_ERR_ILLEGAL_TYPE, "sum over type %d not supported", at);
             }
-            S.acc[i] = sum_acc_kind(at);
+            S.acc[i] = sum_acc_kind(arg_types[i]);
             S.has_cnt[i] = nullable ? 1 : 0;
             a->result_type[i] = S.acc[i] == ACC_F64 ? TFG_FLOAT64
+                                : S.acc[i] == ACC_I256 ? TFG_DECIMAL256
                                 : S.acc[i] == ACC_I128 ? TFG_DECIMAL128
                                 : is_unsigned_type(at) ? TFG_UINT64 : TFG_INT64;
-            a->result_width[i] = S.acc[i] == ACC_I128 ? 16 : 8;
-            cell += S.acc[i] == ACC_I128 ? 16 : 8;
+            a->result_width[i] = 8 * acc_words(S.acc[i]);
+            cell += 8 * acc_words(S.acc[i]);
         } else {
             S.acc[i] = ACC_NONE;
             S.has_cnt[i] = 1;
@@ -1810,7 +1940,7 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
     for (int i = 0; i < n_aggs; ++i) {
         if (S.acc[i] != ACC_NONE) {
             S.acc_off[i] = off;
-            off += (cap + 2) * (S.acc[i] == ACC_I128 ? 16 : 8);
+            off += (cap + 2) * 8 * acc_words(S.acc[i]);
         }
         if (S.has_cnt[i]) {
             S.cnt_off[i] = off;

@@ -83,7 +83,7 @@ static __int128 pow10_128(int e) {
 
 static int make_side(int type, const void *p, int is_const, int scale, int res_type, int res_scale, int op,
                      ArithSide &s) {
-    TFG_CHECK(type_width(type) > 0, TFG_ERR_ILLEGAL_TYPE, "unsupported operand type %d", type);
+    TFG_CHECK(type_width(type) > 0 && type != TFG_DECIMAL256, TFG_ERR_ILLEGAL_TYPE, "unsupported operand type %d", type);
     TFG_CHECK(p, TFG_ERR_INVALID_ARG, "null operand");
     s.type = type;
     s.is_const = is_const;
@@ -119,7 +119,8 @@ extern "C" int tfg_arith(tfg_ctx *ctx, int op, int a_type, const void *a, int a_
                          const void *b, int b_is_const, int b_scale, int res_type, int res_scale, int64_t n, void *out) {
     TFG_CHECK(ctx && (n == 0 || out), TFG_ERR_INVALID_ARG, "null argument");
     TFG_CHECK(op >= TFG_PLUS && op <= TFG_MULTIPLY, TFG_ERR_NOT_IMPLEMENTED, "arithmetic op %d", op);
-    TFG_CHECK(type_width(res_type) > 0, TFG_ERR_ILLEGAL_TYPE, "unsupported result type %d", res_type);
+    TFG_CHECK(type_width(res_type) > 0 && res_type != TFG_DECIMAL256, TFG_ERR_NOT_IMPLEMENTED,
+              "unsupported result type %d (Decimal256 arithmetic is not on the path)", res_type);
     TFG_CHECK(!(is_decimal_type(res_type) && (is_float_type(a_type) || is_float_type(b_type))), TFG_ERR_ILLEGAL_TYPE,
               "decimal result with a float operand");
     if (is_decimal_type(res_type) && op == TFG_MULTIPLY)

@@ -48,6 +48,7 @@ size_t type_width(int t) {
     case TFG_INT32: case TFG_UINT32: case TFG_FLOAT32: case TFG_DECIMAL32: return 4;
     case TFG_INT64: case TFG_UINT64: case TFG_FLOAT64: case TFG_DECIMAL64: return 8;
     case TFG_DECIMAL128: return 16;
+    case TFG_DECIMAL256: return 32;
     default: return 0;
     }
 }

@@ -85,12 +85,15 @@ __global__ void fill_selector_kernel(const uint32_t *h, int64_t n, uint32_t part
     }
 }
 
+struct alignas(16) Bytes32 { // Decimal256 values
+    uint4 a, b;
+};
 template <int W>
 __global__ void gather_kernel(const uint32_t *perm, int64_t n, const void *in, void *out) {
-    using E = typename std::conditional<W == 16, uint4,
+    using E = typename std::conditional<W == 32, Bytes32, typename std::conditional<W == 16, uint4,
               typename std::conditional<W == 8, uint64_t,
               typename std::conditional<W == 4, uint32_t,
-              typename std::conditional<W == 2, uint16_t, uint8_t>::type>::type>::type>::type;
+              typename std::conditional<W == 2, uint16_t, uint8_t>::type>::type>::type>::type>::type;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const uint32_t r = perm[i];
         E v;
@@ -107,7 +110,7 @@ static int make_keycols(int nkeys, const int *idx, const int *types, const void 
     for (int j = 0; j < nkeys; ++j) {
         int c = idx ? idx[j] : j;
         int t = types[c];
-        TFG_CHECK(!is_float_type(t) && type_width(t) > 0, TFG_ERR_ILLEGAL_TYPE,
+        TFG_CHECK(!is_float_type(t) && type_width(t) > 0 && type_width(t) <= 16, TFG_ERR_ILLEGAL_TYPE,
                   "weak hash of type %d is not supported (float keys hash implementation-defined values)", t);
         k.col[j] = cols[c];
         k.nullmap[j] = nullmaps ? nullmaps[c] : nullptr;
@@ -201,6 +204,7 @@ int tfg_gather(tfg_ctx *ctx, const uint32_t *perm, int64_t n, int ncols, const v
         case 4: hipLaunchKernelGGL(gather_kernel<4>, dim3(grid), dim3(256), 0, ctx->stream, perm, n, cols[j], outs[j]); break;
         case 8: hipLaunchKernelGGL(gather_kernel<8>, dim3(grid), dim3(256), 0, ctx->stream, perm, n, cols[j], outs[j]); break;
         case 16: hipLaunchKernelGGL(gather_kernel<16>, dim3(grid), dim3(256), 0, ctx->stream, perm, n, cols[j], outs[j]); break;
+        case 32: hipLaunchKernelGGL(gather_kernel<32>, dim3(grid), dim3(256), 0, ctx->stream, perm, n, cols[j], outs[j]); break;
         default: return fail(TFG_ERR_INVALID_ARG, "bad column width %d", widths[j]);
         }
     }

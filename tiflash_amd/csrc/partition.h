@@ -341,6 +341,10 @@ __device__ __forceinline__ void scatter_row(const PCols &cols, int64_t r, uint64
         case 2: ((uint16_t *)cols.out[j])[pos] = ((const uint16_t *)cols.in[j])[r]; break;
         case 4: ((uint32_t *)cols.out[j])[pos] = ((const uint32_t *)cols.in[j])[r]; break;
         case 8: ((uint64_t *)cols.out[j])[pos] = ((const uint64_t *)cols.in[j])[r]; break;
+        case 32: // Decimal256 sums (two-phase aggregation states)
+            ((uint4 *)cols.out[j])[2 * pos] = ((const uint4 *)cols.in[j])[2 * r];
+            ((uint4 *)cols.out[j])[2 * pos + 1] = ((const uint4 *)cols.in[j])[2 * r + 1];
+            break;
         default: {
             const uint4 v = ((const uint4 *)cols.in[j])[r];
             ((uint4 *)cols.out[j])[pos] = v;
@@ -641,10 +645,12 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
                         }
                     }
                 } else {
+                    const int q = w / 16; // 16- or 32-byte values as 1-2 uint4
 #pragma unroll
                     for (int j = 0; j < ST_MAXR; ++j)
                         if (bq[j] != 0xFFFFFFFFu)
-                            ((uint4 *)st)[sl[j]] = ((const uint4 *)cols.in[c])[tb + (uint32_t)j * ST_T + threadIdx.x];
+                            for (int h = 0; h < q; ++h)
+                                ((uint4 *)st)[sl[j] * q + h] = ((const uint4 *)cols.in[c])[(size_t)(tb + (uint32_t)j * ST_T + threadIdx.x) * q + h];
                 }
             }
         }
@@ -680,6 +686,10 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
                     case 2: ((uint16_t *)cols.out[c])[gp] = ((const uint16_t *)st)[s]; break;
                     case 4: ((uint32_t *)cols.out[c])[gp] = ((const uint32_t *)st)[s]; break;
                     case 8: ((uint64_t *)cols.out[c])[gp] = ((const uint64_t *)st)[s]; break;
+                    case 32:
+                        ((uint4 *)cols.out[c])[2 * gp] = ((const uint4 *)st)[2 * s];
+                        ((uint4 *)cols.out[c])[2 * gp + 1] = ((const uint4 *)st)[2 * s + 1];
+                        break;
                     default: ((uint4 *)cols.out[c])[gp] = ((const uint4 *)st)[s]; break;
                     }
                 }

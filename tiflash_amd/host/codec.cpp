@@ -46,7 +46,10 @@ static DataType typeFromWire(int t, int nullable, const char *name) {
     d.nullable = nullable != 0;
     const char *dec = strstr(name, "Decimal(");
     int prec = 0, scale = 0;
-    if (dec && sscanf(dec, "Decimal(%d,%d)", &prec, &scale) == 2) d.scale = scale;
+    if (dec && sscanf(dec, "Decimal(%d,%d)", &prec, &scale) == 2) {
+        d.scale = scale;
+        d.prec = prec;
+    }
     return d;
 }
 

@@ -35,6 +35,29 @@ DeviceBuffer::~DeviceBuffer() {
 
 size_t DataType::width() const { return isString() ? 0 : tfg_type_width(type); }
 
+int DataType::precision() const {
+    if (prec > 0) return prec;
+    switch (type) {
+    case TFG_DECIMAL32: return 9;
+    case TFG_DECIMAL64: return 18;
+    case TFG_DECIMAL128: return 38;
+    case TFG_DECIMAL256: return 65;
+    default: return 0;
+    }
+}
+
+DataType DataType::decimal(int p, int s, bool nullable) {
+    if (p < 1 || p > 65 || s < 0 || s > p)
+        throw Exception("Decimal(" + std::to_string(p) + "," + std::to_string(s) + ") is out of range",
+                        ErrorCodes::BAD_ARGUMENTS);
+    DataType d;
+    d.type = p <= 9 ? TFG_DECIMAL32 : p <= 18 ? TFG_DECIMAL64 : p <= 38 ? TFG_DECIMAL128 : TFG_DECIMAL256;
+    d.prec = p;
+    d.scale = s;
+    d.nullable = nullable;
+    return d;
+}
+
 std::string DataType::getName() const {
     std::string n;
     switch (type) {
@@ -48,9 +71,10 @@ std::string DataType::getName() const {
     case TFG_UINT64: n = "UInt64"; break;
     case TFG_FLOAT32: n = "Float32"; break;
     case TFG_FLOAT64: n = "Float64"; break;
-    case TFG_DECIMAL32: n = "Decimal(9," + std::to_string(scale) + ")"; break;
-    case TFG_DECIMAL64: n = "Decimal(18," + std::to_string(scale) + ")"; break;
-    case TFG_DECIMAL128: n = "Decimal(38," + std::to_string(scale) + ")"; break;
+    case TFG_DECIMAL32:
+    case TFG_DECIMAL64:
+    case TFG_DECIMAL128:
+    case TFG_DECIMAL256: n = "Decimal(" + std::to_string(precision()) + "," + std::to_string(scale) + ")"; break;
     case TYPE_STRING: n = "String"; break;
     default: n = "Unknown"; break;
     }

@@ -65,13 +65,27 @@ bool ExpressionActions::singleCompare(std::string &column, int &op, Field &const
 
 namespace {
 
-bool isDecimal(int t) { return t == TFG_DECIMAL32 || t == TFG_DECIMAL64 || t == TFG_DECIMAL128; }
+bool isDecimal(int t) { return t == TFG_DECIMAL32 || t == TFG_DECIMAL64 || t == TFG_DECIMAL128 || t == TFG_DECIMAL256; }
+
+// IntPrec<T>::prec (Common/Decimal.h:45-93): an integer operand of decimal arithmetic is
+// Decimal(IntPrec, 0)
+int intPrec(int t) {
+    switch (t) {
+    case TFG_INT8: case TFG_UINT8: return 3;
+    case TFG_INT16: case TFG_UINT16: return 5;
+    case TFG_INT32: case TFG_UINT32: return 10;
+    case TFG_INT64: return 19;
+    default: return 20; // UInt64
+    }
+}
 bool isFloat(int t) { return t == TFG_FLOAT32 || t == TFG_FLOAT64; }
 bool isUnsigned(int t) { return t >= TFG_UINT8 && t <= TFG_UINT64; }
 
 // result type of a +|-|* b (FunctionBinaryArithmetic result-type rules restricted to the path:
-// integers -> 64-bit of the operands' signedness, floats -> Float64, decimals -> the wider
-// decimal with the max scale for +/-, Decimal128 with s1 + s2 for *; MulDecimalInferer)
+// integers -> 64-bit of the operands' signedness, floats -> Float64; decimals by the inferers of
+// Common/Decimal.h:109-163 — PlusDecimalInferer: scale max(s1, s2), precision
+// min(max(p1 - s1, p2 - s2) + scale + 1, 65); MulDecimalInferer: (min(p1 + p2, 65), min(s1 + s2, 30))
+// — stored in the narrowest Decimal of that precision (createDecimal)
 DataType arithResult(int op, const DataType &a, const DataType &b) {
     DataType r;
     r.nullable = a.nullable || b.nullable;
@@ -79,13 +93,20 @@ DataType arithResult(int op, const DataType &a, const DataType &b) {
         if (isFloat(a.type) || isFloat(b.type))
             throw Exception("decimal arithmetic with a float operand", ErrorCodes::ILLEGAL_TYPE_OF_ARGUMENT);
         const int sa = isDecimal(a.type) ? a.scale : 0, sb = isDecimal(b.type) ? b.scale : 0;
+        const int pa = isDecimal(a.type) ? a.precision() : intPrec(a.type);
+        const int pb = isDecimal(b.type) ? b.precision() : intPrec(b.type);
+        int prec, scale;
         if (op == TFG_MULTIPLY) {
-            r.type = TFG_DECIMAL128;
-            r.scale = sa + sb;
+            prec = std::min(pa + pb, 65);
+            scale = std::min(sa + sb, 30);
         } else {
-            r.type = std::max(isDecimal(a.type) ? a.type : TFG_DECIMAL64, isDecimal(b.type) ? b.type : TFG_DECIMAL64);
-            r.scale = std::max(sa, sb);
+            scale = std::max(sa, sb);
+            prec = std::min(std::max(pa - sa, pb - sb) + scale + 1, 65);
         }
+        r = DataType::decimal(prec, scale, r.nullable);
+        if (r.type == TFG_DECIMAL256)
+            throw Exception("Decimal256 arithmetic result " + r.getName() + " is not on the path",
+                            ErrorCodes::NOT_IMPLEMENTED);
         return r;
     }
     if (isFloat(a.type) || isFloat(b.type)) {

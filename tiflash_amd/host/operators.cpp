@@ -43,7 +43,10 @@ Aggregator::Aggregator(Context &ctx, const Params &params) : ctx_(ctx), params_(
         }
         kinds_.push_back(kind);
         arg_types_.push_back(at);
-        arg_types.push_back(kind == TFG_AGG_COUNT_ALL ? 0 : (at.type | (at.nullable ? 0x100 : 0)));
+        arg_types.push_back(kind == TFG_AGG_COUNT_ALL
+                                ? 0
+                                : (at.type | (at.nullable ? TFG_ARG_NULLABLE : 0) |
+                                   (at.isDecimal() ? TFG_ARG_PREC(at.precision()) : 0)));
         arg_scales.push_back(at.scale);
     }
     tfg_agg_params p{params_.bucket_bits, params_.expected_groups};
@@ -200,6 +203,9 @@ Block Aggregator::convertToBlock(bool final) const {
         auto c = std::make_shared<IColumn>();
         c->type.type = t;
         c->type.scale = kinds_[i] == TFG_AGG_SUM ? arg_types_[i].scale : 0;
+        // sum(Decimal(p, s)) -> Decimal(min(p + 22, 65), s) (SumDecimalInferer, Common/Decimal.h:156-163)
+        if (kinds_[i] == TFG_AGG_SUM && arg_types_[i].isDecimal())
+            c->type.prec = std::min(arg_types_[i].precision() + 22, 65);
         // sum over a nullable argument is Nullable (AggregateFunctionNullUnary); count never is
         c->type.nullable = kinds_[i] == TFG_AGG_SUM && arg_types_[i].nullable;
         c->rows = g;

@@ -88,15 +88,26 @@ private:
 using DeviceBufferPtr = std::shared_ptr<DeviceBuffer>;
 
 // ---------------------------------------------------------------- types and columns
+// DataTypeDecimal carries (precision, scale) (DataTypes/DataTypeDecimal.h); prec 0 means the
+// storage type's maximum (Decimal32 9, Decimal64 18, Decimal128 38, Decimal256 65).
 struct DataType {
     int type = TFG_INT64; // tfg_type, or TYPE_STRING
     int scale = 0;        // Decimal scale
+    int prec = 0;         // Decimal precision (0 = the storage type's maximum)
     bool nullable = false;
     static constexpr int TYPE_STRING = 100;
     size_t width() const; // bytes per value (0 for String)
     bool isString() const { return type == TYPE_STRING; }
+    bool isDecimal() const {
+        return type == TFG_DECIMAL32 || type == TFG_DECIMAL64 || type == TFG_DECIMAL128 || type == TFG_DECIMAL256;
+    }
+    int precision() const; // prec, or the storage type's maximum
     std::string getName() const;
-    bool operator==(const DataType &o) const { return type == o.type && scale == o.scale && nullable == o.nullable; }
+    bool operator==(const DataType &o) const {
+        return type == o.type && scale == o.scale && nullable == o.nullable && (!isDecimal() || precision() == o.precision());
+    }
+    // createDecimal(prec, scale): the narrowest storage type of a precision (DataTypes/DataTypeDecimal.h)
+    static DataType decimal(int prec, int scale, bool nullable = false);
 };
 
 // Immutable device column: fixed-width values (`data`), or String chars + UInt64 end offsets
