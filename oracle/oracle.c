@@ -344,8 +344,11 @@ int orc_arith(int op, int a_type, const void *a, int a_const, int a_scale, int b
     for (size_t i = 0; i < n; ++i) {
         size_t ia = a_const ? 0 : i, ib = b_const ? 0 : i;
         if (res_type == TFG_FLOAT64 || res_type == TFG_FLOAT32) {
-            double x = is_float(a_type) ? load_f(a_type, a, ia) : (double)load_s(a_type, a, ia);
-            double y = is_float(b_type) ? load_f(b_type, b, ib) : (double)load_s(b_type, b, ib);
+            /* an integer operand converts to Float64 by value (UInt64 above 2^63 included) */
+            double x = is_float(a_type) ? load_f(a_type, a, ia)
+                       : a_type == TFG_UINT64 ? (double)((const uint64_t *)a)[ia] : (double)load_s(a_type, a, ia);
+            double y = is_float(b_type) ? load_f(b_type, b, ib)
+                       : b_type == TFG_UINT64 ? (double)((const uint64_t *)b)[ib] : (double)load_s(b_type, b, ib);
             double r = op == TFG_PLUS ? x + y : op == TFG_MINUS ? x - y : x * y;
             if (res_type == TFG_FLOAT64) ((double *)out)[i] = r;
             else ((float *)out)[i] = (float)r;
