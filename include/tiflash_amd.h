@@ -224,12 +224,26 @@ int tfg_weak_hash_init(tfg_ctx *ctx, uint32_t *h, int64_t n);
  * (Columns/ColumnVector.cpp:499-535, ColumnDecimal.cpp:658, Common/HashTable/Hash.h:70-145):
  * integers are converted to UInt64 by C++ implicit conversion (signed types sign-extend),
  * Decimal128 hashes its two 64-bit limbs low then high.  NULL rows keep the previous h
- * (ColumnNullable.cpp:131-173).  Float columns are rejected (implementation-defined in C++). */
+ * (ColumnNullable.cpp:131-173).  Float32 / Float64 convert to UInt64 as the reference's x86-64
+ * build does (clang, SSE4.2: cvttsd2si pair; NaN / out of range -> 0x8000000000000000, negative
+ * values wrap), pinned by tests/golden/float_weak_hash.json. */
 int tfg_weak_hash_update(tfg_ctx *ctx, int type, const void *col, const uint8_t *nullmap, int64_t n, uint32_t *h);
+/* BlockInfo::selective (Core/BlockInfo.h:47-49; ColumnVector.cpp:500-535): h has n entries and
+ * h[i] hashes row selective[i] (a DEVICE array of n UInt64 row ids); selective NULL = every row. */
+int tfg_weak_hash_update_selective(tfg_ctx *ctx, int type, const void *col, const uint8_t *nullmap,
+                                   const uint64_t *selective, int64_t n, uint32_t *h);
 /* String keys (ColumnString::updateWeakHash32, Columns/ColumnString.cpp:1228-1327 with
  * ::updateWeakHash32(bytes), Common/HashTable/Hash.h:148-214). */
 int tfg_weak_hash_update_string(tfg_ctx *ctx, const uint8_t *chars, const uint64_t *offsets, const uint8_t *nullmap,
                                 int64_t n, int collator, uint32_t *h);
+/* ColumnString::updateWeakHash32 over selective rows (ColumnString.cpp:1256-1294). */
+int tfg_weak_hash_update_string_selective(tfg_ctx *ctx, const uint8_t *chars, const uint64_t *offsets,
+                                          const uint8_t *nullmap, const uint64_t *selective, int64_t n, int collator,
+                                          uint32_t *h);
+/* out_perm[i] = selective[perm[i]] (perm NULL: selective[i]): a tfg_partition permutation of the
+ * selective rows mapped back to block rows, for tfg_gather (IColumn::scatter with a selective,
+ * IColumn.h:678-721). */
+int tfg_selective_perm(tfg_ctx *ctx, const uint64_t *selective, const uint32_t *perm, int64_t n, uint32_t *out_perm);
 /* selector[i] = (UInt64(h[i]) * part_num) >> 32 (fillSelector, Flash/Mpp/HashBaseWriterHelper.cpp:46-62);
  * with fine_grained_stream_count > 0: selector = part * S + h % S (fillSelectorForFineGrainedShuffle, :64-84). */
 int tfg_fill_selector(tfg_ctx *ctx, const uint32_t *h, int64_t n, uint32_t part_num,

@@ -142,11 +142,34 @@ static uint64_t load_key_bits(int t, const void *p, size_t i)
 /* ColumnVector<T>::updateWeakHash32Impl (Columns/ColumnVector.cpp:499-535): h = crc(h, UInt64(v));
  * ColumnDecimal (ColumnDecimal.cpp:658 -> wideIntHashCRC32, Hash.h:97-145);
  * ColumnNullable keeps the old hash for NULL rows (ColumnNullable.cpp:131-173). */
+/* Float -> UInt64 as the reference's implicit conversion in intHashCRC32(UInt64, UInt32)
+ * (Columns/ColumnVector.cpp:528, Common/HashTable/Hash.h:83-94) compiles on x86-64 with clang
+ * (SSE4.2, no AVX-512): cvttsd2si(x) | (cvttsd2si(x - 2^63) & (cvttsd2si(x) >> 63)), where the
+ * truncating convert gives INT64_MIN for NaN / out-of-range values.  Restated explicitly (a C
+ * cast is undefined there); pinned by tests/golden/float_weak_hash.json. */
+static int64_t cvtt_d(double x) { return (x >= -9223372036854775808.0 && x < 9223372036854775808.0) ? (int64_t)x : INT64_MIN; }
+static int64_t cvtt_f(float x) { return (x >= -9223372036854775808.0f && x < 9223372036854775808.0f) ? (int64_t)x : INT64_MIN; }
+uint64_t orc_float64_to_u64(double x)
+{
+    const int64_t a = cvtt_d(x), b = cvtt_d(x - 9223372036854775808.0);
+    return (uint64_t)(a | (b & (a >> 63)));
+}
+uint64_t orc_float32_to_u64(float x)
+{
+    const float y = x - 9223372036854775808.0f; /* float arithmetic, as subss */
+    const int64_t a = cvtt_f(x), b = cvtt_f(y);
+    return (uint64_t)(a | (b & (a >> 63)));
+}
+
 void orc_weak_hash_update(int type, const void *col, const uint8_t *nullmap, size_t n, uint32_t *h)
 {
     for (size_t i = 0; i < n; ++i) {
         if (nullmap && nullmap[i]) continue;
-        if (type == TFG_DECIMAL128) {
+        if (type == TFG_FLOAT64 || type == TFG_FLOAT32) {
+            const uint64_t v = type == TFG_FLOAT64 ? orc_float64_to_u64(((const double *)col)[i])
+                                                   : orc_float32_to_u64(((const float *)col)[i]);
+            h[i] = orc_crc32c_u64(h[i], v);
+        } else if (type == TFG_DECIMAL128) {
             uint64_t limb[2];
             memcpy(limb, (const char *)col + 16 * i, 16);
             uint32_t x = orc_crc32c_u64(h[i], limb[0]);

@@ -26,6 +26,8 @@ uint32_t orc_crc32c_u64_sw(uint32_t crc, uint64_t x); /* bitwise, reflected 0x82
 uint32_t orc_update_weak_hash32_bytes(const uint8_t *pos, size_t size, uint32_t h);
 
 void orc_weak_hash_update(int type, const void *col, const uint8_t *nullmap, size_t n, uint32_t *h);
+uint64_t orc_float64_to_u64(double x); /* the reference build's Float64 -> UInt64 (x86-64 clang) */
+uint64_t orc_float32_to_u64(float x);
 void orc_weak_hash_update_string(const uint8_t *chars, const uint64_t *offsets, const uint8_t *nullmap, size_t n,
                                  int collator, uint32_t *h);
 void orc_fill_selector(const uint32_t *h, size_t n, uint32_t part_num, uint32_t fgs, uint32_t *sel);

@@ -17,7 +17,7 @@
 #include <sstream>
 
 #include "../../oracle/oracle.h"
-#include "../../tiflash_amd/host/tfa_host.h"
+#include "../../tiflash_amd/host/pipeline.h"
 
 using namespace tfa;
 
@@ -630,6 +630,19 @@ TEST(MPPExchangeSingleRank) {
            (std::vector<std::string>{"a", "", std::string(70, 'q'), "k00000001"}));
     Block es = ex.exchange({bs.cloneEmpty()}); // nothing sent, nothing received
     EXPECT(es.rows() == 0 && es.columns() == 2);
+    // the planes follow the schema: a Nullable(Int64) column that carries no null map on this
+    // rank (no NULLs here) still sends a null plane, and arrives Nullable with no NULLs
+    auto nomap = std::make_shared<IColumn>(*makeColumn(ctx, i64n, k.data(), 4));
+    nomap->nullmap.reset();
+    Block bn{{nomap, i64n, "k"}};
+    Block rn = ex.exchange({bn});
+    EXPECT(rn.getByName("k").type.nullable && rn.getByName("k").column->nullmap);
+    EXPECT(cellStrings(ctx, *rn.getByName("k").column) == (std::vector<std::string>{"5", "6", "7", "8"}));
+    // and a non-Nullable schema never sends one
+    DataType i64;
+    Block bp{{makeColumn(ctx, i64, k.data(), 4), i64, "k"}};
+    Block rp = ex.exchange({bp});
+    EXPECT(!rp.getByName("k").type.nullable && !rp.getByName("k").column->nullmap);
 }
 
 // CHBlockChunkCodecV1 / CHBlockChunkCodec round trips through device packets (the reference's
@@ -1121,6 +1134,67 @@ TEST(AutoPassThroughHashAgg) {
     EXPECT(pass > 0 && st.count((int)AutoPassThroughHashAggContext::State::Selective));
 }
 
+// Two GROUP BY keys (Int64, Nullable(Int32)) through the pass-through state machine: the first
+// key alone collides constantly (1000 values), so a Selective-state lookup on it alone would call
+// new tuples hits.  The lookup runs on the full tuple; tuples holding a NULL pass through.  Every
+// output block carries both keys, and the merged result equals a host aggregation of the input.
+TEST(AutoPassThroughHashAggTwoKeys) {
+    DataType i64, i32n;
+    i32n.type = TFG_INT32;
+    i32n.nullable = true;
+    Aggregator::Params p;
+    p.keys = {"k1", "k2"};
+    p.aggregates = {{"sum", {"v"}, "sum_v"}, {"count", {}, "cnt"}};
+    p.src_header = Block{{nullptr, i64, "k1"}, {nullptr, i32n, "k2"}, {nullptr, i64, "v"}};
+    const size_t B = 8192;
+    AutoPassThroughHashAggContext apt(ctx, p, /*row_limit_unit=*/B);
+    std::mt19937_64 rng(91);
+    using Key = std::tuple<int64_t, int64_t>; // k2 = INT64_MIN stands for NULL
+    std::map<Key, std::pair<int64_t, uint64_t>> want;
+    std::vector<Block> out;
+    std::set<int> states;
+    int64_t next_new = 0;
+    for (size_t bi = 0; bi < 30; ++bi) {
+        std::vector<int64_t> k1(B), v(B);
+        std::vector<int32_t> k2(B);
+        std::vector<uint8_t> k2n(B);
+        for (size_t i = 0; i < B; ++i) {
+            const int64_t key = bi < 9 ? next_new++ : rng() % 2 ? (int64_t)(rng() % 70000) : 1000000 + next_new++;
+            k1[i] = key % 1000;
+            k2[i] = (int32_t)(key / 1000);
+            k2n[i] = rng() % 50 == 0;
+            v[i] = (int64_t)(rng() % 1000) - 500;
+            auto &w = want[Key{k1[i], k2n[i] ? INT64_MIN : (int64_t)k2[i]}];
+            w.first += v[i];
+            w.second += 1;
+        }
+        Block b{{makeColumn(ctx, i64, k1.data(), B), i64, "k1"},
+                {makeColumn(ctx, i32n, k2.data(), B, k2n.data()), i32n, "k2"},
+                {makeColumn(ctx, i64, v.data(), B), i64, "v"}};
+        apt.onBlock(b); // throws "Selective state grew the hash map" on a false hit
+        states.insert((int)apt.state());
+        while (Block r = apt.tryGetDataInAdvance()) out.push_back(r);
+    }
+    if (Block h = apt.getDataFromHashTable()) out.push_back(h);
+    EXPECT(apt.passThroughRows() > 0 && states.count((int)AutoPassThroughHashAggContext::State::Selective));
+    std::map<Key, std::pair<int64_t, uint64_t>> got;
+    for (const Block &b : out) {
+        EXPECT(b.has("k1") && b.has("k2"));
+        auto a1 = toHost<int64_t>(ctx, *materialize(ctx, b.getByName("k1").column));
+        auto a2c = materialize(ctx, b.getByName("k2").column);
+        auto a2 = toHost<int32_t>(ctx, *a2c);
+        auto a2n = toHostNullMap(ctx, *a2c);
+        auto sv = toHost<int64_t>(ctx, *materialize(ctx, b.getByName("sum_v").column));
+        auto c = toHost<uint64_t>(ctx, *materialize(ctx, b.getByName("cnt").column));
+        for (size_t i = 0; i < a1.size(); ++i) {
+            auto &g = got[Key{a1[i], a2n[i] ? INT64_MIN : (int64_t)a2[i]}];
+            g.first += sv[i];
+            g.second += c[i];
+        }
+    }
+    EXPECT(got == want);
+}
+
 // Decimal precision (DataTypeDecimal(prec, scale)) through the operators: sum(Decimal(p, s)) ->
 // Decimal(min(p + 22, 65), s) (SumDecimalInferer, Common/Decimal.h:156-163): Decimal(15,2) keeps an
 // Int128 state, Decimal(18,2) and Decimal(38,4) a Decimal256 one (exact past Int128); and the
@@ -1242,6 +1316,349 @@ TEST(DecimalArithInferers) {
         bad += hx[i] != (__int128)a[i] * b[i];
     }
     EXPECT(bad == 0);
+}
+
+// ================================================================ pipeline engine (b)
+// The reference's operator contract (Operators/Operator.h:32-173) driven the way its
+// PipelineExec does (PipelineExec.cpp:120-180), two execs per pipeline, results vs the oracle.
+static std::vector<Block> splitBlocks(Context &ctx, const Block &b, size_t parts) {
+    std::vector<Block> out;
+    const size_t n = b.rows();
+    for (size_t i = 0; i < parts; ++i) {
+        const size_t lo = n * i / parts, hi = n * (i + 1) / parts;
+        out.push_back(sliceBlock(ctx, b, lo, hi - lo));
+    }
+    return out;
+}
+
+// filter -> aggregation: [BlocksSourceOp -> FilterTransformOp -> AggregateBuildSinkOp] x 2, then
+// [AggregateConvergentSourceOp -> GetResultSinkOp] x 2; also the pushed-down (fused) filter form
+TEST(PipelineFilterAggregate) {
+    std::mt19937_64 rng(101);
+    const size_t n = 200000;
+    std::vector<int64_t> f(n), k(n);
+    std::vector<double> d(n);
+    for (size_t i = 0; i < n; ++i) {
+        f[i] = rng() % 100;
+        k[i] = (int64_t)(rng() % 30000);
+        d[i] = (double)(rng() % (1 << 20)) / 256.0;
+    }
+    DataType i64, f64;
+    f64.type = TFG_FLOAT64;
+    Block b{{makeColumn(ctx, i64, f.data(), n), i64, "f"}, {makeColumn(ctx, i64, k.data(), n), i64, "k"},
+            {makeColumn(ctx, f64, d.data(), n), f64, "d"}};
+    std::vector<Block> blocks = splitBlocks(ctx, b, 6);
+    Aggregator::Params p;
+    p.src_header = b.cloneEmpty();
+    p.keys = {"k"};
+    p.aggregates = {{"sum", {"d"}, "sum_d"}, {"count", {}, "cnt"}};
+    // oracle
+    std::vector<uint8_t> mask(n);
+    for (size_t i = 0; i < n; ++i) mask[i] = f[i] < 40;
+    int kinds[2] = {TFG_AGG_SUM, TFG_AGG_COUNT_ALL};
+    int types[2] = {TFG_FLOAT64, 0};
+    orc_agg *o = orc_agg_create(TFG_INT64, 2, kinds, types);
+    const void *args[2] = {d.data(), nullptr};
+    const uint8_t *an[2] = {nullptr, nullptr};
+    orc_agg_consume(o, k.data(), nullptr, args, an, mask.data(), n);
+    const size_t g = orc_agg_size(o);
+    std::vector<uint64_t> ok(g), oc(g);
+    std::vector<double> od(g);
+    std::vector<uint8_t> okn(g), on0(g), on1(g);
+    void *outs[2] = {od.data(), oc.data()};
+    uint8_t *outn[2] = {on0.data(), on1.data()};
+    orc_agg_result(o, ok.data(), okn.data(), outs, outn);
+    orc_agg_destroy(o);
+    std::map<int64_t, std::pair<double, uint64_t>> want;
+    for (size_t i = 0; i < g; ++i) want[(int64_t)ok[i]] = {od[i], oc[i]};
+    for (int pushed = 0; pushed < 2; ++pushed) {
+        g_current = pushed ? "pushed-down filter" : "FilterTransformOp";
+        PipelineExecutorContext exec;
+        auto agg_ctx = std::make_shared<AggregateContext>(ctx, p, 2);
+        std::vector<PipelineExecPtr> build;
+        for (size_t t = 0; t < 2; ++t) {
+            std::vector<Block> mine;
+            for (size_t i = t; i < blocks.size(); i += 2) mine.push_back(blocks[i]);
+            TransformOps tr;
+            auto sink = std::make_unique<AggregateBuildSinkOp>(exec, ctx, agg_ctx, t);
+            if (pushed) {
+                sink->setPushedDownFilter("f", TFG_LT, Field::Int64(40));
+            } else {
+                auto expr = std::make_shared<ExpressionActions>(ctx);
+                expr->compare("f", TFG_LT, Field::Int64(40), "pred");
+                Block h = b.cloneEmpty();
+                tr.push_back(std::make_unique<FilterTransformOp>(exec, ctx, h, expr, "pred"));
+            }
+            build.push_back(std::make_unique<PipelineExec>(std::make_unique<BlocksSourceOp>(exec, ctx, b, mine),
+                                                           std::move(tr), std::move(sink)));
+        }
+        runPipelineExecs(exec, build);
+        EXPECT(agg_ctx->allBuildFinished());
+        EXPECT(agg_ctx->getTotalBuildRows(0) + agg_ctx->getTotalBuildRows(1) == (pushed ? n : (size_t)std::count(mask.begin(), mask.end(), 1)));
+        std::vector<Block> results;
+        std::vector<PipelineExecPtr> conv;
+        for (size_t t = 0; t < 2; ++t)
+            conv.push_back(std::make_unique<PipelineExec>(
+                std::make_unique<AggregateConvergentSourceOp>(exec, ctx, agg_ctx, t), TransformOps{},
+                std::make_unique<GetResultSinkOp>(exec, ctx, [&](const Block &r) { results.push_back(r); })));
+        runPipelineExecs(exec, conv);
+        EXPECT(results.size() == 2); // one row range per convergent source
+        std::map<int64_t, std::pair<double, uint64_t>> got;
+        for (const Block &r : results) {
+            auto rk = toHost<int64_t>(ctx, *r.getByName("k").column);
+            auto rd = toHost<double>(ctx, *r.getByName("sum_d").column);
+            auto rc = toHost<uint64_t>(ctx, *r.getByName("cnt").column);
+            for (size_t i = 0; i < rk.size(); ++i) EXPECT(got.emplace(rk[i], std::make_pair(rd[i], rc[i])).second);
+        }
+        EXPECT(got == want);
+        const auto &src = build[0]->source().getProfileInfo();
+        EXPECT(src.blocks == 3 && src.rows == blocks[0].rows() + blocks[2].rows() + blocks[4].rows());
+    }
+}
+
+// build -> probe: [BlocksSourceOp -> HashJoinBuildSink] x 2, then [BlocksSourceOp ->
+// HashJoinProbeTransformOp (max_block_size 5000: output sliced through tryOutput) ->
+// GetResultSinkOp] x 2, vs the oracle's pairs; also an empty build side
+TEST(PipelineHashJoin) {
+    std::mt19937_64 rng(102);
+    const size_t nb = 40000, np = 120000;
+    std::vector<int64_t> bk(nb), bp(nb), pk(np);
+    for (size_t i = 0; i < nb; ++i) {
+        bk[i] = rng() % 30000;
+        bp[i] = (int64_t)i;
+    }
+    for (size_t i = 0; i < np; ++i) pk[i] = rng() % 50000;
+    DataType i64;
+    Block build{{makeColumn(ctx, i64, bk.data(), nb), i64, "bk"}, {makeColumn(ctx, i64, bp.data(), nb), i64, "bpay"}};
+    Block probe{{makeColumn(ctx, i64, pk.data(), np), i64, "pk"}};
+    orc_join *oj = orc_join_create(TFG_INT64);
+    orc_join_build(oj, bk.data(), nullptr, nb);
+    std::vector<uint32_t> op(np * 4), ob(np * 4);
+    const size_t m = orc_join_probe(oj, TFG_JOIN_INNER, pk.data(), nullptr, np, op.data(), ob.data(), op.size());
+    orc_join_destroy(oj);
+    std::multiset<std::pair<int64_t, int64_t>> want;
+    for (size_t i = 0; i < m; ++i) want.insert({pk[op[i]], bp[ob[i]]});
+    for (int empty_build = 0; empty_build < 2; ++empty_build) {
+        g_current = empty_build ? "empty build" : "join";
+        PipelineExecutorContext exec;
+        auto join = std::make_shared<Join>(ctx, JoinKind::Inner, "pk", "bk", (int64_t)nb);
+        auto jctx = std::make_shared<JoinBuildContext>(ctx, join, 2, build.cloneEmpty());
+        std::vector<Block> bblocks = empty_build ? std::vector<Block>{} : splitBlocks(ctx, build, 4);
+        std::vector<PipelineExecPtr> bpipe;
+        for (size_t t = 0; t < 2; ++t) {
+            std::vector<Block> mine;
+            for (size_t i = t; i < bblocks.size(); i += 2) mine.push_back(bblocks[i]);
+            bpipe.push_back(std::make_unique<PipelineExec>(std::make_unique<BlocksSourceOp>(exec, ctx, build, mine),
+                                                           TransformOps{},
+                                                           std::make_unique<HashJoinBuildSink>(exec, ctx, jctx, t)));
+        }
+        runPipelineExecs(exec, bpipe);
+        EXPECT(jctx->isFinalized());
+        std::vector<Block> pblocks = splitBlocks(ctx, probe, 3);
+        std::vector<Block> out;
+        std::vector<PipelineExecPtr> ppipe;
+        for (size_t t = 0; t < 2; ++t) {
+            std::vector<Block> mine;
+            for (size_t i = t; i < pblocks.size(); i += 2) mine.push_back(pblocks[i]);
+            TransformOps tr;
+            auto probe_op = std::make_unique<HashJoinProbeTransformOp>(exec, ctx, jctx, t, 5000);
+            Block h = probe.cloneEmpty();
+            probe_op->transformHeader(h);
+            tr.push_back(std::move(probe_op));
+            ppipe.push_back(std::make_unique<PipelineExec>(std::make_unique<BlocksSourceOp>(exec, ctx, probe, mine),
+                                                           std::move(tr),
+                                                           std::make_unique<GetResultSinkOp>(exec, ctx, [&](const Block &r) {
+                                                               out.push_back(r);
+                                                           })));
+        }
+        runPipelineExecs(exec, ppipe);
+        std::multiset<std::pair<int64_t, int64_t>> got;
+        size_t max_rows = 0;
+        for (const Block &r : out) {
+            max_rows = std::max(max_rows, r.rows());
+            auto gk = toHost<int64_t>(ctx, *r.getByName("pk").column);
+            auto gb = toHost<int64_t>(ctx, *r.getByName("bpay").column);
+            for (size_t i = 0; i < gk.size(); ++i) got.insert({gk[i], gb[i]});
+        }
+        if (empty_build) {
+            EXPECT(got.empty());
+        } else {
+            EXPECT(got == want);
+            EXPECT(max_rows <= 5000 && out.size() > 3); // sliced output
+        }
+    }
+}
+
+// exchange: [BlocksSourceOp -> ExchangeSenderSinkOp] x 2 into 4 partitions (partition 1 local,
+// the others captured as remote tunnels), then [ExchangeReceiverSourceOp -> GetResultSinkOp];
+// every partition's rows equal hashPartitionBlock's for the same input.  Then the one-rank MPP
+// exchange (RCCL) path end to end.
+TEST(PipelineExchange) {
+    std::mt19937_64 rng(103);
+    const size_t n = 50000;
+    std::vector<int64_t> k(n), v(n);
+    for (size_t i = 0; i < n; ++i) {
+        k[i] = (int64_t)(rng() % 100000) - 50000;
+        v[i] = (int64_t)i;
+    }
+    DataType i64;
+    Block b{{makeColumn(ctx, i64, k.data(), n), i64, "k"}, {makeColumn(ctx, i64, v.data(), n), i64, "v"}};
+    std::vector<Block> want = hashPartitionBlock(ctx, b, {0}, 4);
+    std::vector<Block> blocks = splitBlocks(ctx, b, 5);
+    PipelineExecutorContext exec;
+    auto receiver = std::make_shared<ExchangeReceiver>();
+    std::vector<std::multiset<std::vector<std::string>>> remote(4);
+    auto tunnels = std::make_shared<MPPTunnelSet>(ctx, 4, 2, receiver, nullptr, 1, [&](uint32_t part, Block &&blk) {
+        for (const auto &row : rowSet(ctx, blk)) remote[part].insert(row);
+    });
+    std::vector<PipelineExecPtr> send;
+    for (size_t t = 0; t < 2; ++t) {
+        std::vector<Block> mine;
+        for (size_t i = t; i < blocks.size(); i += 2) mine.push_back(blocks[i]);
+        send.push_back(std::make_unique<PipelineExec>(std::make_unique<BlocksSourceOp>(exec, ctx, b, mine), TransformOps{},
+                                                      std::make_unique<ExchangeSenderSinkOp>(exec, ctx, tunnels,
+                                                                                             std::vector<size_t>{0})));
+    }
+    runPipelineExecs(exec, send);
+    EXPECT(receiver->finished());
+    std::multiset<std::vector<std::string>> local;
+    std::vector<PipelineExecPtr> recv;
+    recv.push_back(std::make_unique<PipelineExec>(
+        std::make_unique<ExchangeReceiverSourceOp>(exec, ctx, receiver, b), TransformOps{},
+        std::make_unique<GetResultSinkOp>(exec, ctx, [&](const Block &r) {
+            for (const auto &row : rowSet(ctx, r)) local.insert(row);
+        })));
+    runPipelineExecs(exec, recv);
+    EXPECT(local == rowSet(ctx, want[1]));
+    for (uint32_t p : {0u, 2u, 3u}) EXPECT(remote[p] == rowSet(ctx, want[p]));
+    // one-rank MPP exchange: everything comes back
+    uint8_t id[128];
+    check(tfg_comm_unique_id(id, sizeof(id)), "tfg_comm_unique_id");
+    MPPExchange mpp(ctx, 1, 0, id, sizeof(id));
+    auto recv1 = std::make_shared<ExchangeReceiver>();
+    auto t1 = std::make_shared<MPPTunnelSet>(ctx, 1, 1, recv1, &mpp);
+    std::vector<PipelineExecPtr> s1;
+    s1.push_back(std::make_unique<PipelineExec>(std::make_unique<BlocksSourceOp>(exec, ctx, b, blocks), TransformOps{},
+                                                std::make_unique<ExchangeSenderSinkOp>(exec, ctx, t1, std::vector<size_t>{0})));
+    runPipelineExecs(exec, s1);
+    Block all;
+    EXPECT(recv1->tryPop(all) && rowSet(ctx, all) == rowSet(ctx, b));
+}
+
+// PipelineExec's contract: a cancelled context stops execute() with CANCELLED (the reference's
+// SimpleOperatorTestRunner.cancel); an operator returning a status outside its contract throws;
+// a filter that empties a block asks for more input (NEED_INPUT) instead of passing it on.
+TEST(PipelineExecContract) {
+    DataType i64;
+    std::vector<int64_t> x = {1, 2, 3};
+    Block b{{makeColumn(ctx, i64, x.data(), 3), i64, "x"}};
+    {
+        PipelineExecutorContext exec;
+        PipelineExec pe(std::make_unique<BlocksSourceOp>(exec, ctx, b, std::vector<Block>{b}), TransformOps{},
+                        std::make_unique<GetResultSinkOp>(exec, ctx, [](const Block &) {}));
+        exec.cancel();
+        EXPECT(pe.execute() == OperatorStatus::CANCELLED);
+    }
+    {
+        PipelineExecutorContext exec;
+        auto expr = std::make_shared<ExpressionActions>(ctx);
+        expr->compare("x", TFG_GT, Field::Int64(10), "pred"); // filters every row
+        TransformOps tr;
+        tr.push_back(std::make_unique<FilterTransformOp>(exec, ctx, b.cloneEmpty(), expr, "pred"));
+        size_t seen = 0;
+        PipelineExec pe(std::make_unique<BlocksSourceOp>(exec, ctx, b, std::vector<Block>{b, b}), std::move(tr),
+                        std::make_unique<GetResultSinkOp>(exec, ctx, [&](const Block &) { ++seen; }));
+        EXPECT(pe.execute() == OperatorStatus::NEED_INPUT);
+        EXPECT(pe.execute() == OperatorStatus::NEED_INPUT);
+        EXPECT(pe.execute() == OperatorStatus::FINISHED); // the end-of-input block reaches the sink
+        EXPECT(seen == 0);
+    }
+    {
+        struct BadSource : SourceOp {
+            using SourceOp::SourceOp;
+            std::string getName() const override { return "BadSource"; }
+            OperatorStatus readImpl(Block &) override { return OperatorStatus::NEED_INPUT; }
+        };
+        PipelineExecutorContext exec;
+        PipelineExec pe(std::make_unique<BadSource>(exec, ctx), TransformOps{},
+                        std::make_unique<GetResultSinkOp>(exec, ctx, [](const Block &) {}));
+        bool threw = false;
+        try {
+            pe.execute();
+        } catch (const Exception &) {
+            threw = true;
+        }
+        EXPECT(threw);
+    }
+    { // a selective block into an operator that cannot take one
+        PipelineExecutorContext exec;
+        Block sb = b;
+        sb.info.selective = makeSelective(ctx, {0, 2});
+        PipelineExec pe(std::make_unique<BlocksSourceOp>(exec, ctx, b, std::vector<Block>{sb}), TransformOps{},
+                        std::make_unique<GetResultSinkOp>(exec, ctx, [](const Block &) {}));
+        bool threw = false;
+        try {
+            pe.execute();
+        } catch (const Exception &) {
+            threw = true;
+        }
+        EXPECT(threw);
+    }
+}
+
+// BlockInfo::selective through the exchange (gtest_mpp_exchange_writer.cpp:1147-1230): the
+// partitions of a selective block hold exactly the selected rows, each where a full-block
+// partition puts it (selective hash = full hash at the same rows), String and Nullable columns
+// included, through hashPartitionBlock and HashPartitionWriter
+TEST(SelectiveBlockPartition) {
+    std::mt19937_64 rng(104);
+    const size_t n = 4096, ns = 1024;
+    std::vector<int64_t> k(n), v(n);
+    std::vector<uint8_t> kn(n);
+    std::vector<std::string> s(n);
+    for (size_t i = 0; i < n; ++i) {
+        k[i] = (int64_t)(rng() % 3000);
+        v[i] = (int64_t)i;
+        kn[i] = rng() % 13 == 0;
+        s[i] = "s" + std::to_string(rng() % 500) + std::string(rng() % 20, 'x');
+    }
+    std::vector<uint64_t> sel;
+    for (size_t i = 0; i < n && sel.size() < ns; ++i)
+        if (rng() % 4 == 0 || n - i <= ns - sel.size()) sel.push_back(i);
+    DataType i64, i64n, str{DataType::TYPE_STRING};
+    i64n.nullable = true;
+    for (int with_string = 0; with_string < 2; ++with_string) {
+        g_current = with_string ? "string key" : "int key";
+        Block b{{makeColumn(ctx, i64n, k.data(), n, kn.data()), i64n, "k"}, {makeColumn(ctx, i64, v.data(), n), i64, "v"}};
+        if (with_string) b.insert({makeStringColumn(ctx, s), str, "s"});
+        const std::vector<size_t> keys = with_string ? std::vector<size_t>{2, 0} : std::vector<size_t>{0};
+        std::vector<Block> full = hashPartitionBlock(ctx, b, keys, 4);
+        Block sb = b;
+        sb.info.selective = makeSelective(ctx, sel);
+        std::vector<Block> part = hashPartitionBlock(ctx, sb, keys, 4);
+        std::set<int64_t> chosen(sel.begin(), sel.end());
+        size_t total = 0;
+        for (uint32_t p = 0; p < 4; ++p) {
+            auto fv = toHost<int64_t>(ctx, *full[p].getByName("v").column);
+            std::vector<int64_t> expect_v;
+            for (int64_t x : fv)
+                if (chosen.count(x)) expect_v.push_back(x); // same partition, same (stable) order
+            auto pv = toHost<int64_t>(ctx, *part[p].getByName("v").column);
+            EXPECT(pv == expect_v);
+            total += pv.size();
+            if (with_string) EXPECT(part[p].getByName("s").column->rows == pv.size());
+        }
+        EXPECT(total == ns);
+        // HashPartitionWriter: only the listed rows are sent
+        std::vector<std::vector<int64_t>> sent(4);
+        HashPartitionWriter w(ctx, keys, 4, [&](uint32_t p, Block &&blk) {
+            auto pv = toHost<int64_t>(ctx, *blk.getByName("v").column);
+            sent[p].insert(sent[p].end(), pv.begin(), pv.end());
+        });
+        w.write(sb);
+        w.flush();
+        for (uint32_t p = 0; p < 4; ++p) EXPECT(sent[p] == toHost<int64_t>(ctx, *part[p].getByName("v").column));
+    }
 }
 
 int main(int argc, char **argv) {

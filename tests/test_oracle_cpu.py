@@ -296,3 +296,27 @@ def test_decimal256_sums_exact(orc):
     for j in range(3):
         assert dict(zip(keys, [orc.limbs_to_int(x) for x in r["states"][j]])) == exp[j]
     assert max(abs(v) for v in exp[0].values()) >= 2**127
+
+
+def _float_golden(kind):
+    g = _load("float_weak_hash.json")[kind]
+    dt, ut = (np.float64, np.uint64) if kind == "float64" else (np.float32, np.uint32)
+    vals = np.array([int(e["bits"], 16) for e in g], dtype=ut).view(dt)
+    conv = np.array([int(e["u64"], 16) for e in g], dtype=np.uint64)
+    hashes = np.array([e["hash"] for e in g], dtype=np.uint32)
+    return vals, conv, hashes
+
+
+@pytest.mark.parametrize("kind", ["float64", "float32"])
+def test_float_weak_hash_golden(orc, kind):
+    """Float keys hash as intHashCRC32(UInt64(x)) with the reference build's x86-64 conversion
+    (NaN / +-inf / out of range -> 0x8000000000000000, negatives wrap), pinned by the fixture
+    tests/golden/make_float_hash.cpp generated with clang on x86-64."""
+    import ctypes
+    vals, conv, hashes = _float_golden(kind)
+    f = orc.lib().orc_float64_to_u64 if kind == "float64" else orc.lib().orc_float32_to_u64
+    f.restype = ctypes.c_uint64
+    f.argtypes = [ctypes.c_double if kind == "float64" else ctypes.c_float]
+    assert [f(float(x)) for x in vals] == [int(c) for c in conv]
+    h = orc.weak_hash([vals], [orc.FLOAT64 if kind == "float64" else orc.FLOAT32])
+    np.testing.assert_array_equal(h, hashes)

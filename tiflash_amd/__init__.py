@@ -302,24 +302,36 @@ def arith(ctx: Context, op: int, a, b, res_type: int, a_type=None, b_type=None, 
 
 
 # ---- a22-a24 hash / partition -----------------------------------------------------------------
-def weak_hash(ctx: Context, cols: Sequence, types: Optional[Sequence[int]] = None, nullmaps=None, h=None):
-    """WeakHash32 over key columns (IColumn::updateWeakHash32); returns an int32 tensor of u32 bits."""
+def weak_hash(ctx: Context, cols: Sequence, types: Optional[Sequence[int]] = None, nullmaps=None, h=None,
+              selective=None):
+    """WeakHash32 over key columns (IColumn::updateWeakHash32); returns an int32 tensor of u32 bits.
+    selective (int64 tensor of row ids, BlockInfo::selective): one hash per listed row."""
     import torch
-    n = cols[0].shape[0]
+    n = selective.shape[0] if selective is not None else cols[0].shape[0]
     if h is None:
         h = torch.empty(n, dtype=torch.int32, device=cols[0].device)
         check(lib().tfg_weak_hash_init(ctx.h, _p(h), ctypes.c_int64(n)))
     for j, c in enumerate(cols):
         t = types[j] if types else torch_type(c)
         nm = nullmaps[j] if nullmaps else None
-        check(lib().tfg_weak_hash_update(ctx.h, t, _p(c), _p(nm), ctypes.c_int64(n), _p(h)))
+        check(lib().tfg_weak_hash_update_selective(ctx.h, t, _p(c), _p(nm), _p(selective), ctypes.c_int64(n), _p(h)))
     return h
 
 
-def weak_hash_string(ctx: Context, chars, offsets, h, nullmap=None, collator=COLLATOR_NONE):
-    check(lib().tfg_weak_hash_update_string(ctx.h, _p(chars), _p(offsets), _p(nullmap),
-                                            ctypes.c_int64(offsets.shape[0]), collator, _p(h)))
+def weak_hash_string(ctx: Context, chars, offsets, h, nullmap=None, collator=COLLATOR_NONE, selective=None):
+    n = selective.shape[0] if selective is not None else offsets.shape[0]
+    check(lib().tfg_weak_hash_update_string_selective(ctx.h, _p(chars), _p(offsets), _p(nullmap), _p(selective),
+                                                      ctypes.c_int64(n), collator, _p(h)))
     return h
+
+
+def selective_perm(ctx: Context, selective, perm=None):
+    """tfg_selective_perm: out[i] = selective[perm[i]] (perm None: selective[i]) as int32 row ids."""
+    import torch
+    n = perm.shape[0] if perm is not None else selective.shape[0]
+    out = torch.empty(max(n, 1), dtype=torch.int32, device=selective.device)[:n]
+    check(lib().tfg_selective_perm(ctx.h, _p(selective), _p(perm), ctypes.c_int64(n), _p(out)))
+    return out
 
 
 def fill_selector(ctx: Context, h, part_num: int, fine_grained_stream_count: int = 0):

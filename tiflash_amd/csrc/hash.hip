@@ -22,12 +22,13 @@ __global__ void weak_hash_init_kernel(uint32_t *h, int64_t n) {
         h[i] = 0xFFFFFFFFu;
 }
 
-__global__ void __launch_bounds__(256) weak_hash_update_kernel(KeyCols k, int64_t n, uint32_t *h) {
+// sel (optional, BlockInfo::selective): h[i] hashes row sel[i] (ColumnVector.cpp:500-535)
+__global__ void __launch_bounds__(256) weak_hash_update_kernel(KeyCols k, const uint64_t *sel, int64_t n, uint32_t *h) {
     __shared__ uint32_t crc[8][256];
     load_crc_lds(crc);
     __syncthreads();
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        h[i] = hash_key_row(crc, k, i, h[i]);
+        h[i] = hash_key_row(crc, k, sel ? (int64_t)sel[i] : i, h[i]);
 }
 
 // ::updateWeakHash32(bytes) (Hash.h:148-214): 8-byte words, then a length-tagged tail.
@@ -61,15 +62,16 @@ __device__ uint32_t weak_hash_bytes(const uint32_t (*t)[256], const uint8_t *pos
 }
 
 __global__ void __launch_bounds__(256) weak_hash_string_kernel(const uint8_t *chars, const uint64_t *offsets,
-                                                              const uint8_t *nullmap, int64_t n, int collator,
-                                                              uint32_t *h) {
+                                                              const uint8_t *nullmap, const uint64_t *sel, int64_t n,
+                                                              int collator, uint32_t *h) {
     __shared__ uint32_t crc[8][256];
     load_crc_lds(crc);
     __syncthreads();
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        if (nullmap && nullmap[i]) continue;
-        const uint64_t prev = i ? offsets[i - 1] : 0;
-        uint64_t len = offsets[i] - prev - 1; // size - 1: the trailing '\0' is excluded
+        const int64_t r = sel ? (int64_t)sel[i] : i; // ColumnString.cpp:1256-1294 (selective rows)
+        if (nullmap && nullmap[r]) continue;
+        const uint64_t prev = r ? offsets[r - 1] : 0;
+        uint64_t len = offsets[r] - prev - 1; // size - 1: the trailing '\0' is excluded
         const uint8_t *s = chars + prev;
         if (collator == TFG_COLLATOR_BIN_PADDING)
             while (len > 0 && s[len - 1] == ' ') --len;
@@ -83,6 +85,13 @@ __global__ void fill_selector_kernel(const uint32_t *h, int64_t n, uint32_t part
         if (fgs) s = s * fgs + h[i] % fgs;
         sel[i] = (uint32_t)s;
     }
+}
+
+// out[i] = selective[perm[i]] (perm null: selective[i]): the partition permutation of the
+// selective rows mapped back to block rows (IColumn::scatter with a BlockSelective)
+__global__ void selective_perm_kernel(const uint64_t *sel, const uint32_t *perm, int64_t n, uint32_t *out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = (uint32_t)sel[perm ? perm[i] : i];
 }
 
 struct alignas(16) Bytes32 { // Decimal256 values
@@ -110,8 +119,7 @@ static int make_keycols(int nkeys, const int *idx, const int *types, const void 
     for (int j = 0; j < nkeys; ++j) {
         int c = idx ? idx[j] : j;
         int t = types[c];
-        TFG_CHECK(!is_float_type(t) && type_width(t) > 0 && type_width(t) <= 16, TFG_ERR_ILLEGAL_TYPE,
-                  "weak hash of type %d is not supported (float keys hash implementation-defined values)", t);
+        TFG_CHECK(type_width(t) > 0 && type_width(t) <= 16, TFG_ERR_ILLEGAL_TYPE, "weak hash of type %d is not supported", t);
         k.col[j] = cols[c];
         k.nullmap[j] = nullmaps ? nullmaps[c] : nullptr;
         k.type[j] = t;
@@ -134,6 +142,11 @@ int tfg_weak_hash_init(tfg_ctx *ctx, uint32_t *h, int64_t n) {
 }
 
 int tfg_weak_hash_update(tfg_ctx *ctx, int type, const void *col, const uint8_t *nullmap, int64_t n, uint32_t *h) {
+    return tfg_weak_hash_update_selective(ctx, type, col, nullmap, nullptr, n, h);
+}
+
+int tfg_weak_hash_update_selective(tfg_ctx *ctx, int type, const void *col, const uint8_t *nullmap,
+                                   const uint64_t *selective, int64_t n, uint32_t *h) {
     TFG_CHECK(ctx && (n == 0 || (col && h)), TFG_ERR_INVALID_ARG, "null argument");
     KeyCols k{};
     const void *cols[1] = {col};
@@ -142,7 +155,8 @@ int tfg_weak_hash_update(tfg_ctx *ctx, int type, const void *col, const uint8_t 
     if (int rc = make_keycols(1, nullptr, types, cols, nms, k)) return rc;
     if (n <= 0) return TFG_OK;
     { ProfScope _ps(ctx, "hash.weak");
-    hipLaunchKernelGGL(weak_hash_update_kernel, dim3(stream_grid(n, 256, 4096)), dim3(256), 0, ctx->stream, k, n, h);
+    hipLaunchKernelGGL(weak_hash_update_kernel, dim3(stream_grid(n, 256, 4096)), dim3(256), 0, ctx->stream, k, selective,
+                       n, h);
     }
     TFG_LAUNCH_CHECK();
     return TFG_OK;
@@ -150,12 +164,27 @@ int tfg_weak_hash_update(tfg_ctx *ctx, int type, const void *col, const uint8_t 
 
 int tfg_weak_hash_update_string(tfg_ctx *ctx, const uint8_t *chars, const uint64_t *offsets, const uint8_t *nullmap,
                                 int64_t n, int collator, uint32_t *h) {
+    return tfg_weak_hash_update_string_selective(ctx, chars, offsets, nullmap, nullptr, n, collator, h);
+}
+
+int tfg_weak_hash_update_string_selective(tfg_ctx *ctx, const uint8_t *chars, const uint64_t *offsets,
+                                          const uint8_t *nullmap, const uint64_t *selective, int64_t n, int collator,
+                                          uint32_t *h) {
     TFG_CHECK(ctx && (n == 0 || (chars && offsets && h)), TFG_ERR_INVALID_ARG, "null argument");
     TFG_CHECK(collator >= TFG_COLLATOR_NONE && collator <= TFG_COLLATOR_BIN_PADDING, TFG_ERR_NOT_IMPLEMENTED,
               "collator %d not supported", collator);
     if (n <= 0) return TFG_OK;
     hipLaunchKernelGGL(weak_hash_string_kernel, dim3(stream_grid(n, 256, 4096)), dim3(256), 0, ctx->stream, chars,
-                       offsets, nullmap, n, collator, h);
+                       offsets, nullmap, selective, n, collator, h);
+    TFG_LAUNCH_CHECK();
+    return TFG_OK;
+}
+
+int tfg_selective_perm(tfg_ctx *ctx, const uint64_t *selective, const uint32_t *perm, int64_t n, uint32_t *out_perm) {
+    TFG_CHECK(ctx && (n == 0 || (selective && out_perm)), TFG_ERR_INVALID_ARG, "null argument");
+    if (n <= 0) return TFG_OK;
+    hipLaunchKernelGGL(selective_perm_kernel, dim3(stream_grid(n, 256, 4096)), dim3(256), 0, ctx->stream, selective, perm,
+                       n, out_perm);
     TFG_LAUNCH_CHECK();
     return TFG_OK;
 }

@@ -42,6 +42,19 @@ struct KeyCols {
     int nkeys;
 };
 
+// Float -> UInt64 as the reference's implicit conversion (intHashCRC32(UInt64, UInt32) called with
+// a Float, Columns/ColumnVector.cpp:528) compiles on x86-64 (clang, SSE4.2, no AVX-512):
+// cvttsd2si(x) | (cvttsd2si(x - 2^63) & (cvttsd2si(x) >> 63)), where cvttsd2si yields INT64_MIN
+// for NaN and out-of-range values.  Pinned by tests/golden/float_weak_hash.json.
+template <typename F> __device__ __forceinline__ int64_t cvtt_i64(F x) {
+    return (x >= (F)-9223372036854775808.0 && x < (F)9223372036854775808.0) ? (int64_t)x : INT64_MIN;
+}
+template <typename F> __device__ __forceinline__ uint64_t float_to_u64_x86(F x) {
+    const int64_t a = cvtt_i64<F>(x);
+    const int64_t b = cvtt_i64<F>(x - (F)9223372036854775808.0);
+    return (uint64_t)(a | (b & (a >> 63)));
+}
+
 // value of key column j at row r converted to the UInt64 the reference feeds to crc32q
 __device__ __forceinline__ uint32_t hash_key_row(const uint32_t (*t)[256], const KeyCols &k, int64_t r, uint32_t h) {
     for (int j = 0; j < k.nkeys; ++j) {
@@ -55,6 +68,8 @@ __device__ __forceinline__ uint32_t hash_key_row(const uint32_t (*t)[256], const
         case TFG_UINT8: h = crc32c_u64(t, h, (uint64_t)((const uint8_t *)c)[r]); break;
         case TFG_UINT16: h = crc32c_u64(t, h, (uint64_t)((const uint16_t *)c)[r]); break;
         case TFG_UINT32: h = crc32c_u64(t, h, (uint64_t)((const uint32_t *)c)[r]); break;
+        case TFG_FLOAT32: h = crc32c_u64(t, h, float_to_u64_x86(((const float *)c)[r])); break;
+        case TFG_FLOAT64: h = crc32c_u64(t, h, float_to_u64_x86(((const double *)c)[r])); break;
         case TFG_DECIMAL128: {
             const uint64_t *l = (const uint64_t *)c + 2 * r;
             h = crc32c_u64(t, h, l[0]);

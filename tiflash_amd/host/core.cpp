@@ -138,6 +138,14 @@ Block Block::cloneEmpty() const {
 }
 
 // ---------------------------------------------------------------- host <-> device
+BlockSelectivePtr makeSelective(Context &ctx, const std::vector<uint64_t> &rows) {
+    auto s = std::make_shared<BlockSelective>();
+    s->count = rows.size();
+    s->rows = std::make_shared<DeviceBuffer>(ctx, std::max<size_t>(rows.size(), 1) * 8);
+    if (!rows.empty()) check(tfg_upload(ctx.raw(), s->rows->data(), rows.data(), rows.size() * 8), "tfg_upload");
+    return s;
+}
+
 ColumnPtr makeColumn(Context &ctx, DataType type, const void *values, size_t rows, const uint8_t *nullmap) {
     if (type.isString()) throw Exception("use makeStringColumn", ErrorCodes::BAD_ARGUMENTS);
     auto c = std::make_shared<IColumn>();

@@ -49,7 +49,7 @@ Aggregator::Aggregator(Context &ctx, const Params &params) : ctx_(ctx), params_(
                                    (at.isDecimal() ? TFG_ARG_PREC(at.precision()) : 0)));
         arg_scales.push_back(at.scale);
     }
-    tfg_agg_params p{params_.bucket_bits, params_.expected_groups};
+    tfg_agg_params p{params_.bucket_bits, params_.expected_groups, 0};
     if (packed_) {
         std::vector<int> coll = params_.collators;
         coll.resize(params_.keys.size(), TFG_COLLATOR_NONE);
@@ -583,12 +583,16 @@ Block Join::joinBlock(const Block &probe_block) {
 }
 
 // ================================================================ partitioning / exchange
-// Blocks with String columns: weak hash column by column, fillSelector, the stable partition
-// permutation (IColumn::scatter's order), then every column gathered per partition.
+// Blocks with String columns or a selective row list: weak hash column by column (over the
+// selective rows only, HashBaseWriterHelper.cpp:110-130), fillSelector, the stable partition
+// permutation (IColumn::scatter's order), mapped back to block rows through the selective
+// list, then every column gathered per partition (:176-200).
 static std::vector<Block> hashPartitionBlockGather(Context &ctx, const Block &block, const std::vector<size_t> &key_ids,
                                                    uint32_t partition_num, const std::vector<int> &collators) {
-    const size_t n = block.rows();
-    DeviceBuffer h(ctx, std::max<size_t>(n, 1) * 4), sel(ctx, std::max<size_t>(n, 1) * 4),
+    const BlockSelectivePtr &selp = block.info.selective;
+    const uint64_t *sel = selp ? selp->data() : nullptr;
+    const size_t n = selp ? selp->size() : block.rows();
+    DeviceBuffer h(ctx, std::max<size_t>(n, 1) * 4), selector(ctx, std::max<size_t>(n, 1) * 4),
         perm(ctx, std::max<size_t>(n, 1) * 4), offs_dev(ctx, (partition_num + 1) * 8);
     std::vector<uint64_t> offs(partition_num + 1, 0);
     if (n) {
@@ -596,23 +600,27 @@ static std::vector<Block> hashPartitionBlockGather(Context &ctx, const Block &bl
         for (size_t k = 0; k < key_ids.size(); ++k) {
             ColumnPtr c = materialize(ctx, block.safeGetByPosition(key_ids[k]).column);
             if (c->type.isString())
-                check(tfg_weak_hash_update_string(ctx.raw(), (const uint8_t *)c->dataPtr(),
-                                                  (const uint64_t *)c->offsets->data(), c->nullPtr(), (int64_t)n,
-                                                  k < collators.size() ? collators[k] : TFG_COLLATOR_NONE,
-                                                  (uint32_t *)h.data()),
+                check(tfg_weak_hash_update_string_selective(ctx.raw(), (const uint8_t *)c->dataPtr(),
+                                                            (const uint64_t *)c->offsets->data(), c->nullPtr(), sel,
+                                                            (int64_t)n,
+                                                            k < collators.size() ? collators[k] : TFG_COLLATOR_NONE,
+                                                            (uint32_t *)h.data()),
                       "tfg_weak_hash_update_string");
             else
-                check(tfg_weak_hash_update(ctx.raw(), c->type.type, c->dataPtr(), c->nullPtr(), (int64_t)n,
-                                           (uint32_t *)h.data()),
+                check(tfg_weak_hash_update_selective(ctx.raw(), c->type.type, c->dataPtr(), c->nullPtr(), sel,
+                                                     (int64_t)n, (uint32_t *)h.data()),
                       "tfg_weak_hash_update");
         }
         check(tfg_fill_selector(ctx.raw(), (const uint32_t *)h.data(), (int64_t)n, partition_num, 0,
-                                (uint32_t *)sel.data()),
+                                (uint32_t *)selector.data()),
               "tfg_fill_selector");
     }
-    check(tfg_partition(ctx.raw(), (const uint32_t *)sel.data(), (int64_t)n, partition_num, (uint32_t *)perm.data(),
-                        (uint64_t *)offs_dev.data(), offs.data()),
+    check(tfg_partition(ctx.raw(), (const uint32_t *)selector.data(), (int64_t)n, partition_num,
+                        (uint32_t *)perm.data(), (uint64_t *)offs_dev.data(), offs.data()),
           "tfg_partition");
+    if (sel && n) // positions among the selective rows -> block rows
+        check(tfg_selective_perm(ctx.raw(), sel, (const uint32_t *)perm.data(), (int64_t)n, (uint32_t *)perm.data()),
+              "tfg_selective_perm");
     std::vector<Block> parts(partition_num);
     for (uint32_t p = 0; p < partition_num; ++p) {
         const uint32_t *pp = (const uint32_t *)perm.data() + offs[p];
@@ -628,6 +636,7 @@ static std::vector<Block> hashPartitionBlockGather(Context &ctx, const Block &bl
 
 std::vector<Block> hashPartitionBlock(Context &ctx, const Block &block, const std::vector<size_t> &key_ids,
                                       uint32_t partition_num, const std::vector<int> &collators) {
+    if (block.info.selective) return hashPartitionBlockGather(ctx, block, key_ids, partition_num, collators);
     for (const auto &c : block.getColumnsWithTypeAndName())
         if (c.type.isString()) return hashPartitionBlockGather(ctx, block, key_ids, partition_num, collators);
     const size_t n = block.rows();
@@ -693,6 +702,13 @@ HashPartitionWriter::HashPartitionWriter(Context &ctx, std::vector<size_t> parti
 
 void HashPartitionWriter::write(const Block &block) {
     if (!block || block.rows() == 0) return;
+    if (block.info.selective) { // only the listed rows travel (HashPartitionWriter.cpp:121-122, 159, 221)
+        flush();
+        if (block.info.selective->size() == 0) return;
+        std::vector<Block> parts = hashPartitionBlock(ctx_, block, partition_col_ids_, partition_num_, collators_);
+        for (uint32_t p = 0; p < partition_num_; ++p) sink_(p, std::move(parts[p]));
+        return;
+    }
     pending_.push_back(block);
     pending_rows_ += block.rows();
     if ((int64_t)pending_rows_ >= limit_) flush();
@@ -770,10 +786,15 @@ Block MPPExchange::exchange(const std::vector<Block> &partitions) {
     }
     Block out;
     for (size_t j = 0; j < proto.columns(); ++j) {
-        const DataType t = proto.safeGetByPosition(j).column->type;
+        // the schema type, shared by every rank, decides the planes: a rank whose Nullable column
+        // happens to carry no null map still sends a zero plane, so every rank issues the same
+        // sequence of collectives
+        const DataType t = proto.safeGetByPosition(j).type;
         if (t.isString()) throw Exception("exchanging String columns", ErrorCodes::NOT_IMPLEMENTED);
-        bool nullable = false;
-        for (const auto &b : partitions) nullable |= b.safeGetByPosition(j).column->nullmap != nullptr;
+        const bool nullable = t.nullable;
+        for (const auto &b : partitions)
+            if (b.safeGetByPosition(j).column->nullmap && !nullable)
+                throw Exception("null map on a column of non-Nullable type " + t.getName(), ErrorCodes::LOGICAL_ERROR);
         auto c = std::make_shared<IColumn>();
         c->type = t;
         c->type.nullable = nullable;

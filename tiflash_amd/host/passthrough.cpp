@@ -52,18 +52,29 @@ void AutoPassThroughHashAggContext::trySwitchBackAdjustState(size_t block_rows) 
     lookup_.reset();
 }
 
-// the map's keys as a join build side: a LeftOuterSemi probe then says "key is in the map"
+// the map's key tuples as a join build side: a LeftOuterSemi probe then says "key is in the
+// map".  One key: the single-key join (NULL keys are not inserted; the NULL group is tracked in
+// lookup_has_null_).  Several keys: the multi-key join on the full tuple under the aggregator's
+// collators; a tuple holding a NULL never matches, so such rows pass through (always safe: the
+// second stage merges them), and the map never grows in the Selective state.
 void AutoPassThroughHashAggContext::buildLookup() {
     Block keys = agg_.convertToBlock(true);
     Block kb;
-    const auto &k = keys.getByName(params_.keys[0]);
-    kb.insert(k);
-    lookup_ = std::make_unique<Join>(ctx_, JoinKind::LeftOuterSemi, params_.keys[0], params_.keys[0]);
+    for (const auto &name : params_.keys) kb.insert(keys.getByName(name));
+    if (params_.keys.size() == 1) {
+        lookup_ = std::make_unique<Join>(ctx_, JoinKind::LeftOuterSemi, params_.keys[0], params_.keys[0]);
+    } else {
+        std::vector<int> coll;
+        if (params_.collators.size() == params_.keys.size()) coll = params_.collators;
+        lookup_ = std::make_unique<Join>(ctx_, JoinKind::LeftOuterSemi, params_.keys, params_.keys,
+                                         (int64_t)kb.rows(), coll);
+    }
     lookup_->setMatchHelperName("__in_map");
     lookup_->insertFromBlock(kb); // NULL keys are not inserted: tracked separately
     lookup_->finishOneBuild();
     lookup_has_null_ = false;
-    if (k.column->nullmap) {
+    const auto &k = kb.getByName(params_.keys[0]);
+    if (params_.keys.size() == 1 && k.column->nullmap) {
         std::vector<uint8_t> nm = toHostNullMap(ctx_, *k.column);
         for (uint8_t x : nm) lookup_has_null_ |= x != 0;
     }
@@ -72,8 +83,10 @@ void AutoPassThroughHashAggContext::buildLookup() {
 Block AutoPassThroughHashAggContext::getPassThroughBlock(const Block &block) const {
     const size_t n = block.rows();
     Block out;
-    const auto &kc = block.getByName(params_.keys[0]);
-    out.insert({kc.column, kc.column->type, params_.keys[0]});
+    for (const auto &name : params_.keys) { // every GROUP BY key, as the second stage merges on the tuple
+        const auto &kc = block.getByName(name);
+        out.insert({kc.column, kc.column->type, name});
+    }
     for (size_t i = 0; i < params_.aggregates.size(); ++i) {
         const AggregateDescription &d = params_.aggregates[i];
         const DataType rt = header_.getByName(d.column_name).type;
@@ -164,15 +177,27 @@ void AutoPassThroughHashAggContext::onBlock(const Block &block, bool force_strea
         // not grow), the others pass through
         if (!lookup_) buildLookup();
         Block kb;
-        kb.insert(block.getByName(params_.keys[0]));
+        for (const auto &name : params_.keys) kb.insert(block.getByName(name));
         Block probed = lookup_->joinBlock(kb);
-        ColumnPtr m = probed.getByName("__in_map").column;
+        ColumnPtr m = materialize(ctx_, probed.getByName("__in_map").column);
         auto hit = std::make_shared<IColumn>();
         hit->type.type = TFG_UINT8;
         hit->rows = rows;
         hit->data = m->data;
+        if (m->nullmap) { // a NULL match (NULL in the probe tuple) is not a hit
+            auto h2 = std::make_shared<IColumn>(*hit);
+            h2->data = std::make_shared<DeviceBuffer>(ctx_, rows);
+            DeviceBuffer notnull(ctx_, std::max<size_t>(rows, 1));
+            check(tfg_mask_logic(ctx_.raw(), TFG_NOT, m->nullPtr(), nullptr, (int64_t)rows, (uint8_t *)notnull.data()),
+                  "tfg_mask_logic");
+            check(tfg_mask_logic(ctx_.raw(), TFG_AND, (const uint8_t *)hit->dataPtr(), (const uint8_t *)notnull.data(),
+                                 (int64_t)rows, (uint8_t *)h2->data->data()),
+                  "tfg_mask_logic");
+            ctx_.sync();
+            hit = h2;
+        }
         ColumnPtr key = materialize(ctx_, block.getByName(params_.keys[0]).column);
-        if (lookup_has_null_ && key->nullmap) { // the NULL key's group is in the map too
+        if (params_.keys.size() == 1 && lookup_has_null_ && key->nullmap) { // the NULL key's group is in the map too
             auto h2 = std::make_shared<IColumn>(*hit);
             h2->data = std::make_shared<DeviceBuffer>(ctx_, rows);
             check(tfg_mask_logic(ctx_.raw(), TFG_OR, (const uint8_t *)hit->dataPtr(), key->nullPtr(), (int64_t)rows,

@@ -136,6 +136,24 @@ struct ColumnWithTypeAndName {
     std::string name;
 };
 
+// BlockInfo (Core/BlockInfo.h:25-57): bucket_num of a two-level bucket, and the selective row
+// list — when set, only the rows it lists take part (weak hash + scatter of the exchange,
+// HashBaseWriterHelper.cpp:110-260); produced by auto pass-through aggregation.  Here the list
+// is a device array of UInt64 row ids.
+struct BlockSelective {
+    DeviceBufferPtr rows; // count x UInt64 row ids (device)
+    size_t count = 0;
+    size_t size() const { return count; }
+    const uint64_t *data() const { return rows ? (const uint64_t *)rows->data() : nullptr; }
+};
+using BlockSelectivePtr = std::shared_ptr<BlockSelective>;
+BlockSelectivePtr makeSelective(Context &ctx, const std::vector<uint64_t> &rows);
+
+struct BlockInfo {
+    int32_t bucket_num = -1;
+    BlockSelectivePtr selective;
+};
+
 class Block {
 public:
     Block() = default;
@@ -155,6 +173,7 @@ public:
     void clear() { data_.clear(); }
     explicit operator bool() const { return !data_.empty(); }
     const std::vector<ColumnWithTypeAndName> &getColumnsWithTypeAndName() const { return data_; }
+    BlockInfo info;
 
 private:
     std::vector<ColumnWithTypeAndName> data_;
