@@ -126,6 +126,16 @@ def load_pmc_traffic(kernel):
         return None
 
 
+def load_pmc_step(leg):
+    """HBM bytes per bench step of a leg from the same PMC passes (profiles/pmc_traffic.json)."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            return json.load(f).get("_per_step", {}).get(leg, {}).get("hbm_bytes")
+    except Exception:
+        return None
+
+
 def host_cores():
     """Host CPUs this process may use: affinity mask, capped by a cgroup CPU quota and by the
     OMP_NUM_THREADS the GPU box sets to its per-GPU CPU share."""
@@ -640,7 +650,11 @@ def main():
         line["roofline"] = rf
         line["pipeline_roofline"] = {"algorithmic_bytes_per_step": 24 * N, "achieved": round(24 * N / (ms * 1e-3) / 1e9, 1),
                                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                     "frac": round(24 * N / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+                                     "frac": round(24 * N / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                     "traffic": load_pmc_step("C2")}
+        if line["pipeline_roofline"]["traffic"]:
+            line["pipeline_roofline"]["traffic_over_algorithmic"] = round(
+                line["pipeline_roofline"]["traffic"] / (24 * N), 3)
         line["kernels_ms_per_step"] = {kname: round(v[0] / args.steps, 4) for kname, v in sorted(prof.items())}
 
     if world == 1 and not args.no_variants:

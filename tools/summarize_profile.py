@@ -1,17 +1,18 @@
 #!/usr/bin/env python3
-"""Turn a tools/profile.sh run (gpurun_out/prof_<tag>/) into the committed evidence under profiles/.
+"""Turn one tools/profile.sh run (gpurun_out/prof_<tag>/) into the committed evidence under profiles/.
 
 Outputs
-  profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary of the default bench command
-  profiles/<tag>_summary.md         per-kernel average duration + PMC bytes per launch, human-readable
-  profiles/pmc_traffic.json         HBM bytes per launch per pipeline kernel (bench.py's roofline.traffic)
+  profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary of the traced bench run
+  profiles/<tag>_summary.md         the commands that ran, per-kernel durations, PMC bytes per launch
+                                    and per bench step for each leg (C2, C3, C5, codec)
+  profiles/pmc_traffic.json         HBM bytes per launch per kernel (bench.py's roofline.traffic)
 
-HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_SIZE come from separate --pmc passes.
-FETCH_SIZE reports exactly half the bytes of wide coalesced streaming reads on gfx950 (the guide's
-HBM/rocprofv3 section), so it is doubled.  The factor was cross-checked on a kernel with a known
-byte count (agg.part.hist, 16 B per input row: measured 2.000, r01); when that kernel is in the
-run it is re-measured and reported next to the guide's factor.  WRITE_SIZE is used as reported
-(exact for 16-B/lane streaming stores, the record stores of the partition).
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_SIZE come from separate --pmc passes
+and are reported in KB.  FETCH_SIZE reports half the bytes of wide coalesced streaming reads on
+gfx950, so it is doubled; the factor is re-measured on agg.part.tiled, whose reads are the 24 B
+input rows plus nothing else (reported next to the guide's factor).  WRITE_SIZE is used as is.
+Dispatches are assigned to a bench leg by the most recent leg-specific kernel before them (legs
+run one after another), so shared kernels (scan, compact, result, gather) land in their leg.
 """
 import argparse
 import collections
@@ -23,27 +24,36 @@ import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-# demangled kernel name -> pipeline scope name used by bench.py / the library profiler
+# demangled name -> short name (first match wins)
 NAME_MAP = [
+    (r"agg_fused_kernel", "agg.fused"),
+    (r"part_hist_kernel<tfg::SelBucket", "agg.part.hist"),
+    (r"part_scatter_staged_kernel<tfg::SelBucket.*true, true>", "agg.part.tiled"),
+    (r"part_scatter.*<tfg::SelBucket", "agg.part.scatter"),
+    (r"agg_bucket_tiled_kernel", "agg.bucket.tiled"),
     (r"part_hist_kernel<tfg::SelWide", "agg.wide.part.hist"),
     (r"part_scatter.*<tfg::SelWide", "agg.wide.part.scatter"),
     (r"agg_bucket_kernel<tfg::WideOps", "agg.wide.bucket"),
-    (r"pack_keys_kernel", "agg.pack_keys"),
-    (r"part_hist_kernel<tfg::SelBucket", "agg.part.hist"),
-    (r"part_scatter_staged_kernel<tfg::SelBucket.*true, true>", "agg.part.tiled"),
-    (r"part_scatter_staged_kernel<tfg::SelBucket", "agg.part.scatter"),
-    (r"part_scatter_kernel<tfg::SelBucket", "agg.part.scatter"),
     (r"agg_bucket_kernel", "agg.bucket"),
-    (r"agg_bucket_tiled_kernel", "agg.bucket"),
+    (r"pack_keys_kernel", "agg.pack_keys"),
+    (r"unpack_keys_kernel", "agg.unpack_keys"),
     (r"agg_compact_kernel", "agg.compact"),
     (r"agg_result_kernel", "agg.result"),
-    (r"scan_", "scan"),
     (r"part_hist_kernel<tfg::SelRec8", "part.hist.pass2"),
     (r"part_scatter_staged_kernel<tfg::SelRec8", "part.scatter.pass2"),
     (r"part_hist_kernel<tfg::SelJoin", "join.part.hist"),
     (r"part_scatter.*<tfg::SelJoin", "join.part.scatter"),
     (r"join_probe_kernel", "join.probe"),
+    (r"join_build", "join.build"),
     (r"gather_kernel", "gather"),
+    (r"scan_", "scan"),
+]
+# leg-specific kernels (by short name or raw-name regex)
+LEGS = [
+    ("C2", r"^(agg\.fused|agg\.part\.(hist|tiled|scatter)|agg\.bucket\.tiled)$"),
+    ("C3", r"^(join\.|part\.(hist|scatter)\.pass2)"),
+    ("codec", r"tfg::str_|codec"),
+    ("C5", r"^(agg\.wide\.|agg\.(pack|unpack)_keys|agg\.bucket$)|wide_str"),
 ]
 
 
@@ -51,88 +61,152 @@ def short(name):
     for pat, s in NAME_MAP:
         if re.search(pat, name):
             return s
-    return name.split("(")[0][:60]
+    m = re.search(r"tfg::(\w+)", name)
+    return ("tfg::" + m.group(1)) if m else name.split("(")[0][:60]
 
 
-def per_launch(path, counter):
-    """avg counter value per dispatch, per short kernel name (sums over XCD/instance rows)."""
-    tot = collections.defaultdict(float)
-    disp = collections.defaultdict(set)
+def leg_of(short_name, raw):
+    for leg, pat in LEGS:
+        if re.search(pat, short_name) or re.search(pat, raw):
+            return leg
+    return None
+
+
+def dispatches(path, counter=None):
+    """[(dispatch_id, short name, leg-marker or None, value)] in dispatch order; tfg kernels only."""
+    rows = {}
     with open(path) as f:
         for r in csv.DictReader(f):
-            if r["Counter_Name"] != counter:
+            name = r["Kernel_Name"]
+            if "tfg::" not in name:
                 continue
-            k = short(r["Kernel_Name"])
-            tot[k] += float(r["Counter_Value"])
-            disp[k].add(r["Dispatch_Id"])
-    return {k: tot[k] / max(len(disp[k]), 1) for k in tot}
+            if counter and r.get("Counter_Name") != counter:
+                continue
+            d = int(r["Dispatch_Id"])
+            val = float(r["Counter_Value"]) if counter else 0.0
+            s = short(name)
+            if d in rows:
+                rows[d][3] += val  # per-XCD / instance rows of one dispatch
+            else:
+                rows[d] = [d, s, leg_of(s, name), val]
+    out, leg = [], None
+    for d in sorted(rows):
+        _, s, marker, val = rows[d]
+        leg = marker or leg
+        out.append((d, s, leg or "C2", val))
+    return out
+
+
+def commands(src):
+    p = os.path.join(src, "commands.txt")
+    return open(p).read().strip().splitlines() if os.path.exists(p) else []
+
+
+def bench_line(src, log):
+    p = os.path.join(src, log)
+    if os.path.exists(p):
+        for line in open(p):
+            if line.startswith("{"):
+                return json.loads(line)
+    return None
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tag")
-    ap.add_argument("--rows", type=int, default=100_000_000)
-    ap.add_argument("--kept", type=int, default=0, help="kept rows (from the bench log if 0)")
     a = ap.parse_args()
     src = os.path.join(ROOT, "gpurun_out", f"prof_{a.tag}")
     out = os.path.join(ROOT, "profiles")
-    os.makedirs(out, exist_ok=True)
     stats = os.path.join(src, "kt", "run_kernel_stats.csv")
     shutil.copy(stats, os.path.join(out, f"{a.tag}_kernel_stats.csv"))
-    kept = a.kept
-    bench_line = None
-    for log in ("kt_bench.log", "fetch_bench.log"):
-        p = os.path.join(src, log)
-        if os.path.exists(p):
-            for line in open(p):
-                if line.startswith("{"):
-                    bench_line = bench_line or json.loads(line)
-    if not kept and bench_line:
-        kept = bench_line["config"]["kept_rows_per_gpu"]
-    fetch = per_launch(os.path.join(src, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
-    write = per_launch(os.path.join(src, "write", "run_counter_collection.csv"), "WRITE_SIZE")
-    # FETCH_SIZE / WRITE_SIZE are in KB (rocprofv3 derived counters)
-    fetch = {k: v * 1024 for k, v in fetch.items()}
-    write = {k: v * 1024 for k, v in write.items()}
+    cmds = commands(src)
+    kt_line = bench_line(src, "kt_bench.log")
+    pmc_line = bench_line(src, "fetch_bench.log") or kt_line
+    cfg = pmc_line["config"]
+    rows, kept, groups = cfg["rows_per_gpu"], cfg["kept_rows_per_gpu"], cfg["groups"]
+    runs = pmc_line["steps"] + pmc_line["warmup"]
+    fetch = dispatches(os.path.join(src, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+    write = dispatches(os.path.join(src, "write", "run_counter_collection.csv"), "WRITE_SIZE")
     factor = 2.0  # MI355X_MICROARCH.md: FETCH_SIZE = 1/2 of the bytes of wide streaming reads
-    measured = 16 * a.rows / fetch["agg.part.hist"] if fetch.get("agg.part.hist") else None
-    alg = {"agg.part.hist": 16 * a.rows, "agg.part.scatter": 24 * a.rows + 16 * kept,
-           "agg.part.tiled": 24 * a.rows + 16 * kept, "agg.bucket": 16 * kept}
+
+    def per_kernel(ds):  # (leg, short) -> (launches, total KB)
+        acc = collections.defaultdict(lambda: [0, 0.0])
+        for _, s, leg, v in ds:
+            acc[(leg, s)][0] += 1
+            acc[(leg, s)][1] += v
+        return acc
+
+    fk, wk = per_kernel(fetch), per_kernel(write)
+    t2 = fk.get(("C2", "agg.part.tiled"))
+    measured = (24 * rows) / (t2[1] * 1024 / t2[0]) if t2 else None
+    # algorithmic bytes per launch (SURVEY 8(d)) where a kernel carries a leg's whole input
+    alg = {("C2", "agg.part.tiled"): 24 * rows, ("C2", "agg.fused"): 24 * rows + 24 * groups,
+           ("C2", "agg.part.hist"): 16 * rows}
     traffic = {"_calibration": {"fetch_factor": factor, "basis": "MI355X_MICROARCH.md HBM section (x2 on gfx950)",
-                                "measured_on_agg_part_hist": round(measured, 4) if measured else None,
-                                "rows": a.rows, "kept": kept}}
-    for k in sorted(set(fetch) | set(write)):
-        fb = fetch.get(k, 0.0) * factor
-        wb = write.get(k, 0.0)
-        traffic[k] = {"fetch_bytes_raw": int(fetch.get(k, 0.0)), "fetch_bytes": int(fb), "write_bytes": int(wb),
-                      "hbm_bytes_per_launch": int(fb + wb), "algorithmic_bytes": alg.get(k)}
+                                "measured_on_agg_part_tiled": round(measured, 4) if measured else None,
+                                "rows": rows, "kept": kept, "groups": groups, "pmc_runs_per_leg": runs,
+                                "commands": cmds}}
+    legs = collections.defaultdict(float)
+    for key in sorted(set(fk) | set(wk)):
+        leg, s = key
+        fn, fkb = fk.get(key, [0, 0.0])
+        wn, wkb = wk.get(key, [0, 0.0])
+        fb = fkb * 1024 / max(fn, 1) * factor
+        wb = wkb * 1024 / max(wn, 1)
+        name = s if leg == "C2" else f"{leg}:{s}"
+        traffic[name] = {"launches": max(fn, wn), "fetch_bytes_raw": int(fkb * 1024 / max(fn, 1)),
+                         "fetch_bytes": int(fb), "write_bytes": int(wb), "hbm_bytes_per_launch": int(fb + wb),
+                         "algorithmic_bytes": alg.get(key)}
+        legs[leg] += (fkb * 1024 * factor + wkb * 1024) / runs
+    leg_alg = {"C2": 24 * rows + 24 * groups}
+    jl = (kt_line or {}).get("join_probe")
+    if jl:
+        leg_alg["C3"] = jl["pipeline_roofline"]["algorithmic_bytes_per_step"]
+    sl = (kt_line or {}).get("string_agg")
+    if sl:
+        leg_alg["C5"] = sl["pipeline_roofline"]["algorithmic_bytes_per_step"]
+    traffic["_per_step"] = {leg: {"hbm_bytes": int(b), "algorithmic_bytes": leg_alg.get(leg),
+                                  "traffic_over_algorithmic": round(b / leg_alg[leg], 3) if leg_alg.get(leg) else None}
+                            for leg, b in legs.items()}
     with open(os.path.join(out, "pmc_traffic.json"), "w") as f:
         json.dump(traffic, f, indent=1, sort_keys=True)
-    # duration table
-    rows = []
+    # ---- summary
+    srows = []
     with open(stats) as f:
         for r in csv.DictReader(f):
-            rows.append((short(r["Name"]), int(r["Calls"]), float(r["AverageNs"]) / 1e6, float(r["TotalDurationNs"]) / 1e6,
-                         float(r["Percentage"])))
+            srows.append((short(r["Name"]), r["Name"], int(r["Calls"]), float(r["AverageNs"]) / 1e6,
+                          float(r["TotalDurationNs"]) / 1e6, float(r["Percentage"])))
     with open(os.path.join(out, f"{a.tag}_summary.md"), "w") as f:
-        f.write(f"# rocprofv3 summary ({a.tag})\n\n")
-        f.write("Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu --steps 5 --warmup 2` "
-                "(tools/profile.sh); PMC from separate `--pmc FETCH_SIZE` / `--pmc WRITE_SIZE` passes "
-                "over `bench.py --no-cpu --no-join --steps 2 --warmup 1`.\n\n")
-        if bench_line:
-            f.write(f"Bench line of the traced run: value {bench_line['value']:.4g} {bench_line['unit']}, "
-                    f"{bench_line['ms_per_step']} ms/step.\n\n")
+        f.write(f"# rocprofv3 summary ({a.tag})\n\nCommands that ran (tools/profile.sh {a.tag}, verbatim):\n\n")
+        for c in cmds:
+            f.write(f"    {c}\n")
+        for nm, line in (("traced", kt_line), ("PMC (FETCH_SIZE pass)", pmc_line)):
+            if line:
+                f.write(f"\nBench line of the {nm} run: {line['value']:.4g} {line['unit']}, {line['ms_per_step']} ms/step")
+                if line.get("join_probe"):
+                    f.write(f"; join {line['join_probe']['value']:.4g} probe rows/s")
+                if line.get("string_agg"):
+                    f.write(f"; C5 {line['string_agg']['value']:.4g} rows/s")
+                f.write(".\n")
+        f.write("\n## Kernel trace (top 24 by total time; tfg:: kernels are this library's)\n\n")
         f.write("| kernel | calls | avg ms | total ms | % |\n|---|---|---|---|---|\n")
-        for name, calls, avg, tot, pct in sorted(rows, key=lambda x: -x[3])[:20]:
-            f.write(f"| {name} | {calls} | {avg:.4f} | {tot:.3f} | {pct:.1f} |\n")
-        f.write(f"\nFETCH_SIZE factor {factor} (guide); re-measured on agg.part.hist: {measured}\n\n")
-        f.write("| kernel | fetch B/launch (corrected) | write B/launch | HBM B/launch | algorithmic B |\n|---|---|---|---|---|\n")
+        for s, raw, calls, avg, tot, pct in sorted(srows, key=lambda x: -x[4])[:24]:
+            label = s if "tfg::" in raw else "(torch) " + s[:40]
+            f.write(f"| {label} | {calls} | {avg:.4f} | {tot:.3f} | {pct:.1f} |\n")
+        f.write(f"\n## HBM traffic (PMC)\n\nFETCH_SIZE factor {factor} (guide); re-measured on agg.part.tiled "
+                f"(24 B/row input only): {round(measured, 3) if measured else None}.\n\n")
+        f.write("| leg:kernel | launches | fetch B/launch (x2) | write B/launch | HBM B/launch | algorithmic B |\n"
+                "|---|---|---|---|---|---|\n")
         for k, v in sorted(traffic.items()):
             if k.startswith("_"):
                 continue
-            f.write(f"| {k} | {v['fetch_bytes']:.4g} | {v['write_bytes']:.4g} | {v['hbm_bytes_per_launch']:.4g} | "
-                    f"{v['algorithmic_bytes'] if v['algorithmic_bytes'] else '-'} |\n")
-    print(json.dumps({k: v for k, v in traffic.items() if k in alg or k.startswith("_")}, indent=1))
+            f.write(f"| {k} | {v['launches']} | {v['fetch_bytes']:.4g} | {v['write_bytes']:.4g} | "
+                    f"{v['hbm_bytes_per_launch']:.4g} | {v['algorithmic_bytes'] or '-'} |\n")
+        f.write(f"\nPer bench step (PMC run total / {runs} runs of each leg):\n\n"
+                "| leg | HBM bytes / step | algorithmic bytes / step | ratio |\n|---|---|---|---|\n")
+        for leg, v in sorted(traffic["_per_step"].items()):
+            f.write(f"| {leg} | {v['hbm_bytes']:.4g} | {v['algorithmic_bytes'] or '-'} | {v['traffic_over_algorithmic']} |\n")
+    print(json.dumps(traffic["_per_step"], indent=1))
 
 
 if __name__ == "__main__":
