@@ -137,6 +137,49 @@ def test_string_key_c5_shape_spills(tfa, ctx, dev, orc):
     check_same(got, ref.result())
 
 
+@pytest.mark.parametrize("collator,nullable,groups", [(0, False, 2_000_000), (2, True, 600_000)])
+def test_string_key_two_level_tiled(tfa, ctx, dev, orc, collator, nullable, groups):
+    """The wide tiled path at > 256 buckets: String keys packed while the tiled partition reads
+    them, a two-level tile sort (coarse buckets, then 64 fine buckets per coarse bucket), the
+    wide bucket kernel; two blocks, so the second one merges into the first one's groups.
+    Keys of 0-15 bytes with trailing spaces (BIN_PADDING folds them) and NULLs."""
+    rng = np.random.default_rng(12 + collator)
+    n = 4_000_000
+    ids = rng.integers(0, groups, n)
+    pad = rng.integers(0, 3, n) if collator == 2 else np.zeros(n, dtype=np.int64)
+    strs = [(b"k%d" % i)[: 1 + (i % 15)] + b" " * int(p) for i, p in zip(ids, pad)]
+    knull = (rng.random(n) < 0.02).astype(np.uint8) if nullable else None
+    d = rng.integers(-10**12, 10**12, n, dtype=np.int64)
+    aggs = [(tfa.AGG_SUM, tfa.prec(tfa.DECIMAL64, 15)), (tfa.AGG_COUNT_ALL, 0)]
+    agg = tfa.KeysAggregator(ctx, [tfa.STRING], aggs, collators=[collator], expected_groups=groups)
+    cut = n // 3
+    for lo, hi in ((0, cut), (cut, n)):
+        c2, o2 = str_col(strs[lo:hi])
+        agg.consume([to_dev((c2, o2), dev)], [to_dev(d[lo:hi], dev), None],
+                    key_nullmaps=[to_dev(knull[lo:hi], dev)] if nullable else None)
+    got = gpu_groups(agg.result(), [20])
+    chars, offs = str_col(strs)
+    ref = orc.AggKeys([orc.STRING], [(0, orc.prec(orc.DECIMAL64, 15)), (2, 0)], collators=[collator])
+    ref.consume([(chars, offs)], [d, None], key_nulls=[knull] if nullable else None)
+    check_same(got, ref.result())
+
+
+def test_fixed_keys_two_level_tiled(tfa, ctx, dev, orc):
+    """keys128 (Int32, Int64) at 1.5M groups through the packed-key wide tiled path, Float64 sum."""
+    rng = np.random.default_rng(13)
+    n, groups = 3_000_000, 1_500_000
+    gid = rng.integers(0, groups, n)
+    k1 = (gid % 1000).astype(np.int32)
+    k2 = (gid // 1000).astype(np.int64) * 7919
+    v = rng.integers(0, 1 << 20, n).astype(np.float64) / 256.0
+    aggs = [(tfa.AGG_SUM, tfa.FLOAT64), (tfa.AGG_COUNT_ALL, 0)]
+    agg = tfa.KeysAggregator(ctx, [tfa.INT32, tfa.INT64], aggs, expected_groups=groups)
+    agg.consume([to_dev(k1, dev), to_dev(k2, dev)], [to_dev(v, dev), None])
+    ref = orc.AggKeys([orc.INT32, orc.INT64], [(0, orc.FLOAT64), (2, 0)])
+    ref.consume([k1, k2], [v, None])
+    check_same(gpu_groups(agg.result(), [tfa.INT32, tfa.INT64]), ref.result())
+
+
 def test_string_key_lengths_and_empty(tfa, ctx, dev, orc):
     strs = [b"", b"a", b"ab", b"a\x00b"[:1], b"abcdefgh", b"abcdefghi", b"x" * 15, b" ", b"", b"abcdefgh"] * 300
     chars, offs = str_col(strs)

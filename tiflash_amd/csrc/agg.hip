@@ -236,19 +236,32 @@ struct Table {
         const uint32_t below = (uint32_t)(((key * 0x9E3779B97F4A7C15ull) << S.bbits) >> 32);
         return (unsigned)(((uint64_t)below * S.ngroups) >> 32);
     }
+    // A new key first reserves one of the maxfill cells (ctrl->used counts reservations, so
+    // concurrent inserts can never fill the table past maxfill: no headroom for in-flight
+    // inserts is needed), then claims its empty cell by CAS; a lost race returns the reservation.
+    __device__ __forceinline__ bool reserve(bool force) {
+        const unsigned n = atomicAdd(&ctrl->used, 1u);
+        if (force || n < (unsigned)S.maxfill) return true;
+        ctrl->full = 1;
+        atomicSub(&ctrl->used, 1u);
+        return false;
+    }
     __device__ __forceinline__ int try_claim(int cell, uint64_t key, bool force, bool &done) {
         // returns the cell when `key` now owns it, -1 otherwise (done = a definitive miss)
         if (!force && __hip_atomic_load(&ctrl->full, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
             done = true;
             return -1;
         }
+        if (!reserve(force)) {
+            done = true;
+            return -1;
+        }
         const uint64_t old = atomicCAS((unsigned long long *)&keys[cell], 0ull, (unsigned long long)key);
         if (old == 0) {
-            const unsigned n = atomicAdd(&ctrl->used, 1u) + 1;
-            if (n >= (unsigned)S.maxfill) ctrl->full = 1;
             done = true;
             return cell;
         }
+        atomicSub(&ctrl->used, 1u);
         if (old == key) {
             done = true;
             return cell;
@@ -395,8 +408,13 @@ struct Table {
                         live[u] = false;
                         continue;
                     }
+                    if (!reserve(force)) {
+                        live[u] = false;
+                        continue;
+                    }
                     const int c = (int)(grp[u] * GS + empty);
                     const uint64_t old = atomicCAS((unsigned long long *)&keys[c], 0ull, (unsigned long long)tag[u]);
+                    if (old != 0) atomicSub(&ctrl->used, 1u);
                     if (old == 0) {
                         uint4 q;
                         q.x = (unsigned)lo[u];
@@ -406,8 +424,11 @@ struct Table {
                         wk[c] = q;
                         __hip_atomic_store((unsigned long long *)&keys[c], (unsigned long long)(tag[u] | 1ull),
                                            __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        const unsigned n = atomicAdd(&ctrl->used, 1u) + 1;
-                        if (n >= (unsigned)S.maxfill) ctrl->full = 1;
+                        // read back: the loop's exit now depends on the publish, so it cannot be
+                        // deferred past the loop (see the exit below)
+                        if (__hip_atomic_load((unsigned long long *)&keys[c], __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_WORKGROUP) != (tag[u] | 1ull))
+                            any = true;
                         cell[u] = c;
                         live[u] = false;
                     } else {
@@ -418,7 +439,10 @@ struct Table {
                     any = true;
                 }
             }
-            if (!any) break;
+            // leave the loop together: a lane that exits waits at the loop's end for the whole
+            // wave, and the compiler may sink a claimant's publish store there (after the loop) —
+            // a lane of the same wave re-reading that pending cell would then spin forever
+            if (__ballot(any) == 0) break;
         }
     }
 
@@ -717,6 +741,49 @@ template <int NA, bool W = false> struct WideOps {
     }
 };
 
+// Wide keys on the tiled path: records {key lo, key hi, one word per summed argument}; the
+// value ops are FastOps' (1 count, 2 Int64 / UInt64 sum, 3 Float64 sum, 4 Decimal64 -> Decimal128)
+template <int A0, int A1, int A2> struct WideFastOps {
+    static constexpr int op(int i) { return i == 0 ? A0 : (i == 1 ? A1 : A2); }
+    static constexpr int NCOL = 2 + (A0 >= 2) + (A1 >= 2) + (A2 >= 2);
+    static constexpr bool WIDE = true;
+    static constexpr int pos(int i) { return 2 + (i > 0 && A0 >= 2) + (i > 1 && A1 >= 2); }
+    struct Row {
+        uint64_t key, khi;
+        uint64_t v[3];
+    };
+    const AggSpec &S;
+    int mode;
+    __device__ __forceinline__ void load(const RowsIO &rows, int64_t r, Row &v) const {
+        const uint64_t *rec = (const uint64_t *)rows.key + r * NCOL; // 8-byte aligned records
+        v.key = rec[0];
+        v.khi = rec[1];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+            if (op(i) >= 2) v.v[i] = rec[pos(i)];
+    }
+    __device__ __forceinline__ uint64_t key(const Row &v) const { return v.key; }
+    __device__ __forceinline__ uint64_t hi(const Row &v) const { return v.khi; }
+    __device__ __forceinline__ bool knull(const Row &) const { return false; }
+    __device__ __forceinline__ void add(Table &T, int cell, const Row &v) const {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            if (op(i) == 1) atomicAdd((unsigned long long *)T.cnt_cell(i, cell), 1ull);
+            if (op(i) == 2) atomicAdd((unsigned long long *)T.acc_cell(i, cell), (unsigned long long)v.v[i]);
+            if (op(i) == 3) atomicAdd((double *)T.acc_cell(i, cell), __longlong_as_double((long long)v.v[i]));
+            if (op(i) == 4) lds_add_i128(T.acc_cell(i, cell), v.v[i], (int64_t)v.v[i] < 0 ? ~0ull : 0ull);
+        }
+    }
+    __device__ __forceinline__ void store(const RowsIO &sp, int64_t w, const Row &v) const {
+        uint64_t *rec = (uint64_t *)sp.key + w * NCOL;
+        rec[0] = v.key;
+        rec[1] = v.khi;
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+            if (op(i) >= 2) rec[pos(i)] = v.v[i];
+    }
+};
+
 template <typename Ops, int BT>
 __global__ void __launch_bounds__(BT) agg_bucket_kernel(AggSpec S, RowsIO rows0, RowsIO rows1, int mode,
                                                         const uint64_t *stage_off, GroupsIO old,
@@ -840,9 +907,13 @@ __global__ void __launch_bounds__(BT) agg_bucket_kernel(AggSpec S, RowsIO rows0,
 // way; tmp_base[b] tells the compaction where.
 struct TiledIn {
     const uint64_t *rec;       // records of the tiled partition (Ops::NCOL words each)
-    const uint32_t *tile_hist; // [B][T]
+    const uint32_t *tile_hist; // [B][T]; two-level: [1 << fine_bits][T]
     int T;
     int TR;
+    // two-level partition (regroup_tiled_kernel): bucket b = coarse c << fine_bits | fine f reads
+    // row f of tile_hist over the tiles [tile_base[c], tile_base[c + 1]); null: one level
+    const uint32_t *tile_base;
+    int fine_bits;
     uint64_t *spill[2];        // two spill arenas of >= kept rows (records)
     unsigned long long *cursor; // [0] spill rows, [1] temp groups
 };
@@ -861,10 +932,12 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
     Table T(lds, S);
     const Ops ops{S, mode};
     const int b = blockIdx.x;
-    const uint32_t *col = tin.tile_hist + (size_t)b * tin.T;
+    const uint32_t *col = tin.tile_hist + (size_t)(tin.tile_base ? (b & ((1 << tin.fine_bits) - 1)) : b) * tin.T;
+    const int tbeg = tin.tile_base ? (int)tin.tile_base[b >> tin.fine_bits] : 0;
+    const int tend = tin.tile_base ? (int)tin.tile_base[(b >> tin.fine_bits) + 1] : tin.T;
     // rows of this bucket
     unsigned long long tot = 0;
-    for (int t = threadIdx.x; t < tin.T; t += BT) tot += col[t] >> 16;
+    for (int t = tbeg + (int)threadIdx.x; t < tend; t += BT) tot += col[t] >> 16;
     for (int d = 32; d > 0; d >>= 1) tot += __shfl_down(tot, d, 64);
     if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = tot;
     __syncthreads();
@@ -897,24 +970,37 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
         int64_t take = oe - old_cursor;
         if (take > S.maxfill) take = S.maxfill;
         for (int64_t g = old_cursor + threadIdx.x; g < old_cursor + take; g += BT) {
-            const int cell = T.find_or_insert(old.key[g], old.key_null[g] != 0, true, true);
+            int cell;
+            if constexpr (Ops::WIDE) {
+                const uint64_t lo[1] = {old.key[2 * g]}, hi[1] = {old.key[2 * g + 1]};
+                const uint64_t tg[1] = {wide_tag(lo[0], hi[0])};
+                const bool ok1[1] = {true};
+                int c1[1];
+                T.find_wide_multi<1>(lo, hi, tg, ok1, true, c1, true);
+                cell = c1[0];
+            } else {
+                cell = T.find_or_insert(old.key[g], old.key_null[g] != 0, true, true);
+            }
             T.add_group(cell, old, g);
         }
         old_cursor += take;
         const bool allow_insert = old_cursor >= oe;
         __syncthreads();
         // one step: up to RPT rows per thread (v / ok), lookup, add, retry misses after a barrier
-        auto step = [&](typename Ops::Row (&v)[RPT], bool (&ok)[RPT]) {
-            uint64_t ku[RPT];
+        auto step = [&](typename Ops::Row (&v)[RPT], bool (&ok)[RPT]) __attribute__((always_inline)) {
+            uint64_t ku[RPT], kh[RPT], tg[RPT];
             bool nu[RPT];
             int cells[RPT];
             bool miss[RPT];
 #pragma unroll
             for (int u = 0; u < RPT; ++u) {
                 ku[u] = ops.key(v[u]);
+                kh[u] = ops.hi(v[u]);
+                tg[u] = Ops::WIDE ? wide_tag(ku[u], kh[u]) : 0;
                 nu[u] = false;
             }
-            T.find_or_insert_multi<RPT>(ku, nu, ok, allow_insert, cells);
+            if constexpr (Ops::WIDE) T.find_wide_multi<RPT>(ku, kh, tg, ok, allow_insert, cells);
+            else T.find_or_insert_multi<RPT>(ku, nu, ok, allow_insert, cells);
 #pragma unroll
             for (int u = 0; u < RPT; ++u) {
                 miss[u] = false;
@@ -926,7 +1012,16 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
 #pragma unroll
             for (int u = 0; u < RPT; ++u) {
                 if (!miss[u]) continue;
-                const int cell = T.find_or_insert(ku[u], false, false, false);
+                int cell;
+                if constexpr (Ops::WIDE) {
+                    const uint64_t lo[1] = {ku[u]}, hi[1] = {kh[u]}, t1[1] = {tg[u]};
+                    const bool ok1[1] = {true};
+                    int c1[1];
+                    T.find_wide_multi<1>(lo, hi, t1, ok1, false, c1);
+                    cell = c1[0];
+                } else {
+                    cell = T.find_or_insert(ku[u], false, false, false);
+                }
                 if (cell >= 0) {
                     ops.add(T, cell, v[u]);
                 } else {
@@ -939,8 +1034,8 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
             // chunks of CH tiles: their runs are concatenated (prefix of the counts in LDS) and
             // row i of the chunk finds its tile by a log2(CH)-step binary search, so every thread
             // takes RPT rows per step whatever the run lengths
-            for (int t0 = 0; t0 < tin.T; t0 += CH) {
-                const uint32_t e = t0 + (int)threadIdx.x < tin.T ? col[t0 + threadIdx.x] : 0u;
+            for (int t0 = tbeg; t0 < tend; t0 += CH) {
+                const uint32_t e = t0 + (int)threadIdx.x < tend ? col[t0 + threadIdx.x] : 0u;
                 s_ent[threadIdx.x] = e;
                 { // block-wide exclusive scan of the run lengths
                     const uint32_t c = e >> 16;
@@ -962,7 +1057,7 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
                 // software pipeline: the next step's rows are loaded (address search + global
                 // loads issued) before this step's LDS probe / atomics, so HBM latency overlaps
                 // the table work instead of following it after every step barrier
-                auto load_step = [&](uint32_t base, typename Ops::Row (&v)[RPT], bool (&ok)[RPT]) {
+                auto load_step = [&](uint32_t base, typename Ops::Row (&v)[RPT], bool (&ok)[RPT]) __attribute__((always_inline)) {
 #pragma unroll
                     for (int u = 0; u < RPT; ++u) {
                         const uint32_t i = base + u * BT + threadIdx.x;
@@ -1230,6 +1325,247 @@ struct SelWide {
     }
     __device__ __forceinline__ uint32_t operator()(const uint32_t (*t)[256], int64_t r) const { return part(t, load(r), r); }
 };
+
+// Wide keys on the tiled path (consume_wide_tiled): the selector hands the 16-byte key to the
+// staged partition as record words 0 and 1; the radix is the Fibonacci radix of its tag.
+struct SelWide2 { // packed keys (keys128 after pack_keys_kernel)
+    const uint4 *key;
+    uint32_t shift;
+    static constexpr bool needs_crc = false;
+    static constexpr bool fib_radix = false;
+    static constexpr bool wide_key = true;
+    __device__ __forceinline__ Loaded load(int64_t r) const {
+        const uint4 q = key[r];
+        return Loaded{((uint64_t)q.y << 32) | q.x, 0u, ((uint64_t)q.w << 32) | q.z};
+    }
+    __device__ __forceinline__ uint32_t part(const uint32_t (*)[256], const Loaded &l, int64_t) const {
+        return fib_part(wide_tag(l.bits, l.hi), shift);
+    }
+    __device__ __forceinline__ uint32_t operator()(const uint32_t (*t)[256], int64_t r) const { return part(t, load(r), r); }
+};
+
+// key_string (HashMethodString with the collator's sort key, ColumnsHashing.h:179-241) packed
+// while it is loaded, exactly as pack_keys_kernel packs it: bytes 0-14 = the sort key (<= 15
+// bytes), byte 15 = its length, NULL = 0x80 in byte 15.  The bytes come from the aligned 8-byte
+// words that cover them (an aligned word holding a valid byte never leaves its page).
+struct SelWideStr {
+    const uint8_t *chars;
+    const uint64_t *offsets;
+    const uint8_t *nullmap;
+    int collator;
+    unsigned *err; // set when a sort key is longer than 15 bytes (serialized method needed)
+    uint32_t shift;
+    static constexpr bool needs_crc = false;
+    static constexpr bool fib_radix = false;
+    static constexpr bool wide_key = true;
+    __device__ __forceinline__ Loaded load(int64_t r) const {
+        uint64_t lo = 0, hi = 0;
+        if (nullmap && nullmap[r]) return Loaded{0, 0u, 0x80ull << 56};
+        const uint64_t s = r ? offsets[r - 1] : 0, e = offsets[r];
+        int64_t len = (int64_t)(e - s) - 1; // ColumnString rows end with '\0'
+        const uint8_t *c = chars + s;
+        if (collator == TFG_COLLATOR_BIN_PADDING)
+            while (len > 0 && c[len - 1] == ' ') --len; // BinCollatorSortKey<true>: right-trim
+        if (len > 15) {
+            atomicOr(err, 1u);
+            len = 15;
+        }
+        if (len > 0) {
+            const uintptr_t addr = (uintptr_t)c;
+            const uint64_t *w = (const uint64_t *)(addr & ~(uintptr_t)7);
+            const int sh = (int)(addr & 7) * 8;
+            const int nw = (int)(((addr + len - 1) >> 3) - (addr >> 3)) + 1; // 1..3 words
+            const uint64_t w0 = w[0], w1 = nw > 1 ? w[1] : 0ull, w2 = nw > 2 ? w[2] : 0ull;
+            lo = sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
+            hi = sh ? (w1 >> sh) | (w2 << (64 - sh)) : w1;
+            if (len < 8) {
+                lo &= (1ull << (len * 8)) - 1;
+                hi = 0;
+            } else {
+                hi = len == 8 ? 0ull : hi & ((1ull << ((len - 8) * 8)) - 1);
+            }
+        }
+        hi |= (uint64_t)len << 56;
+        return Loaded{lo, 0u, hi};
+    }
+    __device__ __forceinline__ uint32_t part(const uint32_t (*)[256], const Loaded &l, int64_t) const {
+        return fib_part(wide_tag(l.bits, l.hi), shift);
+    }
+    __device__ __forceinline__ uint32_t operator()(const uint32_t (*t)[256], int64_t r) const { return part(t, load(r), r); }
+};
+
+// ---------------------------------------------------------------- two-level tiled partition
+// Buckets past 256 (10M-group GROUP BYs) leave a one-level tiled partition with runs of < 1 row
+// per (bucket, tile).  Pass 1 tiles the rows by the top `coarse` bits of the radix; pass 2
+// (regroup_tiled_kernel) walks each coarse bucket's runs in order, cuts them into new tiles of
+// RG_TR rows that hold one coarse bucket each, and counting-sorts every tile by the next
+// `fine` = 6 bits: the bucket kernel of (coarse c, fine f) then reads runs of ~RG_TR / 64 rows
+// from the tiles [tile_base[c], tile_base[c + 1]).
+constexpr int RG_T = 1024;
+constexpr int RG_TR = 3072;
+constexpr int RG_FINE_BITS = 6;
+constexpr int RG_FINE = 1 << RG_FINE_BITS;
+
+// per coarse bucket: exclusive prefix of its run lengths over the pass-1 tiles (T1 + 1 entries)
+__global__ void __launch_bounds__(1024) regroup_prefix_kernel(const uint32_t *hist1, int T1, uint32_t *runpref) {
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t carry;
+    const int c = blockIdx.x;
+    const uint32_t *h = hist1 + (size_t)c * T1;
+    uint32_t *out = runpref + (size_t)c * (T1 + 1);
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (int t0 = 0; t0 < T1; t0 += 1024) {
+        const int t = t0 + (int)threadIdx.x;
+        const uint32_t v = t < T1 ? h[t] >> 16 : 0u;
+        uint32_t x = v;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d, 64);
+            if ((int)(threadIdx.x & 63) >= d) x += y;
+        }
+        if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = x;
+        __syncthreads();
+        uint32_t off = carry;
+        for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) off += wsum[w];
+        if (t < T1) out[t] = off + x - v;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry = off + x;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[T1] = carry;
+}
+
+// tile_base[c] = first pass-2 tile of coarse bucket c (one workgroup; B1 <= 1024)
+__global__ void regroup_tile_base_kernel(const uint32_t *runpref, int T1, int B1, uint32_t *tile_base) {
+    if (threadIdx.x != 0) return;
+    uint32_t acc = 0;
+    for (int c = 0; c < B1; ++c) {
+        tile_base[c] = acc;
+        acc += (runpref[(size_t)c * (T1 + 1) + T1] + RG_TR - 1) / RG_TR;
+    }
+    tile_base[B1] = acc;
+}
+
+// one workgroup per pass-2 tile (grid = an upper bound; tiles past tile_base[B1] exit)
+template <int NCOL>
+__global__ void __launch_bounds__(RG_T) regroup_tiled_kernel(const uint64_t *rec1, const uint32_t *hist1, int T1, int TR1,
+                                                             const uint32_t *runpref, const uint32_t *tile_base, int B1,
+                                                             uint32_t fine_shift, uint64_t *rec2, uint32_t *hist2, int T2) {
+    __shared__ uint64_t stage[RG_TR * NCOL];
+    __shared__ uint32_t rpref[RG_TR + 2], rent[RG_TR + 2];
+    __shared__ uint32_t fh[RG_FINE], fs[RG_FINE];
+    __shared__ int s_c, s_t0, s_m;
+    __shared__ uint32_t s_x0, s_x1;
+    const int k = blockIdx.x;
+    if (threadIdx.x == 0) {
+        int lo = 0, hi = B1; // coarse bucket of tile k: tile_base[c] <= k < tile_base[c + 1]
+        if ((uint32_t)k >= tile_base[B1]) {
+            s_c = -1;
+        } else {
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) / 2;
+                if (tile_base[mid] <= (uint32_t)k) lo = mid;
+                else hi = mid;
+            }
+            s_c = lo;
+            const uint32_t *pr = runpref + (size_t)lo * (T1 + 1);
+            const uint32_t n_c = pr[T1];
+            const uint32_t x0 = (uint32_t)(k - (int)tile_base[lo]) * RG_TR;
+            const uint32_t x1 = min(x0 + (uint32_t)RG_TR, n_c);
+            // runs covering [x0, x1): t0 = last tile with pr[t] <= x0, t1 = first with pr[t] >= x1
+            int a = 0, b = T1;
+            while (b - a > 1) {
+                const int mid = (a + b) / 2;
+                if (pr[mid] <= x0) a = mid;
+                else b = mid;
+            }
+            int lo2 = a, hi2 = T1; // t1 = first tile after a with pr[t] >= x1 (pr[T1] = n_c >= x1)
+            while (hi2 - lo2 > 1) {
+                const int mid = (lo2 + hi2) / 2;
+                if (pr[mid] >= x1) hi2 = mid;
+                else lo2 = mid;
+            }
+            const int t1 = hi2;
+            s_t0 = a;
+            s_m = t1 - a;
+            s_x0 = x0;
+            s_x1 = x1;
+        }
+    }
+    if (threadIdx.x < RG_FINE) fh[threadIdx.x] = 0;
+    __syncthreads();
+    const int c = s_c;
+    if (c < 0) return;
+    const int t0 = s_t0, m = s_m;
+    const uint32_t x0 = s_x0, x1 = s_x1;
+    const uint32_t *pr = runpref + (size_t)c * (T1 + 1);
+    const uint32_t *hc = hist1 + (size_t)c * T1;
+    constexpr int PER = RG_TR / RG_T;
+    uint64_t v[PER][NCOL];
+    uint32_t bq[PER];
+    int64_t row[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) row[q] = -1;
+    // the runs t0 .. t0 + m - 1 in windows of RG_TR (more than one only when empty runs of a
+    // sparse coarse bucket pile up): a row's run is the last j with rpref[j] <= x
+    for (int w0 = 0; w0 < m; w0 += RG_TR) {
+        const int wm = min(RG_TR, m - w0);
+        for (int j = threadIdx.x; j <= wm; j += RG_T) {
+            rpref[j] = pr[t0 + w0 + j];
+            rent[j] = j < wm ? hc[t0 + w0 + j] : 0u;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const uint32_t x = x0 + (uint32_t)(q * RG_T + threadIdx.x);
+            if (x >= x1 || row[q] >= 0 || x >= rpref[wm]) continue;
+            int lo = 0;
+            for (int st = 1 << 11; st > 0; st >>= 1)
+                if (lo + st < wm && rpref[lo + st] <= x) lo += st;
+            row[q] = (int64_t)(t0 + w0 + lo) * TR1 + (rent[lo] & 0xFFFFu) + (x - rpref[lo]);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        bq[q] = 0xFFFFFFFFu;
+        if (row[q] < 0) continue;
+        const uint64_t *r = rec1 + row[q] * NCOL;
+#pragma unroll
+        for (int w = 0; w < NCOL; ++w) v[q][w] = r[w];
+    }
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        if (row[q] < 0) continue;
+        const uint32_t f = fib_part(wide_tag(v[q][0], v[q][1]), fine_shift) & (RG_FINE - 1);
+        bq[q] = f | (atomicAdd(&fh[f], 1u) << 16);
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) { // one wave: exclusive scan of the 64 fine counts
+        const uint32_t cnt = fh[threadIdx.x];
+        uint32_t xs = cnt;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(xs, d, 64);
+            if ((int)threadIdx.x >= d) xs += y;
+        }
+        fs[threadIdx.x] = xs - cnt;
+        hist2[(size_t)threadIdx.x * T2 + k] = (xs - cnt) | (cnt << 16);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        if (bq[q] == 0xFFFFFFFFu) continue;
+        const uint32_t s = fs[bq[q] & 0xFFFFu] + (bq[q] >> 16);
+#pragma unroll
+        for (int w = 0; w < NCOL; ++w) stage[s * NCOL + w] = v[q][w];
+    }
+    __syncthreads();
+    const uint32_t rows = x1 - x0;
+    uint64_t *out = rec2 + (size_t)k * RG_TR * NCOL;
+    for (uint32_t i = threadIdx.x; i < rows * NCOL; i += RG_T) out[i] = stage[i];
+}
 
 // ---------------------------------------------------------------- wide-key packing
 // keys128 (Aggregator.cpp:394-537 chooses keys128 / nullable_keys128 for several fixed keys of
@@ -1584,6 +1920,171 @@ int consume_fast_tiled(tfg_agg *a, int fast, const RowPred &pred, const void *ke
 int consume_keyed(tfg_agg *a, int mode, const RowPred &pred, const void *keys, int key_width, const uint8_t *key_null,
                   const void *const *vals, const uint8_t *const *val_nulls, const uint64_t *const *val_cnts,
                   const uint64_t *given_off, int64_t n);
+
+// op-code signature of the wide tiled path: the FastOps codes with at most one summed argument
+// (records of 2-3 words: key lo, key hi, value), raw rows without NULL values
+int wide_fast_signature(const AggSpec &S, const uint8_t *const *val_nulls) {
+    if (S.key_width != 16 || S.n_aggs > 3) return 0;
+    int code = 0, sums = 0;
+    for (int i = 0; i < 3; ++i) {
+        int op = 0;
+        if (i < S.n_aggs) {
+            if (val_nulls && val_nulls[i]) return 0;
+            const int k = S.kind[i], t = S.src_type[i];
+            if (k == TFG_AGG_COUNT_ALL || k == TFG_AGG_COUNT) op = 1;
+            else if (S.acc[i] == ACC_I64 && (t == TFG_INT64 || t == TFG_UINT64)) op = 2;
+            else if (S.acc[i] == ACC_F64 && t == TFG_FLOAT64) op = 3;
+            else if (S.acc[i] == ACC_I128 && t == TFG_DECIMAL64) op = 4;
+            else return 0;
+            if (S.has_cnt[i] && op != 1) return 0;
+            sums += op >= 2;
+        }
+        code = code * 10 + op;
+    }
+    return sums <= 1 ? code : 0;
+}
+
+template <typename Ops>
+void launch_bucket_tiled(int B, const AggSpec &S, hipStream_t st, const TiledIn &tin, int mode, const GroupsIO &old,
+                         const uint64_t *ooff, const GroupsIO &tmp, uint64_t *new_cnt, uint64_t *tmp_base);
+
+// Wide keys (packed keys128 / key_string) of a wide fast signature over a tiled partition:
+// one level (B <= 256 buckets) as consume_fast_tiled, or two levels (coarse = B / 64 buckets in
+// pass 1, regroup_tiled_kernel into 64 fine buckets each); then the tiled bucket kernel with
+// WideFastOps, scan and compaction.  `sel` produces the 16-byte keys (SelWide2 over packed keys,
+// SelWideStr straight from the String column).  done = false: not applicable (general path).
+template <typename Sel>
+int consume_wide_tiled(tfg_agg *a, int code, Sel sel, const void *const *vals, int64_t n, unsigned *err, bool &done) {
+    done = false;
+    Ctx *ctx = a->ctx;
+    const AggSpec &S = a->S;
+    const uint32_t B = a->B;
+    const size_t n_old = a->n_groups;
+    if (n <= 0 || n >= (int64_t)0xFFFFFFFFll) return TFG_OK;
+    int ncol = 2;
+    PCols pc{};
+    pc.ncols = 2;
+    pc.width[0] = pc.width[1] = 8;
+    pc.key0 = 1;
+    pc.aos = 1;
+    for (int i = 0, c = code; i < S.n_aggs; ++i) {
+        const int op = (i == 0 ? c / 100 : i == 1 ? c / 10 : c) % 10;
+        if (op < 2) continue;
+        pc.in[pc.ncols] = vals[i];
+        pc.width[pc.ncols++] = 8;
+        ++ncol;
+    }
+    const uint32_t bbits = fib_shift(1) - fib_shift(B); // log2(B)
+    const bool two = bbits > 8;
+    const uint32_t B1 = two ? B >> RG_FINE_BITS : B;
+    TiledGeom tg{};
+    if (!make_tiled_geom(ctx, n, B1, pc, tg)) return TFG_OK;
+    const int T1 = tg.sg.T;
+    const int64_t T2 = two ? (n + RG_TR - 1) / RG_TR + B1 : 0;
+    Carver cv;
+    const size_t o_rec1 = cv.take<uint64_t>((size_t)tg.out_rows * ncol);
+    const size_t o_rec2 = cv.take<uint64_t>(two ? (size_t)T2 * RG_TR * ncol : 0);
+    const size_t o_sp1 = cv.take<uint64_t>((size_t)n * ncol); // spill arena 0 = pass-1 records (two levels)
+    const size_t o_sp0 = cv.take<uint64_t>(two ? 0 : (size_t)n * ncol);
+    const size_t o_hist1 = cv.take<uint32_t>((size_t)B1 * T1);
+    const size_t o_pref = cv.take<uint32_t>(two ? (size_t)B1 * (T1 + 1) : 0);
+    const size_t o_tbase = cv.take<uint32_t>(B1 + 1);
+    const size_t o_hist2 = cv.take<uint32_t>(two ? (size_t)RG_FINE * T2 : 0);
+    const size_t o_cur = cv.take<unsigned long long>(2);
+    const size_t o_new_cnt = cv.take<uint64_t>(B), o_new_off = cv.take<uint64_t>(B + 1), o_tb = cv.take<uint64_t>(B);
+    const size_t tmp_groups = n_old + (size_t)n;
+    const size_t o_tmpg = cv.take<uint8_t>(a->carve_groups(nullptr, tmp_groups, a->st[0]) + 256);
+    const size_t o_scan = cv.take<uint8_t>(scan_tmp_bytes(B + 1));
+    void *sp;
+    if (int rc = scratch_get(ctx, cv.off, &sp)) return rc;
+    char *sb = (char *)sp;
+    pc.out[0] = sb + o_rec1;
+    sel.shift = fib_shift(B1);
+    if (err) TFG_HIP(hipMemsetAsync(err, 0, sizeof(unsigned), ctx->stream));
+    if (int rc = run_partition_tiled(ctx, sel, RowPred{}, tg, pc, (uint32_t *)(sb + o_hist1), "agg.part.tiled"))
+        return rc;
+    if (err) { // a String key longer than 15 bytes: the serialized method, not this one
+        unsigned e = 0;
+        TFG_HIP(hipMemcpyAsync(&e, err, sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
+        TFG_HIP(hipStreamSynchronize(ctx->stream));
+        if (e) return fail(TFG_ERR_NOT_IMPLEMENTED, "String GROUP BY key longer than 15 bytes (serialized method)");
+    }
+    TiledIn tin{};
+    tin.rec = (const uint64_t *)(sb + o_rec1);
+    tin.tile_hist = (const uint32_t *)(sb + o_hist1);
+    tin.T = T1;
+    tin.TR = tg.sg.TR;
+    tin.spill[0] = (uint64_t *)(sb + (two ? o_rec1 : o_sp0));
+    tin.spill[1] = (uint64_t *)(sb + o_sp1);
+    if (two) {
+        uint32_t *pref = (uint32_t *)(sb + o_pref), *tbase = (uint32_t *)(sb + o_tbase);
+        uint32_t *hist2 = (uint32_t *)(sb + o_hist2);
+        ProfScope _ps(ctx, "agg.part.regroup");
+        hipLaunchKernelGGL(regroup_prefix_kernel, dim3(B1), dim3(1024), 0, ctx->stream, tin.tile_hist, T1, pref);
+        hipLaunchKernelGGL(regroup_tile_base_kernel, dim3(1), dim3(64), 0, ctx->stream, pref, T1, (int)B1, tbase);
+        const uint32_t fine_shift = fib_shift(B);
+        if (ncol == 3)
+            hipLaunchKernelGGL(regroup_tiled_kernel<3>, dim3((unsigned)T2), dim3(RG_T), 0, ctx->stream, tin.rec,
+                               tin.tile_hist, T1, tin.TR, pref, tbase, (int)B1, fine_shift, (uint64_t *)(sb + o_rec2),
+                               hist2, (int)T2);
+        else
+            hipLaunchKernelGGL(regroup_tiled_kernel<2>, dim3((unsigned)T2), dim3(RG_T), 0, ctx->stream, tin.rec,
+                               tin.tile_hist, T1, tin.TR, pref, tbase, (int)B1, fine_shift, (uint64_t *)(sb + o_rec2),
+                               hist2, (int)T2);
+        TFG_LAUNCH_CHECK();
+        tin.rec = (const uint64_t *)(sb + o_rec2);
+        tin.tile_hist = hist2;
+        tin.T = (int)T2;
+        tin.TR = RG_TR;
+        tin.tile_base = tbase;
+        tin.fine_bits = RG_FINE_BITS;
+    }
+    tin.cursor = (unsigned long long *)(sb + o_cur);
+    TFG_HIP(hipMemsetAsync(tin.cursor, 0, 16, ctx->stream));
+    GroupsIO tmp{};
+    a->carve_groups(sb + o_tmpg, tmp_groups, tmp);
+    uint64_t *new_cnt = (uint64_t *)(sb + o_new_cnt), *new_off = (uint64_t *)(sb + o_new_off);
+    uint64_t *tbase64 = (uint64_t *)(sb + o_tb);
+    const bool has_old = n_old > 0;
+    const GroupsIO old = a->st[a->cur];
+    const uint64_t *ooff = has_old ? a->bucket_off[a->cur] : (const uint64_t *)nullptr;
+    {
+        ProfScope _ps(ctx, "agg.bucket");
+#define TFG_WBUCKET(...) launch_bucket_tiled<__VA_ARGS__>(B, S, ctx->stream, tin, MODE_RAW, old, ooff, tmp, new_cnt, tbase64)
+        switch (code) {
+        case 410: TFG_WBUCKET(WideFastOps<4, 1, 0>); break;
+        case 310: TFG_WBUCKET(WideFastOps<3, 1, 0>); break;
+        case 210: TFG_WBUCKET(WideFastOps<2, 1, 0>); break;
+        case 140: TFG_WBUCKET(WideFastOps<1, 4, 0>); break;
+        case 130: TFG_WBUCKET(WideFastOps<1, 3, 0>); break;
+        case 120: TFG_WBUCKET(WideFastOps<1, 2, 0>); break;
+        case 400: TFG_WBUCKET(WideFastOps<4, 0, 0>); break;
+        case 300: TFG_WBUCKET(WideFastOps<3, 0, 0>); break;
+        case 200: TFG_WBUCKET(WideFastOps<2, 0, 0>); break;
+        case 100: TFG_WBUCKET(WideFastOps<1, 0, 0>); break;
+        default: return TFG_OK; // other signatures: the general path (nothing enqueued that matters)
+        }
+#undef TFG_WBUCKET
+    }
+    TFG_LAUNCH_CHECK();
+    if (int rc = exclusive_scan_u64(ctx, new_cnt, new_off, B, sb + o_scan)) return rc;
+    uint64_t total = 0;
+    if (int rc = read_back_u64(ctx, new_off + B, &total, 1)) return rc;
+    const int nxt = a->cur ^ 1;
+    if (int rc = a->ensure_state(nxt, total)) return rc;
+    if (!a->bucket_off[nxt]) TFG_HIP(hipMalloc(&a->bucket_off[nxt], (B + 1) * 8));
+    {
+        ProfScope _ps(ctx, "agg.compact");
+        hipLaunchKernelGGL(agg_compact_kernel, dim3(B), dim3(256), 0, ctx->stream, S, tmp, (const uint64_t *)nullptr,
+                           (const uint64_t *)nullptr, new_off, a->st[nxt], (const uint64_t *)tbase64);
+    }
+    TFG_LAUNCH_CHECK();
+    TFG_HIP(hipMemcpyAsync(a->bucket_off[nxt], new_off, (B + 1) * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    a->cur = nxt;
+    a->n_groups = total;
+    done = true;
+    return TFG_OK;
+}
 
 // The fused filter -> GROUP BY kernel (agg_fused.hip) for an empty aggregator of a fast
 // signature with FUSED_BUCKETS buckets: one launch, the bucket tables stay in LDS for the whole
@@ -1996,9 +2497,12 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
     const int64_t eg = (params && params->expected_groups > 0) ? params->expected_groups : (1 << 20);
     int bbits = params ? params->bucket_bits : 0;
     a->fused = params && params->fused;
+    // largest-table fill: inserts reserve cells (Table::reserve), so no headroom for in-flight
+    // inserts is needed; wide keys (48-byte cells with a Decimal128 sum) fill to 7/8
+    const int fill_big = wide ? 7 : 6;
     if (bbits <= 0) {
         const int64_t cells_max = LDS_TABLE_MAX / cell;
-        const int64_t fit = std::min<int64_t>(cells_max * 6 / 8, cells_max - BT_BIG - 8) * 5 / 6;
+        const int64_t fit = (cells_max * fill_big / 8) * 5 / 6;
         bbits = 8;
         while (bbits < 12 && ((int64_t)1 << bbits) * fit < eg) ++bbits;
     }
@@ -2011,14 +2515,13 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
     const int64_t per_bucket = eg / (int64_t)a->B + 1;
     const int64_t need = per_bucket * 5 / 4;
     int cap = 256;
-    while (cap < (1 << 16) && std::min(cap * 5 / 8, cap - BT - 8) < need) cap *= 2;
+    while (cap < (1 << 16) && cap * 5 / 8 < need) cap *= 2;
     int fill_num = 5;
     if ((size_t)(cap + 2) * cell > (size_t)LDS_TABLE_BYTES) {
         int c2 = 256;
-        while ((size_t)(c2 + 256 + 2) * cell <= (size_t)LDS_TABLE_MAX && std::min(c2 * 6 / 8, c2 - BT_BIG - 8) < need)
-            c2 += 256;
+        while ((size_t)(c2 + 256 + 2) * cell <= (size_t)LDS_TABLE_MAX && c2 * fill_big / 8 < need) c2 += 256;
         cap = c2;
-        fill_num = 6;
+        fill_num = fill_big;
     }
     S.cap = cap;
     S.bbits = a->nokey ? 0 : bbits;
@@ -2042,7 +2545,7 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
     S.lds_bytes = off + (int)sizeof(Ctrl) + 16;
     // one workgroup per CU anyway (LDS): make it 16 waves, and keep the in-flight insert headroom
     S.bt = S.lds_bytes > 80 * 1024 ? BT_BIG : BT;
-    S.maxfill = std::max(1, std::min(cap * fill_num / 8, cap - S.bt - 8));
+    S.maxfill = std::max(1, std::min(cap * fill_num / 8, cap - 8));
     if (a->nokey) {
         if (int rc = a->ensure_state(0, 1)) {
             delete a;
@@ -2262,7 +2765,24 @@ int tfg_agg_consume_keys(tfg_agg *a, const void *const *key_cols, const uint64_t
                                arg_nullmaps, mask, n);
     if (n <= 0) return n == 0 ? TFG_OK : fail(TFG_ERR_INVALID_ARG, "negative row count");
     if (int rc = set_device(a->ctx)) return rc;
+    // wide fast signatures: tiled partition of 16-byte keys (a String key packed as it is read)
+    const int code = mask ? 0 : wide_fast_signature(a->S, arg_nullmaps);
+    if (code && a->kp.kind == WK_STRING) {
+        TFG_CHECK(key_cols && key_cols[0] && key_offsets && key_offsets[0], TFG_ERR_INVALID_ARG,
+                  "String key needs its chars and offsets");
+        if (!a->pack_err) TFG_HIP(hipMalloc(&a->pack_err, sizeof(unsigned)));
+        SelWideStr sel{(const uint8_t *)key_cols[0], key_offsets[0], key_nullmaps ? key_nullmaps[0] : nullptr,
+                       a->kp.collator, a->pack_err, 0};
+        bool done = false;
+        if (int rc = consume_wide_tiled(a, code, sel, args, n, a->pack_err, done)) return rc;
+        if (done) return TFG_OK;
+    }
     if (int rc = pack_keys(a, key_cols, key_offsets, key_nullmaps, n)) return rc;
+    if (code) {
+        bool done = false;
+        if (int rc = consume_wide_tiled(a, code, SelWide2{(const uint4 *)a->pack_buf, 0}, args, n, nullptr, done)) return rc;
+        if (done) return TFG_OK;
+    }
     return tfg_agg_consume(a, a->pack_buf, nullptr, args, arg_nullmaps, mask, n);
 }
 

@@ -12,6 +12,8 @@
 // distinct partitions present in the wave), combines the 4 waves through LDS in wave order and
 // scatters every column to base + rank: the result is exactly the stable order.
 #pragma once
+#include <type_traits>
+
 #include "common.h"
 
 namespace tfg {
@@ -105,7 +107,13 @@ inline uint32_t fib_shift(uint32_t parts) { // parts is a power of two
 struct Loaded {
     uint64_t bits;
     uint32_t null;
+    uint64_t hi = 0; // wide-key selectors: the key's second word
 };
+
+// A selector with `static constexpr bool wide_key = true` loads a 16-byte key (Loaded::bits,
+// Loaded::hi) that becomes words 0 and 1 of the staged records.
+template <typename S, typename = void> struct SelWideKey : std::false_type {};
+template <typename S> struct SelWideKey<S, std::void_t<decltype(S::wide_key)>> : std::integral_constant<bool, S::wide_key> {};
 
 __device__ __forceinline__ uint64_t load_width(const void *p, int width, int64_t i) {
     switch (width) {
@@ -547,7 +555,8 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
         uint32_t bq[ST_MAXR]; // destination (low 16 bits) | rank inside the tile (high 16 bits)
         constexpr int VC = NC8 > 0 ? NC8 : 1;
         uint64_t v[VC][ST_MAXR]; // NC8 path: payload words, loaded before the ranks / scan
-        const int c0 = NC8 > 0 && cols.key0 ? 1 : 0;
+        constexpr bool WK = SelWideKey<Sel>::value && NC8 >= 2;
+        const int c0 = NC8 > 0 && cols.key0 ? (WK ? 2 : 1) : 0;
         constexpr int HB = ST_MAXR / 2; // two half-batches keep the live loaded values small
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -571,6 +580,7 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
                     if (b < P) bq[j] = b;
                 }
                 if constexpr (NC8 > 0) v[0][j] = kl[q].bits;
+                if constexpr (WK) v[VC > 1 ? 1 : 0][j] = kl[q].hi;
                 if constexpr (NC8 == 0) {
                     if (bq[j] != 0xFFFFFFFFu) bq[j] |= atomicAdd(&hist[bq[j]], 1u) << 16;
                 }
