@@ -923,6 +923,7 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
                                                               const uint64_t *old_off, GroupsIO out, uint64_t *out_cnt,
                                                               uint64_t *tmp_base) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
+    constexpr int RT = Ops::WIDE ? 2 : RPT; // rows per thread per step (wide rows: 2, fewer VGPRs)
     __shared__ unsigned long long s_red[BT / 64];
     __shared__ unsigned long long s_base[2];
     constexpr int CH = BT; // tiles per pass-0 chunk: one per thread
@@ -955,15 +956,18 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
     }
     __syncthreads();
     const uint64_t sbase = s_base[0], out_base = s_base[1];
-    RowsIO src{}, reg[2]{};
+    // the two spill regions as plain pointers, chosen per pass by value (an array of RowsIO
+    // indexed by the pass would live in scratch memory)
+    RowsIO src{};
     src.key = (void *)tin.rec;
-    for (int r = 0; r < 2; ++r) reg[r].key = tin.spill[r] + sbase * Ops::NCOL;
+    uint64_t *const reg0 = tin.spill[0] + sbase * Ops::NCOL, *const reg1 = tin.spill[1] + sbase * Ops::NCOL;
     int64_t old_cursor = os;
     int64_t pending = -1; // pass 0: the tile runs
     int pass = 0;
     while (pending != 0 || old_cursor < oe) {
-        const RowsIO &rows = reg[(pass + 1) & 1]; // pass p >= 1 reads region (p - 1) & 1
-        const RowsIO &spill = reg[pass & 1];      // ... and spills into region p & 1
+        RowsIO rows{}, spill{};
+        rows.key = (pass & 1) ? reg0 : reg1;  // pass p >= 1 reads region (p - 1) & 1
+        spill.key = (pass & 1) ? reg1 : reg0; // ... and spills into region p & 1
         T.clear();
         __syncthreads();
         if (threadIdx.x == 0) T.ctrl->spill_w = 0;
@@ -986,23 +990,23 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
         old_cursor += take;
         const bool allow_insert = old_cursor >= oe;
         __syncthreads();
-        // one step: up to RPT rows per thread (v / ok), lookup, add, retry misses after a barrier
-        auto step = [&](typename Ops::Row (&v)[RPT], bool (&ok)[RPT]) __attribute__((always_inline)) {
-            uint64_t ku[RPT], kh[RPT], tg[RPT];
-            bool nu[RPT];
-            int cells[RPT];
-            bool miss[RPT];
+        // one step: up to RT rows per thread (v / ok), lookup, add, retry misses after a barrier
+        auto step = [&](typename Ops::Row (&v)[RT], bool (&ok)[RT]) __attribute__((always_inline)) {
+            uint64_t ku[RT], kh[RT], tg[RT];
+            bool nu[RT];
+            int cells[RT];
+            bool miss[RT];
 #pragma unroll
-            for (int u = 0; u < RPT; ++u) {
+            for (int u = 0; u < RT; ++u) {
                 ku[u] = ops.key(v[u]);
                 kh[u] = ops.hi(v[u]);
                 tg[u] = Ops::WIDE ? wide_tag(ku[u], kh[u]) : 0;
                 nu[u] = false;
             }
-            if constexpr (Ops::WIDE) T.find_wide_multi<RPT>(ku, kh, tg, ok, allow_insert, cells);
-            else T.find_or_insert_multi<RPT>(ku, nu, ok, allow_insert, cells);
+            if constexpr (Ops::WIDE) T.find_wide_multi<RT>(ku, kh, tg, ok, allow_insert, cells);
+            else T.find_or_insert_multi<RT>(ku, nu, ok, allow_insert, cells);
 #pragma unroll
-            for (int u = 0; u < RPT; ++u) {
+            for (int u = 0; u < RT; ++u) {
                 miss[u] = false;
                 if (!ok[u]) continue;
                 if (cells[u] >= 0) ops.add(T, cells[u], v[u]);
@@ -1010,7 +1014,7 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
             }
             __syncthreads();
 #pragma unroll
-            for (int u = 0; u < RPT; ++u) {
+            for (int u = 0; u < RT; ++u) {
                 if (!miss[u]) continue;
                 int cell;
                 if constexpr (Ops::WIDE) {
@@ -1033,7 +1037,7 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
         if (pass == 0) {
             // chunks of CH tiles: their runs are concatenated (prefix of the counts in LDS) and
             // row i of the chunk finds its tile by a log2(CH)-step binary search, so every thread
-            // takes RPT rows per step whatever the run lengths
+            // takes RT rows per step whatever the run lengths
             for (int t0 = tbeg; t0 < tend; t0 += CH) {
                 const uint32_t e = t0 + (int)threadIdx.x < tend ? col[t0 + threadIdx.x] : 0u;
                 s_ent[threadIdx.x] = e;
@@ -1057,9 +1061,9 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
                 // software pipeline: the next step's rows are loaded (address search + global
                 // loads issued) before this step's LDS probe / atomics, so HBM latency overlaps
                 // the table work instead of following it after every step barrier
-                auto load_step = [&](uint32_t base, typename Ops::Row (&v)[RPT], bool (&ok)[RPT]) __attribute__((always_inline)) {
+                auto load_step = [&](uint32_t base, typename Ops::Row (&v)[RT], bool (&ok)[RT]) __attribute__((always_inline)) {
 #pragma unroll
-                    for (int u = 0; u < RPT; ++u) {
+                    for (int u = 0; u < RT; ++u) {
                         const uint32_t i = base + u * BT + threadIdx.x;
                         ok[u] = i < tot;
                         if (!ok[u]) continue;
@@ -1071,29 +1075,29 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
                         ops.load(src, r, v[u]);
                     }
                 };
-                typename Ops::Row vn[RPT];
-                bool okn[RPT];
+                typename Ops::Row vn[RT];
+                bool okn[RT];
                 if (tot > 0) load_step(0, vn, okn);
-                for (uint32_t base = 0; base < tot; base += BT * RPT) {
-                    typename Ops::Row v[RPT];
-                    bool ok[RPT];
+                for (uint32_t base = 0; base < tot; base += BT * RT) {
+                    typename Ops::Row v[RT];
+                    bool ok[RT];
 #pragma unroll
-                    for (int u = 0; u < RPT; ++u) {
+                    for (int u = 0; u < RT; ++u) {
                         v[u] = vn[u];
                         ok[u] = okn[u];
                     }
-                    if (base + BT * RPT < tot) load_step(base + BT * RPT, vn, okn);
+                    if (base + BT * RT < tot) load_step(base + BT * RT, vn, okn);
                     step(v, ok);
                 }
                 __syncthreads();
             }
         } else {
             const uint32_t npend = (uint32_t)pending;
-            for (uint32_t base = 0; base < npend; base += BT * RPT) {
-                typename Ops::Row v[RPT];
-                bool ok[RPT];
+            for (uint32_t base = 0; base < npend; base += BT * RT) {
+                typename Ops::Row v[RT];
+                bool ok[RT];
 #pragma unroll
-                for (int u = 0; u < RPT; ++u) {
+                for (int u = 0; u < RT; ++u) {
                     const uint32_t i = base + u * BT + threadIdx.x;
                     ok[u] = i < npend;
                     if (ok[u]) ops.load(rows, i, v[u]);
