@@ -710,6 +710,34 @@ def main():
                                   "frac": round(alg / (jms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
             "kernels_ms_per_step": {kname: round(vv[0] / args.steps, 4) for kname, vv in sorted(jprof.items())},
         }
+        # the same probe through JoinV2's tagged pointer table (no probe-side partitioning)
+        del j
+        j = tfa.Join(ctx, tfa.INT64, expected_build_rows=nb, v2=True, tagged=True)
+        tb0 = time.perf_counter()
+        j.build(bk, payload=[bpay])
+        j.finalize()
+        torch.cuda.synchronize()
+        build2_s = time.perf_counter() - tb0
+        for _ in range(args.warmup):
+            jstep()
+        torch.cuda.synchronize()
+        ctx.profile(True)
+        ctx.profile_reset()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            outj = jstep()
+        torch.cuda.synchronize()
+        jel2 = time.perf_counter() - t0
+        jprof2 = ctx.profile_read()
+        ctx.profile(False)
+        jms2 = jel2 / args.steps * 1e3
+        line["join_probe"]["join_v2"] = {
+            "metric": "probe rows/s through the JoinV2 tagged pointer table", "value": round(npr / (jel2 / args.steps), 1),
+            "ms_per_step": round(jms2, 3), "build_s": round(build2_s, 4), "matches": outj[0].shape[0],
+            "check_ok": outj[0].shape[0] == matches,
+            "pipeline_frac": round(alg / (jms2 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "kernels_ms_per_step": {kname: round(vv[0] / args.steps, 4) for kname, vv in sorted(jprof2.items())},
+        }
 
     if args.c4 == 1 or (args.c4 == -1 and world > 1):
         c4 = c4_leg(args, ctx, dev, world, rank)

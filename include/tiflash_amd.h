@@ -360,6 +360,15 @@ typedef struct tfg_join tfg_join;
  * the partitioning (0 = size from the first block). */
 int tfg_join_create(tfg_ctx *ctx, int key_type, int64_t expected_build_rows, tfg_join **out);
 int tfg_join_build(tfg_join *join, const void *keys, const uint8_t *key_nullmap, int64_t n);
+/* JoinV2 (Interpreters/JoinV2/HashJoinPointerTable.{h,cpp}, §8 f3): the same build / finalize /
+ * probe / probe_rows / destroy calls over a pointer table instead of radix partitions:
+ * 2^d chain heads, d from pointerTableCapacity = max(pow2ceil(2 * build rows), 1024), bucket =
+ * top d bits of the key's 64-bit hash, rows pushed on their chain by exchange; with
+ * TFG_JOIN_V2_TAGGED each head also carries the OR of its rows' low 16 hash bits (tagged
+ * pointer) so a probe skips chains that cannot hold its key.  Probing needs no partition pass.
+ * Same results as tfg_join_create (unordered). */
+#define TFG_JOIN_V2_TAGGED 1
+int tfg_join_create_v2(tfg_ctx *ctx, int key_type, int64_t expected_build_rows, int flags, tfg_join **out);
 int tfg_join_finalize(tfg_join *join);
 int tfg_join_destroy(tfg_join *join);
 /* Join::joinBlock (Join.cpp:1977 -> probeBlockImplTypeCase, JoinPartition.cpp:1465-1644):

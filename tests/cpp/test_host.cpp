@@ -1438,10 +1438,12 @@ TEST(PipelineHashJoin) {
     orc_join_destroy(oj);
     std::multiset<std::pair<int64_t, int64_t>> want;
     for (size_t i = 0; i < m; ++i) want.insert({pk[op[i]], bp[ob[i]]});
-    for (int empty_build = 0; empty_build < 2; ++empty_build) {
-        g_current = empty_build ? "empty build" : "join";
+    for (int variant = 0; variant < 3; ++variant) {
+        const int empty_build = variant == 1;
+        g_current = variant == 0 ? "join" : variant == 1 ? "empty build" : "JoinV2 pointer table";
         PipelineExecutorContext exec;
         auto join = std::make_shared<Join>(ctx, JoinKind::Inner, "pk", "bk", (int64_t)nb);
+        if (variant == 2) join->useJoinV2(true);
         auto jctx = std::make_shared<JoinBuildContext>(ctx, join, 2, build.cloneEmpty());
         std::vector<Block> bblocks = empty_build ? std::vector<Block>{} : splitBlocks(ctx, build, 4);
         std::vector<PipelineExecPtr> bpipe;

@@ -351,10 +351,15 @@ def _pairs(pi, bi):
     return sorted(zip(pi.tolist(), bi.tolist()))
 
 
+JOIN_VERSIONS = [dict(), dict(v2=True, tagged=False), dict(v2=True, tagged=True)]  # v1; JoinV2 pointer table
+JOIN_IDS = ["v1", "v2", "v2tagged"]
+
+
+@pytest.mark.parametrize("ver", JOIN_VERSIONS, ids=JOIN_IDS)
 @pytest.mark.parametrize("kind", [0, 1, 2, 3])
 @pytest.mark.parametrize("nb,np_,dup", [(0, 100, 1), (1, 1, 1), (1000, 5000, 1), (50_000, 400_000, 1),
                                         (20_000, 100_000, 3), (3000, 20_000, 2500)])
-def test_join_kinds(tfa, ctx, dev, orc, kind, nb, np_, dup):
+def test_join_kinds(tfa, ctx, dev, orc, kind, nb, np_, dup, ver):
     rng = np.random.default_rng(nb + np_ + kind)
     distinct = max(1, nb // dup)
     bk = rng.integers(-distinct, distinct, nb, dtype=np.int64) if dup > 1 else rng.permutation(nb).astype(np.int64) * 4 + 1
@@ -363,7 +368,7 @@ def test_join_kinds(tfa, ctx, dev, orc, kind, nb, np_, dup):
                   rng.integers(-2**40, 2**40, np_) * 4 + 3)
     pk[: min(np_, 3)] = [0, -1, 1][: min(np_, 3)]
     pnull = (rng.random(np_) < 0.02).astype(np.uint8)
-    j = tfa.Join(ctx, tfa.INT64)
+    j = tfa.Join(ctx, tfa.INT64, **ver)
     if nb:
         j.build(torch.from_numpy(bk).to(dev), key_nullmap=torch.from_numpy(bnull).to(dev))
     pi, bi = j.probe(torch.from_numpy(pk).to(dev), kind=kind, key_nullmap=torch.from_numpy(pnull).to(dev))
@@ -377,9 +382,10 @@ def test_join_kinds(tfa, ctx, dev, orc, kind, nb, np_, dup):
         assert _pairs(pi.cpu().numpy().view(np.uint32), got_b) == _pairs(epi, ebi)
 
 
-def test_join_multi_block_build_and_small_keys(tfa, ctx, dev, orc):
+@pytest.mark.parametrize("ver", JOIN_VERSIONS, ids=JOIN_IDS)
+def test_join_multi_block_build_and_small_keys(tfa, ctx, dev, orc, ver):
     rng = np.random.default_rng(4)
-    j = tfa.Join(ctx, tfa.INT32)
+    j = tfa.Join(ctx, tfa.INT32, **ver)
     ref = orc.JoinRef(orc.INT32)
     for n in (10, 0, 5000, 20_000):
         bk = rng.integers(-3000, 3000, n).astype(np.int32)
@@ -405,11 +411,12 @@ def test_join_capacity_retry(tfa, ctx, dev):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("ver", JOIN_VERSIONS, ids=JOIN_IDS)
 @pytest.mark.parametrize("kind", [0, 1, 2, 3])
 @pytest.mark.parametrize("key_as_payload", [True, False])
 @pytest.mark.parametrize("nb,np_,dup", [(0, 1000, 1), (3000, 50_000, 1), (20_000, 60_000, 30), (200_000, 300_000, 1),
                                         (9000, 2000, 9000)])
-def test_join_probe_rows_materialised(tfa, ctx, dev, orc, kind, key_as_payload, nb, np_, dup):
+def test_join_probe_rows_materialised(tfa, ctx, dev, orc, kind, key_as_payload, nb, np_, dup, ver):
     """Materialising probe (tfg_join_probe_rows): every output row carries the probe payloads and
     the matched build payload; compared as a multiset with the restatement's pairs."""
     rng = np.random.default_rng(nb + np_ + kind + 17 * key_as_payload)
@@ -422,7 +429,7 @@ def test_join_probe_rows_materialised(tfa, ctx, dev, orc, kind, key_as_payload, 
     pk[:3] = [0, -1, 1]
     pnull = (rng.random(np_) < 0.02).astype(np.uint8)
     ppay = rng.integers(-2**62, 2**62, np_, dtype=np.int64)
-    j = tfa.Join(ctx, tfa.INT64, expected_build_rows=nb)
+    j = tfa.Join(ctx, tfa.INT64, expected_build_rows=nb, **ver)
     half = nb // 2
     for lo, hi in ((0, half), (half, nb)):  # two build blocks
         if hi > lo:
@@ -479,6 +486,28 @@ def test_join_two_pass_partitions(tfa, ctx, dev, orc, with_payload):
         j.build(bkd)
         pi, bi = j.probe(pkd)
         assert _pairs(pi.cpu().numpy().view(np.uint32), bi.cpu().numpy().view(np.uint32)) == _pairs(epi, ebi)
+
+
+@pytest.mark.parametrize("tagged", [False, True])
+def test_join_v2_c3_shape(tfa, ctx, dev, orc, tagged):
+    """JoinV2 pointer table at C3's shape, scaled (2M build rows with unique keys k*4+1, 20M probe
+    rows half hits / half k*4+3 misses, Int64 payloads materialised): the multiset of (probe
+    payload, build payload) rows equals the v1 restatement's."""
+    rng = np.random.default_rng(57)
+    nb, np_ = 2_000_000, 20_000_000
+    bk = rng.permutation(nb).astype(np.int64) * 4 + 1
+    pk = np.where(rng.random(np_) < 0.5, bk[rng.integers(0, nb, np_)], rng.integers(0, 2**40, np_) * 4 + 3)
+    bkd, pkd = torch.from_numpy(bk).to(dev), torch.from_numpy(pk).to(dev)
+    j = tfa.Join(ctx, tfa.INT64, expected_build_rows=nb, v2=True, tagged=tagged)
+    j.build(bkd, payload=[bkd * 7 + 1])
+    op, ob, _ = j.probe_rows(pkd, [pkd], 1)
+    ref = orc.JoinRef(orc.INT64)
+    ref.build(bk)
+    epi, ebi = ref.probe(pk)
+    got = np.stack([op[0].cpu().numpy(), ob[0].cpu().numpy()], 1)
+    want = np.stack([pk[epi], bk[ebi] * 7 + 1], 1)
+    assert got.shape == want.shape
+    np.testing.assert_array_equal(got[np.lexsort(got.T[::-1])], want[np.lexsort(want.T[::-1])])
 
 
 def test_groupby_two_pass_buckets(tfa, ctx, dev, orc):

@@ -43,6 +43,7 @@ PLUS, MINUS, MULTIPLY = range(3)
 AND, OR, NOT = range(3)
 AGG_SUM, AGG_COUNT, AGG_COUNT_ALL = range(3)
 JOIN_INNER, JOIN_LEFT, JOIN_SEMI, JOIN_ANTI = range(4)
+JOIN_V2_TAGGED = 1  # tfg_join_create_v2 flags
 COLLATOR_NONE, COLLATOR_BINARY, COLLATOR_BIN_PADDING = range(3)
 
 WIDTH = {INT8: 1, INT16: 2, INT32: 4, INT64: 8, UINT8: 1, UINT16: 2, UINT32: 4, UINT64: 8,
@@ -557,10 +558,17 @@ class KeysAggregator(Aggregator):
 class Join:
     """tfg_join: hash join v1 semantics (strictness ALL) on one fixed-width key."""
 
-    def __init__(self, ctx: Context, key_type: int, expected_build_rows: int = 0):
+    def __init__(self, ctx: Context, key_type: int, expected_build_rows: int = 0, v2: bool = False,
+                 tagged: bool = True):
+        """v2: JoinV2's pointer table (tfg_join_create_v2; tagged = tagged heads) instead of the
+        radix-partitioned v1 table."""
         self.ctx = ctx
         h = ctypes.c_void_p()
-        check(lib().tfg_join_create(ctx.h, key_type, ctypes.c_int64(expected_build_rows), ctypes.byref(h)))
+        if v2:
+            check(lib().tfg_join_create_v2(ctx.h, key_type, ctypes.c_int64(expected_build_rows),
+                                           JOIN_V2_TAGGED if tagged else 0, ctypes.byref(h)))
+        else:
+            check(lib().tfg_join_create(ctx.h, key_type, ctypes.c_int64(expected_build_rows), ctypes.byref(h)))
         self.h = h
         ctx._children.add(self)
 

@@ -343,6 +343,153 @@ __global__ void join_mark_kernel(const uint32_t *probe_idx, const uint8_t *pass,
         if (!pass || pass[i]) flags[probe_idx[i]] = 1; // benign race: every writer stores 1
 }
 
+// ---------------------------------------------------------------- JoinV2 pointer table (§8 f3)
+// HashJoinPointerTable (Interpreters/JoinV2/HashJoinPointerTable.{h,cpp}): one table of 2^d
+// heads, d from pointerTableCapacity(rows) = max(pow2ceil(2 * rows), 1024); bucket = the top d
+// bits of the row's 64-bit hash; rows are pushed onto their bucket's chain by an exchange of the
+// head (the row keeps the old head as its next link).  A tagged head carries in its top 16 bits
+// the OR of (hash & 0xFFFF) of every row on the chain, so a probe whose 16 hash bits are not all
+// present skips the chain without touching it.  Here a head is (tag << 48) | (row + 1) and the
+// links are a row-indexed array; probing needs no partitioning pass.
+constexpr int V2_TAG_SHIFT = 48;
+constexpr uint64_t V2_ROW_MASK = (1ull << V2_TAG_SHIFT) - 1;
+
+__device__ __forceinline__ uint64_t v2_hash(uint64_t k) { // splitmix64 finaliser
+    k ^= k >> 30;
+    k *= 0xBF58476D1CE4E5B9ull;
+    k ^= k >> 27;
+    k *= 0x94D049BB133111EBull;
+    return k ^ (k >> 31);
+}
+
+// a chain link: the row's key and the next row (+ 1; 0 = end) in one 16-byte record, so every
+// step of a chain walk is a single load
+__global__ void join_v2_build_kernel(const uint64_t *keys, const uint8_t *nulls, int64_t n, uint64_t *heads,
+                                     uint32_t shift, int tagged, uint4 *link) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t key = keys[r];
+        if (nulls && nulls[r]) {
+            link[r] = make_uint4((unsigned)key, (unsigned)(key >> 32), 0u, 0u);
+            continue; // NULL keys never join (never on a chain)
+        }
+        const uint64_t h = v2_hash(key);
+        uint64_t *slot = heads + (h >> shift);
+        uint64_t old = atomicExch((unsigned long long *)slot, (unsigned long long)(r + 1));
+        if (tagged) { // insertRowToList + tag: the chain's tag bits, ours included, on the head
+            const uint64_t tag = (h & 0xFFFFull) | (old >> V2_TAG_SHIFT);
+            atomicOr((unsigned long long *)slot, (unsigned long long)(tag << V2_TAG_SHIFT));
+        }
+        link[r] = make_uint4((unsigned)key, (unsigned)(key >> 32), (unsigned)(old & V2_ROW_MASK), 0u);
+    }
+}
+
+struct V2Probe {
+    const uint4 *link; // {key, next} per build row
+    const uint64_t *heads;
+    uint32_t shift;
+    int tagged;
+    const void *pkeys;
+    int pwidth;
+    const uint8_t *pnull;
+    int64_t n;
+    int kind;
+    int pw, bw;                  // payload words out (0: row ids)
+    const uint64_t *ppay[JMAXW]; // probe payload columns (pw > 0)
+    const uint64_t *bpay[JMAXW]; // build payload columns (bw > 0)
+    void *out_p[JMAXW];
+    void *out_b[JMAXW];
+    uint8_t *out_bnull;
+    uint64_t capacity;
+    unsigned long long *cursor;
+};
+
+// the first build row of r's chain whose key equals `key` at or after link `row` (row + 1; 0 = end)
+// (returns the row + 1, and the link after it in *after)
+__device__ __forceinline__ uint32_t v2_next_match(const V2Probe &A, uint32_t row, uint64_t key, uint32_t &after) {
+    while (row) {
+        const uint4 l = A.link[row - 1];
+        if ((((uint64_t)l.y << 32) | l.x) == key) {
+            after = l.z;
+            return row;
+        }
+        row = l.z;
+    }
+    after = 0;
+    return 0;
+}
+
+// Each probe row counts its output rows (INNER: matches, LEFT: max(matches, 1), SEMI: matched,
+// ANTI: !matched), the wave reserves its slots with one atomic, then the rows walk their chains
+// again (now cache hits) writing probe row / build row outputs.
+__global__ void __launch_bounds__(256) join_v2_probe_kernel(V2Probe A) {
+    const int lane = threadIdx.x & 63;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < A.n; base += stride) {
+        const int64_t r = base + threadIdx.x;
+        const bool valid = r < A.n;
+        const bool isnull = valid && A.pnull && A.pnull[r];
+        uint64_t key = 0;
+        uint32_t head = 0;
+        if (valid && !isnull) {
+            key = jload_bits(A.pkeys, A.pwidth, r);
+            const uint64_t h = v2_hash(key);
+            const uint64_t e = A.heads[h >> A.shift];
+            const uint64_t t = h & 0xFFFFull;
+            if (!A.tagged || ((e >> V2_TAG_SHIFT) & t) == t) head = (uint32_t)(e & V2_ROW_MASK);
+        }
+        uint32_t m = 0, first = 0, after = 0;
+        for (uint32_t row = v2_next_match(A, head, key, after); row; row = v2_next_match(A, after, key, after)) {
+            if (!m) first = row;
+            ++m;
+            if (A.kind >= TFG_JOIN_SEMI) break; // SEMI / ANTI only need "any"
+        }
+        uint32_t e = 0;
+        if (valid) {
+            switch (A.kind) {
+            case TFG_JOIN_INNER: e = m; break;
+            case TFG_JOIN_LEFT: e = m ? m : 1; break;
+            case TFG_JOIN_SEMI: e = m ? 1 : 0; break;
+            default: e = m ? 0 : 1; break;
+            }
+        }
+        uint32_t inc = e; // wave-inclusive scan of the output counts
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(inc, d, 64);
+            if (lane >= d) inc += y;
+        }
+        unsigned long long wbase = 0;
+        if (lane == 63) wbase = atomicAdd(A.cursor, (unsigned long long)inc);
+        wbase = __shfl(wbase, 63, 64);
+        if (!e) continue;
+        uint64_t pos = wbase + inc - e;
+        auto emit = [&](uint32_t brow) __attribute__((always_inline)) { // brow: build row + 1, 0 = none
+            if (pos < A.capacity) {
+                if (A.pw == 0) {
+                    ((uint32_t *)A.out_p[0])[pos] = (uint32_t)r;
+                } else {
+                    for (int w = 0; w < A.pw; ++w) ((uint64_t *)A.out_p[w])[pos] = A.ppay[w][r];
+                }
+                if (A.out_bnull) A.out_bnull[pos] = brow == 0;
+                if (A.bw == 0) {
+                    if (A.out_b[0]) ((uint32_t *)A.out_b[0])[pos] = brow ? brow - 1 : 0xFFFFFFFFu;
+                } else if (A.out_b[0]) {
+                    for (int w = 0; w < A.bw; ++w) ((uint64_t *)A.out_b[w])[pos] = brow ? A.bpay[w][brow - 1] : 0ull;
+                }
+            }
+            ++pos;
+        };
+        if (m == 1 && A.kind <= TFG_JOIN_LEFT) {
+            emit(first); // one match (unique build keys): no second walk
+        } else if (A.kind == TFG_JOIN_INNER || (A.kind == TFG_JOIN_LEFT && m)) {
+            for (uint32_t row = v2_next_match(A, head, key, after); row; row = v2_next_match(A, after, key, after))
+                emit(row);
+        } else {
+            emit(0); // LEFT without a match / SEMI / ANTI: the probe row alone
+        }
+    }
+}
+
 } // namespace tfg
 
 using namespace tfg;
@@ -365,6 +512,13 @@ struct tfg_join {
     uint32_t *brows = nullptr;
     uint64_t *boff = nullptr;
     int64_t n_inserted = 0;
+    // JoinV2 pointer table (tfg_join_create_v2)
+    bool v2 = false;
+    bool tagged = false;
+    uint64_t *heads = nullptr;
+    void *next = nullptr; // uint4 {key, next} links
+    uint32_t v2_shift = 64;
+    uint64_t v2_size = 0;
 };
 
 namespace {
@@ -399,6 +553,10 @@ int join_grow(tfg_join *j, int64_t need) {
 }
 
 void free_build(tfg_join *j) {
+    if (j->heads) (void)hipFree(j->heads);
+    if (j->next) (void)hipFree(j->next);
+    j->heads = nullptr;
+    j->next = nullptr;
     if (j->brec) (void)hipFree(j->brec);
     if (j->brows) (void)hipFree(j->brows);
     if (j->boff) (void)hipFree(j->boff);
@@ -455,6 +613,46 @@ int probe_common(tfg_join *j, int kind, const void *keys, const uint8_t *key_nul
         if (int rc = tfg_join_finalize(j)) return rc;
     if (int rc = set_device(j->ctx)) return rc;
     Ctx *ctx = j->ctx;
+    if (j->v2) { // pointer table: no partitioning, one probe pass
+        void *sp;
+        if (int rc = scratch_get(ctx, 64, &sp)) return rc;
+        unsigned long long *cursor = (unsigned long long *)sp;
+        TFG_HIP(hipMemsetAsync(cursor, 0, 8, ctx->stream));
+        V2Probe A{};
+        A.link = (const uint4 *)j->next;
+        A.heads = j->heads;
+        A.shift = j->v2_shift;
+        A.tagged = j->tagged;
+        A.pkeys = keys;
+        A.pwidth = j->width;
+        A.pnull = key_nullmap;
+        A.n = n;
+        A.kind = kind;
+        A.pw = npay;
+        A.bw = j->bw < 0 ? 0 : j->bw;
+        for (int w = 0; w < JMAXW; ++w) {
+            A.ppay[w] = w < npay ? (const uint64_t *)ppay[w] : nullptr;
+            A.bpay[w] = w < A.bw ? j->pay[w] : nullptr;
+            A.out_p[w] = out_p ? out_p[w] : nullptr;
+            A.out_b[w] = out_b ? out_b[w] : nullptr;
+        }
+        A.out_bnull = out_bnull;
+        A.capacity = capacity;
+        A.cursor = cursor;
+        if (n > 0) {
+            ProfScope _ps(ctx, "join.v2.probe");
+            hipLaunchKernelGGL(join_v2_probe_kernel, dim3(stream_grid(n, 256, 16384)), dim3(256), 0, ctx->stream, A);
+            TFG_LAUNCH_CHECK();
+        }
+        if (out_count_dev) TFG_HIP(hipMemcpyAsync(out_count_dev, cursor, 8, hipMemcpyDeviceToDevice, ctx->stream));
+        uint64_t total = 0;
+        if (int rc = read_back_u64(ctx, (const uint64_t *)cursor, &total, 1)) return rc;
+        if (out_count_host) *out_count_host = total;
+        if (total > capacity)
+            return fail(TFG_ERR_CAPACITY, "join result needs %llu rows, capacity %llu", (unsigned long long)total,
+                        (unsigned long long)capacity);
+        return TFG_OK;
+    }
     const uint32_t P = j->P;
     PartLayout L = make_layout(n, P);
     // payload 0 may be the key column itself (the joined block's key): the record's key word
@@ -726,6 +924,13 @@ int tfg_join_create(tfg_ctx *ctx, int key_type, int64_t expected_build_rows, tfg
     return TFG_OK;
 }
 
+int tfg_join_create_v2(tfg_ctx *ctx, int key_type, int64_t expected_build_rows, int flags, tfg_join **out) {
+    if (int rc = tfg_join_create(ctx, key_type, expected_build_rows, out)) return rc;
+    (*out)->v2 = true;
+    (*out)->tagged = (flags & TFG_JOIN_V2_TAGGED) != 0;
+    return TFG_OK;
+}
+
 int tfg_join_destroy(tfg_join *j) {
     if (!j) return TFG_OK;
     (void)hipSetDevice(j->ctx->device);
@@ -754,6 +959,28 @@ int tfg_join_finalize(tfg_join *j) {
     if (int rc = set_device(j->ctx)) return rc;
     Ctx *ctx = j->ctx;
     if (j->bw < 0) j->bw = 0;
+    if (j->v2) { // HashJoinPointerTable::init + build
+        const int64_t n = j->n_rows;
+        uint64_t size = 1024;
+        while (size < (uint64_t)(2 * n) && size < (1ull << 32)) size <<= 1;
+        uint32_t deg = 0;
+        while ((1ull << deg) < size) ++deg;
+        j->v2_size = size;
+        j->v2_shift = 64 - deg;
+        TFG_HIP(hipMalloc(&j->heads, size * 8));
+        TFG_HIP(hipMalloc(&j->next, std::max<int64_t>(n, 1) * 16)); // {key, next} links
+        TFG_HIP(hipMemsetAsync(j->heads, 0, size * 8, ctx->stream));
+        if (n > 0) {
+            ProfScope _ps(ctx, "join.v2.build");
+            hipLaunchKernelGGL(join_v2_build_kernel, dim3(stream_grid(n, 256, 16384)), dim3(256), 0, ctx->stream, j->keys,
+                               j->nulls, n, j->heads, j->v2_shift, (int)j->tagged, (uint4 *)j->next);
+            TFG_LAUNCH_CHECK();
+        }
+        j->n_inserted = n;
+        j->P = 1;
+        j->finalized = true;
+        return TFG_OK;
+    }
     // partitions of ~JFILL build rows (table load ~0.63); the staged scatter takes P <= 4096
     uint32_t P = 1;
     while ((int64_t)P * JFILL < j->n_rows && P < 4096u) P <<= 1;

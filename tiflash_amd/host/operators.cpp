@@ -294,8 +294,12 @@ void Join::initBuild(const Block &sample_block) {
     const DataType kt = sample_.getByName(build_keys_[0]).type;
     general_keys_ = build_keys_.size() > 1 || kt.isString() || kt.width() > 8 || kt.type == TFG_FLOAT32 ||
                     kt.type == TFG_FLOAT64;
-    check(tfg_join_create(ctx_.raw(), general_keys_ ? (int)TFG_UINT64 : kt.type, expected_, &join_),
-          "tfg_join_create");
+    if (v2_flags_ >= 0)
+        check(tfg_join_create_v2(ctx_.raw(), general_keys_ ? (int)TFG_UINT64 : kt.type, expected_, v2_flags_, &join_),
+              "tfg_join_create_v2");
+    else
+        check(tfg_join_create(ctx_.raw(), general_keys_ ? (int)TFG_UINT64 : kt.type, expected_, &join_),
+              "tfg_join_create");
 }
 
 // The column the table is keyed on: the key itself, or (general keys) the UInt64 fingerprint

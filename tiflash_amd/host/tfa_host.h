@@ -354,6 +354,9 @@ public:
     void setOtherCondition(ExpressionActionsPtr expr, std::string filter_column);
     // LeftOuterSemi / AntiLeftOuterSemi: name of the match column (default "match_helper")
     void setMatchHelperName(std::string name) { match_helper_ = std::move(name); }
+    // JoinV2 (HashJoinPointerTable): build into a pointer table (tagged heads when `tagged`)
+    // instead of radix partitions; call before the first insertFromBlock
+    void useJoinV2(bool tagged = true) { v2_flags_ = tagged ? TFG_JOIN_V2_TAGGED : 0; }
 
 private:
     Context &ctx_;
@@ -370,6 +373,7 @@ private:
     ExpressionActionsPtr other_cond_;
     std::string other_filter_;
     std::string match_helper_ = "match_helper";
+    int v2_flags_ = -1; // >= 0: JoinV2 pointer table
     Block joinBlockWithCondition(const Block &probe_block);
     ColumnPtr joinKey(const Block &block, const std::vector<std::string> &names) const;
     DeviceBufferPtr verifyKeys(const Block &probe_block, const uint32_t *pi, const uint32_t *bi, uint64_t count,
