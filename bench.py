@@ -404,6 +404,49 @@ def c5_leg(args, ctx, dev, world, rank):
     return out
 
 
+def lz4_leg(args, ctx, pkt):
+    """LZ4 packets (CompressionMethod::LZ4, MPPTunnelSetHelper::ToCompressedPacket): compress the
+    uncompressed V1 packet into LZ4 frames, then decompress it; rates in packet bytes per second.
+    The decompressed bytes are checked against the packet."""
+    import torch
+
+    import tiflash_amd as tfa
+    for _ in range(2):
+        lz = tfa.codec_compress(ctx, pkt)
+        back = tfa.codec_decompress(ctx, lz)
+    tc, td = [], []
+    for _ in range(max(args.steps, 3)):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        lz = tfa.codec_compress(ctx, pkt)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        back = tfa.codec_decompress(ctx, lz)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        tc.append(t1 - t0)
+        td.append(t2 - t1)
+    assert torch.equal(back, pkt), "LZ4 round trip"
+    c, d = statistics.median(tc), statistics.median(td)
+    out = {"packet_bytes": int(pkt.numel()), "lz4_bytes": int(lz.numel()),
+           "ratio": round(pkt.numel() / max(lz.numel(), 1), 3), "compress_ms": round(c * 1e3, 3),
+           "decompress_ms": round(d * 1e3, 3), "compress_GBps": round(pkt.numel() / c / 1e9, 1),
+           "decompress_GBps": round(pkt.numel() / d / 1e9, 1)}
+    if not args.no_cpu:  # oracle/lz4.c, one host thread, on a 64 MB prefix of the same packet
+        from oracle import oracle as orc
+        host = pkt[:64 << 20].cpu().numpy().tobytes()
+        t0 = time.perf_counter()
+        hz = orc.lz4_packet_compress(host, 65536)
+        t1 = time.perf_counter()
+        orc.lz4_packet_decompress(hz)
+        t2 = time.perf_counter()
+        out["cpu_baseline"] = {"compress_GBps": round(len(host) / (t1 - t0) / 1e9, 3),
+                               "decompress_GBps": round(len(host) / (t2 - t1) / 1e9, 3), "cores": 1,
+                               "kind": "port", "sample": f"{len(host)} bytes of the packet, oracle/lz4.c"}
+    del lz, back
+    return out
+
+
 def codec_leg(args, ctx, dev):
     """§8 f1: CHBlockChunkCodecV1 (NONE) encode + decode of a C5-shaped block on the device:
     String "k%08d" key (legacy size-prefixed String, the pre-V2 MPP packet form), Decimal(15,2)
@@ -450,6 +493,8 @@ def codec_leg(args, ctx, dev):
         res[label] = {"encode_ms": round(e * 1e3, 3), "decode_ms": round(d * 1e3, 3),
                       "packet_bytes": int(pkt.numel()), "rows_per_s": round(n / (e + d), 1),
                       "packet_GBps": round(2 * pkt.numel() / (e + d) / 1e9, 1)}
+        if label == "string_v2":
+            res["lz4"] = lz4_leg(args, ctx, pkt)
         del pkt, dec
     out = {"metric": "rows/s CHBlockChunkCodecV1 encode + decode (String k%08d, Decimal(15,2), Int64)",
            "value": res["string"]["rows_per_s"], "unit": "rows/s", "rows": n, "legs": res}

@@ -443,8 +443,10 @@ int tfg_alltoallv(tfg_comm *comm, const void *send, const uint64_t *send_bytes, 
  *                      (Flash/Coprocessor/CHBlockChunkCodec.cpp:134-258).
  *   TFG_CODEC_V1:      CHBlockChunkCodecV1::encode / decode with CompressionMethod::NONE
  *                      (Flash/Coprocessor/CHBlockChunkCodecV1.cpp:370-432, 567-583); decode accepts
- *                      packets of several parts (decodeColumnsByBlock, :97-142).  LZ4 / ZSTD
- *                      packets return TFG_ERR_NOT_IMPLEMENTED.
+ *                      packets of several parts (decodeColumnsByBlock, :97-142), and LZ4
+ *                      packets (method byte 0x82: CompressedCHBlockChunkReadBuffer, :567-581)
+ *                      are decompressed on the device first.  ZSTD packets return
+ *                      TFG_ERR_NOT_IMPLEMENTED.
  * Type names as on the wire (IDataType::getName): Int8..Int64, UInt8..UInt64, Float32, Float64,
  * Decimal(P,S) with P <= 38, MyDate, MyDateTime(n), MyDuration(n), String (size-prefixed rows),
  * StringV2 (sizes, then chars), and Nullable(...) of each.  Column data follows the tfg_type
@@ -474,6 +476,27 @@ int tfg_codec_column_info(tfg_codec_packet *p, int i, char *name, size_t name_le
                           int *out_type, int *out_nullable, uint64_t *out_chars_bytes);
 int tfg_codec_column_read(tfg_codec_packet *p, int i, void *out_data, uint64_t *out_offsets, uint8_t *out_nullmap);
 int tfg_codec_packet_destroy(tfg_codec_packet *p);
+
+/* LZ4 packets (CompressionMethod values of IO/Compression/CompressionMethod.h:21-29).
+ * tfg_codec_compress replaces CHBlockChunkCodecV1::encode(std::string_view, method)
+ * (CHBlockChunkCodecV1.cpp:555-565) as MPPTunnelSetHelper::ToCompressedPacket calls it
+ * (Flash/Mpp/MPPTunnelSetHelper.cpp:170-185): the body of an uncompressed V1 `packet` (method
+ * byte 0x02 first) becomes LZ4 frames `0x82 | UInt32 frame bytes | UInt32 raw bytes | LZ4 block`
+ * (64 KB of body per frame).  out == NULL: *out_bytes_host = tfg_codec_compress_bound(bytes);
+ * otherwise the exact size, TFG_ERR_CAPACITY when it exceeds `capacity`.  LZ4HC writes the same
+ * format and is accepted as LZ4.
+ * tfg_codec_decompress is CompressedCHBlockChunkReadBuffer over a whole packet: the frames of an
+ * LZ4 packet (any frame sizes, as any LZ4 encoder wrote them) become the uncompressed V1 packet
+ * (0x02 + body).  out == NULL: the size only.  Malformed frames: TFG_ERR_INVALID_ARG. */
+#define TFG_COMPRESSION_LZ4 1
+#define TFG_COMPRESSION_LZ4HC 2
+#define TFG_COMPRESSION_ZSTD 3
+#define TFG_COMPRESSION_NONE 5
+size_t tfg_codec_compress_bound(size_t bytes);
+int tfg_codec_compress(tfg_ctx *ctx, int method, const uint8_t *packet, size_t bytes, uint8_t *out, size_t capacity,
+                       size_t *out_bytes_host);
+int tfg_codec_decompress(tfg_ctx *ctx, const uint8_t *packet, size_t bytes, uint8_t *out, size_t capacity,
+                         size_t *out_bytes_host);
 
 #ifdef __cplusplus
 }

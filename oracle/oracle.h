@@ -102,6 +102,13 @@ size_t orc_codec_encode(int version, int ncols, const char *const *names, const 
                         const void *const *data, const uint64_t *const *offsets, const uint8_t *const *nullmaps,
                         int64_t n, int nparts, const int64_t *part_rows, uint8_t *out, size_t cap);
 
+/* LZ4 block format and LZ4 MPP packets restated (lz4.c). */
+int64_t orc_lz4_decompress_block(const uint8_t *src, size_t srclen, uint8_t *dst, size_t dstcap);
+size_t orc_lz4_bound(size_t n);
+size_t orc_lz4_compress_block(const uint8_t *src, size_t n, uint8_t *dst);
+size_t orc_lz4_packet_compress(const uint8_t *pkt, size_t bytes, size_t frame_raw, uint8_t *out);
+int64_t orc_lz4_packet_decompress(const uint8_t *pkt, size_t bytes, uint8_t *out, size_t cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -99,6 +99,16 @@ def lib():
         L.orc_join_ref_destroy.argtypes = [ctypes.c_void_p]
         L.orc_codec_encode.restype = ctypes.c_size_t
         L.orc_codec_decode_strings.restype = ctypes.c_size_t
+        L.orc_lz4_decompress_block.restype = ctypes.c_int64
+        L.orc_lz4_decompress_block.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]
+        L.orc_lz4_bound.restype = ctypes.c_size_t
+        L.orc_lz4_bound.argtypes = [ctypes.c_size_t]
+        L.orc_lz4_compress_block.restype = ctypes.c_size_t
+        L.orc_lz4_compress_block.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+        L.orc_lz4_packet_compress.restype = ctypes.c_size_t
+        L.orc_lz4_packet_compress.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p]
+        L.orc_lz4_packet_decompress.restype = ctypes.c_int64
+        L.orc_lz4_packet_decompress.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]
         _L = L
     return _L
 
@@ -451,3 +461,41 @@ def codec_decode_strings(buf: bytes, rows: int, chars_cap: int):
                                           _p(offs))
     assert used != ctypes.c_size_t(-1).value, "truncated"
     return chars[:int(offs[rows - 1]) if rows else 0], offs[:rows], used
+
+
+# ---- (f1) LZ4 packets (oracle/lz4.c) ---------------------------------------------------------
+def lz4_decompress_block(block: bytes, raw_cap: int):
+    """LZ4_decompress_safe restated: decoded bytes, or None when the block is malformed."""
+    src = np.frombuffer(block, np.uint8) if block else np.zeros(1, np.uint8)
+    dst = np.zeros(max(raw_cap, 1), np.uint8)
+    got = lib().orc_lz4_decompress_block(_p(src), len(block), _p(dst), raw_cap)
+    return None if got < 0 else dst[:got].tobytes()
+
+
+def lz4_compress_block(raw: bytes) -> bytes:
+    src = np.frombuffer(raw, np.uint8) if raw else np.zeros(1, np.uint8)
+    dst = np.zeros(lib().orc_lz4_bound(len(raw)), np.uint8)
+    n = lib().orc_lz4_compress_block(_p(src), len(raw), _p(dst))
+    return dst[:n].tobytes()
+
+
+def lz4_packet_compress(packet: bytes, frame_raw: int = 0) -> bytes:
+    """Uncompressed V1 packet (0x02 + body) -> LZ4 frames of frame_raw body bytes (0: one frame)."""
+    src = np.frombuffer(packet, np.uint8)
+    L = lib()
+    cap = L.orc_lz4_packet_compress(_p(src), src.size, frame_raw, None)
+    out = np.zeros(max(cap, 1), np.uint8)
+    n = L.orc_lz4_packet_compress(_p(src), src.size, frame_raw, _p(out))
+    return out[:n].tobytes()
+
+
+def lz4_packet_decompress(packet: bytes):
+    """LZ4 frames -> the uncompressed V1 packet (0x02 + body); None when malformed."""
+    src = np.frombuffer(packet, np.uint8) if packet else np.zeros(1, np.uint8)
+    L = lib()
+    size = L.orc_lz4_packet_decompress(_p(src), len(packet), None, 0)
+    if size < 0:
+        return None
+    out = np.zeros(size, np.uint8)
+    got = L.orc_lz4_packet_decompress(_p(src), len(packet), _p(out), size)
+    return None if got < 0 else out.tobytes()

@@ -1,4 +1,5 @@
-"""MPP packet codec (§8 f1): CHBlockChunkCodec / CHBlockChunkCodecV1 with CompressionMethod::NONE.
+"""MPP packet codec (§8 f1): CHBlockChunkCodec / CHBlockChunkCodecV1 with CompressionMethod::NONE
+(LZ4 packets: tests/test_codec_lz4.py).
 
 CPU: the oracle (oracle/codec.c) against hand-derived packets — the byte layout written out from
 the reference's text (CHBlockChunkCodecV1.cpp:45-58,293-312,370-432; CHBlockChunkCodec.cpp:134-166;
@@ -209,9 +210,12 @@ def test_gpu_legacy_strings_many_chunks(tfa, orc, ctx, dev):
 @pytest.mark.gpu
 def test_gpu_decode_rejects_bad_packets(tfa, ctx, dev):
     import torch
-    with pytest.raises(tfa.TfgError) as e:  # LZ4 method byte
-        tfa.codec_decode(ctx, torch.tensor([0x82, 1, 0], dtype=torch.uint8, device=dev), version=V1)
+    with pytest.raises(tfa.TfgError) as e:  # ZSTD method byte
+        tfa.codec_decode(ctx, torch.tensor([0x90, 1, 0], dtype=torch.uint8, device=dev), version=V1)
     assert e.value.code == -4
+    with pytest.raises(tfa.TfgError) as e:  # LZ4 method byte, truncated frame header
+        tfa.codec_decode(ctx, torch.tensor([0x82, 1, 0], dtype=torch.uint8, device=dev), version=V1)
+    assert e.value.code == -1
     with pytest.raises(tfa.TfgError):  # truncated String column
         tfa.codec_decode(ctx, torch.tensor(list(b"\x01\x02" + sb(b"s") + sb(b"String") + b"\x05ab"),
                                            dtype=torch.uint8, device=dev), version=CHB)

@@ -77,6 +77,8 @@ def lib() -> ctypes.CDLL:
         L.tfg_version.restype = ctypes.c_char_p
         L.tfg_type_width.restype = ctypes.c_size_t
         L.tfg_type_width.argtypes = [ctypes.c_int]
+        L.tfg_codec_compress_bound.restype = ctypes.c_size_t
+        L.tfg_codec_compress_bound.argtypes = [ctypes.c_size_t]
         _lib = L
     return _lib
 
@@ -719,6 +721,34 @@ def codec_encode(ctx: Context, columns: Sequence, n: int, version: int = CODEC_V
     out = torch.empty(max(size.value, 1), dtype=torch.uint8, device=dev)
     check(lib().tfg_codec_encode(ctx.h, version, len(columns), arr, ctypes.c_int64(n), _p(out),
                                  ctypes.c_size_t(out.numel()), ctypes.byref(size)))
+    return out[:size.value]
+
+
+COMPRESSION_LZ4, COMPRESSION_LZ4HC, COMPRESSION_ZSTD, COMPRESSION_NONE = 1, 2, 3, 5
+
+
+def codec_compress(ctx: Context, packet, method: int = COMPRESSION_LZ4):
+    """CHBlockChunkCodecV1::encode(std::string_view, method) of an uncompressed V1 device packet
+    (as MPPTunnelSetHelper::ToCompressedPacket re-encodes a chunk): LZ4 frames, a device tensor."""
+    import torch
+    size = ctypes.c_size_t()
+    check(lib().tfg_codec_compress(ctx.h, method, _p(packet), ctypes.c_size_t(packet.numel()), None,
+                                   ctypes.c_size_t(0), ctypes.byref(size)))
+    out = torch.empty(max(size.value, 1), dtype=torch.uint8, device=packet.device)
+    check(lib().tfg_codec_compress(ctx.h, method, _p(packet), ctypes.c_size_t(packet.numel()), _p(out),
+                                   ctypes.c_size_t(out.numel()), ctypes.byref(size)))
+    return out[:size.value]
+
+
+def codec_decompress(ctx: Context, packet):
+    """CompressedCHBlockChunkReadBuffer over an LZ4 device packet -> the uncompressed V1 packet."""
+    import torch
+    size = ctypes.c_size_t()
+    check(lib().tfg_codec_decompress(ctx.h, _p(packet), ctypes.c_size_t(packet.numel()), None, ctypes.c_size_t(0),
+                                     ctypes.byref(size)))
+    out = torch.empty(max(size.value, 1), dtype=torch.uint8, device=packet.device)
+    check(lib().tfg_codec_decompress(ctx.h, _p(packet), ctypes.c_size_t(packet.numel()), _p(out),
+                                     ctypes.c_size_t(out.numel()), ctypes.byref(size)))
     return out[:size.value]
 
 

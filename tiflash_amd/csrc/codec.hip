@@ -40,6 +40,7 @@
 namespace tfg {
 
 constexpr uint8_t COMP_NONE = 0x02; // CompressionMethodByte::NONE (IO/Compression/CompressionInfo.h:55)
+constexpr uint8_t COMP_LZ4 = 0x82;  // CompressionMethodByte::LZ4 (frames decompressed by lz4.hip)
 constexpr int LCH = 32768;          // legacy parse chunk bytes
 constexpr int LENT = 256;           // entry offsets per chunk (threads of the map kernel)
 constexpr int LGRP = 64;            // chunks per resolution group
@@ -352,7 +353,9 @@ struct tfg_codec_packet {
     std::vector<std::string> names;
     std::vector<tfg::CType> types;
     std::vector<std::vector<tfg::Seg>> segs; // [column][part]
+    uint8_t *owned = nullptr;                // LZ4 packets: the decompressed NONE packet
     ~tfg_codec_packet() {
+        if (owned) (void)hipFree(owned);
         for (auto &c : segs)
             for (auto &s : c)
                 if (s.starts) (void)hipFree(s.starts);
@@ -638,7 +641,18 @@ int tfg_codec_decode(tfg_ctx *ctx, int version, const uint8_t *packet, size_t by
     if (version == TFG_CODEC_V1) {
         uint8_t m;
         if (int rc = rd.byte(m)) return done(rc);
-        if (m != COMP_NONE) return done(fail(TFG_ERR_NOT_IMPLEMENTED, "compressed packet (method byte 0x%02x): only NONE", m));
+        if (m == COMP_LZ4) { // CompressedCHBlockChunkReadBuffer: decompress the frames, then read as NONE
+            size_t raw = 0;
+            if (int rc = tfg_codec_decompress(ctx, packet, bytes, nullptr, 0, &raw)) return done(rc);
+            if (hipMalloc(&p->owned, raw) != hipSuccess) return done(fail(TFG_ERR_OOM, "decompressed packet of %zu bytes", raw));
+            if (int rc = tfg_codec_decompress(ctx, packet, bytes, p->owned, raw, &raw)) return done(rc);
+            p->pkt = p->owned;
+            p->bytes = raw;
+            rd = PacketReader{ctx, p->owned, raw};
+            if (int rc = rd.byte(m)) return done(rc);
+        } else if (m != COMP_NONE) {
+            return done(fail(TFG_ERR_NOT_IMPLEMENTED, "compressed packet (method byte 0x%02x): NONE and LZ4 only", m));
+        }
     }
     uint64_t ncols, rows;
     if (int rc = rd.varuint(ncols)) return done(rc);
