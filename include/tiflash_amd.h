@@ -321,14 +321,23 @@ int tfg_agg_size(tfg_agg *agg, uint64_t *out_groups);
  * Order is the table's (compare unordered, as the reference tests do). */
 int tfg_agg_result(tfg_agg *agg, void *out_keys, uint8_t *out_key_nullmap, void *const *out_states,
                    uint8_t *const *out_state_nullmaps, uint64_t capacity, uint64_t *out_groups_host);
-/* Several GROUP BY keys or one String key (Aggregator::chooseAggregationMethod, Interpreters/
- * Aggregator.cpp:394-537): fixed-width keys whose widths sum to <= 16 bytes take the keys128 /
- * nullable_keys128 method (packFixed, Common/ColumnsHashing.h:324-480; nullable keys need
- * widths summing to <= 15: byte 15 holds their NULL bits); one String key takes key_string
- * (HashMethodString, ColumnsHashing.h:179-241): rows group by the collator's sort key
- * (key_collators[0]: tfg_collator; BIN_PADDING right-trims spaces), which must be <= 15 bytes
- * (longer keys fail with TFG_ERR_NOT_IMPLEMENTED).  Both aggregate on a packed 16-byte key
- * (TFG_KEYS128).  One non-String key falls back to tfg_agg_create.  key_collators may be NULL. */
+/* Several GROUP BY keys, one String key or one 16-byte key (Aggregator::chooseAggregationMethod,
+ * Interpreters/Aggregator.cpp:394-537):
+ *   - fixed-width keys whose widths sum to <= 16 bytes take keys128 / nullable_keys128 (packFixed,
+ *     Common/ColumnsHashing.h:324-480; nullable keys use byte 15 for their NULL bits);
+ *   - one String key takes key_string (HashMethodString, ColumnsHashing.h:179-241): rows group by
+ *     the collator's sort key (key_collators[j]: tfg_collator; BIN_PADDING right-trims spaces);
+ *   - everything else takes the serialized method (HashMethodSerialized, ColumnsHashing.h:578-629):
+ *     String keys with other keys, fixed tuples past 16 bytes (keys256), 5-8 keys.  Each row's key
+ *     tuple is serialised (a NULL byte per key, the value bytes, a String's length + sort key) and
+ *     a device dictionary maps equal byte strings to one group; fingerprint collisions are caught
+ *     by a byte compare and retried with another seed, never merged.
+ * keys128 / key_string aggregate on a packed 16-byte key (TFG_KEYS128).  A block whose keys do not
+ * fit it (a String sort key over 15 bytes; nullable fixed keys of 16 bytes, nullable_keys256)
+ * moves the aggregator to the serialized method, carrying the groups it holds; from then on it has
+ * no packed form (tfg_agg_result / tfg_agg_consume_partial return TFG_ERR_NOT_IMPLEMENTED; use the
+ * *_keys calls).  One fixed key of <= 8 bytes falls back to tfg_agg_create.  key_collators may
+ * be NULL. */
 int tfg_agg_create_keys(tfg_ctx *ctx, int nkeys, const int *key_types, const int *key_collators, int n_aggs,
                         const int *agg_kinds, const int *arg_types, const int *arg_scales, const tfg_agg_params *params,
                         tfg_agg **out);
@@ -342,9 +351,10 @@ int tfg_agg_consume_keys(tfg_agg *agg, const void *const *key_cols, const uint64
 int tfg_agg_consume_partial_keys(tfg_agg *agg, const void *const *key_cols, const uint64_t *const *key_offsets,
                                  const uint8_t *const *key_nullmaps, const void *const *states,
                                  const uint8_t *const *state_nullmaps, int64_t n);
-/* convertToBlockImplFinal with the key columns restored (String: chars + end offsets; chars
- * need *out_chars_host bytes, TFG_ERR_CAPACITY past chars_capacity).  tfg_agg_result on the same
- * agg writes the packed TFG_KEYS128 keys instead, which tfg_agg_consume_partial accepts. */
+/* convertToBlockImplFinal with the key columns restored (String: chars + end offsets).  Every
+ * String key column gets chars_capacity bytes; *out_chars_host = the chars the largest String key
+ * column needs (TFG_ERR_CAPACITY past chars_capacity, nothing written).  tfg_agg_result on a
+ * packed-key agg writes the packed TFG_KEYS128 keys instead, which tfg_agg_consume_partial accepts. */
 int tfg_agg_result_keys(tfg_agg *agg, void *const *out_key_cols, uint64_t *const *out_key_offsets,
                         uint8_t *const *out_key_nullmaps, void *const *out_states, uint8_t *const *out_state_nullmaps,
                         uint64_t capacity, uint64_t chars_capacity, uint64_t *out_groups_host, uint64_t *out_chars_host);

@@ -699,8 +699,8 @@ void orc_agg_result(const orc_agg *a, uint64_t *out_keys, uint8_t *out_key_null,
  * states live in an inner orc_agg keyed by that id. */
 struct orc_aggk {
     int nkeys;
-    int key_types[4];
-    int collators[4];
+    int key_types[8];
+    int collators[8];
     /* byte-string map: open addressing over (hash, id) cells; keys in one arena */
     uint64_t *cells; /* (crc << 32) | (id + 1), 0 = empty */
     size_t cap, size;
@@ -718,7 +718,7 @@ static uint32_t bytes_hash(const uint8_t *p, size_t n) { return orc_update_weak_
 orc_aggk *orc_aggk_create(int nkeys, const int *key_types, const int *collators, int n_aggs, const int *kinds,
                           const int *arg_types)
 {
-    if (nkeys < 1 || nkeys > 4) return NULL;
+    if (nkeys < 1 || nkeys > 8) return NULL;
     orc_aggk *a = (orc_aggk *)calloc(1, sizeof(orc_aggk));
     a->nkeys = nkeys;
     for (int j = 0; j < nkeys; ++j) {

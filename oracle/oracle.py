@@ -285,7 +285,7 @@ class AggKeys:
             else:
                 cols.append(np.ascontiguousarray(k))
                 offs.append(None)
-        n = len(offs[0]) if self.key_types[0] == STRING else len(cols[0])
+        n = len(offs[0]) if self.key_types[0] == STRING else cols[0].nbytes // _KW[self.key_types[0]]
         self._keep = (cols, offs, args, key_nulls, arg_nulls, mask)
         lib().orc_aggk_consume(self.h, _ptrs(cols), _ptrs(offs), _ptrs(key_nulls) if key_nulls else None, _ptrs(args),
                                _ptrs(arg_nulls) if arg_nulls else None, _p(mask), ctypes.c_size_t(n))

@@ -924,7 +924,9 @@ TEST(AggregatorPackedKeysMatchMap) {
     std::vector<uint8_t> bn(n);
     std::vector<int64_t> v(n), f(n);
     std::vector<std::string> s(n);
-    const std::vector<std::string> words = {"", "x", "x ", "k00000001", "k00000001  ", "abcdefghijklmno", " y"};
+    // the last two are past key_string's 15 bytes: the String-key aggregator moves to serialized
+    const std::vector<std::string> words = {"",  "x", "x ", "k00000001", "k00000001  ", "abcdefghijklmno", " y",
+                                            "customer-name-000000000042", "customer-name-000000000042   "};
     for (size_t i = 0; i < n; ++i) {
         a[i] = (int32_t)(rng() % 50) - 25;
         b[i] = (int16_t)(rng() % 7);
@@ -938,17 +940,20 @@ TEST(AggregatorPackedKeysMatchMap) {
               {makeStringColumn(ctx, s), str, "s"},
               {makeColumn(ctx, i64, v.data(), n), i64, "v"},
               {makeColumn(ctx, i64, f.data(), n), i64, "f"}};
-    for (int mode = 0; mode < 2; ++mode) { // 0: (a, b) keys, 1: String key s
+    for (int mode = 0; mode < 3; ++mode) { // 0: (a, b) keys, 1: String key s, 2: (a, s) serialized
         Aggregator::Params p;
-        p.keys = mode == 0 ? std::vector<std::string>{"a", "b"} : std::vector<std::string>{"s"};
+        p.keys = mode == 0   ? std::vector<std::string>{"a", "b"}
+                 : mode == 1 ? std::vector<std::string>{"s"}
+                             : std::vector<std::string>{"a", "s"};
         if (mode == 1) p.collators = {TFG_COLLATOR_BIN_PADDING};
+        if (mode == 2) p.collators = {TFG_COLLATOR_NONE, TFG_COLLATOR_BIN_PADDING};
         p.aggregates = {{"sum", {"v"}, "sum_v"}, {"count", {}, "cnt"}};
         p.src_header = blk.cloneEmpty();
         auto keyOf = [&](size_t i) {
             if (mode == 0) return std::to_string(a[i]) + "," + (bn[i] ? std::string("N") : std::to_string(b[i]));
             std::string t = s[i];
             while (!t.empty() && t.back() == ' ') t.pop_back();
-            return t;
+            return mode == 2 ? std::to_string(a[i]) + "," + t : t;
         };
         for (int filtered = 0; filtered < 2; ++filtered) {
             std::map<std::string, std::pair<int64_t, uint64_t>> want;
@@ -984,8 +989,12 @@ TEST(AggregatorPackedKeysMatchMap) {
                 auto ka = cellStrings(ctx, *r.getByName("a").column);
                 auto kb = cellStrings(ctx, *r.getByName("b").column);
                 for (size_t i = 0; i < r.rows(); ++i) keys.push_back(ka[i] + "," + kb[i]);
-            } else {
+            } else if (mode == 1) {
                 keys = toHostStrings(ctx, *r.getByName("s").column);
+            } else {
+                auto ka = cellStrings(ctx, *r.getByName("a").column);
+                auto ks = toHostStrings(ctx, *r.getByName("s").column);
+                for (size_t i = 0; i < r.rows(); ++i) keys.push_back(ka[i] + "," + ks[i]);
             }
             auto sums = toHost<int64_t>(ctx, *r.getByName("sum_v").column);
             auto cnts = toHost<uint64_t>(ctx, *r.getByName("cnt").column);

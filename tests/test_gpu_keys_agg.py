@@ -48,6 +48,10 @@ def gpu_groups(res, key_types):
         elif t in (9, 10):
             a = k.cpu().numpy().view(np.float32 if t == 9 else np.float64)
             vals = [None if nulls[i] else float(a[i]) for i in range(g)]
+        elif t in (13, 14):  # Decimal128 / Decimal256 keys: (G, limbs) int64
+            from oracle.oracle import limbs_to_int
+            a = k.cpu().numpy()
+            vals = [None if nulls[i] else limbs_to_int(a[i]) for i in range(g)]
         else:
             a = k.cpu().numpy()
             w = a.dtype.itemsize
@@ -195,20 +199,34 @@ def test_string_key_lengths_and_empty(tfa, ctx, dev, orc):
     assert e.size() == 0
 
 
-def test_string_key_too_long_fails_loudly(tfa, ctx, dev):
-    chars, offs = str_col([b"short", b"x" * 16])
-    agg = tfa.KeysAggregator(ctx, [tfa.STRING], [(tfa.AGG_COUNT_ALL, 0)])
-    with pytest.raises(tfa.TfgError) as ei:
-        agg.consume([to_dev((chars, offs), dev)], [None])
-    assert ei.value.code == -4
+@pytest.mark.parametrize("collator", [0, 2])
+def test_string_key_past_15_bytes_moves_to_serialized(tfa, ctx, dev, orc, collator):
+    """key_string over keys of any length: the first block's keys fit the packed form; the second
+    block holds keys of 16-300 bytes, so the aggregator moves to the serialized method carrying the
+    first block's groups (keys of both blocks overlap), then a third block is consumed there."""
+    rng = np.random.default_rng(20 + collator)
+    short = vocab_strings(rng, 500)
+    long_ = [b"L%05d" % i + bytes(rng.integers(33, 127, int(rng.integers(10, 300)), dtype=np.uint8)) for i in range(700)]
+    long_ += [s + b"   " for s in long_[:50]]  # BIN_PADDING folds these onto their unpadded keys
+    blocks = [rand_strings(rng, 20_000, short),
+              rand_strings(rng, 30_000, short + long_),
+              rand_strings(rng, 10_000, long_)]
+    aggs = [(tfa.AGG_SUM, tfa.INT64), (tfa.AGG_COUNT_ALL, 0)]
+    agg = tfa.KeysAggregator(ctx, [tfa.STRING], aggs, collators=[collator])
+    ref = orc.AggKeys([orc.STRING], [(0, orc.INT64), (2, 0)], collators=[collator])
+    for strs in blocks:
+        chars, offs = str_col(strs)
+        v = rng.integers(-1000, 1000, len(strs), dtype=np.int64)
+        agg.consume([to_dev((chars, offs), dev)], [to_dev(v, dev), None])
+        ref.consume([(chars, offs)], [v, None])
+    check_same(gpu_groups(agg.result(), [20]), ref.result())
 
 
 @pytest.mark.parametrize("types", [(3, 5), (4, 4), (2, 7, 1), (1, 2, 3, 8)])
 @pytest.mark.parametrize("nullable", [False, True])
 def test_multi_fixed_keys(tfa, ctx, dev, orc, types, nullable):
     widths = {1: 1, 2: 2, 3: 4, 4: 8, 5: 1, 7: 4, 8: 8}
-    if nullable and sum(widths[t] for t in types) > 15:
-        pytest.skip("nullable keys need a spare byte (nullable_keys256 not supported)")
+    # nullable tuples of 16 bytes have no spare byte in the packed key: the serialized method
     np_t = {1: np.int8, 2: np.int16, 3: np.int32, 4: np.int64, 5: np.uint8, 7: np.uint32, 8: np.uint64}
     rng = np.random.default_rng(sum(types) + nullable)
     n = 50_000
@@ -272,8 +290,8 @@ def test_merge_multi_key(tfa, ctx, dev, orc):
 
 
 def test_groupby_keys_reference_cases(tfa, ctx, dev):
-    """GroupBy string_ and two-column GROUP BYs (gtest_aggregation_executor.cpp:408-482); the
-    String + fixed combinations take the reference's serialized method, not packed here."""
+    """GroupBy string_ and two-column GROUP BYs (gtest_aggregation_executor.cpp:408-482): the
+    String + fixed combinations take the serialized method, nullable 16-byte tuples move to it."""
     import json
     import os
     from test_oracle_cpu import golden_key_columns
@@ -281,16 +299,12 @@ def test_groupby_keys_reference_cases(tfa, ctx, dev):
     ran = 0
     for case in g["cases"]:
         types, keys, nulls, exp = golden_key_columns(case, g["columns"])
-        if 20 in types and len(types) > 1:
-            continue  # serialized method (String + fixed keys): not packed
-        if sum({1: 1, 2: 2, 3: 4, 4: 8, 8: 8, 9: 4, 10: 8}.get(t, 0) for t in types) > 15:
-            continue  # nullable 16-byte key tuples: nullable_keys256, not packed (TFG_ERR_NOT_IMPLEMENTED)
         agg = tfa.KeysAggregator(ctx, types, [(tfa.AGG_COUNT_ALL, 0)])
         agg.consume([to_dev(k, dev) for k in keys], [None], key_nullmaps=[to_dev(x, dev) for x in nulls])
         got = [k for k, _ in gpu_groups(agg.result(), types)]
         assert sorted(got, key=repr) == sorted(exp, key=repr), case["group_by"]
         ran += 1
-    assert ran == 4
+    assert ran == len(g["cases"]) == 7
 
 
 def test_reference_aggregate_values(tfa, ctx, dev, orc):
@@ -318,8 +332,6 @@ def test_reference_aggregate_values(tfa, ctx, dev, orc):
             got = [int(x) for x in g.result()["states"][0].cpu().numpy()]
         else:
             cols = {"country": country, "gender": gender}
-            if len(c["group_by"]) > 1 and not hasattr(tfa, "SERIALIZED_KEYS"):
-                continue  # two String keys: the serialized method
             g = tfa.KeysAggregator(ctx, [tfa.STRING] * len(c["group_by"]), [(kind, word)])
             g.consume([to_dev(cols[k], dev) for k in c["group_by"]], [to_dev(arg, dev) if arg is not None else None],
                       arg_nullmaps=[to_dev(nulls, dev)] if nulls is not None else None)
@@ -329,3 +341,97 @@ def test_reference_aggregate_values(tfa, ctx, dev, orc):
     g = tfa.Aggregator(ctx, 0, [(tfa.AGG_SUM, tfa.INT64)])
     g.consume(None, [to_dev(s2, dev)], n=3)
     assert int(g.result()["states"][0].item()) == case["sums"][0]["expected"][0]
+
+
+def rand_fixed(rng, t, n, card):
+    np_t = {1: np.int8, 2: np.int16, 3: np.int32, 4: np.int64, 5: np.uint8, 6: np.uint16, 7: np.uint32, 8: np.uint64,
+            10: np.float64}[t]
+    if t == 10:
+        base = rng.integers(-50, 50, card).astype(np.float64) / 4
+        base[0] = -0.0  # raw bits: -0.0 and 0.0 are different keys, as serializeValueIntoArena copies bytes
+        base[1] = 0.0
+    else:
+        info = np.iinfo(np_t)
+        base = rng.integers(info.min, info.max, card, dtype=np_t, endpoint=True)
+    return base[rng.integers(0, card, n)]
+
+
+SERIAL_SETS = [
+    [4, 20],            # bigint_, string_ (the reference's serialized case)
+    [20, 20],           # country, gender
+    [20, 3, 20, 1],     # String / fixed interleaved
+    [4, 4, 8],          # 24 bytes: past keys128
+    [4, 4, 4, 8, 3],    # five keys
+    [1, 2, 3, 4, 5, 6, 7, 8],  # eight keys
+    [13, 3],            # Decimal128 + Int32
+    [10, 20],           # Float64 raw bits + String
+]
+
+
+@pytest.mark.parametrize("types", SERIAL_SETS, ids=lambda t: "-".join(map(str, t)))
+@pytest.mark.parametrize("nullable", [False, True])
+def test_serialized_keys(tfa, ctx, dev, orc, types, nullable):
+    """The serialized method (HashMethodSerialized, ColumnsHashing.h:578-629) vs the oracle's
+    serialised-bytes HashMap: two blocks (the second seeds the first's groups), a filter mask on
+    the second, NULLs in every key column, String keys of 0-40 bytes under BIN_PADDING."""
+    rng = np.random.default_rng(sum(types) * 7 + nullable)
+    n = 40_000
+    colls = [2 if t == 20 else 0 for t in types]
+    vocab = vocab_strings(rng, 60, maxlen=40)
+    blocks = []
+    for b in range(2):
+        keys, nulls = [], []
+        for t in types:
+            if t == 20:
+                keys.append(str_col(rand_strings(rng, n, vocab)))
+            elif t == 13:
+                d = rng.integers(-3, 3, n).astype(object) * (1 << 100) + rng.integers(0, 5, n).astype(object)
+                keys.append(np.array([[x & ((1 << 64) - 1), (x >> 64) & ((1 << 64) - 1)] for x in d],
+                                     dtype=np.uint64).view(np.int64).reshape(-1))
+            else:
+                keys.append(rand_fixed(rng, t, n, 5 if len(types) > 3 else 13))
+            nulls.append((rng.random(n) < 0.07).astype(np.uint8) if nullable else None)
+        v = rng.integers(-10**6, 10**6, n, dtype=np.int64)
+        mask = (rng.random(n) < 0.8).astype(np.uint8) if b == 1 else None
+        blocks.append((keys, nulls, v, mask))
+    aggs = [(tfa.AGG_SUM, tfa.INT64), (tfa.AGG_COUNT_ALL, 0)]
+    agg = tfa.KeysAggregator(ctx, list(types), aggs, collators=colls)
+    ref = orc.AggKeys(list(types), [(0, orc.INT64), (2, 0)], collators=colls)
+    for keys, nulls, v, mask in blocks:
+        dk = [to_dev(k, dev) for k in keys]
+        agg.consume(dk, [to_dev(v, dev), None], key_nullmaps=[to_dev(x, dev) for x in nulls] if nullable else None,
+                    mask=to_dev(mask, dev) if mask is not None else None)
+        ref.consume(keys, [v, None], key_nulls=nulls if nullable else None, mask=mask)
+    exp = ref.result()
+    check_same(gpu_groups(agg.result(), list(types)), exp)
+    # two-phase: the result's key columns merged into a fresh aggregator, and merge()
+    res = agg.result()
+    fin = tfa.KeysAggregator(ctx, list(types), aggs, collators=colls)
+    fin.consume_partial(res["keys"], res["states"], key_nullmaps=res["key_null"])
+    check_same(gpu_groups(fin.result(), list(types)), exp)
+    other = tfa.KeysAggregator(ctx, list(types), aggs, collators=colls)
+    other.merge(agg)
+    check_same(gpu_groups(other.result(), list(types)), exp)
+    agg.reset()
+    assert agg.size() == 0
+
+
+def test_serialized_keys_many_groups(tfa, ctx, dev, orc):
+    """(Int64, String > 15 bytes) at 1.5M groups over 3M rows: the dictionary's slot table and key
+    arena grow across blocks, Decimal(15,2) sums in Decimal128."""
+    rng = np.random.default_rng(31)
+    n, groups = 3_000_000, 1_500_000
+    gid = rng.integers(0, groups, n)
+    k1 = (gid % 997).astype(np.int64) - 400
+    strs = [b"customer-%012d" % (g // 997) for g in gid]
+    d = rng.integers(-10**12, 10**12, n, dtype=np.int64)
+    aggs = [(tfa.AGG_SUM, tfa.prec(tfa.DECIMAL64, 15)), (tfa.AGG_COUNT_ALL, 0)]
+    agg = tfa.KeysAggregator(ctx, [tfa.INT64, tfa.STRING], aggs)
+    cut = n // 3
+    for lo, hi in ((0, cut), (cut, n)):
+        c2, o2 = str_col(strs[lo:hi])
+        agg.consume([to_dev(k1[lo:hi], dev), to_dev((c2, o2), dev)], [to_dev(d[lo:hi], dev), None])
+    chars, offs = str_col(strs)
+    ref = orc.AggKeys([orc.INT64, orc.STRING], [(0, orc.prec(orc.DECIMAL64, 15)), (2, 0)])
+    ref.consume([k1, (chars, offs)], [d, None])
+    check_same(gpu_groups(agg.result(), [tfa.INT64, 20]), ref.result())

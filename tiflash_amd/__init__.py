@@ -501,7 +501,8 @@ class KeysAggregator(Aggregator):
             else:
                 cols.append(k)
                 offs.append(None)
-        n = offs[0].shape[0] if self.key_types[0] == STRING else cols[0].shape[0]
+        t0 = self.key_types[0]  # rows: a Decimal128 / Decimal256 key may come as flat int64 limbs
+        n = offs[0].shape[0] if t0 == STRING else cols[0].numel() * cols[0].element_size() // WIDTH[t0]
         return _ptr_array(cols), _ptr_array(offs), n
 
     def consume(self, keys, args: Sequence, key_nullmaps=None, arg_nullmaps=None, mask=None):
@@ -523,15 +524,18 @@ class KeysAggregator(Aggregator):
         """-> dict as Aggregator.result() with keys = (G, 2) int64 packed keys."""
         return Aggregator.result(self, device)
 
-    def result(self, device=None):
-        """-> dict(keys=[col or (chars, offsets)], key_null=[uint8], states=[...], state_null=[...])."""
+    def result(self, device=None, chars_capacity=None):
+        """-> dict(keys=[col or (chars, offsets)], key_null=[uint8], states=[...], state_null=[...]).
+        String keys of the serialized method may need more than 16 bytes a group: the call is
+        repeated with the size TFG_ERR_CAPACITY reports."""
         import torch
         dev = device or torch.device("cuda", self.ctx.device)
         g = self.size()
+        ccap = max(16 * g, 1) if chars_capacity is None else max(chars_capacity, 1)
         cols, offs, nulls = [], [], []
         for t in self.key_types:
             if t == STRING:
-                cols.append(torch.empty(max(16 * g, 1), dtype=torch.uint8, device=dev))
+                cols.append(torch.empty(ccap, dtype=torch.uint8, device=dev))
                 offs.append(torch.empty(max(g, 1), dtype=torch.int64, device=dev))
             else:
                 cols.append(_empty(g, WIDTH[t], dev))
@@ -547,12 +551,15 @@ class KeysAggregator(Aggregator):
             states.append(s)
             snulls.append(torch.empty(max(g, 1), dtype=torch.uint8, device=dev)[:g])
         cnt, chars = ctypes.c_uint64(), ctypes.c_uint64()
-        check(lib().tfg_agg_result_keys(self.h, _ptr_array(cols), _ptr_array(offs), _ptr_array(nulls), _ptr_array(states),
-                                        _ptr_array(snulls), ctypes.c_uint64(g), ctypes.c_uint64(16 * g),
-                                        ctypes.byref(cnt), ctypes.byref(chars)))
+        rc = lib().tfg_agg_result_keys(self.h, _ptr_array(cols), _ptr_array(offs), _ptr_array(nulls), _ptr_array(states),
+                                       _ptr_array(snulls), ctypes.c_uint64(g), ctypes.c_uint64(ccap),
+                                       ctypes.byref(cnt), ctypes.byref(chars))
+        if rc == TFG_ERR_CAPACITY and chars.value > ccap:
+            return self.result(device, chars.value)
+        check(rc)
         keys = []
         for t, c, o in zip(self.key_types, cols, offs):
-            keys.append((c[:chars.value], o[:g]) if t == STRING else c[:g])
+            keys.append((c[:int(o[g - 1].item())] if g else c[:0], o[:g]) if t == STRING else c[:g])
         return {"keys": keys, "key_null": [x[:g] for x in nulls], "states": states, "state_null": snulls}
 
 

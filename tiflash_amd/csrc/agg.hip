@@ -24,6 +24,7 @@
 #include "agg_fused.h"
 #include "common.h"
 #include "partition.h"
+#include "serial.h"
 
 namespace tfg {
 
@@ -1716,7 +1717,17 @@ struct tfg_agg {
     // wide keys (keys128 / key_string): key_type == TFG_KEYS_WIDE, packing spec, and a device
     // buffer holding the packed keys of the block being consumed / the result being written
     KeyPack kp{};
-    int key_types[4] = {};
+    int key_types[8] = {};
+    int key_collators[8] = {};
+    // the serialized method (serial.h): when set, every call goes to `inner`, an aggregator over
+    // the dictionary's UInt32 group ids; a packed-key aggregator moves there (carrying its groups)
+    // the first time a block's keys do not fit 16 bytes (long String keys, nullable key tuples of
+    // 16 bytes).  The creation arguments are kept for that move.
+    SerialDict *sdict = nullptr;
+    tfg_agg *inner = nullptr;
+    bool long_key = false;
+    int c_kinds[AGG_MAX] = {}, c_types[AGG_MAX] = {}, c_scales[AGG_MAX] = {};
+    tfg_agg_params c_params{};
     void *pack_buf = nullptr;
     size_t pack_cap = 0;
     unsigned *pack_err = nullptr;
@@ -2011,7 +2022,10 @@ int consume_wide_tiled(tfg_agg *a, int code, Sel sel, const void *const *vals, i
         unsigned e = 0;
         TFG_HIP(hipMemcpyAsync(&e, err, sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
         TFG_HIP(hipStreamSynchronize(ctx->stream));
-        if (e) return fail(TFG_ERR_NOT_IMPLEMENTED, "String GROUP BY key longer than 15 bytes (serialized method)");
+        if (e) {
+            a->long_key = true;
+            return fail(TFG_ERR_NOT_IMPLEMENTED, "String GROUP BY key longer than 15 bytes (serialized method)");
+        }
     }
     TiledIn tin{};
     tin.rec = (const uint64_t *)(sb + o_rec1);
@@ -2438,6 +2452,128 @@ int consume_common(tfg_agg *a, int mode, const RowPred &pred, const void *keys, 
 
 } // namespace
 
+// ---------------------------------------------------------------- the serialized method (serial.h)
+// Key columns + states of an aggregator's groups in temporary device buffers (tfg_agg_result_keys).
+struct AggExtract {
+    uint64_t G = 0;
+    int nkeys = 0, n_aggs = 0;
+    std::vector<void *> bufs;
+    void *kc[8] = {};
+    uint64_t *ko[8] = {};
+    uint8_t *kn[8] = {};
+    void *st[AGG_MAX] = {};
+    uint8_t *sn[AGG_MAX] = {};
+    Ctx *ctx = nullptr;
+    ~AggExtract() {
+        if (ctx) (void)hipStreamSynchronize(ctx->stream);
+        for (void *p : bufs) (void)hipFree(p);
+    }
+    int alloc(size_t bytes, void **p) {
+        TFG_HIP(hipMalloc(p, std::max<size_t>(bytes, 8)));
+        bufs.push_back(*p);
+        return TFG_OK;
+    }
+};
+
+static int agg_extract(tfg_agg *a, AggExtract &e) {
+    e.ctx = a->ctx;
+    uint64_t G = 0;
+    if (int rc = tfg_agg_size(a, &G)) return rc;
+    e.G = G;
+    e.nkeys = a->kp.nkeys;
+    e.n_aggs = a->sdict ? a->inner->S.n_aggs : a->S.n_aggs;
+    if (G == 0) return TFG_OK;
+    uint64_t chars = 0;
+    bool has_str = false;
+    for (int j = 0; j < e.nkeys; ++j) has_str |= a->key_types[j] == TFG_STRING;
+    if (has_str) { // the chars size first (TFG_ERR_CAPACITY reports it)
+        void *dummy;
+        if (int rc = e.alloc(8, &dummy)) return rc;
+        void *pc[8];
+        uint64_t *po[8];
+        for (int j = 0; j < 8; ++j) {
+            pc[j] = dummy;
+            po[j] = (uint64_t *)dummy;
+        }
+        const int rc = tfg_agg_result_keys(a, pc, po, nullptr, nullptr, nullptr, G, 0, nullptr, &chars);
+        if (rc && rc != TFG_ERR_CAPACITY) return rc;
+    }
+    for (int j = 0; j < e.nkeys; ++j) {
+        void *p;
+        const bool str = a->key_types[j] == TFG_STRING;
+        if (int rc = e.alloc(str ? chars : G * type_width(a->key_types[j]), &p)) return rc;
+        e.kc[j] = p;
+        if (str) {
+            if (int rc = e.alloc(G * 8, &p)) return rc;
+            e.ko[j] = (uint64_t *)p;
+        }
+        if (int rc = e.alloc(G, &p)) return rc;
+        e.kn[j] = (uint8_t *)p;
+    }
+    for (int i = 0; i < e.n_aggs; ++i) {
+        int t = 0, w = 0;
+        if (int rc = tfg_agg_result_type(a, i, &t, &w)) return rc;
+        void *p;
+        if (int rc = e.alloc(G * (size_t)w, &p)) return rc;
+        e.st[i] = p;
+        if (int rc = e.alloc(G, &p)) return rc;
+        e.sn[i] = (uint8_t *)p;
+    }
+    return tfg_agg_result_keys(a, e.kc, e.ko, e.kn, e.st, e.sn, G, chars, nullptr, nullptr);
+}
+
+// rows -> dictionary group ids (in pack_buf) -> the inner aggregator
+static int serial_consume(tfg_agg *a, const void *const *key_cols, const uint64_t *const *key_offsets,
+                          const uint8_t *const *key_nullmaps, const void *const *vals, const uint8_t *const *val_nullmaps,
+                          const uint8_t *mask, int64_t n, bool partial) {
+    if (n <= 0) return n == 0 ? TFG_OK : fail(TFG_ERR_INVALID_ARG, "negative row count");
+    if (int rc = set_device(a->ctx)) return rc;
+    if (int rc = a->ensure_pack((size_t)n)) return rc;
+    uint32_t *gid = (uint32_t *)a->pack_buf;
+    if (int rc = serial_dict_assign(a->sdict, key_cols, key_offsets, key_nullmaps, mask, n, gid)) return rc;
+    if (partial) return tfg_agg_consume_partial(a->inner, gid, nullptr, vals, val_nullmaps, n);
+    return tfg_agg_consume(a->inner, gid, nullptr, vals, val_nullmaps, mask, n);
+}
+
+// Moves an aggregator to the serialized method: a dictionary over its key columns, an inner
+// aggregator over UInt32 group ids, and (for a packed-key aggregator that already holds groups)
+// its groups merged in as partial states.
+static int serial_adopt(tfg_agg *a) {
+    SerialDict *d = nullptr;
+    if (int rc = serial_dict_create(a->ctx, a->kp.nkeys, a->key_types, a->key_collators, &d)) return rc;
+    tfg_agg *in = nullptr;
+    if (int rc = tfg_agg_create(static_cast<tfg_ctx *>(a->ctx), TFG_UINT32, a->S.n_aggs, a->c_kinds, a->c_types, a->c_scales, &a->c_params, &in)) {
+        serial_dict_destroy(d);
+        return rc;
+    }
+    AggExtract e;
+    if (a->n_groups) {
+        if (int rc = agg_extract(a, e)) {
+            serial_dict_destroy(d);
+            tfg_agg_destroy(in);
+            return rc;
+        }
+    }
+    a->sdict = d;
+    a->inner = in;
+    a->long_key = false;
+    if (e.G) return serial_consume(a, e.kc, e.ko, e.kn, e.st, e.sn, nullptr, (int64_t)e.G, true);
+    return TFG_OK;
+}
+
+// tfg_agg_merge when either side uses the serialized method: src's groups as key columns + states
+static int merge_through_keys(tfg_agg *dst, tfg_agg *src) {
+    TFG_CHECK(dst->kp.nkeys == src->kp.nkeys, TFG_ERR_LOGICAL, "merging aggregators of different signatures");
+    for (int j = 0; j < dst->kp.nkeys; ++j)
+        TFG_CHECK(dst->key_types[j] == src->key_types[j], TFG_ERR_LOGICAL, "merging aggregators of different signatures");
+    TFG_HIP(hipStreamSynchronize(src->ctx->stream));
+    AggExtract e;
+    if (int rc = agg_extract(src, e)) return rc;
+    if (e.G == 0) return TFG_OK;
+    TFG_HIP(hipStreamSynchronize(src->ctx->stream));
+    return tfg_agg_consume_partial_keys(dst, e.kc, e.ko, e.kn, e.st, e.sn, (int64_t)e.G);
+}
+
 extern "C" {
 
 int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds, const int *arg_types,
@@ -2573,12 +2709,19 @@ int tfg_agg_destroy(tfg_agg *a) {
     }
     if (a->pack_buf) (void)hipFree(a->pack_buf);
     if (a->pack_err) (void)hipFree(a->pack_err);
+    if (a->sdict) serial_dict_destroy(a->sdict);
+    if (a->inner) tfg_agg_destroy(a->inner);
     delete a;
     return TFG_OK;
 }
 
 int tfg_agg_reset(tfg_agg *a) {
     TFG_CHECK(a, TFG_ERR_INVALID_ARG, "agg is null");
+    if (a->sdict) {
+        if (int rc = set_device(a->ctx)) return rc;
+        serial_dict_reset(a->sdict);
+        return tfg_agg_reset(a->inner);
+    }
     if (a->nokey) {
         if (int rc = set_device(a->ctx)) return rc;
         size_t bytes = a->carve_groups(nullptr, a->cap[a->cur], a->st[a->cur]);
@@ -2592,6 +2735,8 @@ int tfg_agg_reset(tfg_agg *a) {
 
 int tfg_agg_consume(tfg_agg *a, const void *keys, const uint8_t *key_nullmap, const void *const *args,
                     const uint8_t *const *arg_nullmaps, const uint8_t *mask, int64_t n) {
+    TFG_CHECK(a, TFG_ERR_INVALID_ARG, "agg is null");
+    TFG_CHECK(!a->sdict, TFG_ERR_NOT_IMPLEMENTED, "serialized GROUP BY keys: consume through tfg_agg_consume_keys");
     RowPred pred{};
     if (mask) {
         pred.kind = 1;
@@ -2603,7 +2748,8 @@ int tfg_agg_consume(tfg_agg *a, const void *keys, const uint8_t *key_nullmap, co
 int tfg_agg_consume_filtered(tfg_agg *a, int pred_type, const void *pred_col, const uint8_t *pred_nullmap, int op,
                              int scalar_type, const void *scalar_host, const void *keys, const uint8_t *key_nullmap,
                              const void *const *args, const uint8_t *const *arg_nullmaps, int64_t n) {
-    TFG_CHECK(pred_col && scalar_host, TFG_ERR_INVALID_ARG, "null predicate");
+    TFG_CHECK(a && pred_col && scalar_host, TFG_ERR_INVALID_ARG, "null argument");
+    TFG_CHECK(!a->sdict, TFG_ERR_NOT_IMPLEMENTED, "serialized GROUP BY keys: consume through tfg_agg_consume_keys");
     TFG_CHECK(is_fixed_numeric(pred_type) && is_fixed_numeric(scalar_type), TFG_ERR_ILLEGAL_TYPE,
               "unsupported predicate types %d / %d", pred_type, scalar_type);
     TFG_CHECK(op >= TFG_EQ && op <= TFG_GE, TFG_ERR_INVALID_ARG, "bad comparison op %d", op);
@@ -2619,12 +2765,16 @@ int tfg_agg_consume_filtered(tfg_agg *a, int pred_type, const void *pred_col, co
 
 int tfg_agg_consume_partial(tfg_agg *a, const void *keys, const uint8_t *key_nullmap, const void *const *states,
                             const uint8_t *const *state_nullmaps, int64_t n) {
+    TFG_CHECK(a, TFG_ERR_INVALID_ARG, "agg is null");
+    TFG_CHECK(!a->sdict, TFG_ERR_NOT_IMPLEMENTED,
+              "serialized GROUP BY keys have no packed form: merge through tfg_agg_consume_partial_keys");
     RowPred pred{};
     return consume_common(a, MODE_PARTIAL, pred, keys, key_nullmap, states, state_nullmaps, n);
 }
 
 int tfg_agg_merge(tfg_agg *dst, tfg_agg *src) {
     TFG_CHECK(dst && src, TFG_ERR_INVALID_ARG, "null agg");
+    if (dst->sdict || src->sdict) return merge_through_keys(dst, src);
     TFG_CHECK(dst->key_type == src->key_type && dst->S.n_aggs == src->S.n_aggs && dst->B == src->B,
               TFG_ERR_LOGICAL, "merging aggregators of different signatures");
     for (int i = 0; i < dst->S.n_aggs; ++i)
@@ -2654,12 +2804,14 @@ int tfg_agg_merge(tfg_agg *dst, tfg_agg *src) {
 
 int tfg_agg_size(tfg_agg *a, uint64_t *out_groups) {
     TFG_CHECK(a && out_groups, TFG_ERR_INVALID_ARG, "null argument");
-    *out_groups = a->n_groups;
+    *out_groups = a->sdict ? a->inner->n_groups : a->n_groups;
     return TFG_OK;
 }
 
 int tfg_agg_result_type(tfg_agg *a, int i, int *out_type, int *out_width) {
-    TFG_CHECK(a && i >= 0 && i < a->S.n_aggs, TFG_ERR_INVALID_ARG, "bad aggregate index");
+    TFG_CHECK(a, TFG_ERR_INVALID_ARG, "agg is null");
+    if (a->sdict) return tfg_agg_result_type(a->inner, i, out_type, out_width);
+    TFG_CHECK(i >= 0 && i < a->S.n_aggs, TFG_ERR_INVALID_ARG, "bad aggregate index");
     if (out_type) *out_type = a->result_type[i];
     if (out_width) *out_width = a->result_width[i];
     return TFG_OK;
@@ -2668,6 +2820,8 @@ int tfg_agg_result_type(tfg_agg *a, int i, int *out_type, int *out_width) {
 int tfg_agg_result(tfg_agg *a, void *out_keys, uint8_t *out_key_nullmap, void *const *out_states,
                    uint8_t *const *out_state_nullmaps, uint64_t capacity, uint64_t *out_groups_host) {
     TFG_CHECK(a, TFG_ERR_INVALID_ARG, "agg is null");
+    TFG_CHECK(!a->sdict, TFG_ERR_NOT_IMPLEMENTED,
+              "serialized GROUP BY keys have no packed form: read them with tfg_agg_result_keys");
     if (out_groups_host) *out_groups_host = a->n_groups;
     if (a->n_groups > capacity) return fail(TFG_ERR_CAPACITY, "result needs %llu groups, capacity %llu",
                                             (unsigned long long)a->n_groups, (unsigned long long)capacity);
@@ -2696,9 +2850,10 @@ static int pack_keys(tfg_agg *a, const void *const *key_cols, const uint64_t *co
         TFG_CHECK(key_cols[j], TFG_ERR_INVALID_ARG, "key column %d is null", j);
         kp.col[j] = key_cols[j];
         kp.nullmap[j] = key_nullmaps ? key_nullmaps[j] : nullptr;
-        if (kp.nullmap[j] && kp.kind == WK_FIXED)
-            TFG_CHECK(kp.off[kp.nkeys - 1] + kp.width[kp.nkeys - 1] <= 15, TFG_ERR_NOT_IMPLEMENTED,
-                      "nullable keys need a spare byte of the 16-byte packed key (nullable_keys256 not supported)");
+        if (kp.nullmap[j] && kp.kind == WK_FIXED && kp.off[kp.nkeys - 1] + kp.width[kp.nkeys - 1] > 15) {
+            a->long_key = true; // nullable_keys256's tuples: the serialized method takes them
+            return fail(TFG_ERR_NOT_IMPLEMENTED, "nullable keys of 16 bytes: no spare byte in the packed key");
+        }
     }
     if (kp.kind == WK_STRING) {
         TFG_CHECK(key_offsets && key_offsets[0], TFG_ERR_INVALID_ARG, "String key needs its offsets");
@@ -2717,8 +2872,10 @@ static int pack_keys(tfg_agg *a, const void *const *key_cols, const uint64_t *co
         unsigned err = 0;
         TFG_HIP(hipMemcpyAsync(&err, a->pack_err, sizeof(unsigned), hipMemcpyDeviceToHost, a->ctx->stream));
         TFG_HIP(hipStreamSynchronize(a->ctx->stream));
-        TFG_CHECK(!err, TFG_ERR_NOT_IMPLEMENTED,
-                  "String GROUP BY key longer than 15 bytes (after the collator's sort key): not supported");
+        if (err) {
+            a->long_key = true; // key_string past 15 bytes: the serialized method takes them
+            return fail(TFG_ERR_NOT_IMPLEMENTED, "String GROUP BY key longer than 15 bytes");
+        }
     }
     return TFG_OK;
 }
@@ -2726,44 +2883,92 @@ static int pack_keys(tfg_agg *a, const void *const *key_cols, const uint64_t *co
 int tfg_agg_create_keys(tfg_ctx *ctx, int nkeys, const int *key_types, const int *key_collators, int n_aggs,
                         const int *agg_kinds, const int *arg_types, const int *arg_scales, const tfg_agg_params *params,
                         tfg_agg **out) {
-    TFG_CHECK(ctx && out && key_types, TFG_ERR_INVALID_ARG, "null argument");
-    TFG_CHECK(nkeys >= 1 && nkeys <= 4, TFG_ERR_NOT_IMPLEMENTED, "%d GROUP BY keys: 1-4 supported", nkeys);
+    TFG_CHECK(ctx && out && key_types && agg_kinds, TFG_ERR_INVALID_ARG, "null argument");
+    TFG_CHECK(nkeys >= 1 && nkeys <= 8, TFG_ERR_NOT_IMPLEMENTED, "%d GROUP BY keys: 1-8 supported", nkeys);
+    TFG_CHECK(n_aggs >= 1 && n_aggs <= AGG_MAX, TFG_ERR_NOT_IMPLEMENTED, "n_aggs %d out of range [1,%d]", n_aggs, AGG_MAX);
+    if (nkeys == 1 && key_types[0] != TFG_STRING && type_width(key_types[0]) <= 8)
+        return tfg_agg_create(ctx, key_types[0], n_aggs, agg_kinds, arg_types, arg_scales, params, out);
+    // chooseAggregationMethod: one String key -> key_string; fixed keys within 16 bytes -> keys128;
+    // anything else (String with other keys, wider fixed tuples, more than 4 keys) -> serialized
     KeyPack kp{};
     kp.nkeys = nkeys;
-    if (nkeys == 1 && key_types[0] != TFG_STRING)
-        return tfg_agg_create(ctx, key_types[0], n_aggs, agg_kinds, arg_types, arg_scales, params, out);
-    if (key_types[0] == TFG_STRING) {
-        TFG_CHECK(nkeys == 1, TFG_ERR_NOT_IMPLEMENTED, "String keys combined with other keys (serialized method)");
-        kp.kind = WK_STRING;
-        kp.collator = key_collators ? key_collators[0] : TFG_COLLATOR_NONE;
-        TFG_CHECK(kp.collator >= TFG_COLLATOR_NONE && kp.collator <= TFG_COLLATOR_BIN_PADDING, TFG_ERR_NOT_IMPLEMENTED,
-                  "collator %d not supported", kp.collator);
-    } else {
-        kp.kind = WK_FIXED;
-        int off = 0;
-        for (int j = 0; j < nkeys; ++j) {
-            const int t = key_types[j];
-            TFG_CHECK(t != TFG_STRING && type_width(t) > 0, TFG_ERR_ILLEGAL_TYPE,
-                      "GROUP BY key %d of type %d cannot be packed", j, t); // floats: raw bits, like packFixed
-            kp.width[j] = (int)type_width(t);
-            kp.off[j] = off;
-            off += kp.width[j];
+    bool serialized = nkeys > 4;
+    int off = 0;
+    for (int j = 0; j < nkeys; ++j) {
+        const int t = key_types[j];
+        const int c = key_collators ? key_collators[j] : TFG_COLLATOR_NONE;
+        if (t == TFG_STRING) {
+            TFG_CHECK(c >= TFG_COLLATOR_NONE && c <= TFG_COLLATOR_BIN_PADDING, TFG_ERR_NOT_IMPLEMENTED,
+                      "collator %d not supported", c);
+            serialized |= nkeys > 1;
+            continue;
         }
-        TFG_CHECK(off <= 16, TFG_ERR_NOT_IMPLEMENTED, "fixed keys of %d bytes exceed keys128", off);
-        TFG_CHECK(kp.width[0] == 16 ? nkeys == 1 : true, TFG_ERR_NOT_IMPLEMENTED, "Decimal128 key with other keys");
+        const size_t w = type_width(t);
+        TFG_CHECK(w > 0 && w <= 32, TFG_ERR_ILLEGAL_TYPE, "GROUP BY key %d of type %d cannot be packed", j, t);
+        if (j < 4) {
+            kp.width[j] = (int)w; // floats: raw bits, like packFixed
+            kp.off[j] = off;
+        }
+        off += (int)w;
+        serialized |= w > 8 && nkeys > 1; // a Decimal128 key with other keys
     }
+    serialized |= off > 16;
     tfg_agg_params p{};
     if (params) p = *params;
-    if (int rc = tfg_agg_create(ctx, TFG_KEYS128, n_aggs, agg_kinds, arg_types, arg_scales, &p, out)) return rc;
-    (*out)->kp = kp;
-    for (int j = 0; j < nkeys; ++j) (*out)->key_types[j] = key_types[j];
+    tfg_agg *a = nullptr;
+    if (serialized) {
+        a = new tfg_agg();
+        a->ctx = ctx;
+        a->key_type = TFG_KEYS128;
+        a->S.n_aggs = n_aggs;
+    } else {
+        kp.kind = key_types[0] == TFG_STRING ? WK_STRING : WK_FIXED;
+        kp.collator = key_collators ? key_collators[0] : TFG_COLLATOR_NONE;
+        if (int rc = tfg_agg_create(ctx, TFG_KEYS128, n_aggs, agg_kinds, arg_types, arg_scales, &p, &a)) return rc;
+    }
+    a->kp = kp;
+    if (serialized) a->kp.nkeys = nkeys;
+    for (int j = 0; j < nkeys; ++j) {
+        a->key_types[j] = key_types[j];
+        a->key_collators[j] = key_collators ? key_collators[j] : TFG_COLLATOR_NONE;
+    }
+    for (int i = 0; i < n_aggs; ++i) {
+        a->c_kinds[i] = agg_kinds[i];
+        a->c_types[i] = arg_types ? arg_types[i] : 0;
+        a->c_scales[i] = arg_scales ? arg_scales[i] : 0;
+    }
+    a->c_params = p;
+    if (serialized) {
+        if (int rc = serial_adopt(a)) {
+            tfg_agg_destroy(a);
+            return rc;
+        }
+    }
+    *out = a;
     return TFG_OK;
 }
+
+static int consume_keys_packed(tfg_agg *a, const void *const *key_cols, const uint64_t *const *key_offsets,
+                               const uint8_t *const *key_nullmaps, const void *const *args,
+                               const uint8_t *const *arg_nullmaps, const uint8_t *mask, int64_t n);
 
 int tfg_agg_consume_keys(tfg_agg *a, const void *const *key_cols, const uint64_t *const *key_offsets,
                          const uint8_t *const *key_nullmaps, const void *const *args, const uint8_t *const *arg_nullmaps,
                          const uint8_t *mask, int64_t n) {
     TFG_CHECK(a, TFG_ERR_INVALID_ARG, "agg is null");
+    if (a->sdict) return serial_consume(a, key_cols, key_offsets, key_nullmaps, args, arg_nullmaps, mask, n, false);
+    a->long_key = false;
+    int rc = consume_keys_packed(a, key_cols, key_offsets, key_nullmaps, args, arg_nullmaps, mask, n);
+    if (rc == TFG_ERR_NOT_IMPLEMENTED && a->long_key) { // nothing was folded in: move, then take the block
+        if ((rc = serial_adopt(a))) return rc;
+        return serial_consume(a, key_cols, key_offsets, key_nullmaps, args, arg_nullmaps, mask, n, false);
+    }
+    return rc;
+}
+
+static int consume_keys_packed(tfg_agg *a, const void *const *key_cols, const uint64_t *const *key_offsets,
+                               const uint8_t *const *key_nullmaps, const void *const *args,
+                               const uint8_t *const *arg_nullmaps, const uint8_t *mask, int64_t n) {
     if (!a->kp.kind)
         return tfg_agg_consume(a, key_cols ? key_cols[0] : nullptr, key_nullmaps ? key_nullmaps[0] : nullptr, args,
                                arg_nullmaps, mask, n);
@@ -2794,12 +2999,18 @@ int tfg_agg_consume_partial_keys(tfg_agg *a, const void *const *key_cols, const 
                                  const uint8_t *const *key_nullmaps, const void *const *states,
                                  const uint8_t *const *state_nullmaps, int64_t n) {
     TFG_CHECK(a, TFG_ERR_INVALID_ARG, "agg is null");
+    if (a->sdict) return serial_consume(a, key_cols, key_offsets, key_nullmaps, states, state_nullmaps, nullptr, n, true);
     if (!a->kp.kind)
         return tfg_agg_consume_partial(a, key_cols ? key_cols[0] : nullptr, key_nullmaps ? key_nullmaps[0] : nullptr,
                                        states, state_nullmaps, n);
     if (n <= 0) return n == 0 ? TFG_OK : fail(TFG_ERR_INVALID_ARG, "negative row count");
     if (int rc = set_device(a->ctx)) return rc;
-    if (int rc = pack_keys(a, key_cols, key_offsets, key_nullmaps, n)) return rc;
+    a->long_key = false;
+    if (int rc = pack_keys(a, key_cols, key_offsets, key_nullmaps, n)) {
+        if (rc != TFG_ERR_NOT_IMPLEMENTED || !a->long_key) return rc;
+        if ((rc = serial_adopt(a))) return rc;
+        return serial_consume(a, key_cols, key_offsets, key_nullmaps, states, state_nullmaps, nullptr, n, true);
+    }
     return tfg_agg_consume_partial(a, a->pack_buf, nullptr, states, state_nullmaps, n);
 }
 
@@ -2807,6 +3018,21 @@ int tfg_agg_result_keys(tfg_agg *a, void *const *out_key_cols, uint64_t *const *
                         uint8_t *const *out_key_nullmaps, void *const *out_states, uint8_t *const *out_state_nullmaps,
                         uint64_t capacity, uint64_t chars_capacity, uint64_t *out_groups_host, uint64_t *out_chars_host) {
     TFG_CHECK(a, TFG_ERR_INVALID_ARG, "agg is null");
+    if (a->sdict) { // group ids from the inner aggregator, then their key tuples from the dictionary
+        const uint64_t G = a->inner->n_groups;
+        if (out_groups_host) *out_groups_host = G;
+        if (out_chars_host) *out_chars_host = 0;
+        if (G > capacity)
+            return fail(TFG_ERR_CAPACITY, "result needs %llu groups, capacity %llu", (unsigned long long)G,
+                        (unsigned long long)capacity);
+        if (G == 0) return TFG_OK;
+        if (int rc = set_device(a->ctx)) return rc;
+        if (int rc = a->ensure_pack(G)) return rc;
+        if (int rc = tfg_agg_result(a->inner, a->pack_buf, nullptr, out_states, out_state_nullmaps, capacity, nullptr))
+            return rc;
+        return serial_dict_unpack(a->sdict, (const uint32_t *)a->pack_buf, G, out_key_cols, out_key_offsets,
+                                  out_key_nullmaps, chars_capacity, out_chars_host);
+    }
     if (!a->kp.kind) {
         if (out_chars_host) *out_chars_host = 0;
         return tfg_agg_result(a, out_key_cols ? out_key_cols[0] : nullptr, out_key_nullmaps ? out_key_nullmaps[0] : nullptr,

@@ -10,7 +10,8 @@ namespace tfa {
 // ================================================================ Aggregator
 Aggregator::Aggregator(Context &ctx, const Params &params) : ctx_(ctx), params_(params) {
     // chooseAggregationMethod (Aggregator.cpp:394-537): one fixed key -> key8..key64; several
-    // fixed keys or one String key -> the packed 16-byte methods (keys128 / key_string)
+    // fixed keys or one String key -> the packed 16-byte methods (keys128 / key_string), and
+    // past those (String with other keys, wider tuples) serialized: tfg_agg_create_keys decides
     int key_type = 0;
     std::vector<int> packed_types;
     for (const auto &k : params_.keys) {
@@ -21,7 +22,7 @@ Aggregator::Aggregator(Context &ctx, const Params &params) : ctx_(ctx), params_(
         key_type_ = key_types_[0];
         key_type = key_type_.type;
     }
-    packed_ = params_.keys.size() > 1 || (!params_.keys.empty() && key_type_.isString());
+    packed_ = params_.keys.size() > 1 || (!params_.keys.empty() && (key_type_.isString() || key_type_.width() > 8));
     std::vector<int> arg_types, arg_scales;
     for (const auto &d : params_.aggregates) {
         int kind;
@@ -234,16 +235,16 @@ Block Aggregator::convertToBlock(bool final) const {
             kcols.push_back(c);
         }
         uint64_t chars = 0;
-        if (key_types_[0].isString()) { // chars size first (TFG_ERR_CAPACITY reports it)
-            std::shared_ptr<IColumn> &c = kcols[0];
-            DeviceBuffer probe(ctx_, 1);
-            void *pk[1] = {probe.data()};
-            uint64_t *po[1] = {(uint64_t *)c->offsets->data()};
-            uint8_t *pn[1] = {c->nullmap ? (uint8_t *)c->nullmap->data() : nullptr};
-            const int rc = tfg_agg_result_keys(agg_, pk, po, pn, sp.data(), snp.data(), g, 0, &got, &chars);
+        bool has_str = false;
+        for (const DataType &t : key_types_) has_str |= t.isString();
+        if (has_str) { // chars size first (TFG_ERR_CAPACITY reports the largest String key's)
+            DeviceBuffer probe(ctx_, 8);
+            std::vector<void *> pk(kcols.size(), probe.data());
+            std::vector<uint64_t *> po(kcols.size(), (uint64_t *)probe.data());
+            const int rc = tfg_agg_result_keys(agg_, pk.data(), po.data(), nullptr, nullptr, nullptr, g, 0, &got, &chars);
             if (rc != TFG_ERR_CAPACITY) check(rc, "tfg_agg_result_keys");
-            c->chars = chars;
-            c->data = std::make_shared<DeviceBuffer>(ctx_, std::max<uint64_t>(chars, 1));
+            for (auto &c : kcols)
+                if (c->type.isString()) c->data = std::make_shared<DeviceBuffer>(ctx_, std::max<uint64_t>(chars, 1));
         }
         for (auto &c : kcols) {
             kp.push_back(c->data->data());
@@ -254,6 +255,13 @@ Block Aggregator::convertToBlock(bool final) const {
                                   &chars),
               "tfg_agg_result_keys");
         ctx_.sync();
+        for (auto &c : kcols) // each String column's own chars: its last end offset
+            if (c->type.isString()) {
+                uint64_t end = 0;
+                if (g) check(tfg_download(ctx_.raw(), &end, (const uint64_t *)c->offsets->data() + (g - 1), 8),
+                             "tfg_download");
+                c->chars = end;
+            }
         for (size_t j = 0; j < kcols.size(); ++j) out.insert({kcols[j], kcols[j]->type, params_.keys[j]});
         for (size_t i = 0; i < states.size(); ++i)
             out.insert({states[i], states[i]->type, params_.aggregates[i].column_name});
