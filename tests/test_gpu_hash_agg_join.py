@@ -526,3 +526,32 @@ def test_groupby_two_pass_buckets(tfa, ctx, dev, orc):
                      r["states"][1].cpu().tolist()))
     want = sorted(zip(rr["keys"].view(np.int64).tolist(), rr["states"][0].tolist(), rr["states"][1].tolist()))
     assert got == want
+
+
+@pytest.mark.parametrize("filtered", [False, True])
+def test_groupby_tiled_narrow_and_wide_tiles(tfa, ctx, dev, orc, filtered):
+    """The tiled partition writes a tile whose kept keys all fit 32 bits as u32 keys + values
+    (12 B a row) and any other tile as {key, value} records: one consume whose tiles mix both
+    (runs of keys below 2^32, runs of full-range Int64 keys incl. negatives, the 2^32 - 1 / 2^32
+    boundary), through the C2 fast signature (sum Float64 + count) and the filtered consume."""
+    rng = np.random.default_rng(77)
+    n = 3_000_000
+    small = rng.integers(0, 1 << 20, n, dtype=np.int64)
+    big = rng.integers(-2**63, 2**63 - 1, 50_000, dtype=np.int64)[rng.integers(0, 50_000, n)]
+    edge = np.array([2**32 - 1, 2**32, 0, -1], dtype=np.int64)[rng.integers(0, 4, n)]
+    seg = (np.arange(n) // 40_000) % 5  # 40K-row segments: a tile of 8192 rows is all one kind or mixed
+    k = np.where(seg < 3, small, np.where(seg == 3, big, edge))
+    v = rng.integers(0, 1 << 20, n).astype(np.float64) / 256.0
+    f = rng.integers(0, 100, n, dtype=np.int64)
+    aggs = [(tfa.AGG_SUM, tfa.FLOAT64), (tfa.AGG_COUNT_ALL, 0)]
+    g = tfa.Aggregator(ctx, tfa.INT64, aggs)
+    kd, vd, fd = (torch.from_numpy(x).to(dev) for x in (k, v, f))
+    ref = orc.Agg(orc.INT64, [(0, orc.FLOAT64), (2, 0)])
+    if filtered:
+        g.consume_filtered(fd, tfa.LT, 60, kd, [vd, None])
+        ref.consume(k, [v, None], mask=(f < 60).astype(np.uint8))
+    else:
+        g.consume(kd, [vd, None], n=n)
+        ref.consume(k, [v, None], n=n)
+    assert g.size() == ref.size()
+    assert _gpu_rows(g.result(), np.int64, False) == _ref_rows(ref.result(), np.int64, False)

@@ -668,6 +668,7 @@ template <int A0, int A1, int A2> struct FastOps {
     static constexpr int op(int i) { return i == 0 ? A0 : (i == 1 ? A1 : A2); }
     static constexpr int NCOL = 1 + (A0 >= 2) + (A1 >= 2) + (A2 >= 2);
     static constexpr bool WIDE = false;
+    static constexpr bool NARROWABLE = NCOL == 2; // the tiled partition may write {u32 key}[], {value}[] tiles
     static constexpr int pos(int i) { return 1 + (i > 0 && A0 >= 2) + (i > 1 && A1 >= 2); }
     struct Row {
         uint64_t key;
@@ -690,6 +691,15 @@ template <int A0, int A1, int A2> struct FastOps {
             for (int i = 0; i < 3; ++i)
                 if (op(i) >= 2) v.v[i] = rec[pos(i)];
         }
+    }
+    // row `off` of narrow tile `tile` (slot of TRS rows: TRS u32 keys, then TRS u64 values)
+    __device__ __forceinline__ void load_narrow(const uint64_t *rec, int64_t tile, int TRS, uint32_t off, Row &v) const {
+        const uint32_t *ks = reinterpret_cast<const uint32_t *>(rec + tile * (int64_t)TRS * 2);
+        v.key = ks[off];
+        const uint64_t w = reinterpret_cast<const uint64_t *>(ks + TRS)[off];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+            if (op(i) >= 2) v.v[i] = w;
     }
     __device__ __forceinline__ uint64_t key(const Row &v) const { return v.key; }
     __device__ __forceinline__ bool knull(const Row &) const { return false; }
@@ -748,11 +758,13 @@ template <int A0, int A1, int A2> struct WideFastOps {
     static constexpr int op(int i) { return i == 0 ? A0 : (i == 1 ? A1 : A2); }
     static constexpr int NCOL = 2 + (A0 >= 2) + (A1 >= 2) + (A2 >= 2);
     static constexpr bool WIDE = true;
+    static constexpr bool NARROWABLE = false;
     static constexpr int pos(int i) { return 2 + (i > 0 && A0 >= 2) + (i > 1 && A1 >= 2); }
     struct Row {
         uint64_t key, khi;
         uint64_t v[3];
     };
+    __device__ __forceinline__ void load_narrow(const uint64_t *, int64_t, int, uint32_t, Row &) const {}
     const AggSpec &S;
     int mode;
     __device__ __forceinline__ void load(const RowsIO &rows, int64_t r, Row &v) const {
@@ -1072,8 +1084,14 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
 #pragma unroll
                         for (uint32_t st = CH / 2; st > 0; st >>= 1)
                             if (s_pref[lo + st] <= i) lo += st;
-                        int64_t r = (int64_t)(t0 + (int)lo) * tin.TR + (s_ent[lo] & 0xFFFFu) + (i - s_pref[lo]);
-                        ops.load(src, r, v[u]);
+                        const uint32_t ent = s_ent[lo], off = (ent & 0x7FFFu) + (i - s_pref[lo]);
+                        if constexpr (Ops::NARROWABLE) {
+                            if (ent & TILE_NARROW) {
+                                ops.load_narrow(tin.rec, t0 + (int)lo, tin.TR, off, v[u]);
+                                continue;
+                            }
+                        }
+                        ops.load(src, (int64_t)(t0 + (int)lo) * tin.TR + off, v[u]);
                     }
                 };
                 typename Ops::Row vn[RT];
@@ -1881,7 +1899,7 @@ int consume_fast_tiled(tfg_agg *a, int fast, const RowPred &pred, const void *ke
     tin.rec = (const uint64_t *)(sb + o_rec);
     tin.tile_hist = (const uint32_t *)(sb + o_hist);
     tin.T = tg.sg.T;
-    tin.TR = tg.sg.TR;
+    tin.TR = tg.sg.TRS; // tile slot stride
     tin.spill[0] = (uint64_t *)(sb + o_sp0);
     tin.spill[1] = (uint64_t *)(sb + o_sp1);
     tin.cursor = (unsigned long long *)(sb + o_cur);
@@ -2031,7 +2049,7 @@ int consume_wide_tiled(tfg_agg *a, int code, Sel sel, const void *const *vals, i
     tin.rec = (const uint64_t *)(sb + o_rec1);
     tin.tile_hist = (const uint32_t *)(sb + o_hist1);
     tin.T = T1;
-    tin.TR = tg.sg.TR;
+    tin.TR = tg.sg.TRS; // tile slot stride
     tin.spill[0] = (uint64_t *)(sb + (two ? o_rec1 : o_sp0));
     tin.spill[1] = (uint64_t *)(sb + o_sp1);
     if (two) {
