@@ -52,7 +52,7 @@ NAME_MAP = [
 LEGS = [
     ("C2", r"^(agg\.fused|agg\.part\.(hist|tiled|scatter)|agg\.bucket\.tiled)$"),
     ("C3", r"^(join\.|part\.(hist|scatter)\.pass2)"),
-    ("codec", r"tfg::str_|codec"),
+    ("codec", r"tfg::str_|codec|lz4_"),
     ("C5", r"^(agg\.wide\.|agg\.(pack|unpack)_keys|agg\.bucket$)|wide_str"),
 ]
 
@@ -61,7 +61,7 @@ def short(name):
     for pat, s in NAME_MAP:
         if re.search(pat, name):
             return s
-    m = re.search(r"tfg::(\w+)", name)
+    m = re.search(r"tfg::(?:\(anonymous namespace\)::)?(\w+)", name)
     return ("tfg::" + m.group(1)) if m else name.split("(")[0][:60]
 
 
