@@ -1025,7 +1025,10 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
                 if (cells[u] >= 0) ops.add(T, cells[u], v[u]);
                 else miss[u] = true;
             }
-            __syncthreads();
+            // no barrier per step: a missing row (full table / inserts closed) looks its key up
+            // once more and otherwise spills; an insert of the same key by another wave in this
+            // step may not be visible yet, so the pass re-checks its spilled rows against the
+            // final table before flushing (below) — no key ends up in two groups
 #pragma unroll
             for (int u = 0; u < RT; ++u) {
                 if (!miss[u]) continue;
@@ -1074,16 +1077,25 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
                 // software pipeline: the next step's rows are loaded (address search + global
                 // loads issued) before this step's LDS probe / atomics, so HBM latency overlaps
                 // the table work instead of following it after every step barrier
+                // the tile of row i: the last entry with s_pref <= i.  A wave's 64 rows are
+                // consecutive, so two ballots over every CS-th prefix (one read per lane) bracket
+                // the wave's tiles, and each lane searches only that bracket (4-5 dependent LDS
+                // reads instead of log2(CH) = 10)
+                constexpr uint32_t CS = CH / 64;
+                const uint32_t coarse = s_pref[(threadIdx.x & 63u) * CS];
                 auto load_step = [&](uint32_t base, typename Ops::Row (&v)[RT], bool (&ok)[RT]) __attribute__((always_inline)) {
 #pragma unroll
                     for (int u = 0; u < RT; ++u) {
                         const uint32_t i = base + u * BT + threadIdx.x;
+                        const uint32_t w0 = i - (threadIdx.x & 63u);
+                        const uint32_t c_lo = (uint32_t)__popcll(__ballot(coarse <= w0)) - 1u;
+                        const uint32_t c_hi = (uint32_t)__popcll(__ballot(coarse <= w0 + 63u)) - 1u;
                         ok[u] = i < tot;
                         if (!ok[u]) continue;
-                        uint32_t lo = 0;
-#pragma unroll
-                        for (uint32_t st = CH / 2; st > 0; st >>= 1)
-                            if (s_pref[lo + st] <= i) lo += st;
+                        const uint32_t lo0 = c_lo * CS, len = (c_hi - c_lo + 1u) * CS;
+                        uint32_t lo = lo0;
+                        for (uint32_t st = (1u << (32 - __clz(len - 1u))) >> 1; st > 0; st >>= 1)
+                            if (lo + st < lo0 + len && s_pref[lo + st] <= i) lo += st;
                         const uint32_t ent = s_ent[lo], off = (ent & 0x7FFFu) + (i - s_pref[lo]);
                         if constexpr (Ops::NARROWABLE) {
                             if (ent & TILE_NARROW) {
@@ -1125,6 +1137,36 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
             }
         }
         ++pass;
+        __syncthreads();
+        { // re-check this pass's spilled rows against the final table: found -> add, else keep
+            // (kept rows are compacted in place; a chunk is read before any of it is rewritten)
+            const uint32_t nsp = (uint32_t)T.ctrl->spill_w;
+            __shared__ unsigned long long s_keep;
+            if (threadIdx.x == 0) s_keep = 0;
+            for (uint32_t c0 = 0; c0 < nsp; c0 += BT) {
+                typename Ops::Row v1[1];
+                const bool have = c0 + threadIdx.x < nsp;
+                if (have) ops.load(spill, c0 + threadIdx.x, v1[0]);
+                __syncthreads();
+                if (have) {
+                    int cell;
+                    const uint64_t ku = ops.key(v1[0]);
+                    if constexpr (Ops::WIDE) {
+                        const uint64_t lo[1] = {ku}, hi[1] = {ops.hi(v1[0])}, t1[1] = {wide_tag(ku, ops.hi(v1[0]))};
+                        const bool ok1[1] = {true};
+                        int c1[1];
+                        T.find_wide_multi<1>(lo, hi, t1, ok1, false, c1);
+                        cell = c1[0];
+                    } else {
+                        cell = T.find_or_insert(ku, false, false, false);
+                    }
+                    if (cell >= 0) ops.add(T, cell, v1[0]);
+                    else ops.store(spill, (int64_t)atomicAdd(&s_keep, 1ull), v1[0]);
+                }
+                __syncthreads();
+            }
+            if (nsp && threadIdx.x == 0) T.ctrl->spill_w = s_keep;
+        }
         __syncthreads();
         T.flush(out, out_base);
         __syncthreads();
