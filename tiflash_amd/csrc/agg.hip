@@ -713,6 +713,36 @@ template <int A0, int A1, int A2> struct FastOps {
             if (op(i) == 4) lds_add_i128(T.acc_cell(i, cell), v.v[i], (int64_t)v.v[i] < 0 ? ~0ull : 0ull);
         }
     }
+    // the step's rows at once (cell < 0: skip): a Decimal64 -> Int128 sum issues every row's
+    // returning low-word add before any high-word add, so the carries' LDS round trips overlap
+    template <int R>
+    __device__ __forceinline__ void add_multi(Table &T, const int (&cell)[R], const Row (&v)[R]) const {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            if (op(i) != 4) continue;
+            uint64_t old[R];
+#pragma unroll
+            for (int u = 0; u < R; ++u)
+                if (cell[u] >= 0) old[u] = atomicAdd((unsigned long long *)T.acc_cell(i, cell[u]), (unsigned long long)v[u].v[i]);
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                if (cell[u] < 0) continue;
+                const uint64_t lo = v[u].v[i], carry = (old[u] + lo) < old[u] ? 1ull : 0ull;
+                atomicAdd((unsigned long long *)T.acc_cell(i, cell[u]) + 1,
+                          (unsigned long long)(((int64_t)lo < 0 ? ~0ull : 0ull) + carry));
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            if (cell[u] < 0) continue;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                if (op(i) == 1) atomicAdd((unsigned long long *)T.cnt_cell(i, cell[u]), 1ull);
+                if (op(i) == 2) atomicAdd((unsigned long long *)T.acc_cell(i, cell[u]), (unsigned long long)v[u].v[i]);
+                if (op(i) == 3) atomicAdd((double *)T.acc_cell(i, cell[u]), __longlong_as_double((long long)v[u].v[i]));
+            }
+        }
+    }
     __device__ __forceinline__ void store(const RowsIO &sp, int64_t w, const Row &v) const {
         uint64_t *rec = (uint64_t *)sp.key + w * NCOL;
         rec[0] = v.key;
@@ -785,6 +815,36 @@ template <int A0, int A1, int A2> struct WideFastOps {
             if (op(i) == 2) atomicAdd((unsigned long long *)T.acc_cell(i, cell), (unsigned long long)v.v[i]);
             if (op(i) == 3) atomicAdd((double *)T.acc_cell(i, cell), __longlong_as_double((long long)v.v[i]));
             if (op(i) == 4) lds_add_i128(T.acc_cell(i, cell), v.v[i], (int64_t)v.v[i] < 0 ? ~0ull : 0ull);
+        }
+    }
+    // the step's rows at once (cell < 0: skip): a Decimal64 -> Int128 sum issues every row's
+    // returning low-word add before any high-word add, so the carries' LDS round trips overlap
+    template <int R>
+    __device__ __forceinline__ void add_multi(Table &T, const int (&cell)[R], const Row (&v)[R]) const {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            if (op(i) != 4) continue;
+            uint64_t old[R];
+#pragma unroll
+            for (int u = 0; u < R; ++u)
+                if (cell[u] >= 0) old[u] = atomicAdd((unsigned long long *)T.acc_cell(i, cell[u]), (unsigned long long)v[u].v[i]);
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                if (cell[u] < 0) continue;
+                const uint64_t lo = v[u].v[i], carry = (old[u] + lo) < old[u] ? 1ull : 0ull;
+                atomicAdd((unsigned long long *)T.acc_cell(i, cell[u]) + 1,
+                          (unsigned long long)(((int64_t)lo < 0 ? ~0ull : 0ull) + carry));
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            if (cell[u] < 0) continue;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                if (op(i) == 1) atomicAdd((unsigned long long *)T.cnt_cell(i, cell[u]), 1ull);
+                if (op(i) == 2) atomicAdd((unsigned long long *)T.acc_cell(i, cell[u]), (unsigned long long)v[u].v[i]);
+                if (op(i) == 3) atomicAdd((double *)T.acc_cell(i, cell[u]), __longlong_as_double((long long)v[u].v[i]));
+            }
         }
     }
     __device__ __forceinline__ void store(const RowsIO &sp, int64_t w, const Row &v) const {
@@ -1018,13 +1078,13 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
             }
             if constexpr (Ops::WIDE) T.find_wide_multi<RT>(ku, kh, tg, ok, allow_insert, cells);
             else T.find_or_insert_multi<RT>(ku, nu, ok, allow_insert, cells);
+            int hit[RT];
 #pragma unroll
             for (int u = 0; u < RT; ++u) {
-                miss[u] = false;
-                if (!ok[u]) continue;
-                if (cells[u] >= 0) ops.add(T, cells[u], v[u]);
-                else miss[u] = true;
+                miss[u] = ok[u] && cells[u] < 0;
+                hit[u] = ok[u] ? cells[u] : -1;
             }
+            ops.add_multi(T, hit, v);
             // no barrier per step: a missing row (full table / inserts closed) looks its key up
             // once more and otherwise spills; an insert of the same key by another wave in this
             // step may not be visible yet, so the pass re-checks its spilled rows against the
