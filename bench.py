@@ -126,6 +126,17 @@ def load_pmc_traffic(kernel):
         return None
 
 
+def pmc_source():
+    """Which profile run (tools/profile.sh tag) and commit the PMC traffic figures come from."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            c = json.load(f).get("_calibration", {})
+        return {"file": "profiles/pmc_traffic.json", "tag": c.get("tag"), "commit": c.get("commit")}
+    except Exception:
+        return None
+
+
 def load_pmc_step(leg):
     """HBM bytes per bench step of a leg from the same PMC passes (profiles/pmc_traffic.json)."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -692,6 +703,7 @@ def main():
             rf["traffic"] = load_pmc_traffic(rf["kernel"])
             if rf["traffic"]:
                 rf["traffic_over_algorithmic"] = round(rf["traffic"] / rf["algorithmic_bytes_per_launch"], 3)
+                rf["traffic_source"] = pmc_source()
         line["roofline"] = rf
         line["pipeline_roofline"] = {"algorithmic_bytes_per_step": 24 * N, "achieved": round(24 * N / (ms * 1e-3) / 1e9, 1),
                                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -700,6 +712,7 @@ def main():
         if line["pipeline_roofline"]["traffic"]:
             line["pipeline_roofline"]["traffic_over_algorithmic"] = round(
                 line["pipeline_roofline"]["traffic"] / (24 * N), 3)
+            line["pipeline_roofline"]["traffic_source"] = pmc_source()
         line["kernels_ms_per_step"] = {kname: round(v[0] / args.steps, 4) for kname, v in sorted(prof.items())}
 
     if world == 1 and not args.no_variants:

@@ -21,6 +21,7 @@ import json
 import os
 import re
 import shutil
+import subprocess
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -30,7 +31,9 @@ NAME_MAP = [
     (r"part_hist_kernel<tfg::SelBucket", "agg.part.hist"),
     (r"part_scatter_staged_kernel<tfg::SelBucket.*true, true>", "agg.part.tiled"),
     (r"part_scatter.*<tfg::SelBucket", "agg.part.scatter"),
-    (r"agg_bucket_tiled_kernel", "agg.bucket.tiled"),
+    (r"agg_bucket_tiled_kernel<tfg::WideFastOps", "agg.wide.bucket.tiled"),
+    (r"agg_bucket_tiled_kernel<tfg::FastOps", "agg.bucket.tiled"),
+    (r"agg_bucket_tiled_kernel", "agg.bucket.tiled.other"),
     (r"part_hist_kernel<tfg::SelWide", "agg.wide.part.hist"),
     (r"part_scatter.*<tfg::SelWide", "agg.wide.part.scatter"),
     (r"agg_bucket_kernel<tfg::WideOps", "agg.wide.bucket"),
@@ -50,10 +53,11 @@ NAME_MAP = [
 ]
 # leg-specific kernels (by short name or raw-name regex)
 LEGS = [
+    ("C3v2", r"join_v2_"),
     ("C2", r"^(agg\.fused|agg\.part\.(hist|tiled|scatter)|agg\.bucket\.tiled)$"),
     ("C3", r"^(join\.|part\.(hist|scatter)\.pass2)"),
     ("codec", r"tfg::str_|codec|lz4_"),
-    ("C5", r"^(agg\.wide\.|agg\.(pack|unpack)_keys|agg\.bucket$)|wide_str"),
+    ("C5", r"^(agg\.wide\.|agg\.(pack|unpack)_keys|agg\.bucket$)|wide_str|regroup_"),
 ]
 
 
@@ -63,6 +67,25 @@ def short(name):
             return s
     m = re.search(r"tfg::(?:\(anonymous namespace\)::)?(\w+)", name)
     return ("tfg::" + m.group(1)) if m else name.split("(")[0][:60]
+
+
+# the kernel that ends one bench step of a leg: a leg's steady-state step is the window of its
+# dispatches after one step-end kernel up to and including the next (the first window also holds
+# one-off work such as the join build, so it is not used when a later window exists)
+STEP_END = {"C2": r"^agg\.result$", "C5": r"^agg\.result$", "C3": r"^join\.probe$",
+            "C3v2": r"join_v2_probe_kernel"}
+
+
+def step_windows(ds):
+    """{leg: [bytes of each complete step window, in order]} from one counter's dispatch list."""
+    acc, wins = collections.defaultdict(float), collections.defaultdict(list)
+    for _, s, leg, v in ds:
+        acc[leg] += v
+        pat = STEP_END.get(leg)
+        if pat and re.search(pat, s):
+            wins[leg].append(acc[leg])
+            acc[leg] = 0.0
+    return wins
 
 
 def leg_of(short_name, raw):
@@ -114,6 +137,7 @@ def bench_line(src, log):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tag")
+    ap.add_argument("--commit", default=None, help="commit the profiled tree was at (default: HEAD)")
     a = ap.parse_args()
     src = os.path.join(ROOT, "gpurun_out", f"prof_{a.tag}")
     out = os.path.join(ROOT, "profiles")
@@ -142,7 +166,13 @@ def main():
     # algorithmic bytes per launch where a kernel carries a leg's whole input
     alg = {("C2", "agg.part.tiled"): 24 * rows, ("C2", "agg.fused"): 24 * rows + 24 * groups,
            ("C2", "agg.part.hist"): 16 * rows}
-    traffic = {"_calibration": {"fetch_factor": factor, "basis": "MI355X_MICROARCH.md HBM section (x2 on gfx950)",
+    commit = a.commit
+    try:
+        commit = commit or subprocess.run(["git", "-C", ROOT, "rev-parse", "--short", "HEAD"], capture_output=True,
+                                text=True).stdout.strip() or None
+    except OSError:
+        commit = None
+    traffic = {"_calibration": {"tag": a.tag, "commit": commit, "fetch_factor": factor, "basis": "MI355X_MICROARCH.md HBM section (x2 on gfx950)",
                                 "measured_on_agg_part_tiled": round(measured, 4) if measured else None,
                                 "rows": rows, "kept": kept, "groups": groups, "pmc_runs_per_leg": runs,
                                 "commands": cmds}}
@@ -165,9 +195,23 @@ def main():
     sl = (kt_line or {}).get("string_agg")
     if sl:
         leg_alg["C5"] = sl["pipeline_roofline"]["algorithmic_bytes_per_step"]
-    traffic["_per_step"] = {leg: {"hbm_bytes": int(b), "algorithmic_bytes": leg_alg.get(leg),
-                                  "traffic_over_algorithmic": round(b / leg_alg[leg], 3) if leg_alg.get(leg) else None}
-                            for leg, b in legs.items()}
+    if jl and jl.get("join_v2"):
+        leg_alg["C3v2"] = leg_alg["C3"]
+    fw, ww = step_windows(fetch), step_windows(write)
+    per_step = {}
+    for leg, b in legs.items():
+        e = {"hbm_bytes_avg_over_runs": int(b)}
+        if fw.get(leg) and ww.get(leg):
+            # steady state: the last complete step window of each counter pass
+            b = fw[leg][-1] * 1024 * factor + ww[leg][-1] * 1024
+            e.update({"fetch_bytes": int(fw[leg][-1] * 1024 * factor), "write_bytes": int(ww[leg][-1] * 1024),
+                      "basis": "last complete step window (dispatches after one step-end kernel up to the next)"})
+        else:
+            e["basis"] = "all dispatches of the leg / runs (build included once)"
+        e.update({"hbm_bytes": int(b), "algorithmic_bytes": leg_alg.get(leg),
+                  "traffic_over_algorithmic": round(b / leg_alg[leg], 3) if leg_alg.get(leg) else None})
+        per_step[leg] = e
+    traffic["_per_step"] = per_step
     with open(os.path.join(out, "pmc_traffic.json"), "w") as f:
         json.dump(traffic, f, indent=1, sort_keys=True)
     # ---- summary
@@ -202,7 +246,8 @@ def main():
                 continue
             f.write(f"| {k} | {v['launches']} | {v['fetch_bytes']:.4g} | {v['write_bytes']:.4g} | "
                     f"{v['hbm_bytes_per_launch']:.4g} | {v['algorithmic_bytes'] or '-'} |\n")
-        f.write(f"\nPer bench step (PMC run total / {runs} runs of each leg):\n\n"
+        f.write(f"\nPer bench step (the last complete step window of each leg; C3 = partitioned v1 join, "
+                f"C3v2 = JoinV2 pointer table):\n\n"
                 "| leg | HBM bytes / step | algorithmic bytes / step | ratio |\n|---|---|---|---|\n")
         for leg, v in sorted(traffic["_per_step"].items()):
             f.write(f"| {leg} | {v['hbm_bytes']:.4g} | {v['algorithmic_bytes'] or '-'} | {v['traffic_over_algorithmic']} |\n")
