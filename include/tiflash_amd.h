@@ -134,6 +134,9 @@ typedef enum tfg_collator {
     TFG_COLLATOR_NONE = 0,        /* raw bytes                                       */
     TFG_COLLATOR_BINARY = 1,      /* BinCollatorSortKey<false>: raw bytes            */
     TFG_COLLATOR_BIN_PADDING = 2, /* BinCollatorSortKey<true>: right-trim ' ' (utf8mb4_bin etc.) */
+    TFG_COLLATOR_GENERAL_CI = 3,  /* GeneralCICollator (utf8_general_ci / utf8mb4_general_ci): right-trim ' ',
+                                     then each UTF-8 character's 16-bit weight big-endian
+                                     (TiDB/Collation/Collator.cpp:416-455) */
 } tfg_collator;
 
 /* ---------------------------------------------------------------- context & memory */

@@ -19,6 +19,7 @@
 #endif
 
 #include "../include/tiflash_amd.h"
+#include "collation_data.h"
 
 /* ------------------------------------------------------------------ CRC32-C */
 /* intHashCRC32(x, seed) = _mm_crc32_u64(seed, x)  (Common/HashTable/Hash.h:70-95). */
@@ -182,21 +183,94 @@ void orc_weak_hash_update(int type, const void *col, const uint8_t *nullmap, siz
     }
 }
 
+/* ---------------------------------------------------------------- utf8mb4_general_ci
+ * GeneralCICollator::sortKey = convertImpl<false, true> (TiDB/Collation/Collator.cpp:416-455):
+ * right-trim ' ' (RightTrim, CollatorCompare.h:56-61), decode UTF-8 (decodeUtf8Char,
+ * Collator.cpp:43-74: the lead byte sets the length, continuation bytes unchecked), write each
+ * character's weight big-endian; weight (Collator.h:403-407): 0xFFFD past the BMP, else the
+ * GeneralCI::weight_lut entry (collation_data.h, re-encoded as runs).  `row_end` bounds the
+ * decoder's look-ahead (a truncated sequence reads zeros past it). */
+static const uint32_t orc_gci_runs[TFG_GCI_RUNS][3] = {TFG_GCI_RUNS_INIT};
+
+uint32_t orc_general_ci_weight(uint32_t c)
+{
+    if (c > 0xFFFF) return 0xFFFD;
+    int lo = 0, hi = TFG_GCI_RUNS - 1;
+    while (lo <= hi) { /* the last run starting at or before c */
+        const int mid = (lo + hi) / 2;
+        if (orc_gci_runs[mid][0] <= c) lo = mid + 1;
+        else hi = mid - 1;
+    }
+    if (hi < 0 || c > orc_gci_runs[hi][1]) return c;
+    const uint32_t v = orc_gci_runs[hi][2];
+    if (v >> 16) return v & 0xFFFF;
+    return (uint32_t)(c + (int16_t)(v & 0xFFFF)) & 0xFFFF;
+}
+
+size_t orc_general_ci_sort_key(const uint8_t *s, size_t len, size_t row_end, uint8_t *out)
+{
+    while (len > 0 && s[len - 1] == ' ') --len;
+    size_t off = 0, o = 0;
+#define ORC_AT(k) ((size_t)(k) < row_end ? (uint32_t)s[k] : 0u)
+    while (off < len) {
+        const uint32_t b0 = s[off];
+        uint32_t c;
+        if (b0 < 0x80) {
+            c = b0;
+            off += 1;
+        } else if (b0 < 0xE0) {
+            c = (b0 & 0x1F) << 6 | (ORC_AT(off + 1) & 0x3F);
+            off += 2;
+        } else if (b0 < 0xF0) {
+            c = (b0 & 0x0F) << 12 | (ORC_AT(off + 1) & 0x3F) << 6 | (ORC_AT(off + 2) & 0x3F);
+            off += 3;
+        } else {
+            c = (b0 & 0x07) << 18 | (ORC_AT(off + 1) & 0x3F) << 12 | (ORC_AT(off + 2) & 0x3F) << 6 | (ORC_AT(off + 3) & 0x3F);
+            off += 4;
+        }
+        const uint32_t w = orc_general_ci_weight(c);
+        out[o++] = (uint8_t)(w >> 8);
+        out[o++] = (uint8_t)w;
+    }
+#undef ORC_AT
+    return o;
+}
+
+/* the collator's sort key of a ColumnString row's bytes (len = size - 1, '\0' excluded) into buf
+ * (>= 2 * len bytes); returns a pointer to the key and its length */
+static const uint8_t *orc_sort_key(int collator, const uint8_t *s, size_t len, uint8_t *buf, size_t *klen)
+{
+    if (collator == TFG_COLLATOR_GENERAL_CI) {
+        *klen = orc_general_ci_sort_key(s, len, len + 1, buf);
+        return buf;
+    }
+    if (collator == TFG_COLLATOR_BIN_PADDING)
+        while (len > 0 && s[len - 1] == ' ') --len;
+    *klen = len;
+    return s;
+}
+
 /* ColumnString::updateWeakHash32 (Columns/ColumnString.cpp:1228-1327): hashes size-1 bytes (the
  * trailing '\0' excluded) after the collator's sort key; BIN padding collators right-trim ' '
  * (TiDB/Collation/CollatorCompare.h:49-95). */
 void orc_weak_hash_update_string(const uint8_t *chars, const uint64_t *offsets, const uint8_t *nullmap, size_t n,
                                  int collator, uint32_t *h)
 {
+    uint8_t *buf = NULL;
+    size_t cap = 0;
     for (size_t i = 0; i < n; ++i) {
         if (nullmap && nullmap[i]) continue;
         uint64_t prev = i ? offsets[i - 1] : 0;
         size_t len = (size_t)(offsets[i] - prev - 1);
-        const uint8_t *s = chars + prev;
-        if (collator == TFG_COLLATOR_BIN_PADDING)
-            while (len > 0 && s[len - 1] == ' ') --len;
-        h[i] = orc_update_weak_hash32_bytes(s, len, h[i]);
+        if (2 * len + 16 > cap) {
+            cap = 2 * (2 * len + 16);
+            buf = (uint8_t *)realloc(buf, cap);
+        }
+        size_t klen;
+        const uint8_t *k = orc_sort_key(collator, chars + prev, len, buf, &klen);
+        h[i] = orc_update_weak_hash32_bytes(k, klen, h[i]);
     }
+    free(buf);
 }
 
 /* fillSelector / fillSelectorForFineGrainedShuffle (Flash/Mpp/HashBaseWriterHelper.cpp:46-84). */
@@ -794,7 +868,7 @@ static size_t aggk_serialize(const orc_aggk *a, const void *const *cols, const u
 {
     size_t need = 0;
     for (int j = 0; j < a->nkeys; ++j) {
-        if (a->key_types[j] == TFG_STRING) need += 9 + (offs[j][r] - (r ? offs[j][r - 1] : 0));
+        if (a->key_types[j] == TFG_STRING) need += 9 + 2 * (offs[j][r] - (r ? offs[j][r - 1] : 0));
         else need += 17;
     }
     if (need > *bcap) {
@@ -810,6 +884,12 @@ static size_t aggk_serialize(const orc_aggk *a, const void *const *cols, const u
             const uint64_t s = r ? offs[j][r - 1] : 0;
             uint64_t len = offs[j][r] - s - 1;
             const uint8_t *c = (const uint8_t *)cols[j] + s;
+            if (a->collators[j] == TFG_COLLATOR_GENERAL_CI) { /* the sort key, written in place */
+                const uint64_t kl = orc_general_ci_sort_key(c, len, len + 1, o + 8);
+                memcpy(o, &kl, 8);
+                o += 8 + kl;
+                continue;
+            }
             if (a->collators[j] == TFG_COLLATOR_BIN_PADDING)
                 while (len > 0 && c[len - 1] == ' ') --len;
             memcpy(o, &len, 8);

@@ -24,6 +24,10 @@ int orc_has_hw_crc(void);
 uint32_t orc_crc32c_u64(uint32_t crc, uint64_t x);    /* SSE4.2 crc32q when available */
 uint32_t orc_crc32c_u64_sw(uint32_t crc, uint64_t x); /* bitwise, reflected 0x82F63B78 */
 uint32_t orc_update_weak_hash32_bytes(const uint8_t *pos, size_t size, uint32_t h);
+/* utf8mb4_general_ci: weight of a code point; sort key of len bytes (right-trimmed first) into out
+ * (>= 2 * len bytes), look-ahead bounded by row_end; returns the key's length */
+uint32_t orc_general_ci_weight(uint32_t c);
+size_t orc_general_ci_sort_key(const uint8_t *s, size_t len, size_t row_end, uint8_t *out);
 
 void orc_weak_hash_update(int type, const void *col, const uint8_t *nullmap, size_t n, uint32_t *h);
 uint64_t orc_float64_to_u64(double x); /* the reference build's Float64 -> UInt64 (x86-64 clang) */

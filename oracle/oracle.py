@@ -314,6 +314,28 @@ class AggKeys:
                 o += w
         return tuple(out)
 
+    def result_arrays(self):
+        """-> (key bytes, key end offsets, [state arrays], [state null arrays]) without building
+        Python tuples: the serialised keys (per key a NULL byte, then the value bytes, or a String's
+        u64 length + bytes) for callers that decode millions of groups with numpy."""
+        g = self.size()
+        total = lib().orc_aggk_result(self.h, None, None, None, None)
+        kb = np.zeros(max(total, 1), np.uint8)
+        ko = np.zeros(max(g, 1), np.uint64)
+        states, snull = [], []
+        for kind, t in self.aggs:
+            limbs = sum_limbs(kind, t)
+            t &= 0xFF
+            if limbs > 1:
+                states.append(np.zeros((max(g, 1), limbs), np.int64))
+            elif kind == 0 and t in (FLOAT32, FLOAT64):
+                states.append(np.zeros(max(g, 1), np.float64))
+            else:
+                states.append(np.zeros(max(g, 1), np.int64))
+            snull.append(np.zeros(max(g, 1), np.uint8))
+        lib().orc_aggk_result(self.h, _p(kb), _p(ko), _ptrs(states), _ptrs(snull))
+        return kb[:total], ko[:g], [st[:g] for st in states], [sn[:g] for sn in snull]
+
     def result(self):
         g = self.size()
         total = lib().orc_aggk_result(self.h, None, None, None, None)

@@ -17,7 +17,7 @@
 #include <sstream>
 
 #include "../../oracle/oracle.h"
-#include "../../tiflash_amd/host/pipeline.h"
+#include "../../tiflash_amd/host/planner.h"
 
 using namespace tfa;
 
@@ -1143,6 +1143,72 @@ TEST(AutoPassThroughHashAgg) {
     EXPECT(pass > 0 && st.count((int)AutoPassThroughHashAggContext::State::Selective));
 }
 
+// The spill hand-off of auto pass-through (AutoPassThroughHashAggContext.cpp:86-104,
+// Aggregator.cpp:79-92,1236-1243): once the map's revocable bytes pass the spill threshold it is
+// marked for spill, forceState keeps every later block in PassThrough, and tryGetDataInAdvance
+// hands the map's final block over first (once).  The merged output equals a host aggregation;
+// the external trigger (AggregateContext::needSpill with try_mark) refuses an empty map.
+TEST(AutoPassThroughSpillHandOff) {
+    DataType i64;
+    Aggregator::Params p;
+    p.keys = {"k"};
+    p.aggregates = {{"sum", {"v"}, "sum_v"}, {"count", {}, "cnt"}};
+    p.src_header = Block{{nullptr, i64, "k"}, {nullptr, i64, "v"}};
+    const size_t B = 4096;
+    std::mt19937_64 rng(91);
+    for (int external = 0; external < 2; ++external) {
+        g_current = external ? "spill hand-off, external trigger" : "spill hand-off, threshold";
+        // few keys (the map would stay in Init without a spill); threshold ~ 6K groups' bytes
+        AutoPassThroughHashAggContext apt(ctx, p, /*row_limit_unit=*/B, 1, 5, external ? 0 : 200 * 1024);
+        std::map<int64_t, std::pair<int64_t, uint64_t>> want, got;
+        size_t pass_before = 0, marked_at = 0, map_rows = 0;
+        bool handed = false, first_after_mark_is_map = false;
+        for (size_t bi = 0; bi < 24; ++bi) {
+            std::vector<int64_t> k(B), v(B);
+            for (size_t i = 0; i < B; ++i) {
+                k[i] = (int64_t)(rng() % 9000);
+                v[i] = (int64_t)(rng() % 100);
+                want[k[i]].first += v[i];
+                want[k[i]].second += 1;
+            }
+            Block b{{makeColumn(ctx, i64, k.data(), B), i64, "k"}, {makeColumn(ctx, i64, v.data(), B), i64, "v"}};
+            if (external && bi == 5) EXPECT(apt.tryMarkNeedSpill());
+            const bool was_marked = apt.needSpill();
+            pass_before = apt.passThroughRows();
+            apt.onBlock(b);
+            if (was_marked) { // forceState: the block passed through, the map took nothing
+                EXPECT(apt.state() == AutoPassThroughHashAggContext::State::PassThrough);
+                EXPECT(apt.passThroughRows() == pass_before + B);
+            }
+            if (apt.needSpill() && !marked_at) marked_at = bi + 1;
+            bool first = true;
+            while (Block r = apt.tryGetDataInAdvance()) {
+                if (apt.needSpill() && !handed) {
+                    handed = true;
+                    first_after_mark_is_map = first && r.rows() > 0 && r.rows() <= 9000;
+                    map_rows = r.rows();
+                }
+                first = false;
+                auto kk = toHost<int64_t>(ctx, *materialize(ctx, r.getByName("k").column));
+                auto ss = toHost<int64_t>(ctx, *materialize(ctx, r.getByName("sum_v").column));
+                auto cc = toHost<uint64_t>(ctx, *materialize(ctx, r.getByName("cnt").column));
+                for (size_t i = 0; i < kk.size(); ++i) {
+                    got[kk[i]].first += ss[i];
+                    got[kk[i]].second += cc[i];
+                }
+            }
+        }
+        EXPECT(marked_at > 0 && marked_at < 24 && handed && first_after_mark_is_map && map_rows > 0);
+        EXPECT(!apt.getDataFromHashTable()); // already handed over
+        EXPECT(got == want);
+        EXPECT(apt.passThroughRows() >= (24 - marked_at) * B);
+    }
+    { // the external trigger refuses an empty map (tryMarkNeedSpill: empty() -> false)
+        AutoPassThroughHashAggContext apt(ctx, p, B);
+        EXPECT(!apt.tryMarkNeedSpill() && !apt.needSpill());
+    }
+}
+
 // Two GROUP BY keys (Int64, Nullable(Int32)) through the pass-through state machine: the first
 // key alone collides constantly (1000 values), so a Selective-state lookup on it alone would call
 // new tuples hits.  The lookup runs on the full tuple; tuples holding a NULL pass through.  Every
@@ -1669,6 +1735,369 @@ TEST(SelectiveBlockPartition) {
         w.write(sb);
         w.flush();
         for (uint32_t p = 0; p < 4; ++p) EXPECT(sent[p] == toHost<int64_t>(ctx, *part[p].getByName("v").column));
+    }
+}
+
+// ---------------------------------------------------------------- executor descriptors (row b2)
+// PhysicalPlan::build (Flash/Planner/PhysicalPlan.cpp:95-231) from tipb-shaped descriptors: the
+// operators are instantiated by the planner, not by hand, and the results equal the oracle's.
+static std::map<int64_t, std::pair<double, uint64_t>> planAggRows(Context &ctx, const std::vector<Block> &res) {
+    std::map<int64_t, std::pair<double, uint64_t>> got;
+    for (const Block &r : res) { // schema: sum, count, key
+        auto rs = toHost<double>(ctx, *r.safeGetByPosition(0).column);
+        auto rc = toHost<uint64_t>(ctx, *r.safeGetByPosition(1).column);
+        auto rk = toHost<int64_t>(ctx, *r.safeGetByPosition(2).column);
+        for (size_t i = 0; i < rk.size(); ++i) EXPECT(got.emplace(rk[i], std::make_pair(rs[i], rc[i])).second);
+    }
+    return got;
+}
+
+// Aggregation(Selection(TableScan)): filter -> GROUP BY from a descriptor, both with the pushed-down
+// (fused) filter and with FilterTransformOp, through the pipeline engine and the stream engine;
+// then computed arguments: sum(d * 2.0) and sum(100 - f) (a constant-left MinusInt)
+TEST(PlanFilterAggregate) {
+    using namespace dag;
+    std::mt19937_64 rng(201);
+    const size_t n = 150000;
+    std::vector<int64_t> f(n), k(n);
+    std::vector<double> d(n);
+    for (size_t i = 0; i < n; ++i) {
+        f[i] = rng() % 100;
+        k[i] = (int64_t)(rng() % 20000) - 5000;
+        d[i] = (double)(rng() % (1 << 20)) / 256.0;
+    }
+    DataType i64, f64;
+    f64.type = TFG_FLOAT64;
+    Block b{{makeColumn(ctx, i64, f.data(), n), i64, "f"}, {makeColumn(ctx, i64, k.data(), n), i64, "k"},
+            {makeColumn(ctx, f64, d.data(), n), f64, "d"}};
+    std::map<int64_t, std::pair<double, uint64_t>> want;
+    std::map<int64_t, int64_t> want_minus;
+    for (size_t i = 0; i < n; ++i)
+        if (f[i] < 40) {
+            auto &w = want[k[i]];
+            w.first += d[i];
+            w.second += 1;
+            want_minus[k[i]] += 100 - f[i];
+        }
+    // oracle check of the host map (dyadic values: exact in any order)
+    {
+        std::vector<uint8_t> mask(n);
+        for (size_t i = 0; i < n; ++i) mask[i] = f[i] < 40;
+        int kinds[2] = {TFG_AGG_SUM, TFG_AGG_COUNT_ALL};
+        int types[2] = {TFG_FLOAT64, 0};
+        orc_agg *o = orc_agg_create(TFG_INT64, 2, kinds, types);
+        const void *args[2] = {d.data(), nullptr};
+        const uint8_t *an[2] = {nullptr, nullptr};
+        orc_agg_consume(o, k.data(), nullptr, args, an, mask.data(), n);
+        EXPECT(orc_agg_size(o) == want.size());
+        orc_agg_destroy(o);
+    }
+    PlanContext env;
+    env.tables["lineitem"] = {b.cloneEmpty(), splitBlocks(ctx, b, 5)};
+    const Executor root = Executor::aggregation(
+        "agg_1", {Expr::col(1)}, {Expr::sum(Expr::col(2)), Expr::count()},
+        Executor::selection("sel_0", {Expr::func(ScalarFuncSig::LTInt, {Expr::col(0), Expr::i64(40)})},
+                            Executor::tableScan("ts_0", "lineitem")));
+    for (int fuse = 0; fuse < 2; ++fuse) {
+        g_current = fuse ? "PlanFilterAggregate fused" : "PlanFilterAggregate FilterTransformOp";
+        std::vector<Block> res;
+        env.result = [&](const Block &r) { res.push_back(r); };
+        env.fuse_filter_into_aggregation = fuse;
+        PipelineExecutorContext exec;
+        PhysicalPlan plan(ctx, exec, env);
+        plan.build(root);
+        const std::string shape = plan.toString();
+        EXPECT(plan.pipelines().size() == 2);
+        EXPECT((shape.find("FilterTransformOp") != std::string::npos) == !fuse);
+        EXPECT(shape.find("AggregateBuildSinkOp x2") != std::string::npos);
+        EXPECT(shape.find("AggregateConvergentSourceOp") != std::string::npos);
+        EXPECT(plan.outputHeader().columns() == 3);
+        plan.execute();
+        EXPECT(planAggRows(ctx, res) == want);
+    }
+    { // the stream engine's chain of the same descriptor
+        g_current = "PlanFilterAggregate streams";
+        BlockInputStreamPtr s = buildBlockInputStream(ctx, env, root);
+        std::vector<Block> res;
+        for (Block r = s->read(); r; r = s->read()) res.push_back(r);
+        EXPECT(planAggRows(ctx, res) == want);
+    }
+    { // computed arguments: sum(d * 2.0), sum(100 - f), count(*)
+        g_current = "PlanFilterAggregate computed args";
+        const Executor r2 = Executor::aggregation(
+            "agg_2", {Expr::col(1)},
+            {Expr::sum(Expr::func(ScalarFuncSig::MultiplyReal, {Expr::col(2), Expr::f64(2.0)})),
+             Expr::count(), Expr::sum(Expr::func(ScalarFuncSig::MinusInt, {Expr::i64(100), Expr::col(0)}))},
+            Executor::selection("sel_0", {Expr::func(ScalarFuncSig::GTInt, {Expr::i64(40), Expr::col(0)})},
+                                Executor::tableScan("ts_0", "lineitem")));
+        std::vector<Block> res;
+        env.result = [&](const Block &r) { res.push_back(r); };
+        env.fuse_filter_into_aggregation = true;
+        PipelineExecutorContext exec;
+        PhysicalPlan plan(ctx, exec, env);
+        plan.build(r2);
+        EXPECT(plan.toString().find("ExpressionTransformOp") != std::string::npos);
+        plan.execute();
+        std::map<int64_t, std::pair<double, uint64_t>> got;
+        std::map<int64_t, int64_t> got_minus;
+        for (const Block &r : res) { // schema: sum(d*2), count, sum(100-f), key
+            auto rs = toHost<double>(ctx, *r.safeGetByPosition(0).column);
+            auto rc = toHost<uint64_t>(ctx, *r.safeGetByPosition(1).column);
+            auto rm = toHost<int64_t>(ctx, *r.safeGetByPosition(2).column);
+            auto rk = toHost<int64_t>(ctx, *r.safeGetByPosition(3).column);
+            for (size_t i = 0; i < rk.size(); ++i) {
+                got[rk[i]] = {rs[i] / 2.0, rc[i]};
+                got_minus[rk[i]] = rm[i];
+            }
+        }
+        EXPECT(got == want);
+        EXPECT(got_minus == want_minus);
+        if (got != want || got_minus != want_minus) { // bisect: the same aggregation without the planner
+            auto ea = std::make_shared<ExpressionActions>(ctx);
+            ea->arithmeticConst(TFG_MULTIPLY, "d", Field::Float64(2.0), "x2");
+            ea->arithmeticConstLeft(TFG_MINUS, Field::Int64(100), "f", "m");
+            Block bx = b;
+            ea->execute(bx);
+            Aggregator::Params p2;
+            p2.src_header = bx.cloneEmpty();
+            p2.keys = {"k"};
+            p2.aggregates = {{"sum", {"x2"}, "s"}, {"count", {}, "c"}, {"sum", {"m"}, "sm"}};
+            Aggregator direct(ctx, p2);
+            direct.executeOnBlockFiltered(bx, "f", TFG_LT, Field::Int64(40));
+            Block r = direct.convertToBlock();
+            auto rk = toHost<int64_t>(ctx, *r.getByName("k").column);
+            auto rs = toHost<double>(ctx, *r.getByName("s").column);
+            auto rc = toHost<uint64_t>(ctx, *r.getByName("c").column);
+            std::map<int64_t, std::pair<double, uint64_t>> g2;
+            for (size_t i = 0; i < rk.size(); ++i) g2[rk[i]] = {rs[i] / 2.0, rc[i]};
+            fprintf(stderr, "  direct Aggregator (no planner): %s, groups %zu; block rows %zu, cols %zu\n",
+                    g2 == want ? "matches" : "differs", g2.size(), bx.rows(), bx.columns());
+        }
+        if (got != want || got_minus != want_minus) { // diagnostics: the first differing groups
+            fprintf(stderr, "  groups got %zu want %zu\n", got.size(), want.size());
+            int shown = 0;
+            for (const auto &kv : want) {
+                auto it = got.find(kv.first);
+                auto im = got_minus.find(kv.first);
+                const bool bad = it == got.end() || it->second != kv.second || im == got_minus.end() ||
+                                 im->second != want_minus[kv.first];
+                if (bad && shown++ < 5)
+                    fprintf(stderr, "  key %lld: want (%.6f, %llu, %lld) got (%.6f, %llu, %lld)\n", (long long)kv.first,
+                            kv.second.first, (unsigned long long)kv.second.second, (long long)want_minus[kv.first],
+                            it == got.end() ? -1.0 : it->second.first,
+                            it == got.end() ? 0ull : (unsigned long long)it->second.second,
+                            im == got_minus.end() ? -1ll : (long long)im->second);
+            }
+        }
+    }
+}
+
+// Join(TableScan probe, TableScan build) from descriptors: inner (pairs vs the oracle, schema =
+// left then right columns), a GROUP BY over the join (count per key), left outer (unmatched
+// probe rows carry NULL build columns), semi, and the stream engine's inner join
+TEST(PlanHashJoin) {
+    using namespace dag;
+    std::mt19937_64 rng(202);
+    const size_t nb = 30000, np = 90000;
+    std::vector<int64_t> bk(nb), bp(nb), pk(np), pp(np);
+    for (size_t i = 0; i < nb; ++i) {
+        bk[i] = rng() % 25000;
+        bp[i] = (int64_t)i * 7;
+    }
+    for (size_t i = 0; i < np; ++i) {
+        pk[i] = rng() % 40000;
+        pp[i] = (int64_t)i;
+    }
+    DataType i64;
+    Block build{{makeColumn(ctx, i64, bk.data(), nb), i64, "o_key"}, {makeColumn(ctx, i64, bp.data(), nb), i64, "o_pay"}};
+    Block probe{{makeColumn(ctx, i64, pk.data(), np), i64, "l_key"}, {makeColumn(ctx, i64, pp.data(), np), i64, "l_pay"}};
+    orc_join *oj = orc_join_create(TFG_INT64);
+    orc_join_build(oj, bk.data(), nullptr, nb);
+    std::vector<uint32_t> op(np * 4), ob(np * 4);
+    const size_t m = orc_join_probe(oj, TFG_JOIN_INNER, pk.data(), nullptr, np, op.data(), ob.data(), op.size());
+    orc_join_destroy(oj);
+    std::multiset<std::vector<int64_t>> want;
+    std::map<int64_t, uint64_t> want_cnt;
+    std::vector<uint8_t> matched(np, 0);
+    for (size_t i = 0; i < m; ++i) {
+        want.insert({pk[op[i]], pp[op[i]], bk[ob[i]], bp[ob[i]]});
+        ++want_cnt[pk[op[i]]];
+        matched[op[i]] = 1;
+    }
+    const size_t unmatched = (size_t)std::count(matched.begin(), matched.end(), 0);
+    PlanContext env;
+    env.tables["lineitem"] = {probe.cloneEmpty(), splitBlocks(ctx, probe, 4)};
+    env.tables["orders"] = {build.cloneEmpty(), splitBlocks(ctx, build, 3)};
+    env.max_block_size = 20000;
+    auto joinOf = [&](JoinType t) {
+        return Executor::join("join_2", t, {Expr::col(0)}, {Expr::col(0)}, Executor::tableScan("ts_0", "lineitem"),
+                              Executor::tableScan("ts_1", "orders"), 1);
+    };
+    auto rows4 = [&](const std::vector<Block> &res) {
+        std::multiset<std::vector<int64_t>> got;
+        for (const Block &r : res) {
+            std::vector<std::vector<int64_t>> c;
+            for (size_t j = 0; j < 4; ++j) c.push_back(toHost<int64_t>(ctx, *r.safeGetByPosition(j).column));
+            for (size_t i = 0; i < c[0].size(); ++i) got.insert({c[0][i], c[1][i], c[2][i], c[3][i]});
+        }
+        return got;
+    };
+    { // inner
+        g_current = "PlanHashJoin inner";
+        std::vector<Block> res;
+        env.result = [&](const Block &r) { res.push_back(r); };
+        PipelineExecutorContext exec;
+        PhysicalPlan plan(ctx, exec, env);
+        plan.build(joinOf(JoinType::TypeInnerJoin));
+        EXPECT(plan.pipelines().size() == 2);
+        EXPECT(plan.toString().find("HashJoinBuildSink x2") != std::string::npos);
+        EXPECT(plan.toString().find("HashJoinProbeTransformOp") != std::string::npos);
+        EXPECT(plan.outputHeader().columns() == 4 && plan.outputHeader().safeGetByPosition(0).name == "join_2_l_l_key" &&
+               plan.outputHeader().safeGetByPosition(2).name == "join_2_r_o_key");
+        plan.execute();
+        EXPECT(rows4(res) == want);
+        size_t max_rows = 0;
+        for (const Block &r : res) max_rows = std::max(max_rows, r.rows());
+        EXPECT(max_rows <= 20000);
+    }
+    { // GROUP BY the joined key: count(*) per l_key
+        g_current = "PlanHashJoin aggregation over the join";
+        std::vector<Block> res;
+        env.result = [&](const Block &r) { res.push_back(r); };
+        PipelineExecutorContext exec;
+        PhysicalPlan plan(ctx, exec, env);
+        plan.build(Executor::aggregation("agg_3", {Expr::col(0)}, {Expr::count()}, joinOf(JoinType::TypeInnerJoin)));
+        EXPECT(plan.pipelines().size() == 3); // join build, probe -> agg build, convergent
+        plan.execute();
+        std::map<int64_t, uint64_t> got;
+        for (const Block &r : res) {
+            auto rc = toHost<uint64_t>(ctx, *r.safeGetByPosition(0).column);
+            auto rk = toHost<int64_t>(ctx, *r.safeGetByPosition(1).column);
+            for (size_t i = 0; i < rk.size(); ++i) got[rk[i]] = rc[i];
+        }
+        EXPECT(got == want_cnt);
+    }
+    { // left outer: every probe row, unmatched ones with NULL build columns
+        g_current = "PlanHashJoin left outer";
+        std::vector<Block> res;
+        env.result = [&](const Block &r) { res.push_back(r); };
+        PipelineExecutorContext exec;
+        PhysicalPlan plan(ctx, exec, env);
+        plan.build(joinOf(JoinType::TypeLeftOuterJoin));
+        EXPECT(plan.outputHeader().safeGetByPosition(3).type.nullable);
+        plan.execute();
+        size_t rows = 0, nulls = 0;
+        for (const Block &r : res) {
+            rows += r.rows();
+            auto nm = toHostNullMap(ctx, *r.safeGetByPosition(3).column);
+            nulls += (size_t)std::count(nm.begin(), nm.end(), 1);
+        }
+        EXPECT(rows == m + unmatched && nulls == unmatched);
+    }
+    { // semi: the probe rows with a match (left columns only)
+        g_current = "PlanHashJoin semi";
+        std::vector<Block> res;
+        env.result = [&](const Block &r) { res.push_back(r); };
+        PipelineExecutorContext exec;
+        PhysicalPlan plan(ctx, exec, env);
+        plan.build(joinOf(JoinType::TypeSemiJoin));
+        EXPECT(plan.outputHeader().columns() == 2);
+        plan.execute();
+        std::multiset<int64_t> got, exp;
+        for (const Block &r : res)
+            for (int64_t v : toHost<int64_t>(ctx, *r.safeGetByPosition(1).column)) got.insert(v);
+        for (size_t i = 0; i < np; ++i)
+            if (matched[i]) exp.insert(pp[i]);
+        EXPECT(got == exp);
+    }
+    { // the stream engine
+        g_current = "PlanHashJoin streams";
+        BlockInputStreamPtr s = buildBlockInputStream(ctx, env, joinOf(JoinType::TypeInnerJoin));
+        std::vector<Block> res;
+        for (Block r = s->read(); r; r = s->read()) res.push_back(r);
+        EXPECT(rows4(res) == want);
+    }
+}
+
+// ExchangeSender(Hash) -> tunnels (partition 1 local, the others captured), vs hashPartitionBlock;
+// then ExchangeReceiver -> Aggregation on the local partition; PassThrough and Broadcast senders
+TEST(PlanExchange) {
+    using namespace dag;
+    std::mt19937_64 rng(203);
+    const size_t n = 40000;
+    std::vector<int64_t> k(n), v(n);
+    for (size_t i = 0; i < n; ++i) {
+        k[i] = (int64_t)(rng() % 5000) - 2500;
+        v[i] = (int64_t)(rng() % 1000);
+    }
+    DataType i64;
+    Block b{{makeColumn(ctx, i64, k.data(), n), i64, "k"}, {makeColumn(ctx, i64, v.data(), n), i64, "v"}};
+    std::vector<Block> want = hashPartitionBlock(ctx, b, {0}, 4);
+    PlanContext env;
+    env.tables["t"] = {b.cloneEmpty(), splitBlocks(ctx, b, 5)};
+    auto receiver = std::make_shared<ExchangeReceiver>();
+    std::vector<std::multiset<std::vector<std::string>>> remote(4);
+    env.tunnels = std::make_shared<MPPTunnelSet>(ctx, 4, 2, receiver, nullptr, 1, [&](uint32_t part, Block &&blk) {
+        for (const auto &row : rowSet(ctx, blk)) remote[part].insert(row);
+    });
+    {
+        PipelineExecutorContext exec;
+        PhysicalPlan plan(ctx, exec, env);
+        plan.build(Executor::exchangeSender("exchange_sender_1", ExchangeType::Hash, {Expr::col(0)},
+                                            Executor::tableScan("ts_0", "t")));
+        EXPECT(plan.toString().find("ExchangeSenderSinkOp x2") != std::string::npos);
+        plan.execute();
+    }
+    EXPECT(receiver->finished());
+    for (uint32_t p : {0u, 2u, 3u}) EXPECT(remote[p] == rowSet(ctx, want[p]));
+    // the receiving task: GROUP BY k over the local partition
+    std::map<int64_t, std::pair<int64_t, uint64_t>> exp;
+    {
+        auto wk = toHost<int64_t>(ctx, *want[1].safeGetByPosition(0).column);
+        auto wv = toHost<int64_t>(ctx, *want[1].safeGetByPosition(1).column);
+        for (size_t i = 0; i < wk.size(); ++i) {
+            exp[wk[i]].first += wv[i];
+            exp[wk[i]].second += 1;
+        }
+    }
+    PlanContext env2;
+    env2.receivers["exchange_receiver_0"] = {b.cloneEmpty(), receiver};
+    std::vector<Block> res;
+    env2.result = [&](const Block &r) { res.push_back(r); };
+    {
+        PipelineExecutorContext exec;
+        PhysicalPlan plan(ctx, exec, env2);
+        plan.build(Executor::aggregation("agg_1", {Expr::col(0)}, {Expr::sum(Expr::col(1)), Expr::count()},
+                                         Executor::exchangeReceiver("exchange_receiver_0", "exchange_receiver_0")));
+        EXPECT(plan.toString().find("ExchangeReceiverSourceOp") != std::string::npos);
+        plan.execute();
+    }
+    std::map<int64_t, std::pair<int64_t, uint64_t>> got;
+    for (const Block &r : res) {
+        auto rs = toHost<int64_t>(ctx, *r.safeGetByPosition(0).column);
+        auto rc = toHost<uint64_t>(ctx, *r.safeGetByPosition(1).column);
+        auto rk = toHost<int64_t>(ctx, *r.safeGetByPosition(2).column);
+        for (size_t i = 0; i < rk.size(); ++i) got[rk[i]] = {rs[i], rc[i]};
+    }
+    EXPECT(got == exp);
+    // PassThrough: every row to tunnel 0; Broadcast: every row to every tunnel
+    for (int bc = 0; bc < 2; ++bc) {
+        g_current = bc ? "PlanExchange broadcast" : "PlanExchange pass-through";
+        std::vector<size_t> rows(3, 0);
+        auto recv = std::make_shared<ExchangeReceiver>();
+        PlanContext e3;
+        e3.tables["t"] = env.tables["t"];
+        e3.tunnels = std::make_shared<MPPTunnelSet>(ctx, 3, 2, recv, nullptr, 0,
+                                                    [&](uint32_t part, Block &&blk) { rows[part] += blk.rows(); });
+        PipelineExecutorContext exec;
+        PhysicalPlan plan(ctx, exec, e3);
+        plan.build(Executor::exchangeSender("exchange_sender_2", bc ? ExchangeType::Broadcast : ExchangeType::PassThrough,
+                                            {}, Executor::tableScan("ts_0", "t")));
+        plan.execute();
+        size_t local = 0;
+        for (Block blk; recv->tryPop(blk);) local += blk ? blk.rows() : 0;
+        EXPECT(local == n);
+        EXPECT(bc ? (rows[1] == n && rows[2] == n) : (rows[1] == 0 && rows[2] == 0));
     }
 }
 

@@ -18,6 +18,9 @@ reference_cases.json — known answers TRANSCRIBED (as data) from the reference'
     (ReturnTypeForIntegerInputs), Decimal inputs per SumDecimalInferer (Common/Decimal.h:156-163,
     Decimal(min(p+22, 65), s)), the Decimal256 bound of 65 digits (gtest_decimal_type.cpp:52-62) and
     the +/-/* result scales of DataTypeDecimal_test A (gtest_funtions_decimal_arith.cpp:47-77).
+  * general_ci: utf8mb4_general_ci sort keys and comparisons pinned by the reference's collator
+    gtest (dbms/src/TiDB/tests/gtest_tidb_collator.cpp:49-65 cmp_cases and :71-140 sk_cases, the
+    GeneralCI column of each answer tuple), as hex bytes.
 crc_vectors.json — CRC32-C / WeakHash32 vectors computed with the x86 SSE4.2 crc32q instruction,
   the instruction the reference itself hashes with (Common/HashTable/Hash.h:70-95), via oracle.
 """
@@ -131,6 +134,20 @@ def sum_type_cases():
             "arith_scales": {"lhs": [10, 4], "rhs": [10, 6], "plus": 6, "minus": 6, "multiply": 10}}
 
 
+def general_ci_cases():
+    # (input, expected sort key) — the GeneralCI entry (index 2) of sk_cases
+    sk = [("a", "0041"), ("A", "0041"), ("\U0001F603", "fffd"),
+          ("Foo \u00a9 bar \U0001D306 baz \u2603 qux",
+           "0046004f004f002000a900200042004100520020fffd00200042004100" "5a0020260300200051005500" "58"),
+          ("a ", "0041"), ("", ""), ("\u00df", "0053")]
+    # (a, b, expected sign of compare) — the GeneralCI entry of cmp_cases
+    cmp = [("a", "b", -1), ("a", "A", 0), ("\u00c0", "A", 0), ("abc", "abc", 0), ("abc", "ab", 1),
+           ("\U0001F61C", "\U0001F603", 0), ("a", "a ", 0), ("a ", "a  ", 0), ("a\t", "a", 1), ("", "a", -1),
+           ("a", "", 1), ("\u00df", "ss", -1), ("\U0001042D", "\U00010428", 0), ("\u8b3a", "\u8b42", -1)]
+    return {"sort_keys": [{"s": a, "key_hex": k} for a, k in sk],
+            "compare": [{"a": a, "b": b, "sign": c} for a, b, c in cmp]}
+
+
 def crc_vectors():
     from oracle import oracle as orc
     rng = np.random.default_rng(2024)
@@ -150,7 +167,8 @@ if __name__ == "__main__":
     with open(os.path.join(HERE, "reference_cases.json"), "w") as f:
         json.dump({"groupby": groupby_cases(), "groupby_keys": groupby_keys_cases(), "join": join_cases(),
                    "exchange": {"block_rows": 64, "blocks": 64, "parts": 4, "rows_per_part": 1024},
-                   "aggregates": aggregate_cases(), "sum_types": sum_type_cases()}, f, indent=1)
+                   "aggregates": aggregate_cases(), "sum_types": sum_type_cases(),
+                   "general_ci": general_ci_cases()}, f, indent=1)
     with open(os.path.join(HERE, "crc_vectors.json"), "w") as f:
         json.dump(crc_vectors(), f, indent=1)
     print("wrote", os.listdir(HERE))

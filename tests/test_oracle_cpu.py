@@ -320,3 +320,26 @@ def test_float_weak_hash_golden(orc, kind):
     assert [f(float(x)) for x in vals] == [int(c) for c in conv]
     h = orc.weak_hash([vals], [orc.FLOAT64 if kind == "float64" else orc.FLOAT32])
     np.testing.assert_array_equal(h, hashes)
+
+
+def test_oracle_general_ci_sort_keys_match_reference_gtest(orc):
+    """utf8mb4_general_ci sort keys and comparisons: the reference's collator gtest answers
+    (gtest_tidb_collator.cpp:49-65, 71-140; tests/golden/reference_cases.json "general_ci")."""
+    import ctypes
+    import json
+    import os
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "reference_cases.json")))["general_ci"]
+    lib = orc.lib()
+    lib.orc_general_ci_sort_key.restype = ctypes.c_size_t
+
+    def key(s):
+        b = s.encode("utf-8")
+        out = ctypes.create_string_buffer(2 * len(b) + 16)
+        n = lib.orc_general_ci_sort_key(b, ctypes.c_size_t(len(b)), ctypes.c_size_t(len(b) + 1), out)
+        return out.raw[:n]
+
+    for c in gold["sort_keys"]:
+        assert key(c["s"]).hex() == c["key_hex"], c
+    for c in gold["compare"]:
+        ka, kb = key(c["a"]), key(c["b"])
+        assert (ka > kb) - (ka < kb) == c["sign"], c

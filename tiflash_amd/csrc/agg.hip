@@ -24,6 +24,7 @@
 #include "agg_fused.h"
 #include "common.h"
 #include "agg_dev.h"
+#include "collation.h"
 #include "serial.h"
 
 namespace tfg {
@@ -627,7 +628,9 @@ struct tfg_agg {
     // buffer holding the packed keys of the block being consumed / the result being written
     KeyPack kp{};
     int key_types[8] = {};
-    int key_collators[8] = {};
+    int key_collators[8] = {};  // as the packing / dictionary code applies them (NONE for a transformed key)
+    int key_transform[8] = {};  // a case-insensitive collator whose sort keys the raw rows are turned into
+                                // before a consume (collation.h); 0 = none
     // the serialized method (serial.h): when set, every call goes to `inner`, an aggregator over
     // the dictionary's UInt32 group ids; a packed-key aggregator moves there (carrying its groups)
     // the first time a block's keys do not fit 16 bytes (long String keys, nullable key tuples of
@@ -718,7 +721,7 @@ int fast_signature(const AggSpec &S, int mode, int key_width, const uint8_t *key
         }
         code = code * 10 + op;
     }
-    return code;
+    return fast_code_supported(code) ? code : 0; // e.g. count() before sum(): the generic path
 }
 
 // The fast signatures run over a tile-sorted partition: partition -> agg_bucket_tiled_kernel ->
@@ -771,6 +774,7 @@ int consume_fast_tiled(tfg_agg *a, int fast, const RowPred &pred, const void *ke
     tin.spill[0] = (uint64_t *)(sb + o_sp0);
     tin.spill[1] = (uint64_t *)(sb + o_sp1);
     tin.cursor = (unsigned long long *)(sb + o_cur);
+    tin.xcd_remap = 1; // neighbouring runs read by one XCD: FETCH 1.95 -> 1.2 GB per C2 step (r03b)
     TFG_HIP(hipMemsetAsync(tin.cursor, 0, 16, ctx->stream));
     GroupsIO tmp{};
     a->carve_groups(sb + o_tmpg, tmp_groups, tmp);
@@ -828,7 +832,10 @@ int wide_fast_signature(const AggSpec &S, const uint8_t *const *val_nulls) {
         }
         code = code * 10 + op;
     }
-    return sums <= 1 ? code : 0;
+    switch (sums <= 1 ? code : 0) { // the WideFastOps specialisations (launch_bucket_wide_tiled)
+    case 410: case 310: case 210: case 140: case 130: case 120: case 400: case 300: case 200: case 100: return code;
+    default: return 0;
+    }
 }
 
 // Wide keys (packed keys128 / key_string) of a wide fast signature over a tiled partition:
@@ -926,6 +933,7 @@ int consume_wide_tiled(tfg_agg *a, int code, Sel sel, const void *const *vals, i
         tin.fine_bits = RG_FINE_BITS;
     }
     tin.cursor = (unsigned long long *)(sb + o_cur);
+    tin.xcd_remap = 0; // two-level wide tiles: measured slower with the remap (r03b)
     TFG_HIP(hipMemsetAsync(tin.cursor, 0, 16, ctx->stream));
     GroupsIO tmp{};
     a->carve_groups(sb + o_tmpg, tmp_groups, tmp);
@@ -1121,6 +1129,7 @@ int consume_keyed(tfg_agg *a, int mode, const RowPred &pred, const void *keys, i
             pc.width[pc.ncols++] = 8;
         }
         TFG_CHECK(pc.ncols == rec_words, TFG_ERR_LOGICAL, "record layout mismatch");
+        pc.aos = rec_words >= 2; // keys alone (count() only): one plain column
         SelBucket8 sel{(const uint64_t *)keys, fib_shift(B)};
         if (int rc = run_partition<SelBucket8, false>(ctx, sel, pred, L, pc, nullptr, nullptr, stage_off, sb + o_part,
                                                       "agg.part.hist", "agg.part.scatter"))
@@ -1713,8 +1722,7 @@ int tfg_agg_create_keys(tfg_ctx *ctx, int nkeys, const int *key_types, const int
         const int t = key_types[j];
         const int c = key_collators ? key_collators[j] : TFG_COLLATOR_NONE;
         if (t == TFG_STRING) {
-            TFG_CHECK(c >= TFG_COLLATOR_NONE && c <= TFG_COLLATOR_BIN_PADDING, TFG_ERR_NOT_IMPLEMENTED,
-                      "collator %d not supported", c);
+            TFG_CHECK(collator_known(c), TFG_ERR_NOT_IMPLEMENTED, "collator %d not supported", c);
             serialized |= nkeys > 1;
             continue;
         }
@@ -1739,13 +1747,17 @@ int tfg_agg_create_keys(tfg_ctx *ctx, int nkeys, const int *key_types, const int
     } else {
         kp.kind = key_types[0] == TFG_STRING ? WK_STRING : WK_FIXED;
         kp.collator = key_collators ? key_collators[0] : TFG_COLLATOR_NONE;
+        if (collator_transforms(kp.collator)) kp.collator = TFG_COLLATOR_NONE; // the consume collates first
         if (int rc = tfg_agg_create(ctx, TFG_KEYS128, n_aggs, agg_kinds, arg_types, arg_scales, &p, &a)) return rc;
     }
     a->kp = kp;
     if (serialized) a->kp.nkeys = nkeys;
     for (int j = 0; j < nkeys; ++j) {
         a->key_types[j] = key_types[j];
-        a->key_collators[j] = key_collators ? key_collators[j] : TFG_COLLATOR_NONE;
+        const int c = key_collators ? key_collators[j] : TFG_COLLATOR_NONE;
+        const bool tr = key_types[j] == TFG_STRING && collator_transforms(c);
+        a->key_collators[j] = tr ? TFG_COLLATOR_NONE : c;
+        a->key_transform[j] = tr ? c : 0;
     }
     for (int i = 0; i < n_aggs; ++i) {
         a->c_kinds[i] = agg_kinds[i];
@@ -1771,6 +1783,35 @@ int tfg_agg_consume_keys(tfg_agg *a, const void *const *key_cols, const uint64_t
                          const uint8_t *const *key_nullmaps, const void *const *args, const uint8_t *const *arg_nullmaps,
                          const uint8_t *mask, int64_t n) {
     TFG_CHECK(a, TFG_ERR_INVALID_ARG, "agg is null");
+    // String keys under a case-insensitive collator: HashMethodString / serializeValueIntoArena
+    // take the collator's sort key (ColumnsHashing.h:233, AggregationCommon.h:202), so the rows
+    // are collated into sort-key columns first (the result's key column holds the sort keys, as
+    // the reference Aggregator's does)
+    bool any = false;
+    for (int j = 0; j < (a->kp.nkeys ? a->kp.nkeys : 1); ++j) any = any || a->key_transform[j];
+    if (any && n > 0) {
+        TFG_CHECK(key_cols && key_offsets, TFG_ERR_INVALID_ARG, "String keys need chars and offsets");
+        if (int rc = set_device(a->ctx)) return rc;
+        CollatedStrings cs[8];
+        const void *kc[8] = {};
+        const uint64_t *ko[8] = {};
+        for (int j = 0; j < a->kp.nkeys; ++j) {
+            kc[j] = key_cols[j];
+            ko[j] = key_offsets[j];
+            if (!a->key_transform[j]) continue;
+            if (int rc = collate_strings(a->ctx, a->key_transform[j], (const uint8_t *)key_cols[j], key_offsets[j],
+                                         key_nullmaps ? key_nullmaps[j] : nullptr, nullptr, nullptr, n, cs[j]))
+                return rc;
+            kc[j] = cs[j].chars;
+            ko[j] = cs[j].offsets();
+        }
+        const int transforms[8] = {a->key_transform[0], a->key_transform[1], a->key_transform[2], a->key_transform[3],
+                                   a->key_transform[4], a->key_transform[5], a->key_transform[6], a->key_transform[7]};
+        for (int j = 0; j < 8; ++j) a->key_transform[j] = 0;
+        const int rc = tfg_agg_consume_keys(a, kc, ko, key_nullmaps, args, arg_nullmaps, mask, n);
+        for (int j = 0; j < 8; ++j) a->key_transform[j] = transforms[j];
+        return rc;
+    }
     if (a->sdict) return serial_consume(a, key_cols, key_offsets, key_nullmaps, args, arg_nullmaps, mask, n, false);
     a->long_key = false;
     int rc = consume_keys_packed(a, key_cols, key_offsets, key_nullmaps, args, arg_nullmaps, mask, n);

@@ -322,6 +322,34 @@ struct Table {
         }
     }
 
+    // Home-group lookup of R keys at once, branch-free: cell[u] = the key's cell when it sits in
+    // its home group — the common case once a bucket's groups exist (cells of a group fill in
+    // order and are never freed, so a match anywhere in the group is the key's cell) — else -1
+    // (key 0, a key in an overflow group, a key not inserted yet): the caller's slow path.
+    template <int R>
+    __device__ __forceinline__ void find_home(const uint64_t (&key)[R], int (&cell)[R]) const {
+        unsigned grp[R];
+        uint64_t k[R][GS];
+#pragma unroll
+        for (int u = 0; u < R; ++u) grp[u] = slot_group(key[u]);
+#pragma unroll
+        for (int u = 0; u < R; ++u) { // every row's group read before any compare
+            const uint4 a = *reinterpret_cast<const uint4 *>(&keys[grp[u] * GS]);
+            const uint4 b = *reinterpret_cast<const uint4 *>(&keys[grp[u] * GS + 2]);
+            k[u][0] = ((uint64_t)a.y << 32) | a.x;
+            k[u][1] = ((uint64_t)a.w << 32) | a.z;
+            k[u][2] = ((uint64_t)b.y << 32) | b.x;
+            k[u][3] = ((uint64_t)b.w << 32) | b.z;
+        }
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            int c = -1;
+#pragma unroll
+            for (int s = GS - 1; s >= 0; --s) c = k[u][s] == key[u] ? s : c;
+            cell[u] = (c >= 0 && key[u] != 0) ? (int)(grp[u] * GS) + c : -1;
+        }
+    }
+
     // Wide keys (keys128 / packed String keys).  A cell is claimed by a 64-bit CAS of the key's
     // tag into keys[cell]; the claimant then writes the 16-byte key to wkeys[cell] and
     // republishes the tag with bit 0 set.  A reader whose tag equals a cell's unpublished tag
@@ -726,6 +754,33 @@ template <int A0, int A1, int A2> struct FastOps {
             }
         }
     }
+    // the step's rows at once, every cell valid (rows without a cell of their own add into a
+    // dummy cell that is never flushed): no per-row branch
+    template <int R>
+    __device__ __forceinline__ void add_all(Table &T, const int (&cell)[R], const Row (&v)[R]) const {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            if (op(i) != 4) continue;
+            uint64_t old[R];
+#pragma unroll
+            for (int u = 0; u < R; ++u) old[u] = atomicAdd((unsigned long long *)T.acc_cell(i, cell[u]), (unsigned long long)v[u].v[i]);
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                const uint64_t lo = v[u].v[i], carry = (old[u] + lo) < old[u] ? 1ull : 0ull;
+                atomicAdd((unsigned long long *)T.acc_cell(i, cell[u]) + 1,
+                          (unsigned long long)(((int64_t)lo < 0 ? ~0ull : 0ull) + carry));
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                if (op(i) == 1) atomicAdd((unsigned long long *)T.cnt_cell(i, cell[u]), 1ull);
+                if (op(i) == 2) atomicAdd((unsigned long long *)T.acc_cell(i, cell[u]), (unsigned long long)v[u].v[i]);
+                if (op(i) == 3) atomicAdd((double *)T.acc_cell(i, cell[u]), __longlong_as_double((long long)v[u].v[i]));
+            }
+        }
+    }
     __device__ __forceinline__ void store(const RowsIO &sp, int64_t w, const Row &v) const {
         uint64_t *rec = (uint64_t *)sp.key + w * NCOL;
         rec[0] = v.key;
@@ -970,6 +1025,10 @@ struct TiledIn {
     // row f of tile_hist over the tiles [tile_base[c], tile_base[c + 1]); null: one level
     const uint32_t *tile_base;
     int fine_bits;
+    // XCD-aware bucket order: workgroup w (dispatched to XCD w % 8) takes bucket
+    // (w % 8) * (B / 8) + w / 8, so the B / 8 buckets whose runs neighbour each other inside every
+    // tile are read by one XCD and share its L2 (the lines a run shares with the next one)
+    int xcd_remap;
     uint64_t *spill[2];        // two spill arenas of >= kept rows (records)
     unsigned long long *cursor; // [0] spill rows, [1] temp groups
 };
@@ -988,7 +1047,9 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
     __shared__ uint32_t s_wsum[BT / 64];
     Table T(lds, S);
     const Ops ops{S, mode};
-    const int b = blockIdx.x;
+    const int b = (tin.xcd_remap && (gridDim.x & 7) == 0)
+                      ? (int)((blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3))
+                      : (int)blockIdx.x;
     const uint32_t *col = tin.tile_hist + (size_t)(tin.tile_base ? (b & ((1 << tin.fine_bits) - 1)) : b) * tin.T;
     const int tbeg = tin.tile_base ? (int)tin.tile_base[b >> tin.fine_bits] : 0;
     const int tend = tin.tile_base ? (int)tin.tile_base[(b >> tin.fine_bits) + 1] : tin.T;
@@ -1058,6 +1119,36 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
                 kh[u] = ops.hi(v[u]);
                 tg[u] = Ops::WIDE ? wide_tag(ku[u], kh[u]) : 0;
                 nu[u] = false;
+            }
+            if constexpr (!Ops::WIDE) {
+                // fast path (8-byte keys, never NULL): the home-group lookup of every row, the
+                // adds of the found rows (others into the NULL-key slot, unused by these keys:
+                // a dummy), then — one uniform branch — the rare rows that need the full probe
+                // (overflow group, insert) or spill
+                T.find_home<RT>(ku, cells);
+                int acell[RT];
+                bool slow[RT], anyslow = false;
+#pragma unroll
+                for (int u = 0; u < RT; ++u) {
+                    slow[u] = ok[u] && cells[u] < 0;
+                    anyslow = anyslow || slow[u];
+                    acell[u] = (ok[u] && cells[u] >= 0) ? cells[u] : S.cap + 1;
+                }
+                ops.add_all(T, acell, v);
+                if (__ballot(anyslow) == 0) return;
+#pragma unroll
+                for (int u = 0; u < RT; ++u) {
+                    if (!slow[u]) continue;
+                    int cell = T.find_or_insert(ku[u], false, allow_insert, false);
+                    if (cell < 0) cell = T.find_or_insert(ku[u], false, false, false);
+                    if (cell >= 0) {
+                        ops.add(T, cell, v[u]);
+                    } else {
+                        const int64_t w = (int64_t)atomicAdd(&T.ctrl->spill_w, 1ull);
+                        ops.store(spill, w, v[u]);
+                    }
+                }
+                return;
             }
             if constexpr (Ops::WIDE) T.find_wide_multi<RT>(ku, kh, tg, ok, allow_insert, cells);
             else T.find_or_insert_multi<RT>(ku, nu, ok, allow_insert, cells);
@@ -1262,6 +1353,17 @@ template <typename F> bool with_fast_ops(int fast, F &&f) {
     case 331: f(OpsTag<FastOps<3, 3, 1>>{}); return true;
     case 441: f(OpsTag<FastOps<4, 4, 1>>{}); return true;
     default: return false;
+    }
+}
+
+// true for the op-codes with a FastOps specialisation (with_fast_ops); any other code must take
+// the generic path from the start (its rows are staged columnar, not as FastOps records)
+inline bool fast_code_supported(int fast) {
+    switch (fast) {
+    case 310: case 210: case 410: case 300: case 200: case 400: case 100: case 231: case 221: case 331: case 441:
+        return true;
+    default:
+        return false;
     }
 }
 

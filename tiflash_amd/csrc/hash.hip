@@ -6,6 +6,7 @@
 // (Flash/Mpp/HashBaseWriterHelper.cpp:46-84), scatterColumns (:144-172), IColumn::scatter
 // (Columns/IColumn.h:655-721).  CRC32-C is computed in software (slicing-by-8 tables in LDS) and is
 // bit-identical to the reference's _mm_crc32_u64, so partition row sets match exactly.
+#include "collation.h"
 #include "common.h"
 #include "partition.h"
 
@@ -63,15 +64,16 @@ __device__ uint32_t weak_hash_bytes(const uint32_t (*t)[256], const uint8_t *pos
 
 __global__ void __launch_bounds__(256) weak_hash_string_kernel(const uint8_t *chars, const uint64_t *offsets,
                                                               const uint8_t *nullmap, const uint64_t *sel, int64_t n,
-                                                              int collator, uint32_t *h) {
+                                                              int collator, int compact, uint32_t *h) {
     __shared__ uint32_t crc[8][256];
     load_crc_lds(crc);
     __syncthreads();
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = sel ? (int64_t)sel[i] : i; // ColumnString.cpp:1256-1294 (selective rows)
         if (nullmap && nullmap[r]) continue;
-        const uint64_t prev = r ? offsets[r - 1] : 0;
-        uint64_t len = offsets[r] - prev - 1; // size - 1: the trailing '\0' is excluded
+        const int64_t rs = compact ? i : r; // a collated column holds row sel[i] at row i
+        const uint64_t prev = rs ? offsets[rs - 1] : 0;
+        uint64_t len = offsets[rs] - prev - 1; // size - 1: the trailing '\0' is excluded
         const uint8_t *s = chars + prev;
         if (collator == TFG_COLLATOR_BIN_PADDING)
             while (len > 0 && s[len - 1] == ' ') --len;
@@ -171,11 +173,18 @@ int tfg_weak_hash_update_string_selective(tfg_ctx *ctx, const uint8_t *chars, co
                                           const uint8_t *nullmap, const uint64_t *selective, int64_t n, int collator,
                                           uint32_t *h) {
     TFG_CHECK(ctx && (n == 0 || (chars && offsets && h)), TFG_ERR_INVALID_ARG, "null argument");
-    TFG_CHECK(collator >= TFG_COLLATOR_NONE && collator <= TFG_COLLATOR_BIN_PADDING, TFG_ERR_NOT_IMPLEMENTED,
-              "collator %d not supported", collator);
+    TFG_CHECK(collator_known(collator), TFG_ERR_NOT_IMPLEMENTED, "collator %d not supported", collator);
     if (n <= 0) return TFG_OK;
+    if (collator_transforms(collator)) { // ColumnString.cpp:1244: the collator's sort key is hashed
+        CollatedStrings cs;
+        if (int rc = collate_strings(ctx, collator, chars, offsets, nullmap, nullptr, selective, n, cs)) return rc;
+        hipLaunchKernelGGL(weak_hash_string_kernel, dim3(stream_grid(n, 256, 4096)), dim3(256), 0, ctx->stream,
+                           cs.chars, cs.offsets(), nullmap, selective, n, (int)TFG_COLLATOR_NONE, 1, h);
+        TFG_LAUNCH_CHECK();
+        return TFG_OK;
+    }
     hipLaunchKernelGGL(weak_hash_string_kernel, dim3(stream_grid(n, 256, 4096)), dim3(256), 0, ctx->stream, chars,
-                       offsets, nullmap, selective, n, collator, h);
+                       offsets, nullmap, selective, n, collator, 0, h);
     TFG_LAUNCH_CHECK();
     return TFG_OK;
 }

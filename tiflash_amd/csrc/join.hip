@@ -23,6 +23,7 @@
 //   never match (not inserted / not probed); LEFT and ANTI emit them as unmatched rows.
 #include <algorithm>
 
+#include "collation.h"
 #include "common.h"
 #include "partition.h"
 
@@ -762,6 +763,7 @@ struct JoinKeyCols {
     const void *col[JKMAX];
     const uint64_t *offsets[JKMAX];
     const uint8_t *nullmap[JKMAX];
+    int compact[JKMAX]; // tfg_join_keys_equal: the column holds pair i's key at row i (collated)
 };
 
 __device__ __forceinline__ uint64_t jk_mix(uint64_t h, uint64_t w) {
@@ -828,8 +830,8 @@ __global__ void join_keys_equal_kernel(JoinKeyCols pk, JoinKeyCols bk, const uin
             const int wd = pk.width[j];
             if (wd == 0) {
                 int64_t lp, lb;
-                const uint8_t *cp = jk_sort_key(pk, j, p, lp);
-                const uint8_t *cb = jk_sort_key(bk, j, b, lb);
+                const uint8_t *cp = jk_sort_key(pk, j, pk.compact[j] ? i : p, lp);
+                const uint8_t *cb = jk_sort_key(bk, j, bk.compact[j] ? i : b, lb);
                 eq = lp == lb;
                 for (int64_t t = 0; t < lp && eq; ++t) eq = cp[t] == cb[t];
             } else if (wd <= 8) {
@@ -854,8 +856,8 @@ int join_key_cols(int nkeys, const int *types, const int *collators, const void 
         k.col[j] = cols[j];
         k.nullmap[j] = nullmaps ? nullmaps[j] : nullptr;
         k.collator[j] = collators ? collators[j] : TFG_COLLATOR_NONE;
-        TFG_CHECK(k.collator[j] >= TFG_COLLATOR_NONE && k.collator[j] <= TFG_COLLATOR_BIN_PADDING,
-                  TFG_ERR_NOT_IMPLEMENTED, "join key collator %d not supported", k.collator[j]);
+        TFG_CHECK(collator_known(k.collator[j]), TFG_ERR_NOT_IMPLEMENTED, "join key collator %d not supported",
+                  k.collator[j]);
         if (types[j] == TFG_STRING) {
             TFG_CHECK(offsets && offsets[j], TFG_ERR_INVALID_ARG, "String join key %d without offsets", j);
             k.offsets[j] = offsets[j];
@@ -883,6 +885,17 @@ int tfg_join_key_hash(tfg_ctx *ctx, int nkeys, const int *key_types, const int *
     if (n <= 0) return TFG_OK;
     for (int j = 0; j < nkeys; ++j) TFG_CHECK(key_cols[j], TFG_ERR_INVALID_ARG, "null key column %d", j);
     if (int rc = set_device(ctx)) return rc;
+    // String keys under a case-insensitive collator: their sort-key columns (GeneralCI weights)
+    CollatedStrings cs[JKMAX];
+    for (int j = 0; j < nkeys; ++j) {
+        if (k.width[j] != 0 || !collator_transforms(k.collator[j])) continue;
+        if (int rc = collate_strings(ctx, k.collator[j], (const uint8_t *)k.col[j], k.offsets[j], k.nullmap[j], nullptr,
+                                     nullptr, n, cs[j]))
+            return rc;
+        k.col[j] = cs[j].chars;
+        k.offsets[j] = cs[j].offsets();
+        k.collator[j] = TFG_COLLATOR_NONE;
+    }
     hipLaunchKernelGGL(join_key_hash_kernel, dim3(stream_grid(n, 256)), dim3(256), 0, ctx->stream, k, n, out_keys,
                        out_nullmap);
     TFG_LAUNCH_CHECK();
@@ -899,6 +912,23 @@ int tfg_join_keys_equal(tfg_ctx *ctx, int nkeys, const int *key_types, const int
     if (int rc = join_key_cols(nkeys, key_types, key_collators, build_cols, build_offsets, nullptr, bk)) return rc;
     if (n_pairs <= 0) return TFG_OK;
     if (int rc = set_device(ctx)) return rc;
+    // case-insensitive String keys: the sort keys of the pairs' rows, pair i at row i
+    CollatedStrings cp[JKMAX], cb[JKMAX];
+    for (int j = 0; j < nkeys; ++j) {
+        if (pk.width[j] != 0 || !collator_transforms(pk.collator[j])) continue;
+        if (int rc = collate_strings(ctx, pk.collator[j], (const uint8_t *)pk.col[j], pk.offsets[j], nullptr, probe_idx,
+                                     nullptr, n_pairs, cp[j]))
+            return rc;
+        if (int rc = collate_strings(ctx, bk.collator[j], (const uint8_t *)bk.col[j], bk.offsets[j], nullptr, build_idx,
+                                     nullptr, n_pairs, cb[j]))
+            return rc;
+        pk.col[j] = cp[j].chars;
+        pk.offsets[j] = cp[j].offsets();
+        bk.col[j] = cb[j].chars;
+        bk.offsets[j] = cb[j].offsets();
+        pk.collator[j] = bk.collator[j] = TFG_COLLATOR_NONE;
+        pk.compact[j] = bk.compact[j] = 1;
+    }
     hipLaunchKernelGGL(join_keys_equal_kernel, dim3(stream_grid(n_pairs, 256)), dim3(256), 0, ctx->stream, pk, bk,
                        probe_idx, build_idx, pass_in, n_pairs, out_pass);
     TFG_LAUNCH_CHECK();

@@ -917,11 +917,15 @@ int run_partition_tiled(Ctx *ctx, const Sel &sel, const RowPred &pred, TiledGeom
     int nc8 = cols.ncols;
     for (int c = 0; c < cols.ncols; ++c)
         if (cols.width[c] != 8) nc8 = 0;
-    TFG_CHECK(cols.aos && (nc8 == 2 || nc8 == 3), TFG_ERR_INVALID_ARG, "tiled partition needs 2-3 word records");
+    TFG_CHECK(cols.aos && nc8 >= 1 && nc8 <= 3, TFG_ERR_INVALID_ARG, "tiled partition needs 1-3 word records");
     ProfScope _ps(ctx, name);
     return with_pred(pred, [&](auto pr) -> int {
         using PR = decltype(pr);
-        if (nc8 == 2)
+        if (nc8 == 1) // keys alone (GROUP BY with count() only)
+            hipLaunchKernelGGL((part_scatter_staged_kernel<Sel, PR, 1, true, true>), dim3(tg.L.G), dim3(ST_T),
+                               tg.sg.lds_bytes, ctx->stream, sel, pr, tg.L, (const uint64_t *)nullptr, cols,
+                               (uint32_t *)nullptr, tg.sg);
+        else if (nc8 == 2)
             hipLaunchKernelGGL((part_scatter_staged_kernel<Sel, PR, 2, true, true>), dim3(tg.L.G), dim3(ST_T),
                                tg.sg.lds_bytes, ctx->stream, sel, pr, tg.L, (const uint64_t *)nullptr, cols,
                                (uint32_t *)nullptr, tg.sg);

@@ -53,6 +53,10 @@ ExpressionActions &ExpressionActions::arithmeticConst(int op, const std::string 
     actions_.push_back({4, op, a, "", result, b});
     return *this;
 }
+ExpressionActions &ExpressionActions::arithmeticConstLeft(int op, Field a, const std::string &b, const std::string &result) {
+    actions_.push_back({5, op, "", b, result, a});
+    return *this;
+}
 
 bool ExpressionActions::singleCompare(std::string &column, int &op, Field &constant, std::string &result) const {
     if (actions_.size() != 1 || actions_[0].kind != 0) return false;
@@ -179,6 +183,24 @@ void ExpressionActions::execute(Block &block) const {
             res = c;
             break;
         }
+        case 5: { // constant Op column (e.g. 1 - l_discount): the constant-vector form of tfg_arith
+            ColumnPtr b = materialize(ctx_, block.getByName(act.b).column);
+            DataType at;
+            at.type = act.constant.type;
+            at.scale = act.constant.scale;
+            at.prec = act.constant.prec;
+            rt = arithResult(act.op, at, b->type);
+            auto c = std::const_pointer_cast<IColumn>(newColumn(ctx_, rt, n));
+            if (n)
+                check(tfg_arith(ctx_.raw(), act.op, at.type, &act.constant.bits, 1, at.scale, b->type.type, b->dataPtr(), 0,
+                                b->type.scale, rt.type, rt.scale, (int64_t)n, c->data->data()),
+                      "tfg_arith");
+            c->nullmap = mergeNulls(ctx_, *b, nullptr, n);
+            c->type.nullable = c->nullmap != nullptr;
+            rt.nullable = c->type.nullable;
+            res = c;
+            break;
+        }
         default: { // arithmetic, column or constant right operand
             ColumnPtr a = materialize(ctx_, block.getByName(act.a).column);
             ColumnPtr b;
@@ -192,6 +214,7 @@ void ExpressionActions::execute(Block &block) const {
             } else {
                 bt.type = act.constant.type;
                 bt.scale = act.constant.scale;
+                bt.prec = act.constant.prec;
                 bp = &act.constant.bits;
                 b_const = 1;
             }

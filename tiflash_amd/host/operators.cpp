@@ -852,7 +852,10 @@ AggregatingBlockInputStream::AggregatingBlockInputStream(Context &ctx, BlockInpu
                                                          const Aggregator::Params &params, bool final)
     : ctx_(ctx), input_(std::move(input)), aggregator_(ctx, params), final_(final) {}
 
-Block AggregatingBlockInputStream::getHeader() const { return Block(); }
+Block AggregatingBlockInputStream::getHeader() const { // the result block's structure
+    if (!header_) header_ = aggregator_.convertToBlock(final_).cloneEmpty();
+    return header_;
+}
 
 Block AggregatingBlockInputStream::read() {
     if (done_) return Block();

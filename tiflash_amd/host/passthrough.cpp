@@ -8,10 +8,10 @@ namespace tfa {
 
 AutoPassThroughHashAggContext::AutoPassThroughHashAggContext(Context &ctx, const Aggregator::Params &params,
                                                              uint64_t row_limit_unit, uint64_t normal_unit_num,
-                                                             uint64_t dynamic_unit_num)
+                                                             uint64_t dynamic_unit_num, size_t spill_threshold_bytes)
     : ctx_(ctx), params_(params), agg_(ctx, params), normal_row_limit_(row_limit_unit * normal_unit_num),
       dynamic_row_limit_(row_limit_unit * dynamic_unit_num), row_limit_unit_(row_limit_unit),
-      max_dynamic_row_limit_(row_limit_unit * MAX_DYNAMIC_UNIT_LIMIT) {
+      max_dynamic_row_limit_(row_limit_unit * MAX_DYNAMIC_UNIT_LIMIT), spill_threshold_(spill_threshold_bytes) {
     if (params_.keys.empty()) throw Exception("auto pass through needs GROUP BY keys", ErrorCodes::LOGICAL_ERROR);
     header_ = agg_.convertToBlock(true).cloneEmpty();
 }
@@ -23,6 +23,25 @@ size_t AutoPassThroughHashAggContext::hashMapBytes() const {
     size_t cells = 256;
     while (cells < 2 * g) cells *= 2;
     return cells * 16;
+}
+
+// the map's cells plus one aggregate-state record per group (the Arena's share)
+size_t AutoPassThroughHashAggContext::revocableBytes() const {
+    size_t state = 0;
+    for (const auto &d : params_.aggregates) state += d.function == "sum" ? 16 : 8;
+    return hashMapBytes() + agg_.size() * state;
+}
+
+bool AutoPassThroughHashAggContext::tryMarkNeedSpill() {
+    if (need_spill_) return true;
+    if (agg_.size() == 0 || already_get_data_from_hash_table_) return false; // empty(): nothing to spill
+    need_spill_ = true;
+    return true;
+}
+
+// forceState (:86-90): a map marked for spill, or already handed over, takes no more rows
+void AutoPassThroughHashAggContext::forceState() {
+    if (need_spill_ || already_get_data_from_hash_table_) state_ = State::PassThrough;
 }
 
 void AutoPassThroughHashAggContext::trySwitchFromInitState() {
@@ -146,7 +165,7 @@ void AutoPassThroughHashAggContext::onBlock(const Block &block, bool force_strea
         pass_through_rows_ += rows;
         return;
     }
-    if (already_get_data_from_hash_table_) state_ = State::PassThrough; // forceState
+    forceState();
     switch (state_) {
     case State::Init:
         agg_.executeOnBlock(block);
@@ -234,9 +253,14 @@ void AutoPassThroughHashAggContext::onBlock(const Block &block, bool force_strea
         break;
     }
     }
+    // after a block folded into the map: past the spill threshold the map is marked for spill
+    if (spill_threshold_ && !need_spill_ && revocableBytes() > spill_threshold_) tryMarkNeedSpill();
 }
 
 Block AutoPassThroughHashAggContext::tryGetDataInAdvance() {
+    // tryGetDataInAdvance (:92-104): a map marked for spill is handed over first, once
+    if (need_spill_ && !already_get_data_from_hash_table_)
+        if (Block m = getDataFromHashTable()) return m;
     if (buffer_head_ < buffer_.size()) {
         Block b = std::move(buffer_[buffer_head_++]);
         if (buffer_head_ == buffer_.size()) {

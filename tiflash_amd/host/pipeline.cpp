@@ -35,6 +35,8 @@ void checkStructure(const Operator &op, const Block &block) {
         throw Exception(op.getName() + " output does not match its header", ErrorCodes::LOGICAL_ERROR);
 }
 
+} // namespace
+
 // a zero-row block of the header's columns with allocated (1-byte) buffers, as device code expects
 Block emptyLike(Context &ctx, const Block &header) {
     Block out;
@@ -50,7 +52,6 @@ Block emptyLike(Context &ctx, const Block &header) {
     }
     return out;
 }
-} // namespace
 
 const char *toString(OperatorStatus s) {
     switch (s) {

@@ -450,6 +450,9 @@ private:
     bool has_next_ = false;
 };
 
+// A zero-row block of the header's columns with allocated (1-byte) buffers, as device code expects.
+Block emptyLike(Context &ctx, const Block &header);
+
 // Rows [offset, offset + rows) of a block (device gather; String / Nullable columns included).
 Block sliceBlock(Context &ctx, const Block &block, size_t offset, size_t rows);
 

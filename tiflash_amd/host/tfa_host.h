@@ -210,6 +210,7 @@ struct Field {
     static Field Float64(double v);
     static Field Decimal64(int64_t raw, int scale);
     int scale = 0;
+    int prec = 0; // Decimal literal precision (0 = the storage type's maximum)
 };
 
 // ExpressionActions restricted to the functions on the hot path: comparisons, and/or/not,
@@ -227,13 +228,15 @@ public:
     // result = a (+|-|*) b; b may be a constant; result type / scale as FunctionBinaryArithmetic infers
     ExpressionActions &arithmetic(int op, const std::string &a, const std::string &b, const std::string &result);
     ExpressionActions &arithmeticConst(int op, const std::string &a, Field b, const std::string &result);
+    // result = constant (+|-|*) b
+    ExpressionActions &arithmeticConstLeft(int op, Field a, const std::string &b, const std::string &result);
     void execute(Block &block) const;
     // the fused form: a single `column Op constant` predicate feeding a filter / aggregation
     bool singleCompare(std::string &column, int &op, Field &constant, std::string &result) const;
 
 private:
     struct Action {
-        int kind; // 0 compare-const, 1 compare-cols, 2 logical, 3 arith, 4 arith-const
+        int kind; // 0 compare-const, 1 compare-cols, 2 logical, 3 arith, 4 arith-const, 5 const-arith
         int op;
         std::string a, b, result;
         Field constant;
@@ -452,11 +455,26 @@ public:
     static constexpr double PassThroughRateLimit = 0.2;
     static constexpr double PreHashAggRateLimit = 0.9;
 
+    // spill_threshold_bytes (0 = off): the revocable bytes past which the map is marked for
+    // spill after a block (Aggregator::executeOnBlock -> AggSpillContext::
+    // updatePerThreadRevocableMemory -> AggregatedDataVariants::tryMarkNeedSpill,
+    // Aggregator.cpp:79-92,1236-1243).  Auto pass-through never spills to disk: a map marked for
+    // spill is handed over in advance and every later row passes through
+    // (AutoPassThroughHashAggContext.cpp:86-104).
     AutoPassThroughHashAggContext(Context &ctx, const Aggregator::Params &params, uint64_t row_limit_unit,
-                                  uint64_t normal_unit_num = 1, uint64_t dynamic_unit_num = 5);
+                                  uint64_t normal_unit_num = 1, uint64_t dynamic_unit_num = 5,
+                                  size_t spill_threshold_bytes = 0);
     void onBlock(const Block &block, bool force_streaming = false);
-    Block tryGetDataInAdvance();  // the next pass-through block, or an empty Block
+    // the map's final block first when it is marked for spill (once), else the next pass-through
+    // block, or an empty Block
+    Block tryGetDataInAdvance();
     Block getDataFromHashTable(); // the hash map's final block (once; the map is then closed)
+    // AggregateContext::needSpill(task, try_mark_need_spill = true): the query's memory policy
+    // marks the map (no-op on an empty map, as tryMarkNeedSpill)
+    bool tryMarkNeedSpill();
+    bool needSpill() const { return need_spill_; }
+    // hash map + aggregate states in bytes (AggregatedDataVariants::revocableBytes)
+    size_t revocableBytes() const;
     Block getHeader() const { return header_; }
     State state() const { return state_; }
     size_t hashMapBytes() const;
@@ -473,6 +491,9 @@ private:
     size_t adjust_processed_rows_ = 0, adjust_hit_rows_ = 0, state_processed_rows_ = 0;
     size_t pass_through_rows_ = 0, aggregated_rows_ = 0;
     bool already_get_data_from_hash_table_ = false;
+    size_t spill_threshold_ = 0;
+    bool need_spill_ = false;
+    void forceState();
     std::vector<Block> buffer_;
     size_t buffer_head_ = 0;
     std::unique_ptr<Join> lookup_; // Selective: the map's keys (LeftOuterSemi probe = "is in the map")
@@ -580,6 +601,7 @@ private:
     Aggregator aggregator_;
     bool final_;
     bool done_ = false;
+    mutable Block header_;
 };
 
 // HashJoinProbeBlockInputStream: joinBlock per probe block (DataStreams/HashJoinProbeBlockInputStream.cpp)
