@@ -1176,10 +1176,10 @@ TEST(AutoPassThroughSpillHandOff) {
             const bool was_marked = apt.needSpill();
             pass_before = apt.passThroughRows();
             apt.onBlock(b);
-            if (was_marked) { // forceState: the block passed through, the map took nothing
-                EXPECT(apt.state() == AutoPassThroughHashAggContext::State::PassThrough);
-                EXPECT(apt.passThroughRows() == pass_before + B);
-            }
+            // forceState: the block passed through, the map took nothing (the state may read
+            // Adjust afterwards: trySwitchBackAdjustState runs after the block, forceState
+            // puts it back before the next one)
+            if (was_marked) EXPECT(apt.passThroughRows() == pass_before + B);
             if (apt.needSpill() && !marked_at) marked_at = bi + 1;
             bool first = true;
             while (Block r = apt.tryGetDataInAdvance()) {

@@ -488,6 +488,50 @@ def test_join_two_pass_partitions(tfa, ctx, dev, orc, with_payload):
         assert _pairs(pi.cpu().numpy().view(np.uint32), bi.cpu().numpy().view(np.uint32)) == _pairs(epi, ebi)
 
 
+@pytest.mark.parametrize("kind", [0, 1, 2, 3])
+@pytest.mark.parametrize("pays", ["key", "key+pay", "pay2"])
+def test_join_two_level_probe_partition(tfa, ctx, dev, orc, kind, pays):
+    """Probe sides of a build above 1024 x 2560 rows (P = 2048 here) take the two-level tiled
+    partition (join.part.tiled + join.part.regroup) for 1-3 word probe records; NULL keys,
+    duplicate build keys and a skewed probe block (a third of the rows on one key) included."""
+    rng = np.random.default_rng(61 + kind)
+    nb, np_ = 3_000_000, 900_000
+    bk = rng.permutation(nb).astype(np.int64) * 4 + 1
+    bk[: nb // 10] = bk[nb // 10: nb // 5]  # 10% of the keys appear twice
+    bnull = (rng.random(nb) < 0.01).astype(np.uint8)
+    bpay = rng.integers(-2**62, 2**62, nb, dtype=np.int64)
+    pk = np.where(rng.random(np_) < 0.5, bk[rng.integers(0, nb, np_)], rng.integers(0, 2**40, np_) * 4 + 3)
+    pk[: np_ // 3] = bk[nb // 2]
+    pnull = (rng.random(np_) < 0.01).astype(np.uint8)
+    pp1 = rng.integers(-2**62, 2**62, np_, dtype=np.int64)
+    pp2 = rng.integers(-2**62, 2**62, np_, dtype=np.int64)
+    j = tfa.Join(ctx, tfa.INT64, expected_build_rows=nb)
+    j.build(torch.from_numpy(bk).to(dev), key_nullmap=torch.from_numpy(bnull).to(dev),
+            payload=[torch.from_numpy(bpay).to(dev)])
+    pkd = torch.from_numpy(pk).to(dev)
+    cols = {"key": [pk], "key+pay": [pk, pp1], "pay2": [pp1, pp2]}[pays]
+    pay = [pkd if c is pk else torch.from_numpy(c).to(dev) for c in cols]
+    op, ob, bnl = j.probe_rows(pkd, pay, 1, kind=kind, key_nullmap=torch.from_numpy(pnull).to(dev),
+                               capacity=2 * np_)
+    assert j.stats()[1] == 2048
+    ref = orc.JoinRef(orc.INT64)
+    ref.build(bk, bnull)
+    epi, ebi = ref.probe(pk, kind=kind, key_null=pnull)
+    want_p = np.stack([c[epi] for c in cols], 1)
+    got_p = np.stack([o.cpu().numpy() for o in op], 1)
+    if kind in (2, 3):
+        assert len(ob) == 0
+        assert sorted(map(tuple, got_p.tolist())) == sorted(map(tuple, want_p.tolist()))
+        return
+    unmatched = ebi == 0xFFFFFFFF
+    want_b = np.append(bpay, 0)[np.where(unmatched, nb, ebi)]
+    gotn = bnl.cpu().numpy().astype(np.int64) if kind == 1 else np.zeros(len(got_p), dtype=np.int64)
+    got = np.concatenate([got_p, ob[0].cpu().numpy()[:, None], gotn[:, None]], 1)
+    want = np.concatenate([want_p, want_b[:, None], unmatched.astype(np.int64)[:, None]], 1)
+    assert got.shape == want.shape
+    assert np.array_equal(got[np.lexsort(got.T[::-1])], want[np.lexsort(want.T[::-1])])
+
+
 @pytest.mark.parametrize("tagged", [False, True])
 def test_join_v2_c3_shape(tfa, ctx, dev, orc, tagged):
     """JoinV2 pointer table at C3's shape, scaled (2M build rows with unique keys k*4+1, 20M probe

@@ -660,12 +660,23 @@ int probe_common(tfg_join *j, int kind, const void *keys, const uint8_t *key_nul
     // then serves it instead of a second copy
     const bool key_pay0 = npay >= 1 && ppay[0] == keys && j->width == 8;
     const int prw = key_pay0 ? npay : 1 + npay;
+    // P > 1024 with payload records: the two-level tiled partition (no histogram passes, no host
+    // round trip); the index-pair form (row ids) keeps the histogram + scatter passes
+    TiledGeom tg{};
+    bool two_level = false;
+    if (npay > 0 && n > 0 && P > TWO_PASS_MIN) {
+        PCols probe_cols{};
+        probe_cols.ncols = prw;
+        for (int c = 0; c < prw; ++c) probe_cols.width[c] = 8;
+        two_level = make_two_level_geom(ctx, n, P, probe_cols, tg);
+    }
     Carver cv;
     const size_t o_wide = cv.take<uint64_t>(j->width == 8 ? 0 : n);
     const size_t o_prec = cv.take<uint64_t>(n * prw), o_pr = cv.take<uint32_t>(npay == 0 ? n : 0);
     const size_t o_poff = cv.take<uint64_t>(P + 1), o_found = cv.take<uint8_t>(n), o_cur = cv.take<uint64_t>(1);
     const size_t o_pin = cv.take<uint64_t>(JMAXW);
-    const size_t o_tmp = cv.take<uint8_t>(part_tmp_bytes(L, (size_t)prw * 8, npay == 0));
+    const size_t o_tmp = cv.take<uint8_t>(two_level ? two_level_tmp_bytes(tg, P, prw)
+                                                    : part_tmp_bytes(L, (size_t)prw * 8, npay == 0));
     void *sp;
     if (int rc = scratch_get(ctx, cv.off, &sp)) return rc;
     char *sb = (char *)sp;
@@ -713,9 +724,15 @@ int probe_common(tfg_join *j, int kind, const void *keys, const uint8_t *key_nul
         RowPred pred{};
         uint64_t *poff = (uint64_t *)(sb + o_poff);
         uint32_t *prows = npay == 0 ? (uint32_t *)(sb + o_pr) : nullptr;
-        if (int rc = run_partition<SelJoin, false>(ctx, sel, pred, L, pc, prows, nullptr, poff, sb + o_tmp,
-                                                   "join.part.hist", "join.part.scatter"))
+        if (two_level) {
+            pc.aos = 1;
+            if (int rc = run_partition_two_level(ctx, sel, pred, tg, P, pc, poff, sb + o_tmp, "join.part.tiled",
+                                                 "join.part.regroup"))
+                return rc;
+        } else if (int rc = run_partition<SelJoin, false>(ctx, sel, pred, L, pc, prows, nullptr, poff, sb + o_tmp,
+                                                          "join.part.hist", "join.part.scatter")) {
             return rc;
+        }
         TFG_HIP(hipMemsetAsync(sb + o_found, 0, n, ctx->stream));
         A.prec = (const uint64_t *)(sb + o_prec);
         A.prows = prows;

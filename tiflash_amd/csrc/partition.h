@@ -463,6 +463,11 @@ inline size_t part_tmp_bytes(const PartLayout &L) {
     return ((size_t)e * 4 + 255) / 256 * 256 + ((size_t)(e + 1) * 8 + 255) / 256 * 256 + scan_tmp_bytes(e) + 256;
 }
 inline size_t align256(size_t b) { return (b + 255) / 256 * 256; }
+inline uint32_t bits_of_pow2(uint32_t p) {
+    uint32_t b = 0;
+    while ((1u << b) < p) ++b;
+    return b;
+}
 // ... plus, for callers that set PCols::two_pass, the first pass's records (row_bytes per row),
 // row ids and offsets
 inline size_t part_tmp_bytes(const PartLayout &L, size_t row_bytes, bool perm) {
@@ -501,16 +506,25 @@ struct StagedGeom {
     // TRS = TR + (align - 1) * P rows); make_tiled_geom keeps them dense (align 1)
     int align;
     int TRS;
+    // TILED two-level form: the selector returns a (P << fine_bits)-way radix; the tile is sorted
+    // by its top bits (radix >> fine_bits) and every workgroup adds its rows' full radices into
+    // fine_counts (LDS histogram at fh_off, one global atomic per non-zero bin at the end)
+    int fine_bits;
+    int fh_off;
+    uint32_t *fine_counts;
+    int allow_narrow; // TILED narrow tiles (u32 keys) permitted: consumers that read records
+                      // word by word (regroup_scatter_kernel) need the wide form
 };
 
 // LDS bytes a staged-scatter workgroup uses: one workgroup per CU.
 constexpr size_t STAGE_LDS_BUDGET = (size_t)150 * 1024;
 
-inline bool make_staged_geom(uint32_t P, const PCols &cols, bool perm, bool crc, StagedGeom &g) {
+inline bool make_staged_geom(uint32_t P, const PCols &cols, bool perm, bool crc, StagedGeom &g, int fine_bits = 0) {
     if (P > 4096) return false;
     size_t row_bytes = 2 + (perm ? 4 : 0);
     for (int j = 0; j < cols.ncols; ++j) row_bytes += cols.width[j];
-    const size_t fixed = (size_t)P * 16 + (crc ? 8192 : 0) + 16 * (PCOLS + 2);
+    const size_t fh_bytes = fine_bits ? ((size_t)P << fine_bits) * 4 : 0;
+    const size_t fixed = (size_t)P * 16 + (crc ? 8192 : 0) + 16 * (PCOLS + 2) + fh_bytes;
     const size_t budget = STAGE_LDS_BUDGET; // LDS per workgroup (default: one workgroup per CU)
     if (fixed + row_bytes * ST_T * 2 > budget) return false;
     int tr = (int)((budget - fixed) / row_bytes) / ST_T * ST_T;
@@ -528,7 +542,11 @@ inline bool make_staged_geom(uint32_t P, const PCols &cols, bool perm, bool crc,
     if (perm) off += (size_t)tr * 4;
     g.crc_off = (int)((off + 15) & ~size_t(15));
     g.red_off = g.crc_off + (crc ? 8192 : 0);
-    g.lds_bytes = g.red_off + (ST_T / 64 + 2) * 4; // red[]: per-wave sums + the tile total
+    g.fh_off = g.red_off + (ST_T / 64 + 2) * 4; // red[]: per-wave sums + the tile total
+    g.fine_bits = fine_bits;
+    g.fine_counts = nullptr;
+    g.allow_narrow = 1;
+    g.lds_bytes = g.fh_off + (int)fh_bytes;
     return true;
 }
 
@@ -560,6 +578,9 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
     // 32 bits is written as a u32 key array + a u64 value array (12 B a row instead of 16), and
     // its tile_hist entries carry TILE_NARROW; red[ST_T / 64 + 1] collects "a wide key was seen"
     constexpr bool NARROW = TILED && AOS && NC8 == 2 && !SelWideKey<Sel>::value;
+    uint32_t *fh = reinterpret_cast<uint32_t *>(lds + g.fh_off); // TILED && fine_bits: P << fine_bits bins
+    if (TILED && g.fine_bits)
+        for (uint32_t p = threadIdx.x; p < (P << g.fine_bits); p += ST_T) fh[p] = 0;
     for (uint32_t tb = begin; tb < end; tb += (uint32_t)g.TR) {
         for (uint32_t p = threadIdx.x; p < P; p += ST_T) hist[p] = 0;
         if (NARROW && threadIdx.x == 0) red[ST_T / 64 + 1] = 0;
@@ -589,7 +610,11 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
                 bq[j] = 0xFFFFFFFFu;
                 const uint32_t r = tb + (uint32_t)j * ST_T + threadIdx.x;
                 if (j < per && r < end && pred.eval(pl[q])) {
-                    const uint32_t b = sel.part(crc, kl[q], r);
+                    uint32_t b = sel.part(crc, kl[q], r);
+                    if (TILED && g.fine_bits && b < (P << g.fine_bits)) {
+                        atomicAdd(&fh[b], 1u);
+                        b >>= g.fine_bits;
+                    }
                     if (b < P) bq[j] = b;
                 }
                 if constexpr (NC8 > 0) v[0][j] = kl[q].bits;
@@ -656,7 +681,7 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
         __syncthreads();
         const uint32_t kept = red[ST_T / 64];
         const uint32_t tile = blockIdx.x * (uint32_t)g.tps + (tb - begin) / (uint32_t)g.TR;
-        const bool narrow = NARROW && red[ST_T / 64 + 1] == 0;
+        const bool narrow = NARROW && g.allow_narrow && red[ST_T / 64 + 1] == 0;
         if constexpr (TILED)
             for (uint32_t p = threadIdx.x; p < P; p += ST_T)
                 g.tile_hist[(size_t)p * g.T + tile] = pstart[p] | (narrow ? TILE_NARROW : 0u) | (hist[p] << 16);
@@ -761,6 +786,9 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
             for (uint32_t p = threadIdx.x; p < P; p += ST_T) run[p] += hist[p];
         __syncthreads();
     }
+    if (TILED && g.fine_bits)
+        for (uint32_t p = threadIdx.x; p < (P << g.fine_bits); p += ST_T)
+            if (fh[p]) atomicAdd(&g.fine_counts[p], fh[p]);
 }
 
 template <typename Sel, bool STABLE = true>
@@ -896,8 +924,8 @@ struct TiledGeom {
     int64_t out_rows; // T * TRS
 };
 
-inline bool make_tiled_geom(Ctx *ctx, int64_t n, uint32_t P, const PCols &cols, TiledGeom &tg) {
-    if (n <= 0 || !make_staged_geom(P, cols, false, false, tg.sg)) return false;
+inline bool make_tiled_geom(Ctx *ctx, int64_t n, uint32_t P, const PCols &cols, TiledGeom &tg, int fine_bits = 0) {
+    if (n <= 0 || !make_staged_geom(P, cols, false, false, tg.sg, fine_bits)) return false;
     tg.L = make_wide_layout(n, P, ctx->cu_count, 1u << 30, 3); // 3 segments per CU: measured 0.77 vs 0.83 ms at 1
     tg.sg.tps = (int)((tg.L.seg + tg.sg.TR - 1) / tg.sg.TR);
     tg.sg.T = (int)tg.L.G * tg.sg.tps;
@@ -936,6 +964,169 @@ int run_partition_tiled(Ctx *ctx, const Sel &sel, const RowPred &pred, TiledGeom
         TFG_LAUNCH_CHECK();
         return TFG_OK;
     });
+}
+
+// ---------------------------------------------------------------- two-level tiled partition
+// P = RS_C << fine_bits destinations with contiguous, destination-major output, no histogram
+// pass and no host round trip (the join's probe side, P = 2048 / 4096):
+//   pass 1  run_partition_tiled into RS_C coarse radix groups; each tile is written sorted by the
+//           coarse radix and the workgroups add every row's full radix into a P-bin histogram;
+//   scan    of that histogram -> the destinations' offsets (offsets_out) and append cursors;
+//   pass 2  regroup_scatter_kernel: one workgroup per (coarse group, RS_TPC tiles) reads the
+//           group's runs (~128 rows each) from those tiles, counting-sorts a batch of RS_BR rows
+//           by the fine radix in LDS, claims each fine run's place with one global atomic and
+//           writes the runs out contiguously.
+// Bytes: 2 x (read + write) of the records, against 2 x (histogram read + read + write) for the
+// histogram + scatter form (run_two_pass).  Order inside a destination is unspecified.
+constexpr uint32_t RS_C = 64;
+constexpr int RS_T = 512, RS_RPT = 4, RS_BR = RS_T * RS_RPT, RS_TPC = 64;
+
+template <int NW>
+__global__ void __launch_bounds__(RS_T) regroup_scatter_kernel(const uint64_t *rec, const uint32_t *tile_hist, int T,
+                                                               int TRS, int fine_bits, uint32_t shift,
+                                                               unsigned long long *cursor, uint64_t *out) {
+    __shared__ uint32_t tstart[RS_TPC], tpre[RS_TPC + 1];
+    __shared__ uint32_t hist[64], hstart[64];
+    __shared__ unsigned long long gbase[64];
+    __shared__ uint64_t stage[NW][RS_BR];
+    __shared__ uint8_t sf[RS_BR];
+    const unsigned lane = threadIdx.x & 63;
+    const uint32_t c = blockIdx.x % RS_C;
+    const int t0 = (int)(blockIdx.x / RS_C) * RS_TPC;
+    const int nt = min(RS_TPC, T - t0);
+    const uint32_t fmask = (1u << fine_bits) - 1;
+    if (threadIdx.x < 64) { // one wave: the runs of group c in tiles t0 .. t0 + nt, scanned
+        uint32_t cnt = 0, st = 0;
+        if ((int)lane < nt) {
+            const uint32_t h = tile_hist[(size_t)c * T + t0 + lane];
+            st = h & (TILE_NARROW - 1);
+            cnt = h >> 16;
+        }
+        uint32_t x = cnt;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d, 64);
+            if (lane >= (unsigned)d) x += y;
+        }
+        tstart[lane] = st;
+        tpre[lane + 1] = x;
+        if (lane == 0) tpre[0] = 0;
+    }
+    __syncthreads();
+    const uint32_t R = tpre[nt];
+    for (uint32_t b0 = 0; b0 < R; b0 += RS_BR) {
+        if (threadIdx.x < 64) hist[threadIdx.x] = 0;
+        __syncthreads();
+        uint64_t v[NW][RS_RPT];
+        uint32_t fq[RS_RPT];
+#pragma unroll
+        for (int u = 0; u < RS_RPT; ++u) {
+            const uint32_t i = b0 + (uint32_t)u * RS_T + threadIdx.x;
+            fq[u] = 0xFFFFFFFFu;
+            if (i >= R) continue;
+            int lo = 0, hi = nt; // the run holding row i: tpre[lo] <= i < tpre[lo + 1]
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (tpre[mid] <= i) lo = mid;
+                else hi = mid;
+            }
+            const size_t pos = (size_t)(t0 + lo) * (uint32_t)TRS + tstart[lo] + (i - tpre[lo]);
+#pragma unroll
+            for (int w = 0; w < NW; ++w) v[w][u] = rec[pos * NW + w];
+            fq[u] = 0;
+        }
+#pragma unroll
+        for (int u = 0; u < RS_RPT; ++u) {
+            if (fq[u]) continue;
+            const uint32_t f = fib_part(v[0][u], shift) & fmask;
+            fq[u] = f | (atomicAdd(&hist[f], 1u) << 16);
+        }
+        __syncthreads();
+        if (threadIdx.x < 64) {
+            const uint32_t h = hist[lane];
+            uint32_t x = h;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t y = __shfl_up(x, d, 64);
+                if (lane >= (unsigned)d) x += y;
+            }
+            hstart[lane] = x - h;
+            if (h) gbase[lane] = atomicAdd(&cursor[(c << fine_bits) + lane], (unsigned long long)h);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < RS_RPT; ++u) {
+            if (fq[u] == 0xFFFFFFFFu) continue;
+            const uint32_t f = fq[u] & 0xFFFFu, s = hstart[f] + (fq[u] >> 16);
+#pragma unroll
+            for (int w = 0; w < NW; ++w) stage[w][s] = v[w][u];
+            sf[s] = (uint8_t)f;
+        }
+        __syncthreads();
+        const uint32_t kept = min((uint32_t)RS_BR, R - b0);
+        for (uint32_t s = threadIdx.x; s < kept; s += RS_T) {
+            const uint32_t f = sf[s];
+            const uint64_t gp = gbase[f] + (s - hstart[f]);
+#pragma unroll
+            for (int w = 0; w < NW; ++w) out[gp * NW + w] = stage[w][s];
+        }
+        __syncthreads();
+    }
+}
+
+// geometry of the two-level form (false: not applicable -> use run_partition)
+inline bool make_two_level_geom(Ctx *ctx, int64_t n, uint32_t P, const PCols &cols, TiledGeom &tg) {
+    if (P <= RS_C || P > RS_C * 64 || (P & (P - 1)) || cols.ncols < 1 || cols.ncols > 3 || n <= 0) return false;
+    for (int c = 0; c < cols.ncols; ++c)
+        if (cols.width[c] != 8) return false;
+    PCols pc = cols;
+    pc.aos = 1;
+    if (!make_tiled_geom(ctx, n, RS_C, pc, tg, (int)bits_of_pow2(P / RS_C))) return false;
+    tg.sg.allow_narrow = 0;
+    return true;
+}
+inline size_t two_level_tmp_bytes(const TiledGeom &tg, uint32_t P, int ncols) {
+    return align256((size_t)tg.out_rows * ncols * 8) + align256((size_t)RS_C * tg.sg.T * 4) + align256((size_t)P * 4) +
+           align256((size_t)P * 8) + align256(scan_tmp_bytes(P));
+}
+
+// sel: the full P-way radix (its shift for P).  cols: 8-byte columns (key first), written as
+// interleaved records of cols.ncols words at cols.out[0].  offsets_out: device u64[P + 1].
+template <typename Sel>
+int run_partition_two_level(Ctx *ctx, const Sel &sel, const RowPred &pred, TiledGeom tg, uint32_t P, const PCols &cols,
+                            uint64_t *offsets_out, void *tmp, const char *name1, const char *name2) {
+    const int nc = cols.ncols;
+    char *x = (char *)tmp;
+    uint64_t *inter = (uint64_t *)x;
+    x += align256((size_t)tg.out_rows * nc * 8);
+    uint32_t *tile_hist = (uint32_t *)x;
+    x += align256((size_t)RS_C * tg.sg.T * 4);
+    uint32_t *fine = (uint32_t *)x;
+    x += align256((size_t)P * 4);
+    unsigned long long *cursor = (unsigned long long *)x;
+    x += align256((size_t)P * 8);
+    void *scan_tmp = x;
+    const int fine_bits = tg.sg.fine_bits;
+    TFG_CHECK(P == (RS_C << fine_bits) && fine_bits >= 1 && fine_bits <= 6, TFG_ERR_INVALID_ARG,
+              "two-level partition: %u destinations", P);
+    TFG_HIP(hipMemsetAsync(fine, 0, (size_t)P * 4, ctx->stream));
+    tg.sg.fine_counts = fine;
+    PCols c1 = cols;
+    c1.aos = 1;
+    c1.out[0] = inter;
+    if (int rc = run_partition_tiled(ctx, sel, pred, tg, c1, tile_hist, name1)) return rc;
+    if (int rc = exclusive_scan_u32(ctx, fine, offsets_out, P, scan_tmp)) return rc;
+    TFG_HIP(hipMemcpyAsync(cursor, offsets_out, (size_t)P * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    const unsigned grid = RS_C * (unsigned)((tg.sg.T + RS_TPC - 1) / RS_TPC);
+    ProfScope _ps(ctx, name2);
+    uint64_t *out = (uint64_t *)cols.out[0];
+    switch (nc) {
+    case 1: hipLaunchKernelGGL(regroup_scatter_kernel<1>, dim3(grid), dim3(RS_T), 0, ctx->stream, inter, tile_hist, tg.sg.T, tg.sg.TRS, fine_bits, sel.shift, cursor, out); break;
+    case 2: hipLaunchKernelGGL(regroup_scatter_kernel<2>, dim3(grid), dim3(RS_T), 0, ctx->stream, inter, tile_hist, tg.sg.T, tg.sg.TRS, fine_bits, sel.shift, cursor, out); break;
+    default: hipLaunchKernelGGL(regroup_scatter_kernel<3>, dim3(grid), dim3(RS_T), 0, ctx->stream, inter, tile_hist, tg.sg.T, tg.sg.TRS, fine_bits, sel.shift, cursor, out); break;
+    }
+    TFG_LAUNCH_CHECK();
+    return TFG_OK;
 }
 
 } // namespace tfg

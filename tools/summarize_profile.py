@@ -44,6 +44,8 @@ NAME_MAP = [
     (r"agg_result_kernel", "agg.result"),
     (r"part_hist_kernel<tfg::SelRec8", "part.hist.pass2"),
     (r"part_scatter_staged_kernel<tfg::SelRec8", "part.scatter.pass2"),
+    (r"part_scatter_staged_kernel<tfg::SelJoin.*true, true>", "join.part.tiled"),
+    (r"regroup_scatter_kernel", "join.part.regroup"),
     (r"part_hist_kernel<tfg::SelJoin", "join.part.hist"),
     (r"part_scatter.*<tfg::SelJoin", "join.part.scatter"),
     (r"join_probe_kernel", "join.probe"),
