@@ -373,17 +373,14 @@ struct Table {
         }
         for (;;) {
             uint64_t k[R][GS];
-            asm volatile("" ::: "memory"); // re-read the cells every round (other waves publish)
+            // the tags are read with relaxed atomic loads: other waves CAS and publish them
+            // concurrently, and every round must see their current values
 #pragma unroll
             for (int u = 0; u < R; ++u)
-                if (live[u]) {
-                    const uint4 a = *reinterpret_cast<const uint4 *>(&keys[grp[u] * GS]);
-                    const uint4 b = *reinterpret_cast<const uint4 *>(&keys[grp[u] * GS + 2]);
-                    k[u][0] = ((uint64_t)a.y << 32) | a.x;
-                    k[u][1] = ((uint64_t)a.w << 32) | a.z;
-                    k[u][2] = ((uint64_t)b.y << 32) | b.x;
-                    k[u][3] = ((uint64_t)b.w << 32) | b.z;
-                }
+                if (live[u])
+#pragma unroll
+                    for (int s = 0; s < GS; ++s)
+                        k[u][s] = __hip_atomic_load(&keys[grp[u] * GS + s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             bool any = false;
 #pragma unroll
             for (int u = 0; u < R; ++u) {

@@ -13,10 +13,11 @@
 //   probe:    probe rows are partitioned the same way (records {key, payload...}); one workgroup
 //             per partition loads the build partition into an LDS table (u64 keys, grouped
 //             probing of 4 cells per 32-byte read, 64-bit CAS; per key a chain of build rows and
-//             its length), streams the probe records, and emits matches through an LDS buffer of
-//             (probe record, build row) pairs flushed with one global atomic per flush.  The flush
-//             materialises the output rows itself — probe payload words from the probe record,
-//             build payload words from the build record — so the joined block needs no gathers.
+//             its length) and streams the probe records JT * JRPT at a time: a block scan of the
+//             rows' output counts, one global atomic for the step's output range, and every
+//             thread writes its rows at its scanned offset — probe payload words from the record
+//             in registers, build payload words from the build record — so the joined block
+//             needs no gathers.
 //             The index-pair API (tfg_join_probe) is the same kernel with row ids as the payload.
 //   Build partitions larger than one LDS chunk (duplicate-heavy keys) are processed chunk by
 //   chunk with a per-probe-row found flag so LEFT / SEMI / ANTI stay exact.  Rows with a NULL key
@@ -33,7 +34,6 @@ constexpr int JT = 512;      // probe workgroup
 constexpr int JCAP = 4096;   // LDS table cells (power of two)
 constexpr int JGS = 4;       // cells per probe group (one 32-byte read)
 constexpr int JCHUNK = 4096; // build rows per LDS pass (row index fits 16 bits)
-constexpr int JBUF = 992;    // buffered output pairs (JLds stays under 80 KB: two workgroups per CU)
 constexpr int JRPT = 4;      // probe rows per thread per step
 constexpr int JFILL = 2560;  // target build rows per partition (table load ~0.63)
 constexpr int JMAXW = 2;     // payload words per side
@@ -97,10 +97,7 @@ struct JLds {
     uint32_t head[JCAP + 1]; // [JCAP] = chain of key 0 (ZeroValueStorage)
     uint32_t cnt[JCAP + 1];
     uint16_t next[JCHUNK];
-    uint32_t buf_p[JBUF]; // staged probe position
-    uint32_t buf_b[JBUF]; // build row within the chunk, 0xFFFFFFFF = none
     uint32_t red[JT / 64 + 2];
-    unsigned buf_n;
     unsigned long long base;
 };
 
@@ -126,36 +123,6 @@ __device__ __forceinline__ uint32_t jblock_scan(uint32_t v, uint32_t *red, uint3
     __syncthreads();
     total = tot;
     return off + x - v;
-}
-
-// writes buffered pairs as output rows (all threads; caller synchronised)
-__device__ void flush_pairs(const JoinArgs &A, JLds &L, int64_t ps, int64_t chunk_row0) {
-    const unsigned n = L.buf_n;
-    if (n == 0) return;
-    if (threadIdx.x == 0) L.base = atomicAdd(A.cursor, (unsigned long long)n);
-    __syncthreads();
-    const uint64_t base = L.base;
-    for (unsigned i = threadIdx.x; i < n; i += JT) {
-        const uint64_t pos = base + i;
-        if (pos >= A.capacity) continue;
-        const uint32_t p = L.buf_p[i], b = L.buf_b[i];
-        if (A.pw == 0) {
-            ((uint32_t *)A.out_p[0])[pos] = A.prows[ps + p];
-        } else {
-            const uint64_t *rec = A.prec + (ps + p) * A.prw;
-            for (int w = 0; w < A.pw; ++w) ((uint64_t *)A.out_p[w])[pos] = rec[A.pw0 + w];
-        }
-        if (A.out_bnull) A.out_bnull[pos] = b == 0xFFFFFFFFu;
-        if (A.bw == 0) {
-            if (A.out_b[0]) ((uint32_t *)A.out_b[0])[pos] = b == 0xFFFFFFFFu ? 0xFFFFFFFFu : A.brows[chunk_row0 + b];
-        } else if (A.out_b[0]) {
-            const uint64_t *rec = A.brec + (chunk_row0 + (b == 0xFFFFFFFFu ? 0 : b)) * (1 + A.bw);
-            for (int w = 0; w < A.bw; ++w) ((uint64_t *)A.out_b[w])[pos] = b == 0xFFFFFFFFu ? 0ull : rec[1 + w];
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) L.buf_n = 0;
-    __syncthreads();
 }
 
 __device__ __forceinline__ int jfind(const JLds &L, uint64_t key, int slot_shift) {
@@ -192,6 +159,9 @@ __device__ __forceinline__ int jinsert(JLds &L, uint64_t key, int slot_shift) {
     }
 }
 
+// PRW probe record words, BW build payload words: compile-time, so the pipelined registers
+// (two steps' records + the first match's build payload) stay within 4 waves per SIMD
+template <int PRW, int BW>
 __global__ void __launch_bounds__(JT) join_probe_kernel(JoinArgs A) {
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
     JLds &L = *reinterpret_cast<JLds *>(lds_raw);
@@ -201,8 +171,7 @@ __global__ void __launch_bounds__(JT) join_probe_kernel(JoinArgs A) {
     if (pe == ps) return; // no probe rows in this partition
     const int64_t nb = be - bs;
     const int chunks = nb == 0 ? 1 : (int)((nb + JCHUNK - 1) / JCHUNK);
-    const int brw = 1 + A.bw, prw = A.prw;
-    if (threadIdx.x == 0) L.buf_n = 0;
+    constexpr int brw = 1 + BW, prw = PRW;
     for (int c = 0; c < chunks; ++c) {
         for (int i = threadIdx.x; i < JCAP + 1; i += JT) {
             if (i < JCAP) L.keys[i] = 0;
@@ -224,15 +193,25 @@ __global__ void __launch_bounds__(JT) join_probe_kernel(JoinArgs A) {
         // ---- stream the probe partition, JRPT rows per thread per step (their record loads in
         // flight together; one block scan and one barrier pair per JT * JRPT rows)
         const bool pairs = A.kind <= TFG_JOIN_LEFT; // SEMI / ANTI emit the probe row alone
-        for (int64_t step = ps; step < pe; step += (int64_t)JT * JRPT) {
-            uint64_t key[JRPT];
-            unsigned head[JRPT];
-            uint32_t cnt[JRPT], e[JRPT];
+        const bool bpay = pairs && BW > 0 && A.out_b[0];
+        constexpr int64_t STEP = (int64_t)JT * JRPT;
+        // software pipelined: the next step's record loads are issued before this step's output
+        // range is claimed, so their latency overlaps the global atomic and the stores
+        auto load_step = [&](int64_t st, uint64_t (&dst)[JRPT][PRW]) __attribute__((always_inline)) {
 #pragma unroll
             for (int u = 0; u < JRPT; ++u) {
-                const int64_t r = step + u * JT + threadIdx.x;
-                if (r < pe) key[u] = A.prec[r * prw];
+                const int64_t r = st + u * JT + threadIdx.x;
+                if (r < pe)
+#pragma unroll
+                    for (int w = 0; w < PRW; ++w) dst[u][w] = A.prec[r * prw + w];
             }
+        };
+        uint64_t rw[JRPT][PRW]; // the probe records (key + payload words)
+        load_step(ps, rw);
+        for (int64_t step = ps; step < pe; step += STEP) {
+            unsigned head[JRPT];
+            uint32_t cnt[JRPT], e[JRPT];
+            uint64_t bp[JRPT][BW > 0 ? BW : 1]; // the first match's build payload words, loaded early
             uint32_t esum = 0;
 #pragma unroll
             for (int u = 0; u < JRPT; ++u) {
@@ -242,10 +221,15 @@ __global__ void __launch_bounds__(JT) join_probe_kernel(JoinArgs A) {
                 cnt[u] = 0;
                 e[u] = 0;
                 if (!valid) continue;
-                const int cell = jfind(L, key[u], A.slot_shift);
+                const int cell = jfind(L, rw[u][0], A.slot_shift);
                 if (cell >= 0) {
                     head[u] = L.head[cell];
                     cnt[u] = L.cnt[cell];
+                }
+                if (bpay && cnt[u]) {
+                    const uint64_t *rec = A.brec + (c0 + head[u]) * brw;
+#pragma unroll
+                    for (int w = 0; w < BW; ++w) bp[u][w] = rec[1 + w];
                 }
                 bool prev_found = false;
                 if (chunks > 1) {
@@ -260,53 +244,53 @@ __global__ void __launch_bounds__(JT) join_probe_kernel(JoinArgs A) {
                 }
                 esum += e[u];
             }
+            // one output range per workgroup step (one global atomic), each thread's rows at its
+            // scanned offset: consecutive lanes write consecutive rows
             uint32_t total;
             const uint32_t off = jblock_scan(esum, L.red, total);
-            if (total == 0) continue;
-            if (L.buf_n + total > (unsigned)JBUF) flush_pairs(A, L, ps, c0);
-            if (total > (unsigned)JBUF) {
-                // more pairs in this step than the buffer holds: emit it in buffer-sized rounds
-                for (uint32_t lo = 0; lo < total; lo += JBUF) {
-                    const uint32_t hi = std::min<uint32_t>(total, lo + JBUF);
-                    uint32_t slot = off;
+            uint64_t nx[JRPT][PRW];
+            if (step + STEP < pe) load_step(step + STEP, nx);
+            if (total) {
+                if (threadIdx.x == 0) L.base = atomicAdd(A.cursor, (unsigned long long)total);
+                __syncthreads();
+                uint64_t pos = L.base + off;
 #pragma unroll
-                    for (int u = 0; u < JRPT; ++u) {
-                        const int64_t r = step + u * JT + threadIdx.x;
-                        unsigned jb = head[u];
-                        for (uint32_t q = 0; q < e[u]; ++q, ++slot) {
-                            const bool pair = pairs && q < cnt[u];
-                            if (slot >= lo && slot < hi) {
-                                L.buf_p[slot - lo] = (uint32_t)(r - ps);
-                                L.buf_b[slot - lo] = pair ? jb : 0xFFFFFFFFu;
+                for (int u = 0; u < JRPT; ++u) {
+                    const int64_t r = step + u * JT + threadIdx.x;
+                    unsigned jb = head[u];
+                    for (uint32_t q = 0; q < e[u]; ++q, ++pos) {
+                        const bool pair = pairs && q < cnt[u];
+                        if (pos < A.capacity) {
+                            if (A.pw == 0) {
+                                ((uint32_t *)A.out_p[0])[pos] = A.prows[r];
+                            } else {
+#pragma unroll
+                                for (int w = 0; w < PRW; ++w)
+                                    if (w < A.pw) ((uint64_t *)A.out_p[w])[pos] = (A.pw0 ? rw[u][w + 1 < PRW ? w + 1 : w] : rw[u][w]);
                             }
-                            if (pair) jb = L.next[jb];
-                        }
-                    }
-                    __syncthreads();
-                    if (threadIdx.x == 0) L.buf_n = hi - lo;
-                    __syncthreads();
-                    flush_pairs(A, L, ps, c0);
-                }
-                continue;
-            }
-            unsigned pos = L.buf_n + off;
+                            if (A.out_bnull) A.out_bnull[pos] = !pair;
+                            if (A.out_b[0]) {
+                                if constexpr (BW == 0) {
+                                    ((uint32_t *)A.out_b[0])[pos] = pair ? A.brows[c0 + jb] : 0xFFFFFFFFu;
+                                } else if (pair && q == 0) {
 #pragma unroll
-            for (int u = 0; u < JRPT; ++u) {
-                const int64_t r = step + u * JT + threadIdx.x;
-                unsigned jb = head[u];
-                for (uint32_t q = 0; q < e[u]; ++q, ++pos) {
-                    const bool pair = pairs && q < cnt[u];
-                    L.buf_p[pos] = (uint32_t)(r - ps);
-                    L.buf_b[pos] = pair ? jb : 0xFFFFFFFFu;
-                    if (pair) jb = L.next[jb];
+                                    for (int w = 0; w < BW; ++w) ((uint64_t *)A.out_b[w])[pos] = bp[u][w];
+                                } else {
+                                    const uint64_t *rec = A.brec + (c0 + (pair ? jb : 0)) * brw;
+#pragma unroll
+                                    for (int w = 0; w < BW; ++w) ((uint64_t *)A.out_b[w])[pos] = pair ? rec[1 + w] : 0ull;
+                                }
+                            }
+                        }
+                        if (pair) jb = L.next[jb];
+                    }
                 }
             }
-            __syncthreads();
-            if (threadIdx.x == 0) L.buf_n += total;
-            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < JRPT; ++u)
+#pragma unroll
+                for (int w = 0; w < PRW; ++w) rw[u][w] = nx[u][w];
         }
-        __syncthreads();
-        flush_pairs(A, L, ps, c0); // pairs refer to this chunk's build rows
         __syncthreads();
     }
 }
@@ -740,7 +724,20 @@ int probe_common(tfg_join *j, int kind, const void *keys, const uint8_t *key_nul
         A.found = (uint8_t *)(sb + o_found);
         {
             ProfScope _ps(ctx, "join.probe");
-            hipLaunchKernelGGL(join_probe_kernel, dim3(P), dim3(JT), sizeof(JLds), ctx->stream, A);
+            TFG_CHECK(prw >= 1 && prw <= 3 && A.bw >= 0 && A.bw <= 2, TFG_ERR_INVALID_ARG, "join record words");
+            void (*kern)(JoinArgs);
+            switch (prw * 3 + A.bw) {
+            case 3: kern = join_probe_kernel<1, 0>; break;
+            case 4: kern = join_probe_kernel<1, 1>; break;
+            case 5: kern = join_probe_kernel<1, 2>; break;
+            case 6: kern = join_probe_kernel<2, 0>; break;
+            case 7: kern = join_probe_kernel<2, 1>; break;
+            case 8: kern = join_probe_kernel<2, 2>; break;
+            case 9: kern = join_probe_kernel<3, 0>; break;
+            case 10: kern = join_probe_kernel<3, 1>; break;
+            default: kern = join_probe_kernel<3, 2>; break;
+            }
+            hipLaunchKernelGGL(kern, dim3(P), dim3(JT), sizeof(JLds), ctx->stream, A);
         }
         TFG_LAUNCH_CHECK();
         if (key_nullmap && (kind == TFG_JOIN_LEFT || kind == TFG_JOIN_ANTI)) {
