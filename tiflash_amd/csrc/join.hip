@@ -98,6 +98,8 @@ struct JLds {
     uint32_t cnt[JCAP + 1];
     uint16_t next[JCHUNK];
     uint32_t red[JT / 64 + 2];
+    uint64_t red64[JT / 64];
+    uint32_t redbig[JT / 64];
     unsigned long long base;
 };
 
@@ -122,6 +124,38 @@ __device__ __forceinline__ uint32_t jblock_scan(uint32_t v, uint32_t *red, uint3
     }
     __syncthreads();
     total = tot;
+    return off + x - v;
+}
+
+// Block scan of the four 16-bit output counts of a thread's rows (fields u = 0..3 of v, each
+// count <= 127 so no field overflows over 512 threads): off = the exclusive prefix of every
+// field, total = the block totals; any_big = some thread flagged a row with > 127 outputs.
+__device__ __forceinline__ uint64_t jblock_scan4(uint64_t v, bool big, JLds &L, uint64_t &total, bool &any_big) {
+    const unsigned lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint64_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(x, d, 64);
+        if (lane >= (unsigned)d) x += y;
+    }
+    const bool wbig = __ballot(big) != 0;
+    if (lane == 63) {
+        L.red64[wave] = x;
+        L.redbig[wave] = wbig;
+    }
+    __syncthreads();
+    uint64_t off = 0, tot = 0;
+    bool ab = false;
+#pragma unroll
+    for (int w = 0; w < JT / 64; ++w) {
+        const uint64_t sw = L.red64[w];
+        if (w < (int)wave) off += sw;
+        tot += sw;
+        ab |= L.redbig[w] != 0;
+    }
+    __syncthreads();
+    total = tot;
+    any_big = ab;
     return off + x - v;
 }
 
@@ -244,19 +278,39 @@ __global__ void __launch_bounds__(JT) join_probe_kernel(JoinArgs A) {
                 }
                 esum += e[u];
             }
-            // one output range per workgroup step (one global atomic), each thread's rows at its
-            // scanned offset: consecutive lanes write consecutive rows
-            uint32_t total;
-            const uint32_t off = jblock_scan(esum, L.red, total);
+            // one output range per workgroup step (one global atomic).  Rows are placed u-major
+            // (all threads' row u = 0, then u = 1, ...), so the lanes of a store instruction write
+            // consecutive output rows; a step holding a row with > 127 outputs (duplicate-heavy
+            // keys) places them thread-major from a plain scan of the per-thread sums instead.
+            static_assert(JRPT == 4, "four 16-bit count fields");
+            uint64_t packed = 0;
+            bool big = false;
+#pragma unroll
+            for (int u = 0; u < JRPT; ++u) {
+                big |= e[u] > 127;
+                packed |= (uint64_t)(e[u] > 127 ? 0 : e[u]) << (16 * u);
+            }
+            uint64_t ptotal;
+            bool any_big;
+            const uint64_t poff = jblock_scan4(packed, big, L, ptotal, any_big);
+            uint32_t total = 0, toff = 0;
+            if (any_big) toff = jblock_scan(esum, L.red, total);
+            else
+#pragma unroll
+                for (int u = 0; u < JRPT; ++u) total += (uint32_t)(ptotal >> (16 * u)) & 0xFFFFu;
             uint64_t nx[JRPT][PRW];
             if (step + STEP < pe) load_step(step + STEP, nx);
             if (total) {
                 if (threadIdx.x == 0) L.base = atomicAdd(A.cursor, (unsigned long long)total);
                 __syncthreads();
-                uint64_t pos = L.base + off;
+                const uint64_t base = L.base;
+                uint64_t pos = base + toff; // thread-major cursor (any_big)
+                uint32_t ubase = 0;         // u-major: rows of the earlier u
 #pragma unroll
                 for (int u = 0; u < JRPT; ++u) {
                     const int64_t r = step + u * JT + threadIdx.x;
+                    if (!any_big) pos = base + ubase + ((poff >> (16 * u)) & 0xFFFFu);
+                    ubase += (uint32_t)(ptotal >> (16 * u)) & 0xFFFFu;
                     unsigned jb = head[u];
                     for (uint32_t q = 0; q < e[u]; ++q, ++pos) {
                         const bool pair = pairs && q < cnt[u];
