@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--codec-rows", type=int, default=20_000_000, help="packet codec leg rows (0 = skip)")
     ap.add_argument("--c4", type=int, default=-1, help="repartitioned join leg (configs[3]): 1 on, 0 off, -1 = on when N > 1")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                    help="weak: every rank holds --rows (and the other legs' sizes); strong: the sizes are job "
+                         "totals, split evenly over the ranks")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--value-int64", action="store_true", help="Int64 value column instead of Float64 (headline leg)")
     ap.add_argument("--bucket-bits", type=int, default=0, help="aggregation radix buckets (0 = from --groups)")
@@ -262,7 +265,7 @@ def c4_leg(args, ctx, dev, world, rank):
     import torch.distributed as dist
 
     import tiflash_amd as tfa
-    from tiflash_amd.exchange import exchange_partitions
+    from tiflash_amd.exchange import exchange_sides
     nb, npr = args.join_build, args.join_probe
     g = torch.Generator(device=dev)
     g.manual_seed(7 + 1000 * rank)
@@ -279,11 +282,10 @@ def c4_leg(args, ctx, dev, world, rank):
     state = {}
 
     def step():
-        if world > 1:
+        if world > 1:  # both sides repartitioned, then ONE fused exchange (one counts + one data all-to-all)
             bcols, boffs = tfa.hash_partition(ctx, [bk, bpay], [0], world)
-            lb = exchange_partitions(bcols, boffs)
             pcols, poffs = tfa.hash_partition(ctx, [pk, ppay], [0], world)
-            lp = exchange_partitions(pcols, poffs)
+            lb, lp = exchange_sides([(bcols, boffs), (pcols, poffs)])
         else:
             lb, lp = [bk, bpay], [pk, ppay]
         j = tfa.Join(ctx, tfa.INT64, expected_build_rows=lb[0].shape[0])
@@ -327,7 +329,7 @@ def c4_leg(args, ctx, dev, world, rank):
     return {"metric": "probe rows/s on the hash-repartitioned join (C3 per GPU: 10M build x 100M probe, "
                       "weak hash + fillSelector + RCCL all-to-all of both sides, local build + materialising probe)",
             "value": round(npr * world * args.steps / el, 1), "unit": "rows/s", "ms_per_step": round(ms, 3),
-            "scaling": "weak", "config": {"workload": "configs[3] repartitioned join", "build_rows_per_gpu": nb,
+            "scaling": args.scaling, "config": {"workload": "configs[3] repartitioned join", "build_rows_per_gpu": nb,
                                           "probe_rows_per_gpu": npr, "parallelism": f"dp{world}"},
             "check": {"probe_rows_total": probe_total, "expected_probe_rows": npr * world, "matches": matches,
                       "ok": probe_total == npr * world},
@@ -401,6 +403,7 @@ def c5_leg(args, ctx, dev, world, rank):
     out = {"metric": "rows/s on GROUP BY String key (k%08d) sum(Decimal64)->Decimal128 + count" +
                      (" two-phase + RCCL all-to-all" if world > 1 else ""),
            "value": round(n * world * args.steps / el, 1), "unit": "rows/s", "ms_per_step": round(ms, 3),
+           "scaling": args.scaling,
            "config": {"workload": "configs[4] String + Decimal GROUP BY", "rows_per_gpu": n, "groups": G},
            "check": {"count_total": cnt_total, "rows_total": n * world, "groups_total": groups_total,
                      "ok": cnt_total == n * world and groups_total <= G},
@@ -639,6 +642,11 @@ def main():
         else:
             dist.init_process_group(args.dist_backend)
 
+    if args.scaling == "strong" and world > 1:  # job totals -> per-rank shares
+        args.rows //= world
+        args.join_build //= world
+        args.join_probe //= world
+        args.c5_rows //= world
     N, G = args.rows, args.groups
     gen = torch.Generator(device=dev)
     gen.manual_seed(1 + rank)
@@ -688,11 +696,12 @@ def main():
     line = {
         "metric": "rows/sec on filter->hash-agg (TPC-H Q1 shape: 100M rows, 1M-key GROUP BY)",
         "value": round(value, 1), "unit": "rows/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None,
         "dtype": "int64/f64" if vtype == tfa.FLOAT64 else "int64",
         "data": "synthetic: f~U[0,100) (pred f<96), k~U[0,1e6), v dyadic f64; seed 1+rank",
         "config": {"workload": "configs[1] filter + GROUP BY 1M keys" + (" two-phase + RCCL all-to-all" if world > 1 else ""),
-                   "rows_per_gpu": N, "groups": G, "kept_rows_per_gpu": n_kept, "groups_out": groups,
+                   "rows_per_gpu": N, "total_rows": N * world, "groups": G, "kept_rows_per_gpu": n_kept,
+                   "groups_out": groups,
                    "parallelism": f"dp{world}", "dist_backend": args.dist_backend if world > 1 else None},
         "check": {"count_total": count_total, "kept_total": kept_total, "groups_total": groups_total,
                   "ok": count_total == kept_total and groups_total <= G},

@@ -9,8 +9,11 @@ Per rank, on the device through the C-ABI:
   C5  KeysAggregator over a nullable String key with sum(Decimal(15,2)) + count(*) -> weak hash
       of the partial rows' keys -> all-to-all of packed keys + states -> final KeysAggregator
       (two-phase, gtest_compute_server.cpp:738-812);
+  C5L the same with String keys past 15 bytes (the serialized method: keys travel as chars +
+      lengths in the fused exchange), and C5M with a (String, Int64) key pair;
   C2  Aggregator Int64 key, fused f < 96 filter, sum(Float64) + count -> hash_partition of the
       partial rows -> all-to-all -> consume_partial (bench.py's N>1 step).
+The join's build and probe sides travel in ONE fused exchange (exchange_sides).
 Results (and the rows each rank received) are written to <out>/rank<r>.npz; the test compares
 them with the oracle over the union of both ranks' inputs.
 
@@ -58,6 +61,19 @@ def agg_data(rank, n=60_000, groups=5_000):
     return chars, offs, nulls, v
 
 
+def long_agg_data(rank, n=40_000, groups=3_000):
+    """String keys of 1-40 bytes, most past the 15 bytes of the packed key, 2% NULL; an Int64
+    second key column (C5M) with 7 values."""
+    rng = np.random.default_rng(130 + rank)
+    ids = rng.integers(0, groups, n)
+    strs = [("customer#%012d/%s" % (i, "x" * (i % 17))) if i % 4 else ("s%d" % i) for i in ids]
+    chars, offs = string_column(strs)
+    nulls = (rng.random(n) < 0.02).astype(np.uint8)
+    k2 = (ids % 7 - 3).astype(np.int64)
+    v = rng.integers(-10**9, 10**9, n, dtype=np.int64)
+    return chars, offs, nulls, k2, v
+
+
 def c2_data(rank, n=300_000, groups=20_000):
     rng = np.random.default_rng(1 + rank)
     f = rng.integers(0, 100, n, dtype=np.int64)
@@ -74,7 +90,7 @@ def main():
     import torch.distributed as dist
 
     import tiflash_amd as tfa
-    from tiflash_amd.exchange import exchange_partitions, two_phase_merge_keys
+    from tiflash_amd.exchange import exchange_partitions, exchange_sides, two_phase_merge_keys
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
@@ -90,9 +106,8 @@ def main():
         bcols, boffs = tfa.hash_partition(ctx, [T(bk), T(bpay)], [0], world)
         res["send_build_keys"] = bcols[0].cpu().numpy()
         res["send_build_offs"] = np.array(boffs, dtype=np.int64)
-        lb = exchange_partitions(bcols, boffs)
         pcols, poffs = tfa.hash_partition(ctx, [T(pk), T(ppay)], [0], world)
-        lp = exchange_partitions(pcols, poffs)
+        lb, lp = exchange_sides([(bcols, boffs), (pcols, poffs)])
         res["recv_build_keys"] = lb[0].cpu().numpy()
         res["recv_probe_keys"] = lp[0].cpu().numpy()
         j = tfa.Join(ctx, tfa.INT64, expected_build_rows=int(lb[0].shape[0]))
@@ -118,6 +133,27 @@ def main():
         res["c5_cnt"] = r["states"][1].cpu().numpy()
         part.close()
         fin.close()
+
+        # ---- C5L / C5M: String keys past 15 bytes (serialized), and String + Int64 keys
+        chars, offs, nulls, k2, v = long_agg_data(rank)
+        for tag, types in (("c5l", [tfa.STRING]), ("c5m", [tfa.STRING, tfa.INT64])):
+            part = tfa.KeysAggregator(ctx, types, aggs, expected_groups=10_000)
+            fin = tfa.KeysAggregator(ctx, types, aggs, expected_groups=10_000)
+            keys = [(T(chars), T(offs.astype(np.int64)))] + ([T(k2)] if len(types) > 1 else [])
+            knull = [T(nulls)] + ([T(np.zeros(len(k2), np.uint8))] if len(types) > 1 else [])
+            part.consume(keys, [T(v), None], key_nullmaps=knull)
+            two_phase_merge_keys(ctx, part, fin)
+            r = fin.result()
+            (kc, ko) = r["keys"][0]
+            res[tag + "_chars"] = kc.cpu().numpy()
+            res[tag + "_offs"] = ko.cpu().numpy()
+            res[tag + "_key_null"] = r["key_null"][0].cpu().numpy()
+            if len(types) > 1:
+                res[tag + "_k2"] = r["keys"][1].cpu().numpy()
+            res[tag + "_sum"] = r["states"][0].cpu().numpy()
+            res[tag + "_cnt"] = r["states"][1].cpu().numpy()
+            part.close()
+            fin.close()
 
         # ---- C2: two-phase filter -> GROUP BY Int64 key
         f, k, vv = c2_data(rank)

@@ -10,6 +10,8 @@ Checked against the CPU oracle over the union of both ranks' inputs:
     join of the union (JoinRef, Join.cpp semantics), as multisets;
   * C5 — the final groups of all ranks (String key incl. NULL, exact Decimal sum, count) = the
     oracle's GROUP BY of the union, and no key is finalised on two ranks;
+  * C5L / C5M — the same with String keys past 15 bytes (serialized keys through the exchange)
+    and with a (String, Int64) key pair;
   * C2 — two-phase Int64-key GROUP BY with the fused filter = the oracle's.
 """
 import os
@@ -132,3 +134,33 @@ def test_two_phase_filter_groupby_matches_oracle(ranks, orc):
         got += list(zip(d["c2_keys"].tolist(), d["c2_sum"].tolist(), d["c2_cnt"].tolist()))
     assert len(set(k for k, _, _ in got)) == len(got), "a key was finalised on two ranks"
     assert sorted(got) == exp
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tag", ["c5l", "c5m"])
+def test_two_phase_long_string_keys_match_oracle(ranks, orc, tag):
+    types = [orc.STRING] + ([orc.INT64] if tag == "c5m" else [])
+    ref = orc.AggKeys(types, [(0, orc.prec(orc.DECIMAL64, 15)), (2, 0)])
+    for r in range(WORLD):
+        chars, offs, nulls, k2, v = W.long_agg_data(r)
+        keys = [(chars, offs)] + ([k2] if tag == "c5m" else [])
+        ref.consume(keys, [v, None], key_nulls=[nulls] + ([None] if tag == "c5m" else []))
+    exp = {}
+    for key, vals in ref.result():
+        exp[tuple(key)] = (vals[0], vals[1])
+    got = {}
+    long_keys = 0
+    for d in ranks:
+        chars, offs, knull = d[tag + "_chars"], d[tag + "_offs"], d[tag + "_key_null"]
+        s = 0
+        for i in range(len(offs)):
+            e = int(offs[i])
+            key = None if knull[i] else bytes(chars[s:e - 1])
+            long_keys += key is not None and len(key) > 15
+            s = e
+            lo, hi = int(d[tag + "_sum"][i][0]) & ((1 << 64) - 1), int(d[tag + "_sum"][i][1])
+            k = (key,) + ((int(d[tag + "_k2"][i]),) if tag == "c5m" else ())
+            assert k not in got, f"group {k!r} finalised on two ranks"
+            got[k] = (lo | (hi << 64), int(d[tag + "_cnt"][i]))
+    assert long_keys > 0
+    assert got == exp

@@ -270,3 +270,61 @@ def test_two_phase_string_aggregation_gloo():
     want = {k[0]: (s, c) for k, (s, c) in ref.result()}
     assert len(want) > 1000
     assert got == want
+
+
+def _sides_worker(rank, world, port, q):
+    """exchange_sides: three sides in one data all-to-all — (Int64, UInt8, 2-word) rows, Float64
+    rows, and a byte side (String chars) cut at per-partition byte offsets."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import sys
+    sys.path.insert(0, ROOT)
+    from tiflash_amd.exchange import exchange_sides
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        rng = np.random.default_rng(500 + rank)
+        sides, sent = [], []
+        for s, (n, mk) in enumerate(((3000, "a"), (1700, "b"), (9000, "c"))):
+            dest = np.sort(rng.integers(0, world, n))  # partition-major rows
+            if rank == 0 and s == 1:
+                dest[:] = 0  # a side that sends nothing to the other ranks
+            offs = [0] + [int(np.searchsorted(dest, p, side="right")) for p in range(world)]
+            if mk == "a":
+                cols = [rng.integers(-2**62, 2**62, n, dtype=np.int64), rng.integers(0, 255, n).astype(np.uint8),
+                        rng.integers(-2**62, 2**62, (n, 2), dtype=np.int64)]
+            elif mk == "b":
+                cols = [rng.random(n)]
+            else:
+                cols = [rng.integers(0, 255, n).astype(np.uint8)]
+            sides.append(([torch.from_numpy(c) for c in cols], offs))
+            sent.append((cols, offs))
+        got = exchange_sides(sides)
+        # what each rank should receive: its slice of every side from every rank, rank order
+        allsent = [None] * world
+        dist.all_gather_object(allsent, sent)
+        for s in range(3):
+            for j in range(len(sent[s][0])):
+                exp = np.concatenate([allsent[r][s][0][j][allsent[r][s][1][rank]:allsent[r][s][1][rank + 1]]
+                                      for r in range(world)])
+                g = got[s][j].numpy()
+                assert g.dtype == exp.dtype and g.shape == exp.shape, (s, j, g.shape, exp.shape)
+                assert np.array_equal(g, exp), (s, j)
+        q.put("ok")
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put(repr(e))
+        raise
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_fused_exchange_sides_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sides_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    assert res == ["ok"] * world, res

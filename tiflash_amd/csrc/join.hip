@@ -235,9 +235,7 @@ __global__ void __launch_bounds__(JT) join_probe_kernel(JoinArgs A) {
 #pragma unroll
             for (int u = 0; u < JRPT; ++u) {
                 const int64_t r = st + u * JT + threadIdx.x;
-                if (r < pe)
-#pragma unroll
-                    for (int w = 0; w < PRW; ++w) dst[u][w] = A.prec[r * prw + w];
+                if (r < pe) load_rec<PRW>(A.prec, (size_t)r, dst[u]);
             }
         };
         uint64_t rw[JRPT][PRW]; // the probe records (key + payload words)

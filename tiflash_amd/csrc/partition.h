@@ -981,6 +981,18 @@ int run_partition_tiled(Ctx *ctx, const Sel &sel, const RowPred &pred, TiledGeom
 constexpr uint32_t RS_C = 64;
 constexpr int RS_T = 512, RS_RPT = 4, RS_BR = RS_T * RS_RPT, RS_TPC = 64;
 
+template <int NW> __device__ __forceinline__ void load_rec(const uint64_t *rec, size_t pos, uint64_t (&v)[NW]) {
+    if constexpr (NW == 2) { // one 16-byte load
+        typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+        const u64x2 q = reinterpret_cast<const u64x2 *>(rec)[pos];
+        v[0] = q.x;
+        v[1] = q.y;
+    } else {
+#pragma unroll
+        for (int w = 0; w < NW; ++w) v[w] = rec[pos * NW + w];
+    }
+}
+
 template <int NW>
 __global__ void __launch_bounds__(RS_T) regroup_scatter_kernel(const uint64_t *rec, const uint32_t *tile_hist, int T,
                                                                int TRS, int fine_bits, uint32_t shift,
@@ -1011,39 +1023,48 @@ __global__ void __launch_bounds__(RS_T) regroup_scatter_kernel(const uint64_t *r
         tstart[lane] = st;
         tpre[lane + 1] = x;
         if (lane == 0) tpre[0] = 0;
+        hist[lane] = 0;
     }
     __syncthreads();
     const uint32_t R = tpre[nt];
-    for (uint32_t b0 = 0; b0 < R; b0 += RS_BR) {
-        if (threadIdx.x < 64) hist[threadIdx.x] = 0;
-        __syncthreads();
-        uint64_t v[NW][RS_RPT];
-        uint32_t fq[RS_RPT];
+    // a batch's records: row i of the group's concatenated runs -> its run (binary search over
+    // the scanned run lengths) -> its record in the tile slot
+    auto load_batch = [&](uint32_t b0, uint64_t (&v)[RS_RPT][NW], bool (&val)[RS_RPT]) __attribute__((always_inline)) {
 #pragma unroll
         for (int u = 0; u < RS_RPT; ++u) {
             const uint32_t i = b0 + (uint32_t)u * RS_T + threadIdx.x;
-            fq[u] = 0xFFFFFFFFu;
-            if (i >= R) continue;
-            int lo = 0, hi = nt; // the run holding row i: tpre[lo] <= i < tpre[lo + 1]
+            val[u] = i < R;
+            if (!val[u]) continue;
+            int lo = 0, hi = nt; // tpre[lo] <= i < tpre[lo + 1]
             while (hi - lo > 1) {
                 const int mid = (lo + hi) >> 1;
                 if (tpre[mid] <= i) lo = mid;
                 else hi = mid;
             }
-            const size_t pos = (size_t)(t0 + lo) * (uint32_t)TRS + tstart[lo] + (i - tpre[lo]);
-#pragma unroll
-            for (int w = 0; w < NW; ++w) v[w][u] = rec[pos * NW + w];
-            fq[u] = 0;
+            load_rec<NW>(rec, (size_t)(t0 + lo) * (uint32_t)TRS + tstart[lo] + (i - tpre[lo]), v[u]);
         }
+    };
+    uint64_t v[RS_RPT][NW];
+    bool val[RS_RPT];
+    if (R) load_batch(0, v, val);
+    // software pipelined: the next batch's loads are issued before this batch's global cursor
+    // atomics, barriers and stores, so their latency overlaps them
+    for (uint32_t b0 = 0; b0 < R; b0 += RS_BR) {
+        uint32_t fq[RS_RPT];
 #pragma unroll
         for (int u = 0; u < RS_RPT; ++u) {
-            if (fq[u]) continue;
-            const uint32_t f = fib_part(v[0][u], shift) & fmask;
+            fq[u] = 0xFFFFFFFFu;
+            if (!val[u]) continue;
+            const uint32_t f = fib_part(v[u][0], shift) & fmask;
             fq[u] = f | (atomicAdd(&hist[f], 1u) << 16);
         }
+        uint64_t nv[RS_RPT][NW];
+        bool nval[RS_RPT] = {};
+        if (b0 + RS_BR < R) load_batch(b0 + RS_BR, nv, nval);
         __syncthreads();
         if (threadIdx.x < 64) {
             const uint32_t h = hist[lane];
+            hist[lane] = 0; // for the next batch (its atomics come after two more barriers)
             uint32_t x = h;
 #pragma unroll
             for (int d = 1; d < 64; d <<= 1) {
@@ -1059,7 +1080,7 @@ __global__ void __launch_bounds__(RS_T) regroup_scatter_kernel(const uint64_t *r
             if (fq[u] == 0xFFFFFFFFu) continue;
             const uint32_t f = fq[u] & 0xFFFFu, s = hstart[f] + (fq[u] >> 16);
 #pragma unroll
-            for (int w = 0; w < NW; ++w) stage[w][s] = v[w][u];
+            for (int w = 0; w < NW; ++w) stage[w][s] = v[u][w];
             sf[s] = (uint8_t)f;
         }
         __syncthreads();
@@ -1067,10 +1088,24 @@ __global__ void __launch_bounds__(RS_T) regroup_scatter_kernel(const uint64_t *r
         for (uint32_t s = threadIdx.x; s < kept; s += RS_T) {
             const uint32_t f = sf[s];
             const uint64_t gp = gbase[f] + (s - hstart[f]);
+            if constexpr (NW == 2) {
+                typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+                u64x2 q;
+                q.x = stage[0][s];
+                q.y = stage[1][s];
+                reinterpret_cast<u64x2 *>(out)[gp] = q;
+            } else {
 #pragma unroll
-            for (int w = 0; w < NW; ++w) out[gp * NW + w] = stage[w][s];
+                for (int w = 0; w < NW; ++w) out[gp * NW + w] = stage[w][s];
+            }
         }
         __syncthreads();
+#pragma unroll
+        for (int u = 0; u < RS_RPT; ++u) {
+            val[u] = nval[u];
+#pragma unroll
+            for (int w = 0; w < NW; ++w) v[u][w] = nv[u][w];
+        }
     }
 }
 

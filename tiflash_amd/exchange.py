@@ -5,53 +5,140 @@ over xGMI on MI355X; "gloo" on CPU for the multi-process tests).
 
 The sender side is tfg_hash_partition (weak hash -> fillSelector -> stable scatter): its output is
 partition-major, partition p = rows [offsets[p], offsets[p+1]), which is exactly an all-to-all
-send buffer, so an exchange is one counts all-to-all plus one all_to_all_single per column.
+send buffer.  An exchange is fused, whatever the number of columns and of row sets ("sides",
+e.g. a join's build and probe sides, or a String column's chars next to its rows):
+
+* every side's columns are packed side by side into one row record (the reference's packet
+  carries a whole Block too, newMPPExchangeWriter.cpp:64-95);
+* ONE counts all-to-all ([world, sides] row counts) and one host read of it, which sizes the
+  receive buffer (RCCL's send / recv take host sizes);
+* ONE all_to_all_single of a peer-major byte buffer holding, for each peer, its rows of every
+  side in turn.
+
+xGMI is point-to-point, so fewer, larger transfers per peer pair are what the links want.
 """
-from typing import List, Sequence
+from typing import List, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
 
 
-def exchange_partitions(cols: Sequence[torch.Tensor], offsets: Sequence[int], group=None) -> List[torch.Tensor]:
-    """Sends rows [offsets[p], offsets[p+1]) of every column to rank p; returns the received
-    columns, rows from rank 0 first (ExchangeReceiver's concatenation order is unspecified in
-    the reference; consumers must not depend on it)."""
+def _row_bytes(c: torch.Tensor, n: int) -> torch.Tensor:
+    """The first n rows of a column as an [n, row_bytes] uint8 view (copy only if strided)."""
+    c = c[:n]
+    if not c.is_contiguous():
+        c = c.contiguous()
+    return c.view(torch.uint8).reshape(n, -1)
+
+
+def exchange_sides(sides: Sequence[Tuple[Sequence[torch.Tensor], Sequence[int]]], group=None) -> List[List[torch.Tensor]]:
+    """sides: [(columns, offsets)], each side's rows partition-major (rows [offsets[p],
+    offsets[p+1]) go to rank p; offsets are host ints).  Returns, per side, the received columns
+    (rows from rank 0 first; ExchangeReceiver's concatenation order is unspecified in the
+    reference and consumers must not depend on it)."""
     world = dist.get_world_size(group)
-    if len(offsets) != world + 1:
-        raise ValueError(f"need {world + 1} partition offsets, got {len(offsets)}")
-    dev = cols[0].device
+    for _, offs in sides:
+        if len(offs) != world + 1:
+            raise ValueError(f"need {world + 1} partition offsets, got {len(offs)}")
+    dev = sides[0][0][0].device
     if dev.type != "cpu" and dist.get_backend(group) == "gloo":
         # gloo moves host memory only: stage through the host (rehearsal of the N>1 path on one
         # GPU; the production backend is "nccl" = RCCL, which exchanges device buffers directly)
-        outs = exchange_partitions([c.cpu() for c in cols], offsets, group)
-        return [o.to(dev) for o in outs]
-    send_counts = [int(offsets[p + 1] - offsets[p]) for p in range(world)]
-    send = torch.tensor(send_counts, dtype=torch.int64, device=dev)
-    recv = torch.empty_like(send)
-    dist.all_to_all_single(recv, send, group=group)
-    recv_counts = recv.tolist()
+        outs = exchange_sides([([c.cpu() for c in cols], offs) for cols, offs in sides], group)
+        return [[o.to(dev) for o in side] for side in outs]
+    S = len(sides)
+    recs, specs, rowb = [], [], []
+    for cols, offs in sides:
+        n = int(offs[world])
+        parts = [_row_bytes(c, n) for c in cols]
+        specs.append([(p.shape[1], c.dtype, tuple(c.shape[1:])) for p, c in zip(parts, cols)])
+        recs.append(torch.cat(parts, 1) if len(parts) > 1 else parts[0])
+        rowb.append(recs[-1].shape[1])
+    send_counts = [[int(offs[p + 1] - offs[p]) for _, offs in sides] for p in range(world)]
+    cnt = torch.tensor(send_counts, dtype=torch.int64, device=dev).reshape(-1)
+    rcnt = torch.empty_like(cnt)
+    dist.all_to_all_single(rcnt, cnt, group=group)
+    recv_counts = rcnt.reshape(world, S).tolist()
+    send_bytes = [sum(send_counts[p][s] * rowb[s] for s in range(S)) for p in range(world)]
+    recv_bytes = [sum(recv_counts[p][s] * rowb[s] for s in range(S)) for p in range(world)]
+    if S == 1:
+        send = recs[0].reshape(-1)  # already peer-major
+    else:
+        pieces = [recs[s][int(sides[s][1][p]):int(sides[s][1][p + 1])].reshape(-1) for p in range(world) for s in range(S)]
+        send = torch.cat(pieces)
+    recv = torch.empty(max(sum(recv_bytes), 1), dtype=torch.uint8, device=dev)[:sum(recv_bytes)]
+    dist.all_to_all_single(recv, send, recv_bytes, send_bytes, group=group)
+    slices = [[] for _ in range(S)]
+    pos = 0
+    for p in range(world):
+        for s in range(S):
+            nb = recv_counts[p][s] * rowb[s]
+            slices[s].append(recv[pos:pos + nb].reshape(-1, rowb[s]))
+            pos += nb
     outs = []
-    for c in cols:
-        c = c[: int(offsets[world])]
-        o = torch.empty((sum(recv_counts),) + tuple(c.shape[1:]), dtype=c.dtype, device=dev)
-        dist.all_to_all_single(o, c.contiguous(), recv_counts, send_counts, group=group)
-        outs.append(o)
+    for s in range(S):
+        if S == 1:
+            rec = recv.reshape(-1, rowb[s])  # rows of every peer, already contiguous
+        else:
+            rec = torch.cat(slices[s]) if len(slices[s]) > 1 else slices[s][0]
+        cols, a = [], 0
+        for w, dt, shp in specs[s]:
+            piece = rec[:, a:a + w] if len(specs[s]) > 1 else rec
+            cols.append(piece.contiguous().view(dt).reshape((-1,) + shp))
+            a += w
+        outs.append(cols)
     return outs
+
+
+def exchange_partitions(cols: Sequence[torch.Tensor], offsets: Sequence[int], group=None) -> List[torch.Tensor]:
+    """One side: sends rows [offsets[p], offsets[p+1]) of every column to rank p in one fused
+    exchange; returns the received columns."""
+    return exchange_sides([(cols, offsets)], group)[0]
+
+
+def exchange_string_rows(ctx, perm, offs, row_cols, strings, group=None):
+    """Rows with String columns: the fixed-width row columns plus each String's row lengths
+    travel as one side, every String's chars as a side of 1-byte rows cut at the partitions'
+    byte boundaries — all in the same single data all-to-all.  perm / offs: the stable partition
+    (tfa.partition).  strings: [(chars, end offsets)].  Returns (row columns, [(chars, end
+    offsets)]) of the received rows."""
+    import tiflash_amd as tfa
+    world = len(offs) - 1
+    rows = tfa.gather(ctx, perm, list(row_cols)) if row_cols else []
+    lens, chars_sides = [], []
+    for chars, ends in strings:
+        gc, ge = tfa.gather_string(ctx, perm, chars, ends)
+        starts = torch.cat([ge.new_zeros(1), ge[:-1]]) if ge.numel() else ge
+        lens.append(ge - starts)
+        # byte offset of each partition boundary (one small host read)
+        idx = torch.tensor([int(o) - 1 for o in offs[1:]], dtype=torch.int64, device=ge.device)
+        ends_at = torch.where(idx >= 0, ge[idx.clamp(min=0)] if ge.numel() else idx * 0, idx * 0)
+        boff = [0] + [int(x) for x in ends_at.tolist()]
+        chars_sides.append(([gc], boff))
+    got = exchange_sides([(rows + lens, offs)] + chars_sides, group)
+    rcols = got[0][:len(rows)]
+    rlens = got[0][len(rows):]
+    out_strings = []
+    for ln, side in zip(rlens, got[1:]):
+        out_strings.append((side[0], torch.cumsum(ln, 0)))
+    return rcols, out_strings
 
 
 def two_phase_merge_keys(ctx, partial, final, group=None, collators=None):
     """ExchangeSender -> ExchangeReceiver of a two-phase GROUP BY over String / several keys
     (C5): the partial aggregation's rows are routed by the reference's hash of the key columns
-    (IColumn::updateWeakHash32 -> fillSelector, HashBaseWriterHelper.cpp:46-84), travel as packed
-    16-byte keys plus states, and the final aggregation merges them (mergeOnBlock).  `partial` and
-    `final` are tiflash_amd.KeysAggregator objects of the same signature."""
+    (IColumn::updateWeakHash32 -> fillSelector, HashBaseWriterHelper.cpp:46-84) and the final
+    aggregation merges them (mergeOnBlock).  Keys travel packed (16 bytes) while the partial
+    aggregator holds them packed; once it has moved to the serialized method (a String sort key
+    over 15 bytes, String + fixed keys, wide tuples) they travel as their key columns — Strings
+    as chars + lengths — with the states, still in one data all-to-all.  `partial` and `final`
+    are tiflash_amd.KeysAggregator objects of the same signature."""
     import tiflash_amd as tfa
     world = dist.get_world_size(group)
-    packed = partial.result_packed()
     cols = partial.result()
-    n = packed["keys"].shape[0]
-    h = torch.empty(n, dtype=torch.int32, device=packed["keys"].device)
+    n = partial.size()
+    dev = cols["key_null"][0].device
+    h = torch.empty(n, dtype=torch.int32, device=dev)
     tfa.check(tfa.lib().tfg_weak_hash_init(ctx.h, tfa._p(h), tfa.ctypes.c_int64(n)))
     for j, (t, k, kn) in enumerate(zip(partial.key_types, cols["keys"], cols["key_null"])):
         if t == tfa.STRING:
@@ -60,6 +147,30 @@ def two_phase_merge_keys(ctx, partial, final, group=None, collators=None):
             tfa.weak_hash(ctx, [k], types=[t], nullmaps=[kn], h=h)
     sel = tfa.fill_selector(ctx, h, world)
     perm, offs = tfa.partition(ctx, sel, world)
-    send = tfa.gather(ctx, perm, [packed["keys"]] + list(packed["states"]))
-    recv = exchange_partitions(send, offs, group)
-    final.consume_partial_packed(recv[0], recv[1:])
+    try:
+        packed = partial.result_packed()
+    except tfa.TfgError as e:
+        if e.code != -4:  # NOT_IMPLEMENTED: the serialized method has no packed form
+            raise
+        packed = None
+    if packed is not None:
+        send = tfa.gather(ctx, perm, [packed["keys"]] + list(packed["states"]))
+        recv = exchange_partitions(send, offs, group)
+        final.consume_partial_packed(recv[0], recv[1:])
+        return
+    fixed = [k for t, k in zip(partial.key_types, cols["keys"]) if t != tfa.STRING]
+    strings = [k for t, k in zip(partial.key_types, cols["keys"]) if t == tfa.STRING]
+    row_cols = fixed + list(cols["key_null"]) + list(cols["states"]) + list(cols["state_null"])
+    rcols, rstr = exchange_string_rows(ctx, perm, offs, row_cols, strings, group)
+    nk, nkeys, ns = len(fixed), len(partial.key_types), len(cols["states"])
+    rfixed, rknull = rcols[:nk], rcols[nk:nk + nkeys]
+    rstates, rsnull = rcols[nk + nkeys:nk + nkeys + ns], rcols[nk + nkeys + ns:]
+    keys, fi, si = [], 0, 0
+    for t in partial.key_types:
+        if t == tfa.STRING:
+            keys.append(rstr[si])
+            si += 1
+        else:
+            keys.append(rfixed[fi])
+            fi += 1
+    final.consume_partial(keys, rstates, key_nullmaps=rknull, state_nullmaps=rsnull)
