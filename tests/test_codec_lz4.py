@@ -34,6 +34,7 @@ HAND = [
     (b"\xf0\xff\x03" + bytes(range(256)) + bytes(17), bytes(range(256)) + bytes(17)),  # 15+255+3 literals
     (b"\x00", b""),                                                 # empty block
     (b"\x2fxy\x02\x00\xff\x00\x50abcde", b"xy" * 138 + b"abcde"),  # ml 15+255+0+4 = 274
+    (b"\x80abcdefgh\x08\x00\x10z", b"abcdefghabcd" + b"z"),      # offset 8 >= ml 4: no overlap
 ]
 MALFORMED = [
     b"",                          # no token
@@ -122,6 +123,16 @@ def test_gpu_decompress_rejects_bad_frames(tfa, ctx, dev):
             tfa.codec_decompress(ctx, dev_bytes(bad, dev))
     with pytest.raises(tfa.TfgError):  # a NONE packet is not an LZ4 packet
         tfa.codec_decompress(ctx, dev_bytes(b"\x02hello", dev))
+
+
+@pytest.mark.gpu
+def test_gpu_decompress_rejects_forged_raw_sizes(tfa, ctx, dev):
+    # frames of a few bytes that each claim ~4 GiB of raw output: rejected from the headers alone
+    # (more than LZ4 can expand a block to, and past DBMS_MAX_COMPRESSED_SIZE), before any output
+    # is sized
+    for raw in (0xFFFFFFFF, 0x40000001, 5 * 255 + 17):
+        with pytest.raises(tfa.TfgError):
+            tfa.codec_decompress(ctx, dev_bytes(frame(b"\x50hello", raw) * 64, dev))
 
 
 @pytest.mark.gpu

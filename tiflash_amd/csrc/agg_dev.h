@@ -671,6 +671,41 @@ template <int NA, bool W = false> struct GenericOps {
     __device__ __forceinline__ void store(const RowsIO &sp, int64_t w, const Row &v) const { store_row<NA, W>(S, sp, mode, w, v); }
 };
 
+// The value ops of FastOps / WideFastOps for R rows of one step (op codes below).  CHECK: cells
+// < 0 are skipped (add_multi); otherwise every cell is valid (add_all: rows without a cell of
+// their own add into a dummy cell that is never flushed, so no per-row branch).  A Decimal64 ->
+// Int128 sum issues every row's returning low-word add before any high-word add, so the carries'
+// LDS round trips overlap.
+template <int A0, int A1, int A2, bool CHECK, int R, typename Row>
+__device__ __forceinline__ void fast_add_rows(Table &T, const int (&cell)[R], const Row (&v)[R]) {
+    constexpr int ops[3] = {A0, A1, A2};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        if (ops[i] != 4) continue;
+        uint64_t old[R];
+#pragma unroll
+        for (int u = 0; u < R; ++u)
+            if (!CHECK || cell[u] >= 0) old[u] = atomicAdd((unsigned long long *)T.acc_cell(i, cell[u]), (unsigned long long)v[u].v[i]);
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            if (CHECK && cell[u] < 0) continue;
+            const uint64_t lo = v[u].v[i], carry = (old[u] + lo) < old[u] ? 1ull : 0ull;
+            atomicAdd((unsigned long long *)T.acc_cell(i, cell[u]) + 1,
+                      (unsigned long long)(((int64_t)lo < 0 ? ~0ull : 0ull) + carry));
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+        if (CHECK && cell[u] < 0) continue;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            if (ops[i] == 1) atomicAdd((unsigned long long *)T.cnt_cell(i, cell[u]), 1ull);
+            if (ops[i] == 2) atomicAdd((unsigned long long *)T.acc_cell(i, cell[u]), (unsigned long long)v[u].v[i]);
+            if (ops[i] == 3) atomicAdd((double *)T.acc_cell(i, cell[u]), __longlong_as_double((long long)v[u].v[i]));
+        }
+    }
+}
+
 template <int A0, int A1, int A2> struct FastOps {
     // rows are staged as interleaved records: key, then one word per summed argument
     static constexpr int op(int i) { return i == 0 ? A0 : (i == 1 ? A1 : A2); }
@@ -713,70 +748,17 @@ template <int A0, int A1, int A2> struct FastOps {
     __device__ __forceinline__ bool knull(const Row &) const { return false; }
     __device__ __forceinline__ uint64_t hi(const Row &) const { return 0; }
     __device__ __forceinline__ void add(Table &T, int cell, const Row &v) const {
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            if (op(i) == 1) atomicAdd((unsigned long long *)T.cnt_cell(i, cell), 1ull);
-            if (op(i) == 2) atomicAdd((unsigned long long *)T.acc_cell(i, cell), (unsigned long long)v.v[i]);
-            if (op(i) == 3) atomicAdd((double *)T.acc_cell(i, cell), __longlong_as_double((long long)v.v[i]));
-            if (op(i) == 4) lds_add_i128(T.acc_cell(i, cell), v.v[i], (int64_t)v.v[i] < 0 ? ~0ull : 0ull);
-        }
+        const int c1[1] = {cell};
+        const Row v1[1] = {v};
+        fast_add_rows<A0, A1, A2, false>(T, c1, v1);
     }
-    // the step's rows at once (cell < 0: skip): a Decimal64 -> Int128 sum issues every row's
-    // returning low-word add before any high-word add, so the carries' LDS round trips overlap
     template <int R>
     __device__ __forceinline__ void add_multi(Table &T, const int (&cell)[R], const Row (&v)[R]) const {
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            if (op(i) != 4) continue;
-            uint64_t old[R];
-#pragma unroll
-            for (int u = 0; u < R; ++u)
-                if (cell[u] >= 0) old[u] = atomicAdd((unsigned long long *)T.acc_cell(i, cell[u]), (unsigned long long)v[u].v[i]);
-#pragma unroll
-            for (int u = 0; u < R; ++u) {
-                if (cell[u] < 0) continue;
-                const uint64_t lo = v[u].v[i], carry = (old[u] + lo) < old[u] ? 1ull : 0ull;
-                atomicAdd((unsigned long long *)T.acc_cell(i, cell[u]) + 1,
-                          (unsigned long long)(((int64_t)lo < 0 ? ~0ull : 0ull) + carry));
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < R; ++u) {
-            if (cell[u] < 0) continue;
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                if (op(i) == 1) atomicAdd((unsigned long long *)T.cnt_cell(i, cell[u]), 1ull);
-                if (op(i) == 2) atomicAdd((unsigned long long *)T.acc_cell(i, cell[u]), (unsigned long long)v[u].v[i]);
-                if (op(i) == 3) atomicAdd((double *)T.acc_cell(i, cell[u]), __longlong_as_double((long long)v[u].v[i]));
-            }
-        }
+        fast_add_rows<A0, A1, A2, true>(T, cell, v);
     }
-    // the step's rows at once, every cell valid (rows without a cell of their own add into a
-    // dummy cell that is never flushed): no per-row branch
     template <int R>
     __device__ __forceinline__ void add_all(Table &T, const int (&cell)[R], const Row (&v)[R]) const {
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            if (op(i) != 4) continue;
-            uint64_t old[R];
-#pragma unroll
-            for (int u = 0; u < R; ++u) old[u] = atomicAdd((unsigned long long *)T.acc_cell(i, cell[u]), (unsigned long long)v[u].v[i]);
-#pragma unroll
-            for (int u = 0; u < R; ++u) {
-                const uint64_t lo = v[u].v[i], carry = (old[u] + lo) < old[u] ? 1ull : 0ull;
-                atomicAdd((unsigned long long *)T.acc_cell(i, cell[u]) + 1,
-                          (unsigned long long)(((int64_t)lo < 0 ? ~0ull : 0ull) + carry));
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < R; ++u) {
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                if (op(i) == 1) atomicAdd((unsigned long long *)T.cnt_cell(i, cell[u]), 1ull);
-                if (op(i) == 2) atomicAdd((unsigned long long *)T.acc_cell(i, cell[u]), (unsigned long long)v[u].v[i]);
-                if (op(i) == 3) atomicAdd((double *)T.acc_cell(i, cell[u]), __longlong_as_double((long long)v[u].v[i]));
-            }
-        }
+        fast_add_rows<A0, A1, A2, false>(T, cell, v);
     }
     __device__ __forceinline__ void store(const RowsIO &sp, int64_t w, const Row &v) const {
         uint64_t *rec = (uint64_t *)sp.key + w * NCOL;
@@ -844,43 +826,13 @@ template <int A0, int A1, int A2> struct WideFastOps {
     __device__ __forceinline__ uint64_t hi(const Row &v) const { return v.khi; }
     __device__ __forceinline__ bool knull(const Row &) const { return false; }
     __device__ __forceinline__ void add(Table &T, int cell, const Row &v) const {
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            if (op(i) == 1) atomicAdd((unsigned long long *)T.cnt_cell(i, cell), 1ull);
-            if (op(i) == 2) atomicAdd((unsigned long long *)T.acc_cell(i, cell), (unsigned long long)v.v[i]);
-            if (op(i) == 3) atomicAdd((double *)T.acc_cell(i, cell), __longlong_as_double((long long)v.v[i]));
-            if (op(i) == 4) lds_add_i128(T.acc_cell(i, cell), v.v[i], (int64_t)v.v[i] < 0 ? ~0ull : 0ull);
-        }
+        const int c1[1] = {cell};
+        const Row v1[1] = {v};
+        fast_add_rows<A0, A1, A2, false>(T, c1, v1);
     }
-    // the step's rows at once (cell < 0: skip): a Decimal64 -> Int128 sum issues every row's
-    // returning low-word add before any high-word add, so the carries' LDS round trips overlap
     template <int R>
     __device__ __forceinline__ void add_multi(Table &T, const int (&cell)[R], const Row (&v)[R]) const {
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            if (op(i) != 4) continue;
-            uint64_t old[R];
-#pragma unroll
-            for (int u = 0; u < R; ++u)
-                if (cell[u] >= 0) old[u] = atomicAdd((unsigned long long *)T.acc_cell(i, cell[u]), (unsigned long long)v[u].v[i]);
-#pragma unroll
-            for (int u = 0; u < R; ++u) {
-                if (cell[u] < 0) continue;
-                const uint64_t lo = v[u].v[i], carry = (old[u] + lo) < old[u] ? 1ull : 0ull;
-                atomicAdd((unsigned long long *)T.acc_cell(i, cell[u]) + 1,
-                          (unsigned long long)(((int64_t)lo < 0 ? ~0ull : 0ull) + carry));
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < R; ++u) {
-            if (cell[u] < 0) continue;
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                if (op(i) == 1) atomicAdd((unsigned long long *)T.cnt_cell(i, cell[u]), 1ull);
-                if (op(i) == 2) atomicAdd((unsigned long long *)T.acc_cell(i, cell[u]), (unsigned long long)v[u].v[i]);
-                if (op(i) == 3) atomicAdd((double *)T.acc_cell(i, cell[u]), __longlong_as_double((long long)v[u].v[i]));
-            }
-        }
+        fast_add_rows<A0, A1, A2, true>(T, cell, v);
     }
     __device__ __forceinline__ void store(const RowsIO &sp, int64_t w, const Row &v) const {
         uint64_t *rec = (uint64_t *)sp.key + w * NCOL;

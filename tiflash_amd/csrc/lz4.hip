@@ -33,6 +33,7 @@ namespace {
 constexpr uint8_t LZ4_METHOD = 0x82;       // CompressionMethodByte::LZ4
 constexpr uint8_t NONE_METHOD = 0x02;      // CompressionMethodByte::NONE
 constexpr int FRAME_HDR = 9;               // COMPRESSED_BLOCK_HEADER_SIZE
+constexpr uint64_t MAX_FRAME_RAW = 0x40000000ull; // DBMS_MAX_COMPRESSED_SIZE
 constexpr uint32_t ENC_FRAME = 64 * 1024;  // raw bytes per frame this encoder writes
 constexpr int HASH_LOG = 12;
 constexpr uint64_t ENC_SLOT = FRAME_HDR + ENC_FRAME + ENC_FRAME / 255 + 16; // header + LZ4_COMPRESSBOUND
@@ -195,7 +196,11 @@ __global__ void lz4_frames_kernel(const uint8_t *pkt, uint64_t bytes, uint64_t *
             fb |= (uint32_t)pkt[pos + 1 + b] << (8 * b);
             rb |= (uint32_t)pkt[pos + 5 + b] << (8 * b);
         }
-        if (fb <= FRAME_HDR || pos + fb > bytes) {
+        // a frame may not claim more raw bytes than LZ4 can expand its block to (one token byte
+        // yields at most 255 + 16 raw bytes), nor more than DBMS_MAX_COMPRESSED_SIZE
+        // (IO/Compression/CompressionInfo.h:21), so a forged header cannot size the output
+        if (fb <= FRAME_HDR || pos + fb > bytes || rb > MAX_FRAME_RAW ||
+            (uint64_t)rb > (uint64_t)(fb - FRAME_HDR) * 255 + 16) {
             bad = 1;
             break;
         }
@@ -274,7 +279,12 @@ __global__ void __launch_bounds__(64) lz4_decode_kernel(const uint8_t *pkt, cons
         // every lane's earlier stores have completed before any lane reads them back
         __builtin_amdgcn_s_waitcnt(0);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        for (uint64_t i = lane; i < ml; i += 64) o[op + i] = ov[op - off + (i % off)];
+        if (off >= ml) { // no overlap: a straight copy of bytes written before this match
+            for (uint64_t i = lane; i < ml; i += 64) o[op + i] = ov[op - off + i];
+        } else { // overlapping: the off-byte pattern repeats (frame raw sizes fit 32 bits)
+            const uint32_t ml32 = (uint32_t)ml;
+            for (uint32_t i = lane; i < ml32; i += 64) o[op + i] = ov[op - off + (i % off)];
+        }
         op += ml;
     }
     if (lane == 0 && (bad || op != raw)) atomicOr(err, 1u);

@@ -52,7 +52,7 @@ struct SerialDict {
     // per-row buffers
     uint32_t *rows = nullptr; // slot[n] | listA[n] | listB[n]
     uint64_t rows_cap = 0;
-    uint64_t *dcnt = nullptr; // [0] groups, [1] arena bytes, [2] retries
+    uint64_t *dcnt = nullptr; // [0] groups, [1] arena bytes, [2] retries, [3] table-full flag
 };
 
 __device__ __forceinline__ uint64_t ser_mix(uint64_t h, uint64_t w) {
@@ -183,7 +183,8 @@ __device__ bool ser_equal(const SerCols &k, int64_t r, const uint8_t *b, uint32_
 }
 
 __global__ void ser_insert_kernel(SerCols k, int64_t m, const uint32_t *list, const uint8_t *mask, uint64_t seed,
-                                  uint64_t *fp, const uint32_t *gid, uint32_t *owner, uint64_t cmask, uint32_t *slot) {
+                                  uint64_t *fp, const uint32_t *gid, uint32_t *owner, uint64_t cmask, uint32_t *slot,
+                                  uint64_t *cnt) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = list ? list[i] : i;
         if (mask && !mask[r]) {
@@ -192,13 +193,20 @@ __global__ void ser_insert_kernel(SerCols k, int64_t m, const uint32_t *list, co
         }
         const uint64_t h = ser_hash(k, r, seed);
         uint64_t s = h & cmask;
-        for (;;) {
+        // bounded probe: the host sizes the table for every claim of this round at fill <= 1/2,
+        // so a full sweep never happens; if it did, the row lands on a claimed slot (the verify
+        // then fails it) and cnt[3] makes the host report the table as full
+        for (uint64_t step = 0;; ++step) {
             uint64_t cur = fp[s];
             if (cur == 0) {
                 cur = atomicCAS((unsigned long long *)&fp[s], 0ull, (unsigned long long)h);
                 if (cur == 0) cur = h;
             }
             if (cur == h) break;
+            if (step == cmask) {
+                atomicOr((unsigned long long *)&cnt[3], 1ull);
+                break;
+            }
             s = (s + 1) & cmask;
         }
         slot[r] = (uint32_t)s;
@@ -490,23 +498,31 @@ int serial_dict_assign(SerialDict *d, const void *const *key_cols, const uint64_
     uint32_t *slot = d->rows, *lists[2] = {d->rows + d->rows_cap, d->rows + 2 * d->rows_cap};
     const uint32_t *list = nullptr;
     int64_t m = n;
+    uint64_t claimed = d->G + (uint64_t)n; // fingerprint slots this consume may claim
     ProfScope _ps(ctx, "agg.serial_dict");
     for (int round = 0;; ++round) {
         TFG_CHECK(round < 16, TFG_ERR_LOGICAL, "serialized keys: fingerprint collisions persist after 16 seeds");
         const uint8_t *mk = round == 0 ? mask : nullptr; // retries hold unmasked rows only
         uint32_t *retry = lists[round & 1];
+        // a retry round claims up to m slots for fingerprints at the new seed: keep the table at
+        // fill <= 1/2 for them (round 0 was sized above for G + n)
+        if (round > 0) {
+            claimed += (uint64_t)m;
+            if (int rc = ser_grow_table(d, claimed)) return rc;
+        }
         const unsigned grid = stream_grid(m, 256);
         TFG_HIP(hipMemsetAsync(d->dcnt + 2, 0, 8, ctx->stream));
         hipLaunchKernelGGL(ser_insert_kernel, dim3(grid), dim3(256), 0, ctx->stream, k, m, list, mk, (uint64_t)round,
-                           d->fp, d->gid, d->owner, d->cap - 1, slot);
+                           d->fp, d->gid, d->owner, d->cap - 1, slot, d->dcnt);
         hipLaunchKernelGGL(ser_assign_kernel, dim3(grid), dim3(256), 0, ctx->stream, k, m, list, mk, slot, d->gid,
                            d->owner, d->dcnt, d->arena, d->goff, d->glen);
         hipLaunchKernelGGL(ser_verify_kernel, dim3(grid), dim3(256), 0, ctx->stream, k, m, list, mk, slot, d->gid,
                            d->arena, d->goff, d->glen, out_gid, d->dcnt, retry);
         TFG_LAUNCH_CHECK();
-        uint64_t c[3];
+        uint64_t c[4];
         TFG_HIP(hipMemcpyAsync(c, d->dcnt, sizeof(c), hipMemcpyDeviceToHost, ctx->stream));
         TFG_HIP(hipStreamSynchronize(ctx->stream));
+        TFG_CHECK(c[3] == 0, TFG_ERR_LOGICAL, "serialized keys: fingerprint table full");
         d->G = c[0];
         d->arena_used = c[1];
         if (c[2] == 0) break;
