@@ -53,6 +53,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--value-int64", action="store_true", help="Int64 value column instead of Float64 (headline leg)")
     ap.add_argument("--bucket-bits", type=int, default=0, help="aggregation radix buckets (0 = from --groups)")
+    ap.add_argument("--c5-bucket-bits", type=int, default=0, help="C5 aggregation radix buckets (0 = from --c5-groups)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, production) or gloo (rehearsal: all ranks may share one GPU)")
     return ap.parse_args()
@@ -360,8 +361,8 @@ def c5_leg(args, ctx, dev, world, rank):
     offs = torch.arange(1, n + 1, device=dev, dtype=torch.int64) * 10
     v = torch.randint(0, 10**9, (n,), device=dev, generator=g, dtype=torch.int64)
     aggs = [(tfa.AGG_SUM, tfa.prec(tfa.DECIMAL64, 15)), (tfa.AGG_COUNT_ALL, 0)]
-    part = tfa.KeysAggregator(ctx, [tfa.STRING], aggs, expected_groups=G)
-    fin = tfa.KeysAggregator(ctx, [tfa.STRING], aggs, expected_groups=G) if world > 1 else None
+    part = tfa.KeysAggregator(ctx, [tfa.STRING], aggs, expected_groups=G, bucket_bits=args.c5_bucket_bits)
+    fin = tfa.KeysAggregator(ctx, [tfa.STRING], aggs, expected_groups=G, bucket_bits=args.c5_bucket_bits) if world > 1 else None
 
     def step():
         part.reset()

@@ -137,6 +137,11 @@ typedef enum tfg_collator {
     TFG_COLLATOR_GENERAL_CI = 3,  /* GeneralCICollator (utf8_general_ci / utf8mb4_general_ci): right-trim ' ',
                                      then each UTF-8 character's 16-bit weight big-endian
                                      (TiDB/Collation/Collator.cpp:416-455) */
+    TFG_COLLATOR_UNICODE_CI = 4,  /* UCACICollator<Unicode0400, padding> (utf8_unicode_ci / utf8mb4_unicode_ci):
+                                     right-trim ' ', then each non-ignorable character's UCA 4.0.0
+                                     weights as 16-bit big-endian chunks (Collator.cpp:580-629) */
+    TFG_COLLATOR_UCA0900_AI_CI = 5, /* UCACICollator<Unicode0900, no padding> (utf8mb4_0900_ai_ci): the same with
+                                       the UCA 9.0.0 weights and no trim */
 } tfg_collator;
 
 /* ---------------------------------------------------------------- context & memory */

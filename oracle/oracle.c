@@ -20,6 +20,7 @@
 
 #include "../include/tiflash_amd.h"
 #include "collation_data.h"
+#include "uca_data.h"
 
 /* ------------------------------------------------------------------ CRC32-C */
 /* intHashCRC32(x, seed) = _mm_crc32_u64(seed, x)  (Common/HashTable/Hash.h:70-95). */
@@ -207,41 +208,145 @@ uint32_t orc_general_ci_weight(uint32_t c)
     return (uint32_t)(c + (int16_t)(v & 0xFFFF)) & 0xFFFF;
 }
 
+/* decodeUtf8Char (Collator.cpp:43-74): the lead byte sets the length, continuation bytes are not
+ * checked; a sequence cut by the row's end reads zeros past row_end */
+static uint32_t orc_utf8_next(const uint8_t *s, size_t row_end, size_t *off)
+{
+#define ORC_AT(k) ((size_t)(k) < row_end ? (uint32_t)s[k] : 0u)
+    const size_t o = *off;
+    const uint32_t b0 = s[o];
+    uint32_t c;
+    if (b0 < 0x80) {
+        c = b0;
+        *off = o + 1;
+    } else if (b0 < 0xE0) {
+        c = (b0 & 0x1F) << 6 | (ORC_AT(o + 1) & 0x3F);
+        *off = o + 2;
+    } else if (b0 < 0xF0) {
+        c = (b0 & 0x0F) << 12 | (ORC_AT(o + 1) & 0x3F) << 6 | (ORC_AT(o + 2) & 0x3F);
+        *off = o + 3;
+    } else {
+        c = (b0 & 0x07) << 18 | (ORC_AT(o + 1) & 0x3F) << 12 | (ORC_AT(o + 2) & 0x3F) << 6 | (ORC_AT(o + 3) & 0x3F);
+        *off = o + 4;
+    }
+#undef ORC_AT
+    return c;
+}
+
 size_t orc_general_ci_sort_key(const uint8_t *s, size_t len, size_t row_end, uint8_t *out)
 {
     while (len > 0 && s[len - 1] == ' ') --len;
     size_t off = 0, o = 0;
-#define ORC_AT(k) ((size_t)(k) < row_end ? (uint32_t)s[k] : 0u)
     while (off < len) {
-        const uint32_t b0 = s[off];
-        uint32_t c;
-        if (b0 < 0x80) {
-            c = b0;
-            off += 1;
-        } else if (b0 < 0xE0) {
-            c = (b0 & 0x1F) << 6 | (ORC_AT(off + 1) & 0x3F);
-            off += 2;
-        } else if (b0 < 0xF0) {
-            c = (b0 & 0x0F) << 12 | (ORC_AT(off + 1) & 0x3F) << 6 | (ORC_AT(off + 2) & 0x3F);
-            off += 3;
-        } else {
-            c = (b0 & 0x07) << 18 | (ORC_AT(off + 1) & 0x3F) << 12 | (ORC_AT(off + 2) & 0x3F) << 6 | (ORC_AT(off + 3) & 0x3F);
-            off += 4;
-        }
-        const uint32_t w = orc_general_ci_weight(c);
+        const uint32_t w = orc_general_ci_weight(orc_utf8_next(s, row_end, &off));
         out[o++] = (uint8_t)(w >> 8);
         out[o++] = (uint8_t)w;
     }
-#undef ORC_AT
     return o;
 }
 
+/* ---------------------------------------------------------------- UCA collators
+ * utf8_unicode_ci / utf8mb4_unicode_ci = UCACICollator<Unicode0400, padding> and
+ * utf8mb4_0900_ai_ci = UCACICollator<Unicode0900, no padding> (Collator.h:415-437).
+ * sortKey = convertImpl<false, true> (Collator.cpp:580-629): right-trim ' ' when padding, then per
+ * character (weight(), :639-667) skip zero-weight characters, take the LUT weight
+ * (Unicode0400::weight :703-727: 0xFFFD past the BMP; Unicode0900::weight :791-816: an implicit
+ * weight from the code point past the table) or, for the LUT value 0xFFFD, the character's long
+ * weight pair (weightLutLongMap), and write `first` then `second` with writeResult (Collator.h:
+ * 336-344): 16-bit chunks from the low end while the value is non-zero, each big-endian.
+ * The LUTs (uca_data.h) are expanded from their runs on first use (single-threaded checker). */
+typedef struct {
+    uint32_t start, count;
+    uint64_t base, delta;
+} orc_uca_run;
+typedef struct {
+    uint32_t cp;
+    uint64_t first, second;
+} orc_uca_long;
+static const orc_uca_run orc_uca0400_runs[TFG_UCA0400_NRUNS] = {TFG_UCA0400_RUNS_INIT};
+static const orc_uca_run orc_uca0900_runs[TFG_UCA0900_NRUNS] = {TFG_UCA0900_RUNS_INIT};
+static const orc_uca_long orc_uca0400_long[TFG_UCA0400_NLONG] = {TFG_UCA0400_LONG_INIT};
+static const orc_uca_long orc_uca0900_long[TFG_UCA0900_NLONG] = {TFG_UCA0900_LONG_INIT};
+static uint64_t *orc_uca_lut[2];
+
+static const uint64_t *orc_uca_table(int v0900)
+{
+    if (!orc_uca_lut[v0900]) {
+        const orc_uca_run *runs = v0900 ? orc_uca0900_runs : orc_uca0400_runs;
+        const int nr = v0900 ? TFG_UCA0900_NRUNS : TFG_UCA0400_NRUNS;
+        const size_t size = v0900 ? TFG_UCA0900_SIZE : TFG_UCA0400_SIZE;
+        uint64_t *t = (uint64_t *)calloc(size, 8);
+        for (int i = 0; i < nr; ++i)
+            for (uint32_t k = 0; k < runs[i].count; ++k) t[runs[i].start + k] = runs[i].base + (uint64_t)k * runs[i].delta;
+        orc_uca_lut[v0900] = t;
+    }
+    return orc_uca_lut[v0900];
+}
+
+/* T::weight: 0 = a zero-weight character (skipped), else first / second set */
+int orc_uca_weight(int v0900, uint32_t r, uint64_t *first, uint64_t *second)
+{
+    *second = 0;
+    if (!v0900 && r > 0xFFFF) {
+        *first = 0xFFFD;
+        return 1;
+    }
+    if (v0900 && r >= TFG_UCA0900_SIZE) { /* (the reference tests r > 0x2CEA1 and reads one past its LUT at r == 0x2CEA1) */
+        *first = (uint64_t)(r >> 15) + 0xFBC0 + ((uint64_t)((r & 0x7FFF) | 0x8000) << 16);
+        return 1;
+    }
+    const uint64_t w = orc_uca_table(v0900)[r];
+    if (w == 0) return 0;
+    if (w != 0xFFFD) {
+        *first = w;
+        return 1;
+    }
+    const orc_uca_long *lw = v0900 ? orc_uca0900_long : orc_uca0400_long;
+    const int nl = v0900 ? TFG_UCA0900_NLONG : TFG_UCA0400_NLONG;
+    *first = 0; /* weightLutLongMap's default entry: {0, 0} */
+    for (int i = 0; i < nl; ++i)
+        if (lw[i].cp == r) {
+            *first = lw[i].first;
+            *second = lw[i].second;
+        }
+    return 1;
+}
+
+size_t orc_uca_sort_key(int v0900, const uint8_t *s, size_t len, size_t row_end, uint8_t *out)
+{
+    if (!v0900)
+        while (len > 0 && s[len - 1] == ' ') --len;
+    size_t off = 0, o = 0;
+    while (off < len) {
+        uint64_t w[2];
+        if (!orc_uca_weight(v0900, orc_utf8_next(s, row_end, &off), &w[0], &w[1])) continue;
+        for (int h = 0; h < 2; ++h)
+            for (uint64_t x = w[h]; x != 0; x >>= 16) {
+                out[o++] = (uint8_t)(x >> 8);
+                out[o++] = (uint8_t)x;
+            }
+    }
+    return o;
+}
+
+int orc_collator_transforms(int collator)
+{
+    return collator == TFG_COLLATOR_GENERAL_CI || collator == TFG_COLLATOR_UNICODE_CI || collator == TFG_COLLATOR_UCA0900_AI_CI;
+}
+
+/* the sort key of a transforming collator (<= ORC_KEY_MULT bytes per input byte) */
+size_t orc_collate(int collator, const uint8_t *s, size_t len, size_t row_end, uint8_t *out)
+{
+    if (collator == TFG_COLLATOR_GENERAL_CI) return orc_general_ci_sort_key(s, len, row_end, out);
+    return orc_uca_sort_key(collator == TFG_COLLATOR_UCA0900_AI_CI, s, len, row_end, out);
+}
+
 /* the collator's sort key of a ColumnString row's bytes (len = size - 1, '\0' excluded) into buf
- * (>= 2 * len bytes); returns a pointer to the key and its length */
+ * (>= ORC_KEY_MULT * len bytes); returns a pointer to the key and its length */
 static const uint8_t *orc_sort_key(int collator, const uint8_t *s, size_t len, uint8_t *buf, size_t *klen)
 {
-    if (collator == TFG_COLLATOR_GENERAL_CI) {
-        *klen = orc_general_ci_sort_key(s, len, len + 1, buf);
+    if (orc_collator_transforms(collator)) {
+        *klen = orc_collate(collator, s, len, len + 1, buf);
         return buf;
     }
     if (collator == TFG_COLLATOR_BIN_PADDING)
@@ -262,8 +367,8 @@ void orc_weak_hash_update_string(const uint8_t *chars, const uint64_t *offsets, 
         if (nullmap && nullmap[i]) continue;
         uint64_t prev = i ? offsets[i - 1] : 0;
         size_t len = (size_t)(offsets[i] - prev - 1);
-        if (2 * len + 16 > cap) {
-            cap = 2 * (2 * len + 16);
+        if (ORC_KEY_MULT * len + 16 > cap) {
+            cap = 2 * (ORC_KEY_MULT * len + 16);
             buf = (uint8_t *)realloc(buf, cap);
         }
         size_t klen;
@@ -868,7 +973,7 @@ static size_t aggk_serialize(const orc_aggk *a, const void *const *cols, const u
 {
     size_t need = 0;
     for (int j = 0; j < a->nkeys; ++j) {
-        if (a->key_types[j] == TFG_STRING) need += 9 + 2 * (offs[j][r] - (r ? offs[j][r - 1] : 0));
+        if (a->key_types[j] == TFG_STRING) need += 9 + ORC_KEY_MULT * (offs[j][r] - (r ? offs[j][r - 1] : 0));
         else need += 17;
     }
     if (need > *bcap) {
@@ -884,8 +989,8 @@ static size_t aggk_serialize(const orc_aggk *a, const void *const *cols, const u
             const uint64_t s = r ? offs[j][r - 1] : 0;
             uint64_t len = offs[j][r] - s - 1;
             const uint8_t *c = (const uint8_t *)cols[j] + s;
-            if (a->collators[j] == TFG_COLLATOR_GENERAL_CI) { /* the sort key, written in place */
-                const uint64_t kl = orc_general_ci_sort_key(c, len, len + 1, o + 8);
+            if (orc_collator_transforms(a->collators[j])) { /* the sort key, written in place */
+                const uint64_t kl = orc_collate(a->collators[j], c, len, len + 1, o + 8);
                 memcpy(o, &kl, 8);
                 o += 8 + kl;
                 continue;

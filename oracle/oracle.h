@@ -28,6 +28,14 @@ uint32_t orc_update_weak_hash32_bytes(const uint8_t *pos, size_t size, uint32_t 
  * (>= 2 * len bytes), look-ahead bounded by row_end; returns the key's length */
 uint32_t orc_general_ci_weight(uint32_t c);
 size_t orc_general_ci_sort_key(const uint8_t *s, size_t len, size_t row_end, uint8_t *out);
+/* utf8mb4_unicode_ci (v0900 = 0, UCA 4.0.0, padding) / utf8mb4_0900_ai_ci (v0900 = 1): a code
+ * point's weight pair (0 = zero weight, skipped) and a row's sort key; orc_collate dispatches a
+ * transforming collator's sort key (<= ORC_KEY_MULT bytes per input byte) */
+#define ORC_KEY_MULT 8
+int orc_uca_weight(int v0900, uint32_t r, uint64_t *first, uint64_t *second);
+size_t orc_uca_sort_key(int v0900, const uint8_t *s, size_t len, size_t row_end, uint8_t *out);
+int orc_collator_transforms(int collator);
+size_t orc_collate(int collator, const uint8_t *s, size_t len, size_t row_end, uint8_t *out);
 
 void orc_weak_hash_update(int type, const void *col, const uint8_t *nullmap, size_t n, uint32_t *h);
 uint64_t orc_float64_to_u64(double x); /* the reference build's Float64 -> UInt64 (x86-64 clang) */

@@ -20,7 +20,9 @@ reference_cases.json — known answers TRANSCRIBED (as data) from the reference'
     the +/-/* result scales of DataTypeDecimal_test A (gtest_funtions_decimal_arith.cpp:47-77).
   * general_ci: utf8mb4_general_ci sort keys and comparisons pinned by the reference's collator
     gtest (dbms/src/TiDB/tests/gtest_tidb_collator.cpp:49-65 cmp_cases and :71-140 sk_cases, the
-    GeneralCI column of each answer tuple), as hex bytes.
+    GeneralCI column of each answer tuple), as hex bytes;
+  * unicode_ci / uca0900_ai_ci: the same for utf8mb4_unicode_ci and utf8mb4_0900_ai_ci (the
+    UnicodeCI and Utf8Mb40900AICI columns).
 crc_vectors.json — CRC32-C / WeakHash32 vectors computed with the x86 SSE4.2 crc32q instruction,
   the instruction the reference itself hashes with (Common/HashTable/Hash.h:70-95), via oracle.
 """
@@ -148,6 +150,29 @@ def general_ci_cases():
             "compare": [{"a": a, "b": b, "sign": c} for a, b, c in cmp]}
 
 
+def uca_cases():
+    # the UnicodeCI (index 4: utf8mb4_unicode_ci, UCA 4.0.0, padding) and Utf8Mb40900AICI (index 5:
+    # utf8mb4_0900_ai_ci, UCA 9.0.0, no padding) entries of sk_cases / cmp_cases
+    # (gtest_tidb_collator.cpp:49-65, 71-140)
+    foo = "Foo \u00a9 bar \U0001D306 baz \u2603 qux"
+    sk = {
+        "unicode_ci": [("a", "0e33"), ("A", "0e33"), ("\U0001F603", "fffd"),
+                       (foo, "0eb90f820f82020902c502090e4a0e330fc00209fffd0209" "0e4a0e33" "106a020906ff02090fb4101f105a"),
+                       ("a ", "0e33"), ("", ""), ("\u00df", "0fea0fea")],
+        "uca0900_ai_ci": [("a", "1c47"), ("A", "1c47"), ("\U0001F603", "15fe"),
+                          (foo, "1ce51ddd1ddd0209058402091c601c471e3302090ef00209" "1c601c47" "1f210209091b02091e211eb51eff"),
+                          ("a ", "1c470209"), ("", ""), ("\u00df", "1e711e71")],
+    }
+    pairs = [("a", "b"), ("a", "A"), ("\u00c0", "A"), ("abc", "abc"), ("abc", "ab"), ("\U0001F61C", "\U0001F603"),
+             ("a", "a "), ("a ", "a  "), ("a\t", "a"), ("", "a"), ("a", ""), ("\u00df", "ss"),
+             ("\U0001042D", "\U00010428"), ("\u8b3a", "\u8b42")]
+    signs = {"unicode_ci": [-1, 0, 0, 0, 1, 0, 0, 0, 1, -1, 1, 0, 0, -1],
+             "uca0900_ai_ci": [-1, 0, 0, 0, 1, 1, -1, -1, 1, -1, 1, 0, 1, -1]}
+    return {name: {"sort_keys": [{"s": a, "key_hex": k} for a, k in sk[name]],
+                   "compare": [{"a": a, "b": b, "sign": c} for (a, b), c in zip(pairs, signs[name])]}
+            for name in sk}
+
+
 def crc_vectors():
     from oracle import oracle as orc
     rng = np.random.default_rng(2024)
@@ -168,7 +193,7 @@ if __name__ == "__main__":
         json.dump({"groupby": groupby_cases(), "groupby_keys": groupby_keys_cases(), "join": join_cases(),
                    "exchange": {"block_rows": 64, "blocks": 64, "parts": 4, "rows_per_part": 1024},
                    "aggregates": aggregate_cases(), "sum_types": sum_type_cases(),
-                   "general_ci": general_ci_cases()}, f, indent=1)
+                   "general_ci": general_ci_cases(), **uca_cases()}, f, indent=1)
     with open(os.path.join(HERE, "crc_vectors.json"), "w") as f:
         json.dump(crc_vectors(), f, indent=1)
     print("wrote", os.listdir(HERE))

@@ -1,10 +1,12 @@
-"""utf8mb4_general_ci String keys on the GPU (§8 f2): weak hash (exchange routing), GROUP BY
-(key_string and the serialized method) and join keys, each against the oracle's restatement of
-GeneralCICollator::sortKey (oracle/oracle.c orc_general_ci_sort_key, pinned by the reference's
-collator gtest answers in tests/golden/reference_cases.json "general_ci").
+"""Case-insensitive String keys on the GPU (§8 f2): utf8mb4_general_ci, utf8mb4_unicode_ci and
+utf8mb4_0900_ai_ci.  Weak hash (exchange routing), GROUP BY (key_string and the serialized method)
+and join keys, each against the oracle's restatement of the collator's sortKey (oracle/oracle.c
+orc_collate, pinned by the reference's collator gtest answers in tests/golden/reference_cases.json
+"general_ci" / "unicode_ci" / "uca0900_ai_ci").
 
 Reference: GeneralCICollator::convertImpl (TiDB/Collation/Collator.cpp:416-455), weight
-(Collator.h:403-407); consumers: ColumnString::updateWeakHash32 (ColumnString.cpp:1244),
+(Collator.h:403-407); UCACICollator::convertImpl (Collator.cpp:580-629) with Unicode0400 /
+Unicode0900::weight (:703-727, 791-816); consumers: ColumnString::updateWeakHash32 (ColumnString.cpp:1244),
 HashMethodString (ColumnsHashing.h:233), serializeValueIntoArena (AggregationCommon.h:202),
 the join's key_strbin path (JoinHashMap.cpp:83-112)."""
 import ctypes
@@ -16,8 +18,12 @@ import torch
 pytestmark = pytest.mark.gpu
 
 # letters in several cases and accents, CJK, astral characters (weight 0xFFFD), trailing spaces
+# (UCA: a zero-weight control character, long weights U+321D / U+3307 / U+FDFB, a code point past
+# the 9.0.0 table)
 ALPHABET = ["a", "A", "à", "À", "á", "b", "B", "ß", "s", "S", "œ", "é", "E",
-            "謺", "譂", "\U0001F603", "\U0001F61C", "z", "ё", "Ё", "ẞ", "1", "_"]
+            "謺", "譂", "\U0001F603", "\U0001F61C", "z", "ё", "Ё", "ẞ", "1", "_",
+            "\x01", "\u321d", "\u3307", "\ufdfb", "\U00030000"]
+COLLATORS = [3, 4, 5]  # COLLATOR_GENERAL_CI, COLLATOR_UNICODE_CI, COLLATOR_UCA0900_AI_CI
 
 
 def _random_strings(rng, n, maxlen):
@@ -37,23 +43,23 @@ def _column(strs):
     return chars, offsets
 
 
-def _sort_key(orc, s):
+def _sort_key(orc, s, collator):
     lib = orc.lib()
-    lib.orc_general_ci_sort_key.restype = ctypes.c_size_t
-    out = ctypes.create_string_buffer(2 * len(s) + 16)
-    n = lib.orc_general_ci_sort_key(s, ctypes.c_size_t(len(s)), ctypes.c_size_t(len(s) + 1), out)
+    lib.orc_collate.restype = ctypes.c_size_t
+    out = ctypes.create_string_buffer(8 * len(s) + 16)
+    n = lib.orc_collate(collator, s, ctypes.c_size_t(len(s)), ctypes.c_size_t(len(s) + 1), out)
     return out.raw[:n]
 
 
+@pytest.mark.parametrize("collator", COLLATORS)
 @pytest.mark.parametrize("selective", [False, True])
-def test_general_ci_weak_hash(tfa, ctx, dev, orc, selective):
+def test_ci_weak_hash(tfa, ctx, dev, orc, selective, collator):
     rng = np.random.default_rng(71 + selective)
     strs = _random_strings(rng, 20_000, 12)
     chars, offs = _column(strs)
     nulls = (rng.random(len(strs)) < 0.05).astype(np.uint8)
     n = len(strs)
-    exp = orc.weak_hash_string(chars, offs.view(np.int64), np.full(n, 0xFFFFFFFF, np.uint32), nulls,
-                               tfa.COLLATOR_GENERAL_CI)
+    exp = orc.weak_hash_string(chars, offs.view(np.int64), np.full(n, 0xFFFFFFFF, np.uint32), nulls, collator)
     h = torch.full((n,), -1, dtype=torch.int32, device=dev)
     sel = None
     if selective:
@@ -62,25 +68,26 @@ def test_general_ci_weak_hash(tfa, ctx, dev, orc, selective):
         h = torch.full((rows.shape[0],), -1, dtype=torch.int32, device=dev)
         exp = exp[rows.astype(np.int64)]
     got = tfa.weak_hash_string(ctx, torch.from_numpy(chars).to(dev), torch.from_numpy(offs.view(np.int64)).to(dev), h,
-                               nullmap=torch.from_numpy(nulls).to(dev), collator=tfa.COLLATOR_GENERAL_CI, selective=sel)
+                               nullmap=torch.from_numpy(nulls).to(dev), collator=collator, selective=sel)
     assert np.array_equal(got.cpu().numpy().view(np.uint32), exp.view(np.uint32))
     # equal sort keys hash equal: 'a' / 'A' / 'à' ...
-    eq = [b"abc", b"ABC", "àBC".encode(), b"abc  "]
+    eq = [b"abc", b"ABC", "àBC".encode(), b"a\x01bc"] if collator == 5 else [b"abc", b"ABC", "àBC".encode(), b"abc  "]
     c2, o2 = _column(eq)
     h2 = torch.full((4,), -1, dtype=torch.int32, device=dev)
     g2 = tfa.weak_hash_string(ctx, torch.from_numpy(c2).to(dev), torch.from_numpy(o2.view(np.int64)).to(dev), h2,
-                              collator=tfa.COLLATOR_GENERAL_CI).cpu().numpy()
+                              collator=collator).cpu().numpy()
     assert len(set(g2.tolist())) == 1
 
 
-@pytest.mark.parametrize("maxlen", [6, 20])  # 6: packed key_string (<= 7 characters); 20: serialized
-def test_general_ci_group_by_string(tfa, ctx, dev, orc, maxlen):
+@pytest.mark.parametrize("collator", COLLATORS)
+@pytest.mark.parametrize("maxlen", [6, 20])  # 6: mostly packed key_string keys (<= 15 key bytes); 20: serialized
+def test_ci_group_by_string(tfa, ctx, dev, orc, maxlen, collator):
     rng = np.random.default_rng(81 + maxlen)
     strs = _random_strings(rng, 30_000, maxlen)
     chars, offs = _column(strs)
     v = rng.integers(-1000, 1000, len(strs)).astype(np.int64)
     aggs = [(tfa.AGG_SUM, tfa.INT64), (tfa.AGG_COUNT_ALL, 0)]
-    agg = tfa.KeysAggregator(ctx, [tfa.STRING], aggs, collators=[tfa.COLLATOR_GENERAL_CI])
+    agg = tfa.KeysAggregator(ctx, [tfa.STRING], aggs, collators=[collator])
     agg.consume([(torch.from_numpy(chars).to(dev), torch.from_numpy(offs.view(np.int64)).to(dev))],
                 [torch.from_numpy(v).to(dev), None])
     res = agg.result()
@@ -94,24 +101,25 @@ def test_general_ci_group_by_string(tfa, ctx, dev, orc, maxlen):
     agg.close()
     exp = {}
     for s, x in zip(strs, v):
-        k = _sort_key(orc, s)
+        k = _sort_key(orc, s, collator)
         a, c = exp.get(k, (0, 0))
         exp[k] = (a + int(x), c + 1)
     assert got == exp
     # the oracle's own GROUP BY under the collator agrees
-    ref = orc.AggKeys([orc.STRING], [(0, orc.INT64), (2, 0)], collators=[tfa.COLLATOR_GENERAL_CI])
+    ref = orc.AggKeys([orc.STRING], [(0, orc.INT64), (2, 0)], collators=[collator])
     ref.consume([(chars, offs)], [v, None])
     assert ref.size() == len(exp)
 
 
-def test_general_ci_group_by_string_and_int(tfa, ctx, dev, orc):
+@pytest.mark.parametrize("collator", COLLATORS)
+def test_ci_group_by_string_and_int(tfa, ctx, dev, orc, collator):
     """String + Int64 keys: the serialized method, the String part as its sort key."""
     rng = np.random.default_rng(91)
     strs = _random_strings(rng, 20_000, 5)
     chars, offs = _column(strs)
     k2 = rng.integers(0, 3, len(strs)).astype(np.int64)
     agg = tfa.KeysAggregator(ctx, [tfa.STRING, tfa.INT64], [(tfa.AGG_COUNT_ALL, 0)],
-                             collators=[tfa.COLLATOR_GENERAL_CI, 0])
+                             collators=[collator, 0])
     agg.consume([(torch.from_numpy(chars).to(dev), torch.from_numpy(offs.view(np.int64)).to(dev)),
                  torch.from_numpy(k2).to(dev)], [None])
     res = agg.result()
@@ -122,19 +130,20 @@ def test_general_ci_group_by_string_and_int(tfa, ctx, dev, orc):
     agg.close()
     exp = {}
     for s, x in zip(strs, k2):
-        key = (_sort_key(orc, s), int(x))
+        key = (_sort_key(orc, s, collator), int(x))
         exp[key] = exp.get(key, 0) + 1
     assert got == exp
 
 
-def test_general_ci_join_keys(tfa, ctx, dev, orc):
+@pytest.mark.parametrize("collator", COLLATORS)
+def test_ci_join_keys(tfa, ctx, dev, orc, collator):
     rng = np.random.default_rng(101)
     bs = _random_strings(rng, 3000, 4)
     ps = _random_strings(rng, 12_000, 4)
     bc, bo = _column(bs)
     pc, po = _column(ps)
     t = lambda x: torch.from_numpy(x).to(dev)  # noqa: E731
-    ci = [tfa.COLLATOR_GENERAL_CI]
+    ci = [collator]
     fb, nbm = tfa.join_key_hash(ctx, [t(bc)], [tfa.STRING], offsets=[t(bo.view(np.int64))], collators=ci)
     fp, npm = tfa.join_key_hash(ctx, [t(pc)], [tfa.STRING], offsets=[t(po.view(np.int64))], collators=ci)
     j = tfa.Join(ctx, tfa.UINT64)
@@ -145,6 +154,6 @@ def test_general_ci_join_keys(tfa, ctx, dev, orc):
     got = sorted(zip(pi.cpu().numpy().view(np.uint32)[ok].tolist(), bi.cpu().numpy().view(np.uint32)[ok].tolist()))
     idx = {}
     for r, s in enumerate(bs):
-        idx.setdefault(_sort_key(orc, s), []).append(r)
-    exp = sorted((i, r) for i, s in enumerate(ps) for r in idx.get(_sort_key(orc, s), []))
+        idx.setdefault(_sort_key(orc, s, collator), []).append(r)
+    exp = sorted((i, r) for i, s in enumerate(ps) for r in idx.get(_sort_key(orc, s, collator), []))
     assert got == exp and len(exp) > 1000

@@ -322,20 +322,23 @@ def test_float_weak_hash_golden(orc, kind):
     np.testing.assert_array_equal(h, hashes)
 
 
-def test_oracle_general_ci_sort_keys_match_reference_gtest(orc):
-    """utf8mb4_general_ci sort keys and comparisons: the reference's collator gtest answers
-    (gtest_tidb_collator.cpp:49-65, 71-140; tests/golden/reference_cases.json "general_ci")."""
+@pytest.mark.parametrize("name,collator", [("general_ci", 3), ("unicode_ci", 4), ("uca0900_ai_ci", 5)])
+def test_oracle_ci_sort_keys_match_reference_gtest(orc, name, collator):
+    """utf8mb4_general_ci / utf8mb4_unicode_ci / utf8mb4_0900_ai_ci sort keys and comparisons: the
+    reference's collator gtest answers (gtest_tidb_collator.cpp:49-65, 71-140;
+    tests/golden/reference_cases.json).  UCA comparisons walk the same 16-bit weights the sort key
+    holds (Collator.cpp:526-578), so the key order is the comparison's sign."""
     import ctypes
     import json
     import os
-    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "reference_cases.json")))["general_ci"]
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "reference_cases.json")))[name]
     lib = orc.lib()
-    lib.orc_general_ci_sort_key.restype = ctypes.c_size_t
+    lib.orc_collate.restype = ctypes.c_size_t
 
     def key(s):
         b = s.encode("utf-8")
-        out = ctypes.create_string_buffer(2 * len(b) + 16)
-        n = lib.orc_general_ci_sort_key(b, ctypes.c_size_t(len(b)), ctypes.c_size_t(len(b) + 1), out)
+        out = ctypes.create_string_buffer(8 * len(b) + 16)
+        n = lib.orc_collate(collator, b, ctypes.c_size_t(len(b)), ctypes.c_size_t(len(b) + 1), out)
         return out.raw[:n]
 
     for c in gold["sort_keys"]:
@@ -343,3 +346,27 @@ def test_oracle_general_ci_sort_keys_match_reference_gtest(orc):
     for c in gold["compare"]:
         ka, kb = key(c["a"]), key(c["b"])
         assert (ka > kb) - (ka < kb) == c["sign"], c
+
+
+def test_oracle_uca_special_weights(orc):
+    """UCA weight rules beyond the table lookup (Collator.cpp:703-727, 791-816): zero-weight
+    characters vanish from the key, long weights (weightLutLongMap) emit both words, code points
+    past the tables take 0xFFFD (4.0.0) or the implicit 9.0.0 weight."""
+    import ctypes
+    lib = orc.lib()
+    lib.orc_collate.restype = ctypes.c_size_t
+
+    def key(s, c):
+        b = s.encode("utf-8")
+        out = ctypes.create_string_buffer(8 * len(b) + 16)
+        n = lib.orc_collate(c, b, ctypes.c_size_t(len(b)), ctypes.c_size_t(len(b) + 1), out)
+        return out.raw[:n]
+
+    for c in (4, 5):
+        assert key("a\x01b", c) == key("ab", c)               # U+0001 weighs nothing
+        assert len(key("\u321d", c)) > 8                       # a long weight: first and second words
+        assert key("\u321d", c) != key("\u321e", c)
+    assert key("\U00030000", 4) == bytes.fromhex("fffd")
+    r = 0x30000
+    w = (r >> 15) + 0xFBC0 + (((r & 0x7FFF) | 0x8000) << 16)
+    assert key("\U00030000", 5) == bytes.fromhex("%04x%04x" % (w & 0xFFFF, w >> 16))

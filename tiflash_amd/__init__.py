@@ -44,7 +44,7 @@ AND, OR, NOT = range(3)
 AGG_SUM, AGG_COUNT, AGG_COUNT_ALL = range(3)
 JOIN_INNER, JOIN_LEFT, JOIN_SEMI, JOIN_ANTI = range(4)
 JOIN_V2_TAGGED = 1  # tfg_join_create_v2 flags
-COLLATOR_NONE, COLLATOR_BINARY, COLLATOR_BIN_PADDING, COLLATOR_GENERAL_CI = range(4)
+COLLATOR_NONE, COLLATOR_BINARY, COLLATOR_BIN_PADDING, COLLATOR_GENERAL_CI, COLLATOR_UNICODE_CI, COLLATOR_UCA0900_AI_CI = range(6)
 
 WIDTH = {INT8: 1, INT16: 2, INT32: 4, INT64: 8, UINT8: 1, UINT16: 2, UINT32: 4, UINT64: 8,
          FLOAT32: 4, FLOAT64: 8, DECIMAL32: 4, DECIMAL64: 8, DECIMAL128: 16, DECIMAL256: 32, KEYS128: 16}

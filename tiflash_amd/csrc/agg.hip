@@ -317,7 +317,10 @@ struct SelWideStr {
 // `fine` = 6 bits: the bucket kernel of (coarse c, fine f) then reads runs of ~RG_TR / 64 rows
 // from the tiles [tile_base[c], tile_base[c + 1]).
 constexpr int RG_T = 1024;
-constexpr int RG_TR = 3072;
+#ifndef TFG_RG_TR
+#define TFG_RG_TR 3072
+#endif
+constexpr int RG_TR = TFG_RG_TR;
 constexpr int RG_FINE_BITS = 6;
 constexpr int RG_FINE = 1 << RG_FINE_BITS;
 
@@ -362,58 +365,64 @@ __global__ void regroup_tile_base_kernel(const uint32_t *runpref, int T1, int B1
     tile_base[B1] = acc;
 }
 
+// where pass-2 tile k reads from: its coarse bucket c (-1: past the last tile), the pass-1 runs
+// t0 .. t0 + m - 1 that cover its rows [x0, x1) of the bucket.  One thread per tile, all tiles at
+// once (the searches' dependent loads overlap across threads instead of heading every
+// workgroup of the regroup kernel)
+struct RgDesc {
+    int c, t0, m;
+    uint32_t x0, x1;
+};
+
+__global__ void regroup_desc_kernel(const uint32_t *runpref, int T1, const uint32_t *tile_base, int B1, int T2,
+                                    RgDesc *desc) {
+    const int k = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (k >= T2) return;
+    RgDesc d{-1, 0, 0, 0, 0};
+    if ((uint32_t)k < tile_base[B1]) {
+        int lo = 0, hi = B1; // coarse bucket of tile k: tile_base[c] <= k < tile_base[c + 1]
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) / 2;
+            if (tile_base[mid] <= (uint32_t)k) lo = mid;
+            else hi = mid;
+        }
+        const uint32_t *pr = runpref + (size_t)lo * (T1 + 1);
+        const uint32_t n_c = pr[T1];
+        const uint32_t x0 = (uint32_t)(k - (int)tile_base[lo]) * RG_TR;
+        const uint32_t x1 = min(x0 + (uint32_t)RG_TR, n_c);
+        // runs covering [x0, x1): t0 = last tile with pr[t] <= x0, t1 = first with pr[t] >= x1
+        int a = 0, b = T1;
+        while (b - a > 1) {
+            const int mid = (a + b) / 2;
+            if (pr[mid] <= x0) a = mid;
+            else b = mid;
+        }
+        int lo2 = a, hi2 = T1; // pr[T1] = n_c >= x1
+        while (hi2 - lo2 > 1) {
+            const int mid = (lo2 + hi2) / 2;
+            if (pr[mid] >= x1) hi2 = mid;
+            else lo2 = mid;
+        }
+        d = RgDesc{lo, a, hi2 - a, x0, x1};
+    }
+    desc[k] = d;
+}
+
 // one workgroup per pass-2 tile (grid = an upper bound; tiles past tile_base[B1] exit)
 template <int NCOL>
 __global__ void __launch_bounds__(RG_T) regroup_tiled_kernel(const uint64_t *rec1, const uint32_t *hist1, int T1, int TR1,
-                                                             const uint32_t *runpref, const uint32_t *tile_base, int B1,
+                                                             const uint32_t *runpref, const RgDesc *desc,
                                                              uint32_t fine_shift, uint64_t *rec2, uint32_t *hist2, int T2) {
     __shared__ uint64_t stage[RG_TR * NCOL];
     __shared__ uint32_t rpref[RG_TR + 2], rent[RG_TR + 2];
     __shared__ uint32_t fh[RG_FINE], fs[RG_FINE];
-    __shared__ int s_c, s_t0, s_m;
-    __shared__ uint32_t s_x0, s_x1;
     const int k = blockIdx.x;
-    if (threadIdx.x == 0) {
-        int lo = 0, hi = B1; // coarse bucket of tile k: tile_base[c] <= k < tile_base[c + 1]
-        if ((uint32_t)k >= tile_base[B1]) {
-            s_c = -1;
-        } else {
-            while (hi - lo > 1) {
-                const int mid = (lo + hi) / 2;
-                if (tile_base[mid] <= (uint32_t)k) lo = mid;
-                else hi = mid;
-            }
-            s_c = lo;
-            const uint32_t *pr = runpref + (size_t)lo * (T1 + 1);
-            const uint32_t n_c = pr[T1];
-            const uint32_t x0 = (uint32_t)(k - (int)tile_base[lo]) * RG_TR;
-            const uint32_t x1 = min(x0 + (uint32_t)RG_TR, n_c);
-            // runs covering [x0, x1): t0 = last tile with pr[t] <= x0, t1 = first with pr[t] >= x1
-            int a = 0, b = T1;
-            while (b - a > 1) {
-                const int mid = (a + b) / 2;
-                if (pr[mid] <= x0) a = mid;
-                else b = mid;
-            }
-            int lo2 = a, hi2 = T1; // t1 = first tile after a with pr[t] >= x1 (pr[T1] = n_c >= x1)
-            while (hi2 - lo2 > 1) {
-                const int mid = (lo2 + hi2) / 2;
-                if (pr[mid] >= x1) hi2 = mid;
-                else lo2 = mid;
-            }
-            const int t1 = hi2;
-            s_t0 = a;
-            s_m = t1 - a;
-            s_x0 = x0;
-            s_x1 = x1;
-        }
-    }
+    const RgDesc d = desc[k];
     if (threadIdx.x < RG_FINE) fh[threadIdx.x] = 0;
-    __syncthreads();
-    const int c = s_c;
+    const int c = d.c;
     if (c < 0) return;
-    const int t0 = s_t0, m = s_m;
-    const uint32_t x0 = s_x0, x1 = s_x1;
+    const int t0 = d.t0, m = d.m;
+    const uint32_t x0 = d.x0, x1 = d.x1;
     const uint32_t *pr = runpref + (size_t)c * (T1 + 1);
     const uint32_t *hc = hist1 + (size_t)c * T1;
     constexpr int PER = RG_TR / RG_T;
@@ -436,7 +445,7 @@ __global__ void __launch_bounds__(RG_T) regroup_tiled_kernel(const uint64_t *rec
             const uint32_t x = x0 + (uint32_t)(q * RG_T + threadIdx.x);
             if (x >= x1 || row[q] >= 0 || x >= rpref[wm]) continue;
             int lo = 0;
-            for (int st = 1 << 11; st > 0; st >>= 1)
+            for (int st = wm > 1 ? 1 << (31 - __clz(wm - 1)) : 0; st > 0; st >>= 1)
                 if (lo + st < wm && rpref[lo + st] <= x) lo += st;
             row[q] = (int64_t)(t0 + w0 + lo) * TR1 + (rent[lo] & 0xFFFFu) + (x - rpref[lo]);
         }
@@ -880,6 +889,7 @@ int consume_wide_tiled(tfg_agg *a, int code, Sel sel, const void *const *vals, i
     const size_t o_pref = cv.take<uint32_t>(two ? (size_t)B1 * (T1 + 1) : 0);
     const size_t o_tbase = cv.take<uint32_t>(B1 + 1);
     const size_t o_hist2 = cv.take<uint32_t>(two ? (size_t)RG_FINE * T2 : 0);
+    const size_t o_desc = cv.take<RgDesc>(two ? (size_t)T2 : 0);
     const size_t o_cur = cv.take<unsigned long long>(2);
     const size_t o_new_cnt = cv.take<uint64_t>(B), o_new_off = cv.take<uint64_t>(B + 1), o_tb = cv.take<uint64_t>(B);
     const size_t tmp_groups = n_old + (size_t)n;
@@ -915,15 +925,18 @@ int consume_wide_tiled(tfg_agg *a, int code, Sel sel, const void *const *vals, i
         ProfScope _ps(ctx, "agg.part.regroup");
         hipLaunchKernelGGL(regroup_prefix_kernel, dim3(B1), dim3(1024), 0, ctx->stream, tin.tile_hist, T1, pref);
         hipLaunchKernelGGL(regroup_tile_base_kernel, dim3(1), dim3(64), 0, ctx->stream, pref, T1, (int)B1, tbase);
+        RgDesc *desc = (RgDesc *)(sb + o_desc);
+        hipLaunchKernelGGL(regroup_desc_kernel, dim3((unsigned)((T2 + 255) / 256)), dim3(256), 0, ctx->stream,
+                           (const uint32_t *)pref, T1, (const uint32_t *)tbase, (int)B1, (int)T2, desc);
         const uint32_t fine_shift = fib_shift(B);
         if (ncol == 3)
             hipLaunchKernelGGL(regroup_tiled_kernel<3>, dim3((unsigned)T2), dim3(RG_T), 0, ctx->stream, tin.rec,
-                               tin.tile_hist, T1, tin.TR, pref, tbase, (int)B1, fine_shift, (uint64_t *)(sb + o_rec2),
-                               hist2, (int)T2);
+                               tin.tile_hist, T1, tin.TR, pref, (const RgDesc *)desc, fine_shift,
+                               (uint64_t *)(sb + o_rec2), hist2, (int)T2);
         else
             hipLaunchKernelGGL(regroup_tiled_kernel<2>, dim3((unsigned)T2), dim3(RG_T), 0, ctx->stream, tin.rec,
-                               tin.tile_hist, T1, tin.TR, pref, tbase, (int)B1, fine_shift, (uint64_t *)(sb + o_rec2),
-                               hist2, (int)T2);
+                               tin.tile_hist, T1, tin.TR, pref, (const RgDesc *)desc, fine_shift,
+                               (uint64_t *)(sb + o_rec2), hist2, (int)T2);
         TFG_LAUNCH_CHECK();
         tin.rec = (const uint64_t *)(sb + o_rec2);
         tin.tile_hist = hist2;
@@ -1464,13 +1477,20 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
     // largest-table fill: inserts reserve cells (Table::reserve), so no headroom for in-flight
     // inserts is needed; wide keys (48-byte cells with a Decimal128 sum) fill to 7/8
     const int fill_big = wide ? 7 : 6;
+    // wide keys may use up to 2^14 buckets: their two-level partition (coarse B >> 6, fine 64)
+    // stays within 256 coarse destinations.  Their probe (tag, then the 16-byte key) is
+    // latency-bound and slows sharply with the load factor, so they aim at ~3/8 of the largest
+    // table: C5's 10M groups -> 16384 buckets at ~30% load (wide bucket kernel 1.92 ms, against
+    // 2.67 ms at 8192 buckets / ~60% and 3.72 ms at 4096 / ~80%; smaller tables with more
+    // workgroups per CU measured slower: 1024 cells 3.71 ms, 1536 cells 2.84 ms, r03 sweep)
+    const int max_bits = wide ? 14 : 12;
     if (bbits <= 0) {
         const int64_t cells_max = LDS_TABLE_MAX / cell;
-        const int64_t fit = (cells_max * fill_big / 8) * 5 / 6;
+        const int64_t fit = wide ? cells_max * 3 / 8 : (cells_max * fill_big / 8) * 5 / 6;
         bbits = 8;
-        while (bbits < 12 && ((int64_t)1 << bbits) * fit < eg) ++bbits;
+        while (bbits < max_bits && ((int64_t)1 << bbits) * fit < eg) ++bbits;
     }
-    if (bbits > 12) bbits = 12;
+    if (bbits > max_bits) bbits = max_bits;
     a->B = a->nokey ? 1 : (1u << bbits);
     // LDS table geometry: room for a bucket's expected groups with 25% slack and headroom for one
     // step of in-flight inserts.  Power-of-two tables up to LDS_TABLE_BYTES (fill <= 5/8; 2-3

@@ -4,6 +4,10 @@
 // 416-455): right-trim ' ' (RightTrim, CollatorCompare.h:56-61), decode UTF-8 (decodeUtf8Char,
 // Collator.cpp:43-74, no validation), and emit each character's 16-bit weight big-endian
 // (GeneralCICollator::weight, Collator.h:403-407: 0xFFFD past the BMP, else weight_lut).
+// The UCA collators (utf8mb4_unicode_ci = UCACICollator<Unicode0400, padding>, utf8mb4_0900_ai_ci
+// = UCACICollator<Unicode0900, no padding>; sortKey = convertImpl, Collator.cpp:580-629) skip
+// zero-weight characters and write each character's weight words (one or two u64 of 16-bit
+// chunks, low chunk first, each big-endian: writeResult, Collator.h:336-344).
 // Every consumer of a String key under such a collator (weak hash, GROUP BY keys, join keys)
 // hashes / compares the sort key, so the key column is collated once into a sort-key column in
 // the ColumnString layout (bytes + '\0' per row, UInt64 end offsets) and the byte-wise code
@@ -13,9 +17,12 @@
 
 namespace tfg {
 
-inline bool collator_transforms(int collator) { return collator == TFG_COLLATOR_GENERAL_CI; }
+inline bool collator_transforms(int collator) {
+    return collator == TFG_COLLATOR_GENERAL_CI || collator == TFG_COLLATOR_UNICODE_CI ||
+           collator == TFG_COLLATOR_UCA0900_AI_CI;
+}
 inline bool collator_known(int collator) {
-    return collator >= TFG_COLLATOR_NONE && collator <= TFG_COLLATOR_GENERAL_CI;
+    return collator >= TFG_COLLATOR_NONE && collator <= TFG_COLLATOR_UCA0900_AI_CI;
 }
 
 // A collated column in stream-ordered device memory, freed (stream-ordered) with the object.

@@ -1,6 +1,9 @@
-// collation.hip — utf8mb4_general_ci sort keys (see collation.h for the reference map).
+// collation.hip — sort keys of the case-insensitive collators (see collation.h for the reference map).
+#include <mutex>
+
 #include "collation.h"
 #include "collation_data.h"
+#include "uca_data.h"
 
 namespace tfg {
 
@@ -103,6 +106,124 @@ __global__ void gci_write_kernel(const uint8_t *chars, const uint64_t *offsets, 
     }
 }
 
+// ---------------------------------------------------------------- UCA (unicode_ci, 0900_ai_ci)
+// The weight LUTs live expanded in device memory (0.5 MB + 1.4 MB, one per device), filled once
+// from their runs (uca_data.h); long weights are searched in a 22 / 27-entry table.
+struct UcaRun {
+    uint32_t start, count;
+    uint64_t base, delta;
+};
+struct UcaLong {
+    uint32_t cp;
+    uint64_t first, second;
+};
+__device__ const UcaRun uca0400_runs_dev[TFG_UCA0400_NRUNS] = {TFG_UCA0400_RUNS_INIT};
+__device__ const UcaRun uca0900_runs_dev[TFG_UCA0900_NRUNS] = {TFG_UCA0900_RUNS_INIT};
+__constant__ UcaLong uca0400_long_dev[TFG_UCA0400_NLONG] = {TFG_UCA0400_LONG_INIT};
+__constant__ UcaLong uca0900_long_dev[TFG_UCA0900_NLONG] = {TFG_UCA0900_LONG_INIT};
+__device__ uint64_t uca0400_lut_dev[TFG_UCA0400_SIZE];
+__device__ uint64_t uca0900_lut_dev[TFG_UCA0900_SIZE];
+
+// one workgroup per run
+__global__ void uca_expand_kernel(int v0900) {
+    const UcaRun r = v0900 ? uca0900_runs_dev[blockIdx.x] : uca0400_runs_dev[blockIdx.x];
+    uint64_t *lut = v0900 ? uca0900_lut_dev : uca0400_lut_dev;
+    for (uint32_t k = threadIdx.x; k < r.count; k += blockDim.x) lut[r.start + k] = r.base + (uint64_t)k * r.delta;
+}
+
+// Unicode0400::weight / Unicode0900::weight (Collator.cpp:703-727, 791-816): false = a
+// zero-weight character (skipped)
+template <bool V0900>
+__device__ __forceinline__ bool uca_weight(uint32_t r, uint64_t &first, uint64_t &second) {
+    second = 0;
+    if (!V0900 && r > 0xFFFFu) {
+        first = 0xFFFDu;
+        return true;
+    }
+    if (V0900 && r >= (uint32_t)TFG_UCA0900_SIZE) { // implicit weight (the reference reads one past its LUT at 0x2CEA1)
+        first = (uint64_t)(r >> 15) + 0xFBC0u + ((uint64_t)((r & 0x7FFFu) | 0x8000u) << 16);
+        return true;
+    }
+    const uint64_t w = V0900 ? uca0900_lut_dev[r] : uca0400_lut_dev[r];
+    if (w == 0) return false;
+    if (w != 0xFFFDu) {
+        first = w;
+        return true;
+    }
+    first = 0; // weightLutLongMap's default entry {0, 0}
+    const int nl = V0900 ? TFG_UCA0900_NLONG : TFG_UCA0400_NLONG;
+    for (int i = 0; i < nl; ++i) {
+        const UcaLong &e = V0900 ? uca0900_long_dev[i] : uca0400_long_dev[i];
+        if (e.cp == r) {
+            first = e.first;
+            second = e.second;
+        }
+    }
+    return true;
+}
+
+// bytes writeResult (Collator.h:336-344) emits for a weight word: two per non-zero 16-bit chunk
+// from the low end
+__device__ __forceinline__ uint32_t uca_chunk_bytes(uint64_t w) { return w ? 2u * ((64u - __clzll(w) + 15u) / 16u) : 0u; }
+
+// 0400 pads (right-trims ' '); 0900 keeps trailing spaces
+template <bool V0900>
+__device__ __forceinline__ RowSpan uca_span(const uint8_t *chars, const uint64_t *offsets, const uint8_t *nullmap, int64_t r) {
+    RowSpan sp = row_span(chars, offsets, nullmap, r);
+    if (V0900 && !(nullmap && nullmap[r])) sp.len = (uint64_t)(sp.limit - sp.s) - 1;
+    return sp;
+}
+
+template <bool V0900>
+__global__ void uca_len_kernel(const uint8_t *chars, const uint64_t *offsets, const uint8_t *nullmap,
+                               const uint32_t *s32, const uint64_t *s64, int64_t n, uint64_t *len_out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const RowSpan sp = uca_span<V0900>(chars, offsets, nullmap, pick(s32, s64, i));
+        uint64_t off = 0, bytes = 0;
+        while (off < sp.len) {
+            uint64_t f, s;
+            if (uca_weight<V0900>(decode_utf8(sp, off), f, s)) bytes += uca_chunk_bytes(f) + uca_chunk_bytes(s);
+        }
+        len_out[i] = bytes + 1; // then '\0'
+    }
+}
+
+template <bool V0900>
+__global__ void uca_write_kernel(const uint8_t *chars, const uint64_t *offsets, const uint8_t *nullmap,
+                                 const uint32_t *s32, const uint64_t *s64, int64_t n, const uint64_t *start,
+                                 uint8_t *out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const RowSpan sp = uca_span<V0900>(chars, offsets, nullmap, pick(s32, s64, i));
+        uint8_t *o = out + start[i];
+        uint64_t off = 0;
+        while (off < sp.len) {
+            uint64_t w[2];
+            if (!uca_weight<V0900>(decode_utf8(sp, off), w[0], w[1])) continue;
+            for (int h = 0; h < 2; ++h)
+                for (uint64_t x = w[h]; x != 0; x >>= 16) {
+                    *o++ = (uint8_t)(x >> 8);
+                    *o++ = (uint8_t)x;
+                }
+        }
+        *o = 0;
+    }
+}
+
+// the expanded LUTs of device `dev` (filled on its first UCA collation)
+int uca_ready(Ctx *ctx) {
+    static std::mutex mu;
+    static bool ready[64];
+    std::lock_guard<std::mutex> lk(mu);
+    TFG_CHECK(ctx->device >= 0 && ctx->device < 64, TFG_ERR_INVALID_ARG, "device %d", ctx->device);
+    if (ready[ctx->device]) return TFG_OK;
+    hipLaunchKernelGGL(uca_expand_kernel, dim3(TFG_UCA0400_NRUNS), dim3(256), 0, ctx->stream, 0);
+    hipLaunchKernelGGL(uca_expand_kernel, dim3(TFG_UCA0900_NRUNS), dim3(256), 0, ctx->stream, 1);
+    TFG_LAUNCH_CHECK();
+    TFG_HIP(hipStreamSynchronize(ctx->stream));
+    ready[ctx->device] = true;
+    return TFG_OK;
+}
+
 } // namespace
 
 CollatedStrings::~CollatedStrings() {
@@ -113,8 +234,11 @@ CollatedStrings::~CollatedStrings() {
 
 int collate_strings(Ctx *ctx, int collator, const uint8_t *chars, const uint64_t *offsets, const uint8_t *nullmap,
                     const uint32_t *sel32, const uint64_t *sel64, int64_t n, CollatedStrings &out) {
-    TFG_CHECK(collator == TFG_COLLATOR_GENERAL_CI, TFG_ERR_NOT_IMPLEMENTED, "collator %d has no sort-key transform",
+    TFG_CHECK(collator_transforms(collator), TFG_ERR_NOT_IMPLEMENTED, "collator %d has no sort-key transform",
               collator);
+    const bool uca = collator != TFG_COLLATOR_GENERAL_CI, v0900 = collator == TFG_COLLATOR_UCA0900_AI_CI;
+    if (uca)
+        if (int rc = uca_ready(ctx)) return rc;
     TFG_CHECK(n >= 0 && n <= ((int64_t)1 << 26), TFG_ERR_INVALID_ARG, "collated column of %lld rows", (long long)n);
     out.ctx = ctx;
     out.rows = n;
@@ -128,8 +252,15 @@ int collate_strings(Ctx *ctx, int collator, const uint8_t *chars, const uint64_t
     uint64_t *len = nullptr;
     TFG_HIP(hipMallocAsync((void **)&len, (size_t)n * 8, ctx->stream));
     const unsigned grid = stream_grid(n, 256, 4096);
-    hipLaunchKernelGGL(gci_len_kernel, dim3(grid), dim3(256), 0, ctx->stream, chars, offsets, nullmap, sel32, sel64, n,
-                       len);
+    if (!uca)
+        hipLaunchKernelGGL(gci_len_kernel, dim3(grid), dim3(256), 0, ctx->stream, chars, offsets, nullmap, sel32, sel64,
+                           n, len);
+    else if (v0900)
+        hipLaunchKernelGGL(uca_len_kernel<true>, dim3(grid), dim3(256), 0, ctx->stream, chars, offsets, nullmap, sel32,
+                           sel64, n, len);
+    else
+        hipLaunchKernelGGL(uca_len_kernel<false>, dim3(grid), dim3(256), 0, ctx->stream, chars, offsets, nullmap, sel32,
+                           sel64, n, len);
     TFG_LAUNCH_CHECK();
     void *tmp = nullptr;
     TFG_HIP(hipMallocAsync(&tmp, scan_tmp_bytes(n) + 256, ctx->stream));
@@ -137,8 +268,15 @@ int collate_strings(Ctx *ctx, int collator, const uint8_t *chars, const uint64_t
     uint64_t total = 0;
     if (int rc = read_back_u64(ctx, out.scan + n, &total, 1)) return rc;
     TFG_HIP(hipMallocAsync((void **)&out.chars, total + 16, ctx->stream));
-    hipLaunchKernelGGL(gci_write_kernel, dim3(grid), dim3(256), 0, ctx->stream, chars, offsets, nullmap, sel32, sel64, n,
-                       out.scan, out.chars);
+    if (!uca)
+        hipLaunchKernelGGL(gci_write_kernel, dim3(grid), dim3(256), 0, ctx->stream, chars, offsets, nullmap, sel32, sel64,
+                           n, out.scan, out.chars);
+    else if (v0900)
+        hipLaunchKernelGGL(uca_write_kernel<true>, dim3(grid), dim3(256), 0, ctx->stream, chars, offsets, nullmap, sel32,
+                           sel64, n, out.scan, out.chars);
+    else
+        hipLaunchKernelGGL(uca_write_kernel<false>, dim3(grid), dim3(256), 0, ctx->stream, chars, offsets, nullmap, sel32,
+                           sel64, n, out.scan, out.chars);
     TFG_LAUNCH_CHECK();
     TFG_HIP(hipFreeAsync(len, ctx->stream));
     TFG_HIP(hipFreeAsync(tmp, ctx->stream));
