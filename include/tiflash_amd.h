@@ -43,6 +43,7 @@ extern "C" {
 #define TFG_ERR_CAPACITY (-8)           /* output buffer too small (caller retries larger) */
 #define TFG_ERR_NO_DEVICE (-9)          /* no HIP device visible */
 #define TFG_ERR_FAULT_INJECTED (-10)    /* test-only failpoint (TFG_FAILPOINT env var) */
+#define TFG_ERR_OVERFLOW (-11)          /* DECIMAL_OVERFLOW ("Decimal math overflow") */
 
 /* ---------------------------------------------------------------- column types */
 /* Native fixed-width column payloads (ColumnVector<T> / ColumnDecimal<T>). Decimal columns
@@ -199,8 +200,13 @@ int tfg_mask_logic(tfg_ctx *ctx, int op, const uint8_t *a, const uint8_t *b, int
 /* out[i] = a[i] op b[i] (FunctionBinaryArithmetic.h:761-1200, DecimalBinaryOperation :231-500).
  * Either side may be a constant (`*_is_const` != 0: the pointer is a HOST pointer to one value).
  * Decimal operands are aligned to the result scale for +/- (applyScaled) and multiplied raw for
- * * (result scale = a_scale + b_scale, MulDecimalInferer, Common/Decimal.h:109-163).
- * Integer results wrap like the reference's native ops; Decimal128 results are exact Int128. */
+ * * (result scale = a_scale + b_scale, MulDecimalInferer, Common/Decimal.h:109-163); a multiply
+ * whose result scale is capped below a_scale + b_scale (decimal_max_scale 30) divides the product
+ * by 10^(a_scale + b_scale - res_scale), truncating (DataTypeDecimal::getScales).
+ * Integer results wrap like the reference's native ops; Decimal128 results are exact Int128.
+ * Decimal256 results / operands: exact 256-bit values (computed in 512 bits, PromoteType<Int256>);
+ * TFG_ERR_OVERFLOW when a value does not fit Int256, or when a Decimal256 operand's result
+ * exceeds 10^65 - 1 (DecimalBinaryOperation::check_overflow, FunctionBinaryArithmetic.h:250-252). */
 int tfg_arith(tfg_ctx *ctx, int op, int a_type, const void *a, int a_is_const, int a_scale, int b_type,
               const void *b, int b_is_const, int b_scale, int res_type, int res_scale, int64_t n, void *out);
 

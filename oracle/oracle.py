@@ -211,6 +211,36 @@ def arith(op, a, b, res_type, a_type=None, b_type=None, a_const=False, b_const=F
     return out
 
 
+def arith_decimal_wide(op, a, b, a_type, b_type, a_scale, b_scale, res_type, res_scale):
+    """Decimal arithmetic with exact integers (Python ints in, Python ints out) for Decimal256
+    results / operands and multiplies with a capped result scale: DecimalBinaryOperation
+    (Functions/FunctionBinaryArithmetic.h:231-640).  +/-: the operand of lower scale is scaled up to
+    the result scale (DataTypeDecimal::getScales, DataTypes/DataTypeDecimal.h:96-123, applyScaled);
+    *: the raw product divided by 10^(sa + sb - res_scale), truncating toward zero (applyScaledMul).
+    A Decimal256 result must fit Int256 (boost checked_int256_t, common/types.h:35), and when an
+    operand is Decimal256 too (need_promote_type) must not exceed 10^65 - 1 (check_overflow,
+    DecimalMaxValue): else OverflowError, the reference's DECIMAL_OVERFLOW.  Small inputs only
+    (pure Python)."""
+    dec = (11, 12, 13, 14)
+    sa = a_scale if a_type in dec else 0
+    sb = b_scale if b_type in dec else 0
+    promote = res_type == 14 and 14 in (a_type, b_type)
+    out = []
+    for x, y in zip(a, b):
+        if op == 2:
+            r = x * y
+            k = 10 ** (sa + sb - res_scale)
+            r = abs(r) // k * (1 if r >= 0 else -1)
+        else:
+            x *= 10 ** (res_scale - sa)
+            y *= 10 ** (res_scale - sb)
+            r = x + y if op == 0 else x - y
+        if res_type == 14 and (not -(1 << 255) <= r < (1 << 255) or (promote and r > 10 ** 65 - 1)):
+            raise OverflowError("Decimal math overflow")
+        out.append(r)
+    return out
+
+
 class Agg:
     """Reference-semantics Aggregator (HashMap key64 + sum/count states)."""
 

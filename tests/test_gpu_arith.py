@@ -90,7 +90,7 @@ def _run_case(tfa, ctx, dev, orc, rng, ta, pa, sa, tb, pb, sb, op, mode):
     if pa is not None or pb is not None:
         rt, _, rs = _dec_result(op, pa if pa is not None else INT_PREC[ta], sa, pb if pb is not None else INT_PREC[tb], sb)
         if rt is None:
-            return False  # Decimal256 result: not on the path (NOT_IMPLEMENTED)
+            return False  # Decimal256 result: tests/test_gpu_arith_wide.py
     elif ta in (F32, F64) or tb in (F32, F64):
         rt, rs = F64, 0
     else:
@@ -136,10 +136,8 @@ def test_arith_decimal_scale_alignment_known_values(tfa, ctx, dev):
     assert s.cpu().tolist() == [705]
 
 
-def test_arith_rejects_decimal256_and_float_decimal(tfa, ctx, dev):
+def test_arith_rejects_float_decimal(tfa, ctx, dev):
     a = torch.zeros(4, dtype=torch.int64, device=dev)
-    with pytest.raises(tfa.TfgError):
-        tfa.arith(ctx, 0, a, a, 14, a_type=D64, b_type=D64, a_scale=0, b_scale=0, res_scale=0)
     f = torch.zeros(4, dtype=torch.float64, device=dev)
     with pytest.raises(tfa.TfgError):
         tfa.arith(ctx, 0, a, f, D64, a_type=D64, b_type=F64)

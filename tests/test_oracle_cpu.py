@@ -370,3 +370,15 @@ def test_oracle_uca_special_weights(orc):
     r = 0x30000
     w = (r >> 15) + 0xFBC0 + (((r & 0x7FFF) | 0x8000) << 16)
     assert key("\U00030000", 5) == bytes.fromhex("%04x%04x" % (w & 0xFFFF, w >> 16))
+
+
+def test_oracle_decimal_wide_rules(orc):
+    D128, D256, D64, I64 = 13, 14, 12, 4
+    """The oracle's rules on hand-derived values (CPU-side restatement checks)."""
+    assert orc.arith_decimal_wide(2, [-7], [3], D128, D128, 16, 16, D128, 30) == [0]      # -21 / 100 -> 0
+    assert orc.arith_decimal_wide(2, [-700], [3], D128, D128, 16, 16, D128, 30) == [-21]  # truncation toward 0
+    assert orc.arith_decimal_wide(0, [1], [2], D64, D256, 2, 0, D256, 2) == [201]
+    with pytest.raises(OverflowError):
+        orc.arith_decimal_wide(0, [10 ** 65 - 1], [1], D256, I64, 0, 0, D256, 0)
+    # no Decimal256 operand: only the Int256 range applies (10^65 + x is representable)
+    assert orc.arith_decimal_wide(0, [10 ** 38 - 1], [1], D128, D128, 0, 38, D256, 38) == [(10 ** 38 - 1) * 10 ** 38 + 1]

@@ -21,10 +21,11 @@ LIB_PATH = os.path.join(_HERE, "libtiflash_amd.so")
 TFG_OK = 0
 ERRORS = {
     -1: "INVALID_ARG", -2: "HIP", -3: "OOM", -4: "NOT_IMPLEMENTED", -5: "SIZE_MISMATCH",
-    -6: "ILLEGAL_TYPE", -7: "LOGICAL", -8: "CAPACITY", -9: "NO_DEVICE", -10: "FAULT_INJECTED",
+    -6: "ILLEGAL_TYPE", -7: "LOGICAL", -8: "CAPACITY", -9: "NO_DEVICE", -10: "FAULT_INJECTED", -11: "OVERFLOW",
 }
 TFG_ERR_CAPACITY = -8
 TFG_ERR_NO_DEVICE = -9
+TFG_ERR_OVERFLOW = -11
 
 INT8, INT16, INT32, INT64, UINT8, UINT16, UINT32, UINT64, FLOAT32, FLOAT64 = range(1, 11)
 DECIMAL32, DECIMAL64, DECIMAL128, DECIMAL256 = 11, 12, 13, 14
@@ -111,6 +112,10 @@ def _int_array(xs) -> ctypes.Array:
 
 
 def _scalar(type_: int, value):
+    if type_ in (DECIMAL128, DECIMAL256):  # a Python int as little-endian two's complement limbs
+        limbs = 2 if type_ == DECIMAL128 else 4
+        v = int(value) % (1 << (64 * limbs))
+        return (ctypes.c_uint64 * limbs)(*[(v >> (64 * k)) & ((1 << 64) - 1) for k in range(limbs)])
     return _CTYPE[type_](value)
 
 
@@ -284,7 +289,8 @@ def filter_string(ctx: Context, mask, chars, offsets):
 # ---- a3 arithmetic ----------------------------------------------------------------------------
 def arith(ctx: Context, op: int, a, b, res_type: int, a_type=None, b_type=None, a_scale=0, b_scale=0, res_scale=0,
           n=None, device=None):
-    """a/b: tensors or Python scalars (constants); Decimal128 results are (n, 2) int64 tensors."""
+    """a/b: tensors or Python scalars (constants); Decimal128 / Decimal256 operands and results are
+    (n, 2) / (n, 4) int64 tensors of little-endian limbs (constants: Python ints)."""
     import torch
     a_const, b_const = not hasattr(a, "data_ptr"), not hasattr(b, "data_ptr")
     if n is None:

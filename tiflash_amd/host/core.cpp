@@ -15,6 +15,7 @@ void check(int status, const char *what) {
     case TFG_ERR_ILLEGAL_TYPE: code = ErrorCodes::ILLEGAL_TYPE_OF_ARGUMENT; break;
     case TFG_ERR_NOT_IMPLEMENTED: code = ErrorCodes::NOT_IMPLEMENTED; break;
     case TFG_ERR_OOM: code = ErrorCodes::CANNOT_ALLOCATE_MEMORY; break;
+    case TFG_ERR_OVERFLOW: code = ErrorCodes::DECIMAL_OVERFLOW; break;
     default: break;
     }
     throw Exception(std::string(what) + ": " + tfg_last_error(), code);

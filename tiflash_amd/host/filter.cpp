@@ -107,11 +107,7 @@ DataType arithResult(int op, const DataType &a, const DataType &b) {
             scale = std::max(sa, sb);
             prec = std::min(std::max(pa - sa, pb - sb) + scale + 1, 65);
         }
-        r = DataType::decimal(prec, scale, r.nullable);
-        if (r.type == TFG_DECIMAL256)
-            throw Exception("Decimal256 arithmetic result " + r.getName() + " is not on the path",
-                            ErrorCodes::NOT_IMPLEMENTED);
-        return r;
+        return DataType::decimal(prec, scale, r.nullable); // Decimal256 past precision 38
     }
     if (isFloat(a.type) || isFloat(b.type)) {
         r.type = TFG_FLOAT64;

@@ -40,6 +40,7 @@ constexpr int LOGICAL_ERROR = 49;
 constexpr int ILLEGAL_TYPE_OF_COLUMN_FOR_FILTER = 59;
 constexpr int CANNOT_ALLOCATE_MEMORY = 173;
 constexpr int NOT_FOUND_COLUMN_IN_BLOCK = 10;
+constexpr int DECIMAL_OVERFLOW = 446;
 } // namespace ErrorCodes
 
 class Exception : public std::runtime_error {
