@@ -256,6 +256,9 @@ __global__ void arith_wide_kernel(int op, WideSide a, WideSide b, int res_type, 
     }
 }
 
+// any decimal type, Decimal256 included
+static inline bool is_dec(int t) { return is_decimal_type(t) || t == TFG_DECIMAL256; }
+
 static __int128 pow10_128(int e) {
     __int128 r = 1;
     while (e-- > 0) r *= 10;
@@ -295,7 +298,7 @@ static int make_side(int type, const void *p, int is_const, int scale, int res_t
 // the wide path: Decimal256 results / operands, and multiplies with a capped result scale
 static int arith_wide(Ctx *ctx, int op, int a_type, const void *a, int a_is_const, int a_scale, int b_type,
                       const void *b, int b_is_const, int b_scale, int res_type, int res_scale, int64_t n, void *out) {
-    const int sa = is_decimal_type(a_type) ? a_scale : 0, sb = is_decimal_type(b_type) ? b_scale : 0;
+    const int sa = is_dec(a_type) ? a_scale : 0, sb = is_dec(b_type) ? b_scale : 0;
     TFG_CHECK(!is_float_type(a_type) && !is_float_type(b_type), TFG_ERR_ILLEGAL_TYPE, "decimal result with a float operand");
     TFG_CHECK(a && b, TFG_ERR_INVALID_ARG, "null operand");
     WideSide ws[2];
@@ -363,12 +366,12 @@ extern "C" int tfg_arith(tfg_ctx *ctx, int op, int a_type, const void *a, int a_
     TFG_CHECK(ctx && (n == 0 || out), TFG_ERR_INVALID_ARG, "null argument");
     TFG_CHECK(op >= TFG_PLUS && op <= TFG_MULTIPLY, TFG_ERR_NOT_IMPLEMENTED, "arithmetic op %d", op);
     TFG_CHECK(type_width(res_type) > 0, TFG_ERR_NOT_IMPLEMENTED, "unsupported result type %d", res_type);
-    TFG_CHECK(!(is_decimal_type(res_type) && (is_float_type(a_type) || is_float_type(b_type))), TFG_ERR_ILLEGAL_TYPE,
+    TFG_CHECK(!(is_dec(res_type) && (is_float_type(a_type) || is_float_type(b_type))), TFG_ERR_ILLEGAL_TYPE,
               "decimal result with a float operand");
-    TFG_CHECK(is_decimal_type(res_type) || (a_type != TFG_DECIMAL256 && b_type != TFG_DECIMAL256), TFG_ERR_ILLEGAL_TYPE,
+    TFG_CHECK(is_dec(res_type) || (a_type != TFG_DECIMAL256 && b_type != TFG_DECIMAL256), TFG_ERR_ILLEGAL_TYPE,
               "Decimal256 operand with a non-decimal result");
-    const bool capped_mul = is_decimal_type(res_type) && op == TFG_MULTIPLY &&
-                            (is_decimal_type(a_type) ? a_scale : 0) + (is_decimal_type(b_type) ? b_scale : 0) != res_scale;
+    const bool capped_mul = is_dec(res_type) && op == TFG_MULTIPLY &&
+                            (is_dec(a_type) ? a_scale : 0) + (is_dec(b_type) ? b_scale : 0) != res_scale;
     if (res_type == TFG_DECIMAL256 || a_type == TFG_DECIMAL256 || b_type == TFG_DECIMAL256 || capped_mul) {
         if (int rc = set_device(ctx)) return rc;
         return arith_wide(ctx, op, a_type, a, a_is_const, a_scale, b_type, b, b_is_const, b_scale, res_type, res_scale, n,
