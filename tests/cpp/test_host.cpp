@@ -1393,6 +1393,45 @@ TEST(DecimalArithInferers) {
     EXPECT(bad == 0);
 }
 
+// Past precision 38 the inferers give Decimal256 (createDecimal): Decimal(38,2) + Decimal(38,2) ->
+// Decimal(39,2) and Decimal(20,16) * Decimal(20,16) -> Decimal(40,30), whose scale is capped at
+// 30 (the product divided by 10^2, truncating); values vs __int128 arithmetic on small inputs.
+TEST(DecimalArithDecimal256Results) {
+    const size_t n = 777;
+    std::mt19937_64 rng(9);
+    std::vector<__int128> a(n), b(n);
+    for (size_t i = 0; i < n; ++i) {
+        a[i] = (__int128)((int64_t)(rng() >> 1) - (int64_t)(1ll << 61)) * 1000003;
+        b[i] = (__int128)((int64_t)(rng() % 2000001) - 1000000);
+    }
+    DataType t38 = DataType::decimal(38, 2), t20 = DataType::decimal(20, 16);
+    Block blk{{makeColumn(ctx, t38, a.data(), n), t38, "a"}, {makeColumn(ctx, t38, b.data(), n), t38, "b"},
+              {makeColumn(ctx, t20, a.data(), n), t20, "c"}, {makeColumn(ctx, t20, b.data(), n), t20, "d"}};
+    auto e = std::make_shared<ExpressionActions>(ctx);
+    e->arithmetic(TFG_PLUS, "a", "b", "p");
+    e->arithmetic(TFG_MULTIPLY, "c", "d", "x");
+    e->execute(blk);
+    const IColumn &p = *blk.getByName("p").column, &x = *blk.getByName("x").column;
+    EXPECT(p.type.type == TFG_DECIMAL256 && p.type.getName() == "Decimal(39,2)");
+    EXPECT(x.type.type == TFG_DECIMAL256 && x.type.getName() == "Decimal(40,30)");
+    struct L4 {
+        uint64_t w[4];
+    };
+    auto hp = toHost<L4>(ctx, p), hx = toHost<L4>(ctx, x);
+    auto low128 = [](const L4 &v) { return (__int128)(((unsigned __int128)v.w[1] << 64) | v.w[0]); };
+    auto ext_ok = [](const L4 &v) {
+        const uint64_t s = (int64_t)v.w[1] < 0 ? ~0ull : 0ull;
+        return v.w[2] == s && v.w[3] == s;
+    };
+    size_t bad = 0;
+    for (size_t i = 0; i < n; ++i) {
+        const __int128 prod = a[i] * b[i], q = prod / 100; // C++ division truncates toward zero
+        bad += !ext_ok(hp[i]) || low128(hp[i]) != a[i] + b[i];
+        bad += !ext_ok(hx[i]) || low128(hx[i]) != q;
+    }
+    EXPECT(bad == 0);
+}
+
 // ================================================================ pipeline engine (b)
 // The reference's operator contract (Operators/Operator.h:32-173) driven the way its
 // PipelineExec does (PipelineExec.cpp:120-180), two execs per pipeline, results vs the oracle.

@@ -316,11 +316,15 @@ struct SelWideStr {
 // RG_TR rows that hold one coarse bucket each, and counting-sorts every tile by the next
 // `fine` = 6 bits: the bucket kernel of (coarse c, fine f) then reads runs of ~RG_TR / 64 rows
 // from the tiles [tile_base[c], tile_base[c + 1]).
-constexpr int RG_T = 1024;
 #ifndef TFG_RG_TR
-#define TFG_RG_TR 3072
+#define TFG_RG_TR 1536
 #endif
+#ifndef TFG_RG_T
+#define TFG_RG_T 512
+#endif
+constexpr int RG_T = TFG_RG_T;
 constexpr int RG_TR = TFG_RG_TR;
+constexpr int RG_W = 1024; // pass-1 runs staged in LDS per window
 constexpr int RG_FINE_BITS = 6;
 constexpr int RG_FINE = 1 << RG_FINE_BITS;
 
@@ -414,7 +418,7 @@ __global__ void __launch_bounds__(RG_T) regroup_tiled_kernel(const uint64_t *rec
                                                              const uint32_t *runpref, const RgDesc *desc,
                                                              uint32_t fine_shift, uint64_t *rec2, uint32_t *hist2, int T2) {
     __shared__ uint64_t stage[RG_TR * NCOL];
-    __shared__ uint32_t rpref[RG_TR + 2], rent[RG_TR + 2];
+    __shared__ uint32_t rpref[RG_W + 2], rent[RG_W + 2];
     __shared__ uint32_t fh[RG_FINE], fs[RG_FINE];
     const int k = blockIdx.x;
     const RgDesc d = desc[k];
@@ -431,10 +435,10 @@ __global__ void __launch_bounds__(RG_T) regroup_tiled_kernel(const uint64_t *rec
     int64_t row[PER];
 #pragma unroll
     for (int q = 0; q < PER; ++q) row[q] = -1;
-    // the runs t0 .. t0 + m - 1 in windows of RG_TR (more than one only when empty runs of a
-    // sparse coarse bucket pile up): a row's run is the last j with rpref[j] <= x
-    for (int w0 = 0; w0 < m; w0 += RG_TR) {
-        const int wm = min(RG_TR, m - w0);
+    // the runs t0 .. t0 + m - 1 in windows of RG_W (more than one only when many short or empty
+    // runs of a sparse coarse bucket pile up): a row's run is the last j with rpref[j] <= x
+    for (int w0 = 0; w0 < m; w0 += RG_W) {
+        const int wm = min(RG_W, m - w0);
         for (int j = threadIdx.x; j <= wm; j += RG_T) {
             rpref[j] = pr[t0 + w0 + j];
             rent[j] = j < wm ? hc[t0 + w0 + j] : 0u;
