@@ -469,8 +469,8 @@ int tfg_alltoallv(tfg_comm *comm, const void *send, const uint64_t *send_bytes, 
  *                      (Flash/Coprocessor/CHBlockChunkCodecV1.cpp:370-432, 567-583); decode accepts
  *                      packets of several parts (decodeColumnsByBlock, :97-142), and LZ4
  *                      packets (method byte 0x82: CompressedCHBlockChunkReadBuffer, :567-581)
- *                      are decompressed on the device first.  ZSTD packets return
- *                      TFG_ERR_NOT_IMPLEMENTED.
+ *                      and ZSTD packets (0x90, the HIGH_COMPRESSION mode) are decompressed on the
+ *                      device first.
  * Type names as on the wire (IDataType::getName): Int8..Int64, UInt8..UInt64, Float32, Float64,
  * Decimal(P,S) with P <= 38, MyDate, MyDateTime(n), MyDuration(n), String (size-prefixed rows),
  * StringV2 (sizes, then chars), and Nullable(...) of each.  Column data follows the tfg_type
@@ -510,8 +510,11 @@ int tfg_codec_packet_destroy(tfg_codec_packet *p);
  * otherwise the exact size, TFG_ERR_CAPACITY when it exceeds `capacity`.  LZ4HC writes the same
  * format and is accepted as LZ4.
  * tfg_codec_decompress is CompressedCHBlockChunkReadBuffer over a whole packet: the frames of an
- * LZ4 packet (any frame sizes, as any LZ4 encoder wrote them) become the uncompressed V1 packet
- * (0x02 + body).  out == NULL: the size only.  Malformed frames: TFG_ERR_INVALID_ARG. */
+ * LZ4 packet (any frame sizes, as any LZ4 encoder wrote them) or of a ZSTD packet (frames
+ * `0x90 | UInt32 frame bytes | UInt32 raw bytes | ZSTD frame`, CompressionCodecZSTD.cpp:38-65;
+ * RFC 8878 frames without dictionaries, checksums verified) become the uncompressed V1 packet
+ * (0x02 + body).  out == NULL: the size only.  Malformed frames: TFG_ERR_INVALID_ARG.
+ * tfg_codec_compress writes LZ4 only (ZSTD: TFG_ERR_NOT_IMPLEMENTED). */
 #define TFG_COMPRESSION_LZ4 1
 #define TFG_COMPRESSION_LZ4HC 2
 #define TFG_COMPRESSION_ZSTD 3

@@ -1,0 +1,150 @@
+"""ZSTD MPP packets (§8 f1, HIGH_COMPRESSION mode): CHBlockChunkCodecV1 with CompressionMethod::ZSTD.
+
+Format (reference CHBlockChunkCodecV1.cpp:150-160 picks ZSTD for HC mode; CompressedWriteBuffer
+frames `0x90 | UInt32 frame bytes (header included) | UInt32 raw bytes | ZSTD frame`,
+IO/Compression/CompressionInfo.h:58, CompressionCodecZSTD.cpp:38-65).  ZSTD is a third-party
+dependency the reference links and does not vendor (contrib zstd); the checker here is the system
+libzstd (libzstd.so.1, 1.4.8 in this image — the same published format, RFC 8878), loaded with
+ctypes; nothing of the reference runs.  Parity:
+  CPU: tiflash_amd/csrc/zstd_dec.h (the device decoder's source) built for the host decodes
+       libzstd frames of many shapes (levels 1-19, raw / RLE / compressed blocks, Huffman 1 and 4
+       streams, treeless and repeat tables, checksums, multi-block frames) to the original bytes,
+       and rejects corrupted frames;
+  GPU: tfg_codec_decompress / tfg_codec_decode of ZSTD packets built from libzstd frames return
+       the original packet / columns."""
+import ctypes
+import ctypes.util
+import os
+import struct
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _zstd():
+    try:
+        z = ctypes.CDLL("libzstd.so.1")
+    except OSError:
+        pytest.skip("libzstd.so.1 not present")
+    z.ZSTD_compressBound.restype = ctypes.c_size_t
+    z.ZSTD_compress.restype = ctypes.c_size_t
+    z.ZSTD_isError.restype = ctypes.c_uint
+    z.ZSTD_createCCtx.restype = ctypes.c_void_p
+    z.ZSTD_compress2.restype = ctypes.c_size_t
+    z.ZSTD_CCtx_setParameter.restype = ctypes.c_size_t
+    return z
+
+
+def zcompress(data: bytes, level=3, checksum=False) -> bytes:
+    z = _zstd()
+    cap = z.ZSTD_compressBound(ctypes.c_size_t(len(data)))
+    out = ctypes.create_string_buffer(cap)
+    cctx = ctypes.c_void_p(z.ZSTD_createCCtx())
+    z.ZSTD_CCtx_setParameter(cctx, 100, level)          # ZSTD_c_compressionLevel
+    z.ZSTD_CCtx_setParameter(cctx, 201, int(checksum))  # ZSTD_c_checksumFlag
+    n = z.ZSTD_compress2(cctx, out, ctypes.c_size_t(cap), data, ctypes.c_size_t(len(data)))
+    z.ZSTD_freeCCtx(cctx)
+    assert not z.ZSTD_isError(ctypes.c_size_t(n))
+    return out.raw[:n]
+
+
+def cpu_decode(frame: bytes, cap: int):
+    lib = ctypes.CDLL(os.path.join(ROOT, "tiflash_amd", "host", "build", "libzstd_cpu.so"))
+    lib.tfz_decode_frame_cpu.restype = ctypes.c_int64
+    out = ctypes.create_string_buffer(max(cap, 1))
+    n = lib.tfz_decode_frame_cpu(frame, ctypes.c_int64(len(frame)), out, ctypes.c_uint64(cap))
+    return None if n < 0 else out.raw[:n]
+
+
+def payloads(rng):
+    yield b""
+    yield b"x"
+    yield bytes(100)
+    yield bytes(rng.integers(0, 256, 5000, dtype=np.uint8))               # incompressible: raw blocks
+    yield bytes(300_000)                                                   # RLE blocks
+    yield (b"abc" * 100_000)[:300_001]
+    yield bytes(rng.integers(0, 4, 70_000, dtype=np.uint8))               # skewed literals: Huffman
+    yield b"".join(b"key%08d|" % int(i) for i in rng.integers(0, 1000, 40_000))
+    # a V1 column-ish body: k%08d strings, then Int64s of small range
+    yield (b"".join(b"\x09k%08d" % int(i) for i in rng.integers(0, 10**6, 30_000))
+           + rng.integers(0, 1000, 30_000).astype(np.int64).tobytes())
+    yield bytes(rng.integers(0, 256, 1 << 20, dtype=np.uint8) & 0x0F)     # 1 MB, multi-block
+
+
+def frame(block: bytes, raw: int) -> bytes:
+    return b"\x90" + struct.pack("<II", len(block) + 9, raw) + block
+
+
+# ------------------------------------------------------------------ CPU: the decoder's source vs libzstd
+@pytest.mark.parametrize("level", [1, 3, 9, 19])
+def test_cpu_decoder_matches_libzstd(level):
+    rng = np.random.default_rng(level)
+    for raw in payloads(rng):
+        for ck in (False, True):
+            z = zcompress(raw, level, ck)
+            assert cpu_decode(z, len(raw)) == raw, (level, len(raw), ck)
+
+
+def test_cpu_decoder_rejects_corruption():
+    rng = np.random.default_rng(5)
+    raw = b"".join(b"key%08d|" % int(i) for i in rng.integers(0, 1000, 20_000))
+    z = zcompress(raw, 3, True)
+    assert cpu_decode(z, len(raw) - 1) is None          # does not fit
+    assert cpu_decode(z[:-1], len(raw)) is None         # truncated
+    bad = 0
+    for pos in rng.integers(4, len(z), 200):            # flipped bytes: an error or (rarely) other
+        b = bytearray(z)                                # bytes caught by the checksum — never a crash
+        b[int(pos)] ^= 0x5A
+        bad += cpu_decode(bytes(b), len(raw)) is None
+    assert bad == 200
+    assert cpu_decode(b"\x28\xb5\x2f\xfd", 16) is None  # header only
+
+
+# ------------------------------------------------------------------ GPU: packets
+def dev_bytes(b, dev):
+    import torch
+    return torch.from_numpy(np.frombuffer(b, np.uint8).copy()).to(dev)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("level", [1, 3, 19])
+def test_gpu_decompress_zstd_packets(tfa, ctx, dev, level):
+    rng = np.random.default_rng(20 + level)
+    for raw in payloads(rng):
+        body = raw
+        if not body:
+            continue
+        # the reference writes one frame per CompressedWriteBuffer block (<= 1 MB here); several frames
+        pkt = b"".join(frame(zcompress(body[i:i + 65536], level), len(body[i:i + 65536]))
+                       for i in range(0, len(body), 65536))
+        got = tfa.codec_decompress(ctx, dev_bytes(pkt, dev)).cpu().numpy().tobytes()
+        assert got == b"\x02" + body, (level, len(body))
+
+
+@pytest.mark.gpu
+def test_gpu_decompress_zstd_rejects(tfa, ctx, dev):
+    raw = bytes(range(256)) * 100
+    z = zcompress(raw, 3, True)
+    good = frame(z, len(raw))
+    b = bytearray(good)
+    b[20] ^= 0xFF
+    for bad in (good[:-1], frame(z, len(raw) + 1), bytes(b)):
+        with pytest.raises(tfa.TfgError):
+            tfa.codec_decompress(ctx, dev_bytes(bad, dev))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 5000, 200_000])
+def test_gpu_codec_decode_zstd_packets(tfa, orc, ctx, dev, n):
+    """A V1 packet compressed with ZSTD (HC mode) decodes to the original columns."""
+    from test_codec import V1, assert_decoded, make_block
+    rng = np.random.default_rng(n)
+    cols = make_block(rng, n)
+    plain = orc.codec_encode(cols, n, version=V1)
+    body = plain[1:]
+    pkt = b"".join(frame(zcompress(body[i:i + (1 << 20)], 3), len(body[i:i + (1 << 20)]))
+                   for i in range(0, len(body), 1 << 20))
+    rows, dec = tfa.codec_decode(ctx, dev_bytes(pkt, dev), version=V1)
+    assert_decoded(cols, n, rows, dec)

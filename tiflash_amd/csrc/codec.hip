@@ -41,6 +41,7 @@ namespace tfg {
 
 constexpr uint8_t COMP_NONE = 0x02; // CompressionMethodByte::NONE (IO/Compression/CompressionInfo.h:55)
 constexpr uint8_t COMP_LZ4 = 0x82;  // CompressionMethodByte::LZ4 (frames decompressed by lz4.hip)
+constexpr uint8_t COMP_ZSTD = 0x90; // CompressionMethodByte::ZSTD (frames decompressed by lz4.hip + zstd_dec.h)
 constexpr int LCH = 32768;          // legacy parse chunk bytes
 constexpr int LENT = 256;           // entry offsets per chunk (threads of the map kernel)
 constexpr int LGRP = 64;            // chunks per resolution group
@@ -641,7 +642,7 @@ int tfg_codec_decode(tfg_ctx *ctx, int version, const uint8_t *packet, size_t by
     if (version == TFG_CODEC_V1) {
         uint8_t m;
         if (int rc = rd.byte(m)) return done(rc);
-        if (m == COMP_LZ4) { // CompressedCHBlockChunkReadBuffer: decompress the frames, then read as NONE
+        if (m == COMP_LZ4 || m == COMP_ZSTD) { // CompressedCHBlockChunkReadBuffer: decompress, then read as NONE
             size_t raw = 0;
             if (int rc = tfg_codec_decompress(ctx, packet, bytes, nullptr, 0, &raw)) return done(rc);
             if (hipMalloc(&p->owned, raw) != hipSuccess) return done(fail(TFG_ERR_OOM, "decompressed packet of %zu bytes", raw));
@@ -651,7 +652,7 @@ int tfg_codec_decode(tfg_ctx *ctx, int version, const uint8_t *packet, size_t by
             rd = PacketReader{ctx, p->owned, raw};
             if (int rc = rd.byte(m)) return done(rc);
         } else if (m != COMP_NONE) {
-            return done(fail(TFG_ERR_NOT_IMPLEMENTED, "compressed packet (method byte 0x%02x): NONE and LZ4 only", m));
+            return done(fail(TFG_ERR_NOT_IMPLEMENTED, "compressed packet (method byte 0x%02x): NONE, LZ4 and ZSTD only", m));
         }
     }
     uint64_t ncols, rows;

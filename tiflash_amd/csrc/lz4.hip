@@ -26,11 +26,13 @@
 //    before the match began (other lanes' stores are drained and the loads bypass the L1).
 //  * the frame table of a packet comes from one thread walking the 9-byte headers.
 #include "common.h"
+#include "zstd_dec.h"
 
 namespace tfg {
 namespace {
 
 constexpr uint8_t LZ4_METHOD = 0x82;       // CompressionMethodByte::LZ4
+constexpr uint8_t ZSTD_METHOD = 0x90;      // CompressionMethodByte::ZSTD (zstd_dec.h)
 constexpr uint8_t NONE_METHOD = 0x02;      // CompressionMethodByte::NONE
 constexpr int FRAME_HDR = 9;               // COMPRESSED_BLOCK_HEADER_SIZE
 constexpr uint64_t MAX_FRAME_RAW = 0x40000000ull; // DBMS_MAX_COMPRESSED_SIZE
@@ -182,12 +184,12 @@ __global__ void lz4_pack_kernel(const uint8_t *frames, const uint32_t *sizes, co
 
 // one thread walks the frame headers: foff / roff get frame and raw offsets (exclusive sums, up
 // to max_frames entries); out = {frames, raw bytes, malformed}
-__global__ void lz4_frames_kernel(const uint8_t *pkt, uint64_t bytes, uint64_t *foff, uint64_t *roff, uint64_t max_frames,
-                                  uint64_t *out) {
+__global__ void lz4_frames_kernel(const uint8_t *pkt, uint64_t bytes, uint8_t method, uint64_t *foff, uint64_t *roff,
+                                  uint64_t max_frames, uint64_t *out) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     uint64_t pos = 0, raw = 0, k = 0, bad = 0;
     while (pos < bytes) {
-        if (pos + FRAME_HDR > bytes || pkt[pos] != LZ4_METHOD) {
+        if (pos + FRAME_HDR > bytes || pkt[pos] != method) {
             bad = 1;
             break;
         }
@@ -196,11 +198,13 @@ __global__ void lz4_frames_kernel(const uint8_t *pkt, uint64_t bytes, uint64_t *
             fb |= (uint32_t)pkt[pos + 1 + b] << (8 * b);
             rb |= (uint32_t)pkt[pos + 5 + b] << (8 * b);
         }
-        // a frame may not claim more raw bytes than LZ4 can expand its block to (one token byte
-        // yields at most 255 + 16 raw bytes), nor more than DBMS_MAX_COMPRESSED_SIZE
-        // (IO/Compression/CompressionInfo.h:21), so a forged header cannot size the output
+        // a frame may not claim more raw bytes than its codec can expand its block to (LZ4: one
+        // token byte yields at most 255 + 16 raw bytes; ZSTD: a 4-byte RLE block 128 KB), nor
+        // more than DBMS_MAX_COMPRESSED_SIZE (IO/Compression/CompressionInfo.h:21), so a forged
+        // header cannot size the output
+        const uint64_t expand = method == LZ4_METHOD ? 255 : 32768;
         if (fb <= FRAME_HDR || pos + fb > bytes || rb > MAX_FRAME_RAW ||
-            (uint64_t)rb > (uint64_t)(fb - FRAME_HDR) * 255 + 16) {
+            (uint64_t)rb > (uint64_t)(fb - FRAME_HDR) * expand + 16) {
             bad = 1;
             break;
         }
@@ -290,6 +294,17 @@ __global__ void __launch_bounds__(64) lz4_decode_kernel(const uint8_t *pkt, cons
     if (lane == 0 && (bad || op != raw)) atomicOr(err, 1u);
 }
 
+// One thread per ZSTD frame (zstd_dec.h): the frame body after the 9-byte header must decode to
+// exactly its declared raw size, else err |= 1.  `work` holds one ZWork per frame.
+__global__ void __launch_bounds__(64) zstd_decode_kernel(const uint8_t *pkt, const uint64_t *foff, const uint64_t *roff,
+                                                         uint64_t nframes, uint8_t *dst, tfz::ZWork *work, unsigned *err) {
+    const uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= nframes) return;
+    const uint64_t fb = foff[f + 1] - foff[f], raw = roff[f + 1] - roff[f];
+    const int64_t got = tfz::zstd_frame(pkt + foff[f] + FRAME_HDR, (int64_t)(fb - FRAME_HDR), dst + roff[f], raw, work + f);
+    if (got != (int64_t)raw) atomicOr(err, 1u);
+}
+
 int read_method(Ctx *ctx, const uint8_t *packet, uint8_t *m) {
     TFG_HIP(hipMemcpyAsync(ctx->host_pinned, packet, 1, hipMemcpyDeviceToHost, ctx->stream));
     TFG_HIP(hipStreamSynchronize(ctx->stream));
@@ -366,8 +381,8 @@ int tfg_codec_decompress(tfg_ctx *ctx, const uint8_t *packet, size_t bytes, uint
     if (bytes == 0) return TFG_OK;
     uint8_t m = 0;
     if (int rc = read_method(ctx, packet, &m)) return rc;
-    TFG_CHECK(m == LZ4_METHOD, m == NONE_METHOD ? TFG_ERR_INVALID_ARG : TFG_ERR_NOT_IMPLEMENTED,
-              "method byte 0x%02x: only LZ4 frames decompress", m);
+    TFG_CHECK(m == LZ4_METHOD || m == ZSTD_METHOD, m == NONE_METHOD ? TFG_ERR_INVALID_ARG : TFG_ERR_NOT_IMPLEMENTED,
+              "method byte 0x%02x: only LZ4 and ZSTD frames decompress", m);
     uint64_t max_frames = bytes / (ENC_SLOT / 4) + 16; // grown below when the packet has more
     uint64_t res[3] = {0, 0, 0};
     char *sb = nullptr;
@@ -380,11 +395,11 @@ int tfg_codec_decompress(tfg_ctx *ctx, const uint8_t *packet, size_t bytes, uint
         void *sp;
         if (int rc = scratch_get(ctx, cv.off, &sp)) return rc;
         sb = (char *)sp;
-        hipLaunchKernelGGL(lz4_frames_kernel, dim3(1), dim3(64), 0, ctx->stream, packet, (uint64_t)bytes,
+        hipLaunchKernelGGL(lz4_frames_kernel, dim3(1), dim3(64), 0, ctx->stream, packet, (uint64_t)bytes, m,
                            (uint64_t *)(sb + o_foff), (uint64_t *)(sb + o_roff), max_frames, (uint64_t *)(sb + o_res));
         TFG_LAUNCH_CHECK();
         if (int rc = read_back_u64(ctx, (const uint64_t *)(sb + o_res), res, 3)) return rc;
-        TFG_CHECK(!res[2], TFG_ERR_INVALID_ARG, "malformed LZ4 packet (frame headers)");
+        TFG_CHECK(!res[2], TFG_ERR_INVALID_ARG, "malformed %s packet (frame headers)", m == LZ4_METHOD ? "LZ4" : "ZSTD");
         if (res[0] <= max_frames) break;
         max_frames = res[0];
     }
@@ -397,7 +412,13 @@ int tfg_codec_decompress(tfg_ctx *ctx, const uint8_t *packet, size_t bytes, uint
     TFG_HIP(hipMemsetAsync(out, NONE_METHOD, 1, ctx->stream));
     unsigned *err = (unsigned *)ctx->dev_counter;
     TFG_HIP(hipMemsetAsync(err, 0, sizeof(unsigned), ctx->stream));
-    if (res[0]) {
+    tfz::ZWork *work = nullptr;
+    if (res[0] && m == ZSTD_METHOD) { // per-frame decoder state (tables + a block's literals)
+        TFG_HIP(hipMallocAsync((void **)&work, res[0] * sizeof(tfz::ZWork), ctx->stream));
+        ProfScope _ps(ctx, "codec.zstd.decompress");
+        hipLaunchKernelGGL(zstd_decode_kernel, dim3((unsigned)((res[0] + 63) / 64)), dim3(64), 0, ctx->stream, packet,
+                           (const uint64_t *)(sb + o_foff), (const uint64_t *)(sb + o_roff), res[0], out + 1, work, err);
+    } else if (res[0]) {
         ProfScope _ps(ctx, "codec.lz4.decompress");
         hipLaunchKernelGGL(lz4_decode_kernel, dim3((unsigned)res[0]), dim3(64), 0, ctx->stream, packet,
                            (const uint64_t *)(sb + o_foff), (const uint64_t *)(sb + o_roff), res[0], out + 1, err);
@@ -406,7 +427,8 @@ int tfg_codec_decompress(tfg_ctx *ctx, const uint8_t *packet, size_t bytes, uint
     TFG_HIP(hipMemcpyAsync(ctx->host_pinned, err, sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
     TFG_HIP(hipStreamSynchronize(ctx->stream));
     const unsigned e = *(const unsigned *)ctx->host_pinned;
-    TFG_CHECK(!e, TFG_ERR_INVALID_ARG, "corrupted LZ4 block (Cannot decompress)");
+    if (work) TFG_HIP(hipFree(work));
+    TFG_CHECK(!e, TFG_ERR_INVALID_ARG, "corrupted %s frame (Cannot decompress)", m == LZ4_METHOD ? "LZ4" : "ZSTD");
     return TFG_OK;
 }
 

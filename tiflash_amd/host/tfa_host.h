@@ -509,9 +509,10 @@ private:
 // ---------------------------------------------------------------- packet codec (f1)
 // CHBlockChunkCodec / CHBlockChunkCodecV1 (Flash/Coprocessor/CHBlockChunkCodec.cpp:134-258,
 // CHBlockChunkCodecV1.cpp:370-583) over tfg_codec_*: the packet is a device buffer.  Const
-// columns are materialised first (WriteColumnData).  Differences: compression NONE only (LZ4 /
-// ZSTD packets throw NOT_IMPLEMENTED); encode(vector<Block>) writes one part of the concatenated
-// rows (the reference writes one part per block; decode accepts both).
+// columns are materialised first (WriteColumnData).  encode writes NONE packets (LZ4 frames via
+// tfg_codec_compress); decode accepts NONE, LZ4 and ZSTD (HIGH_COMPRESSION) packets, decompressed
+// on the device.  encode(vector<Block>) writes one part of the concatenated rows (the reference
+// writes one part per block; decode accepts both).
 struct DevicePacket {
     DeviceBufferPtr buf;
     size_t bytes = 0;
