@@ -462,6 +462,60 @@ def lz4_leg(args, ctx, pkt):
     return out
 
 
+def zstd_leg(args, ctx, pkt):
+    """ZSTD packets (CompressionMethod::ZSTD, the HIGH_COMPRESSION mode): a 64 MB prefix of the
+    uncompressed V1 packet body compressed on the host by the system libzstd (level 1, one frame
+    per 1 MB CompressedWriteBuffer block, as the reference's sender writes them), then decompressed
+    on the device (one thread per frame, zstd_dec.h); checked against the packet.  The host
+    decompress of the same frames by libzstd on one thread is reported beside it."""
+    import ctypes
+    import struct
+
+    import torch
+
+    import tiflash_amd as tfa
+    try:
+        z = ctypes.CDLL("libzstd.so.1")
+    except OSError:
+        return {"skipped": "libzstd.so.1 not present"}
+    z.ZSTD_compressBound.restype = ctypes.c_size_t
+    z.ZSTD_compress.restype = ctypes.c_size_t
+    z.ZSTD_decompress.restype = ctypes.c_size_t
+    body = pkt[1:1 + (64 << 20)].cpu().numpy().tobytes()
+    frames, fsz = [], 1 << 20
+    for i in range(0, len(body), fsz):
+        chunk = body[i:i + fsz]
+        cap = z.ZSTD_compressBound(ctypes.c_size_t(len(chunk)))
+        buf = ctypes.create_string_buffer(cap)
+        n = z.ZSTD_compress(buf, ctypes.c_size_t(cap), chunk, ctypes.c_size_t(len(chunk)), 1)
+        frames.append(b"\x90" + struct.pack("<II", n + 9, len(chunk)) + buf.raw[:n])
+    zpkt = b"".join(frames)
+    dz = torch.frombuffer(bytearray(zpkt), dtype=torch.uint8).to(pkt.device)
+    for _ in range(2):
+        back = tfa.codec_decompress(ctx, dz)
+    td = []
+    for _ in range(max(args.steps, 3)):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        back = tfa.codec_decompress(ctx, dz)
+        torch.cuda.synchronize()
+        td.append(time.perf_counter() - t0)
+    assert back[1:].cpu().numpy().tobytes() == body, "ZSTD decompress"
+    d = statistics.median(td)
+    out = {"raw_bytes": len(body), "zstd_bytes": len(zpkt), "frames": len(frames), "ratio": round(len(body) / len(zpkt), 3),
+           "decompress_ms": round(d * 1e3, 3), "decompress_GBps": round(len(body) / d / 1e9, 2)}
+    if not args.no_cpu:
+        dst = ctypes.create_string_buffer(fsz)
+        t0 = time.perf_counter()
+        for f in frames:
+            z.ZSTD_decompress(dst, ctypes.c_size_t(fsz), f[9:], ctypes.c_size_t(len(f) - 9))
+        t1 = time.perf_counter()
+        out["cpu_baseline"] = {"decompress_GBps": round(len(body) / (t1 - t0) / 1e9, 3), "cores": 1,
+                               "kind": "library", "sample": f"the same {len(frames)} frames, system libzstd "
+                               "ZSTD_decompress (the reference's codec library), one host thread"}
+    return out
+
+
 def codec_leg(args, ctx, dev):
     """§8 f1: CHBlockChunkCodecV1 (NONE) encode + decode of a C5-shaped block on the device:
     String "k%08d" key (legacy size-prefixed String, the pre-V2 MPP packet form), Decimal(15,2)
@@ -510,6 +564,7 @@ def codec_leg(args, ctx, dev):
                       "packet_GBps": round(2 * pkt.numel() / (e + d) / 1e9, 1)}
         if label == "string_v2":
             res["lz4"] = lz4_leg(args, ctx, pkt)
+            res["zstd"] = zstd_leg(args, ctx, pkt)
         del pkt, dec
     out = {"metric": "rows/s CHBlockChunkCodecV1 encode + decode (String k%08d, Decimal(15,2), Int64)",
            "value": res["string"]["rows_per_s"], "unit": "rows/s", "rows": n, "legs": res}
