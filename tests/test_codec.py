@@ -210,8 +210,11 @@ def test_gpu_legacy_strings_many_chunks(tfa, orc, ctx, dev):
 @pytest.mark.gpu
 def test_gpu_decode_rejects_bad_packets(tfa, ctx, dev):
     import torch
-    with pytest.raises(tfa.TfgError) as e:  # ZSTD method byte
+    with pytest.raises(tfa.TfgError) as e:  # ZSTD method byte, truncated frame header
         tfa.codec_decode(ctx, torch.tensor([0x90, 1, 0], dtype=torch.uint8, device=dev), version=V1)
+    assert e.value.code == -1
+    with pytest.raises(tfa.TfgError) as e:  # an unknown method byte
+        tfa.codec_decode(ctx, torch.tensor([0x83, 1, 0], dtype=torch.uint8, device=dev), version=V1)
     assert e.value.code == -4
     with pytest.raises(tfa.TfgError) as e:  # LZ4 method byte, truncated frame header
         tfa.codec_decode(ctx, torch.tensor([0x82, 1, 0], dtype=torch.uint8, device=dev), version=V1)

@@ -109,28 +109,39 @@ struct FwdBits {
 // `pos` negative (the overflow the decoders check).
 struct BackBits {
     const uint8_t *p;
+    int64_t nbytes;
     int64_t pos; // bits still unread (from bit 0 of p[0] up)
     ZHD bool init(const uint8_t *buf, int64_t n) {
         p = buf;
+        nbytes = n;
         if (n <= 0) return false;
         const uint8_t last = buf[n - 1];
         if (!last) return false;
         pos = (n - 1) * 8 + highbit(last);
         return true;
     }
-    ZHD uint64_t read(int n) { // n <= 56
-        if (n == 0) return 0;
-        uint64_t v = 0;
-        const int64_t lo = pos - n;
-        for (int64_t b = lo; b < pos; ++b) { // bit-exact and simple; streams are short per thread
-            if (b >= 0) v |= (uint64_t)((p[b >> 3] >> (b & 7)) & 1u) << (b - lo);
+    // bits [lo, lo + n) of the stream (n <= 56, lo >= 0) from the 8 bytes that cover them
+    ZHD uint64_t bits_at(int64_t lo, int n) const {
+        const int64_t b0 = lo >> 3;
+        uint64_t w = 0;
+        if (b0 + 8 <= nbytes) {
+            for (int k = 0; k < 8; ++k) w |= (uint64_t)p[b0 + k] << (8 * k);
+        } else {
+            for (int k = 0; b0 + k < nbytes; ++k) w |= (uint64_t)p[b0 + k] << (8 * k);
         }
-        pos = lo;
-        return v;
+        return (w >> (lo & 7)) & ((1ull << n) - 1);
     }
-    ZHD uint64_t peek(int n) const {
-        BackBits t = *this;
-        return t.read(n);
+    ZHD uint64_t peek(int n) const { // n <= 56; bits below the stream's start read as zeros
+        if (n == 0) return 0;
+        const int64_t lo = pos - n;
+        if (lo >= 0) return bits_at(lo, n);
+        if (pos <= 0) return 0;
+        return bits_at(0, (int)pos) << (-lo);
+    }
+    ZHD uint64_t read(int n) {
+        const uint64_t v = peek(n);
+        pos -= n;
+        return v;
     }
 };
 
