@@ -463,7 +463,7 @@ def lz4_leg(args, ctx, pkt):
 
 
 def zstd_leg(args, ctx, pkt):
-    """ZSTD packets (CompressionMethod::ZSTD, the HIGH_COMPRESSION mode): a 64 MB prefix of the
+    """ZSTD packets (CompressionMethod::ZSTD, the HIGH_COMPRESSION mode): a 64 MB slice of the
     uncompressed V1 packet body compressed on the host by the system libzstd (level 1, one frame
     per 1 MB CompressedWriteBuffer block, as the reference's sender writes them), then decompressed
     on the device (one thread per frame, zstd_dec.h); checked against the packet.  The host
@@ -481,7 +481,10 @@ def zstd_leg(args, ctx, pkt):
     z.ZSTD_compressBound.restype = ctypes.c_size_t
     z.ZSTD_compress.restype = ctypes.c_size_t
     z.ZSTD_decompress.restype = ctypes.c_size_t
-    body = pkt[1:1 + (64 << 20)].cpu().numpy().tobytes()
+    # 64 MB from a quarter into the packet: String chars, not the constant StringV2 sizes column
+    # that opens the body (which compresses ~245x and would make a misleading sample)
+    start = max(1, int(pkt.numel()) // 4)
+    body = pkt[start:start + (64 << 20)].cpu().numpy().tobytes()
     frames, fsz = [], 1 << 20
     for i in range(0, len(body), fsz):
         chunk = body[i:i + fsz]

@@ -294,15 +294,17 @@ __global__ void __launch_bounds__(64) lz4_decode_kernel(const uint8_t *pkt, cons
     if (lane == 0 && (bad || op != raw)) atomicOr(err, 1u);
 }
 
-// One thread per ZSTD frame (zstd_dec.h): the frame body after the 9-byte header must decode to
-// exactly its declared raw size, else err |= 1.  `work` holds one ZWork per frame.
+// One wave per ZSTD frame (zstd_dec.h): the 64 lanes decode in lockstep and split the byte
+// copies; the frame body after the 9-byte header must decode to exactly its declared raw size,
+// else err |= 1.  `work` holds one ZWork per frame.
 __global__ void __launch_bounds__(64) zstd_decode_kernel(const uint8_t *pkt, const uint64_t *foff, const uint64_t *roff,
                                                          uint64_t nframes, uint8_t *dst, tfz::ZWork *work, unsigned *err) {
-    const uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t f = blockIdx.x;
     if (f >= nframes) return;
     const uint64_t fb = foff[f + 1] - foff[f], raw = roff[f + 1] - roff[f];
-    const int64_t got = tfz::zstd_frame(pkt + foff[f] + FRAME_HDR, (int64_t)(fb - FRAME_HDR), dst + roff[f], raw, work + f);
-    if (got != (int64_t)raw) atomicOr(err, 1u);
+    const int64_t got = tfz::zstd_frame(pkt + foff[f] + FRAME_HDR, (int64_t)(fb - FRAME_HDR), dst + roff[f], raw, work + f,
+                                        threadIdx.x, 64);
+    if (threadIdx.x == 0 && got != (int64_t)raw) atomicOr(err, 1u);
 }
 
 int read_method(Ctx *ctx, const uint8_t *packet, uint8_t *m) {
@@ -416,7 +418,7 @@ int tfg_codec_decompress(tfg_ctx *ctx, const uint8_t *packet, size_t bytes, uint
     if (res[0] && m == ZSTD_METHOD) { // per-frame decoder state (tables + a block's literals)
         TFG_HIP(hipMallocAsync((void **)&work, res[0] * sizeof(tfz::ZWork), ctx->stream));
         ProfScope _ps(ctx, "codec.zstd.decompress");
-        hipLaunchKernelGGL(zstd_decode_kernel, dim3((unsigned)((res[0] + 63) / 64)), dim3(64), 0, ctx->stream, packet,
+        hipLaunchKernelGGL(zstd_decode_kernel, dim3((unsigned)res[0]), dim3(64), 0, ctx->stream, packet,
                            (const uint64_t *)(sb + o_foff), (const uint64_t *)(sb + o_roff), res[0], out + 1, work, err);
     } else if (res[0]) {
         ProfScope _ps(ctx, "codec.lz4.decompress");

@@ -21,6 +21,17 @@
 #else
 #define ZHD inline
 #endif
+// Wave-cooperative copies: on the device all 64 lanes of a wave run the decoder in lockstep (the
+// entropy decoding is identical in every lane: same loads, same branches) and split only the
+// byte copies, lane i taking bytes i, i + 64, ...; ZSYNC makes the wave's earlier stores visible
+// to its other lanes before they are read back (match sources), ZSYNC_AGENT before the checksum.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define ZSYNC() do { __builtin_amdgcn_s_waitcnt(0); __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); } while (0)
+#define ZSYNC_AGENT() do { __builtin_amdgcn_s_waitcnt(0); __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent"); } while (0)
+#else
+#define ZSYNC() do { } while (0)
+#define ZSYNC_AGENT() do { } while (0)
+#endif
 
 namespace tfz {
 
@@ -417,7 +428,8 @@ ZHD int64_t seq_table(const uint8_t *src, int64_t n, int mode, int kind, ZWork *
 }
 
 // one compressed block -> out[op ...]; reps = the frame's repeat offsets
-ZHD bool zblock(const uint8_t *src, int64_t n, uint8_t *out, uint64_t &op, uint64_t cap, uint32_t *rep, ZWork *w) {
+ZHD bool zblock(const uint8_t *src, int64_t n, uint8_t *out, uint64_t &op, uint64_t cap, uint32_t *rep, ZWork *w,
+                uint32_t lane, uint32_t nl) {
     // ---- literals section
     if (n < 1) return false;
     const int ltype = src[0] & 3, sf = (src[0] >> 2) & 3;
@@ -551,10 +563,19 @@ ZHD bool zblock(const uint8_t *src, int64_t n, uint8_t *out, uint64_t &op, uint6
                 }
             }
             if (lit_pos + ll > lsize || op + ll + ml > cap || off == 0 || off > op + ll) return false;
-            for (uint32_t i = 0; i < ll; ++i) out[op + i] = w->lit[lit_pos + i];
+            for (uint32_t i = lane; i < ll; i += nl) out[op + i] = w->lit[lit_pos + i];
             op += ll;
             lit_pos += ll;
-            for (uint32_t i = 0; i < ml; ++i) out[op + i] = out[op + i - off];
+            // the match repeats the off bytes before op: byte i = out[op - off + i % off], all of
+            // them written before this copy (by any lane: ZSYNC first)
+            ZSYNC();
+            const volatile uint8_t *ov = out;
+            if (off >= ml) {
+                for (uint32_t i = lane; i < ml; i += nl) out[op + i] = ov[op - off + i];
+            } else {
+                const uint32_t o32 = (uint32_t)off;
+                for (uint32_t i = lane; i < ml; i += nl) out[op + i] = ov[op - off + i % o32];
+            }
             op += ml;
         }
         if (bb.pos != 0) return false;
@@ -562,13 +583,15 @@ ZHD bool zblock(const uint8_t *src, int64_t n, uint8_t *out, uint64_t &op, uint6
         return false;
     }
     if (op + (lsize - lit_pos) > cap) return false;
-    for (uint32_t i = lit_pos; i < lsize; ++i) out[op++] = w->lit[i];
+    for (uint32_t i = lane; i < lsize - lit_pos; i += nl) out[op + i] = w->lit[lit_pos + i];
+    op += lsize - lit_pos;
     return true;
 }
 
 // One ZSTD frame src[0, n) -> dst[0, cap); returns the decoded size, or -1 when the frame is
 // malformed, uses a dictionary, or does not fit.  (Skippable frames decode to nothing.)
-ZHD int64_t zstd_frame(const uint8_t *src, int64_t n, uint8_t *dst, uint64_t cap, ZWork *w) {
+ZHD int64_t zstd_frame(const uint8_t *src, int64_t n, uint8_t *dst, uint64_t cap, ZWork *w, uint32_t lane = 0,
+                       uint32_t nl = 1) {
     int64_t ip = 0;
     uint64_t op = 0;
     while (ip < n) {
@@ -614,21 +637,21 @@ ZHD int64_t zstd_frame(const uint8_t *src, int64_t n, uint8_t *dst, uint64_t cap
             if (btype == 3) return -1;
             if (btype == 1) {
                 if (ip + 1 > n || op + bsize > cap) return -1;
-                for (uint32_t i = 0; i < bsize; ++i) dst[op + i] = src[ip];
+                for (uint32_t i = lane; i < bsize; i += nl) dst[op + i] = src[ip];
                 op += bsize;
                 ip += 1;
             } else {
                 if (ip + bsize > n) return -1;
                 if (btype == 0) {
                     if (op + bsize > cap) return -1;
-                    for (uint32_t i = 0; i < bsize; ++i) dst[op + i] = src[ip + i];
+                    for (uint32_t i = lane; i < bsize; i += nl) dst[op + i] = src[ip + i];
                     op += bsize;
                 } else {
                     if (bsize > (uint32_t)ZMAX_BLOCK) return -1;
                     // offsets reach back into this frame's output only (no dictionary)
                     uint8_t *fo = dst + frame_start;
                     uint64_t fop = op - frame_start;
-                    if (!zblock(src + ip, bsize, fo, fop, cap - frame_start, rep, w)) return -1;
+                    if (!zblock(src + ip, bsize, fo, fop, cap - frame_start, rep, w, lane, nl)) return -1;
                     op = frame_start + fop;
                 }
                 ip += bsize;
@@ -638,6 +661,7 @@ ZHD int64_t zstd_frame(const uint8_t *src, int64_t n, uint8_t *dst, uint64_t cap
         if (has_fcs && op - frame_start != fcs) return -1;
         if (checksum) {
             if (ip + 4 > n) return -1;
+            ZSYNC_AGENT();
             if ((uint32_t)xxh64(dst + frame_start, op - frame_start) != rd32(src + ip)) return -1;
             ip += 4;
         }
