@@ -358,15 +358,25 @@ __global__ void __launch_bounds__(1024) regroup_prefix_kernel(const uint32_t *hi
     if (threadIdx.x == 0) out[T1] = carry;
 }
 
-// tile_base[c] = first pass-2 tile of coarse bucket c (one workgroup; B1 <= 1024)
-__global__ void regroup_tile_base_kernel(const uint32_t *runpref, int T1, int B1, uint32_t *tile_base) {
-    if (threadIdx.x != 0) return;
-    uint32_t acc = 0;
-    for (int c = 0; c < B1; ++c) {
-        tile_base[c] = acc;
-        acc += (runpref[(size_t)c * (T1 + 1) + T1] + RG_TR - 1) / RG_TR;
+// tile_base[c] = first pass-2 tile of coarse bucket c: one 1024-thread workgroup scans the
+// buckets' tile counts (B1 <= 1024; a single-thread loop over the buckets' dependent loads took
+// 61 us at 256 buckets)
+__global__ void __launch_bounds__(1024) regroup_tile_base_kernel(const uint32_t *runpref, int T1, int B1, uint32_t *tile_base) {
+    __shared__ uint32_t wsum[16];
+    const int c = (int)threadIdx.x;
+    const uint32_t v = c < B1 ? (runpref[(size_t)c * (T1 + 1) + T1] + RG_TR - 1) / RG_TR : 0u;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if ((c & 63) >= d) x += y;
     }
-    tile_base[B1] = acc;
+    if ((c & 63) == 63) wsum[c >> 6] = x;
+    __syncthreads();
+    uint32_t off = 0;
+    for (int w = 0; w < (c >> 6); ++w) off += wsum[w];
+    if (c < B1) tile_base[c] = off + x - v;
+    if (c == B1 - 1) tile_base[B1] = off + x;
 }
 
 // where pass-2 tile k reads from: its coarse bucket c (-1: past the last tile), the pass-1 runs
@@ -928,7 +938,7 @@ int consume_wide_tiled(tfg_agg *a, int code, Sel sel, const void *const *vals, i
         uint32_t *hist2 = (uint32_t *)(sb + o_hist2);
         ProfScope _ps(ctx, "agg.part.regroup");
         hipLaunchKernelGGL(regroup_prefix_kernel, dim3(B1), dim3(1024), 0, ctx->stream, tin.tile_hist, T1, pref);
-        hipLaunchKernelGGL(regroup_tile_base_kernel, dim3(1), dim3(64), 0, ctx->stream, pref, T1, (int)B1, tbase);
+        hipLaunchKernelGGL(regroup_tile_base_kernel, dim3(1), dim3(1024), 0, ctx->stream, pref, T1, (int)B1, tbase);
         RgDesc *desc = (RgDesc *)(sb + o_desc);
         hipLaunchKernelGGL(regroup_desc_kernel, dim3((unsigned)((T2 + 255) / 256)), dim3(256), 0, ctx->stream,
                            (const uint32_t *)pref, T1, (const uint32_t *)tbase, (int)B1, (int)T2, desc);

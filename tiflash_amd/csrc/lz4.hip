@@ -298,11 +298,15 @@ __global__ void __launch_bounds__(64) lz4_decode_kernel(const uint8_t *pkt, cons
 // copies; the frame body after the 9-byte header must decode to exactly its declared raw size,
 // else err |= 1.  `work` holds one ZWork per frame.
 __global__ void __launch_bounds__(64) zstd_decode_kernel(const uint8_t *pkt, const uint64_t *foff, const uint64_t *roff,
-                                                         uint64_t nframes, uint8_t *dst, tfz::ZWork *work, unsigned *err) {
+                                                         uint64_t nframes, uint8_t *dst, uint8_t *lits, unsigned *err) {
+    __shared__ tfz::ZWork w; // FSE / Huffman tables in LDS (table lookups are the decode's dependent chain)
+    __shared__ uint8_t stage[tfz::ZMAX_BLOCK]; // the compressed block being decoded (bit reads from LDS)
     const uint64_t f = blockIdx.x;
     if (f >= nframes) return;
+    w.lit = lits + f * (uint64_t)(tfz::ZMAX_BLOCK + 32);
+    w.stage = stage;
     const uint64_t fb = foff[f + 1] - foff[f], raw = roff[f + 1] - roff[f];
-    const int64_t got = tfz::zstd_frame(pkt + foff[f] + FRAME_HDR, (int64_t)(fb - FRAME_HDR), dst + roff[f], raw, work + f,
+    const int64_t got = tfz::zstd_frame(pkt + foff[f] + FRAME_HDR, (int64_t)(fb - FRAME_HDR), dst + roff[f], raw, &w,
                                         threadIdx.x, 64);
     if (threadIdx.x == 0 && got != (int64_t)raw) atomicOr(err, 1u);
 }
@@ -414,9 +418,9 @@ int tfg_codec_decompress(tfg_ctx *ctx, const uint8_t *packet, size_t bytes, uint
     TFG_HIP(hipMemsetAsync(out, NONE_METHOD, 1, ctx->stream));
     unsigned *err = (unsigned *)ctx->dev_counter;
     TFG_HIP(hipMemsetAsync(err, 0, sizeof(unsigned), ctx->stream));
-    tfz::ZWork *work = nullptr;
-    if (res[0] && m == ZSTD_METHOD) { // per-frame decoder state (tables + a block's literals)
-        TFG_HIP(hipMallocAsync((void **)&work, res[0] * sizeof(tfz::ZWork), ctx->stream));
+    uint8_t *work = nullptr;
+    if (res[0] && m == ZSTD_METHOD) { // per-frame literal buffers (the tables live in LDS)
+        TFG_HIP(hipMallocAsync((void **)&work, res[0] * (size_t)(tfz::ZMAX_BLOCK + 32), ctx->stream));
         ProfScope _ps(ctx, "codec.zstd.decompress");
         hipLaunchKernelGGL(zstd_decode_kernel, dim3((unsigned)res[0]), dim3(64), 0, ctx->stream, packet,
                            (const uint64_t *)(sb + o_foff), (const uint64_t *)(sb + o_roff), res[0], out + 1, work, err);

@@ -28,7 +28,9 @@
 #if defined(__HIP_DEVICE_COMPILE__)
 #define ZSYNC() do { __builtin_amdgcn_s_waitcnt(0); __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); } while (0)
 #define ZSYNC_AGENT() do { __builtin_amdgcn_s_waitcnt(0); __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent"); } while (0)
+#define ZSYNC_LDS() __syncthreads()
 #else
+#define ZSYNC_LDS() do { } while (0)
 #define ZSYNC() do { } while (0)
 #define ZSYNC_AGENT() do { } while (0)
 #endif
@@ -50,46 +52,48 @@ struct ZWork {
     bool ll_ok, of_ok, ml_ok;             // a table exists for Repeat mode
     uint16_t huf[1 << ZHUF_MAXBITS];      // symbol | nbBits << 8
     int huf_bits;                         // 0: no table yet (Treeless needs one)
-    uint8_t lit[ZMAX_BLOCK + 32];
+    uint8_t *lit;                         // ZMAX_BLOCK + 32 bytes: the block's literals
+    uint8_t *stage;                       // device: an LDS copy of the current compressed block (null: none)
 };
+// (the tables, ~10 KB, live in LDS on the device; the literals in global memory)
 
 // ---------------------------------------------------------------- constants (RFC 8878 §3.1.1.3.2.2)
 ZHD uint32_t ll_base(int c) {
-    const uint32_t t[36] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10,  11,  12,  13,   14,   15,   16,   18,
+    static constexpr uint32_t t[36] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10,  11,  12,  13,   14,   15,   16,   18,
                             20, 22, 24, 28, 32, 40, 48, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536};
     return t[c];
 }
 ZHD int ll_bits(int c) {
-    const uint8_t t[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1,
+    static constexpr uint8_t t[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1,
                            1, 1, 2, 2, 3, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
     return t[c];
 }
 ZHD uint32_t ml_base(int c) {
     if (c < 32) return (uint32_t)c + 3;
-    const uint32_t t[21] = {35, 37, 39, 41, 43, 47, 51, 59, 67, 83, 99, 131, 259, 515, 1027, 2051, 4099, 8195, 16387, 32771, 65539};
+    static constexpr uint32_t t[21] = {35, 37, 39, 41, 43, 47, 51, 59, 67, 83, 99, 131, 259, 515, 1027, 2051, 4099, 8195, 16387, 32771, 65539};
     return t[c - 32];
 }
 ZHD int ml_bits(int c) {
     if (c < 32) return 0;
-    const uint8_t t[21] = {1, 1, 1, 1, 2, 2, 3, 3, 4, 4, 5, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+    static constexpr uint8_t t[21] = {1, 1, 1, 1, 2, 2, 3, 3, 4, 4, 5, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
     return t[c - 32];
 }
 // predefined distributions (RFC 8878 §3.1.1.3.2.2.1-3)
 ZHD int16_t ll_default(int s) {
-    const int16_t t[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2,
+    static constexpr int16_t t[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2,
                            2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1};
     return t[s];
 }
 ZHD int16_t ml_default(int s) {
     if (s == 0) return 1;
     if (s <= 8) {
-        const int16_t t[8] = {4, 3, 2, 2, 2, 2, 2, 2};
+        static constexpr int16_t t[8] = {4, 3, 2, 2, 2, 2, 2, 2};
         return t[s - 1];
     }
     return s <= 45 ? 1 : -1;
 }
 ZHD int16_t of_default(int s) {
-    const int16_t t[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
+    static constexpr int16_t t[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
     return t[s];
 }
 
@@ -117,32 +121,39 @@ struct FwdBits {
 
 // backward (Huffman streams, FSE bitstreams): the stream's last byte holds a 1 marker above the
 // padding; bits are read from the top down.  Reading past the start yields zeros and makes
-// `pos` negative (the overflow the decoders check).
+// `pos` negative (the overflow the decoders check).  A 64-bit window of the stream (bytes
+// [wb, wb + 8)) is kept in registers and refilled only when a read leaves it.
 struct BackBits {
     const uint8_t *p;
     int64_t nbytes;
     int64_t pos; // bits still unread (from bit 0 of p[0] up)
+    uint64_t win;
+    int64_t wb;  // first byte of the window (-1: none)
     ZHD bool init(const uint8_t *buf, int64_t n) {
         p = buf;
         nbytes = n;
+        wb = -1;
+        win = 0;
         if (n <= 0) return false;
         const uint8_t last = buf[n - 1];
         if (!last) return false;
         pos = (n - 1) * 8 + highbit(last);
         return true;
     }
-    // bits [lo, lo + n) of the stream (n <= 56, lo >= 0) from the 8 bytes that cover them
-    ZHD uint64_t bits_at(int64_t lo, int n) const {
-        const int64_t b0 = lo >> 3;
-        uint64_t w = 0;
-        if (b0 + 8 <= nbytes) {
-            for (int k = 0; k < 8; ++k) w |= (uint64_t)p[b0 + k] << (8 * k);
-        } else {
-            for (int k = 0; b0 + k < nbytes; ++k) w |= (uint64_t)p[b0 + k] << (8 * k);
+    // bits [lo, lo + n) of the stream (n <= 56, lo >= 0)
+    ZHD uint64_t bits_at(int64_t lo, int n) {
+        const int64_t b0 = lo >> 3, b1 = (lo + n - 1) >> 3;
+        if (wb < 0 || b0 < wb || b1 >= wb + 8) { // refill: the window ends at the read's last byte
+            int64_t nb = b1 - 7;
+            if (nb < 0) nb = 0;
+            win = 0;
+            for (int k = 0; k < 8; ++k)
+                if (nb + k < nbytes) win |= (uint64_t)p[nb + k] << (8 * k);
+            wb = nb;
         }
-        return (w >> (lo & 7)) & ((1ull << n) - 1);
+        return (win >> (lo - wb * 8)) & ((1ull << n) - 1);
     }
-    ZHD uint64_t peek(int n) const { // n <= 56; bits below the stream's start read as zeros
+    ZHD uint64_t peek(int n) { // n <= 56; bits below the stream's start read as zeros
         if (n == 0) return 0;
         const int64_t lo = pos - n;
         if (lo >= 0) return bits_at(lo, n);
@@ -532,6 +543,7 @@ ZHD bool zblock(const uint8_t *src, int64_t n, uint8_t *out, uint64_t &op, uint6
         BackBits bb;
         if (!bb.init(src + ip, n - ip)) return false;
         uint32_t sll = (uint32_t)bb.read(w->ll_log), sof = (uint32_t)bb.read(w->of_log), sml = (uint32_t)bb.read(w->ml_log);
+        uint64_t synced = 0; // output below this position is visible to every lane (block entry: none assumed)
         for (uint32_t q = 0; q < nseq; ++q) {
             const int llc = w->ll[sll].sym, ofc = w->of[sof].sym, mlc = w->ml[sml].sym;
             if (llc > 35 || mlc > 52 || ofc > 31) return false;
@@ -567,8 +579,12 @@ ZHD bool zblock(const uint8_t *src, int64_t n, uint8_t *out, uint64_t &op, uint6
             op += ll;
             lit_pos += ll;
             // the match repeats the off bytes before op: byte i = out[op - off + i % off], all of
-            // them written before this copy (by any lane: ZSYNC first)
-            ZSYNC();
+            // them written before this copy, by any lane: ZSYNC first unless every source byte lies
+            // below the last sync point (each ZSYNC waits for the wave's outstanding stores)
+            if (op - off + (ml < off ? ml : off) > synced) {
+                ZSYNC();
+                synced = op;
+            }
             const volatile uint8_t *ov = out;
             if (off >= ml) {
                 for (uint32_t i = lane; i < ml; i += nl) out[op + i] = ov[op - off + i];
@@ -651,7 +667,14 @@ ZHD int64_t zstd_frame(const uint8_t *src, int64_t n, uint8_t *dst, uint64_t cap
                     // offsets reach back into this frame's output only (no dictionary)
                     uint8_t *fo = dst + frame_start;
                     uint64_t fop = op - frame_start;
-                    if (!zblock(src + ip, bsize, fo, fop, cap - frame_start, rep, w, lane, nl)) return -1;
+                    const uint8_t *bsrc = src + ip;
+                    if (w->stage) { // the block's bytes into LDS: every bit read then costs an LDS load
+                        ZSYNC_LDS();
+                        for (uint32_t i = lane; i < bsize; i += nl) w->stage[i] = bsrc[i];
+                        ZSYNC_LDS();
+                        bsrc = w->stage;
+                    }
+                    if (!zblock(bsrc, bsize, fo, fop, cap - frame_start, rep, w, lane, nl)) return -1;
                     op = frame_start + fop;
                 }
                 ip += bsize;

@@ -1,11 +1,5 @@
 set -o pipefail
-run() { timeout -k 10 200 python bench.py --no-cpu --no-join --codec-rows 0 --no-variants --rows 10000000 > gpurun_out/c5_$1.json 2>&1 || exit 1
+timeout -k 10 400 python -u -m pytest tests/test_zstd.py tests/test_codec.py tests/test_codec_lz4.py tests/test_gpu_hash_agg_join.py -x -q --timeout 200 --timeout-method thread > gpurun_out/t_zk.log 2>&1; echo "tests rc=$?"; tail -1 gpurun_out/t_zk.log
+timeout -k 10 300 python bench.py --rows 1000000 --no-variants --no-cpu --no-join --c5-rows 0 > gpurun_out/zb.json 2>&1 || exit 1
 python -c "
-import json,sys
-d=json.loads(open('gpurun_out/c5_$1.json').read().strip().splitlines()[-1])['string_agg']
-print('$1', d['ms_per_step'], d['check']['ok'], d['kernels_ms_per_step'])
-"; }
-timeout -k 10 300 python -u -m pytest tests/test_gpu_keys_agg.py tests/test_gpu_full_scale.py -x -q --timeout 200 --timeout-method thread -k "string or fixed_keys or c5" > gpurun_out/t_rg.log 2>&1; echo "rg1536 tests rc=$?"; tail -1 gpurun_out/t_rg.log
-run rg1536
-cp tiflash_amd/exp_a/libtiflash_amd.so tiflash_amd/libtiflash_amd.so
-run rg1024
+import json; d=json.loads(open('gpurun_out/zb.json').read().strip().splitlines()[-1]); print(d['packet_codec']['legs']['zstd'])"
