@@ -23,6 +23,7 @@
 //   chunk with a per-probe-row found flag so LEFT / SEMI / ANTI stay exact.  Rows with a NULL key
 //   never match (not inserted / not probed); LEFT and ANTI emit them as unmatched rows.
 #include <algorithm>
+#include <vector>
 
 #include "collation.h"
 #include "common.h"
@@ -550,6 +551,7 @@ struct tfg_join {
     uint32_t *brows = nullptr;
     uint64_t *boff = nullptr;
     int64_t n_inserted = 0;
+    uint64_t max_part = 0; // build rows of the largest partition (> JCHUNK: chunked probes need found flags)
     // JoinV2 pointer table (tfg_join_create_v2)
     bool v2 = false;
     bool tagged = false;
@@ -770,7 +772,8 @@ int probe_common(tfg_join *j, int kind, const void *keys, const uint8_t *key_nul
                                                           "join.part.hist", "join.part.scatter")) {
             return rc;
         }
-        TFG_HIP(hipMemsetAsync(sb + o_found, 0, n, ctx->stream));
+        if (j->max_part > (uint64_t)JCHUNK) // only chunked partitions read / write the found flags
+            TFG_HIP(hipMemsetAsync(sb + o_found, 0, n, ctx->stream));
         A.prec = (const uint64_t *)(sb + o_prec);
         A.prows = prows;
         A.poff = poff;
@@ -1108,9 +1111,12 @@ int tfg_join_finalize(tfg_join *j) {
     if (int rc = run_partition<SelJoin, false>(ctx, sel, pred, L, pc, j->brows, nullptr, j->boff, tmp, "join.build.hist",
                                                "join.build.scatter"))
         return rc;
-    uint64_t ins = 0;
-    if (int rc = read_back_u64(ctx, j->boff + P, &ins, 1)) return rc;
-    j->n_inserted = (int64_t)ins;
+    std::vector<uint64_t> hb(P + 1);
+    TFG_HIP(hipMemcpyAsync(hb.data(), j->boff, (P + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream));
+    TFG_HIP(hipStreamSynchronize(ctx->stream));
+    j->n_inserted = (int64_t)hb[P];
+    j->max_part = 0;
+    for (uint32_t p = 0; p < P; ++p) j->max_part = std::max<uint64_t>(j->max_part, hb[p + 1] - hb[p]);
     j->finalized = true;
     return TFG_OK;
 }
