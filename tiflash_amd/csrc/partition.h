@@ -581,11 +581,6 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
     uint32_t *fh = reinterpret_cast<uint32_t *>(lds + g.fh_off); // TILED && fine_bits: P << fine_bits bins
     if (TILED && g.fine_bits)
         for (uint32_t p = threadIdx.x; p < (P << g.fine_bits); p += ST_T) fh[p] = 0;
-    // after a tile that kept no row, the next tile loads a row's key only once its predicate
-    // holds (the reference skips all-false blocks, FilterTransformAction.cpp:135-139): at low
-    // selectivity the key bytes are not read; while tiles keep rows the key loads issue beside
-    // the predicate loads as before (workgroup-uniform switch, no cost at high selectivity)
-    bool lazy_keys = false;
     for (uint32_t tb = begin; tb < end; tb += (uint32_t)g.TR) {
         for (uint32_t p = threadIdx.x; p < P; p += ST_T) hist[p] = 0;
         if (NARROW && threadIdx.x == 0) red[ST_T / 64 + 1] = 0;
@@ -604,10 +599,9 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
             for (int q = 0; q < HB; ++q) { // the half-batch's loads first ...
                 const int j = h * HB + q;
                 const uint32_t r = tb + (uint32_t)j * ST_T + threadIdx.x;
-                kl[q] = Loaded{};
                 if (j < per && r < end) {
                     pl[q] = pred.load(r);
-                    if (!lazy_keys) kl[q] = sel.load(r);
+                    kl[q] = sel.load(r);
                 }
             }
 #pragma unroll
@@ -616,7 +610,6 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
                 bq[j] = 0xFFFFFFFFu;
                 const uint32_t r = tb + (uint32_t)j * ST_T + threadIdx.x;
                 if (j < per && r < end && pred.eval(pl[q])) {
-                    if (lazy_keys) kl[q] = sel.load(r);
                     uint32_t b = sel.part(crc, kl[q], r);
                     if (TILED && g.fine_bits && b < (P << g.fine_bits)) {
                         atomicAdd(&fh[b], 1u);
@@ -687,7 +680,6 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
         }
         __syncthreads();
         const uint32_t kept = red[ST_T / 64];
-        lazy_keys = kept == 0;
         const uint32_t tile = blockIdx.x * (uint32_t)g.tps + (tb - begin) / (uint32_t)g.TR;
         const bool narrow = NARROW && g.allow_narrow && red[ST_T / 64 + 1] == 0;
         if constexpr (TILED)
