@@ -79,7 +79,6 @@ def launch_ranks(args) -> int:
 # separately as moved_bytes (and measured by the PMC passes as traffic).
 def kernel_bytes(name, n_in, n_kept, n_groups):
     alg = {
-        "agg.fused": 24 * n_in + 24 * n_groups,
         "agg.part.tiled": 24 * n_in,
         "agg.part.hist": 16 * n_in,
         "agg.part.scatter": 24 * n_in,
@@ -89,7 +88,6 @@ def kernel_bytes(name, n_in, n_kept, n_groups):
         "join.probe": 0,
     }.get(name)
     moved = {
-        "agg.fused": 24 * n_in + 24 * n_groups,
         "agg.part.tiled": 24 * n_in + 16 * n_kept,
         "agg.part.hist": 16 * n_in,
         "agg.part.scatter": 24 * n_in + 16 * n_kept,
@@ -659,22 +657,6 @@ def variants_leg(args, ctx, dev, f, k, v):
                           "pipeline_frac": round(24 * N / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
     agg.close()
     del vi
-    # the opt-in single-launch fused filter -> GROUP BY kernel on the headline signature
-    agg = tfa.Aggregator(ctx, tfa.INT64, [(tfa.AGG_SUM, tfa.FLOAT64), (tfa.AGG_COUNT_ALL, 0)],
-                         bucket_bits=args.bucket_bits, expected_groups=G, fused=True)
-
-    def fstep():
-        agg.reset()
-        agg.consume_filtered(f, tfa.LT, args.threshold, k, [v, None])
-        return agg.result()
-    el, res, _ = timed(fstep, args, ctx, 1)
-    ms = el / args.steps * 1e3
-    kept = int((f < args.threshold).sum().item())
-    out["fused_kernel"] = {"metric": "rows/s filter + GROUP BY through the single-launch fused kernel",
-                           "value": round(N * args.steps / el, 1), "ms_per_step": round(ms, 3),
-                           "check_ok": int(res["states"][1].view(torch.int64).sum().item()) == kept,
-                           "pipeline_frac": round(24 * N / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
-    agg.close()
     return out
 
 

@@ -296,12 +296,6 @@ typedef struct tfg_agg_params {
     int bucket_bits;
     /* hint for the number of distinct keys (0 = unknown: 2^20 assumed). */
     int64_t expected_groups;
-    /* 1 = let the first consume of >= 4M rows of a fast signature (one 8-byte key without NULLs,
-     * sum over Int64 / UInt64 / Float64 and / or count) run as ONE fused filter -> GROUP BY
-     * launch (agg_fused.hip: persistent per-CU bucket tables fed through an Infinity-Cache
-     * ring) instead of partition + bucket kernels.  Opt-in: on C2 it measures 1.46 ms against
-     * 1.40 ms for the two-kernel path. */
-    int fused;
 } tfg_agg_params;
 
 /* Aggregator with one fixed-width GROUP BY key (method key8..key64 / nullable, Interpreters/

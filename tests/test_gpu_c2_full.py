@@ -47,17 +47,15 @@ def test_c2_full_scale_matches_oracle(tfa, ctx, dev, orc):
     assert int(gc.sum()) == int((f < 96).sum())
 
 
-@pytest.mark.parametrize("fused", [False, True])
-def test_c2_full_scale_int64_values_exact(tfa, ctx, dev, fused):
+def test_c2_full_scale_int64_values_exact(tfa, ctx, dev):
     """The §8(d) Int64-value variant at full size: per-group sums checked against an index_add
-    of the kept rows (exact integer arithmetic); also through the opt-in fused kernel."""
+    of the kept rows (exact integer arithmetic)."""
     g = torch.Generator(device=dev)
     g.manual_seed(3)
     f = torch.randint(0, 100, (N,), device=dev, generator=g)
     k = torch.randint(0, G, (N,), device=dev, generator=g)
     v = torch.randint(-(1 << 40), 1 << 40, (N,), device=dev, generator=g)
-    agg = tfa.Aggregator(ctx, tfa.INT64, [(tfa.AGG_SUM, tfa.INT64), (tfa.AGG_COUNT_ALL, 0)], expected_groups=G,
-                         fused=fused)
+    agg = tfa.Aggregator(ctx, tfa.INT64, [(tfa.AGG_SUM, tfa.INT64), (tfa.AGG_COUNT_ALL, 0)], expected_groups=G)
     agg.consume_filtered(f, tfa.LT, 96, k, [v, None])
     res = agg.result()
     m = f < 96

@@ -272,9 +272,11 @@ def test_two_phase_string_aggregation_gloo():
     assert got == want
 
 
-def _sides_worker(rank, world, port, q):
+def _sides_worker(rank, world, port, q, empty=False):
     """exchange_sides: three sides in one data all-to-all — (Int64, UInt8, 2-word) rows, Float64
-    rows, and a byte side (String chars) cut at per-partition byte offsets."""
+    rows, and a byte side (String chars) cut at per-partition byte offsets.  empty: rank 1 has no
+    rows on the first side and no chars on the third (a partial GROUP BY with no groups, an empty
+    join side), which must not change the record layout its peers expect."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import sys
@@ -285,6 +287,8 @@ def _sides_worker(rank, world, port, q):
         rng = np.random.default_rng(500 + rank)
         sides, sent = [], []
         for s, (n, mk) in enumerate(((3000, "a"), (1700, "b"), (9000, "c"))):
+            if empty and rank == 1 and mk in ("a", "c"):
+                n = 0
             dest = np.sort(rng.integers(0, world, n))  # partition-major rows
             if rank == 0 and s == 1:
                 dest[:] = 0  # a side that sends nothing to the other ranks
@@ -316,12 +320,12 @@ def _sides_worker(rank, world, port, q):
         raise
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_fused_exchange_sides_gloo(world):
+@pytest.mark.parametrize("world,empty", [(2, False), (3, False), (2, True), (3, True)])
+def test_fused_exchange_sides_gloo(world, empty):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_sides_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_sides_worker, args=(r, world, port, q, empty)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(world)]

@@ -389,22 +389,21 @@ def hash_partition(ctx: Context, cols: Sequence, key_idx: Sequence[int], part_nu
 
 # ---- a9-a17 aggregation -----------------------------------------------------------------------
 class _AggParams(ctypes.Structure):
-    _fields_ = [("bucket_bits", ctypes.c_int), ("expected_groups", ctypes.c_int64), ("fused", ctypes.c_int)]
+    _fields_ = [("bucket_bits", ctypes.c_int), ("expected_groups", ctypes.c_int64)]
 
 
 class Aggregator:
     """tfg_agg: hash GROUP BY with one fixed-width key (key_type=0: without key)."""
 
     def __init__(self, ctx: Context, key_type: int, aggs: Sequence[tuple], bucket_bits: int = 0,
-                 expected_groups: int = 0, fused: bool = False):
-        """aggs: sequence of (kind, arg_type[|NULLABLE]) — arg_type ignored for AGG_COUNT_ALL.
-        fused: allow the single-launch fused filter -> GROUP BY kernel (tfg_agg_params.fused)."""
+                 expected_groups: int = 0):
+        """aggs: sequence of (kind, arg_type[|NULLABLE]) — arg_type ignored for AGG_COUNT_ALL."""
         self.ctx = ctx
         self.key_type = key_type
         self.aggs = list(aggs)
         kinds = _int_array([k for k, _ in aggs])
         types = _int_array([t for _, t in aggs])
-        params = _AggParams(bucket_bits, expected_groups, int(fused))
+        params = _AggParams(bucket_bits, expected_groups)
         h = ctypes.c_void_p()
         check(lib().tfg_agg_create(ctx.h, key_type, len(aggs), kinds, types, ctypes.c_void_p(0), ctypes.byref(params),
                                    ctypes.byref(h)))

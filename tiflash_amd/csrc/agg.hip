@@ -21,7 +21,6 @@
 #include <algorithm>
 #include <vector>
 
-#include "agg_fused.h"
 #include "common.h"
 #include "agg_dev.h"
 #include "collation.h"
@@ -634,7 +633,6 @@ struct tfg_agg {
     AggSpec S{};
     int key_type = 0;
     bool nokey = false;
-    bool fused = false; // tfg_agg_params.fused: the single-launch path may serve a consume
     uint32_t B = 1;
     int arg_types[AGG_MAX] = {};
     int arg_nullable[AGG_MAX] = {};
@@ -994,85 +992,6 @@ int consume_wide_tiled(tfg_agg *a, int code, Sel sel, const void *const *vals, i
     return TFG_OK;
 }
 
-// The fused filter -> GROUP BY kernel (agg_fused.hip) for an empty aggregator of a fast
-// signature with FUSED_BUCKETS buckets: one launch, the bucket tables stay in LDS for the whole
-// input and the staged records never leave the Infinity Cache.  Then scan + compaction of the
-// tables' groups into the state; rows that found their table full are aggregated afterwards by
-// the two-kernel path (the state then holds the tables' groups, so any distribution is exact).
-int consume_fused(tfg_agg *a, int fast, const RowPred &pred, const void *keys, const void *const *vals, int64_t n,
-                  bool &done) {
-    done = false;
-    Ctx *ctx = a->ctx;
-    const AggSpec &S = a->S;
-    const uint32_t B = a->B;
-    if (B != (uint32_t)FUSED_BUCKETS || a->n_groups != 0) return TFG_OK;
-    int sum_i = -1, cnt_i = -1;
-    for (int i = 0; i < S.n_aggs; ++i) {
-        if (S.kind[i] == TFG_AGG_SUM) sum_i = i;
-        else cnt_i = i;
-    }
-    if (sum_i < 0 || cnt_i < 0 || S.n_aggs != 2) return TFG_OK;
-    const size_t tmp_groups = (size_t)FUSED_BUCKETS * (FUSED_TABLE_CAP + 1);
-    Carver cv;
-    const size_t o_fused = cv.take<uint8_t>(fused_scratch_bytes());
-    const size_t o_spk = cv.take<uint64_t>((size_t)n), o_spv = cv.take<uint64_t>((size_t)n);
-    const size_t o_new_cnt = cv.take<uint64_t>(B), o_new_off = cv.take<uint64_t>(B + 1), o_tbase = cv.take<uint64_t>(B);
-    const size_t o_tmpg = cv.take<uint8_t>(a->carve_groups(nullptr, tmp_groups, a->st[0]) + 256);
-    const size_t o_scan = cv.take<uint8_t>(scan_tmp_bytes(B + 1));
-    void *sp;
-    if (int rc = scratch_get(ctx, cv.off, &sp)) return rc;
-    char *sb = (char *)sp;
-    GroupsIO tmp{};
-    a->carve_groups(sb + o_tmpg, tmp_groups, tmp);
-    FusedIO io{};
-    io.tmp_key = tmp.key;
-    io.tmp_key_null = tmp.key_null;
-    io.tmp_sum = (uint64_t *)tmp.acc[sum_i];
-    io.tmp_cnt = tmp.cnt[cnt_i];
-    io.out_cnt = (uint64_t *)(sb + o_new_cnt);
-    io.tmp_base = (uint64_t *)(sb + o_tbase);
-    io.spill_key = (uint64_t *)(sb + o_spk);
-    io.spill_val = (uint64_t *)(sb + o_spv);
-    uint64_t spilled = 0;
-    bool launched = false;
-    if (int rc = agg_fused_consume(ctx, fast, pred, keys, vals[sum_i], n, io, sb + o_fused, &spilled, launched))
-        return rc;
-    if (!launched) return TFG_OK;
-    uint64_t *new_off = (uint64_t *)(sb + o_new_off);
-    if (int rc = exclusive_scan_u64(ctx, io.out_cnt, new_off, B, sb + o_scan)) return rc;
-    uint64_t total = 0;
-    if (int rc = read_back_u64(ctx, new_off + B, &total, 1)) return rc;
-    const int nxt = a->cur ^ 1;
-    if (int rc = a->ensure_state(nxt, total)) return rc;
-    if (!a->bucket_off[nxt]) TFG_HIP(hipMalloc(&a->bucket_off[nxt], (B + 1) * 8));
-    {
-        ProfScope _ps(ctx, "agg.compact");
-        hipLaunchKernelGGL(agg_compact_kernel, dim3(B), dim3(256), 0, ctx->stream, S, tmp, (const uint64_t *)nullptr,
-                           (const uint64_t *)nullptr, new_off, a->st[nxt], (const uint64_t *)io.tmp_base);
-    }
-    TFG_LAUNCH_CHECK();
-    TFG_HIP(hipMemcpyAsync(a->bucket_off[nxt], new_off, (B + 1) * 8, hipMemcpyDeviceToDevice, ctx->stream));
-    a->cur = nxt;
-    a->n_groups = total;
-    done = true;
-    if (spilled == 0) return TFG_OK;
-    // rows of keys that found their bucket's table full: a second consume over them (copied out
-    // of the scratch arena, which that consume reuses)
-    void *spk = nullptr, *spv = nullptr;
-    TFG_HIP(hipMalloc(&spk, spilled * 8));
-    TFG_HIP(hipMalloc(&spv, spilled * 8));
-    TFG_HIP(hipMemcpyAsync(spk, io.spill_key, spilled * 8, hipMemcpyDeviceToDevice, ctx->stream));
-    TFG_HIP(hipMemcpyAsync(spv, io.spill_val, spilled * 8, hipMemcpyDeviceToDevice, ctx->stream));
-    const void *sv[AGG_MAX] = {};
-    sv[sum_i] = spv;
-    RowPred all{};
-    const int rc = consume_keyed(a, MODE_RAW, all, spk, 8, nullptr, sv, nullptr, nullptr, nullptr, (int64_t)spilled);
-    (void)hipStreamSynchronize(ctx->stream);
-    (void)hipFree(spk);
-    (void)hipFree(spv);
-    return rc;
-}
-
 int consume_keyed(tfg_agg *a, int mode, const RowPred &pred, const void *keys, int key_width, const uint8_t *key_null,
                   const void *const *vals, const uint8_t *const *val_nulls, const uint64_t *const *val_cnts,
                   const uint64_t *given_off, int64_t n) {
@@ -1082,11 +1001,6 @@ int consume_keyed(tfg_agg *a, int mode, const RowPred &pred, const void *keys, i
     const size_t n_old = a->n_groups;
     // fast signature: rows staged as interleaved records (key + summed arguments, 8 B each)
     const int fast = given_off ? 0 : fast_signature(S, mode, key_width, key_null, val_nulls);
-    if (fast && a->fused && n_old == 0 && n >= FUSED_MIN_ROWS) {
-        bool done = false;
-        if (int rc = consume_fused(a, fast, pred, keys, vals, n, done)) return rc;
-        if (done) return TFG_OK;
-    }
     if (fast) {
         bool done = false;
         if (int rc = consume_fast_tiled(a, fast, pred, keys, vals, n, done)) return rc;
@@ -1487,7 +1401,6 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
     // against 512 with 4K-cell tables 48.5G on C2); at least 256 buckets, one per CU
     const int64_t eg = (params && params->expected_groups > 0) ? params->expected_groups : (1 << 20);
     int bbits = params ? params->bucket_bits : 0;
-    a->fused = params && params->fused;
     // largest-table fill: inserts reserve cells (Table::reserve), so no headroom for in-flight
     // inserts is needed; wide keys (48-byte cells with a Decimal128 sum) fill to 7/8
     const int fill_big = wide ? 7 : 6;

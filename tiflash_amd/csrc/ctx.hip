@@ -275,7 +275,12 @@ using namespace tfg;
 extern "C" {
 
 const char *tfg_last_error(void) { return g_last_error.c_str(); }
-const char *tfg_version(void) { return "tiflash_amd 0.1 (gfx950)"; }
+extern "C" const char tfg_build_stamp[]; // build/stamp.cpp, written by the Makefile
+const char *tfg_version(void) {
+    static char v[512];
+    if (!v[0]) snprintf(v, sizeof v, "tiflash_amd 0.2 (%s)", tfg_build_stamp);
+    return v;
+}
 size_t tfg_type_width(int type) { return type_width(type); }
 
 int tfg_device_count(int *out) {

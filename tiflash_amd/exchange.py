@@ -23,12 +23,23 @@ import torch
 import torch.distributed as dist
 
 
+def _row_width(c: torch.Tensor) -> int:
+    """Bytes per row of a column, from its schema (dtype, trailing shape), not from its data, so
+    a rank with no rows agrees with its peers on the record layout."""
+    w = c.element_size()
+    for d in c.shape[1:]:
+        w *= int(d)
+    return w
+
+
 def _row_bytes(c: torch.Tensor, n: int) -> torch.Tensor:
     """The first n rows of a column as an [n, row_bytes] uint8 view (copy only if strided)."""
+    if n == 0:  # empty tensors may carry 0 strides, which view() refuses
+        return torch.empty((0, _row_width(c)), dtype=torch.uint8, device=c.device)
     c = c[:n]
     if not c.is_contiguous():
         c = c.contiguous()
-    return c.view(torch.uint8).reshape(n, -1)
+    return c.view(torch.uint8).reshape(n, _row_width(c))
 
 
 def exchange_sides(sides: Sequence[Tuple[Sequence[torch.Tensor], Sequence[int]]], group=None) -> List[List[torch.Tensor]]:
@@ -84,7 +95,10 @@ def exchange_sides(sides: Sequence[Tuple[Sequence[torch.Tensor], Sequence[int]]]
         cols, a = [], 0
         for w, dt, shp in specs[s]:
             piece = rec[:, a:a + w] if len(specs[s]) > 1 else rec
-            cols.append(piece.contiguous().view(dt).reshape((-1,) + shp))
+            if piece.shape[0] == 0:
+                cols.append(torch.empty((0,) + shp, dtype=dt, device=rec.device))
+            else:
+                cols.append(piece.contiguous().view(dt).reshape((-1,) + shp))
             a += w
         outs.append(cols)
     return outs

@@ -50,7 +50,7 @@ Aggregator::Aggregator(Context &ctx, const Params &params) : ctx_(ctx), params_(
                                    (at.isDecimal() ? TFG_ARG_PREC(at.precision()) : 0)));
         arg_scales.push_back(at.scale);
     }
-    tfg_agg_params p{params_.bucket_bits, params_.expected_groups, 0};
+    tfg_agg_params p{params_.bucket_bits, params_.expected_groups};
     if (packed_) {
         std::vector<int> coll = params_.collators;
         coll.resize(params_.keys.size(), TFG_COLLATOR_NONE);

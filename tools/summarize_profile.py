@@ -27,7 +27,6 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 # demangled name -> short name (first match wins)
 NAME_MAP = [
-    (r"agg_fused_kernel", "agg.fused"),
     (r"part_hist_kernel<tfg::SelBucket", "agg.part.hist"),
     (r"part_scatter_staged_kernel<tfg::SelBucket.*true, true>", "agg.part.tiled"),
     (r"part_scatter.*<tfg::SelBucket", "agg.part.scatter"),
@@ -56,7 +55,7 @@ NAME_MAP = [
 # leg-specific kernels (by short name or raw-name regex)
 LEGS = [
     ("C3v2", r"join_v2_"),
-    ("C2", r"^(agg\.fused|agg\.part\.(hist|tiled|scatter)|agg\.bucket\.tiled)$"),
+    ("C2", r"^(agg\.part\.(hist|tiled|scatter)|agg\.bucket\.tiled)$"),
     ("C3", r"^(join\.|part\.(hist|scatter)\.pass2)"),
     ("codec", r"tfg::str_|codec|lz4_"),
     ("C5", r"^(agg\.wide\.|agg\.(pack|unpack)_keys|agg\.bucket$)|wide_str|regroup_"),
@@ -166,7 +165,7 @@ def main():
     t2 = fk.get(("C2", "agg.part.tiled"))
     measured = (24 * rows) / (t2[1] * 1024 / t2[0]) if t2 else None
     # algorithmic bytes per launch where a kernel carries a leg's whole input
-    alg = {("C2", "agg.part.tiled"): 24 * rows, ("C2", "agg.fused"): 24 * rows + 24 * groups,
+    alg = {("C2", "agg.part.tiled"): 24 * rows,
            ("C2", "agg.part.hist"): 16 * rows}
     commit = a.commit
     try:
