@@ -120,6 +120,18 @@ typedef enum tfg_agg_kind {
     TFG_AGG_SUM = 0,
     TFG_AGG_COUNT = 1,     /* count(arg): non-NULL rows of arg */
     TFG_AGG_COUNT_ALL = 2, /* count(*) / count(1): arg ignored */
+    /* min / max / first_row (AggregateFunctionMinMaxAny.cpp:39-46,155-159; AggregateFunctionMinData /
+     * MaxData / FirstRowData, AggregateFunctionMinMaxAny.h): fixed-width numeric arguments (Int*,
+     * UInt*, Float*, Decimal32 / Decimal64); the result has the argument's type and width.  NULL
+     * arguments are skipped (AggregateFunctionNullUnary); a group whose argument is NULL in every row
+     * yields NULL.  first_row returns the argument of one row of the group: the reference keeps the
+     * first row it processes, whose order is not fixed (threads, merges); here it is the row whose
+     * value orders last, so equal-valued groups (a GROUP BY column carried as first_row) are exact.
+     * Float order is IEEE total order (-0 < +0; NaN past +inf), where the reference's `<` leaves
+     * ties and NaN to row order.  Decimal128 / Decimal256 arguments: TFG_ERR_NOT_IMPLEMENTED. */
+    TFG_AGG_MIN = 3,
+    TFG_AGG_MAX = 4,
+    TFG_AGG_FIRST_ROW = 5,
 } tfg_agg_kind;
 
 /* Join kinds (ASTTableJoin::Kind, dbms/src/Interpreters/Join.h). Strictness ALL. */

@@ -798,6 +798,59 @@ static int64_t agg_lookup(orc_agg *a, uint64_t key, int is_null)
     return *slot;
 }
 
+/* min / max / first_row (AggregateFunctionMinMaxAny.h: SingleValueDataFixed::changeIfLess /
+ * changeIfGreater / changeFirstTime; AggregateFunctionFirstRowData): the value is kept in acc_i
+ * (integers, as __int128) or acc_f (floats), cnt counts the rows that set or offered a value, and for
+ * first_row limb 0 of acc_w records "the first row was NULL" (AggregateFunctionFirstRowNull, flag 2:
+ * a NULL first row makes the result NULL and later rows do not replace it). */
+static int is_ord_kind(int k) { return k == TFG_AGG_MIN || k == TFG_AGG_MAX || k == TFG_AGG_FIRST_ROW; }
+static void ord_offer(orc_agg *a, int i, int64_t g, int t, const void *p, size_t r, int is_null)
+{
+    const int k = a->kinds[i];
+    if (k == TFG_AGG_FIRST_ROW) {
+        if (a->cnt[i][g] || a->acc_w[i][4 * g]) return; /* changeFirstTime: only the first row */
+        if (is_null) { a->acc_w[i][4 * g] = 1; return; }
+        if (is_float(t)) a->acc_f[i][g] = load_f(t, p, r);
+        else a->acc_i[i][g] = is_unsigned(t) ? (__int128)(uint64_t)load_s(t, p, r) : (__int128)load_s(t, p, r);
+        a->cnt[i][g] = 1;
+        return;
+    }
+    if (is_null) return; /* AggregateFunctionNullUnary skips NULL rows */
+    const int have = a->cnt[i][g] != 0;
+    if (is_float(t)) {
+        const double v = load_f(t, p, r), cur = a->acc_f[i][g];
+        if (!have || (k == TFG_AGG_MIN ? v < cur : v > cur)) a->acc_f[i][g] = v;
+    } else {
+        const __int128 v = is_unsigned(t) ? (__int128)(uint64_t)load_s(t, p, r) : (__int128)load_s(t, p, r);
+        const __int128 cur = a->acc_i[i][g];
+        if (!have || (k == TFG_AGG_MIN ? v < cur : v > cur)) a->acc_i[i][g] = v;
+    }
+    a->cnt[i][g]++;
+}
+/* merge of one group's state (changeIfLess(to) / changeIfGreater(to) / changeFirstTime(to)) */
+static void ord_merge(orc_agg *dst, int i, int64_t d, const orc_agg *src, int64_t g)
+{
+    const int k = dst->kinds[i], t = dst->arg_types[i];
+    const int dh = dst->cnt[i][d] != 0 || dst->acc_w[i][4 * d], sh = src->cnt[i][g] != 0 || src->acc_w[i][4 * g];
+    if (!sh) return;
+    if (k == TFG_AGG_FIRST_ROW) {
+        if (dh) return;
+        dst->cnt[i][d] = src->cnt[i][g];
+        dst->acc_w[i][4 * d] = src->acc_w[i][4 * g];
+        dst->acc_i[i][d] = src->acc_i[i][g];
+        dst->acc_f[i][d] = src->acc_f[i][g];
+        return;
+    }
+    const int take = !dst->cnt[i][d] ||
+                     (is_float(t) ? (k == TFG_AGG_MIN ? src->acc_f[i][g] < dst->acc_f[i][d] : src->acc_f[i][g] > dst->acc_f[i][d])
+                                  : (k == TFG_AGG_MIN ? src->acc_i[i][g] < dst->acc_i[i][d] : src->acc_i[i][g] > dst->acc_i[i][d]));
+    if (take) {
+        dst->acc_i[i][d] = src->acc_i[i][g];
+        dst->acc_f[i][d] = src->acc_f[i][g];
+    }
+    dst->cnt[i][d] += src->cnt[i][g];
+}
+
 /* Aggregator::executeOnBlock -> handleOneBatch (Interpreters/Aggregator.cpp:852-1024):
  * emplace key, then IAggregateFunction::addBatch in row order (IAggregateFunction.h:242-266);
  * AggregateFunctionSumData::add (AggregateFunctionSum.h:64-80); count (AggregateFunctionCount.h:46);
@@ -812,6 +865,10 @@ void orc_agg_consume(orc_agg *a, const void *keys, const uint8_t *key_null, cons
         int64_t g = agg_lookup(a, key, kn);
         for (int i = 0; i < a->n_aggs; ++i) {
             if (a->kinds[i] == TFG_AGG_COUNT_ALL) { a->cnt[i][g]++; continue; }
+            if (is_ord_kind(a->kinds[i])) {
+                ord_offer(a, i, g, a->arg_types[i], args[i], r, arg_nulls && arg_nulls[i] && arg_nulls[i][r]);
+                continue;
+            }
             if (arg_nulls && arg_nulls[i] && arg_nulls[i][r]) continue;
             a->cnt[i][g]++;
             if (a->kinds[i] == TFG_AGG_COUNT) continue;
@@ -832,6 +889,10 @@ void orc_agg_merge(orc_agg *dst, const orc_agg *src)
     for (size_t g = 0; g < src->n_groups; ++g) {
         int64_t d = agg_lookup(dst, src->gkeys[g], src->gkey_null[g]);
         for (int i = 0; i < dst->n_aggs; ++i) {
+            if (is_ord_kind(dst->kinds[i])) {
+                ord_merge(dst, i, d, src, g);
+                continue;
+            }
             dst->cnt[i][d] += src->cnt[i][g];
             dst->acc_f[i][d] += src->acc_f[i][g];
             dst->acc_i[i][d] = (__int128)((unsigned __int128)dst->acc_i[i][d] + (unsigned __int128)src->acc_i[i][g]);
@@ -857,6 +918,22 @@ void orc_agg_result(const orc_agg *a, uint64_t *out_keys, uint8_t *out_key_null,
         for (int i = 0; i < a->n_aggs; ++i) {
             if (out_state_null && out_state_null[i]) out_state_null[i][g] = a->cnt[i][g] == 0;
             if (!out_states || !out_states[i]) continue;
+            if (is_ord_kind(a->kinds[i])) { /* the argument's type and width */
+                const int t = a->arg_types[i];
+                char *o = (char *)out_states[i];
+                if (t == TFG_FLOAT64) ((double *)o)[g] = a->acc_f[i][g];
+                else if (t == TFG_FLOAT32) ((float *)o)[g] = (float)a->acc_f[i][g];
+                else {
+                    const int64_t v = (int64_t)a->acc_i[i][g];
+                    switch (t) {
+                    case TFG_INT8: case TFG_UINT8: ((uint8_t *)o)[g] = (uint8_t)v; break;
+                    case TFG_INT16: case TFG_UINT16: ((uint16_t *)o)[g] = (uint16_t)v; break;
+                    case TFG_INT32: case TFG_UINT32: case TFG_DECIMAL32: ((uint32_t *)o)[g] = (uint32_t)v; break;
+                    default: ((int64_t *)o)[g] = v; break;
+                    }
+                }
+                continue;
+            }
             if (a->kinds[i] != TFG_AGG_SUM) { ((uint64_t *)out_states[i])[g] = a->cnt[i][g]; continue; }
             int t = a->arg_types[i];
             if (is_float(t)) ((double *)out_states[i])[g] = a->acc_f[i][g];

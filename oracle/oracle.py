@@ -20,6 +20,10 @@ INT8, INT16, INT32, INT64, UINT8, UINT16, UINT32, UINT64, FLOAT32, FLOAT64 = ran
 DECIMAL32, DECIMAL64, DECIMAL128, DECIMAL256 = 11, 12, 13, 14
 STRING = 20
 NULLABLE = 0x100
+AGG_SUM, AGG_COUNT, AGG_COUNT_ALL, AGG_MIN, AGG_MAX, AGG_FIRST_ROW = range(6)
+NP_DTYPE = {INT8: np.int8, INT16: np.int16, INT32: np.int32, INT64: np.int64, UINT8: np.uint8, UINT16: np.uint16,
+            UINT32: np.uint32, UINT64: np.uint64, FLOAT32: np.float32, FLOAT64: np.float64, DECIMAL32: np.int32,
+            DECIMAL64: np.int64}
 
 
 def prec(t: int, p: int) -> int:
@@ -269,7 +273,9 @@ class Agg:
         states, snull = [], []
         for kind, t in self.aggs:
             limbs = sum_limbs(kind, t)
-            if kind != 0:
+            if kind in (AGG_MIN, AGG_MAX, AGG_FIRST_ROW):  # the argument's type
+                states.append(np.empty(g, dtype=NP_DTYPE[t & 0xFF]))
+            elif kind != 0:
                 states.append(np.empty(g, dtype=np.uint64))
             elif (t & 0xFF) in (FLOAT32, FLOAT64):
                 states.append(np.empty(g, dtype=np.float64))
@@ -356,7 +362,9 @@ class AggKeys:
         for kind, t in self.aggs:
             limbs = sum_limbs(kind, t)
             t &= 0xFF
-            if limbs > 1:
+            if kind in (AGG_MIN, AGG_MAX, AGG_FIRST_ROW):  # the argument's type
+                states.append(np.zeros(max(g, 1), NP_DTYPE[t]))
+            elif limbs > 1:
                 states.append(np.zeros((max(g, 1), limbs), np.int64))
             elif kind == 0 and t in (FLOAT32, FLOAT64):
                 states.append(np.zeros(max(g, 1), np.float64))
@@ -375,7 +383,9 @@ class AggKeys:
         for kind, t in self.aggs:
             limbs = sum_limbs(kind, t)
             t &= 0xFF
-            if limbs > 1:
+            if kind in (AGG_MIN, AGG_MAX, AGG_FIRST_ROW):  # the argument's type
+                states.append(np.zeros(max(g, 1), NP_DTYPE[t]))
+            elif limbs > 1:
                 states.append(np.zeros((max(g, 1), limbs), np.int64))
             elif kind == 0 and t in (FLOAT32, FLOAT64):
                 states.append(np.zeros(max(g, 1), np.float64))

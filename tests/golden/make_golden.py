@@ -121,8 +121,20 @@ def aggregate_cases():
         {"func": "count(pr)", "group_by": ["country"], "expected": [4, 3, 1, 1]},
     ]
     test_table = {"s1": [1, 2, 3], "s2": [1, 2, 3]}  # :102-106
+    # AggregationMaxAndMin (:503-545): max / min of a nullable column per group, expected values in
+    # unspecified group order (N = a group whose values are all NULL)
+    min_max = [
+        {"func": "max(age)", "group_by": ["country"], "expected": [36, 32, 30, N]},
+        {"func": "max(salary)", "group_by": ["country", "gender"], "expected": [2000.7, 1300.2, 1000.1, 0.3, -300.8, N]},
+        {"func": "min(age)", "group_by": ["country"], "expected": [30, 25, 22, N]},
+        {"func": "min(salary)", "group_by": ["country", "gender"], "expected": [1300.2, 1000.1, 900.5, -200.4, -999.6, N]},
+    ]
+    # AggKeyOptimization case 1 (:1053-1137): 1024 rows, four groups of 256 rows (col_int = i,
+    # col_tinyint = i): count(1), first_row(col_tinyint) GROUP BY col_int, col_tinyint
+    first_row = {"rows": 1024, "row_types": 4, "count": [256, 256, 256, 256], "first_row_tinyint": [0, 1, 2, 3]}
     return {"clerk": clerk, "counts": counts, "test_table": test_table,
-            "sums": [{"func": "sum(s2)", "group_by": [], "expected": [6]}]}  # :755-757
+            "sums": [{"func": "sum(s2)", "group_by": [], "expected": [6]}],  # :755-757
+            "min_max": min_max, "first_row": first_row}
 
 
 def sum_type_cases():

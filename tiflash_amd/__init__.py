@@ -42,7 +42,7 @@ def prec(t: int, p: int) -> int:
 EQ, NE, LT, LE, GT, GE = range(6)
 PLUS, MINUS, MULTIPLY = range(3)
 AND, OR, NOT = range(3)
-AGG_SUM, AGG_COUNT, AGG_COUNT_ALL = range(3)
+AGG_SUM, AGG_COUNT, AGG_COUNT_ALL, AGG_MIN, AGG_MAX, AGG_FIRST_ROW = range(6)
 JOIN_INNER, JOIN_LEFT, JOIN_SEMI, JOIN_ANTI = range(4)
 JOIN_V2_TAGGED = 1  # tfg_join_create_v2 flags
 COLLATOR_NONE, COLLATOR_BINARY, COLLATOR_BIN_PADDING, COLLATOR_GENERAL_CI, COLLATOR_UNICODE_CI, COLLATOR_UCA0900_AI_CI = range(6)
@@ -457,6 +457,8 @@ class Aggregator:
             s = _empty(g, w.value, dev)
             if t.value == FLOAT64:
                 s = s.view(torch.float64)
+            elif t.value == FLOAT32:
+                s = s.view(torch.float32)
             states.append(s)
             snulls.append(torch.empty(max(g, 1), dtype=torch.uint8, device=dev)[:g])
         cnt = ctypes.c_uint64()
@@ -553,6 +555,8 @@ class KeysAggregator(Aggregator):
             s = _empty(g, w.value, dev)
             if t.value == FLOAT64:
                 s = s.view(torch.float64)
+            elif t.value == FLOAT32:
+                s = s.view(torch.float32)
             states.append(s)
             snulls.append(torch.empty(max(g, 1), dtype=torch.uint8, device=dev)[:g])
         cnt, chars = ctypes.c_uint64(), ctypes.c_uint64()

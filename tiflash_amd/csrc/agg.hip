@@ -75,6 +75,12 @@ __global__ void __launch_bounds__(NK_T) agg_nokey_kernel(AggSpec S, RowsIO rows,
         for (int i = 0; i < S.n_aggs; ++i) {
             if (mode == MODE_RAW && S.kind[i] == TFG_AGG_COUNT_ALL) { p.cnt[i]++; continue; }
             if (rows.val_null[i] && rows.val_null[i][r]) continue;
+            if (S.acc[i] == ACC_ORD) { // min / max / first_row: running max of order keys
+                const uint64_t k = ord_enc(S.kind[i], S.src_type[i], load_bits(rows.val[i], val_width(S, mode, i), r));
+                p.lo[i] = k > p.lo[i] ? k : p.lo[i];
+                p.cnt[i]++;
+                continue;
+            }
             if (S.kind[i] != TFG_AGG_SUM) {
                 p.cnt[i] += mode == MODE_RAW ? 1 : ((const uint64_t *)rows.val[i])[r];
                 continue;
@@ -111,6 +117,8 @@ __global__ void __launch_bounds__(NK_T) agg_nokey_kernel(AggSpec S, RowsIO rows,
                 if (S.acc[i] == ACC_I256) {
                     const uint64_t q[4] = {red[t].lo[i], red[t].hi[i], red[t].x2[i], red[t].x3[i]};
                     nk_add(s, i, q);
+                } else if (S.acc[i] == ACC_ORD) {
+                    s.lo[i] = red[t].lo[i] > s.lo[i] ? red[t].lo[i] : s.lo[i];
                 } else {
                     const uint64_t o = s.lo[i];
                     s.lo[i] += red[t].lo[i];
@@ -138,6 +146,10 @@ __global__ void agg_nokey_fold_kernel(AggSpec S, const NoKeyPartial *partials, i
                 a[0] += p.lo[i];
                 a[1] += p.hi[i] + (a[0] < o ? 1 : 0);
             } else if (S.acc[i] == ACC_I64) ((uint64_t *)st.acc[i])[0] += p.lo[i];
+            else if (S.acc[i] == ACC_ORD) {
+                uint64_t *a = (uint64_t *)st.acc[i];
+                if (p.lo[i] > a[0]) a[0] = p.lo[i];
+            }
             if (S.has_cnt[i]) st.cnt[i][0] += p.cnt[i];
         }
 }
@@ -164,7 +176,15 @@ __global__ void agg_result_kernel(AggSpec S, GroupsIO st, uint64_t n, int key_wi
         }
         if (out_key_null) out_key_null[g] = st.key_null[g];
         for (int i = 0; i < S.n_aggs; ++i) {
-            if (res.state[i]) {
+            if (res.state[i] && S.acc[i] == ACC_ORD) { // min / max / first_row: the argument's width
+                const uint64_t x = ord_dec(S.kind[i], S.src_type[i], ((const uint64_t *)st.acc[i])[g]);
+                switch (val_width(S, MODE_RAW, i)) {
+                case 1: ((uint8_t *)res.state[i])[g] = (uint8_t)x; break;
+                case 2: ((uint16_t *)res.state[i])[g] = (uint16_t)x; break;
+                case 4: ((uint32_t *)res.state[i])[g] = (uint32_t)x; break;
+                default: ((uint64_t *)res.state[i])[g] = x; break;
+                }
+            } else if (res.state[i]) {
                 if (S.kind[i] != TFG_AGG_SUM) ((uint64_t *)res.state[i])[g] = st.cnt[i][g];
                 else if (S.acc[i] == ACC_I256) {
                     ((uint4 *)res.state[i])[2 * g] = ((const uint4 *)st.acc[i])[2 * g];
@@ -173,7 +193,7 @@ __global__ void agg_result_kernel(AggSpec S, GroupsIO st, uint64_t n, int key_wi
                 else ((uint64_t *)res.state[i])[g] = ((const uint64_t *)st.acc[i])[g];
             }
             if (res.state_null[i])
-                res.state_null[i][g] = (S.kind[i] == TFG_AGG_SUM && S.has_cnt[i]) ? (st.cnt[i][g] == 0) : 0;
+                res.state_null[i][g] = ((S.kind[i] == TFG_AGG_SUM || S.acc[i] == ACC_ORD) && S.has_cnt[i]) ? (st.cnt[i][g] == 0) : 0;
         }
     }
 }
@@ -190,6 +210,10 @@ __global__ void agg_state_add_kernel(AggSpec S, GroupsIO dst, GroupsIO src) { //
             a[0] += b[0];
             a[1] += b[1] + (a[0] < o ? 1 : 0);
         } else if (S.acc[i] == ACC_I64) ((uint64_t *)dst.acc[i])[0] += ((const uint64_t *)src.acc[i])[0];
+        else if (S.acc[i] == ACC_ORD) {
+            const uint64_t b = ((const uint64_t *)src.acc[i])[0];
+            if (b > ((uint64_t *)dst.acc[i])[0]) ((uint64_t *)dst.acc[i])[0] = b;
+        }
         if (S.has_cnt[i]) dst.cnt[i][0] += src.cnt[i][0];
     }
 }
@@ -1017,7 +1041,7 @@ int consume_keyed(tfg_agg *a, int mode, const RowPred &pred, const void *keys, i
         if (val_nulls && val_nulls[i]) o_vnull[i] = cv.take<uint8_t>(n);
         if (val_cnts && val_cnts[i]) o_vcnt[i] = cv.take<uint64_t>(n);
         if (!vals[i]) continue;
-        if (mode == MODE_RAW) vw[i] = (int)type_width(S.src_type[i]);
+        if (mode == MODE_RAW || (mode == MODE_PARTIAL && S.acc[i] == ACC_ORD)) vw[i] = (int)type_width(S.src_type[i]);
         else vw[i] = 8 * std::max(1, acc_words(S.acc[i]));
         o_val[i] = cv.take<uint4>((n * vw[i] + 15) / 16);
     }
@@ -1206,7 +1230,7 @@ int consume_common(tfg_agg *a, int mode, const RowPred &pred, const void *keys, 
         TFG_CHECK(args && args[i], TFG_ERR_INVALID_ARG, "argument %d is null", i);
         vals[i] = args[i];
         vnull[i] = arg_nullmaps ? arg_nullmaps[i] : nullptr;
-        if (vnull[i] && mode == MODE_RAW && a->S.kind[i] == TFG_AGG_SUM && !a->S.has_cnt[i])
+        if (vnull[i] && mode == MODE_RAW && (a->S.kind[i] == TFG_AGG_SUM || a->S.acc[i] == ACC_ORD) && !a->S.has_cnt[i])
             return fail(TFG_ERR_ILLEGAL_TYPE, "argument %d has a null map but was declared not nullable", i);
     }
     if (a->nokey) return consume_nokey(a, mode, pred, vals, vnull, n);
@@ -1365,7 +1389,7 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
             delete a;
             return fail(TFG_ERR_ILLEGAL_TYPE, "decimal precision %d of argument %d exceeds 65", TFG_ARG_PREC_OF(arg_types[i]), i);
         }
-        if (kind < TFG_AGG_SUM || kind > TFG_AGG_COUNT_ALL) {
+        if (kind < TFG_AGG_SUM || kind > TFG_AGG_FIRST_ROW) {
             delete a;
             return fail(TFG_ERR_NOT_IMPLEMENTED, "aggregate kind %d not supported", kind);
         }
@@ -1386,6 +1410,17 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
                                 : is_unsigned_type(at) ? TFG_UINT64 : TFG_INT64;
             a->result_width[i] = 8 * acc_words(S.acc[i]);
             cell += 8 * acc_words(S.acc[i]);
+        } else if (kind == TFG_AGG_MIN || kind == TFG_AGG_MAX || kind == TFG_AGG_FIRST_ROW) {
+            if (!(is_fixed_numeric(at) || at == TFG_DECIMAL32 || at == TFG_DECIMAL64)) {
+                delete a;
+                return fail(at == TFG_DECIMAL128 || at == TFG_DECIMAL256 ? TFG_ERR_NOT_IMPLEMENTED : TFG_ERR_ILLEGAL_TYPE,
+                            "min / max / first_row over type %d not supported", at);
+            }
+            S.acc[i] = ACC_ORD;
+            S.has_cnt[i] = nullable ? 1 : 0; // NULL result for a group of NULLs only
+            a->result_type[i] = at;
+            a->result_width[i] = (int)type_width(at);
+            cell += 8;
         } else {
             S.acc[i] = ACC_NONE;
             S.has_cnt[i] = 1;

@@ -17,7 +17,7 @@ constexpr int BT_BIG = 1024; // for tables too large for two workgroups per CU (
 constexpr int LDS_TABLE_BYTES = 100 * 1024;  // preferred table size (two workgroups per CU)
 constexpr int LDS_TABLE_MAX = 150 * 1024;    // largest table (one 16-wave workgroup per CU)
 
-enum AccKind { ACC_NONE = 0, ACC_I64 = 1, ACC_F64 = 2, ACC_I128 = 3, ACC_I256 = 4 };
+enum AccKind { ACC_NONE = 0, ACC_I64 = 1, ACC_F64 = 2, ACC_I128 = 3, ACC_I256 = 4, ACC_ORD = 5 };
 // 64-bit words of an accumulator of kind k
 __host__ __device__ constexpr int acc_words(int k) { return k == ACC_I256 ? 4 : k == ACC_I128 ? 2 : k == ACC_NONE ? 0 : 1; }
 enum RowMode { MODE_RAW = 0, MODE_PARTIAL = 1, MODE_STATE = 2 };
@@ -98,6 +98,56 @@ __device__ __forceinline__ void load_sum_value(int type, const void *p, int64_t 
     default: lo = 0; break;
     }
     hi = (int64_t)lo < 0 ? ~0ull : 0ull; // sign extension into Int128
+}
+
+// min / max / first_row (ACC_ORD): the state is one u64 "order key" combined by unsigned max
+// (ds_max_u64 / atomicMax), identity 0 — so a zeroed cell is an empty state and partial states merge
+// by the same max.  ord_base maps a value to a u64 in the value's order (signed: flip the sign bit;
+// floats: IEEE total order, Float32 widened exactly to Float64); max keeps it, min keeps its
+// complement, first_row keeps the max (any row of the group is a valid first row).
+__host__ __device__ __forceinline__ uint64_t ord_base(int type, uint64_t bits) {
+    switch (type) {
+    case TFG_INT8: return (uint64_t)(int64_t)(int8_t)bits ^ 0x8000000000000000ull;
+    case TFG_INT16: return (uint64_t)(int64_t)(int16_t)bits ^ 0x8000000000000000ull;
+    case TFG_INT32: case TFG_DECIMAL32: return (uint64_t)(int64_t)(int32_t)bits ^ 0x8000000000000000ull;
+    case TFG_INT64: case TFG_DECIMAL64: return bits ^ 0x8000000000000000ull;
+    case TFG_FLOAT32: case TFG_FLOAT64: {
+        uint64_t b = bits;
+        if (type == TFG_FLOAT32) {
+            float f;
+            uint32_t u = (uint32_t)bits;
+            memcpy(&f, &u, 4);
+            const double d = (double)f;
+            memcpy(&b, &d, 8);
+        }
+        return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+    }
+    default: return bits; // unsigned: zero-extended
+    }
+}
+__host__ __device__ __forceinline__ uint64_t ord_unbase(int type, uint64_t k) {
+    switch (type) {
+    case TFG_INT8: case TFG_INT16: case TFG_INT32: case TFG_DECIMAL32: case TFG_INT64: case TFG_DECIMAL64:
+        return k ^ 0x8000000000000000ull; // sign-extended; the caller stores the type's width
+    case TFG_FLOAT32: case TFG_FLOAT64: {
+        const uint64_t b = (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k;
+        if (type == TFG_FLOAT64) return b;
+        double d;
+        memcpy(&d, &b, 8);
+        const float f = (float)d; // exact: the value was a Float32
+        uint32_t u;
+        memcpy(&u, &f, 4);
+        return u;
+    }
+    default: return k;
+    }
+}
+__host__ __device__ __forceinline__ uint64_t ord_enc(int kind, int type, uint64_t bits) {
+    const uint64_t b = ord_base(type, bits);
+    return kind == TFG_AGG_MIN ? ~b : b;
+}
+__host__ __device__ __forceinline__ uint64_t ord_dec(int kind, int type, uint64_t k) {
+    return ord_unbase(type, kind == TFG_AGG_MIN ? ~k : k);
 }
 
 __device__ __forceinline__ void lds_add_i128(uint64_t *cell, uint64_t lo, uint64_t hi) {
@@ -467,6 +517,17 @@ struct Table {
 #pragma unroll
         for (int i = 0; i < NA; ++i) {
             const int kind = S.kind[i];
+            if (S.acc[i] == ACC_ORD) { // min / max / first_row: max of order keys
+                if (mode == MODE_STATE) {
+                    atomicMax((unsigned long long *)acc_cell(i, cell), (unsigned long long)v.lo[i]);
+                    if (S.has_cnt[i]) atomicAdd((unsigned long long *)cnt_cell(i, cell), (unsigned long long)v.cnt[i]);
+                    continue;
+                }
+                if (v.vnull[i]) continue;
+                atomicMax((unsigned long long *)acc_cell(i, cell), (unsigned long long)ord_enc(kind, S.src_type[i], v.lo[i]));
+                if (S.has_cnt[i]) atomicAdd((unsigned long long *)cnt_cell(i, cell), 1ull);
+                continue;
+            }
             if (mode == MODE_STATE) {
                 if constexpr (W)
                     if (S.acc[i] == ACC_I256) lds_add_i256(acc_cell(i, cell), v.lo[i], v.hi[i], v.x2[i], v.x3[i]);
@@ -522,6 +583,8 @@ struct Table {
                 atomicAdd((double *)acc_cell(i, cell), ((const double *)grp.acc[i])[g]);
             } else if (S.acc[i] == ACC_I64) {
                 atomicAdd((unsigned long long *)acc_cell(i, cell), ((const unsigned long long *)grp.acc[i])[g]);
+            } else if (S.acc[i] == ACC_ORD) {
+                atomicMax((unsigned long long *)acc_cell(i, cell), ((const unsigned long long *)grp.acc[i])[g]);
             }
             if (S.has_cnt[i]) atomicAdd((unsigned long long *)cnt_cell(i, cell), grp.cnt[i][g]);
         }
@@ -565,6 +628,8 @@ struct Table {
 
 // width in bytes of value column i for a row mode
 __device__ __forceinline__ int val_width(const AggSpec &S, int mode, int i) {
+    // partial min / max / first_row values have the argument's type (the result type)
+    if (mode == MODE_PARTIAL && S.acc[i] == ACC_ORD) mode = MODE_RAW;
     if (mode != MODE_RAW) return S.acc[i] == ACC_I256 ? 32 : S.acc[i] == ACC_I128 ? 16 : 8;
     switch (S.src_type[i]) {
     case TFG_DECIMAL256: return 32;

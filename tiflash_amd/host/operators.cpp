@@ -27,7 +27,22 @@ Aggregator::Aggregator(Context &ctx, const Params &params) : ctx_(ctx), params_(
     for (const auto &d : params_.aggregates) {
         int kind;
         DataType at;
-        if (d.function == "sum") {
+        int ref = -1;
+        if (d.function == "first_row" && d.argument_names.size() == 1)
+            for (size_t j = 0; j < params_.keys.size(); ++j)
+                if (params_.keys[j] == d.argument_names[0]) ref = (int)j;
+        ref_key_.push_back(ref);
+        if (ref >= 0) { // first_row of a key: the key column itself, nothing on the device
+            dev_index_.push_back(-1);
+            continue;
+        }
+        dev_index_.push_back((int)kinds_.size());
+        if (d.function == "min" || d.function == "max" || d.function == "first_row") {
+            if (d.argument_names.size() != 1)
+                throw Exception(d.function + " takes one argument", ErrorCodes::BAD_ARGUMENTS);
+            kind = d.function == "min" ? TFG_AGG_MIN : d.function == "max" ? TFG_AGG_MAX : TFG_AGG_FIRST_ROW;
+            at = params_.src_header.getByName(d.argument_names[0]).type;
+        } else if (d.function == "sum") {
             if (d.argument_names.size() != 1)
                 throw Exception("sum takes one argument", ErrorCodes::BAD_ARGUMENTS);
             kind = TFG_AGG_SUM;
@@ -49,6 +64,13 @@ Aggregator::Aggregator(Context &ctx, const Params &params) : ctx_(ctx), params_(
                                 : (at.type | (at.nullable ? TFG_ARG_NULLABLE : 0) |
                                    (at.isDecimal() ? TFG_ARG_PREC(at.precision()) : 0)));
         arg_scales.push_back(at.scale);
+    }
+    if (kinds_.empty()) { // only key references: the device aggregator still needs one aggregate
+        hidden_count_ = true;
+        kinds_.push_back(TFG_AGG_COUNT_ALL);
+        arg_types_.push_back(DataType{});
+        arg_types.push_back(0);
+        arg_scales.push_back(0);
     }
     tfg_agg_params p{params_.bucket_bits, params_.expected_groups};
     if (packed_) {
@@ -81,8 +103,10 @@ Aggregator::~Aggregator() {
 
 void Aggregator::argPointers(const Block &b, std::vector<const void *> &args, std::vector<const uint8_t *> &nulls,
                              std::vector<ColumnPtr> &hold) const {
-    for (size_t i = 0; i < params_.aggregates.size(); ++i) {
-        if (kinds_[i] == TFG_AGG_COUNT_ALL) {
+    for (size_t i = 0; i < params_.aggregates.size() + (hidden_count_ ? 1 : 0); ++i) {
+        if (i < params_.aggregates.size() && dev_index_[i] < 0) continue; // a key reference
+        const int k = hidden_count_ ? TFG_AGG_COUNT_ALL : kinds_[dev_index_[i]];
+        if (k == TFG_AGG_COUNT_ALL) {
             args.push_back(nullptr);
             nulls.push_back(nullptr);
             continue;
@@ -150,11 +174,18 @@ void Aggregator::mergeOnBlock(const Block &partial) {
     std::vector<const void *> states;
     std::vector<const uint8_t *> nulls;
     std::vector<ColumnPtr> hold;
-    for (const auto &d : params_.aggregates) {
-        ColumnPtr c = materialize(ctx_, partial.getByName(d.column_name).column);
+    for (size_t i = 0; i < params_.aggregates.size(); ++i) {
+        if (dev_index_[i] < 0) continue; // a key reference: the keys carry it
+        ColumnPtr c = materialize(ctx_, partial.getByName(params_.aggregates[i].column_name).column);
         hold.push_back(c);
         states.push_back(c->dataPtr());
         nulls.push_back(c->nullPtr());
+    }
+    std::shared_ptr<DeviceBuffer> zeros;
+    if (hidden_count_) { // partial counts of the hidden count(): never output, any value will do
+        zeros = std::make_shared<DeviceBuffer>(ctx_, std::max<size_t>(n, 1) * 8);
+        states.push_back(zeros->data());
+        nulls.push_back(nullptr);
     }
     if (packed_) {
         std::vector<const void *> kc;
@@ -198,17 +229,21 @@ Block Aggregator::convertToBlock(bool final) const {
     std::vector<std::shared_ptr<IColumn>> states;
     std::vector<void *> sp;
     std::vector<uint8_t *> snp;
-    for (size_t i = 0; i < params_.aggregates.size(); ++i) {
+    for (size_t i = 0; i < kinds_.size(); ++i) { // the device aggregates
         int t = 0, w = 0;
         check(tfg_agg_result_type(agg_, (int)i, &t, &w), "tfg_agg_result_type");
         auto c = std::make_shared<IColumn>();
+        const bool ord = kinds_[i] == TFG_AGG_MIN || kinds_[i] == TFG_AGG_MAX || kinds_[i] == TFG_AGG_FIRST_ROW;
         c->type.type = t;
-        c->type.scale = kinds_[i] == TFG_AGG_SUM ? arg_types_[i].scale : 0;
+        c->type.scale = kinds_[i] == TFG_AGG_SUM || ord ? arg_types_[i].scale : 0;
+        if (ord) c->type.prec = arg_types_[i].prec; // min / max / first_row: the argument's type
         // sum(Decimal(p, s)) -> Decimal(min(p + 22, 65), s) (SumDecimalInferer, Common/Decimal.h:156-163)
         if (kinds_[i] == TFG_AGG_SUM && arg_types_[i].isDecimal())
             c->type.prec = std::min(arg_types_[i].precision() + 22, 65);
-        // sum over a nullable argument is Nullable (AggregateFunctionNullUnary); count never is
-        c->type.nullable = kinds_[i] == TFG_AGG_SUM && arg_types_[i].nullable;
+        // sum / min / max over a nullable argument are Nullable (AggregateFunctionNullUnary);
+        // first_row always is (AggregateFunctionFirstRowNull, the reference's first_row column
+        // types: gtest_aggregation_executor.cpp:1129); count never is
+        c->type.nullable = ((kinds_[i] == TFG_AGG_SUM || ord) && arg_types_[i].nullable) || kinds_[i] == TFG_AGG_FIRST_ROW;
         c->rows = g;
         c->data = std::make_shared<DeviceBuffer>(ctx_, g * (size_t)w);
         if (c->type.nullable) c->nullmap = std::make_shared<DeviceBuffer>(ctx_, g);
@@ -263,8 +298,7 @@ Block Aggregator::convertToBlock(bool final) const {
                 c->chars = end;
             }
         for (size_t j = 0; j < kcols.size(); ++j) out.insert({kcols[j], kcols[j]->type, params_.keys[j]});
-        for (size_t i = 0; i < states.size(); ++i)
-            out.insert({states[i], states[i]->type, params_.aggregates[i].column_name});
+        insertAggregateColumns(out, states, std::vector<ColumnPtr>(kcols.begin(), kcols.end()), g);
         return out;
     }
     check(tfg_agg_result(agg_, key ? key->data->data() : nullptr, key && key->nullmap ? (uint8_t *)key->nullmap->data() : nullptr,
@@ -272,9 +306,32 @@ Block Aggregator::convertToBlock(bool final) const {
           "tfg_agg_result");
     ctx_.sync();
     if (key) out.insert({key, key->type, params_.keys[0]});
-    for (size_t i = 0; i < states.size(); ++i)
-        out.insert({states[i], states[i]->type, params_.aggregates[i].column_name});
+    insertAggregateColumns(out, states, key ? std::vector<ColumnPtr>{key} : std::vector<ColumnPtr>{}, g);
     return out;
+}
+
+// aggregate columns in their declared order: a device aggregate's result, or (first_row of a
+// GROUP BY column) the key column itself, Nullable like every first_row result
+void Aggregator::insertAggregateColumns(Block &out, const std::vector<std::shared_ptr<IColumn>> &states,
+                                        const std::vector<ColumnPtr> &keys, size_t g) const {
+    for (size_t i = 0; i < params_.aggregates.size(); ++i) {
+        const std::string &name = params_.aggregates[i].column_name;
+        if (dev_index_[i] >= 0) {
+            out.insert({states[dev_index_[i]], states[dev_index_[i]]->type, name});
+            continue;
+        }
+        ColumnPtr k = keys.at(ref_key_[i]);
+        if (k->type.nullable) {
+            out.insert({k, k->type, name});
+            continue;
+        }
+        auto c = std::make_shared<IColumn>(*k); // shares the key's buffers
+        c->type.nullable = true;
+        c->nullmap = std::make_shared<DeviceBuffer>(ctx_, std::max<size_t>(g, 1));
+        const std::vector<uint8_t> zero(std::max<size_t>(g, 1), 0);
+        check(tfg_upload(ctx_.raw(), c->nullmap->data(), zero.data(), zero.size()), "tfg_upload");
+        out.insert({c, c->type, name});
+    }
 }
 
 // ================================================================ Join

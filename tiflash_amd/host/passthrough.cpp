@@ -28,7 +28,7 @@ size_t AutoPassThroughHashAggContext::hashMapBytes() const {
 // the map's cells plus one aggregate-state record per group (the Arena's share)
 size_t AutoPassThroughHashAggContext::revocableBytes() const {
     size_t state = 0;
-    for (const auto &d : params_.aggregates) state += d.function == "sum" ? 16 : 8;
+    for (const auto &d : params_.aggregates) state += d.function == "sum" ? 16 : 8; // min / max / first_row: 8
     return hashMapBytes() + agg_.size() * state;
 }
 
@@ -119,6 +119,17 @@ Block AutoPassThroughHashAggContext::getPassThroughBlock(const Block &block) con
             continue;
         }
         ColumnPtr arg = materialize(ctx_, block.getByName(d.argument_names[0]).column);
+        if (d.function == "min" || d.function == "max" || d.function == "first_row") { // the value itself
+            auto v = std::make_shared<IColumn>(*arg); // shares the argument's buffers
+            v->type = rt;
+            if (rt.nullable && !v->nullmap) {
+                v->nullmap = std::make_shared<DeviceBuffer>(ctx_, std::max<size_t>(n, 1));
+                const std::vector<uint8_t> zero(std::max<size_t>(n, 1), 0);
+                check(tfg_upload(ctx_.raw(), v->nullmap->data(), zero.data(), zero.size()), "tfg_upload");
+            }
+            out.insert({v, v->type, d.column_name});
+            continue;
+        }
         c->data = std::make_shared<DeviceBuffer>(ctx_, std::max<size_t>(n, 1) * std::max<size_t>(rt.width(), 1));
         if (d.function == "count") { // count(x) -> 1, 0 where x is NULL
             c->type.type = TFG_UINT64;

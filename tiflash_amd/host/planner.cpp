@@ -60,6 +60,15 @@ Expr Expr::sum(Expr arg) {
     e.children.push_back(std::move(arg));
     return e;
 }
+static Expr unaryAgg(ExprType tp, Expr arg) {
+    Expr e;
+    e.tp = tp;
+    e.children.push_back(std::move(arg));
+    return e;
+}
+Expr Expr::min(Expr arg) { return unaryAgg(ExprType::Min, std::move(arg)); }
+Expr Expr::max(Expr arg) { return unaryAgg(ExprType::Max, std::move(arg)); }
+Expr Expr::firstRow(Expr arg) { return unaryAgg(ExprType::First, std::move(arg)); }
 Expr Expr::count() {
     Expr e;
     e.tp = ExprType::Count;
@@ -342,6 +351,11 @@ AggPlan planAggregation(Context &ctx, const dag::Executor &e, const Block &heade
         } else if (f.tp == ExprType::Count) {
             if (f.children.size() > 1) throw Exception("count takes at most one argument", ErrorCodes::BAD_ARGUMENTS);
             d.function = "count";
+        } else if (f.tp == ExprType::Min || f.tp == ExprType::Max || f.tp == ExprType::First) {
+            // AggregateFunctionMinMaxAny.cpp:155-159 (tipb Min / Max / First -> min / max / first_row,
+            // DAGUtils.cpp:69)
+            d.function = f.tp == ExprType::Min ? "min" : f.tp == ExprType::Max ? "max" : "first_row";
+            if (f.children.size() != 1) throw Exception(d.function + " needs one argument", ErrorCodes::BAD_ARGUMENTS);
         } else {
             unsupported("this aggregate function");
         }

@@ -34,7 +34,7 @@
 namespace tfa {
 namespace dag {
 
-enum class ExprType { ColumnRef, Int64, Uint64, Float64, MysqlDecimal, ScalarFunc, Sum, Count };
+enum class ExprType { ColumnRef, Int64, Uint64, Float64, MysqlDecimal, ScalarFunc, Sum, Count, Min, Max, First };
 
 // the tipb::ScalarFuncSig values on the path (DAGUtils.cpp scalar_func_map names their functions)
 enum class ScalarFuncSig {
@@ -50,7 +50,7 @@ struct Expr {
     int64_t column = 0;         // ColumnRef: offset in the child's output schema
     Field literal;              // Int64 / Uint64 / Float64 / MysqlDecimal
     ScalarFuncSig sig = ScalarFuncSig::LTInt;
-    std::vector<Expr> children; // ScalarFunc operands; Sum / Count arguments (count(*): none)
+    std::vector<Expr> children; // ScalarFunc operands; aggregate arguments (count(*): none)
 
     static Expr col(int64_t offset);
     static Expr i64(int64_t v);
@@ -61,6 +61,10 @@ struct Expr {
     static Expr sum(Expr arg);
     static Expr count();          // count(*)
     static Expr count(Expr arg);  // count(arg): non-NULL values
+    // tipb::ExprType::Min / Max / First (first_row: TiDB's GROUP BY output columns, DAGUtils.cpp:69)
+    static Expr min(Expr arg);
+    static Expr max(Expr arg);
+    static Expr firstRow(Expr arg);
 };
 
 enum class ExecType { TypeTableScan, TypeSelection, TypeAggregation, TypeJoin, TypeExchangeSender, TypeExchangeReceiver, TypeProjection };

@@ -269,7 +269,7 @@ private:
 
 // ---------------------------------------------------------------- aggregation (a9-a17)
 struct AggregateDescription {
-    std::string function;                    // "sum" | "count"
+    std::string function;                    // "sum" | "count" | "min" | "max" | "first_row"
     std::vector<std::string> argument_names; // count() has none
     std::string column_name;
 };
@@ -312,10 +312,17 @@ private:
     DataType key_type_;
     std::vector<DataType> key_types_; // every key (packed methods)
     bool packed_ = false;             // keys128 / key_string through tfg_agg_*_keys
-    std::vector<int> kinds_;
-    std::vector<DataType> arg_types_;
+    std::vector<int> kinds_;          // device aggregates (tfg_agg_kind)
+    std::vector<DataType> arg_types_; // ... and their argument types
+    // aggregate i -> its device aggregate, or -1 for first_row of a GROUP BY column, which is the
+    // key itself (agg_func_ref_key: AggKeyOptimization, gtest_aggregation_executor.cpp:1053-1137)
+    std::vector<int> dev_index_;
+    std::vector<int> ref_key_; // aggregate i -> the key index it repeats (-1: none)
+    bool hidden_count_ = false; // every aggregate repeats a key: the device aggregator counts rows
     void argPointers(const Block &b, std::vector<const void *> &args, std::vector<const uint8_t *> &nulls,
                      std::vector<ColumnPtr> &hold) const;
+    void insertAggregateColumns(Block &out, const std::vector<std::shared_ptr<IColumn>> &states,
+                                const std::vector<ColumnPtr> &keys, size_t g) const;
     void keyPointers(const Block &b, std::vector<const void *> &cols, std::vector<const uint64_t *> &offs,
                      std::vector<const uint8_t *> &nulls, std::vector<ColumnPtr> &hold) const;
 };
