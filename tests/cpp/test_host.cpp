@@ -608,6 +608,82 @@ TEST(HashPartitionWriterKnownAnswer) {
     EXPECT(sends == parts); // 4096 rows < 8192 * P: one flush
 }
 
+// FineGrainedShuffleWriter: the reference's known answers (gtest_mpp_exchange_writer.cpp:391-450,
+// 542-607, numbers in tests/golden/reference_cases.json "fine_grained"): blocks of ten Int64
+// columns 0..rows-1 partitioned on column 0, P = 4, S = 8.
+//  * testBatchWriteFineGrainedShuffle: 1024 rows < batch 4096 * 8 -> one packet per partition,
+//    S chunks each (stream ids 0..7), every chunk 1024 / 32 rows;
+//  * testFineGrainedShuffleWriter(V1): 64 blocks of 64 rows + 64 empty blocks, batch 108 ->
+//    1024 rows per partition and 512 rows per stream id over all packets.
+TEST(FineGrainedShuffleWriterKnownAnswers) {
+    Json fx = load_fixture();
+    const Json &fg = fx["fine_grained"];
+    const uint32_t P = (uint32_t)fg["parts"].num, S = (uint32_t)fg["streams"].num;
+    DataType i64;
+    auto block_of = [&](size_t rows) {
+        std::vector<int64_t> v(std::max<size_t>(rows, 1));
+        for (size_t i = 0; i < rows; ++i) v[i] = (int64_t)i;
+        Block b;
+        for (int c = 0; c < 10; ++c) b.insert({makeColumn(ctx, i64, v.data(), rows), i64, "col" + std::to_string(c)});
+        return b;
+    };
+    { // one batch
+        g_current = "FineGrainedShuffleWriter one batch";
+        const Json &c = fg["batch"];
+        Block block = block_of((size_t)c["block_rows"].num);
+        std::map<uint32_t, FineGrainedPacket> report;
+        FineGrainedShuffleWriter w(ctx, {0}, P, S, (uint64_t)c["batch_size"].num, [&](uint32_t p, FineGrainedPacket &&pk) {
+            EXPECT(report.count(p) == 0); // a single flush: one packet per partition
+            report[p] = std::move(pk);
+        });
+        w.write(block);
+        w.flush();
+        EXPECT(report.size() == P);
+        size_t chunks = 0;
+        for (auto &kv : report) {
+            EXPECT(kv.second.chunks.size() == S && kv.second.stream_ids.size() == S);
+            for (size_t i = 0; i < kv.second.chunks.size(); ++i) {
+                Block d = CHBlockChunkCodecV1::decode(ctx, block.cloneEmpty(), kv.second.chunks[i]);
+                EXPECT(d.rows() == (size_t)c["rows_per_chunk"].num);
+                EXPECT(kv.second.stream_ids[i] == i);
+                ++chunks;
+            }
+        }
+        EXPECT(chunks == (size_t)P * S);
+    }
+    { // many small blocks, empty ones among them
+        g_current = "FineGrainedShuffleWriter many blocks";
+        const Json &c = fg["blocks"];
+        const size_t rows = (size_t)c["block_rows"].num, nblocks = (size_t)c["block_num"].num;
+        std::vector<size_t> part_rows(P, 0), stream_rows(S, 0);
+        size_t packets = 0;
+        Block header = block_of(0).cloneEmpty();
+        FineGrainedShuffleWriter w(ctx, {0}, P, S, (uint64_t)c["batch_size"].num, [&](uint32_t p, FineGrainedPacket &&pk) {
+            ++packets;
+            EXPECT(pk.chunks.size() == pk.stream_ids.size());
+            for (size_t i = 0; i < pk.chunks.size(); ++i) {
+                Block d = CHBlockChunkCodecV1::decode(ctx, header, pk.chunks[i]);
+                part_rows[p] += d.rows();
+                stream_rows[pk.stream_ids[i]] += d.rows();
+                // every row of the chunk routes to (p, stream id) under the reference's selector
+                std::vector<int64_t> k = toHost<int64_t>(ctx, *d.getByName("col0").column);
+                for (int64_t x : k) {
+                    const uint32_t h = orc_crc32c_u64(0xFFFFFFFFu, (uint64_t)x); // intHashCRC32: crc32q
+                    EXPECT((uint32_t)(((uint64_t)h * P) >> 32) == p && h % S == pk.stream_ids[i]);
+                }
+            }
+        });
+        for (size_t i = 0; i < nblocks; ++i) {
+            w.write(block_of(rows));
+            w.write(block_of(0));
+        }
+        w.flush();
+        for (uint32_t p = 0; p < P; ++p) EXPECT(part_rows[p] == (size_t)c["rows_per_part"].num);
+        for (uint32_t s = 0; s < S; ++s) EXPECT(stream_rows[s] == (size_t)c["rows_per_stream"].num);
+        EXPECT(packets % P == 0 && packets > P); // several flushes, P packets each
+    }
+}
+
 // one-rank RCCL exchange (the N>1 path runs in the multi-GPU bench): identity
 TEST(MPPExchangeSingleRank) {
     uint8_t id[128];
@@ -2254,6 +2330,102 @@ TEST(PlanExchange) {
         for (Block blk; recv->tryPop(blk);) local += blk ? blk.rows() : 0;
         EXPECT(local == n);
         EXPECT(bc ? (rows[1] == n && rows[2] == n) : (rows[1] == 0 && rows[2] == 0));
+    }
+}
+
+// ExchangeSender with fine_grained_shuffle_stream_count = 4 from a descriptor: the sink op runs a
+// FineGrainedShuffleWriter; the local partition's blocks reach the receiver tagged with their
+// streams (every row of stream s has weak hash % 4 == s and partition 0), the remote partition's
+// rows are the partition's rows, and a fine-grained receiver plan (concurrency 4, one stream per
+// source) aggregates the local partition exactly.
+TEST(PlanExchangeFineGrained) {
+    using namespace dag;
+    std::mt19937_64 rng(204);
+    const size_t n = 30000;
+    const uint32_t P = 2, S = 4;
+    std::vector<int64_t> k(n), v(n);
+    for (size_t i = 0; i < n; ++i) {
+        k[i] = (int64_t)(rng() % 4000) - 2000;
+        v[i] = (int64_t)(rng() % 1000);
+    }
+    DataType i64;
+    Block b{{makeColumn(ctx, i64, k.data(), n), i64, "k"}, {makeColumn(ctx, i64, v.data(), n), i64, "v"}};
+    auto part_of = [&](int64_t x, uint32_t &stream) {
+        const uint32_t h = orc_crc32c_u64(0xFFFFFFFFu, (uint64_t)x);
+        stream = h % S;
+        return (uint32_t)(((uint64_t)h * P) >> 32);
+    };
+    std::map<int64_t, std::pair<int64_t, uint64_t>> exp_local;
+    size_t remote_want = 0;
+    for (size_t i = 0; i < n; ++i) {
+        uint32_t s;
+        if (part_of(k[i], s) == 0) {
+            exp_local[k[i]].first += v[i];
+            exp_local[k[i]].second += 1;
+        } else {
+            ++remote_want;
+        }
+    }
+    auto run_sender = [&](std::shared_ptr<ExchangeReceiver> receiver, size_t &remote_rows) {
+        PlanContext env;
+        env.tables["t"] = {b.cloneEmpty(), splitBlocks(ctx, b, 6)};
+        env.tunnels = std::make_shared<MPPTunnelSet>(ctx, P, 2, receiver, nullptr, 0,
+                                                     [&](uint32_t part, Block &&blk) {
+                                                         EXPECT(part == 1);
+                                                         remote_rows += blk.rows();
+                                                     });
+        Executor root = Executor::exchangeSender("exchange_sender_1", ExchangeType::Hash, {Expr::col(0)},
+                                                 Executor::tableScan("ts_0", "t"));
+        root.fine_grained_shuffle_stream_count = S;
+        root.fine_grained_shuffle_batch_size = 1000;
+        PipelineExecutorContext exec;
+        PhysicalPlan plan(ctx, exec, env);
+        plan.build(root);
+        plan.execute();
+        EXPECT(receiver->finished());
+    };
+    { // the streams as the receiver holds them
+        g_current = "PlanExchangeFineGrained streams";
+        auto receiver = std::make_shared<ExchangeReceiver>();
+        size_t remote_rows = 0;
+        run_sender(receiver, remote_rows);
+        EXPECT(remote_rows == remote_want);
+        size_t local_rows = 0;
+        for (uint32_t s = 0; s < S; ++s)
+            for (Block blk; receiver->tryPop(blk, S, s);) {
+                std::vector<int64_t> kk = toHost<int64_t>(ctx, *blk.getByName("k").column);
+                for (int64_t x : kk) {
+                    uint32_t st;
+                    EXPECT(part_of(x, st) == 0 && st == s);
+                }
+                local_rows += kk.size();
+            }
+        EXPECT(local_rows == n - remote_want);
+    }
+    { // a fine-grained receiver plan: GROUP BY k over the local partition, one stream per source
+        g_current = "PlanExchangeFineGrained receiver plan";
+        auto receiver = std::make_shared<ExchangeReceiver>();
+        size_t remote_rows = 0;
+        run_sender(receiver, remote_rows);
+        PlanContext env2;
+        env2.concurrency = S;
+        env2.receivers["exchange_receiver_0"] = {b.cloneEmpty(), receiver};
+        std::vector<Block> res;
+        env2.result = [&](const Block &r) { res.push_back(r); };
+        Executor recv = Executor::exchangeReceiver("exchange_receiver_0", "exchange_receiver_0");
+        recv.fine_grained_shuffle_stream_count = S;
+        PipelineExecutorContext exec;
+        PhysicalPlan plan(ctx, exec, env2);
+        plan.build(Executor::aggregation("agg_1", {Expr::col(0)}, {Expr::sum(Expr::col(1)), Expr::count()}, recv));
+        plan.execute();
+        std::map<int64_t, std::pair<int64_t, uint64_t>> got;
+        for (const Block &r : res) {
+            auto rs = toHost<int64_t>(ctx, *r.safeGetByPosition(0).column);
+            auto rc = toHost<uint64_t>(ctx, *r.safeGetByPosition(1).column);
+            auto rk = toHost<int64_t>(ctx, *r.safeGetByPosition(2).column);
+            for (size_t i = 0; i < rk.size(); ++i) got[rk[i]] = {rs[i], rc[i]};
+        }
+        EXPECT(got == exp_local);
     }
 }
 

@@ -204,6 +204,12 @@ if __name__ == "__main__":
     with open(os.path.join(HERE, "reference_cases.json"), "w") as f:
         json.dump({"groupby": groupby_cases(), "groupby_keys": groupby_keys_cases(), "join": join_cases(),
                    "exchange": {"block_rows": 64, "blocks": 64, "parts": 4, "rows_per_part": 1024},
+                   # gtest_mpp_exchange_writer.cpp:391-450 (testBatchWriteFineGrainedShuffle) and
+                   # :542-607 (testFineGrainedShuffleWriter): P = 4, S = 8, partition column 0
+                   "fine_grained": {"parts": 4, "streams": 8,
+                                    "batch": {"block_rows": 1024, "batch_size": 4096, "rows_per_chunk": 32},
+                                    "blocks": {"block_rows": 64, "block_num": 64, "batch_size": 108,
+                                               "rows_per_part": 1024, "rows_per_stream": 512}},
                    "aggregates": aggregate_cases(), "sum_types": sum_type_cases(),
                    "general_ci": general_ci_cases(), **uca_cases()}, f, indent=1)
     with open(os.path.join(HERE, "crc_vectors.json"), "w") as f:

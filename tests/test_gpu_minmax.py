@@ -38,9 +38,11 @@ def _by_key(keys, states, nulls):
     return out
 
 
-def _dev_result(res, nullable):
+def _dev_result(res, nullable, types=None):
     keys = res["keys"].cpu().numpy()
     states = [s.cpu().numpy() for s in res["states"]]
+    if types:  # the argument's numpy type (UInt64 results come back in an int64 tensor)
+        states = [s.view(NP[t & 0xFF]) for s, t in zip(states, types)]
     nulls = [res["state_null"][i].cpu().numpy() if nullable[i] else None for i in range(len(states))]
     return _by_key(keys, states, nulls)
 
@@ -86,7 +88,7 @@ def test_min_max_vs_oracle(tfa, ctx, dev, orc, n, groups):
         agg = tfa.Aggregator(ctx, tfa.INT64, aggs)
         agg.consume(_t(k, dev), [_t(a, dev) for a in args[sl]],
                     arg_nullmaps=[_t(x, dev) if x is not None else None for x in nulls[sl]])
-        g = _dev_result(agg.result(), nullable[sl])
+        g = _dev_result(agg.result(), nullable[sl], TYPES[sl])
         agg.close()
         ref = orc.Agg(orc.INT64, aggs)
         ref.consume(k, args[sl], arg_nulls=nulls[sl])
@@ -187,11 +189,11 @@ def test_min_max_two_phase_and_merge(tfa, ctx, dev, orc):
     for a in parts:
         r = a.result()
         fin.consume_partial(r["keys"], r["states"], state_nullmaps=r["state_null"])
-    assert _dev_result(fin.result(), nullable) == exp
+    assert _dev_result(fin.result(), nullable, types) == exp
     fin.close()
     # merge of the two aggregators' states
     parts[0].merge(parts[1])
-    assert _dev_result(parts[0].result(), nullable) == exp
+    assert _dev_result(parts[0].result(), nullable, types) == exp
     for a in parts:
         a.close()
 

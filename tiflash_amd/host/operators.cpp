@@ -656,14 +656,18 @@ Block Join::joinBlock(const Block &probe_block) {
 // selective rows only, HashBaseWriterHelper.cpp:110-130), fillSelector, the stable partition
 // permutation (IColumn::scatter's order), mapped back to block rows through the selective
 // list, then every column gathered per partition (:176-200).
+// fine_grained_stream_count S > 0: partition_num * S buckets, bucket = part * S + hash % S
+// (fillSelectorForFineGrainedShuffle, HashBaseWriterHelper.cpp:64-84)
 static std::vector<Block> hashPartitionBlockGather(Context &ctx, const Block &block, const std::vector<size_t> &key_ids,
-                                                   uint32_t partition_num, const std::vector<int> &collators) {
+                                                   uint32_t partition_num, const std::vector<int> &collators,
+                                                   uint32_t fine_grained_stream_count = 0) {
+    const uint32_t buckets = partition_num * std::max<uint32_t>(fine_grained_stream_count, 1);
     const BlockSelectivePtr &selp = block.info.selective;
     const uint64_t *sel = selp ? selp->data() : nullptr;
     const size_t n = selp ? selp->size() : block.rows();
     DeviceBuffer h(ctx, std::max<size_t>(n, 1) * 4), selector(ctx, std::max<size_t>(n, 1) * 4),
-        perm(ctx, std::max<size_t>(n, 1) * 4), offs_dev(ctx, (partition_num + 1) * 8);
-    std::vector<uint64_t> offs(partition_num + 1, 0);
+        perm(ctx, std::max<size_t>(n, 1) * 4), offs_dev(ctx, (buckets + 1) * 8);
+    std::vector<uint64_t> offs(buckets + 1, 0);
     if (n) {
         check(tfg_weak_hash_init(ctx.raw(), (uint32_t *)h.data(), (int64_t)n), "tfg_weak_hash_init");
         for (size_t k = 0; k < key_ids.size(); ++k) {
@@ -680,18 +684,18 @@ static std::vector<Block> hashPartitionBlockGather(Context &ctx, const Block &bl
                                                      (int64_t)n, (uint32_t *)h.data()),
                       "tfg_weak_hash_update");
         }
-        check(tfg_fill_selector(ctx.raw(), (const uint32_t *)h.data(), (int64_t)n, partition_num, 0,
-                                (uint32_t *)selector.data()),
+        check(tfg_fill_selector(ctx.raw(), (const uint32_t *)h.data(), (int64_t)n, partition_num,
+                                fine_grained_stream_count, (uint32_t *)selector.data()),
               "tfg_fill_selector");
     }
-    check(tfg_partition(ctx.raw(), (const uint32_t *)selector.data(), (int64_t)n, partition_num,
+    check(tfg_partition(ctx.raw(), (const uint32_t *)selector.data(), (int64_t)n, buckets,
                         (uint32_t *)perm.data(), (uint64_t *)offs_dev.data(), offs.data()),
           "tfg_partition");
     if (sel && n) // positions among the selective rows -> block rows
         check(tfg_selective_perm(ctx.raw(), sel, (const uint32_t *)perm.data(), (int64_t)n, (uint32_t *)perm.data()),
               "tfg_selective_perm");
-    std::vector<Block> parts(partition_num);
-    for (uint32_t p = 0; p < partition_num; ++p) {
+    std::vector<Block> parts(buckets);
+    for (uint32_t p = 0; p < buckets; ++p) {
         const uint32_t *pp = (const uint32_t *)perm.data() + offs[p];
         const size_t rows = offs[p + 1] - offs[p];
         for (const auto &c : block.getColumnsWithTypeAndName()) {
@@ -790,6 +794,78 @@ void HashPartitionWriter::flush() {
     pending_rows_ = 0;
     std::vector<Block> parts = hashPartitionBlock(ctx_, all, partition_col_ids_, partition_num_, collators_);
     for (uint32_t p = 0; p < partition_num_; ++p) sink_(p, std::move(parts[p]));
+}
+
+std::vector<Block> fineGrainedPartitionBlock(Context &ctx, const Block &block, const std::vector<size_t> &key_ids,
+                                             uint32_t partition_num, uint32_t stream_count,
+                                             const std::vector<int> &collators) {
+    if (stream_count == 0 || stream_count > 1024)
+        throw Exception("fine_grained_shuffle_stream_count must be in (0, 1024]", ErrorCodes::BAD_ARGUMENTS);
+    return hashPartitionBlockGather(ctx, block, key_ids, partition_num, collators, stream_count);
+}
+
+// ================================================================ FineGrainedShuffleWriter
+FineGrainedShuffleWriter::FineGrainedShuffleWriter(Context &ctx, std::vector<size_t> partition_col_ids,
+                                                   uint32_t partition_num, uint32_t stream_count, uint64_t batch_size,
+                                                   Sink sink, uint64_t max_buffered_bytes)
+    : ctx_(ctx), partition_col_ids_(std::move(partition_col_ids)), partition_num_(partition_num),
+      stream_count_(stream_count), max_buffered_rows_(batch_size * stream_count), max_buffered_bytes_(max_buffered_bytes),
+      sink_(std::move(sink)) {
+    if (partition_num_ == 0) throw Exception("partition_num must be positive", ErrorCodes::BAD_ARGUMENTS);
+    if (stream_count_ == 0 || stream_count_ > 1024)
+        throw Exception("fine_grained_shuffle_stream_count must be in (0, 1024]", ErrorCodes::BAD_ARGUMENTS);
+}
+
+// FineGrainedShuffleWriter::write (FineGrainedShuffleWriter.cpp:117-141): rows are buffered; a
+// flush follows when the buffer reaches batch_size * stream_count rows or max_buffered_bytes, or
+// holds stream_count blocks
+void FineGrainedShuffleWriter::write(const Block &block) {
+    if (!header_set_ && block) {
+        header_ = block.cloneEmpty();
+        header_set_ = true;
+    }
+    const size_t rows = block.info.selective ? block.info.selective->size() : block.rows();
+    if (rows > 0) {
+        buffered_rows_ += rows;
+        for (const auto &c : block.getColumnsWithTypeAndName()) {
+            ColumnPtr m = c.column;
+            buffered_bytes_ += (m->data ? m->data->bytes() : 0) + (m->offsets ? m->offsets->bytes() : 0) +
+                               (m->nullmap ? m->nullmap->bytes() : 0);
+        }
+        blocks_.push_back(block);
+    }
+    if (buffered_rows_ >= max_buffered_rows_ || buffered_bytes_ >= max_buffered_bytes_ || blocks_.size() == stream_count_)
+        flush();
+}
+
+// batchWriteFineGrainedShuffle (:159-228): every buffered block scattered into partition_num *
+// stream_count buckets (weak hash of the partition columns -> fine-grained selector), then one
+// packet per partition holding the non-empty buckets of its streams as V1 chunks with their
+// stream ids (MPPTunnelSetHelper::ToFineGrainedPacket)
+void FineGrainedShuffleWriter::flush() {
+    if (buffered_rows_ == 0) return;
+    const uint32_t nb = partition_num_ * stream_count_;
+    std::vector<std::vector<Block>> pieces(nb);
+    for (const Block &b : blocks_) {
+        std::vector<Block> parts = hashPartitionBlockGather(ctx_, b, partition_col_ids_, partition_num_, collators_, stream_count_);
+        for (uint32_t k = 0; k < nb; ++k)
+            if (parts[k].rows()) pieces[k].push_back(std::move(parts[k]));
+    }
+    blocks_.clear();
+    buffered_rows_ = buffered_bytes_ = 0;
+    for (uint32_t p = 0; p < partition_num_; ++p) {
+        FineGrainedPacket packet;
+        for (uint32_t s = 0; s < stream_count_; ++s) {
+            const std::vector<Block> &v = pieces[p * stream_count_ + s];
+            if (v.empty()) continue; // empty chunks are not sent
+            CHBlockChunkCodecV1 codec(ctx_, header_);
+            DevicePacket chunk = codec.encode(v);
+            if (chunk.empty()) continue;
+            packet.chunks.push_back(std::move(chunk));
+            packet.stream_ids.push_back(s);
+        }
+        sink_(p, std::move(packet));
+    }
 }
 
 MPPExchange::MPPExchange(Context &ctx, int nranks, int rank, const uint8_t *unique_id, size_t id_len)

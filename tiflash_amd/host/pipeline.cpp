@@ -523,9 +523,9 @@ OperatorStatus HashJoinProbeTransformOp::tryOutputImpl(Block &block) {
 }
 
 // ================================================================ exchange
-void ExchangeReceiver::push(Block block) {
+void ExchangeReceiver::push(Block block, uint32_t stream) {
     std::lock_guard<std::mutex> g(mu_);
-    queue_.push_back(std::move(block));
+    queue_.emplace_back(stream, std::move(block));
 }
 
 void ExchangeReceiver::finish() { finished_ = true; }
@@ -533,16 +533,28 @@ void ExchangeReceiver::finish() { finished_ = true; }
 bool ExchangeReceiver::tryPop(Block &block) {
     std::lock_guard<std::mutex> g(mu_);
     if (queue_.empty()) return false;
-    block = std::move(queue_.front());
+    block = std::move(queue_.front().second);
     queue_.pop_front();
     return true;
+}
+
+bool ExchangeReceiver::tryPop(Block &block, uint32_t stride, uint32_t index) {
+    if (stride == 0) return tryPop(block);
+    std::lock_guard<std::mutex> g(mu_);
+    for (auto it = queue_.begin(); it != queue_.end(); ++it)
+        if (it->first % stride == index) {
+            block = std::move(it->second);
+            queue_.erase(it);
+            return true;
+        }
+    return false;
 }
 
 MPPTunnelSet::MPPTunnelSet(Context &ctx, uint32_t partition_num, size_t sender_concurrency, ExchangeReceiverPtr receiver,
                            MPPExchange *exchange, uint32_t local_partition, RemoteSink remote)
     : ctx_(ctx), partition_num_(partition_num), active_(std::max<size_t>(sender_concurrency, 1)),
       receiver_(std::move(receiver)), exchange_(exchange), local_partition_(local_partition), remote_(std::move(remote)),
-      parts_(partition_num) {
+      parts_(partition_num), streams_(partition_num) {
     if (partition_num == 0) throw Exception("partition_num must be positive", ErrorCodes::BAD_ARGUMENTS);
     if (exchange_ && (uint32_t)exchange_->nranks() != partition_num)
         throw Exception("an MPP exchange sends one partition per rank", ErrorCodes::BAD_ARGUMENTS);
@@ -550,27 +562,34 @@ MPPTunnelSet::MPPTunnelSet(Context &ctx, uint32_t partition_num, size_t sender_c
         throw Exception("local partition out of range", ErrorCodes::BAD_ARGUMENTS);
 }
 
-void MPPTunnelSet::write(uint32_t part, Block &&block) {
+void MPPTunnelSet::write(uint32_t part, Block &&block, uint32_t stream) {
     if (part >= partition_num_) throw Exception("partition out of range", ErrorCodes::BAD_ARGUMENTS);
     std::lock_guard<std::mutex> g(mu_);
+    if (exchange_ && stream != 0) // the RCCL all-to-all moves one block per rank, without stream ids
+        throw Exception("fine-grained shuffle over the RCCL exchange", ErrorCodes::NOT_IMPLEMENTED);
     if (!exchange_ && part != local_partition_) {
         if (remote_) remote_(part, std::move(block));
         return;
     }
     parts_[part].push_back(std::move(block));
+    streams_[part].push_back(stream);
 }
 
 void MPPTunnelSet::finishOneSender() {
     std::vector<std::vector<Block>> parts;
+    std::vector<std::vector<uint32_t>> streams;
     {
         std::lock_guard<std::mutex> g(mu_);
         if (active_ == 0) throw Exception("finishOneSender called too often", ErrorCodes::LOGICAL_ERROR);
         if (--active_ > 0) return;
         parts.swap(parts_);
+        streams.swap(streams_);
     }
     if (!exchange_) {
-        for (Block &b : parts[local_partition_])
-            if (b && b.rows()) receiver_->push(std::move(b));
+        for (size_t i = 0; i < parts[local_partition_].size(); ++i) {
+            Block &b = parts[local_partition_][i];
+            if (b && b.rows()) receiver_->push(std::move(b), streams[local_partition_][i]);
+        }
         receiver_->finish();
         return;
     }
@@ -594,12 +613,27 @@ void MPPTunnelSet::finishOneSender() {
 
 ExchangeSenderSinkOp::ExchangeSenderSinkOp(PipelineExecutorContext &exec, Context &ctx, MPPTunnelSetPtr tunnels,
                                            std::vector<size_t> partition_col_ids, std::vector<int> collators,
-                                           int64_t batch_send_min_limit)
+                                           int64_t batch_send_min_limit, uint32_t fine_grained_stream_count,
+                                           uint64_t fine_grained_batch_size)
     : SinkOp(exec, ctx), tunnels_(std::move(tunnels)), partition_col_ids_(std::move(partition_col_ids)),
-      collators_(std::move(collators)), limit_(batch_send_min_limit) {}
+      collators_(std::move(collators)), limit_(batch_send_min_limit), fg_streams_(fine_grained_stream_count),
+      fg_batch_(fine_grained_batch_size) {}
 
 void ExchangeSenderSinkOp::operatePrefixImpl() {
     MPPTunnelSet *t = tunnels_.get();
+    if (fg_streams_ > 0) { // each packet's chunks reach the tunnel as blocks tagged with their stream ids
+        Context &ctx = ctx_;
+        auto header = std::make_shared<Block>();
+        fg_writer_ = std::make_unique<FineGrainedShuffleWriter>(
+            ctx_, partition_col_ids_, t->partitionNum(), fg_streams_, fg_batch_,
+            [t, &ctx, header](uint32_t part, FineGrainedPacket &&pk) {
+                for (size_t i = 0; i < pk.chunks.size(); ++i)
+                    t->write(part, CHBlockChunkCodecV1::decode(ctx, *header, pk.chunks[i]), pk.stream_ids[i]);
+            });
+        fg_header_ = header;
+        fg_writer_->setCollators(collators_);
+        return;
+    }
     writer_ = std::make_unique<HashPartitionWriter>(
         ctx_, partition_col_ids_, t->partitionNum(), [t](uint32_t part, Block &&b) { t->write(part, std::move(b)); },
         limit_);
@@ -608,7 +642,18 @@ void ExchangeSenderSinkOp::operatePrefixImpl() {
 
 // ExchangeSenderSinkOp::writeImpl: rows to the writer; the end-of-input block flushes
 OperatorStatus ExchangeSenderSinkOp::writeImpl(Block &&block) {
-    if (!writer_) operatePrefixImpl();
+    if (!writer_ && !fg_writer_) operatePrefixImpl();
+    if (fg_writer_) {
+        if (block) {
+            if (!*fg_header_) *fg_header_ = block.cloneEmpty();
+            total_rows_ += block.rows();
+            fg_writer_->write(block);
+            return OperatorStatus::NEED_INPUT;
+        }
+        fg_writer_->flush();
+        tunnels_->finishOneSender();
+        return OperatorStatus::FINISHED;
+    }
     if (block) {
         total_rows_ += block.rows();
         writer_->write(block);
@@ -620,8 +665,9 @@ OperatorStatus ExchangeSenderSinkOp::writeImpl(Block &&block) {
 }
 
 ExchangeReceiverSourceOp::ExchangeReceiverSourceOp(PipelineExecutorContext &exec, Context &ctx,
-                                                   ExchangeReceiverPtr receiver, Block header)
-    : SourceOp(exec, ctx), receiver_(std::move(receiver)) {
+                                                   ExchangeReceiverPtr receiver, Block header, uint32_t stride,
+                                                   uint32_t index)
+    : SourceOp(exec, ctx), receiver_(std::move(receiver)), stride_(stride), index_(index) {
     setHeader(header.cloneEmpty());
 }
 
@@ -631,9 +677,9 @@ OperatorStatus ExchangeReceiverSourceOp::readImpl(Block &block) {
         has_next_ = false;
         return OperatorStatus::HAS_OUTPUT;
     }
-    if (receiver_->tryPop(block)) return OperatorStatus::HAS_OUTPUT;
+    if (receiver_->tryPop(block, stride_, index_)) return OperatorStatus::HAS_OUTPUT;
     if (receiver_->finished()) { // drained after the last sender finished: end of input
-        if (receiver_->tryPop(block)) return OperatorStatus::HAS_OUTPUT;
+        if (receiver_->tryPop(block, stride_, index_)) return OperatorStatus::HAS_OUTPUT;
         block = Block();
         return OperatorStatus::HAS_OUTPUT;
     }
@@ -641,7 +687,7 @@ OperatorStatus ExchangeReceiverSourceOp::readImpl(Block &block) {
 }
 
 OperatorStatus ExchangeReceiverSourceOp::awaitImpl() {
-    if (!has_next_ && receiver_->tryPop(next_)) has_next_ = true;
+    if (!has_next_ && receiver_->tryPop(next_, stride_, index_)) has_next_ = true;
     return has_next_ || receiver_->finished() ? OperatorStatus::HAS_OUTPUT : OperatorStatus::WAITING;
 }
 

@@ -372,14 +372,19 @@ private:
 // pipeline pop from it).  finish() marks the end of every sender's stream.
 class ExchangeReceiver {
 public:
-    void push(Block block);
+    // stream: the fine-grained shuffle stream id of the chunk the block came in (0 otherwise);
+    // the reference routes such chunks to per-stream channels (ExchangeReceiver.cpp, fine-grained
+    // msg channels), read by the stream's own source
+    void push(Block block, uint32_t stream = 0);
     void finish();
     bool tryPop(Block &block); // false when nothing is queued
+    // the first queued block of a stream s with s % stride == index (fine-grained sources)
+    bool tryPop(Block &block, uint32_t stride, uint32_t index);
     bool finished() const { return finished_; }
 
 private:
     std::mutex mu_;
-    std::deque<Block> queue_;
+    std::deque<std::pair<uint32_t, Block>> queue_;
     std::atomic<bool> finished_{false};
 };
 using ExchangeReceiverPtr = std::shared_ptr<ExchangeReceiver>;
@@ -394,7 +399,7 @@ public:
     using RemoteSink = std::function<void(uint32_t, Block &&)>;
     MPPTunnelSet(Context &ctx, uint32_t partition_num, size_t sender_concurrency, ExchangeReceiverPtr receiver,
                  MPPExchange *exchange = nullptr, uint32_t local_partition = 0, RemoteSink remote = nullptr);
-    void write(uint32_t part, Block &&block);
+    void write(uint32_t part, Block &&block, uint32_t stream = 0); // stream: fine-grained stream id
     void finishOneSender(); // the last one sends
     uint32_t partitionNum() const { return partition_num_; }
 
@@ -407,6 +412,7 @@ private:
     uint32_t local_partition_;
     RemoteSink remote_;
     std::vector<std::vector<Block>> parts_;
+    std::vector<std::vector<uint32_t>> streams_; // the stream id of each block of parts_
     std::mutex mu_;
 };
 using MPPTunnelSetPtr = std::shared_ptr<MPPTunnelSet>;
@@ -416,9 +422,12 @@ using MPPTunnelSetPtr = std::shared_ptr<MPPTunnelSet>;
 // to the tunnels; the end-of-input block flushes.
 class ExchangeSenderSinkOp : public SinkOp {
 public:
+    // fine_grained_stream_count > 0: a FineGrainedShuffleWriter (newMPPExchangeWriter.cpp:66-78)
+    // with batches of fine_grained_batch_size rows per stream
     ExchangeSenderSinkOp(PipelineExecutorContext &exec, Context &ctx, MPPTunnelSetPtr tunnels,
                          std::vector<size_t> partition_col_ids, std::vector<int> collators = {},
-                         int64_t batch_send_min_limit = -1);
+                         int64_t batch_send_min_limit = -1, uint32_t fine_grained_stream_count = 0,
+                         uint64_t fine_grained_batch_size = 8192);
     std::string getName() const override { return "ExchangeSenderSinkOp"; }
     uint64_t totalRows() const { return total_rows_; }
 
@@ -429,15 +438,21 @@ protected:
 private:
     MPPTunnelSetPtr tunnels_;
     std::unique_ptr<HashPartitionWriter> writer_;
+    std::unique_ptr<FineGrainedShuffleWriter> fg_writer_;
+    std::shared_ptr<Block> fg_header_; // the chunks' schema (the first block's), shared with the sink
     std::vector<size_t> partition_col_ids_;
     std::vector<int> collators_;
     int64_t limit_;
+    uint32_t fg_streams_;
+    uint64_t fg_batch_;
     uint64_t total_rows_ = 0;
 };
 
 class ExchangeReceiverSourceOp : public SourceOp {
 public:
-    ExchangeReceiverSourceOp(PipelineExecutorContext &exec, Context &ctx, ExchangeReceiverPtr receiver, Block header);
+    // stride > 0: reads only the fine-grained streams s with s % stride == index
+    ExchangeReceiverSourceOp(PipelineExecutorContext &exec, Context &ctx, ExchangeReceiverPtr receiver, Block header,
+                             uint32_t stride = 0, uint32_t index = 0);
     std::string getName() const override { return "ExchangeReceiverSourceOp"; }
 
 protected:
@@ -446,6 +461,7 @@ protected:
 
 private:
     ExchangeReceiverPtr receiver_;
+    uint32_t stride_, index_;
     Block next_;
     bool has_next_ = false;
 };

@@ -594,8 +594,10 @@ PhysicalPlan::Stage PhysicalPlan::lower(const dag::Executor &e) {
         s.header = it->second.header.cloneEmpty();
         const Block h = s.header;
         ExchangeReceiverPtr q = it->second.queue;
-        s.source = [&exec, &ctx, h, q](size_t) -> SourceOpPtr {
-            return std::make_unique<ExchangeReceiverSourceOp>(exec, ctx, q, h);
+        // fine-grained shuffle: PipelineExec i reads the streams s with s % concurrency == i
+        const uint32_t stride = e.fine_grained_shuffle_stream_count ? (uint32_t)std::max<size_t>(env_.concurrency, 1) : 0;
+        s.source = [&exec, &ctx, h, q, stride](size_t i) -> SourceOpPtr {
+            return std::make_unique<ExchangeReceiverSourceOp>(exec, ctx, q, h, stride, stride ? (uint32_t)i : 0);
         };
         s.ops.push_back("ExchangeReceiverSourceOp");
         return s;
@@ -706,8 +708,10 @@ void PhysicalPlan::build(const dag::Executor &root) {
                 ids.push_back((size_t)k.column);
             }
             std::vector<int> coll = root.partition_collators;
-            emit(s, [&exec, &ctx, tunnels, ids, coll](size_t) -> SinkOpPtr {
-                return std::make_unique<ExchangeSenderSinkOp>(exec, ctx, tunnels, ids, coll);
+            const uint32_t fgs = root.fine_grained_shuffle_stream_count;
+            const uint64_t fgb = root.fine_grained_shuffle_batch_size;
+            emit(s, [&exec, &ctx, tunnels, ids, coll, fgs, fgb](size_t) -> SinkOpPtr {
+                return std::make_unique<ExchangeSenderSinkOp>(exec, ctx, tunnels, ids, coll, -1, fgs, fgb);
             });
         } else {
             const bool bc = root.exchange_type == dag::ExchangeType::Broadcast;

@@ -92,6 +92,11 @@ struct Executor {
     ExchangeType exchange_type = ExchangeType::Hash;
     std::vector<Expr> partition_keys;
     std::vector<int> partition_collators;
+    // tipb::Executor.fine_grained_shuffle_stream_count (ExchangeSender / ExchangeReceiver, > 0 =
+    // fine-grained shuffle: a FineGrainedShuffleWriter on the sender, per-stream sources on the
+    // receiver) and the batch size of a stream (the fine_grained_shuffle_batch_size setting)
+    uint32_t fine_grained_shuffle_stream_count = 0;
+    uint64_t fine_grained_shuffle_batch_size = 8192;
     // TypeExchangeReceiver: the PlanContext receiver of this name
     std::string receiver;
 

@@ -417,6 +417,52 @@ private:
     std::vector<int> collators_;
 };
 
+// A device packet (codec output): `bytes` valid bytes of `buf`.
+struct DevicePacket {
+    DeviceBufferPtr buf;
+    size_t bytes = 0;
+    bool empty() const { return bytes == 0; }
+};
+
+// FineGrainedShuffleWriter (Flash/Mpp/FineGrainedShuffleWriter.cpp; chosen by newMPPExchangeWriter.cpp:66-78
+// for a Hash exchange with fine_grained_shuffle_stream_count > 0): rows are routed to
+// partition_num * stream_count buckets (fillSelectorForFineGrainedShuffle, HashBaseWriterHelper.cpp:64-84:
+// bucket = ((h * P) >> 32) * S + h % S), and each flush sends ONE packet per partition whose chunks
+// are that partition's non-empty stream buckets, V1-encoded, tagged with their stream ids
+// (MPPTunnelSetHelper::ToFineGrainedPacket).  The receiving side routes chunk i to stream
+// stream_ids[i] (ExchangeReceiver's fine-grained queues).
+struct FineGrainedPacket {
+    std::vector<uint32_t> stream_ids;
+    std::vector<DevicePacket> chunks; // CHBlockChunkCodecV1 packets (compression NONE)
+};
+class FineGrainedShuffleWriter {
+public:
+    using Sink = std::function<void(uint32_t, FineGrainedPacket &&)>;
+    FineGrainedShuffleWriter(Context &ctx, std::vector<size_t> partition_col_ids, uint32_t partition_num,
+                             uint32_t stream_count, uint64_t batch_size, Sink sink,
+                             uint64_t max_buffered_bytes = (uint64_t)16 << 20);
+    void write(const Block &block);
+    void flush();
+    void setCollators(std::vector<int> collators) { collators_ = std::move(collators); }
+
+private:
+    Context &ctx_;
+    std::vector<size_t> partition_col_ids_;
+    uint32_t partition_num_, stream_count_;
+    uint64_t max_buffered_rows_, max_buffered_bytes_;
+    Sink sink_;
+    std::vector<int> collators_;
+    Block header_;
+    bool header_set_ = false;
+    std::vector<Block> blocks_;
+    uint64_t buffered_rows_ = 0, buffered_bytes_ = 0;
+};
+
+// Partition a block into partition_num * stream_count fine-grained buckets (bucket p * S + s).
+std::vector<Block> fineGrainedPartitionBlock(Context &ctx, const Block &block, const std::vector<size_t> &key_ids,
+                                             uint32_t partition_num, uint32_t stream_count,
+                                             const std::vector<int> &collators = {});
+
 // Partition a block into partition_num blocks (the scatterColumns step alone).
 // String columns (keys hashed by ColumnString::updateWeakHash32 under collators[k], the k-th
 // key's collator) are scattered through the stable partition permutation.
@@ -520,11 +566,6 @@ private:
 // tfg_codec_compress); decode accepts NONE, LZ4 and ZSTD (HIGH_COMPRESSION) packets, decompressed
 // on the device.  encode(vector<Block>) writes one part of the concatenated rows (the reference
 // writes one part per block; decode accepts both).
-struct DevicePacket {
-    DeviceBufferPtr buf;
-    size_t bytes = 0;
-    bool empty() const { return bytes == 0; }
-};
 
 class CHBlockChunkCodecV1 {
 public:
