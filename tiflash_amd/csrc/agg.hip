@@ -53,23 +53,25 @@ __global__ void agg_compact_kernel(AggSpec S, GroupsIO tmp, const uint64_t *stag
 // ---------------------------------------------------------------- without key (single group)
 constexpr int NK_T = 256;
 struct NoKeyPartial {
-    uint64_t lo[AGG_MAX], hi[AGG_MAX], x2[AGG_MAX], x3[AGG_MAX], cnt[AGG_MAX];
+    uint64_t lo[AGG_MAX], hi[AGG_MAX], x2[AGG_MAX], x3[AGG_MAX], x4[AGG_MAX], cnt[AGG_MAX];
     double f[AGG_MAX];
 };
-// p (4 limbs at lo/hi/x2/x3[i]) += q
-__device__ __forceinline__ void nk_add(NoKeyPartial &p, int i, const uint64_t *q) {
-    uint64_t a[4] = {p.lo[i], p.hi[i], p.x2[i], p.x3[i]};
-    add_i256(a, q);
+// p (5 limbs at lo/hi/x2/x3/x4[i]: the exact sum, see lds_add_i256) += q (4 limbs, or 5 when q5)
+__device__ __forceinline__ void nk_add(NoKeyPartial &p, int i, const uint64_t *q, const uint64_t *q4 = nullptr) {
+    uint64_t a[5] = {p.lo[i], p.hi[i], p.x2[i], p.x3[i], p.x4[i]};
+    add_i320(a, q);
+    if (q4) a[4] += *q4 - ((int64_t)q[3] < 0 ? ~0ull : 0ull); // q's own fifth limb instead of its sign
     p.lo[i] = a[0];
     p.hi[i] = a[1];
     p.x2[i] = a[2];
     p.x3[i] = a[3];
+    p.x4[i] = a[4];
 }
 
 __global__ void __launch_bounds__(NK_T) agg_nokey_kernel(AggSpec S, RowsIO rows, int mode, RowPred pred, int64_t n,
                                                          NoKeyPartial *partials) {
     NoKeyPartial p;
-    for (int i = 0; i < AGG_MAX; ++i) p.lo[i] = p.hi[i] = p.x2[i] = p.x3[i] = p.cnt[i] = 0, p.f[i] = 0;
+    for (int i = 0; i < AGG_MAX; ++i) p.lo[i] = p.hi[i] = p.x2[i] = p.x3[i] = p.x4[i] = p.cnt[i] = 0, p.f[i] = 0;
     for (int64_t r = (int64_t)blockIdx.x * NK_T + threadIdx.x; r < n; r += (int64_t)gridDim.x * NK_T) {
         if (!pred(r)) continue;
         for (int i = 0; i < S.n_aggs; ++i) {
@@ -116,7 +118,7 @@ __global__ void __launch_bounds__(NK_T) agg_nokey_kernel(AggSpec S, RowsIO rows,
             for (int i = 0; i < S.n_aggs; ++i) {
                 if (S.acc[i] == ACC_I256) {
                     const uint64_t q[4] = {red[t].lo[i], red[t].hi[i], red[t].x2[i], red[t].x3[i]};
-                    nk_add(s, i, q);
+                    nk_add(s, i, q, &red[t].x4[i]);
                 } else if (S.acc[i] == ACC_ORD) {
                     s.lo[i] = red[t].lo[i] > s.lo[i] ? red[t].lo[i] : s.lo[i];
                 } else {
@@ -137,9 +139,12 @@ __global__ void agg_nokey_fold_kernel(AggSpec S, const NoKeyPartial *partials, i
         for (int i = 0; i < S.n_aggs; ++i) {
             const NoKeyPartial &p = partials[b];
             if (S.acc[i] == ACC_F64) ((double *)st.acc[i])[0] += p.f[i];
-            else if (S.acc[i] == ACC_I256) {
-                const uint64_t q[4] = {p.lo[i], p.hi[i], p.x2[i], p.x3[i]};
-                add_i256((uint64_t *)st.acc[i], q);
+            else if (S.acc[i] == ACC_I256) { // state (Int256) + partial (5 limbs), checked
+                uint64_t *a = (uint64_t *)st.acc[i];
+                uint64_t s5[5] = {p.lo[i], p.hi[i], p.x2[i], p.x3[i], p.x4[i]};
+                add_i320(s5, a);
+                if (!fits_i256(s5) && S.ovf) *S.ovf = 1;
+                for (int k = 0; k < 4; ++k) a[k] = s5[k];
             } else if (S.acc[i] == ACC_I128) {
                 uint64_t *a = (uint64_t *)st.acc[i];
                 const uint64_t o = a[0];
@@ -202,7 +207,14 @@ __global__ void agg_state_add_kernel(AggSpec S, GroupsIO dst, GroupsIO src) { //
     if (threadIdx.x || blockIdx.x) return;
     for (int i = 0; i < S.n_aggs; ++i) {
         if (S.acc[i] == ACC_F64) ((double *)dst.acc[i])[0] += ((const double *)src.acc[i])[0];
-        else if (S.acc[i] == ACC_I256) add_i256((uint64_t *)dst.acc[i], (const uint64_t *)src.acc[i]);
+        else if (S.acc[i] == ACC_I256) { // checked (types.h:35)
+            uint64_t *a = (uint64_t *)dst.acc[i];
+            const uint64_t *b = (const uint64_t *)src.acc[i];
+            uint64_t s5[5] = {a[0], a[1], a[2], a[3], (int64_t)a[3] < 0 ? ~0ull : 0ull};
+            add_i320(s5, b);
+            if (!fits_i256(s5) && S.ovf) *S.ovf = 1;
+            for (int k = 0; k < 4; ++k) a[k] = s5[k];
+        }
         else if (S.acc[i] == ACC_I128) {
             uint64_t *a = (uint64_t *)dst.acc[i];
             const uint64_t *b = (const uint64_t *)src.acc[i];
@@ -1216,6 +1228,18 @@ int sum_acc_kind(int word) {
     return ACC_I64;
 }
 
+// A Decimal256 sum that left Int256 during the last call (the device flag S.ovf): the reference's
+// checked_int256_t throws (libs/libcommon/include/common/types.h:35) -> TFG_ERR_OVERFLOW
+int check_overflow(tfg_agg *a) {
+    if (!a->S.ovf) return TFG_OK;
+    unsigned f = 0;
+    TFG_HIP(hipMemcpyAsync(&f, a->S.ovf, sizeof f, hipMemcpyDeviceToHost, a->ctx->stream));
+    TFG_HIP(hipStreamSynchronize(a->ctx->stream));
+    if (!f) return TFG_OK;
+    TFG_HIP(hipMemsetAsync(a->S.ovf, 0, sizeof f, a->ctx->stream));
+    return fail(TFG_ERR_OVERFLOW, "Decimal256 sum overflow (DECIMAL_OVERFLOW: the sum left Int256)");
+}
+
 int consume_common(tfg_agg *a, int mode, const RowPred &pred, const void *keys, const uint8_t *key_nullmap,
                    const void *const *args, const uint8_t *const *arg_nullmaps, int64_t n) {
     TFG_CHECK(a, TFG_ERR_INVALID_ARG, "agg is null");
@@ -1233,10 +1257,14 @@ int consume_common(tfg_agg *a, int mode, const RowPred &pred, const void *keys, 
         if (vnull[i] && mode == MODE_RAW && (a->S.kind[i] == TFG_AGG_SUM || a->S.acc[i] == ACC_ORD) && !a->S.has_cnt[i])
             return fail(TFG_ERR_ILLEGAL_TYPE, "argument %d has a null map but was declared not nullable", i);
     }
-    if (a->nokey) return consume_nokey(a, mode, pred, vals, vnull, n);
+    if (a->nokey) {
+        if (int rc = consume_nokey(a, mode, pred, vals, vnull, n)) return rc;
+        return check_overflow(a);
+    }
     TFG_CHECK(keys, TFG_ERR_INVALID_ARG, "keys are null");
     if (a->S.key_width == 16) TFG_CHECK(!key_nullmap, TFG_ERR_INVALID_ARG, "packed keys carry their NULL bits");
-    return consume_keyed(a, mode, pred, keys, a->S.key_width, key_nullmap, vals, vnull, nullptr, nullptr, n);
+    if (int rc = consume_keyed(a, mode, pred, keys, a->S.key_width, key_nullmap, vals, vnull, nullptr, nullptr, n)) return rc;
+    return check_overflow(a);
 }
 
 } // namespace
@@ -1409,7 +1437,7 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
                                 : S.acc[i] == ACC_I128 ? TFG_DECIMAL128
                                 : is_unsigned_type(at) ? TFG_UINT64 : TFG_INT64;
             a->result_width[i] = 8 * acc_words(S.acc[i]);
-            cell += 8 * acc_words(S.acc[i]);
+            cell += 8 * lds_acc_words(S.acc[i]);
         } else if (kind == TFG_AGG_MIN || kind == TFG_AGG_MAX || kind == TFG_AGG_FIRST_ROW) {
             if (!(is_fixed_numeric(at) || at == TFG_DECIMAL32 || at == TFG_DECIMAL64)) {
                 delete a;
@@ -1480,7 +1508,7 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
     for (int i = 0; i < n_aggs; ++i) {
         if (S.acc[i] != ACC_NONE) {
             S.acc_off[i] = off;
-            off += (cap + 2) * 8 * acc_words(S.acc[i]);
+            off += (cap + 2) * 8 * lds_acc_words(S.acc[i]);
         }
         if (S.has_cnt[i]) {
             S.cnt_off[i] = off;
@@ -1489,6 +1517,16 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
     }
     S.ctrl_off = off;
     S.lds_bytes = off + (int)sizeof(Ctrl) + 16;
+    S.ovf = nullptr;
+    for (int i = 0; i < n_aggs; ++i)
+        if (S.acc[i] == ACC_I256 && !S.ovf) {
+            if (hipMalloc((void **)&S.ovf, sizeof(unsigned)) != hipSuccess ||
+                hipMemsetAsync(S.ovf, 0, sizeof(unsigned), ctx->stream) != hipSuccess) {
+                if (S.ovf) (void)hipFree(S.ovf);
+                delete a;
+                return fail(TFG_ERR_OOM, "overflow flag allocation failed");
+            }
+        }
     // one workgroup per CU anyway (LDS): make it 16 waves, and keep the in-flight insert headroom
     S.bt = S.lds_bytes > 80 * 1024 ? BT_BIG : BT;
     S.maxfill = std::max(1, std::min(cap * fill_num / 8, cap - 8));
@@ -1515,6 +1553,7 @@ int tfg_agg_destroy(tfg_agg *a) {
     }
     if (a->pack_buf) (void)hipFree(a->pack_buf);
     if (a->pack_err) (void)hipFree(a->pack_err);
+    if (a->S.ovf) (void)hipFree(a->S.ovf);
     if (a->sdict) serial_dict_destroy(a->sdict);
     if (a->inner) tfg_agg_destroy(a->inner);
     delete a;
@@ -1592,7 +1631,7 @@ int tfg_agg_merge(tfg_agg *dst, tfg_agg *src) {
         hipLaunchKernelGGL(agg_state_add_kernel, dim3(1), dim3(64), 0, dst->ctx->stream, dst->S, dst->st[dst->cur],
                            src->st[src->cur]);
         TFG_LAUNCH_CHECK();
-        return TFG_OK;
+        return check_overflow(dst);
     }
     if (src->n_groups == 0) return TFG_OK;
     const GroupsIO &g = src->st[src->cur];
@@ -1603,9 +1642,10 @@ int tfg_agg_merge(tfg_agg *dst, tfg_agg *src) {
         cnts[i] = g.cnt[i];
     }
     RowPred pred{};
-    return consume_keyed(dst, MODE_STATE, pred, g.key, dst->S.key_width == 16 ? 16 : 8, g.key_null, vals, nullptr, cnts,
-                         src->bucket_off[src->cur],
-                         (int64_t)src->n_groups);
+    if (int rc = consume_keyed(dst, MODE_STATE, pred, g.key, dst->S.key_width == 16 ? 16 : 8, g.key_null, vals, nullptr,
+                               cnts, src->bucket_off[src->cur], (int64_t)src->n_groups))
+        return rc;
+    return check_overflow(dst);
 }
 
 int tfg_agg_size(tfg_agg *a, uint64_t *out_groups) {

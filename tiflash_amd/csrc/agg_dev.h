@@ -20,6 +20,9 @@ constexpr int LDS_TABLE_MAX = 150 * 1024;    // largest table (one 16-wave workg
 enum AccKind { ACC_NONE = 0, ACC_I64 = 1, ACC_F64 = 2, ACC_I128 = 3, ACC_I256 = 4, ACC_ORD = 5 };
 // 64-bit words of an accumulator of kind k
 __host__ __device__ constexpr int acc_words(int k) { return k == ACC_I256 ? 4 : k == ACC_I128 ? 2 : k == ACC_NONE ? 0 : 1; }
+// ... and in an LDS table: a Decimal256 sum carries a fifth limb there, the sign extension of
+// the exact sum, so a sum past Int256 is detected when the table is flushed (lds_add_i256)
+__host__ __device__ constexpr int lds_acc_words(int k) { return k == ACC_I256 ? 5 : acc_words(k); }
 enum RowMode { MODE_RAW = 0, MODE_PARTIAL = 1, MODE_STATE = 2 };
 
 struct AggSpec {
@@ -39,6 +42,7 @@ struct AggSpec {
     int bt;         // bucket kernel workgroup size (BT or BT_BIG)
     int wkey_off;   // wide keys (key_width 16): LDS byte offset of the 16-byte keys (cells' tags sit in
                     // the u64 key array); 0 for keys of <= 8 bytes
+    unsigned *ovf;      // Decimal256 sums: set to 1 when a sum leaves Int256 (TFG_ERR_OVERFLOW); null otherwise
     int bbits;          // bucket radix bits: the in-table slot group comes from the 32 bits of
                         // key * 2^64/phi just below them (one multiply instead of a mixer) ...
     unsigned ngroups;   // ... scaled to the table's cap / GS groups (any count: LDS-sized tables)
@@ -157,9 +161,11 @@ __device__ __forceinline__ void lds_add_i128(uint64_t *cell, uint64_t lo, uint64
 }
 
 // Decimal256 sum state (AggregateFunctionSumData<Decimal256>, boost checked_int256_t): four
-// 64-bit limbs added limb by limb with LDS atomics.  Every adder carries its own carry-outs into
-// the next limb (a carry from x_k + c_k itself, or from the atomic add), so the cell ends at the
-// exact two's complement sum mod 2^256 whatever the interleaving of concurrent adders.
+// 64-bit limbs added limb by limb with LDS atomics, plus a fifth that receives the addend's sign
+// extension and the carry out of limb 3.  Every adder carries its own carry-outs into the next
+// limb (a carry from x_k + c_k itself, or from the atomic add), so the five limbs end at the
+// exact sum whatever the interleaving of concurrent adders: it fits Int256 iff limb 4 is the
+// sign extension of limb 3 (checked_int256_t throws past that: types.h:35; checked at flush).
 __device__ __forceinline__ void lds_add_i256(uint64_t *cell, uint64_t x0, uint64_t x1, uint64_t x2, uint64_t x3) {
     uint64_t old = atomicAdd((unsigned long long *)&cell[0], (unsigned long long)x0);
     uint64_t c = (old + x0) < old ? 1ull : 0ull;
@@ -171,7 +177,27 @@ __device__ __forceinline__ void lds_add_i256(uint64_t *cell, uint64_t x0, uint64
     ca = t < c ? 1ull : 0ull;
     old = atomicAdd((unsigned long long *)&cell[2], (unsigned long long)t);
     c = ((old + t) < old ? 1ull : 0ull) + ca;
-    atomicAdd((unsigned long long *)&cell[3], (unsigned long long)(x3 + c));
+    t = x3 + c;
+    ca = t < c ? 1ull : 0ull;
+    old = atomicAdd((unsigned long long *)&cell[3], (unsigned long long)t);
+    c = ((old + t) < old ? 1ull : 0ull) + ca;
+    atomicAdd((unsigned long long *)&cell[4], (unsigned long long)(((int64_t)x3 < 0 ? ~0ull : 0ull) + c));
+}
+
+// five-limb register form (a[0..4] += x[0..3] sign-extended); fits Int256 iff a[4] == sign(a[3])
+__host__ __device__ __forceinline__ void add_i320(uint64_t *a, const uint64_t *x) {
+    uint64_t c = 0;
+    for (int k = 0; k < 5; ++k) {
+        const uint64_t xk = k < 4 ? x[k] : ((int64_t)x[3] < 0 ? ~0ull : 0ull);
+        const uint64_t t = xk + c;
+        const uint64_t c1 = t < c ? 1ull : 0ull;
+        const uint64_t s = a[k] + t;
+        c = (s < t ? 1ull : 0ull) + c1;
+        a[k] = s;
+    }
+}
+__host__ __device__ __forceinline__ bool fits_i256(const uint64_t *a5) {
+    return a5[4] == ((int64_t)a5[3] < 0 ? ~0ull : 0ull);
 }
 
 // register form: a += x (mod 2^256)
@@ -506,7 +532,7 @@ struct Table {
     }
 
     __device__ __forceinline__ uint64_t *acc_cell(int i, int cell) const {
-        return reinterpret_cast<uint64_t *>(base + S.acc_off[i]) + (int64_t)cell * acc_words(S.acc[i]);
+        return reinterpret_cast<uint64_t *>(base + S.acc_off[i]) + (int64_t)cell * lds_acc_words(S.acc[i]);
     }
     __device__ __forceinline__ uint64_t *cnt_cell(int i, int cell) const {
         return reinterpret_cast<uint64_t *>(base + S.cnt_off[i]) + cell;
@@ -617,6 +643,7 @@ struct Table {
                     const int nw = acc_words(S.acc[i]);
                     const uint64_t *a = acc_cell(i, c);
                     for (int k = 0; k < nw; ++k) ((uint64_t *)out.acc[i])[nw * pos + k] = a[k];
+                    if (S.acc[i] == ACC_I256 && !fits_i256(a) && S.ovf) atomicOr(S.ovf, 1u);
                 } else if (S.acc[i] != ACC_NONE) {
                     ((uint64_t *)out.acc[i])[pos] = *acc_cell(i, c);
                 }
