@@ -8,11 +8,21 @@
 // FSE-compressed or direct weights, treeless reuse), FSE-coded sequences (predefined, RLE,
 // compressed and repeat modes) with the three repeat offsets, and the XXH64 content checksum.
 // No dictionaries.  Every read is bounds-checked: a malformed frame returns an error, never
-// writes outside [dst, dst + cap).
+// writes outside its buffers.
 //
-// The same code runs on the device (one thread per frame, lz4.hip's frame walk) and on the host
-// (the CPU check of the decoder against libzstd, tests/test_zstd.py).  State lives in a ZWork the
-// caller provides (tables + the block's literals).
+// Decoding is split in two stages, so that neither waits on the other's memory:
+//   1. entropy (zstd_frame_entropy): block headers, Huffman literals and FSE sequences are decoded
+//      into a flat list of ZSeq records {literal length, match length, resolved offset} and the
+//      literal bytes, in output order.  Raw blocks become literal runs, RLE blocks one literal and
+//      an offset-1 match; frame starts and content checksums become marker records.
+//   2. execution: the records are replayed into the output (literal runs, then LZ77 matches).
+// On the device (lz4.hip) stage 1 is one wave per packet frame with the compressed block staged in
+// LDS (the wave decodes the sequences in lockstep; the four Huffman streams of a block go to four
+// lanes) and stage 2 a second kernel, one wave per frame, whose output passes through a 64 KB LDS
+// window: literal runs are copied by all lanes at once, matches are replayed one after another
+// with all lanes copying, and the window is flushed to HBM once per batch of records.  The same
+// stage-1 source runs on the host with zstd_exec_serial as stage 2 (zstd_frame): the CPU check of
+// the decoder against the system libzstd (tests/test_zstd.py).
 #pragma once
 #include <stdint.h>
 
@@ -21,18 +31,16 @@
 #else
 #define ZHD inline
 #endif
-// Wave-cooperative copies: on the device all 64 lanes of a wave run the decoder in lockstep (the
-// entropy decoding is identical in every lane: same loads, same branches) and split only the
-// byte copies, lane i taking bytes i, i + 64, ...; ZSYNC makes the wave's earlier stores visible
-// to its other lanes before they are read back (match sources), ZSYNC_AGENT before the checksum.
+// Stage 1 on the device: all 64 lanes of a wave run the entropy decoding in lockstep (identical
+// loads and branches in every lane) and split the stores: record q is stored by lane q % 64,
+// literal bytes by lanes in turn, the four Huffman streams by lanes 0-3.  ZANY combines a per-lane
+// condition over the wave (the Huffman stream checks).
 #if defined(__HIP_DEVICE_COMPILE__)
-#define ZSYNC() do { __builtin_amdgcn_s_waitcnt(0); __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); } while (0)
-#define ZSYNC_AGENT() do { __builtin_amdgcn_s_waitcnt(0); __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent"); } while (0)
 #define ZSYNC_LDS() __syncthreads()
+#define ZANY(x) (__ballot((int)(x)) != 0)
 #else
 #define ZSYNC_LDS() do { } while (0)
-#define ZSYNC() do { } while (0)
-#define ZSYNC_AGENT() do { } while (0)
+#define ZANY(x) (x)
 #endif
 
 namespace tfz {
@@ -52,10 +60,26 @@ struct ZWork {
     bool ll_ok, of_ok, ml_ok;             // a table exists for Repeat mode
     uint16_t huf[1 << ZHUF_MAXBITS];      // symbol | nbBits << 8
     int huf_bits;                         // 0: no table yet (Treeless needs one)
-    uint8_t *lit;                         // ZMAX_BLOCK + 32 bytes: the block's literals
     uint8_t *stage;                       // device: an LDS copy of the current compressed block (null: none)
 };
-// (the tables, ~10 KB, live in LDS on the device; the literals in global memory)
+// (the tables, ~10 KB, live in LDS on the device)
+
+// One replay record of stage 1.  tag ZS_SEQ: ll literal bytes (the next ones of the literal
+// stream), then ml bytes copied from `off` bytes back; ZS_START: a ZSTD frame begins (offsets may
+// not reach before it); ZS_CHECK: the frame ends with content checksum `off` (XXH64 low 32 bits).
+struct ZSeq {
+    uint32_t ll, ml, off, tag;
+};
+constexpr uint32_t ZS_SEQ = 0, ZS_START = 1, ZS_CHECK = 2;
+
+// Stage-1 outputs of one packet frame (caller-sized: at most raw/3 + blocks + 2 * zstd frames
+// records, at most raw literal bytes)
+struct ZOut {
+    ZSeq *seq;
+    uint64_t seq_cap, nseq;
+    uint8_t *lit;
+    uint64_t lit_cap, nlit;
+};
 
 // ---------------------------------------------------------------- constants (RFC 8878 §3.1.1.3.2.2)
 ZHD uint32_t ll_base(int c) {
@@ -405,7 +429,7 @@ ZHD uint64_t xxh64(const uint8_t *p, uint64_t len) {
     return h;
 }
 
-// ---------------------------------------------------------------- blocks
+// ---------------------------------------------------------------- stage 1: blocks -> records
 // a sequence-table description of one kind (mode from the compression-modes byte)
 ZHD int64_t seq_table(const uint8_t *src, int64_t n, int mode, int kind, ZWork *w) {
     FseEntry *t = kind == 0 ? w->ll : kind == 1 ? w->of : w->ml;
@@ -438,9 +462,19 @@ ZHD int64_t seq_table(const uint8_t *src, int64_t n, int mode, int kind, ZWork *
     return ok ? 0 : -1; // repeat: the previous block's table
 }
 
-// one compressed block -> out[op ...]; reps = the frame's repeat offsets
-ZHD bool zblock(const uint8_t *src, int64_t n, uint8_t *out, uint64_t &op, uint64_t cap, uint32_t *rep, ZWork *w,
-                uint32_t lane, uint32_t nl) {
+// appends record r (stored by lane nseq % nl; every lane counts)
+ZHD bool put_seq(ZOut &o, const ZSeq &r, uint32_t lane, uint32_t nl) {
+    if (o.nseq >= o.seq_cap) return false;
+    if (o.nseq % nl == lane) o.seq[o.nseq] = r;
+    ++o.nseq;
+    return true;
+}
+
+// One compressed block: its literals appended to o.lit, its sequences (repeat offsets resolved)
+// appended as records.  op = the packet frame's output so far, fstart = where the current ZSTD
+// frame's output began (offsets reach back into this frame only), cap = the output capacity.
+ZHD bool zblock_entropy(const uint8_t *src, int64_t n, uint64_t &op, uint64_t fstart, uint64_t cap, uint32_t *rep,
+                        ZWork *w, ZOut &o, uint32_t lane, uint32_t nl) {
     // ---- literals section
     if (n < 1) return false;
     const int ltype = src[0] & 3, sf = (src[0] >> 2) & 3;
@@ -460,14 +494,15 @@ ZHD bool zblock(const uint8_t *src, int64_t n, uint8_t *out, uint64_t &op, uint6
             lsize = (src[0] >> 4) | ((uint32_t)src[1] << 4) | ((uint32_t)src[2] << 12);
             ip = 3;
         }
-        if (lsize > (uint32_t)ZMAX_BLOCK) return false;
+        if (lsize > (uint32_t)ZMAX_BLOCK || o.nlit + lsize > o.lit_cap) return false;
+        uint8_t *lit = o.lit + o.nlit;
         if (ltype == 0) {
             if (ip + lsize > n) return false;
-            for (uint32_t i = 0; i < lsize; ++i) w->lit[i] = src[ip + i];
+            for (uint32_t i = lane; i < lsize; i += nl) lit[i] = src[ip + i];
             ip += lsize;
         } else {
             if (ip + 1 > n) return false;
-            for (uint32_t i = 0; i < lsize; ++i) w->lit[i] = src[ip];
+            for (uint32_t i = lane; i < lsize; i += nl) lit[i] = src[ip];
             ip += 1;
         }
     } else {
@@ -480,7 +515,7 @@ ZHD bool zblock(const uint8_t *src, int64_t n, uint8_t *out, uint64_t &op, uint6
         csize = (uint32_t)((v >> (4 + bits)) & ((1u << bits) - 1));
         streams = sf == 0 ? 1 : 4;
         ip = hl;
-        if (lsize > (uint32_t)ZMAX_BLOCK || ip + csize > n) return false;
+        if (lsize > (uint32_t)ZMAX_BLOCK || ip + csize > n || o.nlit + lsize > o.lit_cap) return false;
         const uint8_t *cs = src + ip;
         int64_t cn = csize;
         if (ltype == 2) {
@@ -491,8 +526,10 @@ ZHD bool zblock(const uint8_t *src, int64_t n, uint8_t *out, uint64_t &op, uint6
         } else if (!w->huf_bits) {
             return false; // treeless without a previous table
         }
+        uint8_t *lit = o.lit + o.nlit;
+        bool bad = false;
         if (streams == 1) {
-            if (!huf_stream(w, cs, cn, w->lit, lsize)) return false;
+            if (lane == 0) bad = !huf_stream(w, cs, cn, lit, lsize);
         } else {
             if (cn < 6) return false;
             const int64_t s1 = cs[0] | (cs[1] << 8), s2 = cs[2] | (cs[3] << 8), s3 = cs[4] | (cs[5] << 8);
@@ -501,11 +538,14 @@ ZHD bool zblock(const uint8_t *src, int64_t n, uint8_t *out, uint64_t &op, uint6
             const int64_t seg = (lsize + 3) / 4;
             if (3 * seg > lsize) return false;
             const uint8_t *b = cs + 6;
-            if (!huf_stream(w, b, s1, w->lit, seg)) return false;
-            if (!huf_stream(w, b + s1, s2, w->lit + seg, seg)) return false;
-            if (!huf_stream(w, b + s1 + s2, s3, w->lit + 2 * seg, seg)) return false;
-            if (!huf_stream(w, b + s1 + s2 + s3, s4, w->lit + 3 * seg, lsize - 3 * seg)) return false;
+            const int64_t st[5] = {0, s1, s1 + s2, s1 + s2 + s3, s1 + s2 + s3 + s4};
+            // stream k by lane k (every stream by lane 0 when the caller runs one lane)
+            for (uint32_t k = lane; k < 4; k += nl) {
+                const int64_t cnt = k < 3 ? seg : (int64_t)lsize - 3 * seg;
+                bad = bad || !huf_stream(w, b + st[k], st[k + 1] - st[k], lit + k * seg, cnt);
+            }
         }
+        if (ZANY(bad)) return false;
         ip += csize;
     }
     // ---- sequences section
@@ -543,7 +583,6 @@ ZHD bool zblock(const uint8_t *src, int64_t n, uint8_t *out, uint64_t &op, uint6
         BackBits bb;
         if (!bb.init(src + ip, n - ip)) return false;
         uint32_t sll = (uint32_t)bb.read(w->ll_log), sof = (uint32_t)bb.read(w->of_log), sml = (uint32_t)bb.read(w->ml_log);
-        uint64_t synced = 0; // output below this position is visible to every lane (block entry: none assumed)
         for (uint32_t q = 0; q < nseq; ++q) {
             const int llc = w->ll[sll].sym, ofc = w->of[sof].sym, mlc = w->ml[sml].sym;
             if (llc > 35 || mlc > 52 || ofc > 31) return false;
@@ -574,40 +613,29 @@ ZHD bool zblock(const uint8_t *src, int64_t n, uint8_t *out, uint64_t &op, uint6
                     off = t;
                 }
             }
-            if (lit_pos + ll > lsize || op + ll + ml > cap || off == 0 || off > op + ll) return false;
-            for (uint32_t i = lane; i < ll; i += nl) out[op + i] = w->lit[lit_pos + i];
-            op += ll;
+            if (lit_pos + ll > lsize || op + ll + ml > cap || off == 0 || off > op - fstart + ll) return false;
+            if (!put_seq(o, ZSeq{ll, ml, (uint32_t)off, ZS_SEQ}, lane, nl)) return false;
+            op += ll + ml;
             lit_pos += ll;
-            // the match repeats the off bytes before op: byte i = out[op - off + i % off], all of
-            // them written before this copy, by any lane: ZSYNC first unless every source byte lies
-            // below the last sync point (each ZSYNC waits for the wave's outstanding stores)
-            if (op - off + (ml < off ? ml : off) > synced) {
-                ZSYNC();
-                synced = op;
-            }
-            const volatile uint8_t *ov = out;
-            if (off >= ml) {
-                for (uint32_t i = lane; i < ml; i += nl) out[op + i] = ov[op - off + i];
-            } else {
-                const uint32_t o32 = (uint32_t)off;
-                for (uint32_t i = lane; i < ml; i += nl) out[op + i] = ov[op - off + i % o32];
-            }
-            op += ml;
         }
         if (bb.pos != 0) return false;
     } else if (ip != n) {
         return false;
     }
-    if (op + (lsize - lit_pos) > cap) return false;
-    for (uint32_t i = lane; i < lsize - lit_pos; i += nl) out[op + i] = w->lit[lit_pos + i];
-    op += lsize - lit_pos;
+    const uint32_t rest = lsize - lit_pos; // the block's last literals
+    if (rest) {
+        if (op + rest > cap || !put_seq(o, ZSeq{rest, 0, 0, ZS_SEQ}, lane, nl)) return false;
+        op += rest;
+    }
+    o.nlit += lsize;
     return true;
 }
 
-// One ZSTD frame src[0, n) -> dst[0, cap); returns the decoded size, or -1 when the frame is
-// malformed, uses a dictionary, or does not fit.  (Skippable frames decode to nothing.)
-ZHD int64_t zstd_frame(const uint8_t *src, int64_t n, uint8_t *dst, uint64_t cap, ZWork *w, uint32_t lane = 0,
-                       uint32_t nl = 1) {
+// Stage 1 of one packet frame: every ZSTD frame of src[0, n) (skippable frames decode to
+// nothing) into records and literals.  Returns the decoded size, or -1 when the frame is
+// malformed, uses a dictionary, or does not fit `cap` / the ZOut capacities.
+ZHD int64_t zstd_frame_entropy(const uint8_t *src, int64_t n, uint64_t cap, ZWork *w, ZOut &o, uint32_t lane = 0,
+                               uint32_t nl = 1) {
     int64_t ip = 0;
     uint64_t op = 0;
     while (ip < n) {
@@ -640,7 +668,8 @@ ZHD int64_t zstd_frame(const uint8_t *src, int64_t n, uint8_t *dst, uint64_t cap
         for (int k = 0; k < fcs_len; ++k) fcs |= (uint64_t)src[ip + k] << (8 * k);
         if (fcs_len == 2) fcs += 256;
         ip += fcs_len;
-        const uint64_t frame_start = op;
+        const uint64_t fstart = op;
+        if (!put_seq(o, ZSeq{0, 0, 0, ZS_START}, lane, nl)) return -1;
         uint32_t rep[3] = {1, 4, 8};
         w->ll_ok = w->of_ok = w->ml_ok = false;
         w->huf_bits = 0;
@@ -651,22 +680,26 @@ ZHD int64_t zstd_frame(const uint8_t *src, int64_t n, uint8_t *dst, uint64_t cap
             const int last = bh & 1, btype = (bh >> 1) & 3;
             const uint32_t bsize = bh >> 3;
             if (btype == 3) return -1;
-            if (btype == 1) {
+            if (btype == 1) { // RLE: one literal byte, then an offset-1 match of bsize - 1
                 if (ip + 1 > n || op + bsize > cap) return -1;
-                for (uint32_t i = lane; i < bsize; i += nl) dst[op + i] = src[ip];
-                op += bsize;
+                if (bsize) {
+                    if (o.nlit + 1 > o.lit_cap) return -1;
+                    if (lane == 0) o.lit[o.nlit] = src[ip];
+                    o.nlit += 1;
+                    if (!put_seq(o, ZSeq{1, bsize - 1, bsize > 1 ? 1u : 0u, ZS_SEQ}, lane, nl)) return -1;
+                    op += bsize;
+                }
                 ip += 1;
             } else {
                 if (ip + bsize > n) return -1;
-                if (btype == 0) {
-                    if (op + bsize > cap) return -1;
-                    for (uint32_t i = lane; i < bsize; i += nl) dst[op + i] = src[ip + i];
+                if (btype == 0) { // raw: a literal run
+                    if (op + bsize > cap || o.nlit + bsize > o.lit_cap) return -1;
+                    for (uint32_t i = lane; i < bsize; i += nl) o.lit[o.nlit + i] = src[ip + i];
+                    o.nlit += bsize;
+                    if (bsize && !put_seq(o, ZSeq{bsize, 0, 0, ZS_SEQ}, lane, nl)) return -1;
                     op += bsize;
                 } else {
                     if (bsize > (uint32_t)ZMAX_BLOCK) return -1;
-                    // offsets reach back into this frame's output only (no dictionary)
-                    uint8_t *fo = dst + frame_start;
-                    uint64_t fop = op - frame_start;
                     const uint8_t *bsrc = src + ip;
                     if (w->stage) { // the block's bytes into LDS: every bit read then costs an LDS load
                         ZSYNC_LDS();
@@ -674,22 +707,70 @@ ZHD int64_t zstd_frame(const uint8_t *src, int64_t n, uint8_t *dst, uint64_t cap
                         ZSYNC_LDS();
                         bsrc = w->stage;
                     }
-                    if (!zblock(bsrc, bsize, fo, fop, cap - frame_start, rep, w, lane, nl)) return -1;
-                    op = frame_start + fop;
+                    if (!zblock_entropy(bsrc, bsize, op, fstart, cap, rep, w, o, lane, nl)) return -1;
                 }
                 ip += bsize;
             }
             if (last) break;
         }
-        if (has_fcs && op - frame_start != fcs) return -1;
+        if (has_fcs && op - fstart != fcs) return -1;
         if (checksum) {
             if (ip + 4 > n) return -1;
-            ZSYNC_AGENT();
-            if ((uint32_t)xxh64(dst + frame_start, op - frame_start) != rd32(src + ip)) return -1;
+            if (!put_seq(o, ZSeq{0, 0, rd32(src + ip), ZS_CHECK}, lane, nl)) return -1;
             ip += 4;
         }
     }
     return (int64_t)op;
 }
+
+// record capacity of a packet frame of `raw` output bytes and `comp` compressed bytes: sequences
+// have a match of >= 3 bytes; every block adds at most one literal-run record and every ZSTD frame
+// (>= 8 bytes: magic, descriptor, one block header) two markers
+ZHD uint64_t zstd_seq_cap(uint64_t raw, uint64_t comp) { return raw / 3 + comp * 2 / 3 + 16; }
+
+// ---------------------------------------------------------------- stage 2 (host form)
+// Replays the records of one packet frame into dst[0, cap); -1 on any inconsistency (a record
+// past the literals or the output, an offset before its frame, a checksum mismatch).
+ZHD int64_t zstd_exec_serial(const ZSeq *seq, uint64_t nseq, const uint8_t *lit, uint64_t nlit, uint8_t *dst,
+                             uint64_t cap) {
+    uint64_t op = 0, lp = 0, fstart = 0;
+    for (uint64_t q = 0; q < nseq; ++q) {
+        const ZSeq r = seq[q];
+        if (r.tag == ZS_START) {
+            fstart = op;
+            continue;
+        }
+        if (r.tag == ZS_CHECK) {
+            if ((uint32_t)xxh64(dst + fstart, op - fstart) != r.off) return -1;
+            continue;
+        }
+        if (r.tag != ZS_SEQ || lp + r.ll > nlit || op + r.ll + r.ml > cap) return -1;
+        for (uint32_t i = 0; i < r.ll; ++i) dst[op + i] = lit[lp + i];
+        op += r.ll;
+        lp += r.ll;
+        if (r.ml) {
+            if (r.off == 0 || r.off > op - fstart) return -1;
+            for (uint32_t i = 0; i < r.ml; ++i) dst[op + i] = dst[op - r.off + i];
+            op += r.ml;
+        }
+    }
+    return lp == nlit ? (int64_t)op : -1;
+}
+
+#if !defined(__HIP_DEVICE_COMPILE__)
+// Host decode of one frame body (both stages): the decoded size, or -1 (tests/cpp/zstd_cpu.cpp).
+inline int64_t zstd_frame(const uint8_t *src, int64_t n, uint8_t *dst, uint64_t cap, ZWork *w) {
+    ZOut o{};
+    o.seq_cap = zstd_seq_cap(cap, (uint64_t)n);
+    o.lit_cap = cap;
+    o.seq = new ZSeq[o.seq_cap];
+    o.lit = new uint8_t[o.lit_cap + 1];
+    int64_t r = zstd_frame_entropy(src, n, cap, w, o);
+    if (r >= 0 && zstd_exec_serial(o.seq, o.nseq, o.lit, o.nlit, dst, cap) != r) r = -1;
+    delete[] o.seq;
+    delete[] o.lit;
+    return r;
+}
+#endif
 
 } // namespace tfz
