@@ -466,6 +466,21 @@ int tfg_alltoall_counts(tfg_comm *comm, const uint64_t *send_bytes_host, uint64_
 int tfg_alltoallv(tfg_comm *comm, const void *send, const uint64_t *send_bytes, const uint64_t *send_displs,
                   void *recv, const uint64_t *recv_bytes, const uint64_t *recv_displs);
 
+/* Fused exchange of fixed-width column planes: ONE all-to-all of a peer-major buffer instead of
+ * one per column (the reference's packet carries the whole Block, newMPPExchangeWriter.cpp:64-95).
+ * tfg_pack_planes writes, for each destination p in turn, every plane's rows of p:
+ * planes[p * nplanes + j] = partition p's plane j, rows[p * nplanes + j] values of widths[j] bytes
+ * (NULL = zero bytes, e.g. the null map of a Nullable column that carries none).  Planes may count
+ * different rows (a String's chars travel as a plane of 1-byte rows next to its rows' planes).
+ * out_seg_bytes (host, nparts) = each segment's bytes; out holds their sum.  tfg_unpack_planes is
+ * the receiving side: nparts segments of `in` (rows[s * nplanes + j], that layout) into nplanes
+ * output planes, source s's rows after source s-1's.  Both are asynchronous on the context's
+ * stream (one launch per 120 non-empty pieces). */
+int tfg_pack_planes(tfg_ctx *ctx, int nparts, int nplanes, const void *const *planes, const int *widths,
+                    const uint64_t *rows, void *out, uint64_t *out_seg_bytes);
+int tfg_unpack_planes(tfg_ctx *ctx, int nparts, int nplanes, const int *widths, const uint64_t *rows, const void *in,
+                      void *const *planes);
+
 /* ---------------------------------------------------------------- (f1) MPP packet codec */
 /* The Block wire format of MPP packets, encoded from / decoded into device columns; the packet
  * itself is a device buffer (the tunnel moves its bytes).

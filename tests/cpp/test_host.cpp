@@ -16,6 +16,11 @@
 #include <set>
 #include <sstream>
 
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
 #include "../../oracle/oracle.h"
 #include "../../tiflash_amd/host/planner.h"
 
@@ -2429,6 +2434,190 @@ TEST(PlanExchangeFineGrained) {
     }
 }
 
+// ================================================================ two ranks over TCP
+// The MPPExchange transport seam: a host-staged TCP transport between two test processes
+// (test infrastructure; the product's transport is RcclTransport).  Rank 0 listens on
+// 127.0.0.1:port, rank 1 connects.  Counts and bytes cross as host buffers; a rank's own slice is a
+// device copy.  Rank 0 writes before it reads, rank 1 reads before it writes (no write/write stall).
+class TcpTransport : public ExchangeTransport {
+public:
+    TcpTransport(Context &ctx, int rank, int port) : ctx_(ctx), rank_(rank) {
+        if (rank == 0) {
+            const int ls = ::socket(AF_INET, SOCK_STREAM, 0);
+            int one = 1;
+            ::setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+            sockaddr_in a{};
+            a.sin_family = AF_INET;
+            a.sin_port = htons((uint16_t)port);
+            a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+            if (::bind(ls, (sockaddr *)&a, sizeof a) || ::listen(ls, 1)) throw std::runtime_error("bind/listen");
+            fd_ = ::accept(ls, nullptr, nullptr);
+            ::close(ls);
+        } else {
+            for (int attempt = 0; attempt < 600 && fd_ < 0; ++attempt) {
+                const int c = ::socket(AF_INET, SOCK_STREAM, 0);
+                sockaddr_in a{};
+                a.sin_family = AF_INET;
+                a.sin_port = htons((uint16_t)port);
+                a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+                if (::connect(c, (sockaddr *)&a, sizeof a) == 0) fd_ = c;
+                else {
+                    ::close(c);
+                    usleep(100000);
+                }
+            }
+        }
+        if (fd_ < 0) throw std::runtime_error("tcp transport: no peer");
+    }
+    ~TcpTransport() override {
+        if (fd_ >= 0) ::close(fd_);
+    }
+    int nranks() const override { return 2; }
+    int rank() const override { return rank_; }
+    void alltoallCounts(const uint64_t *send, uint64_t *recv) override {
+        uint64_t peer[2];
+        swap(send, sizeof(uint64_t) * 2, peer, sizeof peer);
+        recv[rank_] = send[rank_];
+        recv[1 - rank_] = peer[rank_];
+    }
+    void alltoallv(const void *send, const uint64_t *sb, const uint64_t *sd, void *recv, const uint64_t *rb,
+                   const uint64_t *rd) override {
+        const int q = 1 - rank_;
+        std::vector<uint8_t> out(sb[q]), in(rb[q]);
+        if (sb[q]) check(tfg_download(ctx_.raw(), out.data(), (const char *)send + sd[q], sb[q]), "tfg_download");
+        swap(out.data(), out.size(), in.data(), in.size());
+        if (rb[q]) check(tfg_upload(ctx_.raw(), (char *)recv + rd[q], in.data(), rb[q]), "tfg_upload");
+        if (sb[rank_]) check(tfg_copy(ctx_.raw(), (char *)recv + rd[rank_], (const char *)send + sd[rank_], sb[rank_]), "tfg_copy");
+    }
+
+private:
+    Context &ctx_;
+    int rank_, fd_ = -1;
+    void put(const void *p, size_t n) {
+        for (size_t d = 0; d < n;) {
+            const ssize_t w = ::write(fd_, (const char *)p + d, n - d);
+            if (w <= 0) throw std::runtime_error("tcp write");
+            d += (size_t)w;
+        }
+    }
+    void get(void *p, size_t n) {
+        for (size_t d = 0; d < n;) {
+            const ssize_t r = ::read(fd_, (char *)p + d, n - d);
+            if (r <= 0) throw std::runtime_error("tcp read");
+            d += (size_t)r;
+        }
+    }
+    void swap(const void *out, size_t n_out, void *in, size_t n_in) {
+        if (rank_ == 0) {
+            put(out, n_out);
+            get(in, n_in);
+        } else {
+            get(in, n_in);
+            put(out, n_out);
+        }
+    }
+};
+
+// Rank r's input of case c (deterministic, so each rank can rebuild its peer's rows): c = 0 fixed
+// columns (Int64 key, Nullable Int32 with and without a null map, Decimal(30,2) as 16-byte values,
+// Float64), c = 1 String key + Int64, c = 2 fixed columns with rank 1 sending no rows at all.
+static Block exchangeInput(Context &ctx, int c, int r) {
+    std::mt19937_64 rng(1000 * c + r + 1);
+    const size_t n = (c == 2 && r == 1) ? 0 : 20000 + 3000 * r;
+    std::vector<int64_t> k(std::max<size_t>(n, 1)), f(std::max<size_t>(n, 1));
+    std::vector<int32_t> v(std::max<size_t>(n, 1));
+    std::vector<uint8_t> vn(std::max<size_t>(n, 1));
+    std::vector<int64_t> dec(2 * std::max<size_t>(n, 1));
+    std::vector<double> x(std::max<size_t>(n, 1));
+    std::vector<std::string> strs;
+    for (size_t i = 0; i < n; ++i) {
+        k[i] = (int64_t)(rng() % 7000) - 3000;
+        v[i] = (int32_t)(rng() % 100000);
+        vn[i] = rng() % 5 == 0;
+        dec[2 * i] = (int64_t)(rng() >> 2);
+        dec[2 * i + 1] = (int64_t)(rng() % 3) - 1;
+        x[i] = (double)(rng() % (1 << 20)) / 8.0;
+        f[i] = (int64_t)i;
+        strs.push_back("s" + std::to_string(rng() % 5000) + (rng() % 2 ? "_tail_beyond_16_bytes" : ""));
+    }
+    DataType i64, i32n, d30, f64, str;
+    i32n.type = TFG_INT32;
+    i32n.nullable = true;
+    d30 = DataType::decimal(30, 2);
+    f64.type = TFG_FLOAT64;
+    str.type = DataType::TYPE_STRING;
+    if (c == 1) {
+        return Block{{makeStringColumn(ctx, strs), str, "s"},
+                     {makeColumn(ctx, i64, f.data(), n), i64, "f"}};
+    }
+    DataType i32n_nomap = i32n; // a Nullable column that carries no null map on this rank
+    return Block{{makeColumn(ctx, i64, k.data(), n), i64, "k"},
+                 {makeColumn(ctx, i32n, v.data(), n, vn.data()), i32n, "v"},
+                 {r == 0 ? makeColumn(ctx, i32n_nomap, v.data(), n) : makeColumn(ctx, i32n, v.data(), n, vn.data()),
+                  i32n, "w"},
+                 {makeColumn(ctx, d30, dec.data(), n), d30, "d"},
+                 {makeColumn(ctx, f64, x.data(), n), f64, "x"}};
+}
+
+// rows as tuples of cell bytes (hex), any width, Strings as their text, NULL as "N"
+static std::multiset<std::vector<std::string>> byteRowSet(Context &ctx, const Block &b) {
+    std::vector<std::vector<std::string>> cols;
+    for (const auto &cw : b.getColumnsWithTypeAndName()) {
+        ColumnPtr c = materialize(ctx, cw.column);
+        std::vector<std::string> out(c->rows);
+        const std::vector<uint8_t> nm = toHostNullMap(ctx, *c);
+        if (c->type.isString()) {
+            out = toHostStrings(ctx, *c);
+        } else {
+            const std::vector<uint8_t> v = toHostBytes(ctx, *c);
+            const size_t w = c->type.width();
+            static const char hx[] = "0123456789abcdef";
+            for (size_t i = 0; i < c->rows; ++i)
+                for (size_t k = 0; k < w; ++k) {
+                    out[i].push_back(hx[v[i * w + k] >> 4]);
+                    out[i].push_back(hx[v[i * w + k] & 15]);
+                }
+        }
+        for (size_t i = 0; i < c->rows; ++i)
+            if (!nm.empty() && nm[i]) out[i] = "N";
+        cols.push_back(std::move(out));
+    }
+    std::multiset<std::vector<std::string>> rows;
+    for (size_t r = 0; r < b.rows(); ++r) {
+        std::vector<std::string> t;
+        for (auto &c : cols) t.push_back(c[r]);
+        rows.insert(t);
+    }
+    return rows;
+}
+
+// rank: exchange each case's partition-major blocks with the peer; what arrives must be, as a row
+// multiset, partition `rank` of both ranks' inputs (the oracle's routing: weak hash of column 0)
+static int runExchangeRank(Context &ctx, int rank, int port) {
+    auto t = std::make_shared<TcpTransport>(ctx, rank, port);
+    MPPExchange ex(ctx, t);
+    int bad = 0;
+    for (int c = 0; c < 3; ++c) {
+        g_current = "exchange case " + std::to_string(c) + " rank " + std::to_string(rank);
+        std::vector<Block> parts = hashPartitionBlock(ctx, exchangeInput(ctx, c, rank), {0}, 2);
+        Block got = ex.exchange(parts);
+        std::multiset<std::vector<std::string>> want;
+        for (int r = 0; r < 2; ++r) {
+            Block in = exchangeInput(ctx, c, r);
+            if (!in.rows()) continue;
+            for (const auto &row : byteRowSet(ctx, hashPartitionBlock(ctx, in, {0}, 2)[rank])) want.insert(row);
+        }
+        const auto have = byteRowSet(ctx, got);
+        const int before = g_failures;
+        EXPECT(got.columns() == parts[0].columns());
+        EXPECT(have == want);
+        printf("[%s] exchange case %d rank %d: %zu rows\n", g_failures == before ? "  OK  " : " FAIL ", c, rank,
+               (size_t)got.rows());
+        bad += g_failures != before;
+    }
+    return bad ? 1 : 0;
+}
+
 int main(int argc, char **argv) {
     g_root = argc > 1 ? argv[1] : ".";
     const char *filter = argc > 2 ? argv[2] : nullptr;
@@ -2440,6 +2629,15 @@ int main(int argc, char **argv) {
         return 2;
     }
     Context &ctx = *owned;
+    if (filter && !strcmp(filter, "--exchange-rank")) { // test_host <root> --exchange-rank <rank> <port>
+        if (argc < 5) return 2;
+        try {
+            return runExchangeRank(ctx, atoi(argv[3]), atoi(argv[4]));
+        } catch (const std::exception &e) {
+            fprintf(stderr, "  EXCEPTION in exchange rank: %s\n", e.what());
+            return 1;
+        }
+    }
     int failed_tests = 0, ran = 0;
     for (const auto &t : registry()) {
         if (filter && !strstr(t.name, filter)) continue;

@@ -37,3 +37,28 @@ def test_host_operators_cpp():
     print(r.stderr)
     assert r.returncode == 0, r.stdout + r.stderr
     assert " failed" in r.stdout and "0 failed" in r.stdout
+
+
+@pytest.mark.gpu
+def test_mpp_exchange_two_ranks_cpp():
+    """MPPExchange's fused exchange between two processes on one GPU, through the ExchangeTransport
+    seam (a host-staged TCP transport in the test driver): fixed-width columns with and without
+    null maps and a Decimal(30,2), a String key block, and a case where rank 1 sends no rows.
+    Each rank checks that it received partition `rank` of both ranks' inputs."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = [subprocess.Popen([BIN, ROOT, "--exchange-rank", str(r), str(port)], stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT, text=True) for r in range(2)]
+    outs = []
+    try:
+        for p in procs:
+            outs.append(p.communicate(timeout=180)[0])
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    print("\n".join(outs))
+    assert [p.returncode for p in procs] == [0, 0], "\n".join(outs)
+    assert sum(o.count("[  OK  ] exchange case") for o in outs) == 6

@@ -207,7 +207,7 @@ __global__ void __launch_bounds__(JT) join_probe_kernel(JoinArgs A) {
     if (pe == ps) return; // no probe rows in this partition
     const int64_t nb = be - bs;
     const int chunks = nb == 0 ? 1 : (int)((nb + JCHUNK - 1) / JCHUNK);
-    constexpr int brw = 1 + BW, prw = PRW;
+    constexpr int brw = 1 + BW;
     for (int c = 0; c < chunks; ++c) {
         for (int i = threadIdx.x; i < JCAP + 1; i += JT) {
             if (i < JCAP) L.keys[i] = 0;

@@ -330,6 +330,11 @@ __global__ void __launch_bounds__(64) zstd_entropy_kernel(const uint8_t *pkt, co
 constexpr int ZW = 1 << 16, ZWM = ZW - 1, ZHALF = ZW / 2; // stage-2 LDS output window
 
 __device__ __forceinline__ void lds_order() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// lane j's value (j wave-uniform): v_readlane, no LDS round trip
+__device__ __forceinline__ uint32_t rl32(uint32_t v, uint32_t j) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)j); }
+__device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t j) {
+    return (uint64_t)rl32((uint32_t)v, j) | ((uint64_t)rl32((uint32_t)(v >> 32), j) << 32);
+}
 // the wave's global stores are complete and visible to its own later loads (match sources and
 // checksum bytes written by other lanes)
 __device__ __forceinline__ void zsync_global() {
@@ -419,13 +424,27 @@ __global__ void __launch_bounds__(64) zstd_exec_kernel(const tfz::ZSeq *seq, con
     const uint64_t raw = roff[f + 1] - roff[f];
     uint64_t op = 0, lp = 0, fstart = 0, synced = 0;
     bool bad = false;
-    // byte at output position sp for a write at position >= wpos_min: the window while its ring
-    // slot still holds sp (sp + ZW above every position written so far), else HBM
-    uint64_t q = 0;
-    while (q < n && !bad) {
+    // the next batch is loaded while the current one is replayed: its 64 records and the first
+    // 1 KB of its literals (16 bytes a lane, all in flight together)
+    auto load_rec = [&](uint64_t q) -> tfz::ZSeq {
         tfz::ZSeq r{0, 0, 0, 0};
+        if (q + lane < n) r = s[q + lane];
+        return r;
+    };
+    auto load_lits = [&](uint64_t at, uint8_t (&v)[16]) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint64_t i = at + lane * 16 + k;
+            v[k] = i < nlit ? lit[i] : 0;
+        }
+    };
+    uint64_t q = 0;
+    tfz::ZSeq rec = load_rec(0);
+    uint8_t pl[16];
+    load_lits(0, pl);
+    while (q < n && !bad) {
+        const tfz::ZSeq r = rec;
         const bool valid = q + lane < n;
-        if (valid) r = s[q + lane];
         const uint64_t mk = __ballot(valid && r.tag != tfz::ZS_SEQ);
         if (mk & 1ull) { // a marker first: on its own
             const uint32_t tag = __builtin_amdgcn_readfirstlane(r.tag), val = __builtin_amdgcn_readfirstlane(r.off);
@@ -439,6 +458,7 @@ __global__ void __launch_bounds__(64) zstd_exec_kernel(const tfz::ZSeq *seq, con
                 bad = true;
             }
             ++q;
+            rec = load_rec(q);
             continue;
         }
         uint64_t lim = mk ? (uint64_t)__builtin_ctzll(mk) : 64;
@@ -455,15 +475,21 @@ __global__ void __launch_bounds__(64) zstd_exec_kernel(const tfz::ZSeq *seq, con
         }
         const uint32_t cnt = (uint32_t)__popcll(__ballot(lane < lim && incl <= (uint64_t)ZHALF));
         if (cnt == 0) { // one record of more than ZHALF bytes: written through to HBM as well
-            const uint64_t ll = __shfl(r.ll, 0, 64), ml = __shfl(r.ml, 0, 64), off = __shfl(r.off, 0, 64);
+            const uint64_t ll = rl32(r.ll, 0), ml = rl32(r.ml, 0), off = rl32(r.off, 0);
             if (op + ll + ml > raw || lp + ll > nlit || (ml && (off == 0 || off > op + ll - fstart))) {
                 bad = true;
                 break;
             }
-            for (uint64_t i = lane; i < ll; i += 64) {
-                const uint8_t v = lit[lp + i];
-                win[(op + i) & ZWM] = v;
-                out[op + i] = v;
+            for (uint64_t i0 = lane * 16; i0 < ll; i0 += 64 * 16) {
+                uint8_t v[16];
+#pragma unroll
+                for (int k = 0; k < 16; ++k) v[k] = i0 + k < ll ? lit[lp + i0 + k] : 0;
+#pragma unroll
+                for (int k = 0; k < 16; ++k)
+                    if (i0 + k < ll) {
+                        win[(op + i0 + k) & ZWM] = v[k];
+                        out[op + i0 + k] = v[k];
+                    }
             }
             lds_order();
             const uint64_t d = op + ll;
@@ -475,7 +501,7 @@ __global__ void __launch_bounds__(64) zstd_exec_kernel(const tfz::ZSeq *seq, con
                     synced = d + base;
                 }
                 if (i < ml) {
-                    const uint64_t sp = off < 64 ? d - off + (i % off) : d + i - off;
+                    const uint64_t sp = off < 64 ? d - off + (uint32_t)i % (uint32_t)off : d + i - off;
                     const uint8_t v = near ? win[sp & ZWM] : out[sp];
                     win[(d + i) & ZWM] = v;
                     out[d + i] = v;
@@ -485,14 +511,31 @@ __global__ void __launch_bounds__(64) zstd_exec_kernel(const tfz::ZSeq *seq, con
             op += ll + ml;
             lp += ll;
             ++q;
+            rec = load_rec(q);
+            load_lits(lp, pl);
             continue;
         }
-        const uint64_t total_span = __shfl(incl, (int)cnt - 1, 64), total_ll = __shfl(inl, (int)cnt - 1, 64);
+        const uint64_t total_span = rl64(incl, cnt - 1), total_ll = rl64(inl, cnt - 1);
         if (op + total_span > raw || lp + total_ll > nlit) {
             bad = true;
             break;
         }
-        for (uint64_t i = lane; i < total_ll; i += 64) lbuf[i] = lit[lp + i]; // the batch's literals
+        // the next batch's loads go out now and land while this one is replayed
+        rec = load_rec(q + cnt);
+        uint8_t npl[16];
+        load_lits(lp + total_ll, npl);
+        // this batch's literals into LDS: the prefetched first KB, the rest (long runs) loaded here
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (lane * 16 + k < total_ll) lbuf[lane * 16 + k] = pl[k];
+        for (uint64_t i0 = 1024 + lane * 16; i0 < total_ll; i0 += 64 * 16) {
+            uint8_t v[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) v[k] = i0 + k < total_ll ? lit[lp + i0 + k] : 0;
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if (i0 + k < total_ll) lbuf[i0 + k] = v[k];
+        }
         lds_order();
         const uint64_t ex_span = incl - span, ex_ll = inl - (lane < lim ? r.ll : 0);
         if (lane < cnt) // literal runs, one lane each
@@ -500,10 +543,10 @@ __global__ void __launch_bounds__(64) zstd_exec_kernel(const tfz::ZSeq *seq, con
         lds_order();
         const uint64_t bop = op; // window-resident: positions >= bop - ZHALF
         for (uint32_t j = 0; j < cnt; ++j) { // matches in order
-            const uint64_t ml = __shfl(r.ml, (int)j, 64);
+            const uint32_t ml = rl32(r.ml, j);
             if (!ml) continue;
-            const uint64_t off = __shfl(r.off, (int)j, 64);
-            const uint64_t d = op + __shfl(ex_span, (int)j, 64) + __shfl(r.ll, (int)j, 64);
+            const uint32_t off = rl32(r.off, j);
+            const uint64_t d = op + rl64(ex_span, j) + rl32(r.ll, j);
             if (off == 0 || off > d - fstart) {
                 bad = true;
                 break;
@@ -513,10 +556,10 @@ __global__ void __launch_bounds__(64) zstd_exec_kernel(const tfz::ZSeq *seq, con
                 zsync_global();
                 synced = bop;
             }
-            for (uint64_t base = 0; base < ml; base += 64) {
-                const uint64_t i = base + lane;
+            for (uint32_t base = 0; base < ml; base += 64) {
+                const uint32_t i = base + lane;
                 if (i < ml) {
-                    const uint64_t sp = off < 64 ? d - off + (i % off) : d + i - off;
+                    const uint64_t sp = off < 64 ? d - off + i % off : d + i - off;
                     win[(d + i) & ZWM] = (near || sp >= bop) ? win[sp & ZWM] : out[sp];
                 }
                 lds_order();
@@ -526,6 +569,8 @@ __global__ void __launch_bounds__(64) zstd_exec_kernel(const tfz::ZSeq *seq, con
         op += total_span;
         lp += total_ll;
         q += cnt;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) pl[k] = npl[k];
     }
     if (lane == 0 && (bad || op != raw || lp != nlit)) atomicOr(err, 1u);
 }

@@ -54,8 +54,19 @@ struct FseEntry {
     uint8_t bits;
 };
 
+// A sequence decoding-table entry: the FSE state transition (base, bits) and the symbol's
+// baseline + additional bits (literal / match length codes, or offset code c: 1 << c, c bits),
+// so each of the three codes of a sequence costs one table read (zstd's ZSTD_seqSymbol).
+struct ZSeqEntry {
+    uint32_t value; // baseline of the decoded value
+    uint16_t base;  // next-state base
+    uint8_t bits;   // next-state bits
+    uint8_t sym;    // the code (while the table is built)
+    uint8_t add;    // additional bits of the value
+};
+
 struct ZWork {
-    FseEntry ll[512], of[256], ml[512]; // accuracy logs <= 9 / 8 / 9
+    ZSeqEntry ll[512], of[256], ml[512]; // accuracy logs <= 9 / 8 / 9
     int ll_log, of_log, ml_log;
     bool ll_ok, of_ok, ml_ok;             // a table exists for Repeat mode
     uint16_t huf[1 << ZHUF_MAXBITS];      // symbol | nbBits << 8
@@ -243,7 +254,7 @@ ZHD int64_t fse_read_ncount(const uint8_t *src, int64_t n, int max_log, int max_
 }
 
 // decoding table from normalized counts (FSE_buildDTable)
-ZHD bool fse_build(FseEntry *t, const int16_t *norm, int nsym, int log) {
+template <typename E> ZHD bool fse_build(E *t, const int16_t *norm, int nsym, int log) {
     const int size = 1 << log;
     int high = size - 1;
     uint16_t next[256];
@@ -275,7 +286,7 @@ ZHD bool fse_build(FseEntry *t, const int16_t *norm, int nsym, int log) {
     return true;
 }
 
-ZHD void fse_rle(FseEntry *t, int sym) {
+template <typename E> ZHD void fse_rle(E *t, int sym) {
     t[0].sym = (uint8_t)sym;
     t[0].bits = 0;
     t[0].base = 0;
@@ -429,10 +440,23 @@ ZHD uint64_t xxh64(const uint8_t *p, uint64_t len) {
     return h;
 }
 
+// symbol -> baseline and additional bits for every entry of a sequence table of `size` entries
+// (kind 0 literal lengths, 1 offsets, 2 match lengths); false on a symbol past the kind's range
+ZHD bool seq_finish(ZSeqEntry *t, int size, int kind) {
+    const int max_sym = kind == 0 ? 35 : kind == 1 ? 31 : 52;
+    for (int u = 0; u < size; ++u) {
+        const int c = t[u].sym;
+        if (c > max_sym) return false;
+        t[u].value = kind == 0 ? ll_base(c) : kind == 1 ? (1u << c) : ml_base(c);
+        t[u].add = (uint8_t)(kind == 0 ? ll_bits(c) : kind == 1 ? c : ml_bits(c));
+    }
+    return true;
+}
+
 // ---------------------------------------------------------------- stage 1: blocks -> records
 // a sequence-table description of one kind (mode from the compression-modes byte)
 ZHD int64_t seq_table(const uint8_t *src, int64_t n, int mode, int kind, ZWork *w) {
-    FseEntry *t = kind == 0 ? w->ll : kind == 1 ? w->of : w->ml;
+    ZSeqEntry *t = kind == 0 ? w->ll : kind == 1 ? w->of : w->ml;
     int &log = kind == 0 ? w->ll_log : kind == 1 ? w->of_log : w->ml_log;
     bool &ok = kind == 0 ? w->ll_ok : kind == 1 ? w->of_ok : w->ml_ok;
     const int max_sym = kind == 0 ? 35 : kind == 1 ? 31 : 52, max_log = kind == 1 ? 8 : 9;
@@ -441,22 +465,22 @@ ZHD int64_t seq_table(const uint8_t *src, int64_t n, int mode, int kind, ZWork *
         const int nsym = kind == 0 ? 36 : kind == 1 ? 29 : 53;
         for (int s = 0; s < nsym; ++s) norm[s] = kind == 0 ? ll_default(s) : kind == 1 ? of_default(s) : ml_default(s);
         log = kind == 1 ? 5 : 6;
-        ok = fse_build(t, norm, nsym, log);
+        ok = fse_build(t, norm, nsym, log) && seq_finish(t, 1 << log, kind);
         return ok ? 0 : -1;
     }
     if (mode == 1) { // RLE
         if (n < 1 || src[0] > max_sym) return -1;
         fse_rle(t, src[0]);
         log = 0;
-        ok = true;
-        return 1;
+        ok = seq_finish(t, 1, kind);
+        return ok ? 1 : -1;
     }
     if (mode == 2) {
         int16_t norm[53];
         int nsym;
         const int64_t used = fse_read_ncount(src, n, max_log, max_sym, norm, log, nsym);
         if (used < 0) return -1;
-        ok = fse_build(t, norm, nsym, log);
+        ok = fse_build(t, norm, nsym, log) && seq_finish(t, 1 << log, kind);
         return ok ? used : -1;
     }
     return ok ? 0 : -1; // repeat: the previous block's table
@@ -473,7 +497,7 @@ ZHD bool put_seq(ZOut &o, const ZSeq &r, uint32_t lane, uint32_t nl) {
 // One compressed block: its literals appended to o.lit, its sequences (repeat offsets resolved)
 // appended as records.  op = the packet frame's output so far, fstart = where the current ZSTD
 // frame's output began (offsets reach back into this frame only), cap = the output capacity.
-ZHD bool zblock_entropy(const uint8_t *src, int64_t n, uint64_t &op, uint64_t fstart, uint64_t cap, uint32_t *rep,
+ZHD bool zblock_entropy(const uint8_t *src, int64_t n, uint64_t &op, uint64_t fstart, uint64_t cap, uint32_t (&rep)[3],
                         ZWork *w, ZOut &o, uint32_t lane, uint32_t nl) {
     // ---- literals section
     if (n < 1) return false;
@@ -538,11 +562,12 @@ ZHD bool zblock_entropy(const uint8_t *src, int64_t n, uint64_t &op, uint64_t fs
             const int64_t seg = (lsize + 3) / 4;
             if (3 * seg > lsize) return false;
             const uint8_t *b = cs + 6;
-            const int64_t st[5] = {0, s1, s1 + s2, s1 + s2 + s3, s1 + s2 + s3 + s4};
             // stream k by lane k (every stream by lane 0 when the caller runs one lane)
             for (uint32_t k = lane; k < 4; k += nl) {
                 const int64_t cnt = k < 3 ? seg : (int64_t)lsize - 3 * seg;
-                bad = bad || !huf_stream(w, b + st[k], st[k + 1] - st[k], lit + k * seg, cnt);
+                const int64_t at = k == 0 ? 0 : k == 1 ? s1 : k == 2 ? s1 + s2 : s1 + s2 + s3;
+                const int64_t len = k == 0 ? s1 : k == 1 ? s2 : k == 2 ? s3 : s4;
+                bad = bad || !huf_stream(w, b + at, len, lit + k * seg, cnt);
             }
         }
         if (ZANY(bad)) return false;
@@ -583,33 +608,34 @@ ZHD bool zblock_entropy(const uint8_t *src, int64_t n, uint64_t &op, uint64_t fs
         BackBits bb;
         if (!bb.init(src + ip, n - ip)) return false;
         uint32_t sll = (uint32_t)bb.read(w->ll_log), sof = (uint32_t)bb.read(w->of_log), sml = (uint32_t)bb.read(w->ml_log);
+        uint32_t r0 = rep[0], r1 = rep[1], r2 = rep[2]; // the repeat offsets, in registers
         for (uint32_t q = 0; q < nseq; ++q) {
-            const int llc = w->ll[sll].sym, ofc = w->of[sof].sym, mlc = w->ml[sml].sym;
-            if (llc > 35 || mlc > 52 || ofc > 31) return false;
-            const uint64_t ofv = (1ull << ofc) + bb.read(ofc);
-            const uint32_t ml = ml_base(mlc) + (uint32_t)bb.read(ml_bits(mlc));
-            const uint32_t ll = ll_base(llc) + (uint32_t)bb.read(ll_bits(llc));
+            // one table read per code (the symbols were checked when the tables were built)
+            const ZSeqEntry el = w->ll[sll], eo = w->of[sof], em = w->ml[sml];
+            const uint64_t ofv = (uint64_t)eo.value + bb.read(eo.add);
+            const uint32_t ml = em.value + (uint32_t)bb.read(em.add);
+            const uint32_t ll = el.value + (uint32_t)bb.read(el.add);
             if (q + 1 < nseq) { // state updates: LL, ML, OF
-                sll = w->ll[sll].base + (uint32_t)bb.read(w->ll[sll].bits);
-                sml = w->ml[sml].base + (uint32_t)bb.read(w->ml[sml].bits);
-                sof = w->of[sof].base + (uint32_t)bb.read(w->of[sof].bits);
+                sll = el.base + (uint32_t)bb.read(el.bits);
+                sml = em.base + (uint32_t)bb.read(em.bits);
+                sof = eo.base + (uint32_t)bb.read(eo.bits);
             }
             if (bb.pos < 0) return false;
             uint64_t off;
             if (ofv > 3) {
                 off = ofv - 3;
-                rep[2] = rep[1];
-                rep[1] = rep[0];
-                rep[0] = (uint32_t)off;
+                r2 = r1;
+                r1 = r0;
+                r0 = (uint32_t)off;
             } else {
                 const int idx = (int)ofv - 1 + (ll == 0 ? 1 : 0);
                 if (idx == 0) {
-                    off = rep[0];
+                    off = r0;
                 } else {
-                    const uint32_t t = idx == 3 ? rep[0] - 1 : rep[idx];
-                    if (idx != 1) rep[2] = rep[1];
-                    rep[1] = rep[0];
-                    rep[0] = t;
+                    const uint32_t t = idx == 3 ? r0 - 1 : idx == 1 ? r1 : r2;
+                    if (idx != 1) r2 = r1;
+                    r1 = r0;
+                    r0 = t;
                     off = t;
                 }
             }
@@ -619,6 +645,9 @@ ZHD bool zblock_entropy(const uint8_t *src, int64_t n, uint64_t &op, uint64_t fs
             lit_pos += ll;
         }
         if (bb.pos != 0) return false;
+        rep[0] = r0;
+        rep[1] = r1;
+        rep[2] = r2;
     } else if (ip != n) {
         return false;
     }
@@ -703,7 +732,14 @@ ZHD int64_t zstd_frame_entropy(const uint8_t *src, int64_t n, uint64_t cap, ZWor
                     const uint8_t *bsrc = src + ip;
                     if (w->stage) { // the block's bytes into LDS: every bit read then costs an LDS load
                         ZSYNC_LDS();
-                        for (uint32_t i = lane; i < bsize; i += nl) w->stage[i] = bsrc[i];
+                        for (uint32_t i0 = lane * 16; i0 < bsize; i0 += nl * 16) { // 16 loads in flight a lane
+                            uint8_t v[16];
+#pragma unroll
+                            for (int k = 0; k < 16; ++k) v[k] = i0 + k < bsize ? bsrc[i0 + k] : 0;
+#pragma unroll
+                            for (int k = 0; k < 16; ++k)
+                                if (i0 + k < bsize) w->stage[i0 + k] = v[k];
+                        }
                         ZSYNC_LDS();
                         bsrc = w->stage;
                     }

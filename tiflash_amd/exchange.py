@@ -6,17 +6,23 @@ over xGMI on MI355X; "gloo" on CPU for the multi-process tests).
 The sender side is tfg_hash_partition (weak hash -> fillSelector -> stable scatter): its output is
 partition-major, partition p = rows [offsets[p], offsets[p+1]), which is exactly an all-to-all
 send buffer.  An exchange is fused, whatever the number of columns and of row sets ("sides",
-e.g. a join's build and probe sides, or a String column's chars next to its rows):
+e.g. a join's build and probe sides, or a String column's chars next to its rows) — the same
+exchange as the C++ boundary's tfa::MPPExchange::exchange (host/operators.cpp), over the same
+ABI calls and the same wire layout:
 
-* every side's columns are packed side by side into one row record (the reference's packet
-  carries a whole Block too, newMPPExchangeWriter.cpp:64-95);
+* the send buffer is peer-major; peer p's segment holds every column plane's rows of p in turn
+  (side by side, planar: a column's values, not row records), packed on the device by ONE
+  tfg_pack_planes launch (the reference's packet carries a whole Block too,
+  newMPPExchangeWriter.cpp:64-95);
 * ONE counts all-to-all ([world, sides] row counts) and one host read of it, which sizes the
   receive buffer (RCCL's send / recv take host sizes);
-* ONE all_to_all_single of a peer-major byte buffer holding, for each peer, its rows of every
-  side in turn.
+* ONE all_to_all_single of the packed bytes, then ONE tfg_unpack_planes launch into the received
+  columns (source rank r's rows after rank r-1's).
 
-xGMI is point-to-point, so fewer, larger transfers per peer pair are what the links want.
+xGMI is point-to-point, so fewer, larger transfers per peer pair are what the links want.  On CPU
+tensors (gloo) the same layout is built with torch slicing.
 """
+import ctypes
 from typing import List, Sequence, Tuple
 
 import torch
@@ -25,7 +31,7 @@ import torch.distributed as dist
 
 def _row_width(c: torch.Tensor) -> int:
     """Bytes per row of a column, from its schema (dtype, trailing shape), not from its data, so
-    a rank with no rows agrees with its peers on the record layout."""
+    a rank with no rows agrees with its peers on the layout."""
     w = c.element_size()
     for d in c.shape[1:]:
         w *= int(d)
@@ -42,11 +48,30 @@ def _row_bytes(c: torch.Tensor, n: int) -> torch.Tensor:
     return c.view(torch.uint8).reshape(n, _row_width(c))
 
 
-def exchange_sides(sides: Sequence[Tuple[Sequence[torch.Tensor], Sequence[int]]], group=None) -> List[List[torch.Tensor]]:
+_CTX = {}
+
+
+def _default_ctx(dev):
+    """A tfg context on the current stream of `dev` (one per device and stream)."""
+    import tiflash_amd as tfa
+    st = torch.cuda.current_stream(dev)
+    key = (dev.index, st.cuda_stream)
+    if key not in _CTX:
+        _CTX[key] = tfa.Context(dev.index if dev.index is not None else 0, stream=st)
+    return _CTX[key]
+
+
+def _empty_col(rows, dt, shp, dev):
+    return torch.empty((rows,) + shp, dtype=dt, device=dev)
+
+
+def exchange_sides(sides: Sequence[Tuple[Sequence[torch.Tensor], Sequence[int]]], group=None,
+                   ctx=None) -> List[List[torch.Tensor]]:
     """sides: [(columns, offsets)], each side's rows partition-major (rows [offsets[p],
     offsets[p+1]) go to rank p; offsets are host ints).  Returns, per side, the received columns
     (rows from rank 0 first; ExchangeReceiver's concatenation order is unspecified in the
-    reference and consumers must not depend on it)."""
+    reference and consumers must not depend on it).  ctx: the tfg context of device columns (a
+    context on the current stream when None)."""
     world = dist.get_world_size(group)
     for _, offs in sides:
         if len(offs) != world + 1:
@@ -58,56 +83,72 @@ def exchange_sides(sides: Sequence[Tuple[Sequence[torch.Tensor], Sequence[int]]]
         outs = exchange_sides([([c.cpu() for c in cols], offs) for cols, offs in sides], group)
         return [[o.to(dev) for o in side] for side in outs]
     S = len(sides)
-    recs, specs, rowb = [], [], []
-    for cols, offs in sides:
+    # the planes, in wire order: side by side, each side's columns in turn
+    planes, widths, side_of, specs = [], [], [], []
+    for s, (cols, offs) in enumerate(sides):
         n = int(offs[world])
-        parts = [_row_bytes(c, n) for c in cols]
-        specs.append([(p.shape[1], c.dtype, tuple(c.shape[1:])) for p, c in zip(parts, cols)])
-        recs.append(torch.cat(parts, 1) if len(parts) > 1 else parts[0])
-        rowb.append(recs[-1].shape[1])
+        for c in cols:
+            planes.append(_row_bytes(c, n))
+            widths.append(_row_width(c))
+            side_of.append(s)
+            specs.append((c.dtype, tuple(c.shape[1:])))
+    NP = len(planes)
     send_counts = [[int(offs[p + 1] - offs[p]) for _, offs in sides] for p in range(world)]
     cnt = torch.tensor(send_counts, dtype=torch.int64, device=dev).reshape(-1)
     rcnt = torch.empty_like(cnt)
     dist.all_to_all_single(rcnt, cnt, group=group)
     recv_counts = rcnt.reshape(world, S).tolist()
-    send_bytes = [sum(send_counts[p][s] * rowb[s] for s in range(S)) for p in range(world)]
-    recv_bytes = [sum(recv_counts[p][s] * rowb[s] for s in range(S)) for p in range(world)]
-    if S == 1:
-        send = recs[0].reshape(-1)  # already peer-major
+    send_bytes = [sum(send_counts[p][side_of[k]] * widths[k] for k in range(NP)) for p in range(world)]
+    recv_bytes = [sum(recv_counts[p][side_of[k]] * widths[k] for k in range(NP)) for p in range(world)]
+    total_rows = [sum(recv_counts[p][side_of[k]] for p in range(world)) for k in range(NP)]
+    outs = [_empty_col(total_rows[k], specs[k][0], specs[k][1], dev) for k in range(NP)]
+    if dev.type == "cpu":
+        send = torch.cat([planes[k][int(sides[side_of[k]][1][p]):int(sides[side_of[k]][1][p + 1])].reshape(-1)
+                          for p in range(world) for k in range(NP)] + [torch.empty(0, dtype=torch.uint8)])
+        recv = torch.empty(sum(recv_bytes), dtype=torch.uint8)
+        dist.all_to_all_single(recv, send, recv_bytes, send_bytes, group=group)
+        pos, r0 = 0, [0] * NP
+        for p in range(world):
+            for k in range(NP):
+                r = recv_counts[p][side_of[k]]
+                if r:
+                    dst = outs[k].reshape(-1).view(torch.uint8)
+                    dst[r0[k] * widths[k]:(r0[k] + r) * widths[k]] = recv[pos:pos + r * widths[k]]
+                pos += r * widths[k]
+                r0[k] += r
     else:
-        pieces = [recs[s][int(sides[s][1][p]):int(sides[s][1][p + 1])].reshape(-1) for p in range(world) for s in range(S)]
-        send = torch.cat(pieces)
-    recv = torch.empty(max(sum(recv_bytes), 1), dtype=torch.uint8, device=dev)[:sum(recv_bytes)]
-    dist.all_to_all_single(recv, send, recv_bytes, send_bytes, group=group)
-    slices = [[] for _ in range(S)]
-    pos = 0
-    for p in range(world):
-        for s in range(S):
-            nb = recv_counts[p][s] * rowb[s]
-            slices[s].append(recv[pos:pos + nb].reshape(-1, rowb[s]))
-            pos += nb
-    outs = []
-    for s in range(S):
-        if S == 1:
-            rec = recv.reshape(-1, rowb[s])  # rows of every peer, already contiguous
-        else:
-            rec = torch.cat(slices[s]) if len(slices[s]) > 1 else slices[s][0]
-        cols, a = [], 0
-        for w, dt, shp in specs[s]:
-            piece = rec[:, a:a + w] if len(specs[s]) > 1 else rec
-            if piece.shape[0] == 0:
-                cols.append(torch.empty((0,) + shp, dtype=dt, device=rec.device))
-            else:
-                cols.append(piece.contiguous().view(dt).reshape((-1,) + shp))
-            a += w
-        outs.append(cols)
-    return outs
+        import tiflash_amd as tfa
+        ctx = ctx or _default_ctx(dev)
+        send = torch.empty(max(sum(send_bytes), 1), dtype=torch.uint8, device=dev)
+        recv = torch.empty(max(sum(recv_bytes), 1), dtype=torch.uint8, device=dev)
+        ptrs = (ctypes.c_void_p * (world * NP))()
+        rows = (ctypes.c_uint64 * (world * NP))()
+        for p in range(world):
+            for k in range(NP):
+                o0 = int(sides[side_of[k]][1][p])
+                r = send_counts[p][side_of[k]]
+                rows[p * NP + k] = r
+                ptrs[p * NP + k] = planes[k].data_ptr() + o0 * widths[k] if r else 0
+        w_arr = (ctypes.c_int * NP)(*widths)
+        seg = (ctypes.c_uint64 * world)()
+        tfa.check(tfa.lib().tfg_pack_planes(ctx.h, ctypes.c_int(world), ctypes.c_int(NP), ptrs, w_arr, rows,
+                                            tfa._p(send), seg))
+        assert list(seg) == send_bytes
+        dist.all_to_all_single(recv[:sum(recv_bytes)], send[:sum(send_bytes)], recv_bytes, send_bytes, group=group)
+        rrows = (ctypes.c_uint64 * (world * NP))(*[recv_counts[p][side_of[k]] for p in range(world) for k in range(NP)])
+        tfa.check(tfa.lib().tfg_unpack_planes(ctx.h, ctypes.c_int(world), ctypes.c_int(NP), w_arr, rrows,
+                                              tfa._p(recv), tfa._ptr_array(outs)))
+    res, k = [], 0
+    for cols, _ in sides:
+        res.append(outs[k:k + len(cols)])
+        k += len(cols)
+    return res
 
 
-def exchange_partitions(cols: Sequence[torch.Tensor], offsets: Sequence[int], group=None) -> List[torch.Tensor]:
+def exchange_partitions(cols: Sequence[torch.Tensor], offsets: Sequence[int], group=None, ctx=None) -> List[torch.Tensor]:
     """One side: sends rows [offsets[p], offsets[p+1]) of every column to rank p in one fused
     exchange; returns the received columns."""
-    return exchange_sides([(cols, offsets)], group)[0]
+    return exchange_sides([(cols, offsets)], group, ctx)[0]
 
 
 def exchange_string_rows(ctx, perm, offs, row_cols, strings, group=None):
@@ -129,7 +170,7 @@ def exchange_string_rows(ctx, perm, offs, row_cols, strings, group=None):
         ends_at = torch.where(idx >= 0, ge[idx.clamp(min=0)] if ge.numel() else idx * 0, idx * 0)
         boff = [0] + [int(x) for x in ends_at.tolist()]
         chars_sides.append(([gc], boff))
-    got = exchange_sides([(rows + lens, offs)] + chars_sides, group)
+    got = exchange_sides([(rows + lens, offs)] + chars_sides, group, ctx)
     rcols = got[0][:len(rows)]
     rlens = got[0][len(rows):]
     out_strings = []
@@ -169,7 +210,7 @@ def two_phase_merge_keys(ctx, partial, final, group=None, collators=None):
         packed = None
     if packed is not None:
         send = tfa.gather(ctx, perm, [packed["keys"]] + list(packed["states"]))
-        recv = exchange_partitions(send, offs, group)
+        recv = exchange_partitions(send, offs, group, ctx)
         final.consume_partial_packed(recv[0], recv[1:])
         return
     fixed = [k for t, k in zip(partial.key_types, cols["keys"]) if t != tfa.STRING]

@@ -868,13 +868,41 @@ void FineGrainedShuffleWriter::flush() {
     }
 }
 
-MPPExchange::MPPExchange(Context &ctx, int nranks, int rank, const uint8_t *unique_id, size_t id_len)
-    : ctx_(ctx), nranks_(nranks), rank_(rank) {
+RcclTransport::RcclTransport(Context &ctx, int nranks, int rank, const uint8_t *unique_id, size_t id_len)
+    : nranks_(nranks), rank_(rank) {
     check(tfg_comm_init(ctx.raw(), nranks, rank, unique_id, id_len, &comm_), "tfg_comm_init");
 }
 
-MPPExchange::~MPPExchange() {
+RcclTransport::~RcclTransport() {
     if (comm_) tfg_comm_destroy(comm_);
+}
+
+void RcclTransport::alltoallCounts(const uint64_t *send, uint64_t *recv) {
+    check(tfg_alltoall_counts(comm_, send, recv), "tfg_alltoall_counts");
+}
+
+void RcclTransport::alltoallv(const void *send, const uint64_t *send_bytes, const uint64_t *send_displs, void *recv,
+                              const uint64_t *recv_bytes, const uint64_t *recv_displs) {
+    check(tfg_alltoallv(comm_, send, send_bytes, send_displs, recv, recv_bytes, recv_displs), "tfg_alltoallv");
+}
+
+MPPExchange::MPPExchange(Context &ctx, int nranks, int rank, const uint8_t *unique_id, size_t id_len)
+    : MPPExchange(ctx, std::make_shared<RcclTransport>(ctx, nranks, rank, unique_id, id_len)) {}
+
+MPPExchange::MPPExchange(Context &ctx, std::shared_ptr<ExchangeTransport> transport)
+    : ctx_(ctx), t_(std::move(transport)), nranks_(t_->nranks()), rank_(t_->rank()) {}
+
+static Block emptyOfHeader(Context &ctx, const Block &header) { // zero-row columns of the header's types
+    Block empty;
+    for (const auto &c : header.getColumnsWithTypeAndName()) {
+        auto z = std::make_shared<IColumn>();
+        z->type = c.type;
+        z->data = std::make_shared<DeviceBuffer>(ctx, 1);
+        if (c.type.isString()) z->offsets = std::make_shared<DeviceBuffer>(ctx, 8);
+        if (c.type.nullable) z->nullmap = std::make_shared<DeviceBuffer>(ctx, 1);
+        empty.insert({z, z->type, c.name});
+    }
+    return empty;
 }
 
 Block MPPExchange::exchangePackets(const std::vector<Block> &partitions) {
@@ -889,7 +917,7 @@ Block MPPExchange::exchangePackets(const std::vector<Block> &partitions) {
         sd[p] = so;
         so += sb[p];
     }
-    check(tfg_alltoall_counts(comm_, sb.data(), rb.data()), "tfg_alltoall_counts");
+    t_->alltoallCounts(sb.data(), rb.data());
     for (int p = 0; p < nranks_; ++p) {
         rd[p] = ro;
         ro += rb[p];
@@ -897,22 +925,13 @@ Block MPPExchange::exchangePackets(const std::vector<Block> &partitions) {
     DeviceBuffer send(ctx_, std::max<uint64_t>(so, 1)), recv(ctx_, std::max<uint64_t>(ro, 1));
     for (int p = 0; p < nranks_; ++p)
         if (sb[p]) check(tfg_copy(ctx_.raw(), (char *)send.data() + sd[p], pk[p].buf->data(), sb[p]), "tfg_copy");
-    check(tfg_alltoallv(comm_, send.data(), sb.data(), sd.data(), recv.data(), rb.data(), rd.data()), "tfg_alltoallv");
+    t_->alltoallv(send.data(), sb.data(), sd.data(), recv.data(), rb.data(), rd.data());
     ctx_.sync();
     std::vector<Block> got;
     for (int p = 0; p < nranks_; ++p)
         if (rb[p]) got.push_back(decodeBlockPacket(ctx_, header, (const uint8_t *)recv.data() + rd[p], rb[p], TFG_CODEC_V1));
     if (!got.empty()) return concatenateBlocks(ctx_, got);
-    Block empty; // no rows arrived: zero-row columns of the header's types
-    for (const auto &c : header.getColumnsWithTypeAndName()) {
-        auto z = std::make_shared<IColumn>();
-        z->type = c.type;
-        z->data = std::make_shared<DeviceBuffer>(ctx_, 1);
-        if (c.type.isString()) z->offsets = std::make_shared<DeviceBuffer>(ctx_, 8);
-        if (c.type.nullable) z->nullmap = std::make_shared<DeviceBuffer>(ctx_, 1);
-        empty.insert({z, z->type, c.name});
-    }
-    return empty;
+    return emptyOfHeader(ctx_, header);
 }
 
 Block MPPExchange::exchange(const std::vector<Block> &partitions) {
@@ -921,62 +940,84 @@ Block MPPExchange::exchange(const std::vector<Block> &partitions) {
     const Block &proto = partitions[0];
     for (const auto &c : proto.getColumnsWithTypeAndName())
         if (c.type.isString()) return exchangePackets(partitions);
+    const size_t ncols = proto.columns();
+    // the planes, decided by the schema every rank shares: each column's values, then its null
+    // map when the type is Nullable (a partition whose column carries none sends zeros)
+    std::vector<int> widths, plane_col;
+    for (size_t j = 0; j < ncols; ++j) {
+        const DataType t = proto.safeGetByPosition(j).type;
+        widths.push_back((int)t.width());
+        plane_col.push_back((int)j);
+        if (t.nullable) {
+            widths.push_back(1);
+            plane_col.push_back(-(int)j - 1);
+        }
+    }
+    const int np = (int)widths.size();
     std::vector<uint64_t> send_rows(nranks_), recv_rows(nranks_);
-    for (int p = 0; p < nranks_; ++p) send_rows[p] = partitions[p].rows();
-    check(tfg_alltoall_counts(comm_, send_rows.data(), recv_rows.data()), "tfg_alltoall_counts");
-    uint64_t total_send = 0, total_recv = 0;
+    std::vector<ColumnPtr> hold;
+    std::vector<const void *> planes((size_t)nranks_ * np, nullptr);
+    for (int p = 0; p < nranks_; ++p) {
+        const Block &b = partitions[p];
+        if (b.columns() != ncols) throw Exception("partitions of different schemas", ErrorCodes::LOGICAL_ERROR);
+        send_rows[p] = b.rows();
+        for (int k = 0; k < np; ++k) {
+            const int j = plane_col[k] >= 0 ? plane_col[k] : -plane_col[k] - 1;
+            ColumnPtr c = materialize(ctx_, b.safeGetByPosition(j).column);
+            hold.push_back(c);
+            if (plane_col[k] >= 0) {
+                planes[(size_t)p * np + k] = c->dataPtr();
+            } else {
+                if (c->nullmap && !proto.safeGetByPosition(j).type.nullable)
+                    throw Exception("null map on a column of non-Nullable type", ErrorCodes::LOGICAL_ERROR);
+                planes[(size_t)p * np + k] = c->nullPtr(); // null: a zero plane
+            }
+        }
+    }
+    t_->alltoallCounts(send_rows.data(), recv_rows.data());
+    std::vector<uint64_t> send_pr((size_t)nranks_ * np), recv_pr((size_t)nranks_ * np); // rows per plane
+    for (int p = 0; p < nranks_; ++p)
+        for (int k = 0; k < np; ++k) {
+            send_pr[(size_t)p * np + k] = send_rows[p];
+            recv_pr[(size_t)p * np + k] = recv_rows[p];
+        }
+    uint64_t row_bytes = 0, total_send = 0, total_recv = 0;
+    for (int w : widths) row_bytes += (uint64_t)w;
     for (int p = 0; p < nranks_; ++p) {
         total_send += send_rows[p];
         total_recv += recv_rows[p];
     }
-    Block out;
-    for (size_t j = 0; j < proto.columns(); ++j) {
-        // the schema type, shared by every rank, decides the planes: a rank whose Nullable column
-        // happens to carry no null map still sends a zero plane, so every rank issues the same
-        // sequence of collectives
-        const DataType t = proto.safeGetByPosition(j).type;
-        if (t.isString()) throw Exception("exchanging String columns", ErrorCodes::NOT_IMPLEMENTED);
-        const bool nullable = t.nullable;
-        for (const auto &b : partitions)
-            if (b.safeGetByPosition(j).column->nullmap && !nullable)
-                throw Exception("null map on a column of non-Nullable type " + t.getName(), ErrorCodes::LOGICAL_ERROR);
-        auto c = std::make_shared<IColumn>();
-        c->type = t;
-        c->type.nullable = nullable;
-        c->rows = total_recv;
-        // one pass per byte plane: values, then the null map
-        for (int plane = 0; plane < (nullable ? 2 : 1); ++plane) {
-            const size_t w = plane == 0 ? t.width() : 1;
-            DeviceBuffer send(ctx_, total_send * w);
-            auto recv = std::make_shared<DeviceBuffer>(ctx_, total_recv * w);
-            std::vector<uint64_t> sb(nranks_), sd(nranks_), rb(nranks_), rd(nranks_);
-            uint64_t so = 0, ro = 0;
-            for (int p = 0; p < nranks_; ++p) {
-                ColumnPtr src = materialize(ctx_, partitions[p].safeGetByPosition(j).column);
-                const size_t bytes = send_rows[p] * w;
-                if (plane == 0) {
-                    check(tfg_copy(ctx_.raw(), (char *)send.data() + so, src->dataPtr(), bytes), "tfg_copy");
-                } else if (src->nullmap) {
-                    check(tfg_copy(ctx_.raw(), (char *)send.data() + so, src->nullPtr(), bytes), "tfg_copy");
-                } else if (bytes) {
-                    std::vector<uint8_t> z(bytes, 0);
-                    check(tfg_upload(ctx_.raw(), (char *)send.data() + so, z.data(), bytes), "tfg_upload");
-                }
-                sb[p] = bytes;
-                sd[p] = so;
-                so += bytes;
-                rb[p] = recv_rows[p] * w;
-                rd[p] = ro;
-                ro += rb[p];
-            }
-            check(tfg_alltoallv(comm_, send.data(), sb.data(), sd.data(), recv->data(), rb.data(), rd.data()),
-                  "tfg_alltoallv");
-            ctx_.sync();
-            if (plane == 0) c->data = recv;
-            else c->nullmap = recv;
-        }
-        out.insert({c, c->type, proto.safeGetByPosition(j).name});
+    DeviceBuffer send(ctx_, std::max<uint64_t>(total_send * row_bytes, 1));
+    auto recv = std::make_shared<DeviceBuffer>(ctx_, std::max<uint64_t>(total_recv * row_bytes, 1));
+    std::vector<uint64_t> sb(nranks_), sd(nranks_), rb(nranks_), rd(nranks_);
+    check(tfg_pack_planes(ctx_.raw(), nranks_, np, planes.data(), widths.data(), send_pr.data(), send.data(), sb.data()),
+          "tfg_pack_planes");
+    for (int p = 0; p < nranks_; ++p) {
+        sd[p] = p ? sd[p - 1] + sb[p - 1] : 0;
+        rb[p] = recv_rows[p] * row_bytes;
+        rd[p] = p ? rd[p - 1] + rb[p - 1] : 0;
     }
+    t_->alltoallv(send.data(), sb.data(), sd.data(), recv->data(), rb.data(), rd.data());
+    // the received planes: every source's rows concatenated in rank order
+    Block out;
+    std::vector<std::shared_ptr<IColumn>> cols(ncols);
+    std::vector<void *> outp(np);
+    for (int k = 0; k < np; ++k) {
+        const int j = plane_col[k] >= 0 ? plane_col[k] : -plane_col[k] - 1;
+        if (!cols[j]) {
+            cols[j] = std::make_shared<IColumn>();
+            cols[j]->type = proto.safeGetByPosition(j).type;
+            cols[j]->rows = total_recv;
+        }
+        auto buf = std::make_shared<DeviceBuffer>(ctx_, std::max<uint64_t>(total_recv * widths[k], 1));
+        if (plane_col[k] >= 0) cols[j]->data = buf;
+        else cols[j]->nullmap = buf;
+        outp[k] = buf->data();
+    }
+    check(tfg_unpack_planes(ctx_.raw(), nranks_, np, widths.data(), recv_pr.data(), recv->data(), outp.data()),
+          "tfg_unpack_planes");
+    ctx_.sync(); // the send / recv buffers are released on return
+    for (size_t j = 0; j < ncols; ++j) out.insert({cols[j], cols[j]->type, proto.safeGetByPosition(j).name});
     return out;
 }
 

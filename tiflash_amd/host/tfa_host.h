@@ -469,19 +469,56 @@ std::vector<Block> fineGrainedPartitionBlock(Context &ctx, const Block &block, c
 std::vector<Block> hashPartitionBlock(Context &ctx, const Block &block, const std::vector<size_t> &key_ids,
                                       uint32_t partition_num, const std::vector<int> &collators = {});
 
-// One-node exchange over RCCL: every rank contributes partition_num == nranks blocks and
-// receives the concatenation of its partition from every rank (ExchangeReceiver output).
+// The collective under an MPP exchange between the ranks of one query (what MPPTunnelSet's
+// tunnels carry between tasks): a counts exchange, then one byte all-to-all of device buffers.
+// RcclTransport is the product's (tfg_comm: RCCL over xGMI, one process per GPU); tests plug in
+// other transports (tests/cpp/test_host.cpp runs two processes over TCP).
+class ExchangeTransport {
+public:
+    virtual ~ExchangeTransport() = default;
+    virtual int nranks() const = 0;
+    virtual int rank() const = 0;
+    // recv[p] = send[this rank] of rank p (host arrays of nranks entries)
+    virtual void alltoallCounts(const uint64_t *send, uint64_t *recv) = 0;
+    // device buffers, host byte counts / displacements: slice p of send goes to rank p, rank p's
+    // slice lands at recv + recv_displs[p]
+    virtual void alltoallv(const void *send, const uint64_t *send_bytes, const uint64_t *send_displs, void *recv,
+                           const uint64_t *recv_bytes, const uint64_t *recv_displs) = 0;
+};
+
+class RcclTransport : public ExchangeTransport {
+public:
+    RcclTransport(Context &ctx, int nranks, int rank, const uint8_t *unique_id, size_t id_len);
+    ~RcclTransport() override;
+    int nranks() const override { return nranks_; }
+    int rank() const override { return rank_; }
+    void alltoallCounts(const uint64_t *send, uint64_t *recv) override;
+    void alltoallv(const void *send, const uint64_t *send_bytes, const uint64_t *send_displs, void *recv,
+                   const uint64_t *recv_bytes, const uint64_t *recv_displs) override;
+
+private:
+    tfg_comm *comm_ = nullptr;
+    int nranks_, rank_;
+};
+
+// One-node exchange: every rank contributes partition_num == nranks blocks and receives the
+// concatenation of its partition from every rank (ExchangeReceiver output).  Fused: one counts
+// exchange and ONE data all-to-all per call, whatever the number of columns — every column's value
+// plane and null plane of every destination packed peer-major on the device (tfg_pack_planes,
+// Nullable columns without a null map send a zero plane written on the device) and unpacked on
+// arrival (tfg_unpack_planes); no host sync besides the counts.  Blocks with String columns travel
+// as CHBlockChunkCodecV1 packets through the same single all-to-all.
 class MPPExchange {
 public:
-    MPPExchange(Context &ctx, int nranks, int rank, const uint8_t *unique_id, size_t id_len);
-    ~MPPExchange();
+    MPPExchange(Context &ctx, int nranks, int rank, const uint8_t *unique_id, size_t id_len); // over RCCL
+    MPPExchange(Context &ctx, std::shared_ptr<ExchangeTransport> transport);
     Block exchange(const std::vector<Block> &partitions);
     int nranks() const { return nranks_; }
     int rank() const { return rank_; }
 
 private:
     Context &ctx_;
-    tfg_comm *comm_ = nullptr;
+    std::shared_ptr<ExchangeTransport> t_;
     int nranks_, rank_;
     // blocks with String columns travel as CHBlockChunkCodecV1 packets (ExchangeSender ->
     // ExchangeReceiver): encoded on the device, packet bytes all-to-all, decoded on arrival
