@@ -110,8 +110,9 @@ typedef enum tfg_logic_op {
  * An aggregate argument type word is the tfg_type, optionally or-ed with TFG_ARG_NULLABLE (the
  * argument carries a null map) and, for Decimal arguments, TFG_ARG_PREC(p): the column's
  * DataTypeDecimal precision (0 = the type's maximum, 9 / 18 / 38 / 65).  Decimal256 sums are
- * exact: a Decimal(<=65) value is below 10^65 < 2^216, so fewer than 2^39 rows cannot reach the
- * 2^255 bound where checked_int256_t would throw. */
+ * exact and checked like the reference's checked_int256_t (libs/libcommon/include/common/types.h:35):
+ * the device keeps a fifth limb, and a consume or merge whose exact sum leaves Int256 returns
+ * TFG_ERR_OVERFLOW. */
 #define TFG_ARG_NULLABLE 0x100
 #define TFG_ARG_PREC(p) ((int)(p) << 16)
 #define TFG_ARG_TYPE(w) ((w) & 0xFF)

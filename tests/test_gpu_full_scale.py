@@ -7,10 +7,12 @@ row for row — the sizes the bench runs, where the kernels take paths small tes
   multiset of output rows against orc.JoinRef (Join::joinBlock restated, oracle/oracle.c
   orc_join_*; reference JoinPartition.cpp:1465-1644 probeBlockImplTypeCase).
 * C5: GROUP BY a String key "k%08d" over 10M ids, sum(Decimal(15,2)) -> Decimal(37,2) + count(*),
-  40M rows (~9.8M groups present): 4096 buckets (bbits 12), two-level 64 x 64 tiles, LDS tables at
-  capacity so buckets run spill passes.  Checked group by group against orc.AggKeys (Aggregator
-  with key_string / StringHashMap restated; reference Aggregator.cpp:566-1246).  Decimal sums are
-  exact 128-bit integers: bit-exact."""
+  100M rows as the bench (all but ~450 of the 10M ids present): the wide tiled path at its bench
+  geometry — 16384 buckets (two-level: 256 coarse tile-sorted buckets, regrouped 64 ways), LDS
+  tables at ~30 % load.  Spill passes are not reached at this load; the forced-spill cases (16
+  buckets at the C5 shape) are in tests/test_gpu_keys_agg.py.  Checked group by group against
+  orc.AggKeys (Aggregator with key_string / StringHashMap restated; reference
+  Aggregator.cpp:566-1246).  Decimal sums are exact 128-bit integers: bit-exact."""
 import numpy as np
 import pytest
 import torch
@@ -52,7 +54,7 @@ def test_c3_full_scale_join_matches_oracle(tfa, ctx, dev, orc):
 
 
 def test_c5_full_scale_string_groupby_matches_oracle(tfa, ctx, dev, orc):
-    n, G = 40_000_000, 10_000_000
+    n, G = 100_000_000, 10_000_000
     rng = np.random.default_rng(11)
     ids = rng.integers(0, G, n)
     v = rng.integers(0, 10**9, n, dtype=np.int64)

@@ -26,7 +26,7 @@
 //    before the match began (other lanes' stores are drained and the loads bypass the L1).
 //  * the frame table of a packet comes from one thread walking the 9-byte headers.
 #include "common.h"
-#include "zstd_dec.h"
+#include "codec_zstd.h"
 
 namespace tfg {
 namespace {
@@ -40,7 +40,6 @@ constexpr uint32_t ENC_FRAME = 64 * 1024;  // raw bytes per frame this encoder w
 constexpr int HASH_LOG = 12;
 constexpr uint64_t ENC_SLOT = FRAME_HDR + ENC_FRAME + ENC_FRAME / 255 + 16; // header + LZ4_COMPRESSBOUND
 constexpr int MIN_MATCH = 4, LAST_LITERALS = 5, MF_LIMIT = 12;
-constexpr uint64_t ZSTD_SCRATCH = (uint64_t)512 << 20; // stage-1 outputs per launch group (records + literals)
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 
@@ -295,286 +294,6 @@ __global__ void __launch_bounds__(64) lz4_decode_kernel(const uint8_t *pkt, cons
     if (lane == 0 && (bad || op != raw)) atomicOr(err, 1u);
 }
 
-// ---------------------------------------------------------------- ZSTD (zstd_dec.h)
-// Records of packet frame f start at zseq_base(f) - zseq_base(f0) of a launch over frames f0...:
-// zstd_seq_cap(raw_f, comp_f) apart (a monotone function of the exclusive sums, no scan needed).
-__host__ __device__ __forceinline__ uint64_t zseq_base(const uint64_t *foff, const uint64_t *roff, uint64_t f) {
-    return roff[f] / 3 + foff[f] * 2 / 3 + 16 * f;
-}
-
-// Stage 1: one wave per packet frame.  The compressed block is staged in LDS, the wave decodes it
-// in lockstep and writes the frame's records and literals; counts[2b] / [2b + 1] = records /
-// literal bytes.  err |= 1 when the frame is malformed or does not decode to its raw size.
-__global__ void __launch_bounds__(64) zstd_entropy_kernel(const uint8_t *pkt, const uint64_t *foff, const uint64_t *roff,
-                                                          uint64_t f0, tfz::ZSeq *seq, uint8_t *lits, uint64_t *counts,
-                                                          unsigned *err) {
-    __shared__ tfz::ZWork w;                  // FSE / Huffman tables (the decode's dependent chain)
-    __shared__ uint8_t stage[tfz::ZMAX_BLOCK]; // the compressed block being decoded (bit reads from LDS)
-    const uint64_t b = blockIdx.x, f = f0 + b;
-    w.stage = stage;
-    const uint64_t fb = foff[f + 1] - foff[f], raw = roff[f + 1] - roff[f];
-    tfz::ZOut o{};
-    o.seq = seq + (zseq_base(foff, roff, f) - zseq_base(foff, roff, f0));
-    o.seq_cap = zseq_base(foff, roff, f + 1) - zseq_base(foff, roff, f);
-    o.lit = lits + (roff[f] - roff[f0]);
-    o.lit_cap = raw;
-    const int64_t got = tfz::zstd_frame_entropy(pkt + foff[f] + FRAME_HDR, (int64_t)(fb - FRAME_HDR), raw, &w, o,
-                                                threadIdx.x, 64);
-    if (threadIdx.x == 0) {
-        counts[2 * b] = got == (int64_t)raw ? o.nseq : 0;
-        counts[2 * b + 1] = o.nlit;
-        if (got != (int64_t)raw) atomicOr(err, 1u);
-    }
-}
-
-constexpr int ZW = 1 << 16, ZWM = ZW - 1, ZHALF = ZW / 2; // stage-2 LDS output window
-
-__device__ __forceinline__ void lds_order() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-// lane j's value (j wave-uniform): v_readlane, no LDS round trip
-__device__ __forceinline__ uint32_t rl32(uint32_t v, uint32_t j) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)j); }
-__device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t j) {
-    return (uint64_t)rl32((uint32_t)v, j) | ((uint64_t)rl32((uint32_t)(v >> 32), j) << 32);
-}
-// the wave's global stores are complete and visible to its own later loads (match sources and
-// checksum bytes written by other lanes)
-__device__ __forceinline__ void zsync_global() {
-    __builtin_amdgcn_s_waitcnt(0);
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-}
-
-__device__ __forceinline__ uint64_t load8_bytes(const uint8_t *p) {
-    uint64_t v = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v |= (uint64_t)p[k] << (8 * k);
-    return v;
-}
-
-// XXH64 of out[0, len) by the wave: 16 stripes of 32 bytes loaded per step (lane 4s + k holds word
-// k of stripe s), folded in order by lanes 0-3 (accumulator k), then lane 0 merges and hashes the
-// tail.  Returns the low 32 bits (in every lane).
-__device__ uint32_t wave_xxh64(const uint8_t *p, uint64_t len) {
-    const uint64_t P1 = 11400714785074694791ull, P2 = 14029467366897019727ull, P3 = 1609587929392839161ull,
-                   P4 = 9650029242287828579ull, P5 = 2870177450012600261ull;
-    const uint32_t lane = threadIdx.x & 63, k = lane & 3;
-    uint64_t h = 0;
-    const uint64_t ns = len / 32;
-    if (ns) {
-        uint64_t v = k == 0 ? P1 + P2 : k == 1 ? P2 : k == 2 ? 0 : 0 - P1;
-        for (uint64_t s0 = 0; s0 < ns; s0 += 16) {
-            const uint64_t s = s0 + lane / 4;
-            const uint64_t wd = s < ns ? load8_bytes(p + 32 * s + 8 * k) : 0;
-            const int steps = (int)(ns - s0 < 16 ? ns - s0 : 16);
-            for (int t = 0; t < steps; ++t) {
-                const uint64_t x = __shfl(wd, 4 * t + (int)k, 64);
-                v = tfz::rotl64(v + x * P2, 31) * P1;
-            }
-        }
-        const uint64_t v1 = __shfl(v, 0, 64), v2 = __shfl(v, 1, 64), v3 = __shfl(v, 2, 64), v4 = __shfl(v, 3, 64);
-        h = tfz::rotl64(v1, 1) + tfz::rotl64(v2, 7) + tfz::rotl64(v3, 12) + tfz::rotl64(v4, 18);
-        const uint64_t vs[4] = {v1, v2, v3, v4};
-        for (int q = 0; q < 4; ++q) h = (h ^ (tfz::rotl64(vs[q] * P2, 31) * P1)) * P1 + P4;
-    } else {
-        h = P5;
-    }
-    h += len;
-    const uint8_t *e = p + len, *t = p + 32 * ns; // the tail: lane 0 (<= 31 bytes)
-    if (lane == 0) {
-        while (t + 8 <= e) {
-            h ^= tfz::rotl64(load8_bytes(t) * P2, 31) * P1;
-            h = tfz::rotl64(h, 27) * P1 + P4;
-            t += 8;
-        }
-        if (t + 4 <= e) {
-            h ^= (uint64_t)tfz::rd32(t) * P1;
-            h = tfz::rotl64(h, 23) * P2 + P3;
-            t += 4;
-        }
-        while (t < e) {
-            h ^= (*t) * P5;
-            h = tfz::rotl64(h, 11) * P1;
-            ++t;
-        }
-        h ^= h >> 33;
-        h *= P2;
-        h ^= h >> 29;
-        h *= P3;
-        h ^= h >> 32;
-    }
-    return (uint32_t)__shfl(h, 0, 64);
-}
-
-// Stage 2: one wave per packet frame replays its records through a 64 KB LDS window.  Records go
-// in batches of up to 64 that add at most 32 KB of output: one load of the batch, scans of the
-// lengths, the batch's literal bytes loaded once (coalesced) into LDS, every literal run copied to
-// the window by its own lane, then the matches in order, all lanes copying (a match of offset < 64
-// repeats the `off` bytes before it, byte i from i % off; longer offsets copy from off bytes back,
-// 64 bytes a step), and one flush of the batch to HBM.  A match source older than the window
-// comes from HBM (synced first).  A record of more than 32 KB goes alone, written through.
-__global__ void __launch_bounds__(64) zstd_exec_kernel(const tfz::ZSeq *seq, const uint64_t *foff, const uint64_t *roff,
-                                                       uint64_t f0, const uint8_t *lits, const uint64_t *counts,
-                                                       uint8_t *dst, unsigned *err) {
-    __shared__ uint8_t win[ZW];
-    __shared__ uint8_t lbuf[ZHALF];
-    const uint64_t b = blockIdx.x, f = f0 + b;
-    const uint32_t lane = threadIdx.x & 63;
-    const tfz::ZSeq *s = seq + (zseq_base(foff, roff, f) - zseq_base(foff, roff, f0));
-    const uint64_t n = counts[2 * b], nlit = counts[2 * b + 1];
-    const uint8_t *lit = lits + (roff[f] - roff[f0]);
-    uint8_t *out = dst + roff[f];
-    const uint64_t raw = roff[f + 1] - roff[f];
-    uint64_t op = 0, lp = 0, fstart = 0, synced = 0;
-    bool bad = false;
-    // the next batch is loaded while the current one is replayed: its 64 records and the first
-    // 1 KB of its literals (16 bytes a lane, all in flight together)
-    auto load_rec = [&](uint64_t q) -> tfz::ZSeq {
-        tfz::ZSeq r{0, 0, 0, 0};
-        if (q + lane < n) r = s[q + lane];
-        return r;
-    };
-    auto load_lits = [&](uint64_t at, uint8_t (&v)[16]) {
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const uint64_t i = at + lane * 16 + k;
-            v[k] = i < nlit ? lit[i] : 0;
-        }
-    };
-    uint64_t q = 0;
-    tfz::ZSeq rec = load_rec(0);
-    uint8_t pl[16];
-    load_lits(0, pl);
-    while (q < n && !bad) {
-        const tfz::ZSeq r = rec;
-        const bool valid = q + lane < n;
-        const uint64_t mk = __ballot(valid && r.tag != tfz::ZS_SEQ);
-        if (mk & 1ull) { // a marker first: on its own
-            const uint32_t tag = __builtin_amdgcn_readfirstlane(r.tag), val = __builtin_amdgcn_readfirstlane(r.off);
-            if (tag == tfz::ZS_START) {
-                fstart = op;
-            } else if (tag == tfz::ZS_CHECK) {
-                zsync_global();
-                synced = op;
-                if (wave_xxh64(out + fstart, op - fstart) != val) bad = true;
-            } else {
-                bad = true;
-            }
-            ++q;
-            rec = load_rec(q);
-            continue;
-        }
-        uint64_t lim = mk ? (uint64_t)__builtin_ctzll(mk) : 64;
-        if (lim > n - q) lim = n - q;
-        const uint64_t span = lane < lim ? (uint64_t)r.ll + r.ml : 0;
-        uint64_t incl = span, inl = lane < lim ? r.ll : 0;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint64_t y = __shfl_up(incl, d, 64), z = __shfl_up(inl, d, 64);
-            if (lane >= (uint32_t)d) {
-                incl += y;
-                inl += z;
-            }
-        }
-        const uint32_t cnt = (uint32_t)__popcll(__ballot(lane < lim && incl <= (uint64_t)ZHALF));
-        if (cnt == 0) { // one record of more than ZHALF bytes: written through to HBM as well
-            const uint64_t ll = rl32(r.ll, 0), ml = rl32(r.ml, 0), off = rl32(r.off, 0);
-            if (op + ll + ml > raw || lp + ll > nlit || (ml && (off == 0 || off > op + ll - fstart))) {
-                bad = true;
-                break;
-            }
-            for (uint64_t i0 = lane * 16; i0 < ll; i0 += 64 * 16) {
-                uint8_t v[16];
-#pragma unroll
-                for (int k = 0; k < 16; ++k) v[k] = i0 + k < ll ? lit[lp + i0 + k] : 0;
-#pragma unroll
-                for (int k = 0; k < 16; ++k)
-                    if (i0 + k < ll) {
-                        win[(op + i0 + k) & ZWM] = v[k];
-                        out[op + i0 + k] = v[k];
-                    }
-            }
-            lds_order();
-            const uint64_t d = op + ll;
-            for (uint64_t base = 0; base < ml; base += 64) {
-                const uint64_t i = base + lane;
-                const bool near = off + 64 <= (uint64_t)ZW;
-                if (!near && d + base - off + 64 > synced) { // HBM sources written by this wave: sync
-                    zsync_global();
-                    synced = d + base;
-                }
-                if (i < ml) {
-                    const uint64_t sp = off < 64 ? d - off + (uint32_t)i % (uint32_t)off : d + i - off;
-                    const uint8_t v = near ? win[sp & ZWM] : out[sp];
-                    win[(d + i) & ZWM] = v;
-                    out[d + i] = v;
-                }
-                lds_order();
-            }
-            op += ll + ml;
-            lp += ll;
-            ++q;
-            rec = load_rec(q);
-            load_lits(lp, pl);
-            continue;
-        }
-        const uint64_t total_span = rl64(incl, cnt - 1), total_ll = rl64(inl, cnt - 1);
-        if (op + total_span > raw || lp + total_ll > nlit) {
-            bad = true;
-            break;
-        }
-        // the next batch's loads go out now and land while this one is replayed
-        rec = load_rec(q + cnt);
-        uint8_t npl[16];
-        load_lits(lp + total_ll, npl);
-        // this batch's literals into LDS: the prefetched first KB, the rest (long runs) loaded here
-#pragma unroll
-        for (int k = 0; k < 16; ++k)
-            if (lane * 16 + k < total_ll) lbuf[lane * 16 + k] = pl[k];
-        for (uint64_t i0 = 1024 + lane * 16; i0 < total_ll; i0 += 64 * 16) {
-            uint8_t v[16];
-#pragma unroll
-            for (int k = 0; k < 16; ++k) v[k] = i0 + k < total_ll ? lit[lp + i0 + k] : 0;
-#pragma unroll
-            for (int k = 0; k < 16; ++k)
-                if (i0 + k < total_ll) lbuf[i0 + k] = v[k];
-        }
-        lds_order();
-        const uint64_t ex_span = incl - span, ex_ll = inl - (lane < lim ? r.ll : 0);
-        if (lane < cnt) // literal runs, one lane each
-            for (uint32_t t = 0; t < r.ll; ++t) win[(op + ex_span + t) & ZWM] = lbuf[ex_ll + t];
-        lds_order();
-        const uint64_t bop = op; // window-resident: positions >= bop - ZHALF
-        for (uint32_t j = 0; j < cnt; ++j) { // matches in order
-            const uint32_t ml = rl32(r.ml, j);
-            if (!ml) continue;
-            const uint32_t off = rl32(r.off, j);
-            const uint64_t d = op + rl64(ex_span, j) + rl32(r.ll, j);
-            if (off == 0 || off > d - fstart) {
-                bad = true;
-                break;
-            }
-            const bool near = d - off + ZHALF >= bop;
-            if (!near && synced < bop) { // older than the window: from HBM, flushed by earlier batches
-                zsync_global();
-                synced = bop;
-            }
-            for (uint32_t base = 0; base < ml; base += 64) {
-                const uint32_t i = base + lane;
-                if (i < ml) {
-                    const uint64_t sp = off < 64 ? d - off + i % off : d + i - off;
-                    win[(d + i) & ZWM] = (near || sp >= bop) ? win[sp & ZWM] : out[sp];
-                }
-                lds_order();
-            }
-        }
-        for (uint64_t i = lane; i < total_span; i += 64) out[op + i] = win[(op + i) & ZWM]; // flush
-        op += total_span;
-        lp += total_ll;
-        q += cnt;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) pl[k] = npl[k];
-    }
-    if (lane == 0 && (bad || op != raw || lp != nlit)) atomicOr(err, 1u);
-}
-
 int read_method(Ctx *ctx, const uint8_t *packet, uint8_t *m) {
     TFG_HIP(hipMemcpyAsync(ctx->host_pinned, packet, 1, hipMemcpyDeviceToHost, ctx->stream));
     TFG_HIP(hipStreamSynchronize(ctx->stream));
@@ -683,49 +402,15 @@ int tfg_codec_decompress(tfg_ctx *ctx, const uint8_t *packet, size_t bytes, uint
     unsigned *err = (unsigned *)ctx->dev_counter;
     TFG_HIP(hipMemsetAsync(err, 0, sizeof(unsigned), ctx->stream));
     if (res[0] && m == ZSTD_METHOD) {
-        // two stages per group of frames whose records + literals fit ZSTD_SCRATCH (frame tables
-        // read back once); the stages' buffers come from the stream-ordered pool and are released
-        // on every return path
+        // zstd.hip: scan, per-block entropy, resolve, parallel execution (frame tables read once)
         const uint64_t nf = res[0];
         std::vector<uint64_t> fo(nf + 1), ro(nf + 1);
         TFG_HIP(hipMemcpyAsync(fo.data(), sb + o_foff, (nf + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
         TFG_HIP(hipMemcpyAsync(ro.data(), sb + o_roff, (nf + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
         TFG_HIP(hipStreamSynchronize(ctx->stream));
-        const uint64_t *dfo = (const uint64_t *)(sb + o_foff), *dro = (const uint64_t *)(sb + o_roff);
-        auto need = [&](uint64_t a, uint64_t z) { // bytes of records + literals + counts of frames [a, z)
-            return (zseq_base(fo.data(), ro.data(), z) - zseq_base(fo.data(), ro.data(), a)) * sizeof(tfz::ZSeq) +
-                   (ro[z] - ro[a]) + 16 * (z - a) + 256;
-        };
-        struct PoolBuf { // hipMallocAsync'd, hipFreeAsync'd on every exit
-            hipStream_t st;
-            void *p = nullptr;
-            ~PoolBuf() { if (p) (void)hipFreeAsync(p, st); }
-        } buf{ctx->stream};
-        uint64_t cap = 0;
-        for (uint64_t a = 0; a < nf;) {
-            uint64_t z = a + 1;
-            while (z < nf && need(a, z + 1) <= ZSTD_SCRATCH) ++z;
-            const uint64_t bytes = need(a, z);
-            if (bytes > cap) {
-                if (buf.p) TFG_HIP(hipFreeAsync(buf.p, ctx->stream));
-                buf.p = nullptr;
-                TFG_HIP(hipMallocAsync(&buf.p, bytes, ctx->stream));
-                cap = bytes;
-            }
-            const uint64_t nrec = zseq_base(fo.data(), ro.data(), z) - zseq_base(fo.data(), ro.data(), a);
-            tfz::ZSeq *seq = (tfz::ZSeq *)buf.p;
-            uint64_t *counts = (uint64_t *)((char *)buf.p + nrec * sizeof(tfz::ZSeq));
-            uint8_t *lits = (uint8_t *)(counts + 2 * (z - a));
-            ProfScope _ps(ctx, "codec.zstd.decompress");
-            hipLaunchKernelGGL(zstd_entropy_kernel, dim3((unsigned)(z - a)), dim3(64), 0, ctx->stream, packet, dfo, dro, a,
-                               seq, lits, counts, err);
-            TFG_LAUNCH_CHECK();
-            hipLaunchKernelGGL(zstd_exec_kernel, dim3((unsigned)(z - a)), dim3(64), 0, ctx->stream,
-                               (const tfz::ZSeq *)seq, dfo, dro, a, (const uint8_t *)lits, (const uint64_t *)counts, out + 1,
-                               err);
-            TFG_LAUNCH_CHECK();
-            a = z;
-        }
+        if (int rc = zstd_decode_frames(ctx, packet, nf, (const uint64_t *)(sb + o_foff), (const uint64_t *)(sb + o_roff),
+                                        fo.data(), ro.data(), out + 1, err))
+            return rc;
         TFG_HIP(hipMemcpyAsync(ctx->host_pinned, err, sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
         TFG_HIP(hipStreamSynchronize(ctx->stream));
     } else if (res[0]) {

@@ -7,22 +7,26 @@
 // format: frame header, raw / RLE / compressed blocks, Huffman-coded literals (1 or 4 streams,
 // FSE-compressed or direct weights, treeless reuse), FSE-coded sequences (predefined, RLE,
 // compressed and repeat modes) with the three repeat offsets, and the XXH64 content checksum.
-// No dictionaries.  Every read is bounds-checked: a malformed frame returns an error, never
-// writes outside its buffers.
+// No dictionaries.  Every read is bounds-checked: a malformed frame is an error, never a write
+// outside the caller's buffers.
 //
-// Decoding is split in two stages, so that neither waits on the other's memory:
-//   1. entropy (zstd_frame_entropy): block headers, Huffman literals and FSE sequences are decoded
-//      into a flat list of ZSeq records {literal length, match length, resolved offset} and the
-//      literal bytes, in output order.  Raw blocks become literal runs, RLE blocks one literal and
-//      an offset-1 match; frame starts and content checksums become marker records.
-//   2. execution: the records are replayed into the output (literal runs, then LZ77 matches).
-// On the device (lz4.hip) stage 1 is one wave per packet frame with the compressed block staged in
-// LDS (the wave decodes the sequences in lockstep; the four Huffman streams of a block go to four
-// lanes) and stage 2 a second kernel, one wave per frame, whose output passes through a 64 KB LDS
-// window: literal runs are copied by all lanes at once, matches are replayed one after another
-// with all lanes copying, and the window is flushed to HBM once per batch of records.  The same
-// stage-1 source runs on the host with zstd_exec_serial as stage 2 (zstd_frame): the CPU check of
-// the decoder against the system libzstd (tests/test_zstd.py).
+// The decode is split so that the serial parts are short and the byte work is parallel:
+//   1. scan (zstd_scan, one thread per packet frame): frame and block headers, the literal-section
+//      and sequence-section headers and the table descriptions' extents — no entropy decoding.
+//      Emits one ZBlockDesc per block (where its literals / sequences start, which Huffman and
+//      FSE table descriptions are in force — treeless / repeat modes point at an earlier block's)
+//      and one ZFrameDesc per ZSTD frame; a first pass only counts, so the outputs are sized
+//      exactly.  Every block's literals and records then have fixed slots.
+//   2. entropy (per block, independently): tables from the descriptions, Huffman literals,
+//      FSE sequences -> records {literal length, match length, offset code} (repeat codes
+//      unresolved: they depend on earlier blocks).  Every block ends with a literal-run record.
+//   3. resolve (one wave per packet frame): repeat offsets in order, each record's output and
+//      literal positions (wave scans), and the checks (offsets inside their frame, sizes).
+//   4. execution: every output byte at once — literal bytes copied, a match byte points at its
+//      source byte; pointer jumping (src = src[src]) until every byte points at a literal; one
+//      gather.  Matches that copy matches (chains) resolve in log2(chain) rounds.
+// The device runs 2-4 as kernels (zstd.hip); zstd_frame below runs 1-3 on the host plus a serial
+// replay: the CPU check of the decoder's source against the system libzstd (tests/test_zstd.py).
 #pragma once
 #include <stdint.h>
 
@@ -31,22 +35,13 @@
 #else
 #define ZHD inline
 #endif
-// Stage 1 on the device: all 64 lanes of a wave run the entropy decoding in lockstep (identical
-// loads and branches in every lane) and split the stores: record q is stored by lane q % 64,
-// literal bytes by lanes in turn, the four Huffman streams by lanes 0-3.  ZANY combines a per-lane
-// condition over the wave (the Huffman stream checks).
-#if defined(__HIP_DEVICE_COMPILE__)
-#define ZSYNC_LDS() __syncthreads()
-#define ZANY(x) (__ballot((int)(x)) != 0)
-#else
-#define ZSYNC_LDS() do { } while (0)
-#define ZANY(x) (x)
-#endif
 
 namespace tfz {
 
 constexpr int ZMAX_BLOCK = 128 * 1024;
 constexpr int ZHUF_MAXBITS = 11;
+constexpr uint32_t ZNONE = 0xFFFFFFFFu;
+constexpr uint32_t ZDIRECT = 0x80000000u; // ZRec::of flag: a literal run / RLE copy, not a sequence
 
 struct FseEntry {
     uint16_t base; // newState base
@@ -65,31 +60,55 @@ struct ZSeqEntry {
     uint8_t add;    // additional bits of the value
 };
 
-struct ZWork {
+// The tables of one block (LDS on the device, ~14 KB)
+struct ZTables {
     ZSeqEntry ll[512], of[256], ml[512]; // accuracy logs <= 9 / 8 / 9
     int ll_log, of_log, ml_log;
-    bool ll_ok, of_ok, ml_ok;             // a table exists for Repeat mode
-    uint16_t huf[1 << ZHUF_MAXBITS];      // symbol | nbBits << 8
-    int huf_bits;                         // 0: no table yet (Treeless needs one)
-    uint8_t *stage;                       // device: an LDS copy of the current compressed block (null: none)
+    uint16_t huf[1 << ZHUF_MAXBITS];     // symbol | nbBits << 8
+    int huf_bits;
 };
-// (the tables, ~10 KB, live in LDS on the device)
 
-// One replay record of stage 1.  tag ZS_SEQ: ll literal bytes (the next ones of the literal
-// stream), then ml bytes copied from `off` bytes back; ZS_START: a ZSTD frame begins (offsets may
-// not reach before it); ZS_CHECK: the frame ends with content checksum `off` (XXH64 low 32 bits).
-struct ZSeq {
-    uint32_t ll, ml, off, tag;
+// One block (scan output).  Offsets are into the packet frame's ZSTD body.
+struct ZBlockDesc {
+    uint32_t src, size; // block content
+    uint8_t type;       // 0 raw, 1 RLE, 2 compressed
+    uint8_t ltype;      // literals: 0 raw, 1 RLE, 2 compressed, 3 treeless
+    uint8_t streams;    // Huffman streams (1 / 4)
+    uint8_t pad;
+    uint32_t lit_at;    // literal section payload: raw / RLE bytes, or the Huffman streams
+    uint32_t lsize;     // regenerated literal bytes (raw block: size, RLE block: 1)
+    uint32_t lbytes;    // compressed literal bytes (streams incl. the jump table)
+    uint32_t huf;       // Huffman tree description in force (ltype 2 / 3), its extent huf_n
+    uint32_t huf_n;
+    uint32_t tab[3];    // LL / OF / ML: mode << 30 | offset of the description (mode 2) / byte (mode 1)
+    uint32_t tab_n[3];  // description extents (mode 2)
+    uint32_t seq_at, seq_n; // sequence bitstream
+    uint32_t nseq;
+    uint32_t pframe;    // packet frame (launch-relative)
+    uint32_t rec, lit;  // launch-relative index of the block's first record / literal byte
 };
-constexpr uint32_t ZS_SEQ = 0, ZS_START = 1, ZS_CHECK = 2;
 
-// Stage-1 outputs of one packet frame (caller-sized: at most raw/3 + blocks + 2 * zstd frames
-// records, at most raw literal bytes)
-struct ZOut {
-    ZSeq *seq;
-    uint64_t seq_cap, nseq;
-    uint8_t *lit;
-    uint64_t lit_cap, nlit;
+// One ZSTD frame (scan output; resolve fills out0 / out1, frame-relative output positions)
+struct ZFrameDesc {
+    uint32_t rec0, rec1;   // its records, launch-relative
+    uint64_t fcs;          // content size, ~0 = absent
+    uint32_t checksum, has_checksum;
+    uint32_t out0, out1;
+    uint32_t pframe, pad;
+};
+
+// A record.  Stage 2 writes {ll, ml, of, 0}: of = the sequence's offset value (RFC "Offset_Value":
+// 1-3 repeat codes, offset + 3 otherwise), or ZDIRECT | offset for a literal run / RLE copy.
+// Resolve rewrites it in place as {pos, ll, lpos, off}: output position (packet-frame-relative),
+// literal run length, literal position (launch-relative) and the resolved offset; the record's
+// end is the next record's pos.
+struct ZRec {
+    uint32_t a, b, c, d;
+};
+
+// counts of one packet frame (scan pass 1)
+struct ZCounts {
+    uint32_t blocks, frames, recs, max_comp;
 };
 
 // ---------------------------------------------------------------- constants (RFC 8878 §3.1.1.3.2.2)
@@ -154,50 +173,62 @@ struct FwdBits {
     ZHD void skip(int n) { pos += n; }
 };
 
-// backward (Huffman streams, FSE bitstreams): the stream's last byte holds a 1 marker above the
-// padding; bits are read from the top down.  Reading past the start yields zeros and makes
-// `pos` negative (the overflow the decoders check).  A 64-bit window of the stream (bytes
-// [wb, wb + 8)) is kept in registers and refilled only when a read leaves it.
-struct BackBits {
+// backward bitstream (Huffman streams, FSE bitstreams): the stream's last byte holds a 1 marker
+// above the padding; bits are read from the top down.  `pos` = bits still unread; a 64-bit window
+// of stream bits [wlo, wlo + 64) (wlo a multiple of 8) is refilled when a read would leave it:
+// after a refill at least 57 bits can be read.  Bytes outside the stream read as zeros (a read
+// past the start makes pos negative: the overflow the decoders check).  ALIGNED: the stream lives
+// in a buffer that may be read in aligned 8-byte words up to 15 bytes past its end (the LDS stage).
+ZHD uint64_t zload64(const uint8_t *p, int64_t off, int64_t n) {
+    uint64_t v = 0;
+    for (int k = 0; k < 8; ++k)
+        if (off + k >= 0 && off + k < n) v |= (uint64_t)p[off + k] << (8 * k);
+    return v;
+}
+template <bool ALIGNED = false> struct BitR {
     const uint8_t *p;
-    int64_t nbytes;
-    int64_t pos; // bits still unread (from bit 0 of p[0] up)
+    int64_t n;
+    int64_t pos;
+    int64_t wlo;
     uint64_t win;
-    int64_t wb;  // first byte of the window (-1: none)
-    ZHD bool init(const uint8_t *buf, int64_t n) {
+    ZHD bool init(const uint8_t *buf, int64_t len) {
         p = buf;
-        nbytes = n;
-        wb = -1;
-        win = 0;
-        if (n <= 0) return false;
-        const uint8_t last = buf[n - 1];
+        n = len;
+        if (len <= 0) return false;
+        const uint8_t last = buf[len - 1];
         if (!last) return false;
-        pos = (n - 1) * 8 + highbit(last);
+        int hb = 0;
+        for (uint32_t v = last; v >>= 1;) ++hb;
+        pos = (len - 1) * 8 + hb;
+        refill();
         return true;
     }
-    // bits [lo, lo + n) of the stream (n <= 56, lo >= 0)
-    ZHD uint64_t bits_at(int64_t lo, int n) {
-        const int64_t b0 = lo >> 3, b1 = (lo + n - 1) >> 3;
-        if (wb < 0 || b0 < wb || b1 >= wb + 8) { // refill: the window ends at the read's last byte
-            int64_t nb = b1 - 7;
-            if (nb < 0) nb = 0;
-            win = 0;
-            for (int k = 0; k < 8; ++k)
-                if (nb + k < nbytes) win |= (uint64_t)p[nb + k] << (8 * k);
-            wb = nb;
+    ZHD void refill() { // the window ends at the byte holding bit pos - 1
+        const int64_t b0 = ((pos + 7) >> 3) - 8;
+        wlo = b0 * 8;
+#if defined(__HIP_DEVICE_COMPILE__)
+        if (ALIGNED && b0 >= 0 && b0 + 8 <= n) {
+            const uintptr_t a = (uintptr_t)(p + b0);
+            const uint64_t *w = (const uint64_t *)(a & ~(uintptr_t)7);
+            const uint32_t sh = (uint32_t)(a & 7) * 8;
+            const uint64_t lo = w[0], hi = w[1];
+            win = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+            return;
         }
-        return (win >> (lo - wb * 8)) & ((1ull << n) - 1);
+#endif
+        win = zload64(p, b0, n);
     }
-    ZHD uint64_t peek(int n) { // n <= 56; bits below the stream's start read as zeros
-        if (n == 0) return 0;
-        const int64_t lo = pos - n;
-        if (lo >= 0) return bits_at(lo, n);
-        if (pos <= 0) return 0;
-        return bits_at(0, (int)pos) << (-lo);
+    ZHD void need(int k) { // the next k bits (k <= 57) are in the window
+        if (pos - k < wlo) refill();
     }
-    ZHD uint64_t read(int n) {
-        const uint64_t v = peek(n);
-        pos -= n;
+    ZHD uint64_t peek(int k) const { // k <= 57, after need(k)
+        if (k == 0) return 0;
+        return (win >> (pos - k - wlo)) & ((1ull << k) - 1);
+    }
+    ZHD uint64_t read(int k) {
+        need(k);
+        const uint64_t v = peek(k);
+        pos -= k;
         return v;
     }
 };
@@ -293,8 +324,9 @@ template <typename E> ZHD void fse_rle(E *t, int sym) {
 }
 
 // ---------------------------------------------------------------- Huffman
-// Huffman tree description -> w->huf; returns bytes used or -1
-ZHD int64_t huf_read(const uint8_t *src, int64_t n, ZWork *w) {
+// Huffman tree description (RFC 8878 §4.2.1) -> t.huf; returns bytes used or -1.  Every caller
+// lane parses; the table fill is split over lanes (lane, lane + nl, ...).
+ZHD int64_t huf_read(const uint8_t *src, int64_t n, ZTables &t, uint32_t lane = 0, uint32_t nl = 1) {
     if (n < 1) return -1;
     uint8_t weight[256];
     int nw = 0;
@@ -315,23 +347,23 @@ ZHD int64_t huf_read(const uint8_t *src, int64_t n, ZWork *w) {
         int log, nsym;
         const int64_t hd = fse_read_ncount(src + 1, hb, 6, 15, norm, log, nsym);
         if (hd < 0 || hd >= hb) return -1;
-        FseEntry t[64];
-        if (!fse_build(t, norm, nsym, log)) return -1;
-        BackBits bb;
+        FseEntry ft[64];
+        if (!fse_build(ft, norm, nsym, log)) return -1;
+        BitR<> bb;
         if (!bb.init(src + 1 + hd, hb - hd)) return -1;
         uint32_t s1 = (uint32_t)bb.read(log), s2 = (uint32_t)bb.read(log);
         for (;;) {
             if (nw > 253) return -1;
-            weight[nw++] = t[s1].sym;
-            s1 = t[s1].base + (uint32_t)bb.read(t[s1].bits);
+            weight[nw++] = ft[s1].sym;
+            s1 = ft[s1].base + (uint32_t)bb.read(ft[s1].bits);
             if (bb.pos < 0) {
-                weight[nw++] = t[s2].sym;
+                weight[nw++] = ft[s2].sym;
                 break;
             }
-            weight[nw++] = t[s2].sym;
-            s2 = t[s2].base + (uint32_t)bb.read(t[s2].bits);
+            weight[nw++] = ft[s2].sym;
+            s2 = ft[s2].base + (uint32_t)bb.read(ft[s2].bits);
             if (bb.pos < 0) {
-                weight[nw++] = t[s1].sym;
+                weight[nw++] = ft[s1].sym;
                 break;
             }
         }
@@ -363,25 +395,50 @@ ZHD int64_t huf_read(const uint8_t *src, int64_t n, ZWork *w) {
         if (!wt) continue;
         const uint32_t len = 1u << (wt - 1);
         const uint16_t e = (uint16_t)(i | ((maxbits + 1 - wt) << 8));
-        for (uint32_t k = 0; k < len; ++k) w->huf[start[wt] + k] = e;
+        for (uint32_t k = lane; k < len; k += nl) t.huf[start[wt] + k] = e;
         start[wt] += len;
     }
-    w->huf_bits = maxbits;
+    t.huf_bits = maxbits;
     return used;
 }
 
 // one Huffman stream of `count` literals into out
-ZHD bool huf_stream(const ZWork *w, const uint8_t *src, int64_t n, uint8_t *out, int64_t count) {
-    BackBits bb;
+template <bool AL = false> ZHD bool huf_stream(const ZTables &t, const uint8_t *src, int64_t n, uint8_t *out, int64_t count) {
+    BitR<AL> bb;
     if (!bb.init(src, n)) return false;
-    const int mb = w->huf_bits;
+    const int mb = t.huf_bits;
     for (int64_t i = 0; i < count; ++i) {
-        const uint16_t e = w->huf[bb.peek(mb)];
+        bb.need(mb);
+        const uint16_t e = t.huf[bb.peek(mb)];
         out[i] = (uint8_t)e;
         bb.pos -= e >> 8;
         if (bb.pos < 0) return false;
     }
     return bb.pos == 0;
+}
+
+// the four streams of a block's literals: extents from the 6-byte jump table; stream k decodes
+// literals [k * seg, ...) of the block (seg = ceil(lsize / 4)); false when the table is invalid
+struct Huf4 {
+    int64_t at[4], len[4], cnt[4], seg;
+};
+ZHD bool huf4_split(const uint8_t *cs, int64_t cn, uint32_t lsize, Huf4 &h) {
+    if (cn < 6) return false;
+    const int64_t s1 = cs[0] | (cs[1] << 8), s2 = cs[2] | (cs[3] << 8), s3 = cs[4] | (cs[5] << 8);
+    const int64_t s4 = cn - 6 - s1 - s2 - s3;
+    if (s4 < 1) return false;
+    h.seg = (lsize + 3) / 4;
+    if (3 * h.seg > (int64_t)lsize) return false;
+    h.at[0] = 6;
+    h.at[1] = 6 + s1;
+    h.at[2] = 6 + s1 + s2;
+    h.at[3] = 6 + s1 + s2 + s3;
+    h.len[0] = s1;
+    h.len[1] = s2;
+    h.len[2] = s3;
+    h.len[3] = s4;
+    for (int k = 0; k < 4; ++k) h.cnt[k] = k < 3 ? h.seg : (int64_t)lsize - 3 * h.seg;
+    return true;
 }
 
 // ---------------------------------------------------------------- XXH64 (content checksum)
@@ -440,10 +497,13 @@ ZHD uint64_t xxh64(const uint8_t *p, uint64_t len) {
     return h;
 }
 
+// ---------------------------------------------------------------- sequence tables
 // symbol -> baseline and additional bits for every entry of a sequence table of `size` entries
-// (kind 0 literal lengths, 1 offsets, 2 match lengths); false on a symbol past the kind's range
+// (kind 0 literal lengths, 1 offsets, 2 match lengths); false on a symbol past the kind's range.
+// Offset codes stop at 30: a larger offset cannot fall inside a packet frame (<= 1 GB), and the
+// record's offset field keeps its top bit for ZDIRECT.
 ZHD bool seq_finish(ZSeqEntry *t, int size, int kind) {
-    const int max_sym = kind == 0 ? 35 : kind == 1 ? 31 : 52;
+    const int max_sym = kind == 0 ? 35 : kind == 1 ? 30 : 52;
     for (int u = 0; u < size; ++u) {
         const int c = t[u].sym;
         if (c > max_sym) return false;
@@ -453,359 +513,403 @@ ZHD bool seq_finish(ZSeqEntry *t, int size, int kind) {
     return true;
 }
 
-// ---------------------------------------------------------------- stage 1: blocks -> records
-// a sequence-table description of one kind (mode from the compression-modes byte)
-ZHD int64_t seq_table(const uint8_t *src, int64_t n, int mode, int kind, ZWork *w) {
-    ZSeqEntry *t = kind == 0 ? w->ll : kind == 1 ? w->of : w->ml;
-    int &log = kind == 0 ? w->ll_log : kind == 1 ? w->of_log : w->ml_log;
-    bool &ok = kind == 0 ? w->ll_ok : kind == 1 ? w->of_ok : w->ml_ok;
+// the table of one kind from its description (ZBlockDesc::tab: mode << 30 | offset into `body`)
+ZHD bool seq_table_build(ZTables &t, int kind, uint32_t tab, uint32_t tab_n, const uint8_t *body) {
+    ZSeqEntry *e = kind == 0 ? t.ll : kind == 1 ? t.of : t.ml;
+    int &log = kind == 0 ? t.ll_log : kind == 1 ? t.of_log : t.ml_log;
+    const int mode = (int)(tab >> 30);
+    const uint32_t at = tab & 0x3FFFFFFFu;
     const int max_sym = kind == 0 ? 35 : kind == 1 ? 31 : 52, max_log = kind == 1 ? 8 : 9;
     if (mode == 0) { // predefined
         int16_t norm[53];
         const int nsym = kind == 0 ? 36 : kind == 1 ? 29 : 53;
         for (int s = 0; s < nsym; ++s) norm[s] = kind == 0 ? ll_default(s) : kind == 1 ? of_default(s) : ml_default(s);
         log = kind == 1 ? 5 : 6;
-        ok = fse_build(t, norm, nsym, log) && seq_finish(t, 1 << log, kind);
-        return ok ? 0 : -1;
+        return fse_build(e, norm, nsym, log) && seq_finish(e, 1 << log, kind);
     }
     if (mode == 1) { // RLE
-        if (n < 1 || src[0] > max_sym) return -1;
-        fse_rle(t, src[0]);
+        fse_rle(e, body[at]);
         log = 0;
-        ok = seq_finish(t, 1, kind);
-        return ok ? 1 : -1;
+        return seq_finish(e, 1, kind);
     }
-    if (mode == 2) {
-        int16_t norm[53];
-        int nsym;
-        const int64_t used = fse_read_ncount(src, n, max_log, max_sym, norm, log, nsym);
-        if (used < 0) return -1;
-        ok = fse_build(t, norm, nsym, log) && seq_finish(t, 1 << log, kind);
-        return ok ? used : -1;
-    }
-    return ok ? 0 : -1; // repeat: the previous block's table
+    int16_t norm[53];
+    int nsym;
+    if (fse_read_ncount(body + at, tab_n, max_log, max_sym, norm, log, nsym) < 0) return false;
+    return fse_build(e, norm, nsym, log) && seq_finish(e, 1 << log, kind);
 }
 
-// appends record r (stored by lane nseq % nl; every lane counts)
-ZHD bool put_seq(ZOut &o, const ZSeq &r, uint32_t lane, uint32_t nl) {
-    if (o.nseq >= o.seq_cap) return false;
-    if (o.nseq % nl == lane) o.seq[o.nseq] = r;
-    ++o.nseq;
-    return true;
-}
-
-// One compressed block: its literals appended to o.lit, its sequences (repeat offsets resolved)
-// appended as records.  op = the packet frame's output so far, fstart = where the current ZSTD
-// frame's output began (offsets reach back into this frame only), cap = the output capacity.
-ZHD bool zblock_entropy(const uint8_t *src, int64_t n, uint64_t &op, uint64_t fstart, uint64_t cap, uint32_t (&rep)[3],
-                        ZWork *w, ZOut &o, uint32_t lane, uint32_t nl) {
-    // ---- literals section
-    if (n < 1) return false;
-    const int ltype = src[0] & 3, sf = (src[0] >> 2) & 3;
-    int64_t ip = 0;
-    uint32_t lsize = 0, csize = 0;
-    int streams = 1;
-    if (ltype <= 1) {
-        if ((sf & 1) == 0) {
-            lsize = src[0] >> 3;
-            ip = 1;
-        } else if (sf == 1) {
-            if (n < 2) return false;
-            lsize = (src[0] >> 4) | ((uint32_t)src[1] << 4);
-            ip = 2;
-        } else {
-            if (n < 3) return false;
-            lsize = (src[0] >> 4) | ((uint32_t)src[1] << 4) | ((uint32_t)src[2] << 12);
-            ip = 3;
-        }
-        if (lsize > (uint32_t)ZMAX_BLOCK || o.nlit + lsize > o.lit_cap) return false;
-        uint8_t *lit = o.lit + o.nlit;
-        if (ltype == 0) {
-            if (ip + lsize > n) return false;
-            for (uint32_t i = lane; i < lsize; i += nl) lit[i] = src[ip + i];
-            ip += lsize;
-        } else {
-            if (ip + 1 > n) return false;
-            for (uint32_t i = lane; i < lsize; i += nl) lit[i] = src[ip];
-            ip += 1;
-        }
-    } else {
-        const int hl = sf <= 1 ? 3 : sf == 2 ? 4 : 5;
-        if (n < hl) return false;
-        uint64_t v = 0;
-        for (int k = 0; k < hl; ++k) v |= (uint64_t)src[k] << (8 * k);
-        const int bits = sf <= 1 ? 10 : sf == 2 ? 14 : 18;
-        lsize = (uint32_t)((v >> 4) & ((1u << bits) - 1));
-        csize = (uint32_t)((v >> (4 + bits)) & ((1u << bits) - 1));
-        streams = sf == 0 ? 1 : 4;
-        ip = hl;
-        if (lsize > (uint32_t)ZMAX_BLOCK || ip + csize > n || o.nlit + lsize > o.lit_cap) return false;
-        const uint8_t *cs = src + ip;
-        int64_t cn = csize;
-        if (ltype == 2) {
-            const int64_t hu = huf_read(cs, cn, w);
-            if (hu < 0) return false;
-            cs += hu;
-            cn -= hu;
-        } else if (!w->huf_bits) {
-            return false; // treeless without a previous table
-        }
-        uint8_t *lit = o.lit + o.nlit;
-        bool bad = false;
-        if (streams == 1) {
-            if (lane == 0) bad = !huf_stream(w, cs, cn, lit, lsize);
-        } else {
-            if (cn < 6) return false;
-            const int64_t s1 = cs[0] | (cs[1] << 8), s2 = cs[2] | (cs[3] << 8), s3 = cs[4] | (cs[5] << 8);
-            const int64_t s4 = cn - 6 - s1 - s2 - s3;
-            if (s4 < 1) return false;
-            const int64_t seg = (lsize + 3) / 4;
-            if (3 * seg > lsize) return false;
-            const uint8_t *b = cs + 6;
-            // stream k by lane k (every stream by lane 0 when the caller runs one lane)
-            for (uint32_t k = lane; k < 4; k += nl) {
-                const int64_t cnt = k < 3 ? seg : (int64_t)lsize - 3 * seg;
-                const int64_t at = k == 0 ? 0 : k == 1 ? s1 : k == 2 ? s1 + s2 : s1 + s2 + s3;
-                const int64_t len = k == 0 ? s1 : k == 1 ? s2 : k == 2 ? s3 : s4;
-                bad = bad || !huf_stream(w, b + at, len, lit + k * seg, cnt);
-            }
-        }
-        if (ZANY(bad)) return false;
-        ip += csize;
-    }
-    // ---- sequences section
-    if (ip >= n) return false;
-    uint32_t nseq;
-    const int b0 = src[ip];
-    if (b0 == 0) {
-        nseq = 0;
-        ip += 1;
-    } else if (b0 < 128) {
-        nseq = b0;
-        ip += 1;
-    } else if (b0 < 255) {
-        if (ip + 2 > n) return false;
-        nseq = ((uint32_t)(b0 - 128) << 8) + src[ip + 1];
-        ip += 2;
-    } else {
-        if (ip + 3 > n) return false;
-        nseq = src[ip + 1] + ((uint32_t)src[ip + 2] << 8) + 0x7F00;
-        ip += 3;
-    }
+// The sequences of one block: put(q, record) for q = 0 .. nseq (the last: the block's trailing
+// literal run).  false when the bitstream is malformed or a literal length runs past lsize.
+template <bool AL, typename Put>
+ZHD bool seq_decode(const ZTables &t, const uint8_t *bits, int64_t n, uint32_t nseq, uint32_t lsize, Put &&put) {
     uint32_t lit_pos = 0;
-    if (nseq > 0) {
-        if (ip >= n) return false;
-        const int modes = src[ip++];
-        if (modes & 3) return false; // reserved bits
-        const int mll = modes >> 6, mof = (modes >> 4) & 3, mml = (modes >> 2) & 3;
-        int64_t u;
-        if ((u = seq_table(src + ip, n - ip, mll, 0, w)) < 0) return false;
-        ip += u;
-        if ((u = seq_table(src + ip, n - ip, mof, 1, w)) < 0) return false;
-        ip += u;
-        if ((u = seq_table(src + ip, n - ip, mml, 2, w)) < 0) return false;
-        ip += u;
-        BackBits bb;
-        if (!bb.init(src + ip, n - ip)) return false;
-        uint32_t sll = (uint32_t)bb.read(w->ll_log), sof = (uint32_t)bb.read(w->of_log), sml = (uint32_t)bb.read(w->ml_log);
-        uint32_t r0 = rep[0], r1 = rep[1], r2 = rep[2]; // the repeat offsets, in registers
+    if (nseq) {
+        BitR<AL> bb;
+        if (!bb.init(bits, n)) return false;
+        uint32_t sll = (uint32_t)bb.read(t.ll_log), sof = (uint32_t)bb.read(t.of_log), sml = (uint32_t)bb.read(t.ml_log);
         for (uint32_t q = 0; q < nseq; ++q) {
-            // one table read per code (the symbols were checked when the tables were built)
-            const ZSeqEntry el = w->ll[sll], eo = w->of[sof], em = w->ml[sml];
-            const uint64_t ofv = (uint64_t)eo.value + bb.read(eo.add);
-            const uint32_t ml = em.value + (uint32_t)bb.read(em.add);
-            const uint32_t ll = el.value + (uint32_t)bb.read(el.add);
+            const ZSeqEntry el = t.ll[sll], eo = t.of[sof], em = t.ml[sml];
+            const uint32_t ofv = eo.value + (uint32_t)bb.read(eo.add);
+            bb.need(32);
+            const uint32_t ml = em.value + (uint32_t)bb.peek(em.add);
+            bb.pos -= em.add;
+            const uint32_t ll = el.value + (uint32_t)bb.peek(el.add);
+            bb.pos -= el.add;
             if (q + 1 < nseq) { // state updates: LL, ML, OF
-                sll = el.base + (uint32_t)bb.read(el.bits);
-                sml = em.base + (uint32_t)bb.read(em.bits);
-                sof = eo.base + (uint32_t)bb.read(eo.bits);
+                bb.need(26);
+                sll = el.base + (uint32_t)bb.peek(el.bits);
+                bb.pos -= el.bits;
+                sml = em.base + (uint32_t)bb.peek(em.bits);
+                bb.pos -= em.bits;
+                sof = eo.base + (uint32_t)bb.peek(eo.bits);
+                bb.pos -= eo.bits;
             }
-            if (bb.pos < 0) return false;
-            uint64_t off;
-            if (ofv > 3) {
-                off = ofv - 3;
-                r2 = r1;
-                r1 = r0;
-                r0 = (uint32_t)off;
-            } else {
-                const int idx = (int)ofv - 1 + (ll == 0 ? 1 : 0);
-                if (idx == 0) {
-                    off = r0;
-                } else {
-                    const uint32_t t = idx == 3 ? r0 - 1 : idx == 1 ? r1 : r2;
-                    if (idx != 1) r2 = r1;
-                    r1 = r0;
-                    r0 = t;
-                    off = t;
-                }
-            }
-            if (lit_pos + ll > lsize || op + ll + ml > cap || off == 0 || off > op - fstart + ll) return false;
-            if (!put_seq(o, ZSeq{ll, ml, (uint32_t)off, ZS_SEQ}, lane, nl)) return false;
-            op += ll + ml;
+            if (bb.pos < 0 || lit_pos + ll > lsize) return false;
+            put(q, ZRec{ll, ml, ofv, 0});
             lit_pos += ll;
         }
         if (bb.pos != 0) return false;
-        rep[0] = r0;
-        rep[1] = r1;
-        rep[2] = r2;
-    } else if (ip != n) {
-        return false;
     }
-    const uint32_t rest = lsize - lit_pos; // the block's last literals
-    if (rest) {
-        if (op + rest > cap || !put_seq(o, ZSeq{rest, 0, 0, ZS_SEQ}, lane, nl)) return false;
-        op += rest;
-    }
-    o.nlit += lsize;
+    put(nseq, ZRec{lsize - lit_pos, 0, ZDIRECT, 0});
     return true;
 }
 
-// Stage 1 of one packet frame: every ZSTD frame of src[0, n) (skippable frames decode to
-// nothing) into records and literals.  Returns the decoded size, or -1 when the frame is
-// malformed, uses a dictionary, or does not fit `cap` / the ZOut capacities.
-ZHD int64_t zstd_frame_entropy(const uint8_t *src, int64_t n, uint64_t cap, ZWork *w, ZOut &o, uint32_t lane = 0,
-                               uint32_t nl = 1) {
+// ---------------------------------------------------------------- stage 1: scan
+// One packet frame's ZSTD body (n bytes), which decodes to `raw` bytes.  Pass 1 (blocks null)
+// only counts; pass 2 writes the descriptors at the launch-relative bases (by `writer` lanes).
+struct ZScan {
+    ZBlockDesc *blocks = nullptr;
+    ZFrameDesc *frames = nullptr;
+    uint32_t block0 = 0, frame0 = 0, rec0 = 0, lit0 = 0, pframe = 0;
+    bool writer = true;
+    ZCounts c{};
+};
+
+// byte source of the scan: at(off, k) -> k readable bytes at off (k <= ZSCAN_WIN, off + k <= n)
+constexpr int ZSCAN_WIN = 512; // covers a sequence section's header and its three table descriptions
+struct ZSrcMem {
+    const uint8_t *p;
+    ZHD const uint8_t *at(int64_t off, int64_t) const { return p + off; }
+};
+
+template <typename Src> ZHD bool zstd_scan(Src &S, int64_t n, uint64_t raw, ZScan &o) {
+    if (n >= (1ll << 30)) return false; // description offsets keep 30 bits
+    o.c = ZCounts{0, 0, 0, 0};
     int64_t ip = 0;
-    uint64_t op = 0;
+    uint64_t lits = 0;
     while (ip < n) {
-        if (ip + 4 > n) return -1;
-        const uint32_t magic = rd32(src + ip);
+        if (ip + 4 > n) return false;
+        const uint32_t magic = rd32(S.at(ip, 4));
         ip += 4;
         if ((magic & 0xFFFFFFF0u) == 0x184D2A50u) { // skippable
-            if (ip + 4 > n) return -1;
-            const uint32_t sz = rd32(src + ip);
+            if (ip + 4 > n) return false;
+            const uint32_t sz = rd32(S.at(ip, 4));
             ip += 4 + (int64_t)sz;
-            if (ip > n) return -1;
+            if (ip > n) return false;
             continue;
         }
-        if (magic != 0xFD2FB528u) return -1;
-        if (ip >= n) return -1;
-        const int fhd = src[ip++];
+        if (magic != 0xFD2FB528u || ip >= n) return false;
+        const uint8_t *h = S.at(ip, n - ip < 14 ? n - ip : 14); // descriptor .. content size: <= 14 bytes
+        const int64_t h0 = ip;
+        const int fhd = h[0];
+        ++ip;
         const int fcs_flag = fhd >> 6, single = (fhd >> 5) & 1, checksum = (fhd >> 2) & 1, did = fhd & 3;
-        if (fhd & 8) return -1; // reserved bit
-        if (!single) ++ip;      // window descriptor (the output buffer is the whole frame)
+        if (fhd & 8) return false; // reserved bit
+        if (!single) ++ip;         // window descriptor (the output buffer is the whole frame)
         const int did_len = did == 0 ? 0 : did == 1 ? 1 : did == 2 ? 2 : 4;
-        if (ip + did_len > n) return -1;
+        if (ip + did_len > n) return false;
         uint32_t dict = 0;
-        for (int k = 0; k < did_len; ++k) dict |= (uint32_t)src[ip + k] << (8 * k);
-        if (dict) return -1;
+        for (int k = 0; k < did_len; ++k) dict |= (uint32_t)h[ip - h0 + k] << (8 * k);
+        if (dict) return false;
         ip += did_len;
         const int fcs_len = fcs_flag == 0 ? (single ? 1 : 0) : fcs_flag == 1 ? 2 : fcs_flag == 2 ? 4 : 8;
-        if (ip + fcs_len > n) return -1;
+        if (ip + fcs_len > n) return false;
         uint64_t fcs = 0;
-        bool has_fcs = fcs_len > 0;
-        for (int k = 0; k < fcs_len; ++k) fcs |= (uint64_t)src[ip + k] << (8 * k);
+        for (int k = 0; k < fcs_len; ++k) fcs |= (uint64_t)h[ip - h0 + k] << (8 * k);
         if (fcs_len == 2) fcs += 256;
         ip += fcs_len;
-        const uint64_t fstart = op;
-        if (!put_seq(o, ZSeq{0, 0, 0, ZS_START}, lane, nl)) return -1;
-        uint32_t rep[3] = {1, 4, 8};
-        w->ll_ok = w->of_ok = w->ml_ok = false;
-        w->huf_bits = 0;
+        ZFrameDesc fd{};
+        fd.rec0 = o.rec0 + o.c.recs;
+        fd.fcs = fcs_len ? fcs : ~0ull;
+        fd.pframe = o.pframe;
+        uint32_t huf = ZNONE, huf_n = 0, tab[3] = {ZNONE, ZNONE, ZNONE}, tab_n[3] = {0, 0, 0};
         for (;;) {
-            if (ip + 3 > n) return -1;
-            const uint32_t bh = (uint32_t)src[ip] | (uint32_t)src[ip + 1] << 8 | (uint32_t)src[ip + 2] << 16;
+            if (ip + 3 > n) return false;
+            const int64_t hk = n - ip < 8 ? n - ip : 8; // block header + the literals header
+            const uint8_t *bh8 = S.at(ip, hk);
+            const uint32_t bh = (uint32_t)bh8[0] | (uint32_t)bh8[1] << 8 | (uint32_t)bh8[2] << 16;
             ip += 3;
             const int last = bh & 1, btype = (bh >> 1) & 3;
             const uint32_t bsize = bh >> 3;
-            if (btype == 3) return -1;
-            if (btype == 1) { // RLE: one literal byte, then an offset-1 match of bsize - 1
-                if (ip + 1 > n || op + bsize > cap) return -1;
-                if (bsize) {
-                    if (o.nlit + 1 > o.lit_cap) return -1;
-                    if (lane == 0) o.lit[o.nlit] = src[ip];
-                    o.nlit += 1;
-                    if (!put_seq(o, ZSeq{1, bsize - 1, bsize > 1 ? 1u : 0u, ZS_SEQ}, lane, nl)) return -1;
-                    op += bsize;
-                }
+            if (btype == 3 || bsize > (uint32_t)ZMAX_BLOCK) return false;
+            ZBlockDesc d{};
+            d.src = (uint32_t)ip;
+            d.size = bsize;
+            d.type = (uint8_t)(btype == 0 ? 0 : btype == 1 ? 1 : 2);
+            d.pframe = o.pframe;
+            d.rec = o.rec0 + o.c.recs;
+            d.lit = o.lit0 + (uint32_t)lits;
+            uint32_t nrec = 1;
+            if (btype == 0) {
+                if (ip + bsize > n) return false;
+                d.lsize = bsize;
+                ip += bsize;
+            } else if (btype == 1) {
+                if (ip + 1 > n) return false;
+                d.lsize = bsize ? 1 : 0;
                 ip += 1;
             } else {
-                if (ip + bsize > n) return -1;
-                if (btype == 0) { // raw: a literal run
-                    if (op + bsize > cap || o.nlit + bsize > o.lit_cap) return -1;
-                    for (uint32_t i = lane; i < bsize; i += nl) o.lit[o.nlit + i] = src[ip + i];
-                    o.nlit += bsize;
-                    if (bsize && !put_seq(o, ZSeq{bsize, 0, 0, ZS_SEQ}, lane, nl)) return -1;
-                    op += bsize;
-                } else {
-                    if (bsize > (uint32_t)ZMAX_BLOCK) return -1;
-                    const uint8_t *bsrc = src + ip;
-                    if (w->stage) { // the block's bytes into LDS: every bit read then costs an LDS load
-                        ZSYNC_LDS();
-                        for (uint32_t i0 = lane * 16; i0 < bsize; i0 += nl * 16) { // 16 loads in flight a lane
-                            uint8_t v[16];
-#pragma unroll
-                            for (int k = 0; k < 16; ++k) v[k] = i0 + k < bsize ? bsrc[i0 + k] : 0;
-#pragma unroll
-                            for (int k = 0; k < 16; ++k)
-                                if (i0 + k < bsize) w->stage[i0 + k] = v[k];
-                        }
-                        ZSYNC_LDS();
-                        bsrc = w->stage;
+                if (ip + bsize > n || bsize < 1) return false;
+                const int64_t bn = bsize;
+                const uint8_t *b = bh8 + 3; // the literals header (bytes past the block read as 0)
+                uint8_t lh[5];
+                for (int k = 0; k < 5; ++k) lh[k] = 3 + k < hk && k < bn ? b[k] : 0;
+                // literals section header
+                const int ltype = lh[0] & 3, sf = (lh[0] >> 2) & 3;
+                int64_t lp = 0;
+                uint32_t lsize = 0, csize = 0;
+                int streams = 1;
+                if (ltype <= 1) {
+                    if ((sf & 1) == 0) {
+                        lsize = lh[0] >> 3;
+                        lp = 1;
+                    } else if (sf == 1) {
+                        if (bn < 2) return false;
+                        lsize = (lh[0] >> 4) | ((uint32_t)lh[1] << 4);
+                        lp = 2;
+                    } else {
+                        if (bn < 3) return false;
+                        lsize = (lh[0] >> 4) | ((uint32_t)lh[1] << 4) | ((uint32_t)lh[2] << 12);
+                        lp = 3;
                     }
-                    if (!zblock_entropy(bsrc, bsize, op, fstart, cap, rep, w, o, lane, nl)) return -1;
+                    csize = ltype == 0 ? lsize : 1;
+                } else {
+                    const int hl = sf <= 1 ? 3 : sf == 2 ? 4 : 5;
+                    if (bn < hl) return false;
+                    uint64_t v = 0;
+                    for (int k = 0; k < hl; ++k) v |= (uint64_t)lh[k] << (8 * k);
+                    const int bits = sf <= 1 ? 10 : sf == 2 ? 14 : 18;
+                    lsize = (uint32_t)((v >> 4) & ((1u << bits) - 1));
+                    csize = (uint32_t)((v >> (4 + bits)) & ((1u << bits) - 1));
+                    streams = sf == 0 ? 1 : 4;
+                    lp = hl;
                 }
+                if (lsize > (uint32_t)ZMAX_BLOCK || lp + csize > bn) return false;
+                d.ltype = (uint8_t)ltype;
+                d.streams = (uint8_t)streams;
+                d.lsize = lsize;
+                d.lit_at = (uint32_t)(ip + lp);
+                d.lbytes = csize;
+                if (ltype == 2) { // the tree description, then the streams
+                    if (csize < 1) return false;
+                    const int hb = S.at(ip + lp, 1)[0];
+                    const int64_t tl = hb >= 128 ? 1 + (hb - 127 + 1) / 2 : 1 + hb;
+                    if (tl >= (int64_t)csize) return false;
+                    huf = d.lit_at;
+                    huf_n = (uint32_t)tl;
+                    d.lit_at += (uint32_t)tl;
+                    d.lbytes -= (uint32_t)tl;
+                } else if (ltype == 3 && huf == ZNONE) {
+                    return false; // treeless without a previous table
+                }
+                d.huf = ltype >= 2 ? huf : ZNONE;
+                d.huf_n = ltype >= 2 ? huf_n : 0;
+                // sequences section header and table descriptions (within ZSCAN_WIN bytes)
+                int64_t sp = lp + csize;
+                if (sp >= bn) return false;
+                const int64_t sw = bn - sp < ZSCAN_WIN ? bn - sp : ZSCAN_WIN;
+                const uint8_t *q = S.at(ip + sp, sw); // q[x] = block byte sp + x, x < sw
+                int64_t x = 0;
+                uint32_t nseq;
+                const int b0 = q[0];
+                if (b0 < 128) {
+                    nseq = (uint32_t)b0;
+                    x = 1;
+                } else if (b0 < 255) {
+                    if (2 > sw) return false;
+                    nseq = ((uint32_t)(b0 - 128) << 8) + q[1];
+                    x = 2;
+                } else {
+                    if (3 > sw) return false;
+                    nseq = q[1] + ((uint32_t)q[2] << 8) + 0x7F00;
+                    x = 3;
+                }
+                if (nseq > (uint32_t)ZMAX_BLOCK / 3 + 1) return false; // every match is >= 3 bytes
+                d.nseq = nseq;
+                if (nseq) {
+                    if (x >= sw) return false;
+                    const int modes = q[x++];
+                    if (modes & 3) return false; // reserved bits
+                    const int mk[3] = {modes >> 6, (modes >> 4) & 3, (modes >> 2) & 3};
+                    for (int k = 0; k < 3; ++k) {
+                        const int m = mk[k];
+                        if (m == 0) {
+                            tab[k] = 0;
+                            tab_n[k] = 0;
+                        } else if (m == 1) {
+                            if (x + 1 > sw) return false;
+                            tab[k] = 1u << 30 | (uint32_t)(ip + sp + x);
+                            tab_n[k] = 1;
+                            x += 1;
+                        } else if (m == 2) {
+                            int16_t norm[53];
+                            int log, nsym;
+                            const int64_t u = fse_read_ncount(q + x, sw - x, k == 1 ? 8 : 9, k == 0 ? 35 : k == 1 ? 31 : 52,
+                                                              norm, log, nsym);
+                            if (u < 0) return false;
+                            tab[k] = 2u << 30 | (uint32_t)(ip + sp + x);
+                            tab_n[k] = (uint32_t)u;
+                            x += u;
+                        } else if (tab[k] == ZNONE) {
+                            return false; // repeat mode without a previous table
+                        }
+                        d.tab[k] = tab[k];
+                        d.tab_n[k] = tab_n[k];
+                    }
+                    if (sp + x >= bn) return false; // the bitstream holds at least its marker byte
+                    d.seq_at = (uint32_t)(ip + sp + x);
+                    d.seq_n = (uint32_t)(bn - sp - x);
+                } else if (sp + x != bn) {
+                    return false;
+                }
+                nrec = nseq + 1;
+                if (bsize > o.c.max_comp) o.c.max_comp = bsize;
                 ip += bsize;
             }
+            lits += d.lsize;
+            if (lits > raw) return false;
+            if (o.blocks && o.writer) o.blocks[o.block0 + o.c.blocks] = d;
+            ++o.c.blocks;
+            o.c.recs += nrec;
             if (last) break;
         }
-        if (has_fcs && op - fstart != fcs) return -1;
         if (checksum) {
-            if (ip + 4 > n) return -1;
-            if (!put_seq(o, ZSeq{0, 0, rd32(src + ip), ZS_CHECK}, lane, nl)) return -1;
+            if (ip + 4 > n) return false;
+            fd.checksum = rd32(S.at(ip, 4));
+            fd.has_checksum = 1;
             ip += 4;
         }
+        fd.rec1 = o.rec0 + o.c.recs;
+        if (o.frames && o.writer) o.frames[o.frame0 + o.c.frames] = fd;
+        ++o.c.frames;
     }
-    return (int64_t)op;
+    return true;
+}
+ZHD bool zstd_scan(const uint8_t *src, int64_t n, uint64_t raw, ZScan &o) {
+    ZSrcMem m{src};
+    return zstd_scan(m, n, raw, o);
 }
 
-// record capacity of a packet frame of `raw` output bytes and `comp` compressed bytes: sequences
-// have a match of >= 3 bytes; every block adds at most one literal-run record and every ZSTD frame
-// (>= 8 bytes: magic, descriptor, one block header) two markers
-ZHD uint64_t zstd_seq_cap(uint64_t raw, uint64_t comp) { return raw / 3 + comp * 2 / 3 + 16; }
-
-// ---------------------------------------------------------------- stage 2 (host form)
-// Replays the records of one packet frame into dst[0, cap); -1 on any inconsistency (a record
-// past the literals or the output, an offset before its frame, a checksum mismatch).
-ZHD int64_t zstd_exec_serial(const ZSeq *seq, uint64_t nseq, const uint8_t *lit, uint64_t nlit, uint8_t *dst,
-                             uint64_t cap) {
-    uint64_t op = 0, lp = 0, fstart = 0;
-    for (uint64_t q = 0; q < nseq; ++q) {
-        const ZSeq r = seq[q];
-        if (r.tag == ZS_START) {
-            fstart = op;
-            continue;
-        }
-        if (r.tag == ZS_CHECK) {
-            if ((uint32_t)xxh64(dst + fstart, op - fstart) != r.off) return -1;
-            continue;
-        }
-        if (r.tag != ZS_SEQ || lp + r.ll > nlit || op + r.ll + r.ml > cap) return -1;
-        for (uint32_t i = 0; i < r.ll; ++i) dst[op + i] = lit[lp + i];
-        op += r.ll;
-        lp += r.ll;
-        if (r.ml) {
-            if (r.off == 0 || r.off > op - fstart) return -1;
-            for (uint32_t i = 0; i < r.ml; ++i) dst[op + i] = dst[op - r.off + i];
-            op += r.ml;
-        }
+// ---------------------------------------------------------------- stage 3: resolve (one ZSTD frame)
+// Repeat offsets in record order (RFC 8878 §3.1.2.5), positions, checks.  `pos` / `lpos`: the
+// frame's first output position (packet-frame-relative) and literal index; advanced past it.
+// One record: returns the resolved offset (0 = malformed) and updates the repeat offsets.
+ZHD uint32_t rep_resolve(uint32_t of, uint32_t ll, uint32_t &r0, uint32_t &r1, uint32_t &r2) {
+    if (of & ZDIRECT) return of & ~ZDIRECT;
+    if (of > 3) {
+        const uint32_t off = of - 3;
+        r2 = r1;
+        r1 = r0;
+        r0 = off;
+        return off;
     }
-    return lp == nlit ? (int64_t)op : -1;
+    const int idx = (int)of - 1 + (ll == 0 ? 1 : 0);
+    if (idx == 0) return r0;
+    const uint32_t t = idx == 3 ? r0 - 1 : idx == 1 ? r1 : r2;
+    if (idx != 1) r2 = r1;
+    r1 = r0;
+    r0 = t;
+    return t;
+}
+
+ZHD bool zstd_resolve_serial(ZRec *recs, ZFrameDesc &fr, uint64_t raw, uint64_t &pos, uint64_t &lpos) {
+    const uint64_t zstart = pos;
+    uint32_t r0 = 1, r1 = 4, r2 = 8;
+    fr.out0 = (uint32_t)pos;
+    for (uint32_t q = fr.rec0; q < fr.rec1; ++q) {
+        const ZRec r = recs[q];
+        const uint32_t ll = r.a, ml = r.b;
+        const uint32_t off = rep_resolve(r.c, ll, r0, r1, r2);
+        if (ml && (off == 0 || off > pos + ll - zstart)) return false;
+        if (pos + ll + ml > raw) return false;
+        recs[q] = ZRec{(uint32_t)pos, ll, (uint32_t)lpos, off};
+        pos += (uint64_t)ll + ml;
+        lpos += ll;
+    }
+    fr.out1 = (uint32_t)pos;
+    return fr.fcs == ~0ull || pos - zstart == fr.fcs;
 }
 
 #if !defined(__HIP_DEVICE_COMPILE__)
-// Host decode of one frame body (both stages): the decoded size, or -1 (tests/cpp/zstd_cpu.cpp).
-inline int64_t zstd_frame(const uint8_t *src, int64_t n, uint8_t *dst, uint64_t cap, ZWork *w) {
-    ZOut o{};
-    o.seq_cap = zstd_seq_cap(cap, (uint64_t)n);
-    o.lit_cap = cap;
-    o.seq = new ZSeq[o.seq_cap];
-    o.lit = new uint8_t[o.lit_cap + 1];
-    int64_t r = zstd_frame_entropy(src, n, cap, w, o);
-    if (r >= 0 && zstd_exec_serial(o.seq, o.nseq, o.lit, o.nlit, dst, cap) != r) r = -1;
-    delete[] o.seq;
-    delete[] o.lit;
-    return r;
+// ---------------------------------------------------------------- host form (tests)
+// Stage 2 of one block on the host: literals to lits[d.lit ...], records to recs[d.rec ...].
+inline bool zblock_decode_host(const uint8_t *body, const ZBlockDesc &d, ZTables &t, uint8_t *lits, ZRec *recs) {
+    if (d.type == 0) {
+        for (uint32_t i = 0; i < d.size; ++i) lits[d.lit + i] = body[d.src + i];
+        recs[d.rec] = ZRec{d.size, 0, ZDIRECT, 0};
+        return true;
+    }
+    if (d.type == 1) {
+        if (d.size) lits[d.lit] = body[d.src];
+        recs[d.rec] = ZRec{d.size ? 1u : 0u, d.size ? d.size - 1 : 0u, ZDIRECT | (d.size > 1 ? 1u : 0u), 0};
+        return true;
+    }
+    uint8_t *lit = lits + d.lit;
+    const uint8_t *ls = body + d.lit_at;
+    if (d.ltype == 0) {
+        for (uint32_t i = 0; i < d.lsize; ++i) lit[i] = ls[i];
+    } else if (d.ltype == 1) {
+        for (uint32_t i = 0; i < d.lsize; ++i) lit[i] = ls[0];
+    } else {
+        if (huf_read(body + d.huf, d.huf_n, t) < 0) return false;
+        if (d.streams == 1) {
+            if (!huf_stream(t, ls, d.lbytes, lit, d.lsize)) return false;
+        } else {
+            Huf4 h;
+            if (!huf4_split(ls, d.lbytes, d.lsize, h)) return false;
+            for (int k = 0; k < 4; ++k)
+                if (!huf_stream(t, ls + h.at[k], h.len[k], lit + k * h.seg, h.cnt[k])) return false;
+        }
+    }
+    if (d.nseq)
+        for (int k = 0; k < 3; ++k)
+            if (!seq_table_build(t, k, d.tab[k], d.tab_n[k], body)) return false;
+    return seq_decode<false>(t, body + d.seq_at, d.seq_n, d.nseq, d.lsize, [&](uint32_t q, const ZRec &r) { recs[d.rec + q] = r; });
+}
+
+// Host decode of one frame body that decodes to exactly `raw` bytes: the decoded size, or -1
+// (tests/cpp/zstd_cpu.cpp).  Stages 1-3 as the device runs them, then a serial replay.
+inline int64_t zstd_frame(const uint8_t *src, int64_t n, uint8_t *dst, uint64_t raw, uint64_t *nrec_out = nullptr) {
+    ZScan s;
+    if (!zstd_scan(src, n, raw, s)) return -1;
+    ZScan f;
+    f.blocks = new ZBlockDesc[s.c.blocks + 1];
+    f.frames = new ZFrameDesc[s.c.frames + 1];
+    ZRec *recs = new ZRec[s.c.recs + 1];
+    uint8_t *lits = new uint8_t[raw + 1];
+    ZTables *t = new ZTables;
+    bool ok = zstd_scan(src, n, raw, f);
+    for (uint32_t b = 0; ok && b < f.c.blocks; ++b) ok = zblock_decode_host(src, f.blocks[b], *t, lits, recs);
+    uint64_t pos = 0, lpos = 0;
+    for (uint32_t z = 0; ok && z < f.c.frames; ++z) ok = zstd_resolve_serial(recs, f.frames[z], raw, pos, lpos);
+    ok = ok && pos == raw;
+    for (uint32_t z = 0; ok && z < f.c.frames; ++z) {
+        const ZFrameDesc &fr = f.frames[z];
+        for (uint32_t q = fr.rec0; q < fr.rec1; ++q) {
+            const ZRec r = recs[q];
+            const uint64_t end = q + 1 < fr.rec1 ? recs[q + 1].a : fr.out1;
+            for (uint32_t i = 0; i < r.b; ++i) dst[r.a + i] = lits[r.c + i];
+            for (uint64_t p = r.a + r.b; p < end; ++p) dst[p] = dst[p - r.d];
+        }
+        if (fr.has_checksum && (uint32_t)xxh64(dst + fr.out0, fr.out1 - fr.out0) != fr.checksum) ok = false;
+    }
+    if (nrec_out) *nrec_out = s.c.recs;
+    delete[] f.blocks;
+    delete[] f.frames;
+    delete[] recs;
+    delete[] lits;
+    delete t;
+    return ok ? (int64_t)raw : -1;
 }
 #endif
 
