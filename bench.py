@@ -464,7 +464,8 @@ def zstd_leg(args, ctx, pkt):
     """ZSTD packets (CompressionMethod::ZSTD, the HIGH_COMPRESSION mode): a 64 MB slice of the
     uncompressed V1 packet body compressed on the host by the system libzstd (level 1, one frame
     per 1 MB CompressedWriteBuffer block, as the reference's sender writes them), then decompressed
-    on the device (one thread per frame, zstd_dec.h); checked against the packet.  The host
+    on the device (zstd.hip: header scan, per-block entropy, resolve, byte-parallel execution);
+    checked against the packet.  The host
     decompress of the same frames by libzstd on one thread is reported beside it."""
     import ctypes
     import struct

@@ -1081,7 +1081,7 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
     extern __shared__ __attribute__((aligned(16))) char lds[];
     constexpr int RT = Ops::WIDE ? 2 : RPT; // rows per thread per step (wide rows: 2, fewer VGPRs)
     __shared__ unsigned long long s_red[BT / 64];
-    __shared__ unsigned long long s_base[2];
+    __shared__ unsigned long long s_base[3];
     constexpr int CH = BT; // tiles per pass-0 chunk: one per thread
     __shared__ uint32_t s_ent[CH];
     __shared__ uint32_t s_pref[CH + 1];
@@ -1110,10 +1110,19 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
         for (int w = 0; w < BT / 64; ++w) t += s_red[w];
         s_base[0] = atomicAdd(&tin.cursor[0], t);
         s_base[1] = atomicAdd(&tin.cursor[1], t + (unsigned long long)(oe - os));
+        s_base[2] = t;
         T.ctrl->out_count = 0;
     }
     __syncthreads();
     const uint64_t sbase = s_base[0], out_base = s_base[1];
+    const bool no_rows = s_base[2] == 0; // a bucket no kept row reached: pass 0 has nothing to walk
+    if (no_rows && os == oe) { // nothing at all: no table to build or flush
+        if (threadIdx.x == 0) {
+            out_cnt[b] = 0;
+            tmp_base[b] = out_base;
+        }
+        return;
+    }
     // the two spill regions as plain pointers, chosen per pass by value (an array of RowsIO
     // indexed by the pass would live in scratch memory)
     RowsIO src{};
@@ -1225,7 +1234,9 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
                 }
             }
         };
-        if (pass == 0) {
+        if (pass == 0 && no_rows) {
+            // only the bucket's older groups (seeded above) pass through
+        } else if (pass == 0) {
             // chunks of CH tiles: their runs are concatenated (prefix of the counts in LDS) and
             // row i of the chunk finds its tile by a log2(CH)-step binary search, so every thread
             // takes RT rows per step whatever the run lengths

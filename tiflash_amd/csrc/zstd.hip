@@ -8,12 +8,13 @@
 //                                 staged in LDS; wave 0 decodes the literals (the four Huffman
 //                                 streams on lanes 0-3), wave 1 the sequences (FSE, lockstep,
 //                                 records flushed 64 at a time) — the two halves are independent
-//   resolve  zstd_resolve_kernel  one wave per packet frame: repeat offsets in order (readlane),
-//                                 positions by wave scans, every check
+//   resolve  zstd_resolve_kernel  one wave per packet frame: repeat offsets and positions by wave
+//                                 scans (the repeat-offset updates compose), every check
 //   execute  zstd_expand_kernel   every output byte: literal bytes copied, match bytes get their
-//                                 source index; zstd_jump_kernel (src = src[src], repeated until no
-//                                 byte points at a match byte: log2 of the longest match chain
-//                                 rounds); zstd_gather_kernel copies the match bytes
+//                                 source index and join a list; zstd_jump_kernel (src = src[src]
+//                                 over the list, the still-unresolved bytes forming the next list:
+//                                 log2 of the longest match chain rounds, each shorter than the
+//                                 last); zstd_gather_kernel copies the match bytes
 //   checksum zstd_check_kernel    one wave per ZSTD frame with a content checksum (XXH64)
 // Every kernel is memory-safe on any input: a malformed frame raises the error flag and the later
 // kernels keep every index inside the launch's buffers.
@@ -30,7 +31,6 @@ constexpr uint32_t ZCHUNK = 4096;                         // output bytes per ex
 constexpr int ZMAX_ROUNDS = 40;                           // pointer-jumping rounds (chains < 2^40)
 
 __device__ __forceinline__ void lds_order() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-__device__ __forceinline__ uint32_t rl32(uint32_t v, uint32_t j) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)j); }
 
 // ---------------------------------------------------------------- scan
 // The scan's byte source on the device: a ZSCAN_WIN-byte LDS window, loaded by all lanes (8 bytes
@@ -89,7 +89,7 @@ __global__ void __launch_bounds__(64) zstd_scan_kernel(const uint8_t *pkt, const
 // ---------------------------------------------------------------- entropy
 // The four-lane Huffman decode of a block's literals: lane k < ns decodes stream k.
 template <bool AL>
-__device__ bool huf_lanes(const tfz::ZTables &T, const uint8_t *ls, int64_t lbytes, uint32_t lsize, int ns, uint8_t *lit,
+__device__ __forceinline__ bool huf_lanes(const tfz::ZTables &T, const uint8_t *ls, int64_t lbytes, uint32_t lsize, int ns, uint8_t *lit,
                           uint32_t lane) {
     int64_t at = 0, len = lbytes, cnt = lsize, o = 0;
     if (ns == 4) {
@@ -119,7 +119,7 @@ __device__ bool huf_lanes(const tfz::ZTables &T, const uint8_t *ls, int64_t lbyt
 }
 
 template <bool AL>
-__device__ bool seq_wave(const tfz::ZTables &T, const uint8_t *bits, int64_t n, const tfz::ZBlockDesc &d, tfz::ZRec *recs,
+__device__ __forceinline__ bool seq_wave(const tfz::ZTables &T, const uint8_t *bits, int64_t n, const tfz::ZBlockDesc &d, tfz::ZRec *recs,
                          uint32_t lane) {
     tfz::ZRec mine{0, 0, 0, 0};
     const bool ok = tfz::seq_decode<AL>(T, bits, n, d.nseq, d.lsize, [&](uint32_t q, const tfz::ZRec &r) {
@@ -198,9 +198,54 @@ __global__ void __launch_bounds__(128) zstd_block_kernel(const uint8_t *pkt, con
 }
 
 // ---------------------------------------------------------------- resolve
-// One wave per packet frame.  Records go 64 at a time (the next batch loaded while this one is
-// resolved): scans give positions, the repeat offsets run through the 64 in order.  Records are
-// rewritten as {pos, ll, lpos, off}.
+// The repeat offsets as a scan.  A record maps the state (r0, r1, r2) to a new state whose every
+// slot is an old slot plus a delta, or a constant (RFC 8878 §3.1.2.5: a new offset shifts the
+// three; a repeat code moves one to the front, code 3 with no literals takes r0 - 1).  Such maps
+// compose, so a wave scan gives every record the map from the batch's incoming state to the
+// state before it, and its offset follows with no serial loop.
+struct RepMap {
+    uint32_t kinds; // slot k: bits 2k..2k+1 = the old slot it copies (0-2) or 3 = a constant
+    uint32_t v[3];  // delta (slot) or value (constant)
+};
+__device__ __forceinline__ RepMap rep_identity() { return RepMap{0u | 1u << 2 | 2u << 4, {0, 0, 0}}; }
+// b after a
+__device__ __forceinline__ RepMap rep_compose(const RepMap &a, const RepMap &b) {
+    RepMap c;
+    c.kinds = 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const uint32_t kb = (b.kinds >> (2 * k)) & 3u;
+        uint32_t kind, val;
+        if (kb == 3) {
+            kind = 3;
+            val = b.v[k];
+        } else {
+            const uint32_t ka = (a.kinds >> (2 * kb)) & 3u;
+            const uint32_t va = kb == 0 ? a.v[0] : kb == 1 ? a.v[1] : a.v[2];
+            kind = ka;
+            val = va + b.v[k];
+        }
+        c.kinds |= kind << (2 * k);
+        c.v[k] = val;
+    }
+    return c;
+}
+__device__ __forceinline__ uint32_t rep_slot(const RepMap &m, int k, uint32_t r0, uint32_t r1, uint32_t r2) {
+    const uint32_t kind = (m.kinds >> (2 * k)) & 3u;
+    return kind == 3 ? m.v[k] : (kind == 0 ? r0 : kind == 1 ? r1 : r2) + m.v[k];
+}
+__device__ __forceinline__ RepMap rep_shfl_up(const RepMap &m, int d) {
+    RepMap o;
+    o.kinds = __shfl_up(m.kinds, d, 64);
+    o.v[0] = __shfl_up(m.v[0], d, 64);
+    o.v[1] = __shfl_up(m.v[1], d, 64);
+    o.v[2] = __shfl_up(m.v[2], d, 64);
+    return o;
+}
+
+// One wave per packet frame, records 64 at a time (the next batch loaded while this one is
+// resolved): scans give positions and repeat-offset maps; records are rewritten as
+// {pos, ll, lpos, off}.
 __global__ void __launch_bounds__(64) zstd_resolve_kernel(const uint64_t *roff, uint64_t f0, const uint32_t *bases,
                                                           tfz::ZFrameDesc *frames, tfz::ZRec *recs, unsigned *err) {
     const uint32_t i = blockIdx.x, lane = threadIdx.x;
@@ -208,7 +253,7 @@ __global__ void __launch_bounds__(64) zstd_resolve_kernel(const uint64_t *roff, 
     uint32_t pos = 0, lpos = (uint32_t)(roff[f] - roff[f0]);
     bool bad = false;
     for (uint32_t z = bases[4 * i + 1]; z < bases[4 * i + 5] && !bad; ++z) {
-        tfz::ZFrameDesc fr = frames[z];
+        const tfz::ZFrameDesc fr = frames[z];
         const uint32_t zstart = pos;
         uint32_t r0 = 1, r1 = 4, r2 = 8;
         tfz::ZRec nxt{0, 0, tfz::ZDIRECT, 0};
@@ -218,7 +263,48 @@ __global__ void __launch_bounds__(64) zstd_resolve_kernel(const uint64_t *roff, 
             const uint32_t cnt = fr.rec1 - q0 < 64 ? fr.rec1 - q0 : 64;
             nxt = tfz::ZRec{0, 0, tfz::ZDIRECT, 0};
             if (q0 + 64 + lane < fr.rec1) nxt = recs[q0 + 64 + lane];
-            const uint32_t ll = lane < cnt ? r.a : 0, ml = lane < cnt ? r.b : 0;
+            const bool valid = lane < cnt;
+            const uint32_t ll = valid ? r.a : 0, ml = valid ? r.b : 0, of = valid ? r.c : tfz::ZDIRECT;
+            // this record's map and its offset's expression (a map slot over the state before it)
+            RepMap m = rep_identity();
+            uint32_t ekind = 3, eval = of & ~tfz::ZDIRECT; // the offset: slot ekind + eval, or eval
+            if (!(of & tfz::ZDIRECT)) {
+                if (of > 3) {
+                    m = RepMap{3u | 0u << 2 | 1u << 4, {of - 3, 0, 0}};
+                    eval = of - 3;
+                } else {
+                    const uint32_t idx = of - 1 + (ll == 0 ? 1u : 0u);
+                    if (idx == 0) {
+                        ekind = 0;
+                        eval = 0;
+                    } else if (idx == 1) {
+                        m = RepMap{1u | 0u << 2 | 2u << 4, {0, 0, 0}};
+                        ekind = 1;
+                        eval = 0;
+                    } else if (idx == 2) {
+                        m = RepMap{2u | 0u << 2 | 1u << 4, {0, 0, 0}};
+                        ekind = 2;
+                        eval = 0;
+                    } else {
+                        m = RepMap{0u | 0u << 2 | 1u << 4, {0xFFFFFFFFu, 0, 0}};
+                        ekind = 0;
+                        eval = 0xFFFFFFFFu;
+                    }
+                }
+            }
+            // inclusive scan of the maps, then the exclusive one (the state before each record)
+            RepMap inc = m;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const RepMap y = rep_shfl_up(inc, d);
+                if (lane >= (uint32_t)d) inc = rep_compose(y, inc);
+            }
+            RepMap exc = rep_shfl_up(inc, 1);
+            if (lane == 0) exc = rep_identity();
+            const uint32_t s0 = rep_slot(exc, 0, r0, r1, r2), s1 = rep_slot(exc, 1, r0, r1, r2),
+                           s2 = rep_slot(exc, 2, r0, r1, r2);
+            const uint32_t myoff = ekind == 3 ? eval : (ekind == 0 ? s0 : ekind == 1 ? s1 : s2) + eval;
+            // positions
             uint64_t span = (uint64_t)ll + ml, incl = span;
             uint32_t linc = ll;
 #pragma unroll
@@ -232,26 +318,29 @@ __global__ void __launch_bounds__(64) zstd_resolve_kernel(const uint64_t *roff, 
             }
             const uint64_t mypos = pos + incl - span;
             const uint32_t mylpos = lpos + linc - ll;
-            uint32_t myoff = 0;
-            for (uint32_t j = 0; j < cnt; ++j) {
-                const uint32_t off = tfz::rep_resolve(rl32(r.c, j), rl32(r.a, j), r0, r1, r2);
-                myoff = lane == j ? off : myoff;
-            }
-            if (lane < cnt) {
+            if (valid) {
                 if (ml && (myoff == 0 || (uint64_t)myoff > mypos + ll - zstart)) bad = true;
                 if (mypos + span > raw) bad = true;
                 recs[q0 + lane] = tfz::ZRec{(uint32_t)mypos, ll, mylpos, myoff};
             }
+            // the batch's outgoing state: the last lane's inclusive map (lanes past cnt: identity)
+            const RepMap last = RepMap{(uint32_t)__shfl(inc.kinds, 63, 64),
+                                       {(uint32_t)__shfl(inc.v[0], 63, 64), (uint32_t)__shfl(inc.v[1], 63, 64),
+                                        (uint32_t)__shfl(inc.v[2], 63, 64)}};
+            const uint32_t n0 = rep_slot(last, 0, r0, r1, r2), n1 = rep_slot(last, 1, r0, r1, r2),
+                           n2 = rep_slot(last, 2, r0, r1, r2);
+            r0 = n0;
+            r1 = n1;
+            r2 = n2;
             const uint64_t tot = __shfl(incl, 63, 64);
             const uint32_t ltot = __shfl(linc, 63, 64);
-            if (pos + tot > raw) {
+            bad = __ballot(bad) != 0;
+            if (bad || pos + tot > raw) {
                 bad = true;
                 break;
             }
             pos += (uint32_t)tot;
             lpos += ltot;
-            bad = __ballot(bad) != 0;
-            if (bad) break;
         }
         if (lane == 0) {
             frames[z].out0 = zstart;
@@ -264,13 +353,26 @@ __global__ void __launch_bounds__(64) zstd_resolve_kernel(const uint64_t *roff, 
 }
 
 // ---------------------------------------------------------------- execute
+// Worklists of byte indices (launch-relative): count + entries.  Appends are wave-aggregated.
+__device__ __forceinline__ void wl_append(bool want, uint32_t g, uint32_t *list, unsigned *count) {
+    const uint64_t m = __ballot(want);
+    if (!m) return;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t leader = (uint32_t)__builtin_ctzll(m);
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(count, (unsigned)__popcll(m));
+    base = __shfl(base, (int)leader, 64);
+    if (want) list[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = g;
+}
+
 // One workgroup per ZCHUNK output bytes of a packet frame (cbase: prefix of the frames' chunk
-// counts); 16 bytes a thread.  Literal bytes are written to `out`; src[g] = g for them, g - off
-// for match bytes (g: launch-relative output index).
+// counts); 16 bytes a thread.  Literal bytes are written to `out` and point at themselves
+// (src[g] = g); a match byte points at its source byte (src[g] = g - off) and joins the list of
+// match bytes.
 __global__ void __launch_bounds__(256) zstd_expand_kernel(const uint64_t *roff, uint64_t f0, uint32_t nf,
                                                           const uint32_t *cbase, const uint32_t *bases, const tfz::ZRec *recs,
                                                           const uint8_t *lits, uint64_t nlits, uint8_t *out, uint32_t *src,
-                                                          unsigned *err) {
+                                                          uint32_t *mlist, unsigned *mcount, unsigned *err) {
     __shared__ uint32_t range[2];
     const uint32_t c = blockIdx.x;
     uint32_t lo = 0, hi = nf; // the frame: last i with cbase[i] <= c
@@ -297,59 +399,91 @@ __global__ void __launch_bounds__(256) zstd_expand_kernel(const uint64_t *roff, 
     if (threadIdx.x == 1) range[1] = last_le(r0, r1, b1 ? b1 - 1 : 0) + 1;
     __syncthreads();
     const uint32_t s = b0 + threadIdx.x * 16;
-    if (s >= b1) return;
-    const uint32_t e = s + 16 < b1 ? s + 16 : b1;
-    uint32_t r = last_le(range[0], range[1], s);
-    tfz::ZRec rec = recs[r];
-    uint32_t end = r + 1 < r1 ? recs[r + 1].a : (uint32_t)raw;
+    const uint32_t e = s < b1 ? (s + 16 < b1 ? s + 16 : b1) : s;
     bool bad = false;
-    for (uint32_t b = s; b < e; ++b) {
-        while (b >= end && r + 1 < r1) {
-            ++r;
-            rec = recs[r];
-            end = r + 1 < r1 ? recs[r + 1].a : (uint32_t)raw;
+    uint32_t sv[16];
+    uint32_t mmask = 0;
+    if (s < e) {
+        uint32_t r = last_le(range[0], range[1], s);
+        tfz::ZRec rec = recs[r];
+        uint32_t end = r + 1 < r1 ? recs[r + 1].a : (uint32_t)raw;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint32_t b = s + k;
+            if (b >= e) break;
+            while (b >= end && r + 1 < r1) {
+                ++r;
+                rec = recs[r];
+                end = r + 1 < r1 ? recs[r + 1].a : (uint32_t)raw;
+            }
+            const uint64_t g = g0 + b;
+            sv[k] = (uint32_t)g;
+            if (b < rec.a) {
+                bad = true; // inconsistent positions (a malformed frame)
+            } else if (b - rec.a < rec.b) {
+                const uint64_t li = (uint64_t)rec.c + (b - rec.a);
+                if (li < nlits) out[g] = lits[li];
+                else bad = true;
+            } else if (rec.d == 0 || rec.d > b) {
+                bad = true;
+            } else {
+                sv[k] = (uint32_t)(g - rec.d);
+                mmask |= 1u << k;
+            }
         }
-        const uint64_t g = g0 + b;
-        uint32_t sv = (uint32_t)g;
-        if (b < rec.a) {
-            bad = true; // inconsistent positions (a malformed frame)
-        } else if (b - rec.a < rec.b) {
-            const uint64_t li = (uint64_t)rec.c + (b - rec.a);
-            if (li < nlits) out[g] = lits[li];
-            else bad = true;
-        } else if (rec.d == 0 || rec.d > b) {
-            bad = true;
-        } else {
-            sv = (uint32_t)(g - rec.d);
-        }
-        src[g] = sv;
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (s + k < e) src[g0 + s + k] = sv[k];
     }
+    // the match bytes into the list: a wave scan of the per-thread counts, one atomic per wave
+    const uint32_t lane = threadIdx.x & 63, cnt = (uint32_t)__popc(mmask);
+    uint32_t x = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= (uint32_t)d) x += y;
+    }
+    const uint32_t total = __shfl(x, 63, 64);
+    uint32_t base = 0;
+    if (lane == 63 && total) base = atomicAdd(mcount, total);
+    base = __shfl(base, 63, 64) + x - cnt;
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        if (mmask & (1u << k)) mlist[base++] = (uint32_t)(g0 + s + k);
     if (bad) atomicOr(err, 1u);
 }
 
-// One pointer-jumping round over src[0, n): src[g] = src[src[g]]; *flag = 1 while some byte
-// still points at a byte that is not a literal.
-__global__ void __launch_bounds__(256) zstd_jump_kernel(uint32_t *src, uint64_t n, unsigned *flag) {
-    const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    bool more = false;
-    if (g < n) {
-        const uint32_t s = src[g];
-        if (s != (uint32_t)g) {
+// One pointer-jumping round over the bytes of list `in` (count *nin): src[g] = src[src[g]]; the
+// bytes whose source is still not a literal go to list `out`.  Grid-stride over the count read
+// on the device, so rounds are launched without a host read between them.
+__global__ void __launch_bounds__(256) zstd_jump_kernel(uint32_t *src, const uint32_t *in, const unsigned *nin,
+                                                        uint32_t *outl, unsigned *nout) {
+    const uint32_t n = *nin;
+    const uint32_t stride = gridDim.x * 256;
+    for (uint32_t i0 = blockIdx.x * 256; i0 < n; i0 += stride) {
+        const uint32_t i = i0 + threadIdx.x;
+        bool more = false;
+        uint32_t g = 0;
+        if (i < n) {
+            g = in[i];
+            const uint32_t s = src[g];
             const uint32_t t = src[s];
             if (t != s) {
                 src[g] = t;
                 more = src[t] != t;
             }
         }
+        wl_append(more, g, outl, nout);
     }
-    if (__ballot(more) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
 }
 
-__global__ void __launch_bounds__(256) zstd_gather_kernel(const uint32_t *src, uint64_t n, uint8_t *out) {
-    const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (g < n) {
-        const uint32_t s = src[g];
-        if (s != (uint32_t)g) out[g] = out[s];
+// match bytes (list, count *n) take their source byte: a literal byte once the rounds are done
+__global__ void __launch_bounds__(256) zstd_gather_kernel(const uint32_t *src, const uint32_t *list, const unsigned *n,
+                                                          uint8_t *out) {
+    const uint32_t cnt = *n, stride = gridDim.x * 256;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < cnt; i += stride) {
+        const uint32_t g = list[i];
+        out[g] = out[src[g]];
     }
 }
 
@@ -459,13 +593,14 @@ int zstd_decode_frames(Ctx *ctx, const uint8_t *packet, uint64_t nf, const uint6
         TFG_LAUNCH_CHECK();
     }
     std::vector<tfz::ZCounts> counts(nf);
-    if (int rc = read_back_u64(ctx, (const uint64_t *)dcounts, (uint64_t *)counts.data(), nf * 2)) return rc;
+    TFG_HIP(hipMemcpyAsync(counts.data(), dcounts, nf * sizeof(tfz::ZCounts), hipMemcpyDeviceToHost, ctx->stream));
+    TFG_HIP(hipStreamSynchronize(ctx->stream));
     for (uint64_t f = 0; f < nf; ++f)
         TFG_CHECK(counts[f].blocks != tfz::ZNONE, TFG_ERR_INVALID_ARG, "corrupted ZSTD frame (Cannot decompress)");
     auto need = [&](uint64_t f) { // launch bytes of frame f: descriptors, records, literals, sources
         const uint64_t raw = ro[f + 1] - ro[f];
         return (uint64_t)counts[f].blocks * sizeof(tfz::ZBlockDesc) + (uint64_t)counts[f].frames * sizeof(tfz::ZFrameDesc) +
-               (uint64_t)counts[f].recs * sizeof(tfz::ZRec) + raw * 5 + 64;
+               (uint64_t)counts[f].recs * sizeof(tfz::ZRec) + raw * 17 + 64; // literals + src + 3 byte lists
     };
     for (uint64_t a = 0; a < nf;) {
         // ---- a launch group: frames [a, z) within ZSTD_SCRATCH and 32-bit indices
@@ -500,7 +635,8 @@ int zstd_decode_frames(Ctx *ctx, const uint8_t *packet, uint64_t nf, const uint6
         const size_t o_blk = cv.take<tfz::ZBlockDesc>(nb + 1), o_frm = cv.take<tfz::ZFrameDesc>(nz + 1);
         const size_t o_rec = cv.take<tfz::ZRec>(nr + 1), o_lit = cv.take<uint8_t>(raw + 1);
         const size_t o_src = cv.take<uint32_t>(raw + 1), o_bas = cv.take<uint32_t>(bases.size());
-        const size_t o_cb = cv.take<uint32_t>(cbase.size()), o_flag = cv.take<uint64_t>(1);
+        const size_t o_cb = cv.take<uint32_t>(cbase.size()), o_cnt = cv.take<unsigned>(4);
+        const size_t o_l0 = cv.take<uint32_t>(raw + 1), o_l1 = cv.take<uint32_t>(raw + 1), o_l2 = cv.take<uint32_t>(raw + 1);
         if (int rc = buf.reserve(cv.off)) return rc;
         char *sb = (char *)buf.p;
         tfz::ZBlockDesc *blk = (tfz::ZBlockDesc *)(sb + o_blk);
@@ -508,7 +644,9 @@ int zstd_decode_frames(Ctx *ctx, const uint8_t *packet, uint64_t nf, const uint6
         tfz::ZRec *rec = (tfz::ZRec *)(sb + o_rec);
         uint8_t *lit = (uint8_t *)(sb + o_lit);
         uint32_t *src = (uint32_t *)(sb + o_src), *dbases = (uint32_t *)(sb + o_bas), *dcb = (uint32_t *)(sb + o_cb);
-        unsigned *flag = (unsigned *)(sb + o_flag);
+        unsigned *lcount = (unsigned *)(sb + o_cnt); // [0] match bytes, [1] / [2] the round lists
+        uint32_t *mlist = (uint32_t *)(sb + o_l0), *wl[2] = {(uint32_t *)(sb + o_l1), (uint32_t *)(sb + o_l2)};
+        TFG_HIP(hipMemsetAsync(lcount, 0, 4 * sizeof(unsigned), ctx->stream));
         TFG_HIP(hipMemcpyAsync(dbases, bases.data(), bases.size() * 4, hipMemcpyHostToDevice, ctx->stream));
         TFG_HIP(hipMemcpyAsync(dcb, cbase.data(), cbase.size() * 4, hipMemcpyHostToDevice, ctx->stream));
         uint8_t *out = dst + ro[a];
@@ -530,29 +668,36 @@ int zstd_decode_frames(Ctx *ctx, const uint8_t *packet, uint64_t nf, const uint6
             if (nc) {
                 hipLaunchKernelGGL(zstd_expand_kernel, dim3(nc), dim3(256), 0, ctx->stream, dro, a, (uint32_t)g,
                                    (const uint32_t *)dcb, (const uint32_t *)dbases, (const tfz::ZRec *)rec,
-                                   (const uint8_t *)lit, raw, out, src, err);
+                                   (const uint8_t *)lit, raw, out, src, mlist, lcount, err);
                 TFG_LAUNCH_CHECK();
             }
         }
-        const unsigned jg = (unsigned)((raw + 255) / 256);
+        // pointer jumping over the match bytes: rounds go in batches of 4 without a host read
+        // between them (an empty list costs one launch); the batch's last list count decides
+        const unsigned jg = (unsigned)std::min<uint64_t>((raw + 255) / 256, 16384);
         if (raw) {
+            const uint32_t *in = mlist;
+            const unsigned *nin = lcount;
             int round = 0;
-            for (;; ++round) {
-                TFG_CHECK(round < ZMAX_ROUNDS, TFG_ERR_INVALID_ARG, "corrupted ZSTD frame (Cannot decompress)");
-                TFG_HIP(hipMemsetAsync(flag, 0, sizeof(unsigned), ctx->stream));
-                {
+            for (bool more = true; more;) {
+                for (int k = 0; k < 4; ++k, ++round) {
+                    TFG_CHECK(round < ZMAX_ROUNDS, TFG_ERR_INVALID_ARG, "corrupted ZSTD frame (Cannot decompress)");
+                    uint32_t *o = wl[round & 1];
+                    unsigned *no = lcount + 1 + (round & 1);
+                    TFG_HIP(hipMemsetAsync(no, 0, sizeof(unsigned), ctx->stream));
                     ProfScope _ps(ctx, "codec.zstd.decompress");
-                    hipLaunchKernelGGL(zstd_jump_kernel, dim3(jg), dim3(256), 0, ctx->stream, src, raw, flag);
+                    hipLaunchKernelGGL(zstd_jump_kernel, dim3(jg), dim3(256), 0, ctx->stream, src, in, nin, o, no);
                     TFG_LAUNCH_CHECK();
+                    in = o;
+                    nin = no;
                 }
-                uint64_t more = 0;
-                TFG_HIP(hipMemcpyAsync(ctx->host_pinned, flag, sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
+                TFG_HIP(hipMemcpyAsync(ctx->host_pinned, nin, sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
                 TFG_HIP(hipStreamSynchronize(ctx->stream));
-                more = *(const unsigned *)ctx->host_pinned;
-                if (!more) break;
+                more = *(const unsigned *)ctx->host_pinned != 0;
             }
             ProfScope _ps(ctx, "codec.zstd.decompress");
-            hipLaunchKernelGGL(zstd_gather_kernel, dim3(jg), dim3(256), 0, ctx->stream, (const uint32_t *)src, raw, out);
+            hipLaunchKernelGGL(zstd_gather_kernel, dim3(jg), dim3(256), 0, ctx->stream, (const uint32_t *)src,
+                               (const uint32_t *)mlist, (const unsigned *)lcount, out);
             TFG_LAUNCH_CHECK();
         }
         if (nz) {

@@ -52,12 +52,11 @@ struct FseEntry {
 // A sequence decoding-table entry: the FSE state transition (base, bits) and the symbol's
 // baseline + additional bits (literal / match length codes, or offset code c: 1 << c, c bits),
 // so each of the three codes of a sequence costs one table read (zstd's ZSTD_seqSymbol).
-struct ZSeqEntry {
+struct alignas(8) ZSeqEntry { // 8 bytes: one LDS read per code
     uint32_t value; // baseline of the decoded value
     uint16_t base;  // next-state base
     uint8_t bits;   // next-state bits
-    uint8_t sym;    // the code (while the table is built)
-    uint8_t add;    // additional bits of the value
+    uint8_t sym;    // the code while the table is built, then the value's additional bits
 };
 
 // The tables of one block (LDS on the device, ~14 KB)
@@ -207,10 +206,11 @@ template <bool ALIGNED = false> struct BitR {
         const int64_t b0 = ((pos + 7) >> 3) - 8;
         wlo = b0 * 8;
 #if defined(__HIP_DEVICE_COMPILE__)
-        if (ALIGNED && b0 >= 0 && b0 + 8 <= n) {
-            const uintptr_t a = (uintptr_t)(p + b0);
-            const uint64_t *w = (const uint64_t *)(a & ~(uintptr_t)7);
-            const uint32_t sh = (uint32_t)(a & 7) * 8;
+        if (ALIGNED && b0 >= 0 && b0 + 8 <= n) { // two aligned LDS words (local address space)
+            typedef __attribute__((address_space(3))) const uint64_t lds_u64;
+            const uint8_t *q = p + b0;
+            const uint32_t sh = (uint32_t)((uintptr_t)q & 7) * 8;
+            lds_u64 *w = (lds_u64 *)(q - ((uintptr_t)q & 7));
             const uint64_t lo = w[0], hi = w[1];
             win = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
             return;
@@ -508,7 +508,7 @@ ZHD bool seq_finish(ZSeqEntry *t, int size, int kind) {
         const int c = t[u].sym;
         if (c > max_sym) return false;
         t[u].value = kind == 0 ? ll_base(c) : kind == 1 ? (1u << c) : ml_base(c);
-        t[u].add = (uint8_t)(kind == 0 ? ll_bits(c) : kind == 1 ? c : ml_bits(c));
+        t[u].sym = (uint8_t)(kind == 0 ? ll_bits(c) : kind == 1 ? c : ml_bits(c)); // now: additional bits
     }
     return true;
 }
@@ -549,12 +549,12 @@ ZHD bool seq_decode(const ZTables &t, const uint8_t *bits, int64_t n, uint32_t n
         uint32_t sll = (uint32_t)bb.read(t.ll_log), sof = (uint32_t)bb.read(t.of_log), sml = (uint32_t)bb.read(t.ml_log);
         for (uint32_t q = 0; q < nseq; ++q) {
             const ZSeqEntry el = t.ll[sll], eo = t.of[sof], em = t.ml[sml];
-            const uint32_t ofv = eo.value + (uint32_t)bb.read(eo.add);
+            const uint32_t ofv = eo.value + (uint32_t)bb.read(eo.sym);
             bb.need(32);
-            const uint32_t ml = em.value + (uint32_t)bb.peek(em.add);
-            bb.pos -= em.add;
-            const uint32_t ll = el.value + (uint32_t)bb.peek(el.add);
-            bb.pos -= el.add;
+            const uint32_t ml = em.value + (uint32_t)bb.peek(em.sym);
+            bb.pos -= em.sym;
+            const uint32_t ll = el.value + (uint32_t)bb.peek(el.sym);
+            bb.pos -= el.sym;
             if (q + 1 < nseq) { // state updates: LL, ML, OF
                 bb.need(26);
                 sll = el.base + (uint32_t)bb.peek(el.bits);

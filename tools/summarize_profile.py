@@ -49,6 +49,13 @@ NAME_MAP = [
     (r"part_scatter.*<tfg::SelJoin", "join.part.scatter"),
     (r"join_probe_kernel", "join.probe"),
     (r"join_build", "join.build"),
+    (r"zstd_scan_kernel", "codec.zstd.scan"),
+    (r"zstd_block_kernel", "codec.zstd.block"),
+    (r"zstd_resolve_kernel", "codec.zstd.resolve"),
+    (r"zstd_expand_kernel", "codec.zstd.expand"),
+    (r"zstd_jump_kernel", "codec.zstd.jump"),
+    (r"zstd_gather_kernel", "codec.zstd.gather"),
+    (r"zstd_check_kernel", "codec.zstd.check"),
     (r"gather_kernel", "gather"),
     (r"scan_", "scan"),
 ]
@@ -57,7 +64,7 @@ LEGS = [
     ("C3v2", r"join_v2_"),
     ("C2", r"^(agg\.part\.(hist|tiled|scatter)|agg\.bucket\.tiled)$"),
     ("C3", r"^(join\.|part\.(hist|scatter)\.pass2)"),
-    ("codec", r"tfg::str_|codec|lz4_"),
+    ("codec", r"tfg::str_|codec|lz4_|zstd_"),
     ("C5", r"^(agg\.wide\.|agg\.(pack|unpack)_keys|agg\.bucket$)|wide_str|regroup_"),
 ]
 
