@@ -106,7 +106,18 @@ __device__ __forceinline__ bool huf_lanes(const tfz::ZTables &T, const uint8_t *
         tfz::BitR<AL> bb;
         ok = bb.init(ls + at, len);
         const int mb = T.huf_bits;
-        for (int64_t i = 0; ok && i < cnt; ++i) {
+        int64_t i = 0;
+        for (; ok && i + 1 < cnt;) { // two symbols a lookup while two remain
+            bb.need(mb);
+            const uint32_t e = T.huf2[bb.peek(mb)];
+            const bool two = (e >> 25) & 1u;
+            lit[o + i] = (uint8_t)e;
+            if (two) lit[o + i + 1] = (uint8_t)(e >> 8);
+            bb.pos -= two ? (e >> 20) & 31u : (e >> 16) & 15u;
+            i += two ? 2 : 1;
+            ok = bb.pos >= 0;
+        }
+        if (ok && i < cnt) { // the last one
             bb.need(mb);
             const uint16_t e = T.huf[bb.peek(mb)];
             lit[o + i] = (uint8_t)e;
@@ -118,17 +129,119 @@ __device__ __forceinline__ bool huf_lanes(const tfz::ZTables &T, const uint8_t *
     return __ballot(!ok) == 0;
 }
 
-template <bool AL>
-__device__ __forceinline__ bool seq_wave(const tfz::ZTables &T, const uint8_t *bits, int64_t n, const tfz::ZBlockDesc &d, tfz::ZRec *recs,
-                         uint32_t lane) {
+// the two-symbol table from the one-symbol table (all lanes): entry u decodes its first code;
+// the second is taken when its code lies wholly inside the index's remaining bits
+__device__ __forceinline__ void huf2_build(tfz::ZTables &T, uint32_t lane) {
+    const int mb = T.huf_bits;
+    const uint32_t mask = (1u << mb) - 1;
+    for (uint32_t u = lane; u <= mask; u += 64) {
+        const uint32_t e1 = T.huf[u], l1 = e1 >> 8;
+        uint32_t e = (e1 & 0xFFu) | l1 << 16 | l1 << 20;
+        if ((int)l1 < mb) {
+            const uint32_t e2 = T.huf[(u << l1) & mask], l2 = e2 >> 8;
+            if ((int)(l1 + l2) <= mb) e = (e1 & 0xFFu) | (e2 & 0xFFu) << 8 | l1 << 16 | (l1 + l2) << 20 | 1u << 25;
+        }
+        T.huf2[u] = e;
+    }
+}
+
+__device__ __forceinline__ uint32_t ufl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ uint64_t ufl64(uint64_t v) {
+    return (uint64_t)ufl((uint32_t)v) | ((uint64_t)ufl((uint32_t)(v >> 32)) << 32);
+}
+
+// The sequence bitstream reader of a wave decoding in lockstep: the same bits as tfz::BitR over
+// the LDS-staged block, its state held in scalar registers (every LDS value is made wave-uniform
+// with readfirstlane, so the bit arithmetic runs on the scalar unit).
+struct UBits {
+    const uint8_t *p; // LDS
+    int32_t n, pos, wlo;
+    uint64_t win;
+    __device__ __forceinline__ bool init(const uint8_t *buf, int32_t len) {
+        p = buf;
+        n = len;
+        if (len <= 0) return false;
+        const uint32_t last = ufl(buf[len - 1]);
+        if (!last) return false;
+        pos = (len - 1) * 8 + (31 - __clz((int)last));
+        refill();
+        return true;
+    }
+    __device__ __forceinline__ void refill() {
+        const int32_t b0 = ((pos + 7) >> 3) - 8;
+        wlo = b0 * 8;
+        if (b0 >= 0 && b0 + 8 <= n) { // two aligned LDS words (the stage has 16 bytes of slack)
+            typedef __attribute__((address_space(3))) const uint64_t lds_u64;
+            const uint8_t *q = p + b0;
+            const uint32_t sh = (uint32_t)((uintptr_t)q & 7) * 8;
+            lds_u64 *w = (lds_u64 *)(q - ((uintptr_t)q & 7));
+            const uint64_t lo = w[0], hi = w[1];
+            win = ufl64(sh ? (lo >> sh) | (hi << (64 - sh)) : lo);
+        } else {
+            uint64_t v = 0;
+            for (int k = 0; k < 8; ++k)
+                if (b0 + k >= 0 && b0 + k < n) v |= (uint64_t)p[b0 + k] << (8 * k);
+            win = ufl64(v);
+        }
+    }
+    __device__ __forceinline__ void need(int k) {
+        if (pos - k < wlo) refill();
+    }
+    __device__ __forceinline__ uint32_t take(int k) { // k <= 32, after need
+        if (k == 0) return 0;
+        pos -= k;
+        return (uint32_t)((win >> (pos - wlo)) & ((1ull << k) - 1));
+    }
+};
+
+struct USeq { // one decoding-table entry, wave-uniform
+    uint32_t value, base, bits, add;
+};
+__device__ __forceinline__ USeq useq(const tfz::ZSeqEntry *t, uint32_t s) {
+    typedef __attribute__((address_space(3))) const uint64_t lds_u64;
+    const uint64_t e = ufl64(*(lds_u64 *)(t + s));
+    const uint32_t hi = (uint32_t)(e >> 32);
+    return USeq{(uint32_t)e, hi & 0xFFFFu, (hi >> 16) & 0xFFu, hi >> 24};
+}
+
+// The sequences of one block (tfz::seq_decode's steps): records {ll, ml, offset value}, the
+// block's trailing literal run last; record q kept by lane q % 64, 64 stored at a time.
+__device__ __forceinline__ bool seq_wave(const tfz::ZTables &T, const uint8_t *bits, int32_t n, uint32_t nseq, uint32_t lsize,
+                                         tfz::ZRec *recs, uint32_t lane) {
     tfz::ZRec mine{0, 0, 0, 0};
-    const bool ok = tfz::seq_decode<AL>(T, bits, n, d.nseq, d.lsize, [&](uint32_t q, const tfz::ZRec &r) {
-        if ((q & 63) == lane) mine = r;
-        if ((q & 63) == 63) recs[d.rec + q - 63 + lane] = mine; // 64 records, one coalesced store
-    });
-    const uint32_t total = d.nseq + 1, part = total & 63;
-    if (ok && part && lane < part) recs[d.rec + total - part + lane] = mine;
-    return ok;
+    uint32_t lit_pos = 0;
+    if (nseq) {
+        UBits bb;
+        if (!bb.init(bits, n)) return false;
+        const int ll_log = (int)ufl((uint32_t)T.ll_log), of_log = (int)ufl((uint32_t)T.of_log),
+                  ml_log = (int)ufl((uint32_t)T.ml_log);
+        bb.need(ll_log + of_log + ml_log);
+        uint32_t sll = bb.take(ll_log), sof = bb.take(of_log), sml = bb.take(ml_log);
+        for (uint32_t q = 0; q < nseq; ++q) {
+            const USeq el = useq(T.ll, sll), eo = useq(T.of, sof), em = useq(T.ml, sml);
+            bb.need((int)eo.add);
+            const uint32_t ofv = eo.value + bb.take((int)eo.add);
+            bb.need(32);
+            const uint32_t ml = em.value + bb.take((int)em.add);
+            const uint32_t ll = el.value + bb.take((int)el.add);
+            if (q + 1 < nseq) { // state updates: LL, ML, OF
+                bb.need(26);
+                sll = el.base + bb.take((int)el.bits);
+                sml = em.base + bb.take((int)em.bits);
+                sof = eo.base + bb.take((int)eo.bits);
+            }
+            if (bb.pos < 0 || lit_pos + ll > lsize) return false;
+            if ((q & 63) == lane) mine = tfz::ZRec{ll, ml, ofv, 0};
+            if ((q & 63) == 63) recs[q - 63 + lane] = mine; // 64 records, one coalesced store
+            lit_pos += ll;
+        }
+        if (bb.pos != 0) return false;
+    }
+    if ((nseq & 63) == lane) mine = tfz::ZRec{lsize - lit_pos, 0, tfz::ZDIRECT, 0};
+    const uint32_t total = nseq + 1, part = total & 63;
+    if (part == 0) recs[nseq - 63 + lane] = mine;
+    else if (lane < part) recs[total - part + lane] = mine;
+    return true;
 }
 
 // One workgroup (2 waves) per block; LDS = ZTables + the staged block (dynamic, stage_cap bytes + 16).
@@ -153,8 +266,8 @@ __global__ void __launch_bounds__(128) zstd_block_kernel(const uint8_t *pkt, con
         }
         return;
     }
-    const bool staged = d.size <= stage_cap;
-    if (staged) { // the block's bytes into LDS, 16 loads in flight a thread; 16 zero bytes of slack
+    { // the block's bytes into LDS (stage_cap >= every compressed block of the launch), 16 loads
+      // in flight a thread; 16 zero bytes of slack
         for (uint32_t i0 = tid * 16; i0 < d.size + 16; i0 += 128 * 16) {
             uint8_t v[16];
 #pragma unroll
@@ -176,9 +289,10 @@ __global__ void __launch_bounds__(128) zstd_block_kernel(const uint8_t *pkt, con
         } else {
             ok = tfz::huf_read(body + d.huf, d.huf_n, T, lane, 64) >= 0;
             lds_order();
+            if (ok) huf2_build(T, lane);
+            lds_order();
             if (ok) {
-                if (staged) ok = huf_lanes<true>(T, stage + (d.lit_at - d.src), d.lbytes, d.lsize, d.streams, lit, lane);
-                else ok = huf_lanes<false>(T, body + d.lit_at, d.lbytes, d.lsize, d.streams, lit, lane);
+                ok = huf_lanes<true>(T, stage + (d.lit_at - d.src), d.lbytes, d.lsize, d.streams, lit, lane);
             }
         }
     } else { // ---- sequences
@@ -190,8 +304,8 @@ __global__ void __launch_bounds__(128) zstd_block_kernel(const uint8_t *pkt, con
             ok = __ballot(lane == 0 && !built) == 0;
         }
         if (ok) {
-            if (staged) ok = seq_wave<true>(T, stage + (d.seq_at - d.src), d.seq_n, d, recs, lane);
-            else ok = seq_wave<false>(T, body + d.seq_at, d.seq_n, d, recs, lane);
+            ok = seq_wave(T, stage + (ufl(d.seq_at) - ufl(d.src)), (int32_t)ufl(d.seq_n), ufl(d.nseq), ufl(d.lsize),
+                          recs + ufl(d.rec), lane);
         }
     }
     if (lane == 0 && !ok) atomicOr(err, 1u);

@@ -65,6 +65,9 @@ struct ZTables {
     int ll_log, of_log, ml_log;
     uint16_t huf[1 << ZHUF_MAXBITS];     // symbol | nbBits << 8
     int huf_bits;
+    // device: two symbols per lookup where both codes fit the index (huf2_build):
+    // sym1 | sym2 << 8 | len1 << 16 | (len1 + len2) << 20 | two << 25
+    uint32_t huf2[1 << ZHUF_MAXBITS];
 };
 
 // One block (scan output).  Offsets are into the packet frame's ZSTD body.
