@@ -8,8 +8,8 @@
 //                                 staged in LDS; wave 0 decodes the literals (the four Huffman
 //                                 streams on lanes 0-3), wave 1 the sequences (FSE, lockstep,
 //                                 records flushed 64 at a time) — the two halves are independent
-//   resolve  zstd_resolve_kernel  one wave per packet frame: repeat offsets and positions by wave
-//                                 scans (the repeat-offset updates compose), every check
+//   resolve  zstd_resolve_kernel  one 1024-thread workgroup per packet frame: repeat offsets and
+//                                 positions by scans (the repeat-offset updates compose), every check
 //   execute  zstd_expand_kernel   every output byte: literal bytes copied, match bytes get their
 //                                 source index and join a list; zstd_jump_kernel (src = src[src]
 //                                 over the list, the still-unresolved bytes forming the next list:
@@ -87,6 +87,46 @@ __global__ void __launch_bounds__(64) zstd_scan_kernel(const uint8_t *pkt, const
 }
 
 // ---------------------------------------------------------------- entropy
+// A lane's backward bitstream over the LDS-staged block (tfz::BitR's bits, 32-bit positions: a
+// block is at most 128 KB).  `win` holds stream bits [wlo, wlo + 64); after a refill at least 57
+// bits can be read.
+struct LBits {
+    const uint8_t *p; // LDS, 16 bytes of slack past the block
+    int32_t n, pos, wlo;
+    uint64_t win;
+    __device__ __forceinline__ bool init(const uint8_t *buf, int32_t len) {
+        p = buf;
+        n = len;
+        const uint32_t last = len > 0 ? buf[len - 1] : 0u;
+        pos = last ? (len - 1) * 8 + (31 - __clz((int)last)) : 0;
+        wlo = pos;
+        win = 0;
+        if (!last) return false;
+        refill();
+        return true;
+    }
+    __device__ __forceinline__ void refill() {
+        const int32_t b0 = ((pos + 7) >> 3) - 8;
+        wlo = b0 * 8;
+        if (b0 >= 0 && b0 + 8 <= n) {
+            typedef __attribute__((address_space(3))) const uint64_t lds_u64;
+            const uint8_t *q = p + b0;
+            const uint32_t sh = (uint32_t)((uintptr_t)q & 7) * 8;
+            lds_u64 *w = (lds_u64 *)(q - ((uintptr_t)q & 7));
+            const uint64_t lo = w[0], hi = w[1];
+            win = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+        } else {
+            uint64_t v = 0;
+            for (int k = 0; k < 8; ++k)
+                if (b0 + k >= 0 && b0 + k < n) v |= (uint64_t)p[b0 + k] << (8 * k);
+            win = v;
+        }
+    }
+    __device__ __forceinline__ uint32_t peek(int k) const { // 1 <= k <= 57
+        return (uint32_t)((win >> (pos - k - wlo)) & ((1ull << k) - 1));
+    }
+};
+
 // The four-lane Huffman decode of a block's literals: lane k < ns decodes stream k.
 template <bool AL>
 __device__ __forceinline__ bool huf_lanes(const tfz::ZTables &T, const uint8_t *ls, int64_t lbytes, uint32_t lsize, int ns, uint8_t *lit,
@@ -103,12 +143,14 @@ __device__ __forceinline__ bool huf_lanes(const tfz::ZTables &T, const uint8_t *
     }
     bool ok = true;
     if (lane < (uint32_t)ns) {
-        tfz::BitR<AL> bb;
-        ok = bb.init(ls + at, len);
+        LBits bb;
+        ok = bb.init(ls + at, (int32_t)len);
         const int mb = T.huf_bits;
         int64_t i = 0;
         for (; ok && i + 1 < cnt;) { // two symbols a lookup while two remain
-            bb.need(mb);
+            // the lanes refill together when one needs it: one refill every few lookups instead
+            // of a masked refill in most iterations (the four streams consume at different rates)
+            if (__ballot(bb.pos - mb < bb.wlo)) bb.refill();
             const uint32_t e = T.huf2[bb.peek(mb)];
             const bool two = (e >> 25) & 1u;
             lit[o + i] = (uint8_t)e;
@@ -118,7 +160,7 @@ __device__ __forceinline__ bool huf_lanes(const tfz::ZTables &T, const uint8_t *
             ok = bb.pos >= 0;
         }
         if (ok && i < cnt) { // the last one
-            bb.need(mb);
+            if (bb.pos - mb < bb.wlo) bb.refill();
             const uint16_t e = T.huf[bb.peek(mb)];
             lit[o + i] = (uint8_t)e;
             bb.pos -= e >> 8;
@@ -357,126 +399,183 @@ __device__ __forceinline__ RepMap rep_shfl_up(const RepMap &m, int d) {
     return o;
 }
 
-// One wave per packet frame, records 64 at a time (the next batch loaded while this one is
-// resolved): scans give positions and repeat-offset maps; records are rewritten as
-// {pos, ll, lpos, off}.
-__global__ void __launch_bounds__(64) zstd_resolve_kernel(const uint64_t *roff, uint64_t f0, const uint32_t *bases,
-                                                          tfz::ZFrameDesc *frames, tfz::ZRec *recs, unsigned *err) {
-    const uint32_t i = blockIdx.x, lane = threadIdx.x;
+// this record's map and its offset's expression: slot ekind of the state before it, plus eval
+// (ekind 3: the constant eval)
+__device__ __forceinline__ RepMap rec_map(uint32_t of, uint32_t ll, uint32_t &ekind, uint32_t &eval) {
+    ekind = 3;
+    eval = of & ~tfz::ZDIRECT;
+    if (of & tfz::ZDIRECT) return rep_identity();
+    if (of > 3) {
+        eval = of - 3;
+        return RepMap{3u | 0u << 2 | 1u << 4, {of - 3, 0, 0}};
+    }
+    const uint32_t idx = of - 1 + (ll == 0 ? 1u : 0u);
+    eval = idx == 3 ? 0xFFFFFFFFu : 0u;
+    ekind = idx == 3 ? 0u : idx;
+    if (idx == 1) return RepMap{1u | 0u << 2 | 2u << 4, {0, 0, 0}};
+    if (idx == 2) return RepMap{2u | 0u << 2 | 1u << 4, {0, 0, 0}};
+    if (idx == 3) return RepMap{0u | 0u << 2 | 1u << 4, {0xFFFFFFFFu, 0, 0}};
+    return rep_identity();
+}
+
+// One 1024-thread workgroup per packet frame, 1024 records a step (the next step's loaded while
+// this one is resolved): every wave scans its 64 records (repeat-offset maps, output and literal
+// positions), wave 0 scans the 16 wave totals, and every record gets its offset and positions
+// from the step's carry.  Records are rewritten as {pos, ll, lpos, off}.
+constexpr int RS_T = 1024;
+__global__ void __launch_bounds__(RS_T) zstd_resolve_kernel(const uint64_t *roff, uint64_t f0, const uint32_t *bases,
+                                                            tfz::ZFrameDesc *frames, tfz::ZRec *recs, unsigned *err) {
+    constexpr int NW = RS_T / 64;
+    __shared__ RepMap s_map[NW];      // wave totals, then the waves' exclusive prefixes
+    __shared__ uint32_t s_sp[NW], s_ll[NW];
+    __shared__ uint32_t s_carry[5];   // pos, lpos, r0, r1, r2 before the step
+    __shared__ uint32_t s_next[5];    // ... after it
+    __shared__ int s_bad;
+    const uint32_t i = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t f = f0 + i, raw = roff[f + 1] - roff[f];
-    uint32_t pos = 0, lpos = (uint32_t)(roff[f] - roff[f0]);
-    bool bad = false;
-    for (uint32_t z = bases[4 * i + 1]; z < bases[4 * i + 5] && !bad; ++z) {
+    if (tid == 0) {
+        s_carry[0] = 0;
+        s_carry[1] = (uint32_t)(roff[f] - roff[f0]);
+        s_bad = 0;
+    }
+    __syncthreads();
+    for (uint32_t z = bases[4 * i + 1]; z < bases[4 * i + 5]; ++z) {
         const tfz::ZFrameDesc fr = frames[z];
-        const uint32_t zstart = pos;
-        uint32_t r0 = 1, r1 = 4, r2 = 8;
+        const uint32_t zstart = s_carry[0];
+        __syncthreads();
+        if (tid == 0) { // every ZSTD frame starts from the initial repeat offsets
+            s_carry[2] = 1;
+            s_carry[3] = 4;
+            s_carry[4] = 8;
+        }
         tfz::ZRec nxt{0, 0, tfz::ZDIRECT, 0};
-        if (fr.rec0 + lane < fr.rec1) nxt = recs[fr.rec0 + lane];
-        for (uint32_t q0 = fr.rec0; q0 < fr.rec1; q0 += 64) {
+        if (fr.rec0 + tid < fr.rec1) nxt = recs[fr.rec0 + tid];
+        __syncthreads();
+        for (uint32_t q0 = fr.rec0; q0 < fr.rec1; q0 += RS_T) {
             const tfz::ZRec r = nxt;
-            const uint32_t cnt = fr.rec1 - q0 < 64 ? fr.rec1 - q0 : 64;
             nxt = tfz::ZRec{0, 0, tfz::ZDIRECT, 0};
-            if (q0 + 64 + lane < fr.rec1) nxt = recs[q0 + 64 + lane];
-            const bool valid = lane < cnt;
+            if (q0 + RS_T + tid < fr.rec1) nxt = recs[q0 + RS_T + tid];
+            const bool valid = q0 + tid < fr.rec1;
             const uint32_t ll = valid ? r.a : 0, ml = valid ? r.b : 0, of = valid ? r.c : tfz::ZDIRECT;
-            // this record's map and its offset's expression (a map slot over the state before it)
-            RepMap m = rep_identity();
-            uint32_t ekind = 3, eval = of & ~tfz::ZDIRECT; // the offset: slot ekind + eval, or eval
-            if (!(of & tfz::ZDIRECT)) {
-                if (of > 3) {
-                    m = RepMap{3u | 0u << 2 | 1u << 4, {of - 3, 0, 0}};
-                    eval = of - 3;
-                } else {
-                    const uint32_t idx = of - 1 + (ll == 0 ? 1u : 0u);
-                    if (idx == 0) {
-                        ekind = 0;
-                        eval = 0;
-                    } else if (idx == 1) {
-                        m = RepMap{1u | 0u << 2 | 2u << 4, {0, 0, 0}};
-                        ekind = 1;
-                        eval = 0;
-                    } else if (idx == 2) {
-                        m = RepMap{2u | 0u << 2 | 1u << 4, {0, 0, 0}};
-                        ekind = 2;
-                        eval = 0;
-                    } else {
-                        m = RepMap{0u | 0u << 2 | 1u << 4, {0xFFFFFFFFu, 0, 0}};
-                        ekind = 0;
-                        eval = 0xFFFFFFFFu;
-                    }
-                }
-            }
-            // inclusive scan of the maps, then the exclusive one (the state before each record)
-            RepMap inc = m;
+            uint32_t ekind, eval;
+            RepMap inc = rec_map(of, ll, ekind, eval);
+            uint32_t incl = ll + ml, linc = ll; // spans: a step covers at most 1024 x 128 KB + 128 KB
 #pragma unroll
             for (int d = 1; d < 64; d <<= 1) {
                 const RepMap y = rep_shfl_up(inc, d);
-                if (lane >= (uint32_t)d) inc = rep_compose(y, inc);
-            }
-            RepMap exc = rep_shfl_up(inc, 1);
-            if (lane == 0) exc = rep_identity();
-            const uint32_t s0 = rep_slot(exc, 0, r0, r1, r2), s1 = rep_slot(exc, 1, r0, r1, r2),
-                           s2 = rep_slot(exc, 2, r0, r1, r2);
-            const uint32_t myoff = ekind == 3 ? eval : (ekind == 0 ? s0 : ekind == 1 ? s1 : s2) + eval;
-            // positions
-            uint64_t span = (uint64_t)ll + ml, incl = span;
-            uint32_t linc = ll;
-#pragma unroll
-            for (int k = 1; k < 64; k <<= 1) {
-                const uint64_t y = __shfl_up(incl, k, 64);
-                const uint32_t w = __shfl_up(linc, k, 64);
-                if (lane >= (uint32_t)k) {
-                    incl += y;
-                    linc += w;
+                const uint32_t yp = __shfl_up(incl, d, 64), yl = __shfl_up(linc, d, 64);
+                if (lane >= (uint32_t)d) {
+                    inc = rep_compose(y, inc);
+                    incl += yp;
+                    linc += yl;
                 }
             }
-            const uint64_t mypos = pos + incl - span;
-            const uint32_t mylpos = lpos + linc - ll;
-            if (valid) {
-                if (ml && (myoff == 0 || (uint64_t)myoff > mypos + ll - zstart)) bad = true;
-                if (mypos + span > raw) bad = true;
-                recs[q0 + lane] = tfz::ZRec{(uint32_t)mypos, ll, mylpos, myoff};
+            if (lane == 63) {
+                s_map[wave] = inc;
+                s_sp[wave] = incl;
+                s_ll[wave] = linc;
             }
-            // the batch's outgoing state: the last lane's inclusive map (lanes past cnt: identity)
-            const RepMap last = RepMap{(uint32_t)__shfl(inc.kinds, 63, 64),
-                                       {(uint32_t)__shfl(inc.v[0], 63, 64), (uint32_t)__shfl(inc.v[1], 63, 64),
-                                        (uint32_t)__shfl(inc.v[2], 63, 64)}};
-            const uint32_t n0 = rep_slot(last, 0, r0, r1, r2), n1 = rep_slot(last, 1, r0, r1, r2),
-                           n2 = rep_slot(last, 2, r0, r1, r2);
-            r0 = n0;
-            r1 = n1;
-            r2 = n2;
-            const uint64_t tot = __shfl(incl, 63, 64);
-            const uint32_t ltot = __shfl(linc, 63, 64);
-            bad = __ballot(bad) != 0;
-            if (bad || pos + tot > raw) {
-                bad = true;
-                break;
+            __syncthreads();
+            if (wave == 0) { // exclusive scan of the wave totals (lanes < NW), and the step's carry out
+                RepMap m = lane < NW ? s_map[lane] : rep_identity();
+                uint32_t sp = lane < NW ? s_sp[lane] : 0u, sl = lane < NW ? s_ll[lane] : 0u;
+#pragma unroll
+                for (int d = 1; d < NW; d <<= 1) {
+                    const RepMap y = rep_shfl_up(m, d);
+                    const uint32_t yp = __shfl_up(sp, d, 64), yl = __shfl_up(sl, d, 64);
+                    if (lane >= (uint32_t)d) {
+                        m = rep_compose(y, m);
+                        sp += yp;
+                        sl += yl;
+                    }
+                }
+                RepMap e = rep_shfl_up(m, 1);
+                const uint32_t ep = __shfl_up(sp, 1, 64), el = __shfl_up(sl, 1, 64);
+                if (lane < NW) {
+                    s_map[lane] = lane == 0 ? rep_identity() : e;
+                    s_sp[lane] = lane == 0 ? 0u : ep;
+                    s_ll[lane] = lane == 0 ? 0u : el;
+                }
+                if (lane == NW - 1) {
+                    const uint32_t c2 = s_carry[2], c3 = s_carry[3], c4 = s_carry[4];
+                    const uint64_t np = (uint64_t)s_carry[0] + sp;
+                    if (np > raw) s_bad = 1;
+                    s_next[0] = (uint32_t)np;
+                    s_next[1] = s_carry[1] + sl;
+                    s_next[2] = rep_slot(m, 0, c2, c3, c4);
+                    s_next[3] = rep_slot(m, 1, c2, c3, c4);
+                    s_next[4] = rep_slot(m, 2, c2, c3, c4);
+                }
             }
-            pos += (uint32_t)tot;
-            lpos += ltot;
+            __syncthreads();
+            { // this wave's incoming state, then each record's
+                const RepMap pw = s_map[wave];
+                const uint32_t c2 = s_carry[2], c3 = s_carry[3], c4 = s_carry[4];
+                const uint32_t w0 = rep_slot(pw, 0, c2, c3, c4), w1 = rep_slot(pw, 1, c2, c3, c4), w2 = rep_slot(pw, 2, c2, c3, c4);
+                RepMap exc = rep_shfl_up(inc, 1);
+                if (lane == 0) exc = rep_identity();
+                const uint32_t s0 = rep_slot(exc, 0, w0, w1, w2), s1 = rep_slot(exc, 1, w0, w1, w2),
+                               s2 = rep_slot(exc, 2, w0, w1, w2);
+                const uint32_t myoff = ekind == 3 ? eval : (ekind == 0 ? s0 : ekind == 1 ? s1 : s2) + eval;
+                const uint64_t mypos = (uint64_t)s_carry[0] + s_sp[wave] + incl - (ll + ml);
+                const uint32_t mylpos = s_carry[1] + s_ll[wave] + linc - ll;
+                if (valid) {
+                    bool bad = false;
+                    if (ml && (myoff == 0 || (uint64_t)myoff > mypos + ll - zstart)) bad = true;
+                    if (mypos + ll + ml > raw) bad = true;
+                    if (bad) s_bad = 1;
+                    recs[q0 + tid] = tfz::ZRec{(uint32_t)mypos, ll, mylpos, myoff};
+                }
+            }
+            __syncthreads();
+            if (tid < 5) s_carry[tid] = s_next[tid];
+            __syncthreads();
+            if (s_bad) break;
         }
-        if (lane == 0) {
+        if (tid == 0) {
             frames[z].out0 = zstart;
-            frames[z].out1 = pos;
+            frames[z].out1 = s_carry[0];
+            if (fr.fcs != ~0ull && (uint64_t)(s_carry[0] - zstart) != fr.fcs) s_bad = 1;
         }
-        if (fr.fcs != ~0ull && (uint64_t)(pos - zstart) != fr.fcs) bad = true;
+        __syncthreads();
+        if (s_bad) break;
     }
-    if (pos != raw) bad = true;
-    if (lane == 0 && bad) atomicOr(err, 1u);
+    if (tid == 0 && (s_bad || s_carry[0] != raw)) atomicOr(err, 1u);
 }
 
 // ---------------------------------------------------------------- execute
-// Worklists of byte indices (launch-relative): count + entries.  Appends are wave-aggregated.
-__device__ __forceinline__ void wl_append(bool want, uint32_t g, uint32_t *list, unsigned *count) {
-    const uint64_t m = __ballot(want);
-    if (!m) return;
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t leader = (uint32_t)__builtin_ctzll(m);
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(count, (unsigned)__popcll(m));
-    base = __shfl(base, (int)leader, 64);
-    if (want) list[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = g;
+// Worklists of byte indices (launch-relative): count + entries.  A block appends its threads'
+// entries contiguously with ONE global atomic (per-wave atomics on one counter serialise: a
+// first round of 25M entries spent 4.6 ms in them).  Every thread of the block calls it;
+// entry k of a thread is vals[k] when bit k of mask is set.  s_w: (blockDim / 64 + 1) words.
+template <int K>
+__device__ __forceinline__ void block_append(uint32_t mask, const uint32_t (&vals)[K], uint32_t *list, unsigned *count,
+                                             uint32_t *s_w) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const uint32_t cnt = (uint32_t)__popc(mask);
+    uint32_t x = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= (uint32_t)d) x += y;
+    }
+    if (lane == 63) s_w[wave] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+        for (uint32_t w = 0; w < nw; ++w) {
+            const uint32_t v = s_w[w];
+            s_w[w] = tot;
+            tot += v;
+        }
+        s_w[nw] = tot ? atomicAdd(count, tot) : 0u;
+    }
+    __syncthreads();
+    uint32_t pos = s_w[nw] + s_w[wave] + x - cnt;
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        if (mask & (1u << k)) list[pos++] = vals[k];
+    __syncthreads(); // s_w is reused by the next call
 }
 
 // One workgroup per ZCHUNK output bytes of a packet frame (cbase: prefix of the frames' chunk
@@ -549,45 +648,43 @@ __global__ void __launch_bounds__(256) zstd_expand_kernel(const uint64_t *roff, 
         for (int k = 0; k < 16; ++k)
             if (s + k < e) src[g0 + s + k] = sv[k];
     }
-    // the match bytes into the list: a wave scan of the per-thread counts, one atomic per wave
-    const uint32_t lane = threadIdx.x & 63, cnt = (uint32_t)__popc(mmask);
-    uint32_t x = cnt;
+    // the match bytes into the list: one atomic per workgroup
+    __shared__ uint32_t s_w[256 / 64 + 1];
+    uint32_t gv[16];
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d, 64);
-        if (lane >= (uint32_t)d) x += y;
-    }
-    const uint32_t total = __shfl(x, 63, 64);
-    uint32_t base = 0;
-    if (lane == 63 && total) base = atomicAdd(mcount, total);
-    base = __shfl(base, 63, 64) + x - cnt;
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-        if (mmask & (1u << k)) mlist[base++] = (uint32_t)(g0 + s + k);
+    for (int k = 0; k < 16; ++k) gv[k] = (uint32_t)(g0 + s + k);
+    block_append<16>(mmask, gv, mlist, mcount, s_w);
     if (bad) atomicOr(err, 1u);
 }
 
 // One pointer-jumping round over the bytes of list `in` (count *nin): src[g] = src[src[g]]; the
-// bytes whose source is still not a literal go to list `out`.  Grid-stride over the count read
-// on the device, so rounds are launched without a host read between them.
+// bytes whose source is still not a literal go to list `out`.  Tiles of 4096 entries (16 a
+// thread, all their loads in flight together), grid-stride over the count read on the device,
+// so rounds are launched without a host read between them.
 __global__ void __launch_bounds__(256) zstd_jump_kernel(uint32_t *src, const uint32_t *in, const unsigned *nin,
                                                         uint32_t *outl, unsigned *nout) {
+    __shared__ uint32_t s_w[256 / 64 + 1];
     const uint32_t n = *nin;
-    const uint32_t stride = gridDim.x * 256;
-    for (uint32_t i0 = blockIdx.x * 256; i0 < n; i0 += stride) {
-        const uint32_t i = i0 + threadIdx.x;
-        bool more = false;
-        uint32_t g = 0;
-        if (i < n) {
-            g = in[i];
-            const uint32_t s = src[g];
-            const uint32_t t = src[s];
-            if (t != s) {
-                src[g] = t;
-                more = src[t] != t;
+    for (uint32_t t0 = blockIdx.x * 4096u; t0 < n; t0 += gridDim.x * 4096u) {
+        uint32_t g[16], sv[16];
+        uint32_t mask = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint32_t i = t0 + (uint32_t)k * 256 + threadIdx.x;
+            g[k] = i < n ? in[i] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) sv[k] = t0 + (uint32_t)k * 256 + threadIdx.x < n ? src[g[k]] : 0u;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            if (t0 + (uint32_t)k * 256 + threadIdx.x >= n) continue;
+            const uint32_t t = src[sv[k]];
+            if (t != sv[k]) {
+                src[g[k]] = t;
+                if (src[t] != t) mask |= 1u << k;
             }
         }
-        wl_append(more, g, outl, nout);
+        block_append<16>(mask, g, outl, nout, s_w);
     }
 }
 
@@ -776,7 +873,7 @@ int zstd_decode_frames(Ctx *ctx, const uint8_t *packet, uint64_t nf, const uint6
                                    (const tfz::ZBlockDesc *)blk, lit, rec, cap, err);
                 TFG_LAUNCH_CHECK();
             }
-            hipLaunchKernelGGL(zstd_resolve_kernel, dim3((unsigned)g), dim3(64), 0, ctx->stream, dro, a,
+            hipLaunchKernelGGL(zstd_resolve_kernel, dim3((unsigned)g), dim3(RS_T), 0, ctx->stream, dro, a,
                                (const uint32_t *)dbases, frm, rec, err);
             TFG_LAUNCH_CHECK();
             if (nc) {
@@ -788,7 +885,8 @@ int zstd_decode_frames(Ctx *ctx, const uint8_t *packet, uint64_t nf, const uint6
         }
         // pointer jumping over the match bytes: rounds go in batches of 4 without a host read
         // between them (an empty list costs one launch); the batch's last list count decides
-        const unsigned jg = (unsigned)std::min<uint64_t>((raw + 255) / 256, 16384);
+        const unsigned jg = (unsigned)std::min<uint64_t>((raw + 4095) / 4096, 2048); // jump tiles of 4096
+        const unsigned gg = (unsigned)std::min<uint64_t>((raw + 255) / 256, 16384);
         if (raw) {
             const uint32_t *in = mlist;
             const unsigned *nin = lcount;
@@ -810,7 +908,7 @@ int zstd_decode_frames(Ctx *ctx, const uint8_t *packet, uint64_t nf, const uint6
                 more = *(const unsigned *)ctx->host_pinned != 0;
             }
             ProfScope _ps(ctx, "codec.zstd.decompress");
-            hipLaunchKernelGGL(zstd_gather_kernel, dim3(jg), dim3(256), 0, ctx->stream, (const uint32_t *)src,
+            hipLaunchKernelGGL(zstd_gather_kernel, dim3(gg), dim3(256), 0, ctx->stream, (const uint32_t *)src,
                                (const uint32_t *)mlist, (const unsigned *)lcount, out);
             TFG_LAUNCH_CHECK();
         }
