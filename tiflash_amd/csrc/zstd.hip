@@ -869,6 +869,9 @@ int zstd_decode_frames(Ctx *ctx, const uint8_t *packet, uint64_t nf, const uint6
             if (nb) {
                 const uint32_t cap = (max_comp + 15) & ~15u;
                 const size_t lds = ((sizeof(tfz::ZTables) + 15) & ~size_t(15)) + cap + 16;
+                // <= 22.5 KB of tables + a 128 KB block + slack: within gfx950's 160 KB of LDS (one or
+                // two workgroups per CU, by the launch's largest compressed block)
+                TFG_CHECK(lds <= 160 * 1024, TFG_ERR_LOGICAL, "ZSTD block stage of %zu bytes", lds);
                 hipLaunchKernelGGL(zstd_block_kernel, dim3(nb), dim3(128), lds, ctx->stream, packet, dfo, a,
                                    (const tfz::ZBlockDesc *)blk, lit, rec, cap, err);
                 TFG_LAUNCH_CHECK();
