@@ -87,6 +87,23 @@ __global__ void __launch_bounds__(64) zstd_scan_kernel(const uint8_t *pkt, const
 }
 
 // ---------------------------------------------------------------- entropy
+// The tables of one block in LDS (~18.7 KB, so that two blocks of up to ~60 KB share a CU): the
+// sequence tables and a two-symbol Huffman table built from the weights (sym1 | sym2 << 8 |
+// len1 << 16 | (len1 + len2) << 20 | two << 25), with the symbols sorted by weight class.
+struct ZBlockLds : tfz::ZSeqTables {
+    uint32_t huf2[1 << tfz::ZHUF_MAXBITS];
+    int huf_bits;
+    uint16_t cstart[tfz::ZHUF_MAXBITS + 2], cbase[tfz::ZHUF_MAXBITS + 2]; // class k: first entry, first sorted symbol
+    uint8_t syms[256];                                                      // symbols by (weight, symbol)
+    // work space of the table builds (private arrays would live in scratch memory, ~1 us a
+    // dependent access): the literal wave's Huffman weights, the sequence wave's FSE builds
+    uint8_t weight[256];
+    tfz::FseEntry hft[64];
+    int16_t hnorm[16];
+    uint16_t hnext[256];
+    int16_t snorm[53];
+    uint16_t snext[256];
+};
 // A lane's backward bitstream over the LDS-staged block (tfz::BitR's bits, 32-bit positions: a
 // block is at most 128 KB).  `win` holds stream bits [wlo, wlo + 64); after a refill at least 57
 // bits can be read.
@@ -129,7 +146,7 @@ struct LBits {
 
 // The four-lane Huffman decode of a block's literals: lane k < ns decodes stream k.
 template <bool AL>
-__device__ __forceinline__ bool huf_lanes(const tfz::ZTables &T, const uint8_t *ls, int64_t lbytes, uint32_t lsize, int ns, uint8_t *lit,
+__device__ __forceinline__ bool huf_lanes(const ZBlockLds &T, const uint8_t *ls, int64_t lbytes, uint32_t lsize, int ns, uint8_t *lit,
                           uint32_t lane) {
     int64_t at = 0, len = lbytes, cnt = lsize, o = 0;
     if (ns == 4) {
@@ -159,11 +176,11 @@ __device__ __forceinline__ bool huf_lanes(const tfz::ZTables &T, const uint8_t *
             i += two ? 2 : 1;
             ok = bb.pos >= 0;
         }
-        if (ok && i < cnt) { // the last one
+        if (ok && i < cnt) { // the last one: the entry's first symbol
             if (bb.pos - mb < bb.wlo) bb.refill();
-            const uint16_t e = T.huf[bb.peek(mb)];
+            const uint32_t e = T.huf2[bb.peek(mb)];
             lit[o + i] = (uint8_t)e;
-            bb.pos -= e >> 8;
+            bb.pos -= (e >> 16) & 15u;
             ok = bb.pos >= 0;
         }
         ok = ok && bb.pos == 0;
@@ -171,20 +188,70 @@ __device__ __forceinline__ bool huf_lanes(const tfz::ZTables &T, const uint8_t *
     return __ballot(!ok) == 0;
 }
 
-// the two-symbol table from the one-symbol table (all lanes): entry u decodes its first code;
-// the second is taken when its code lies wholly inside the index's remaining bits
-__device__ __forceinline__ void huf2_build(tfz::ZTables &T, uint32_t lane) {
-    const int mb = T.huf_bits;
+// The Huffman table of a block from its tree description (all lanes of the wave): the weights
+// (every lane, in lockstep), the symbols sorted by weight class (lane 0), then the two-symbol
+// entries split over the lanes: entry u decodes its first code from the weight classes, and
+// the second when its code lies wholly inside the index's remaining bits.
+__device__ __forceinline__ bool huf2_read(const uint8_t *src, int64_t n, ZBlockLds &T, uint32_t lane) {
+    int nw = 0, mb = 0;
+    if (tfz::huf_weights(src, n, T.weight, nw, mb, T.hft, T.hnorm, T.hnext) < 0) return false;
+    lds_order();
+    // classes by ballots over the weights (64 symbols at a time): counts, starts, sorted symbols
+    uint32_t run[tfz::ZHUF_MAXBITS + 2] = {}; // symbols of class k placed so far (wave-uniform)
+    uint32_t cnt[tfz::ZHUF_MAXBITS + 2] = {};
+    for (int i0 = 0; i0 < nw; i0 += 64) {
+        const int i = i0 + (int)lane;
+        const uint32_t w = i < nw ? T.weight[i] : 0u;
+#pragma unroll
+        for (int k = 1; k <= tfz::ZHUF_MAXBITS; ++k) cnt[k] += (uint32_t)__popcll(__ballot(w == (uint32_t)k));
+    }
+    uint32_t acc = 0, sacc = 0;
+#pragma unroll
+    for (int k = 1; k <= tfz::ZHUF_MAXBITS + 1; ++k) {
+        const bool in = k <= mb;
+        if (lane == 0) {
+            T.cstart[k] = (uint16_t)(in ? acc : (1u << mb));
+            T.cbase[k] = (uint16_t)sacc;
+        }
+        run[k] = sacc;
+        if (in) {
+            acc += cnt[k] << (k - 1);
+            sacc += cnt[k];
+        }
+    }
+    if (acc != (1u << mb)) return false;
+    for (int i0 = 0; i0 < nw; i0 += 64) {
+        const int i = i0 + (int)lane;
+        const uint32_t w = i < nw ? T.weight[i] : 0u;
+        const uint64_t below = (1ull << lane) - 1;
+#pragma unroll
+        for (int k = 1; k <= tfz::ZHUF_MAXBITS; ++k) {
+            const uint64_t m = __ballot(w == (uint32_t)k);
+            if (w == (uint32_t)k) T.syms[run[k] + (uint32_t)__popcll(m & below)] = (uint8_t)i;
+            run[k] += (uint32_t)__popcll(m);
+        }
+    }
+    if (lane == 0) T.huf_bits = mb;
+    lds_order();
     const uint32_t mask = (1u << mb) - 1;
+    auto first = [&](uint32_t u, uint32_t &len) -> uint32_t { // the code at the top of index u
+        int k = 1;
+        while (k < mb && T.cstart[k + 1] <= u) ++k;
+        len = (uint32_t)(mb + 1 - k);
+        return T.syms[T.cbase[k] + ((u - T.cstart[k]) >> (k - 1))];
+    };
     for (uint32_t u = lane; u <= mask; u += 64) {
-        const uint32_t e1 = T.huf[u], l1 = e1 >> 8;
-        uint32_t e = (e1 & 0xFFu) | l1 << 16 | l1 << 20;
+        uint32_t l1, l2;
+        const uint32_t s1 = first(u, l1);
+        uint32_t e = s1 | l1 << 16 | l1 << 20;
         if ((int)l1 < mb) {
-            const uint32_t e2 = T.huf[(u << l1) & mask], l2 = e2 >> 8;
-            if ((int)(l1 + l2) <= mb) e = (e1 & 0xFFu) | (e2 & 0xFFu) << 8 | l1 << 16 | (l1 + l2) << 20 | 1u << 25;
+            const uint32_t s2 = first((u << l1) & mask, l2);
+            if ((int)(l1 + l2) <= mb) e = s1 | s2 << 8 | l1 << 16 | (l1 + l2) << 20 | 1u << 25;
         }
         T.huf2[u] = e;
     }
+    lds_order();
+    return true;
 }
 
 __device__ __forceinline__ uint32_t ufl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
@@ -248,7 +315,7 @@ __device__ __forceinline__ USeq useq(const tfz::ZSeqEntry *t, uint32_t s) {
 
 // The sequences of one block (tfz::seq_decode's steps): records {ll, ml, offset value}, the
 // block's trailing literal run last; record q kept by lane q % 64, 64 stored at a time.
-__device__ __forceinline__ bool seq_wave(const tfz::ZTables &T, const uint8_t *bits, int32_t n, uint32_t nseq, uint32_t lsize,
+__device__ __forceinline__ bool seq_wave(const ZBlockLds &T, const uint8_t *bits, int32_t n, uint32_t nseq, uint32_t lsize,
                                          tfz::ZRec *recs, uint32_t lane) {
     tfz::ZRec mine{0, 0, 0, 0};
     uint32_t lit_pos = 0;
@@ -286,13 +353,13 @@ __device__ __forceinline__ bool seq_wave(const tfz::ZTables &T, const uint8_t *b
     return true;
 }
 
-// One workgroup (2 waves) per block; LDS = ZTables + the staged block (dynamic, stage_cap bytes + 16).
+// One workgroup (2 waves) per block; LDS = ZBlockLds + the staged block (dynamic, stage_cap bytes + 16).
 __global__ void __launch_bounds__(128) zstd_block_kernel(const uint8_t *pkt, const uint64_t *foff, uint64_t f0,
                                                          const tfz::ZBlockDesc *blocks, uint8_t *lits, tfz::ZRec *recs,
                                                          uint32_t stage_cap, unsigned *err) {
     extern __shared__ __attribute__((aligned(16))) uint8_t zl[];
-    tfz::ZTables &T = *reinterpret_cast<tfz::ZTables *>(zl);
-    uint8_t *stage = zl + ((sizeof(tfz::ZTables) + 15) & ~size_t(15));
+    ZBlockLds &T = *reinterpret_cast<ZBlockLds *>(zl);
+    uint8_t *stage = zl + ((sizeof(ZBlockLds) + 15) & ~size_t(15));
     const tfz::ZBlockDesc d = blocks[blockIdx.x];
     const uint8_t *body = pkt + foff[f0 + d.pframe] + FRAME_HDR;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -329,10 +396,7 @@ __global__ void __launch_bounds__(128) zstd_block_kernel(const uint8_t *pkt, con
             const uint8_t c = body[d.lit_at];
             for (uint32_t i = lane; i < d.lsize; i += 64) lit[i] = c;
         } else {
-            ok = tfz::huf_read(body + d.huf, d.huf_n, T, lane, 64) >= 0;
-            lds_order();
-            if (ok) huf2_build(T, lane);
-            lds_order();
+            ok = huf2_read(body + d.huf, d.huf_n, T, lane);
             if (ok) {
                 ok = huf_lanes<true>(T, stage + (d.lit_at - d.src), d.lbytes, d.lsize, d.streams, lit, lane);
             }
@@ -341,7 +405,8 @@ __global__ void __launch_bounds__(128) zstd_block_kernel(const uint8_t *pkt, con
         if (d.nseq) {
             bool built = true;
             if (lane == 0)
-                for (int k = 0; k < 3; ++k) built = built && tfz::seq_table_build(T, k, d.tab[k], d.tab_n[k], body);
+                for (int k = 0; k < 3; ++k)
+                    built = built && tfz::seq_table_build(T, k, d.tab[k], d.tab_n[k], body, T.snorm, T.snext);
             lds_order();
             ok = __ballot(lane == 0 && !built) == 0;
         }
@@ -868,9 +933,9 @@ int zstd_decode_frames(Ctx *ctx, const uint8_t *packet, uint64_t nf, const uint6
             TFG_LAUNCH_CHECK();
             if (nb) {
                 const uint32_t cap = (max_comp + 15) & ~15u;
-                const size_t lds = ((sizeof(tfz::ZTables) + 15) & ~size_t(15)) + cap + 16;
-                // <= 22.5 KB of tables + a 128 KB block + slack: within gfx950's 160 KB of LDS (one or
-                // two workgroups per CU, by the launch's largest compressed block)
+                const size_t lds = ((sizeof(ZBlockLds) + 15) & ~size_t(15)) + cap + 16;
+                // <= 18.7 KB of tables + a 128 KB block + slack: within gfx950's 160 KB of LDS (two
+                // workgroups per CU while the launch's largest compressed block is under ~61 KB)
                 TFG_CHECK(lds <= 160 * 1024, TFG_ERR_LOGICAL, "ZSTD block stage of %zu bytes", lds);
                 hipLaunchKernelGGL(zstd_block_kernel, dim3(nb), dim3(128), lds, ctx->stream, packet, dfo, a,
                                    (const tfz::ZBlockDesc *)blk, lit, rec, cap, err);

@@ -59,15 +59,16 @@ struct alignas(8) ZSeqEntry { // 8 bytes: one LDS read per code
     uint8_t sym;    // the code while the table is built, then the value's additional bits
 };
 
-// The tables of one block (LDS on the device, ~14 KB)
-struct ZTables {
+// The sequence tables of one block (LDS on the device, 10 KB)
+struct ZSeqTables {
     ZSeqEntry ll[512], of[256], ml[512]; // accuracy logs <= 9 / 8 / 9
     int ll_log, of_log, ml_log;
-    uint16_t huf[1 << ZHUF_MAXBITS];     // symbol | nbBits << 8
+};
+// ... and the one-symbol Huffman table (the host form; the device builds a two-symbol table
+// straight from the weights, zstd.hip)
+struct ZTables : ZSeqTables {
+    uint16_t huf[1 << ZHUF_MAXBITS]; // symbol | nbBits << 8
     int huf_bits;
-    // device: two symbols per lookup where both codes fit the index (huf2_build):
-    // sym1 | sym2 << 8 | len1 << 16 | (len1 + len2) << 20 | two << 25
-    uint32_t huf2[1 << ZHUF_MAXBITS];
 };
 
 // One block (scan output).  Offsets are into the packet frame's ZSTD body.
@@ -288,10 +289,10 @@ ZHD int64_t fse_read_ncount(const uint8_t *src, int64_t n, int max_log, int max_
 }
 
 // decoding table from normalized counts (FSE_buildDTable)
-template <typename E> ZHD bool fse_build(E *t, const int16_t *norm, int nsym, int log) {
+// next: 256 words of work space (device: LDS — a private array would live in scratch memory)
+template <typename E> ZHD bool fse_build(E *t, const int16_t *norm, int nsym, int log, uint16_t *next) {
     const int size = 1 << log;
     int high = size - 1;
-    uint16_t next[256];
     for (int s = 0; s < nsym; ++s) {
         if (norm[s] == -1) {
             t[high--].sym = (uint8_t)s;
@@ -327,11 +328,12 @@ template <typename E> ZHD void fse_rle(E *t, int sym) {
 }
 
 // ---------------------------------------------------------------- Huffman
-// Huffman tree description (RFC 8878 §4.2.1) -> t.huf; returns bytes used or -1.  Every caller
-// lane parses; the table fill is split over lanes (lane, lane + nl, ...).
-ZHD int64_t huf_read(const uint8_t *src, int64_t n, ZTables &t, uint32_t lane = 0, uint32_t nl = 1) {
+// Huffman tree description (RFC 8878 §4.2.1) -> the weights of symbols 0 .. nw - 1 (the last
+// one completed to a power of two) and the table's index bits; returns bytes used or -1.
+// Work space: ft (64 entries), norm (16), next (256) — LDS on the device.
+ZHD int64_t huf_weights(const uint8_t *src, int64_t n, uint8_t *weight, int &nw_out, int &maxbits_out, FseEntry *ft,
+                        int16_t *norm, uint16_t *next) {
     if (n < 1) return -1;
-    uint8_t weight[256];
     int nw = 0;
     int64_t used;
     const int hb = src[0];
@@ -346,12 +348,10 @@ ZHD int64_t huf_read(const uint8_t *src, int64_t n, ZTables &t, uint32_t lane = 
     } else { // FSE-compressed weights, two interleaved states
         used = 1 + hb;
         if (used > n || hb == 0) return -1;
-        int16_t norm[16];
         int log, nsym;
         const int64_t hd = fse_read_ncount(src + 1, hb, 6, 15, norm, log, nsym);
         if (hd < 0 || hd >= hb) return -1;
-        FseEntry ft[64];
-        if (!fse_build(ft, norm, nsym, log)) return -1;
+        if (!fse_build(ft, norm, nsym, log, next)) return -1;
         BitR<> bb;
         if (!bb.init(src + 1 + hd, hb - hd)) return -1;
         uint32_t s1 = (uint32_t)bb.read(log), s2 = (uint32_t)bb.read(log);
@@ -383,22 +383,43 @@ ZHD int64_t huf_read(const uint8_t *src, int64_t n, ZTables &t, uint32_t lane = 
     const uint32_t rest = (1u << maxbits) - sum;
     if (rest & (rest - 1)) return -1; // not a power of two
     weight[nw++] = (uint8_t)(highbit(rest) + 1);
-    // table: weight w -> nbBits = maxbits + 1 - w, 2^(w-1) entries, symbols in order (HUF_readDTableX1)
-    uint32_t start[ZHUF_MAXBITS + 2] = {};
+    nw_out = nw;
+    maxbits_out = maxbits;
+    return used;
+}
+
+// weight class k of a table of `maxbits` index bits: symbols of weight k take 2^(k-1) entries
+// each, in symbol order, from start[k] (HUF_readDTableX1); false when the weights do not fill it
+ZHD bool huf_class_starts(const uint8_t *weight, int nw, int maxbits, uint32_t (&start)[ZHUF_MAXBITS + 2]) {
     uint32_t cnt[ZHUF_MAXBITS + 2] = {};
     for (int i = 0; i < nw; ++i) cnt[weight[i]]++;
     uint32_t acc = 0;
+    for (int k = 0; k <= ZHUF_MAXBITS + 1; ++k) start[k] = 0;
     for (int k = 1; k <= maxbits; ++k) {
         start[k] = acc;
         acc += cnt[k] << (k - 1);
     }
-    if (acc != (1u << maxbits)) return -1;
+    start[maxbits + 1] = acc;
+    return acc == (1u << maxbits);
+}
+
+// the one-symbol table: entry = symbol | nbBits << 8, nbBits = maxbits + 1 - weight
+ZHD int64_t huf_read(const uint8_t *src, int64_t n, ZTables &t) {
+    uint8_t weight[256];
+    FseEntry ft[64];
+    int16_t norm[16];
+    uint16_t next[256];
+    int nw = 0, maxbits = 0;
+    const int64_t used = huf_weights(src, n, weight, nw, maxbits, ft, norm, next);
+    if (used < 0) return -1;
+    uint32_t start[ZHUF_MAXBITS + 2];
+    if (!huf_class_starts(weight, nw, maxbits, start)) return -1;
     for (int i = 0; i < nw; ++i) {
         const int wt = weight[i];
         if (!wt) continue;
         const uint32_t len = 1u << (wt - 1);
         const uint16_t e = (uint16_t)(i | ((maxbits + 1 - wt) << 8));
-        for (uint32_t k = lane; k < len; k += nl) t.huf[start[wt] + k] = e;
+        for (uint32_t k = 0; k < len; ++k) t.huf[start[wt] + k] = e;
         start[wt] += len;
     }
     t.huf_bits = maxbits;
@@ -517,34 +538,34 @@ ZHD bool seq_finish(ZSeqEntry *t, int size, int kind) {
 }
 
 // the table of one kind from its description (ZBlockDesc::tab: mode << 30 | offset into `body`)
-ZHD bool seq_table_build(ZTables &t, int kind, uint32_t tab, uint32_t tab_n, const uint8_t *body) {
+// norm (53 entries) and next (256): work space, LDS on the device
+ZHD bool seq_table_build(ZSeqTables &t, int kind, uint32_t tab, uint32_t tab_n, const uint8_t *body, int16_t *norm,
+                         uint16_t *next) {
     ZSeqEntry *e = kind == 0 ? t.ll : kind == 1 ? t.of : t.ml;
     int &log = kind == 0 ? t.ll_log : kind == 1 ? t.of_log : t.ml_log;
     const int mode = (int)(tab >> 30);
     const uint32_t at = tab & 0x3FFFFFFFu;
     const int max_sym = kind == 0 ? 35 : kind == 1 ? 31 : 52, max_log = kind == 1 ? 8 : 9;
     if (mode == 0) { // predefined
-        int16_t norm[53];
         const int nsym = kind == 0 ? 36 : kind == 1 ? 29 : 53;
         for (int s = 0; s < nsym; ++s) norm[s] = kind == 0 ? ll_default(s) : kind == 1 ? of_default(s) : ml_default(s);
         log = kind == 1 ? 5 : 6;
-        return fse_build(e, norm, nsym, log) && seq_finish(e, 1 << log, kind);
+        return fse_build(e, norm, nsym, log, next) && seq_finish(e, 1 << log, kind);
     }
     if (mode == 1) { // RLE
         fse_rle(e, body[at]);
         log = 0;
         return seq_finish(e, 1, kind);
     }
-    int16_t norm[53];
     int nsym;
     if (fse_read_ncount(body + at, tab_n, max_log, max_sym, norm, log, nsym) < 0) return false;
-    return fse_build(e, norm, nsym, log) && seq_finish(e, 1 << log, kind);
+    return fse_build(e, norm, nsym, log, next) && seq_finish(e, 1 << log, kind);
 }
 
 // The sequences of one block: put(q, record) for q = 0 .. nseq (the last: the block's trailing
 // literal run).  false when the bitstream is malformed or a literal length runs past lsize.
 template <bool AL, typename Put>
-ZHD bool seq_decode(const ZTables &t, const uint8_t *bits, int64_t n, uint32_t nseq, uint32_t lsize, Put &&put) {
+ZHD bool seq_decode(const ZSeqTables &t, const uint8_t *bits, int64_t n, uint32_t nseq, uint32_t lsize, Put &&put) {
     uint32_t lit_pos = 0;
     if (nseq) {
         BitR<AL> bb;
@@ -874,9 +895,12 @@ inline bool zblock_decode_host(const uint8_t *body, const ZBlockDesc &d, ZTables
                 if (!huf_stream(t, ls + h.at[k], h.len[k], lit + k * h.seg, h.cnt[k])) return false;
         }
     }
-    if (d.nseq)
+    if (d.nseq) {
+        int16_t norm[53];
+        uint16_t next[256];
         for (int k = 0; k < 3; ++k)
-            if (!seq_table_build(t, k, d.tab[k], d.tab_n[k], body)) return false;
+            if (!seq_table_build(t, k, d.tab[k], d.tab_n[k], body, norm, next)) return false;
+    }
     return seq_decode<false>(t, body + d.seq_at, d.seq_n, d.nseq, d.lsize, [&](uint32_t q, const ZRec &r) { recs[d.rec + q] = r; });
 }
 
