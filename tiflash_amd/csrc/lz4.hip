@@ -37,7 +37,13 @@ constexpr uint8_t NONE_METHOD = 0x02;      // CompressionMethodByte::NONE
 constexpr int FRAME_HDR = 9;               // COMPRESSED_BLOCK_HEADER_SIZE
 constexpr uint64_t MAX_FRAME_RAW = 0x40000000ull; // DBMS_MAX_COMPRESSED_SIZE
 constexpr uint32_t ENC_FRAME = 64 * 1024;  // raw bytes per frame this encoder writes
-constexpr int HASH_LOG = 12;
+// match-finder table: 2^HASH_LOG x 6 B of LDS per frame.  11 bits (12 KB): 13 encode waves per CU
+// instead of 6 at 12 bits; measured on 256 MB of k%08d rows (tools/lz4_probe.py): 12 bits 8.6 GB/s
+// at ratio 1.371, 11 bits 12.1 GB/s at 1.320, 10 bits 17.8 GB/s at 1.266.
+#ifndef TFG_LZ4_HASH_LOG
+#define TFG_LZ4_HASH_LOG 11
+#endif
+constexpr int HASH_LOG = TFG_LZ4_HASH_LOG;
 constexpr uint64_t ENC_SLOT = FRAME_HDR + ENC_FRAME + ENC_FRAME / 255 + 16; // header + LZ4_COMPRESSBOUND
 constexpr int MIN_MATCH = 4, LAST_LITERALS = 5, MF_LIMIT = 12;
 
