@@ -148,3 +148,49 @@ def test_gpu_codec_decode_zstd_packets(tfa, orc, ctx, dev, n):
                    for i in range(0, len(body), 1 << 20))
     rows, dec = tfa.codec_decode(ctx, dev_bytes(pkt, dev), version=V1)
     assert_decoded(cols, n, rows, dec)
+
+
+# ------------------------------------------------------------------ frame-level shapes (RFC 8878 §3.1)
+def _skippable(payload: bytes, nibble=0) -> bytes:
+    return struct.pack("<II", 0x184D2A50 | nibble, len(payload)) + payload
+
+
+def _shapes(rng):
+    """(ZSTD body of one packet frame, the bytes it decodes to)"""
+    a = b"".join(b"key%08d|" % int(i) for i in rng.integers(0, 1000, 30_000))
+    b = bytes(rng.integers(0, 4, 50_000, dtype=np.uint8))
+    yield zcompress(a, 3) + zcompress(b, 1, True), a + b                     # two ZSTD frames, one checksummed
+    yield _skippable(b"meta" * 10) + zcompress(a, 3), a                      # a skippable frame first
+    yield zcompress(a, 1) + _skippable(b"", 7) + zcompress(b"", 3), a        # skippable between, an empty frame
+    yield zcompress(b"", 1), b""                                             # one empty frame
+    yield b"".join(zcompress(a[i:i + 4000], 5) for i in range(0, len(a), 4000)), a  # many small frames
+
+
+def _dict_frame():
+    """a frame header that names a dictionary (id 7): unsupported, must be rejected"""
+    z = bytearray(zcompress(b"hello hello hello", 3))
+    fhd = z[4]
+    assert fhd & 3 == 0
+    z[4] = fhd | 1  # dictionary id field of 1 byte follows the descriptor / window byte
+    pos = 5 if fhd & 0x20 else 6
+    return bytes(z[:pos]) + b"\x07" + bytes(z[pos:])
+
+
+def test_cpu_decoder_frame_shapes():
+    rng = np.random.default_rng(41)
+    for body, want in _shapes(rng):
+        assert cpu_decode(body, len(want)) == want
+    assert cpu_decode(_dict_frame(), 17) is None
+    assert cpu_decode(_skippable(b"abc")[:-1], 0) is None  # truncated skippable frame
+
+
+@pytest.mark.gpu
+def test_gpu_decompress_frame_shapes(tfa, ctx, dev):
+    rng = np.random.default_rng(41)
+    cases = list(_shapes(rng))
+    pkt = b"".join(frame(body, len(want)) for body, want in cases)
+    got = tfa.codec_decompress(ctx, dev_bytes(pkt, dev)).cpu().numpy().tobytes()
+    assert got == b"\x02" + b"".join(want for _, want in cases)
+    for bad in (frame(_dict_frame(), 17), frame(_skippable(b"abc")[:-1], 0)):
+        with pytest.raises(tfa.TfgError):
+            tfa.codec_decompress(ctx, dev_bytes(bad, dev))
