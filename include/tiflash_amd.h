@@ -528,15 +528,17 @@ int tfg_codec_packet_destroy(tfg_codec_packet *p);
  * (CHBlockChunkCodecV1.cpp:555-565) as MPPTunnelSetHelper::ToCompressedPacket calls it
  * (Flash/Mpp/MPPTunnelSetHelper.cpp:170-185): the body of an uncompressed V1 `packet` (method
  * byte 0x02 first) becomes LZ4 frames `0x82 | UInt32 frame bytes | UInt32 raw bytes | LZ4 block`
- * (64 KB of body per frame).  out == NULL: *out_bytes_host = tfg_codec_compress_bound(bytes);
- * otherwise the exact size, TFG_ERR_CAPACITY when it exceeds `capacity`.  LZ4HC writes the same
- * format and is accepted as LZ4.
+ * (64 KB of body per frame), or with TFG_COMPRESSION_ZSTD ZSTD frames
+ * `0x90 | UInt32 frame bytes | UInt32 raw bytes | ZSTD frame` (one RFC 8878 frame per 64 KB:
+ * single-segment header with the content size, one block, raw literals + FSE sequences with the
+ * predefined tables, or a raw block when that is smaller; no checksum).  out == NULL:
+ * *out_bytes_host = tfg_codec_compress_bound(bytes) (covers both); otherwise the exact size,
+ * TFG_ERR_CAPACITY when it exceeds `capacity`.  LZ4HC writes the same format and is accepted as LZ4.
  * tfg_codec_decompress is CompressedCHBlockChunkReadBuffer over a whole packet: the frames of an
  * LZ4 packet (any frame sizes, as any LZ4 encoder wrote them) or of a ZSTD packet (frames
  * `0x90 | UInt32 frame bytes | UInt32 raw bytes | ZSTD frame`, CompressionCodecZSTD.cpp:38-65;
  * RFC 8878 frames without dictionaries, checksums verified) become the uncompressed V1 packet
- * (0x02 + body).  out == NULL: the size only.  Malformed frames: TFG_ERR_INVALID_ARG.
- * tfg_codec_compress writes LZ4 only (ZSTD: TFG_ERR_NOT_IMPLEMENTED). */
+ * (0x02 + body).  out == NULL: the size only.  Malformed frames: TFG_ERR_INVALID_ARG. */
 #define TFG_COMPRESSION_LZ4 1
 #define TFG_COMPRESSION_LZ4HC 2
 #define TFG_COMPRESSION_ZSTD 3

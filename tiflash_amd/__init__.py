@@ -745,7 +745,8 @@ COMPRESSION_LZ4, COMPRESSION_LZ4HC, COMPRESSION_ZSTD, COMPRESSION_NONE = 1, 2, 3
 
 def codec_compress(ctx: Context, packet, method: int = COMPRESSION_LZ4):
     """CHBlockChunkCodecV1::encode(std::string_view, method) of an uncompressed V1 device packet
-    (as MPPTunnelSetHelper::ToCompressedPacket re-encodes a chunk): LZ4 frames, a device tensor."""
+    (as MPPTunnelSetHelper::ToCompressedPacket re-encodes a chunk): LZ4 frames (LZ4 / LZ4HC) or ZSTD
+    frames (COMPRESSION_ZSTD, the HIGH_COMPRESSION mode), 64 KB of body each, a device tensor."""
     import torch
     size = ctypes.c_size_t()
     check(lib().tfg_codec_compress(ctx.h, method, _p(packet), ctypes.c_size_t(packet.numel()), None,

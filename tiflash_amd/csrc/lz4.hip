@@ -178,11 +178,11 @@ __global__ void lz4_offsets_kernel(const uint32_t *sizes, uint64_t nframes, uint
 }
 
 // frame f's bytes -> dst + offs[f]
-__global__ void lz4_pack_kernel(const uint8_t *frames, const uint32_t *sizes, const uint64_t *offs, uint64_t nframes,
-                                uint8_t *dst) {
+__global__ void lz4_pack_kernel(const uint8_t *frames, uint64_t slot, const uint32_t *sizes, const uint64_t *offs,
+                                uint64_t nframes, uint8_t *dst) {
     const uint64_t f = blockIdx.x;
     if (f >= nframes) return;
-    const uint8_t *s = frames + f * ENC_SLOT;
+    const uint8_t *s = frames + f * slot;
     const uint32_t sz = sizes[f];
     uint8_t *d = dst + offs[f];
     for (uint32_t i = threadIdx.x; i < sz; i += blockDim.x) d[i] = s[i];
@@ -323,8 +323,8 @@ size_t tfg_codec_compress_bound(size_t bytes) {
 int tfg_codec_compress(tfg_ctx *ctx, int method, const uint8_t *packet, size_t bytes, uint8_t *out, size_t capacity,
                        size_t *out_bytes_host) {
     TFG_CHECK(ctx && out_bytes_host && (bytes == 0 || packet), TFG_ERR_INVALID_ARG, "null argument");
-    TFG_CHECK(method == TFG_COMPRESSION_LZ4 || method == TFG_COMPRESSION_LZ4HC, TFG_ERR_NOT_IMPLEMENTED,
-              "compression method %d: only LZ4", method);
+    TFG_CHECK(method == TFG_COMPRESSION_LZ4 || method == TFG_COMPRESSION_LZ4HC || method == TFG_COMPRESSION_ZSTD,
+              TFG_ERR_NOT_IMPLEMENTED, "compression method %d: LZ4 / LZ4HC / ZSTD", method);
     if (int rc = set_device(ctx)) return rc;
     *out_bytes_host = 0;
     if (bytes == 0) return TFG_OK; // the empty Block: no packet body
@@ -337,23 +337,29 @@ int tfg_codec_compress(tfg_ctx *ctx, int method, const uint8_t *packet, size_t b
         return TFG_OK;
     }
     const uint8_t *body = packet + 1;
+    static_assert(ZE_FRAME == ENC_FRAME, "both senders frame the body in 64 KB units");
+    const bool zstd = method == TFG_COMPRESSION_ZSTD;
     const uint64_t n = bytes - 1, nframes = (n + ENC_FRAME - 1) / ENC_FRAME;
+    const uint64_t slot = zstd ? ZE_SLOT : ENC_SLOT;
     TFG_CHECK(nframes < (1ull << 31), TFG_ERR_INVALID_ARG, "packet of %llu bytes", (unsigned long long)bytes);
     Carver cv;
-    const size_t o_frames = cv.take<uint8_t>(nframes * ENC_SLOT), o_sizes = cv.take<uint32_t>(nframes);
+    const size_t o_frames = cv.take<uint8_t>(nframes * slot), o_sizes = cv.take<uint32_t>(nframes);
     const size_t o_offs = cv.take<uint64_t>(nframes + 1);
+    const size_t o_tmp = cv.take<uint8_t>(zstd ? zstd_encode_tmp_bytes(nframes) : 0);
     void *sp;
     if (int rc = scratch_get(ctx, cv.off, &sp)) return rc;
     char *sb = (char *)sp;
     uint8_t *frames = (uint8_t *)(sb + o_frames);
     uint32_t *sizes = (uint32_t *)(sb + o_sizes);
     uint64_t *offs = (uint64_t *)(sb + o_offs);
-    {
+    if (zstd) {
+        if (int rc = zstd_encode_frames(ctx, body, n, nframes, frames, sizes, sb + o_tmp)) return rc;
+    } else {
         ProfScope _ps(ctx, "codec.lz4.compress");
         hipLaunchKernelGGL(lz4_encode_kernel, dim3((unsigned)nframes), dim3(64), 0, ctx->stream, body, n, nframes, frames,
                            sizes);
+        TFG_LAUNCH_CHECK();
     }
-    TFG_LAUNCH_CHECK();
     hipLaunchKernelGGL(lz4_offsets_kernel, dim3(1), dim3(64), 0, ctx->stream, (const uint32_t *)sizes, nframes, offs);
     TFG_LAUNCH_CHECK();
     uint64_t total = 0;
@@ -361,7 +367,7 @@ int tfg_codec_compress(tfg_ctx *ctx, int method, const uint8_t *packet, size_t b
     *out_bytes_host = total;
     TFG_CHECK(capacity >= total, TFG_ERR_CAPACITY, "compressed packet needs %llu bytes, capacity %llu",
               (unsigned long long)total, (unsigned long long)capacity);
-    hipLaunchKernelGGL(lz4_pack_kernel, dim3((unsigned)nframes), dim3(256), 0, ctx->stream, (const uint8_t *)frames,
+    hipLaunchKernelGGL(lz4_pack_kernel, dim3((unsigned)nframes), dim3(256), 0, ctx->stream, (const uint8_t *)frames, slot,
                        (const uint32_t *)sizes, (const uint64_t *)offs, nframes, out);
     TFG_LAUNCH_CHECK();
     TFG_HIP(hipStreamSynchronize(ctx->stream));
