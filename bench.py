@@ -465,8 +465,9 @@ def zstd_leg(args, ctx, pkt):
     uncompressed V1 packet body compressed on the host by the system libzstd (level 1, one frame
     per 1 MB CompressedWriteBuffer block, as the reference's sender writes them), then decompressed
     on the device (zstd.hip: header scan, per-block entropy, resolve, byte-parallel execution);
-    checked against the packet.  The host
-    decompress of the same frames by libzstd on one thread is reported beside it."""
+    checked against the packet.  The device sender (zstd_enc.hip) then compresses the whole
+    packet into ZSTD frames, and the device decodes its own frames; both checked.  The host
+    compress / decompress of the same 64 MB by libzstd on one thread is reported beside it."""
     import ctypes
     import struct
 
@@ -485,12 +486,14 @@ def zstd_leg(args, ctx, pkt):
     start = max(1, int(pkt.numel()) // 4)
     body = pkt[start:start + (64 << 20)].cpu().numpy().tobytes()
     frames, fsz = [], 1 << 20
+    tz0 = time.perf_counter()
     for i in range(0, len(body), fsz):
         chunk = body[i:i + fsz]
         cap = z.ZSTD_compressBound(ctypes.c_size_t(len(chunk)))
         buf = ctypes.create_string_buffer(cap)
         n = z.ZSTD_compress(buf, ctypes.c_size_t(cap), chunk, ctypes.c_size_t(len(chunk)), 1)
         frames.append(b"\x90" + struct.pack("<II", n + 9, len(chunk)) + buf.raw[:n])
+    host_compress = time.perf_counter() - tz0
     zpkt = b"".join(frames)
     dz = torch.frombuffer(bytearray(zpkt), dtype=torch.uint8).to(pkt.device)
     for _ in range(2):
@@ -506,7 +509,32 @@ def zstd_leg(args, ctx, pkt):
     d = statistics.median(td)
     out = {"raw_bytes": len(body), "zstd_bytes": len(zpkt), "frames": len(frames), "ratio": round(len(body) / len(zpkt), 3),
            "decompress_ms": round(d * 1e3, 3), "decompress_GBps": round(len(body) / d / 1e9, 2)}
+    del dz, back
+    # the device sender over the whole packet, and the device decode of its frames
+    for _ in range(2):
+        zs = tfa.codec_compress(ctx, pkt, method=tfa.COMPRESSION_ZSTD)
+    tc, tu = [], []
+    for _ in range(max(args.steps, 3)):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        zs = tfa.codec_compress(ctx, pkt, method=tfa.COMPRESSION_ZSTD)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        back = tfa.codec_decompress(ctx, zs)
+        torch.cuda.synchronize()
+        tc.append(t1 - t0)
+        tu.append(time.perf_counter() - t1)
+    assert torch.equal(back, pkt), "ZSTD sender round trip"
+    c, u = statistics.median(tc), statistics.median(tu)
+    out["sender"] = {"packet_bytes": int(pkt.numel()), "zstd_bytes": int(zs.numel()),
+                     "ratio": round(pkt.numel() / max(zs.numel(), 1), 3), "compress_ms": round(c * 1e3, 3),
+                     "compress_GBps": round(pkt.numel() / c / 1e9, 2), "decompress_ms": round(u * 1e3, 3),
+                     "decompress_GBps": round(pkt.numel() / u / 1e9, 2)}
+    del zs, back
     if not args.no_cpu:
+        out["cpu_compress"] = {"compress_GBps": round(len(body) / host_compress / 1e9, 3), "cores": 1,
+                               "kind": "library", "sample": f"{len(body)} bytes, system libzstd ZSTD_compress "
+                               "level 1, 1 MB frames, one host thread"}
         dst = ctypes.create_string_buffer(fsz)
         t0 = time.perf_counter()
         for f in frames:

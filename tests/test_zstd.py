@@ -230,6 +230,10 @@ def sender_payloads(rng):
     far = bytes(rng.integers(0, 256, 40_000, dtype=np.uint8))
     yield far + bytes(rng.integers(0, 256, 20_000, dtype=np.uint8)) + far[:5000]  # a far match (offset 60000)
     yield bytes(rng.integers(0, 256, 70_000, dtype=np.uint8) % 3) + b"z" * 70_000  # long matches
+    # literal alphabets past 128 symbols: FSE-compressed Huffman weights
+    yield rng.integers(0, 1000, 40_000).astype(np.int64).tobytes()
+    yield (rng.geometric(0.02, 200_000) % 256).astype(np.uint8).tobytes()
+    yield bytes(rng.integers(0, 256, 3000, dtype=np.uint8)) * 3 + bytes(rng.integers(200, 256, 9000, dtype=np.uint8))
 
 
 @pytest.mark.gpu

@@ -12,8 +12,9 @@
 //             equal to the previous one with literals before it is sent as repeat code 1)
 //   literals  Huffman (histogram by LDS atomics, leaves ranked by the wave, minimum-redundancy
 //             lengths limited to 11 bits on one lane, canonical codes as HUF_buildCTable assigns
-//             them, weights in the direct 4-bit form; 4 streams, each written 64 symbols per step
-//             at prefix-sum bit offsets), RLE for one byte value, raw when that is smaller
+//             them, weights FSE-compressed or in the direct 4-bit form; 4 streams, each written
+//             64 symbols per step at prefix-sum bit offsets), RLE for one byte value, raw when
+//             that is smaller
 //   sequences per code kind (LL / OF / ML): counted by LDS atomics, then RLE when one code is
 //             used, a table description of the counts (normalized, FSE_optimalTableLog's
 //             accuracy) when that costs fewer bits than the predefined distribution, predefined
@@ -301,123 +302,6 @@ __device__ __forceinline__ uint32_t huf_stream(const uint8_t *lt, uint32_t a, ui
     return bytes;
 }
 
-// The literal section of lt[0, nlit) at dst: Huffman-compressed (4 streams from 256 literals, 1
-// below; weights in the direct 4-bit form, so every literal byte < 129) when smaller, RLE when
-// one byte value, raw otherwise.  All lanes; returns the section's bytes.
-__device__ uint32_t literal_section(const uint8_t *lt, uint32_t nlit, uint8_t *dst, ZHufLds &H) {
-    const uint32_t lane = __lane_id();
-    if (nlit < 64) return raw_literals(lt, nlit, dst);
-    for (uint32_t i = lane; i < 256; i += 64) H.hist[i] = 0;
-    __syncthreads();
-    for (uint32_t i = lane; i < nlit; i += 64) atomicAdd(&H.hist[lt[i]], 1u);
-    __syncthreads();
-    uint32_t present = 0, maxs = 0;
-    for (uint32_t k = 0; k < 4; ++k) {
-        const uint32_t sy = lane + 64 * k;
-        if (H.hist[sy]) {
-            ++present;
-            maxs = sy;
-        }
-    }
-    const uint32_t nsym = ufl(wave_sum(present)), maxsym = ufl(wave_max(maxs));
-    if (nsym == 1) { // RLE: 3-byte header (20-bit size) + the byte
-        if (lane == 0) {
-            dst[0] = (uint8_t)(0x0D | ((nlit & 0xF) << 4));
-            dst[1] = (uint8_t)(nlit >> 4);
-            dst[2] = (uint8_t)(nlit >> 12);
-            dst[3] = (uint8_t)maxsym;
-        }
-        return 4;
-    }
-    if (maxsym > 128) return raw_literals(lt, nlit, dst);
-    // leaves in ascending (count, symbol) order
-    for (uint32_t k = 0; k < 4; ++k) {
-        const uint32_t sy = lane + 64 * k, c = H.hist[sy];
-        if (!c) continue;
-        uint32_t rank = 0;
-        for (uint32_t t = 0; t <= maxsym; ++t) {
-            const uint32_t ct = H.hist[t];
-            rank += ct && (ct < c || (ct == c && t < sy));
-        }
-        H.len[rank] = (int32_t)c;
-        H.sym[rank] = (uint8_t)sy;
-    }
-    __syncthreads();
-    if (lane == 0) {
-        huf_lengths(H.len, (int)nsym);
-        uint32_t mb = 0;
-        for (uint32_t i = 0; i < nsym; ++i) mb = max(mb, (uint32_t)H.len[i]);
-        for (uint32_t sy = 0; sy < 256; ++sy) H.code[sy] = 0;
-        for (uint32_t i = 0; i < nsym; ++i) H.code[H.sym[i]] = (uint32_t)H.len[i] << 16;
-        // canonical values (HUF_buildCTable): longest codes first from 0, symbol order within a length
-        uint32_t per[ZHUF_MAXBITS + 2] = {0}, start[ZHUF_MAXBITS + 2] = {0};
-        for (uint32_t i = 0; i < nsym; ++i) ++per[H.len[i]];
-        uint32_t m = 0;
-        for (uint32_t nb = mb; nb > 0; --nb) {
-            start[nb] = m;
-            m += per[nb];
-            m >>= 1;
-        }
-        for (uint32_t sy = 0; sy <= maxsym; ++sy) {
-            const uint32_t nb = H.code[sy] >> 16;
-            if (nb) H.code[sy] |= start[nb]++;
-        }
-        H.maxbits = mb;
-    }
-    __syncthreads();
-    const uint32_t mb = ufl(H.maxbits);
-    // exact payload bits: is it worth it
-    uint32_t tb = 0;
-    for (uint32_t k = 0; k < 4; ++k) {
-        const uint32_t sy = lane + 64 * k;
-        tb += H.hist[sy] * (H.code[sy] >> 16);
-    }
-    tb = ufl(wave_sum(tb));
-    const bool four = nlit >= 256;
-    const uint32_t hdr = four ? 5 : 3, nw = maxsym, tree = 1 + (nw + 1) / 2;
-    const uint32_t est = hdr + tree + (four ? 6 : 0) + tb / 8 + 4;
-    if (est >= 3 + nlit) return raw_literals(lt, nlit, dst);
-    // tree description: header byte 127 + weights, then 4-bit weights (high nibble first)
-    if (lane == 0) dst[hdr] = (uint8_t)(127 + nw);
-    for (uint32_t j = lane; j < (nw + 1) / 2; j += 64) {
-        uint32_t w2[2];
-        for (uint32_t h = 0; h < 2; ++h) {
-            const uint32_t sy = 2 * j + h, nb = sy < nw ? H.code[sy] >> 16 : 0;
-            w2[h] = nb ? mb + 1 - nb : 0;
-        }
-        dst[hdr + 1 + j] = (uint8_t)((w2[0] << 4) | w2[1]);
-    }
-    uint32_t at = hdr + tree;
-    uint32_t csz;
-    if (four) {
-        const uint32_t seg = (nlit + 3) / 4;
-        uint32_t sz[4];
-        at += 6;
-        for (uint32_t k = 0; k < 4; ++k) {
-            const uint32_t a = k * seg, b = k == 3 ? nlit : a + seg;
-            sz[k] = huf_stream(lt, a, b, dst + at, H);
-            at += sz[k];
-        }
-        if (lane < 3) {
-            dst[hdr + tree + 2 * lane] = (uint8_t)sz[lane == 0 ? 0 : lane == 1 ? 1 : 2];
-            dst[hdr + tree + 2 * lane + 1] = (uint8_t)(sz[lane == 0 ? 0 : lane == 1 ? 1 : 2] >> 8);
-        }
-        csz = at - hdr;
-        if (lane == 0) { // compressed, 4 streams, 18-bit sizes: 5-byte header
-            const uint64_t v = 2u | (3u << 2) | ((uint64_t)nlit << 4) | ((uint64_t)csz << 22);
-            for (int q = 0; q < 5; ++q) dst[q] = (uint8_t)(v >> (8 * q));
-        }
-    } else {
-        at += huf_stream(lt, 0, nlit, dst + at, H);
-        csz = at - hdr;
-        if (lane == 0) { // compressed, 1 stream, 10-bit sizes: 3-byte header
-            const uint32_t v = 2u | (nlit << 4) | (csz << 14);
-            for (int q = 0; q < 3; ++q) dst[q] = (uint8_t)(v >> (8 * q));
-        }
-    }
-    return at;
-}
-
 // LDS of the sequence coder
 struct ZSeqLds {
     ZEncFse t[3];           // LL / OF / ML tables in force
@@ -427,18 +311,6 @@ struct ZSeqLds {
     uint32_t desc_n[3], log[3], mode[3];
     uint8_t sym_at[512];
     uint32_t cumul[64];
-};
-
-// LDS of one encode wave: the match finder's tables, then (dead by then) the coders' state
-union ZEncLds {
-    struct {
-        uint16_t tpos[1 << ZE_HASH];
-        uint32_t tseq[1 << ZE_HASH];
-    } m;
-    struct {
-        ZHufLds H;
-        ZSeqLds S;
-    } c;
 };
 
 __device__ __forceinline__ uint32_t lg256(uint32_t x) { // log2(x) * 256, linear between powers of two
@@ -533,6 +405,221 @@ __device__ uint32_t zenc_write_ncount(uint8_t *out, const int16_t *norm, int max
     out[o + 1] = (uint8_t)(bs >> 8);
     return o + (uint32_t)(bc + 7) / 8;
 }
+
+// The Huffman weights of symbols [0, nw) (codes in H.code, longest mb) FSE-compressed as
+// HUF_compressWeights does (lane 0): a description of the weight counts (accuracy log <= 6) and
+// a two-state FSE bitstream (even weights through state 1, odd through state 2, the last two
+// seeding the states).  Writes header byte + description + bitstream at dst and returns their
+// bytes, or 0 when the direct form is as small (or the weights do not compress).  Work space:
+// H.len / H.hist (free by now), S's first table.
+__device__ uint32_t huf_weights_fse(uint8_t *dst, ZHufLds &H, ZSeqLds &S, uint32_t nw, uint32_t mb) {
+    int32_t *w = H.len;
+    uint32_t *wh = H.hist;
+    for (int c = 0; c < 16; ++c) wh[c] = 0;
+    for (uint32_t i = 0; i < nw; ++i) {
+        const uint32_t nb = H.code[i] >> 16;
+        w[i] = nb ? (int32_t)(mb + 1 - nb) : 0;
+        ++wh[w[i]];
+    }
+    int maxw = 0, distinct = 0;
+    for (int c = 0; c <= ZHUF_MAXBITS + 1; ++c)
+        if (wh[c]) {
+            maxw = c;
+            ++distinct;
+        }
+    if (distinct < 2 || nw < 3) return 0;
+    int L = 6;
+    const int max_src = zhb(nw - 1) - 2, min_bits = min(zhb(nw) + 1, zhb((uint32_t)maxw) + 2);
+    if (max_src < L) L = max_src;
+    if (min_bits > L) L = min_bits;
+    L = max(5, min(L, 6));
+    zenc_normalize(wh, maxw, nw, L, S.norm[0]);
+    const uint32_t nc = zenc_write_ncount(dst + 1, S.norm[0], maxw, L);
+    ZEncFse &t = S.t[0];
+    zenc_build(t, S.norm[0], maxw + 1, L, S.sym_at, S.cumul);
+    uint8_t *bs = dst + 1 + nc;
+    uint64_t bc = 0;
+    int bn = 0;
+    uint32_t o = 0;
+    auto put = [&](uint32_t v, int n) {
+        bc |= (uint64_t)(v & ((1u << n) - 1)) << bn;
+        bn += n;
+        while (bn >= 8) {
+            bs[o++] = (uint8_t)bc;
+            bc >>= 8;
+            bn -= 8;
+        }
+    };
+    auto init = [&](int sym) {
+        const uint32_t nb = (uint32_t)(t.dnb[sym] + (1 << 15)) >> 16;
+        const uint32_t v = (nb << 16) - (uint32_t)t.dnb[sym];
+        return (uint32_t)t.state[(v >> nb) + t.dfs[sym]];
+    };
+    auto enc = [&](uint32_t &st, int sym) {
+        const uint32_t nb = (st + (uint32_t)t.dnb[sym]) >> 16;
+        put(st, (int)nb);
+        st = t.state[(st >> nb) + t.dfs[sym]];
+    };
+    int i = (int)nw - 1;
+    uint32_t s1, s2;
+    if (nw & 1) {
+        s1 = init(w[i]);
+        s2 = init(w[i - 1]);
+        enc(s1, w[i - 2]);
+        i -= 3;
+    } else {
+        s2 = init(w[i]);
+        s1 = init(w[i - 1]);
+        i -= 2;
+    }
+    for (; i >= 0; --i) enc((i & 1) ? s2 : s1, w[i]);
+    put(s2, L);
+    put(s1, L);
+    put(1, 1); // end mark
+    if (bn > 0) bs[o++] = (uint8_t)bc;
+    const uint32_t total = nc + o;
+    if (total >= 128 || (nw <= 128 && total >= (nw + 1) / 2)) return 0;
+    dst[0] = (uint8_t)total;
+    return 1 + total;
+}
+
+// The literal section of lt[0, nlit) at dst: Huffman-compressed (4 streams from 256 literals, 1
+// below; weights FSE-compressed, or in the direct 4-bit form when that is as small) when smaller,
+// RLE when one byte value, raw otherwise.  All lanes; returns the section's bytes.  S: work space
+// of the weight coder (its counts are left alone).
+__device__ uint32_t literal_section(const uint8_t *lt, uint32_t nlit, uint8_t *dst, ZHufLds &H, ZSeqLds &S) {
+    const uint32_t lane = __lane_id();
+    if (nlit < 64) return raw_literals(lt, nlit, dst);
+    for (uint32_t i = lane; i < 256; i += 64) H.hist[i] = 0;
+    __syncthreads();
+    for (uint32_t i = lane; i < nlit; i += 64) atomicAdd(&H.hist[lt[i]], 1u);
+    __syncthreads();
+    uint32_t present = 0, maxs = 0;
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint32_t sy = lane + 64 * k;
+        if (H.hist[sy]) {
+            ++present;
+            maxs = sy;
+        }
+    }
+    const uint32_t nsym = ufl(wave_sum(present)), maxsym = ufl(wave_max(maxs));
+    if (nsym == 1) { // RLE: 3-byte header (20-bit size) + the byte
+        if (lane == 0) {
+            dst[0] = (uint8_t)(0x0D | ((nlit & 0xF) << 4));
+            dst[1] = (uint8_t)(nlit >> 4);
+            dst[2] = (uint8_t)(nlit >> 12);
+            dst[3] = (uint8_t)maxsym;
+        }
+        return 4;
+    }
+    // leaves in ascending (count, symbol) order
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint32_t sy = lane + 64 * k, c = H.hist[sy];
+        if (!c) continue;
+        uint32_t rank = 0;
+        for (uint32_t t = 0; t <= maxsym; ++t) {
+            const uint32_t ct = H.hist[t];
+            rank += ct && (ct < c || (ct == c && t < sy));
+        }
+        H.len[rank] = (int32_t)c;
+        H.sym[rank] = (uint8_t)sy;
+    }
+    __syncthreads();
+    if (lane == 0) {
+        huf_lengths(H.len, (int)nsym);
+        uint32_t mb = 0;
+        for (uint32_t i = 0; i < nsym; ++i) mb = max(mb, (uint32_t)H.len[i]);
+        for (uint32_t sy = 0; sy < 256; ++sy) H.code[sy] = 0;
+        for (uint32_t i = 0; i < nsym; ++i) H.code[H.sym[i]] = (uint32_t)H.len[i] << 16;
+        // canonical values (HUF_buildCTable): longest codes first from 0, symbol order within a length
+        uint32_t per[ZHUF_MAXBITS + 2] = {0}, start[ZHUF_MAXBITS + 2] = {0};
+        for (uint32_t i = 0; i < nsym; ++i) ++per[H.len[i]];
+        uint32_t m = 0;
+        for (uint32_t nb = mb; nb > 0; --nb) {
+            start[nb] = m;
+            m += per[nb];
+            m >>= 1;
+        }
+        for (uint32_t sy = 0; sy <= maxsym; ++sy) {
+            const uint32_t nb = H.code[sy] >> 16;
+            if (nb) H.code[sy] |= start[nb]++;
+        }
+        H.maxbits = mb;
+    }
+    __syncthreads();
+    const uint32_t mb = ufl(H.maxbits);
+    // exact payload bits: is it worth it
+    uint32_t tb = 0;
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint32_t sy = lane + 64 * k;
+        tb += H.hist[sy] * (H.code[sy] >> 16);
+    }
+    tb = ufl(wave_sum(tb));
+    const bool four = nlit >= 256;
+    const uint32_t hdr = four ? 5 : 3, nw = maxsym;
+    __syncthreads(); // every lane has read H.hist
+    uint32_t tree = 0;
+    if (lane == 0) tree = huf_weights_fse(dst + hdr, H, S, nw, mb);
+    tree = ufl(tree);
+    const bool direct = tree == 0;
+    if (direct) {
+        if (nw > 128) return raw_literals(lt, nlit, dst);
+        tree = 1 + (nw + 1) / 2;
+    }
+    const uint32_t est = hdr + tree + (four ? 6 : 0) + tb / 8 + 4;
+    if (est >= 3 + nlit) return raw_literals(lt, nlit, dst);
+    // direct tree description: header byte 127 + weights, then 4-bit weights (high nibble first)
+    if (direct && lane == 0) dst[hdr] = (uint8_t)(127 + nw);
+    for (uint32_t j = lane; direct && j < (nw + 1) / 2; j += 64) {
+        uint32_t w2[2];
+        for (uint32_t h = 0; h < 2; ++h) {
+            const uint32_t sy = 2 * j + h, nb = sy < nw ? H.code[sy] >> 16 : 0;
+            w2[h] = nb ? mb + 1 - nb : 0;
+        }
+        dst[hdr + 1 + j] = (uint8_t)((w2[0] << 4) | w2[1]);
+    }
+    uint32_t at = hdr + tree;
+    uint32_t csz;
+    if (four) {
+        const uint32_t seg = (nlit + 3) / 4;
+        uint32_t sz[4];
+        at += 6;
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t a = k * seg, b = k == 3 ? nlit : a + seg;
+            sz[k] = huf_stream(lt, a, b, dst + at, H);
+            at += sz[k];
+        }
+        if (lane < 3) {
+            dst[hdr + tree + 2 * lane] = (uint8_t)sz[lane == 0 ? 0 : lane == 1 ? 1 : 2];
+            dst[hdr + tree + 2 * lane + 1] = (uint8_t)(sz[lane == 0 ? 0 : lane == 1 ? 1 : 2] >> 8);
+        }
+        csz = at - hdr;
+        if (lane == 0) { // compressed, 4 streams, 18-bit sizes: 5-byte header
+            const uint64_t v = 2u | (3u << 2) | ((uint64_t)nlit << 4) | ((uint64_t)csz << 22);
+            for (int q = 0; q < 5; ++q) dst[q] = (uint8_t)(v >> (8 * q));
+        }
+    } else {
+        at += huf_stream(lt, 0, nlit, dst + at, H);
+        csz = at - hdr;
+        if (lane == 0) { // compressed, 1 stream, 10-bit sizes: 3-byte header
+            const uint32_t v = 2u | (nlit << 4) | (csz << 14);
+            for (int q = 0; q < 3; ++q) dst[q] = (uint8_t)(v >> (8 * q));
+        }
+    }
+    return at;
+}
+
+// LDS of one encode wave: the match finder's tables, then (dead by then) the coders' state
+union ZEncLds {
+    struct {
+        uint16_t tpos[1 << ZE_HASH];
+        uint32_t tseq[1 << ZE_HASH];
+    } m;
+    struct {
+        ZHufLds H;
+        ZSeqLds S;
+    } c;
+};
 
 // The table of kind k for the nseq sequences counted in S.hist[k] (lane 0): RLE when one code is
 // used, else a description of the counts when it costs fewer bits than the predefined
@@ -663,7 +750,7 @@ __global__ void __launch_bounds__(64) zstd_encode_kernel(const uint8_t *src, uin
     ZSeqLds &S = E.c.S;
     uint32_t csize = 0;
     bool comp = false;
-    if (nseq > 0 && 3 + nlit / 4 < len) {
+    if (3 + nlit / 4 < len) {
         // code counts and the extra bits of the sequences
         for (uint32_t i = lane; i < 3 * 64; i += 64) (&S.hist[0][0])[i] = 0;
         __syncthreads();
@@ -678,6 +765,8 @@ __global__ void __launch_bounds__(64) zstd_encode_kernel(const uint8_t *src, uin
         }
         ex = ufl(wave_sum(ex));
         __syncthreads();
+        const uint32_t lsz = literal_section(lt, nlit, content, H, S);
+        __syncthreads();
         if (lane == 0)
             for (int k = 0; k < 3; ++k) zenc_choose(S, k, nseq);
         __syncthreads();
@@ -685,14 +774,18 @@ __global__ void __launch_bounds__(64) zstd_encode_kernel(const uint8_t *src, uin
             if (ufl(S.mode[k]) == 0)
                 for (uint32_t i = lane; i < sizeof(ZEncFse) / 4; i += 64)
                     ((uint32_t *)&S.t[k])[i] = ((const uint32_t *)&tabs->t[k])[i];
-        const uint32_t lsz = literal_section(lt, nlit, content, H);
+        __syncthreads();
         const uint32_t nsh = nseq < 128 ? 1 : 2;
         const uint32_t d0 = ufl(S.desc_n[0]), d1 = ufl(S.desc_n[1]), d2 = ufl(S.desc_n[2]);
         const uint32_t lg0 = ufl(S.log[0]), lg1 = ufl(S.log[1]), lg2 = ufl(S.log[2]);
-        const uint32_t hdr = nsh + 1 + d0 + d1 + d2;
+        const uint32_t hdr = nseq ? nsh + 1 + d0 + d1 + d2 : 1;
         const uint64_t bits = ex + (uint64_t)nseq * (lg0 + lg1 + lg2) + 1;
-        const uint64_t bound = lsz + hdr + (bits + 7) / 8;
-        if (bound < len) {
+        const uint64_t bound = lsz + hdr + (nseq ? (bits + 7) / 8 : 0);
+        if (bound < len && !nseq) { // literals only: the sequence section is its count
+            comp = true;
+            if (lane == 0) content[lsz] = 0;
+            csize = lsz + 1;
+        } else if (bound < len) {
             comp = true;
             uint8_t *h = content + lsz;
             if (lane == 0) {

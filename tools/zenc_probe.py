@@ -24,6 +24,7 @@ def payloads():
     yield "Float64 prices", np.round(rng.random(mb // 8) * 1000, 2).tobytes()
     words = [b"alpha", b"beta", b"gamma", b"delta", b"epsilon", b"zeta", b"eta", b"theta"]
     yield "text-ish", b" ".join(words[i] for i in rng.integers(0, 8, mb // 6).tolist())[:mb]
+    yield "geometric bytes", (rng.geometric(0.02, mb) % 256).astype(np.uint8).tobytes()
 
 
 def zstd1(raw):
@@ -38,6 +39,43 @@ def zstd1(raw):
         c = raw[i:i + 65536]
         total += z.ZSTD_compress(out, ctypes.c_size_t(70000), c, ctypes.c_size_t(len(c)), 1) + 9
     return total
+
+
+def frame_stats(pkt: bytes):
+    """block / literal / sequence-table modes of the sender's frames (one block each)"""
+    from collections import Counter
+    st, pos = Counter(), 0
+    while pos < len(pkt):
+        fb = int.from_bytes(pkt[pos + 1:pos + 5], "little")
+        c = pkt[pos + 18:pos + fb]
+        bh = int.from_bytes(c[:3], "little")
+        c = c[3:]
+        btype = (bh >> 1) & 3
+        if btype == 0:
+            st["raw block"] += 1
+        else:
+            lt, fmt = c[0] & 3, (c[0] >> 2) & 3
+            if lt == 0:
+                st["lit raw"] += 1
+                lsz = 3 + (int.from_bytes(c[:3], "little") >> 4)
+            elif lt == 1:
+                st["lit rle"] += 1
+                lsz = 4
+            else:
+                h = 5 if fmt == 3 else 4 if fmt == 2 else 3
+                v = int.from_bytes(c[:h], "little")
+                csz = (v >> 22) & 0x3FFFF if fmt == 3 else (v >> 14) & 0x3FF
+                st["lit huf " + ("fse" if c[h] < 128 else "direct")] += 1
+                lsz = h + csz
+            q = c[lsz:]
+            ns = q[0] if q[0] < 128 else ((q[0] - 128) << 8) + q[1]
+            if ns:
+                m = q[1 if q[0] < 128 else 2]
+                st["seq modes %d%d%d" % (m >> 6, (m >> 4) & 3, (m >> 2) & 3)] += 1
+            else:
+                st["no sequences"] += 1
+        pos += fb
+    return dict(st)
 
 
 def main():
@@ -58,7 +96,7 @@ def main():
                 assert torch.equal(tfa.codec_decompress(ctx, z), pkt), name
                 lz = tfa.codec_compress(ctx, pkt).numel()
                 print(f"  {name:24s} zstd {len(raw) / z.numel():6.3f}  libzstd-1 {len(raw) / ref if ref else 0:6.3f}"
-                      f"  lz4 {len(raw) / lz:6.3f}")
+                      f"  lz4 {len(raw) / lz:6.3f}  {frame_stats(z.cpu().numpy().tobytes())}")
             pkt = torch.frombuffer(bytearray(b"\x02" + big), dtype=torch.uint8).to("cuda")
             ts = []
             for _ in range(5):
