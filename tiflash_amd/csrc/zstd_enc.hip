@@ -6,8 +6,9 @@
 //
 // A frame (RFC 8878): magic, a single-segment header with a 4-byte content size, one block.  The
 // block is compressed when that is smaller, raw otherwise:
-//   matcher   LZ77 over the frame, lanes in lockstep: 4-byte hash into an LDS table (the LZ4
-//             sender's match finder), matches extended 64 bytes per step by a ballot; literal
+//   matcher   LZ77 over the frame, 64 positions per step (one a lane: 4-byte hash, LDS table
+//             slot read, candidates taken in order), matches extended 64 bytes per step by a
+//             ballot; literal
 //             bytes and sequences {ll, ml, offset value} to a per-frame work area (an offset
 //             equal to the previous one with literals before it is sent as repeat code 1)
 //   literals  Huffman (histogram by LDS atomics, leaves ranked by the wave, minimum-redundancy
@@ -32,12 +33,13 @@ namespace {
 
 using namespace tfz;
 
-// match finder: 2^11 table entries and matches of >= 5 bytes; measured on 4 MB payloads and
+// match finder: 2^10 table entries and matches of >= 5 bytes; measured on 4 MB payloads and
 // 256 MB of k%08d rows (tools/zenc_probe.py): 11/5 ratio 2.405 at 7.45 GB/s, 11/4 2.227 at 7.35,
 // 12/4 2.145 at 5.14, 12/5 2.394 at 5.29, 13/5 2.384 at 2.89, 12/6 2.323 at 4.96 (libzstd -1:
-// 2.501); shorter matches cost more sequence bits than the literals they replace
+// 2.501); shorter matches cost more sequence bits than the literals they replace.  10 bits
+// (8.7 KB of LDS a wave: every frame of a 256 MB packet resident at once) 2.391 at 9.54 GB/s.
 #ifndef TFG_ZE_HASH
-#define TFG_ZE_HASH 11
+#define TFG_ZE_HASH 10
 #endif
 #ifndef TFG_ZE_MINMATCH
 #define TFG_ZE_MINMATCH 5
@@ -45,9 +47,9 @@ using namespace tfz;
 constexpr int ZE_HASH = TFG_ZE_HASH;         // match-finder table bits
 constexpr uint32_t ZE_MINMATCH = TFG_ZE_MINMATCH; // shorter matches stay literals
 
-// FSE compression table (FSE_buildCTable's stateTable / symbolTT), accuracy log <= 9
+// FSE compression table (FSE_buildCTable's stateTable / symbolTT), accuracy log <= 8
 struct ZEncFse {
-    uint16_t state[512];
+    uint16_t state[256];
     int32_t dnb[53]; // deltaNbBits
     int32_t dfs[53]; // deltaFindState
 };
@@ -55,7 +57,7 @@ struct ZEncTables { // the predefined LL / OF / ML distributions (kind 0 / 1 / 2
     ZEncFse t[3];
 };
 constexpr int ZE_DEF_LOG[3] = {6, 5, 6};  // predefined accuracy logs
-constexpr int ZE_MAX_LOG[3] = {9, 8, 9};  // largest accuracy logs a description may carry
+constexpr int ZE_MAX_LOG[3] = {8, 8, 8};  // largest accuracy logs written (the format allows 9 / 8 / 9)
 constexpr int ZE_NSYM[3] = {36, 32, 53};  // code alphabet sizes
 constexpr uint32_t ZE_CUSTOM_MIN = 32;    // fewer sequences: no table descriptions
 
@@ -64,7 +66,7 @@ ZHD int16_t zdef_norm(int kind, int s) {
 }
 
 // The table of a distribution norm[0, nsym) (> 0 or -1 entries; sum 2^log).  The spread is the
-// decoder's (fse_build): -1 symbols at the top, the rest stepped through the table.  sym_at: 512
+// decoder's (fse_build): -1 symbols at the top, the rest stepped through the table.  sym_at: 256
 // bytes, cumul: 54 words of work space.
 ZHD void zenc_build(ZEncFse &t, const int16_t *norm, int nsym, int log, uint8_t *sym_at, uint32_t *cumul) {
     const int size = 1 << log, mask = size - 1, step = (size >> 1) + (size >> 3) + 3;
@@ -108,7 +110,7 @@ ZHD void zenc_build(ZEncFse &t, const int16_t *norm, int nsym, int log, uint8_t 
 __global__ void zenc_tables_kernel(ZEncTables *t) {
     if (threadIdx.x == 0 && blockIdx.x == 0) {
         int16_t norm[53];
-        uint8_t sym_at[512];
+        uint8_t sym_at[256];
         uint32_t cumul[54];
         for (int k = 0; k < 3; ++k) {
             for (int s = 0; s < 53; ++s) norm[s] = zdef_norm(k, s);
@@ -140,25 +142,6 @@ __device__ __forceinline__ uint32_t zml_code(uint32_t ml) {
     if (m < 96) return 40 + ((m - 64) >> 4);
     return 42;
 }
-
-// register window over the frame: lane l holds src[base + l] (0 past `end`)
-struct EWin {
-    const uint8_t *src;
-    uint32_t end;
-    uint32_t base = ~0u;
-    uint32_t v = 0;
-    __device__ __forceinline__ uint32_t word(uint32_t p) {
-        if (p < base || p + 4 > base + 64) {
-            base = p;
-            const uint32_t q = p + __lane_id();
-            v = q < end ? src[q] : 0u;
-        }
-        const int r = (int)(p - base);
-        return (uint32_t)__builtin_amdgcn_readlane((int)v, r) | ((uint32_t)__builtin_amdgcn_readlane((int)v, r + 1) << 8) |
-               ((uint32_t)__builtin_amdgcn_readlane((int)v, r + 2) << 16) |
-               ((uint32_t)__builtin_amdgcn_readlane((int)v, r + 3) << 24);
-    }
-};
 
 __device__ __forceinline__ uint32_t wave_incl(uint32_t x) { // inclusive prefix sum over the wave
     const uint32_t lane = __lane_id();
@@ -309,7 +292,7 @@ struct ZSeqLds {
     int16_t norm[3][64];    // a custom distribution
     uint8_t desc[3][128];   // its description (mode 2) or the RLE code (mode 1)
     uint32_t desc_n[3], log[3], mode[3];
-    uint8_t sym_at[512];
+    uint8_t sym_at[256];
     uint32_t cumul[64];
 };
 
@@ -668,6 +651,18 @@ __device__ void zenc_choose(ZSeqLds &S, int k, uint32_t nseq) {
     zenc_build(S.t[k], norm, maxs + 1, L, S.sym_at, S.cumul);
 }
 
+#ifdef TFG_ZE_PROF // development: per-phase wall-clock totals over the frames (tools/zenc_probe.py)
+__device__ unsigned long long g_zprof[8];
+#define ZPROF(i)                                                                                   \
+    do {                                                                                           \
+        const uint64_t t1_ = wall_clock64();                                                       \
+        if (lane == 0) atomicAdd(&g_zprof[i], (unsigned long long)(t1_ - t0_));                    \
+        t0_ = t1_;                                                                                 \
+    } while (0)
+#else
+#define ZPROF(i) ((void)0)
+#endif
+
 // One wave (= one workgroup) per frame: the packet frame (9-byte header + ZSTD frame) to
 // out + f * ZE_SLOT, its size to sizes[f].  tmp: 2 * ZE_FRAME bytes per frame, the literal bytes
 // from the front and the sequence list from the back (a sequence covers >= 4 bytes, so
@@ -678,6 +673,9 @@ __global__ void __launch_bounds__(64) zstd_encode_kernel(const uint8_t *src, uin
     const uint64_t f = blockIdx.x;
     if (f >= nframes) return;
     const uint32_t lane = __lane_id();
+#ifdef TFG_ZE_PROF
+    uint64_t t0_ = wall_clock64();
+#endif
     uint16_t *tpos = E.m.tpos;
     uint32_t *tseq = E.m.tseq;
     for (int i = lane; i < (1 << ZE_HASH); i += 64) {
@@ -700,50 +698,95 @@ __global__ void __launch_bounds__(64) zstd_encode_kernel(const uint8_t *src, uin
     };
     uint32_t anchor = 0;
     if (len >= 8) {
-        EWin win{s, len};
-        const uint32_t last = len - 3; // a match needs 4 readable bytes
-        uint32_t ip = 0, misses = 1u << 6;
-        while (ip < last) {
-            const uint32_t w = win.word(ip);
+        // 64 positions at a time, one a lane: every lane hashes the 4 bytes at its position and
+        // reads its table slot at once; the candidates (4 bytes verified against the slot's
+        // copy) are then taken in order, each extended 64 bytes per step by a ballot; the
+        // chunk's positions enter the table after it is read (a match's source lies in an
+        // earlier chunk, or is the repeat offset)
+        const uint32_t last = len - 3; // positions with 4 readable bytes
+        uint32_t ip = 0;               // the cursor: next position not yet covered
+        uint32_t dry = 0;              // chunks since the last match
+        for (uint32_t cbase = 0; cbase < last;) {
+            const uint32_t pos = cbase + lane, cbase_ip0 = ip;
+            const bool valid = pos < last;
+            uint32_t w = 0;
+            if (valid) w = (uint32_t)s[pos] | ((uint32_t)s[pos + 1] << 8) | ((uint32_t)s[pos + 2] << 16) | ((uint32_t)s[pos + 3] << 24);
             const uint32_t h = (w * 2654435761u) >> (32 - ZE_HASH);
-            const uint32_t ref = tpos[h], rw = tseq[h];
-            __builtin_amdgcn_wave_barrier();
-            tpos[h] = (uint16_t)ip; // every lane writes the same value
-            tseq[h] = w;
-            __builtin_amdgcn_wave_barrier();
-            uint32_t ml = 0;
-            if (ref < ip && rw == w) {
-                ml = 4;
-                for (;;) { // extend 64 bytes per step
-                    const uint32_t a = ip + ml + lane;
-                    const bool eq = a < len && s[ref + ml + lane] == s[a];
+            // candidates: the table slot, and the repeat offset in force at the chunk's start
+            // (preferred: its offset costs a repeat code while it stays in force)
+            const uint32_t rep0 = rep;
+            uint32_t wr = ~w;
+            if (valid && pos >= rep0)
+                wr = (uint32_t)s[pos - rep0] | ((uint32_t)s[pos - rep0 + 1] << 8) | ((uint32_t)s[pos - rep0 + 2] << 16) |
+                     ((uint32_t)s[pos - rep0 + 3] << 24);
+            const uint32_t tref = tpos[h], rw = tseq[h];
+            const bool by_rep = valid && pos >= ip && wr == w;
+            const bool by_tab = valid && pos >= ip && tref < pos && rw == w && (!by_rep || tref != pos - rep0);
+            const uint64_t mrep = __ballot(by_rep), mtab = __ballot(by_tab);
+            uint64_t mask = mrep | mtab, covered = 0;
+            auto extend = [&](uint32_t at, uint32_t from) __attribute__((always_inline)) {
+                uint32_t ml = 4;
+                for (;;) { // 64 bytes per step
+                    const uint32_t x = at + ml + lane;
+                    const bool eq = x < len && s[from + ml + lane] == s[x];
                     const uint64_t neq = ~__ballot(eq);
                     if (neq == 0) {
                         ml += 64;
                         continue;
                     }
-                    ml += (uint32_t)__builtin_ctzll(neq);
-                    break;
+                    return ml + (uint32_t)__builtin_ctzll(neq);
                 }
-            }
-            if (ml >= ZE_MINMATCH) {
-                const uint32_t ll = ip - anchor, off = ip - ref;
-                copy_lits(anchor, ip);
+            };
+            while (mask) {
+                const uint32_t j = (uint32_t)__builtin_ctzll(mask);
+                const uint32_t at = cbase + j;
+                // the longer of the two candidates; the repeat offset when within a byte
+                const uint32_t ml_r = (mrep >> j) & 1 ? extend(at, at - rep0) : 0;
+                const uint32_t tfrom = (uint32_t)__builtin_amdgcn_readlane((int)tref, (int)j);
+                const uint32_t ml_t = (mtab >> j) & 1 ? extend(at, tfrom) : 0;
+                const bool use_rep = ml_r >= ZE_MINMATCH && ml_r + 1 >= ml_t;
+                const uint32_t ml = use_rep ? ml_r : ml_t, from = use_rep ? at - rep0 : tfrom;
+                if (ml < ZE_MINMATCH) {
+                    mask &= mask - 1;
+                    continue;
+                }
+                const uint32_t ll = at - anchor, off = at - from;
+                copy_lits(anchor, at);
                 uint32_t ofv = off + 3;
                 if (off == rep && ll > 0) ofv = 1; // repeat offset 1 (history unchanged)
                 rep = off;
                 if (lane == 0) seq_end[-1 - (int64_t)nseq] = make_uint2(ll | (ml << 16), ofv);
                 ++nseq;
-                ip += ml;
+                ip = at + ml;
                 anchor = ip;
-                misses = 1u << 6;
-            } else {
-                ip += misses++ >> 6; // skip acceleration on incompressible runs
+                const uint64_t after = j == 63 ? 0ull : ~0ull << (j + 1); // lanes past the match start
+                if (ip >= cbase + 64) {
+                    covered |= after;
+                    break;
+                }
+                covered |= after & ((1ull << (ip - cbase)) - 1);
+                mask &= ~0ull << (ip - cbase); // candidates inside the match are covered
             }
+            // the chunk's positions enter the table (one of the lanes sharing a slot wins), but
+            // not those inside its matches (a slot keeps an older entry rather than a position
+            // no search starts from); after chunks without a match only every stride-th, the
+            // stride doubling every two dry chunks up to 64, so incompressible stretches do not
+            // flush the older entries.  Measured (tools/zenc_probe.py, 4 MB, ratio): all
+            // positions: k%08d 2.402, Int64 3.40, text 5.30; without those inside matches 2.392,
+            // 3.75, 4.92 — Int64 columns weigh more in packets than prose.
+            dry = ip > cbase_ip0 ? 0 : dry + 1;
+            const uint32_t stride = 1u << min(6u, dry >> 1);
+            if (valid && !((covered >> lane) & 1) && (pos & (stride - 1)) == 0) {
+                tpos[h] = (uint16_t)pos;
+                tseq[h] = w;
+            }
+            __builtin_amdgcn_wave_barrier();
+            cbase = max(cbase + 64, ip);
         }
     }
     copy_lits(anchor, len);
     __syncthreads(); // the literal / list stores land before they are read back; the match tables are dead
+    ZPROF(0);
 
     // ---- block: compressed when its size bound is below the raw size
     ZHufLds &H = E.c.H;
@@ -765,8 +808,10 @@ __global__ void __launch_bounds__(64) zstd_encode_kernel(const uint8_t *src, uin
         }
         ex = ufl(wave_sum(ex));
         __syncthreads();
+        ZPROF(1);
         const uint32_t lsz = literal_section(lt, nlit, content, H, S);
         __syncthreads();
+        ZPROF(2);
         if (lane == 0)
             for (int k = 0; k < 3; ++k) zenc_choose(S, k, nseq);
         __syncthreads();
@@ -775,6 +820,7 @@ __global__ void __launch_bounds__(64) zstd_encode_kernel(const uint8_t *src, uin
                 for (uint32_t i = lane; i < sizeof(ZEncFse) / 4; i += 64)
                     ((uint32_t *)&S.t[k])[i] = ((const uint32_t *)&tabs->t[k])[i];
         __syncthreads();
+        ZPROF(3);
         const uint32_t nsh = nseq < 128 ? 1 : 2;
         const uint32_t d0 = ufl(S.desc_n[0]), d1 = ufl(S.desc_n[1]), d2 = ufl(S.desc_n[2]);
         const uint32_t lg0 = ufl(S.log[0]), lg1 = ufl(S.log[1]), lg2 = ufl(S.log[2]);
@@ -804,7 +850,7 @@ __global__ void __launch_bounds__(64) zstd_encode_kernel(const uint8_t *src, uin
             uint64_t bc = 0;
             uint32_t bn = 0, wp = 0;
             auto add = [&](uint32_t v, uint32_t nb) __attribute__((always_inline)) {
-                bc |= (uint64_t)(v & ((1u << nb) - 1)) << bn;
+                bc |= ((uint64_t)v & ((1ull << nb) - 1)) << bn; // nb <= 32
                 bn += nb;
                 if (bn >= 32) {
                     if (lane < 4) bs[wp + lane] = (uint8_t)(bc >> (8 * lane));
@@ -813,56 +859,64 @@ __global__ void __launch_bounds__(64) zstd_encode_kernel(const uint8_t *src, uin
                     bn -= 32;
                 }
             };
-            uint32_t vx = 0, vy = 0;
+            // 64 sequences at a time, one a lane: codes, extra bits (LL, ML, OF packed low to
+            // high) and the three codes' table entries, so the serial walk below only chains
+            // the states and appends bits
+            uint32_t vc = 0, velo = 0, vehi = 0;
+            int32_t vdnb0 = 0, vdnb1 = 0, vdnb2 = 0, vdfs0 = 0, vdfs1 = 0, vdfs2 = 0;
             int64_t bbase = -1;
-            auto get = [&](uint32_t q, uint32_t &ll, uint32_t &ml, uint32_t &ofv) __attribute__((always_inline)) {
-                if (bbase < 0 || (int64_t)q < bbase) {
-                    bbase = q & ~63u;
-                    const uint32_t i = (uint32_t)bbase + lane;
-                    const uint2 v = i < nseq ? seq_end[-1 - (int64_t)i] : make_uint2(0, 0);
-                    vx = v.x;
-                    vy = v.y;
-                }
-                const int r = (int)(q - (uint32_t)bbase);
-                const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)vx, r);
-                ll = x & 0xFFFF;
-                ml = x >> 16;
-                ofv = (uint32_t)__builtin_amdgcn_readlane((int)vy, r);
+            auto load = [&](uint32_t q) __attribute__((always_inline)) {
+                bbase = q & ~63u;
+                const uint32_t i = (uint32_t)bbase + lane;
+                const uint2 v = i < nseq ? seq_end[-1 - (int64_t)i] : make_uint2(3u << 16, 4);
+                const uint32_t ll = v.x & 0xFFFF, ml = v.x >> 16, ofv = v.y;
+                const uint32_t llc = zll_code(ll), mlc = zml_code(ml), ofc = (uint32_t)zhb(ofv);
+                const uint32_t llb = (uint32_t)ll_bits((int)llc), mlb = (uint32_t)ml_bits((int)mlc);
+                const uint64_t e = (uint64_t)(ll - ll_base((int)llc)) | ((uint64_t)(ml - ml_base((int)mlc)) << llb) |
+                                   ((uint64_t)(ofv - (1u << ofc)) << (llb + mlb));
+                velo = (uint32_t)e;
+                vehi = (uint32_t)(e >> 32);
+                vc = llc | (mlc << 8) | (ofc << 16) | ((llb + mlb + ofc) << 24);
+                vdnb0 = S.t[0].dnb[llc];
+                vdfs0 = S.t[0].dfs[llc];
+                vdnb1 = S.t[1].dnb[ofc];
+                vdfs1 = S.t[1].dfs[ofc];
+                vdnb2 = S.t[2].dnb[mlc];
+                vdfs2 = S.t[2].dfs[mlc];
             };
-            auto init = [&](const ZEncFse &t, uint32_t sym) __attribute__((always_inline)) {
-                const int32_t dnb = __builtin_amdgcn_readfirstlane(t.dnb[sym]);
-                const int32_t dfs = __builtin_amdgcn_readfirstlane(t.dfs[sym]);
+            auto rl = [&](int32_t v, int r) __attribute__((always_inline)) { return __builtin_amdgcn_readlane(v, r); };
+            auto extras = [&](int r, uint32_t eb) __attribute__((always_inline)) {
+                const uint32_t lo = (uint32_t)rl((int32_t)velo, r);
+                if (eb <= 32) {
+                    add(lo, eb);
+                } else {
+                    add(lo, 32);
+                    add((uint32_t)rl((int32_t)vehi, r), eb - 32);
+                }
+            };
+            auto init = [&](const ZEncFse &t, int32_t dnb, int32_t dfs) __attribute__((always_inline)) {
                 const uint32_t nb = (uint32_t)(dnb + (1 << 15)) >> 16;
                 const uint32_t v = (nb << 16) - (uint32_t)dnb;
                 return ufl(t.state[(v >> nb) + dfs]);
             };
-            auto enc = [&](const ZEncFse &t, uint32_t &st, uint32_t sym) __attribute__((always_inline)) {
-                const int32_t dnb = __builtin_amdgcn_readfirstlane(t.dnb[sym]);
-                const int32_t dfs = __builtin_amdgcn_readfirstlane(t.dfs[sym]);
+            auto enc = [&](const ZEncFse &t, uint32_t &st, int32_t dnb, int32_t dfs) __attribute__((always_inline)) {
                 const uint32_t nb = (st + (uint32_t)dnb) >> 16;
                 add(st, nb);
                 st = ufl(t.state[(st >> nb) + dfs]);
             };
-            auto extras = [&](uint32_t ll, uint32_t llc, uint32_t ml, uint32_t mlc, uint32_t ofv, uint32_t ofc)
-                __attribute__((always_inline)) {
-                    add(ll - ll_base((int)llc), (uint32_t)ll_bits((int)llc));
-                    add(ml - ml_base((int)mlc), (uint32_t)ml_bits((int)mlc));
-                    add(ofv - (1u << ofc), ofc);
-                };
-            uint32_t ll, ml, ofv;
-            get(nseq - 1, ll, ml, ofv);
-            uint32_t llc = zll_code(ll), mlc = zml_code(ml), ofc = (uint32_t)zhb(ofv);
-            uint32_t s_ml = init(S.t[2], mlc), s_of = init(S.t[1], ofc), s_ll = init(S.t[0], llc);
-            extras(ll, llc, ml, mlc, ofv, ofc);
+            load(nseq - 1);
+            int r = (int)(nseq - 1 - (uint32_t)bbase);
+            uint32_t s_ml = init(S.t[2], rl(vdnb2, r), rl(vdfs2, r));
+            uint32_t s_of = init(S.t[1], rl(vdnb1, r), rl(vdfs1, r));
+            uint32_t s_ll = init(S.t[0], rl(vdnb0, r), rl(vdfs0, r));
+            extras(r, (uint32_t)rl((int32_t)vc, r) >> 24);
             for (int64_t q = (int64_t)nseq - 2; q >= 0; --q) {
-                get((uint32_t)q, ll, ml, ofv);
-                llc = zll_code(ll);
-                mlc = zml_code(ml);
-                ofc = (uint32_t)zhb(ofv);
-                enc(S.t[1], s_of, ofc);
-                enc(S.t[2], s_ml, mlc);
-                enc(S.t[0], s_ll, llc);
-                extras(ll, llc, ml, mlc, ofv, ofc);
+                if (q < bbase) load((uint32_t)q);
+                r = (int)(q - bbase);
+                enc(S.t[1], s_of, rl(vdnb1, r), rl(vdfs1, r));
+                enc(S.t[2], s_ml, rl(vdnb2, r), rl(vdfs2, r));
+                enc(S.t[0], s_ll, rl(vdnb0, r), rl(vdfs0, r));
+                extras(r, (uint32_t)rl((int32_t)vc, r) >> 24);
             }
             add(s_ml, lg2);
             add(s_of, lg1);
@@ -872,6 +926,7 @@ __global__ void __launch_bounds__(64) zstd_encode_kernel(const uint8_t *src, uin
             if (lane < tail) bs[wp + lane] = (uint8_t)(bc >> (8 * lane));
             wp += tail;
             csize = lsz + hdr + wp;
+            ZPROF(4);
         }
     }
     __syncthreads();
@@ -895,6 +950,7 @@ __global__ void __launch_bounds__(64) zstd_encode_kernel(const uint8_t *src, uin
         frame[13] = 0xA0;
         sizes[f] = fbytes;
     }
+    ZPROF(5);
 }
 
 } // namespace
@@ -917,5 +973,14 @@ int zstd_encode_frames(Ctx *ctx, const uint8_t *body, uint64_t n, uint64_t nfram
     TFG_LAUNCH_CHECK();
     return TFG_OK;
 }
+
+#ifdef TFG_ZE_PROF
+extern "C" int tfg_zenc_prof(unsigned long long *out) { // reads and clears the phase totals
+    TFG_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_zprof), sizeof(g_zprof)));
+    static const unsigned long long zero[8] = {0};
+    TFG_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_zprof), zero, sizeof(zero)));
+    return 0;
+}
+#endif
 
 } // namespace tfg

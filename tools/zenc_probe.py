@@ -99,6 +99,8 @@ def main():
                       f"  lz4 {len(raw) / lz:6.3f}  {frame_stats(z.cpu().numpy().tobytes())}")
             pkt = torch.frombuffer(bytearray(b"\x02" + big), dtype=torch.uint8).to("cuda")
             ts = []
+            if hasattr(tfa.lib(), "tfg_zenc_prof"):
+                tfa.lib().tfg_zenc_prof((ctypes.c_ulonglong * 8)())
             for _ in range(5):
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
@@ -106,6 +108,14 @@ def main():
                 torch.cuda.synchronize()
                 ts.append(time.perf_counter() - t0)
             t = sorted(ts)[2]
+            L = tfa.lib()
+            if hasattr(L, "tfg_zenc_prof"):  # a TFG_ZE_PROF build: phase totals over the last 5 calls
+                ph = (ctypes.c_ulonglong * 8)()
+                L.tfg_zenc_prof(ph)
+                names = ["match", "seq counts", "literals", "tables", "sequences", "headers"]
+                tot = sum(ph[:6]) or 1
+                print("  phases (share of wave time): " + ", ".join(f"{n} {ph[i] / tot:.1%}" for i, n in enumerate(names)))
+                print(f"  per frame: {tot / 100e6 / (5 * ((len(big) + 65535) // 65536)) * 1e6:.1f} us of wave time")
             print(f"  256 MB k%08d rows: ratio {len(big) / z.numel():.3f}, compress {t * 1e3:.2f} ms, "
                   f"{len(big) / t / 1e9:.2f} GB/s", flush=True)
 
