@@ -16,11 +16,12 @@
 // compress and decompress in parallel — the reference's CompressedReadBuffer reads either.
 //
 // GPU design: one wave per frame for both directions, control flow uniform across the wave.
-//  * encode: the source streams through a 64-byte register window (lane l holds byte base + l,
-//    the 4-byte sequence at the cursor comes from readlanes); the match finder is LZ4's greedy
-//    single-probe hash table (4096 entries of {position, sequence} in LDS, so a candidate is
-//    verified without a global load) with LZ4's skip acceleration after 64 misses; match
-//    extension compares 64 bytes per step with a ballot; literals are copied by all lanes.
+//  * encode: 64 positions per step, one a lane: each lane hashes the 4 bytes at its position and
+//    reads its slot of a single-probe hash table ({position, sequence} entries in LDS, so a
+//    candidate is verified without a global load); the candidates are taken greedily in order,
+//    match extension compares 64 bytes per step with a ballot; the chunk's positions outside its
+//    matches then enter the table (sparser after chunks without a match, as LZ4's skip
+//    acceleration); literals are copied by all lanes.
 //  * decode: the token stream goes through the same register window; literal runs are copied by
 //    all lanes; a match copies lane i's byte from out[start - offset + i % offset], bytes written
 //    before the match began (other lanes' stores are drained and the loads bypass the L1).
@@ -37,11 +38,12 @@ constexpr uint8_t NONE_METHOD = 0x02;      // CompressionMethodByte::NONE
 constexpr int FRAME_HDR = 9;               // COMPRESSED_BLOCK_HEADER_SIZE
 constexpr uint64_t MAX_FRAME_RAW = 0x40000000ull; // DBMS_MAX_COMPRESSED_SIZE
 constexpr uint32_t ENC_FRAME = 64 * 1024;  // raw bytes per frame this encoder writes
-// match-finder table: 2^HASH_LOG x 6 B of LDS per frame.  11 bits (12 KB): 13 encode waves per CU
-// instead of 6 at 12 bits; measured on 256 MB of k%08d rows (tools/lz4_probe.py): 12 bits 8.6 GB/s
-// at ratio 1.371, 11 bits 12.1 GB/s at 1.320, 10 bits 17.8 GB/s at 1.266.
+// match-finder table: 2^HASH_LOG x 6 B of LDS per frame.  Measured on 256 MB of k%08d rows
+// (tools/lz4_probe.py) with the serial matcher (one position a step): 12 bits 8.6 GB/s at ratio
+// 1.371, 11 bits 12.1 GB/s at 1.320, 10 bits 17.8 GB/s at 1.266; with 64 positions a step: 11
+// bits 23.6 GB/s at 1.320, 10 bits 38.9 GB/s at 1.267 (6 KB: every frame of 256 MB resident).
 #ifndef TFG_LZ4_HASH_LOG
-#define TFG_LZ4_HASH_LOG 11
+#define TFG_LZ4_HASH_LOG 10
 #endif
 constexpr int HASH_LOG = TFG_LZ4_HASH_LOG;
 constexpr uint64_t ENC_SLOT = FRAME_HDR + ENC_FRAME + ENC_FRAME / 255 + 16; // header + LZ4_COMPRESSBOUND
@@ -94,7 +96,6 @@ __global__ void __launch_bounds__(64) lz4_encode_kernel(const uint8_t *src, uint
     uint8_t *frame = out + f * ENC_SLOT;
     uint8_t *o = frame + FRAME_HDR;
     uint32_t op = 0; // uniform output cursor
-    Window win{s, len};
     auto put_len = [&](uint32_t v) __attribute__((always_inline)) { // extension of a length field at 15
         v -= 15;
         while (v >= 255) {
@@ -124,21 +125,28 @@ __global__ void __launch_bounds__(64) lz4_encode_kernel(const uint8_t *src, uint
     };
     uint32_t anchor = 0;
     if (len >= MF_LIMIT + 1) {
+        // 64 positions per step, one a lane (as the ZSTD sender, zstd_enc.hip): every lane hashes
+        // the 4 bytes at its position and reads its table slot at once; the verified candidates
+        // are taken in order, each extended 64 bytes per step by a ballot; then the chunk's
+        // positions outside its matches enter the table (every stride-th after chunks without
+        // a match, so incompressible stretches keep older entries)
         const uint32_t mflimit = len - MF_LIMIT, matchlimit = len - LAST_LITERALS;
-        uint32_t ip = 0, misses = 1u << 6;
-        while (ip < mflimit) {
-            const uint32_t seq = win.word(ip);
-            const uint32_t h = (seq * 2654435761u) >> (32 - HASH_LOG);
-            const uint32_t ref = tpos[h], rseq = tseq[h];
-            __builtin_amdgcn_wave_barrier();
-            tpos[h] = (uint16_t)ip; // every lane writes the same value
-            tseq[h] = seq;
-            __builtin_amdgcn_wave_barrier();
-            if (ref < ip && rseq == seq) {
+        uint32_t ip = 0, dry = 0;
+        for (uint32_t cbase = 0; cbase < mflimit;) {
+            const uint32_t pos = cbase + lane, ip0 = ip;
+            const bool valid = pos < mflimit;
+            uint32_t w = 0;
+            if (valid) w = (uint32_t)s[pos] | ((uint32_t)s[pos + 1] << 8) | ((uint32_t)s[pos + 2] << 16) | ((uint32_t)s[pos + 3] << 24);
+            const uint32_t h = (w * 2654435761u) >> (32 - HASH_LOG);
+            const uint32_t ref = tpos[h], rw = tseq[h];
+            uint64_t mask = __ballot(valid && pos >= ip && ref < pos && rw == w), covered = 0;
+            while (mask) {
+                const uint32_t j = (uint32_t)__builtin_ctzll(mask);
+                const uint32_t at = cbase + j, from = (uint32_t)__builtin_amdgcn_readlane((int)ref, (int)j);
                 uint32_t ml = MIN_MATCH;
                 for (;;) { // extend 64 bytes per step
-                    const uint32_t a = ip + ml + lane;
-                    const bool eq = a < matchlimit && s[ref + ml + lane] == s[a];
+                    const uint32_t x = at + ml + lane;
+                    const bool eq = x < matchlimit && s[from + ml + lane] == s[x];
                     const uint64_t neq = ~__ballot(eq);
                     if (neq == 0) {
                         ml += 64;
@@ -147,13 +155,26 @@ __global__ void __launch_bounds__(64) lz4_encode_kernel(const uint8_t *src, uint
                     ml += (uint32_t)__builtin_ctzll(neq);
                     break;
                 }
-                emit(anchor, ip, ip - ref, ml);
-                ip += ml;
+                emit(anchor, at, at - from, ml);
+                ip = at + ml;
                 anchor = ip;
-                misses = 1u << 6;
-            } else {
-                ip += misses++ >> 6; // LZ4's skip acceleration on incompressible runs
+                const uint64_t after = j == 63 ? 0ull : ~0ull << (j + 1); // lanes past the match start
+                if (ip >= cbase + 64) {
+                    covered |= after;
+                    break;
+                }
+                covered |= after & ((1ull << (ip - cbase)) - 1);
+                mask &= ~0ull << (ip - cbase); // candidates inside the match are covered
             }
+            dry = ip > ip0 ? 0 : dry + 1;
+            const uint32_t stride = 1u << min(6u, dry >> 1);
+            __builtin_amdgcn_wave_barrier();
+            if (valid && !((covered >> lane) & 1) && (pos & (stride - 1)) == 0) { // one of a slot's lanes wins
+                tpos[h] = (uint16_t)pos;
+                tseq[h] = w;
+            }
+            __builtin_amdgcn_wave_barrier();
+            cbase = max(cbase + 64, ip);
         }
     }
     emit(anchor, len, 0, 0); // last literals
