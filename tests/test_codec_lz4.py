@@ -203,3 +203,20 @@ def test_gpu_codec_decode_lz4_packets(tfa, orc, ctx, dev, n):
     assert orc.lz4_packet_decompress(host_bytes(lz)) == plain
     rows, dec = tfa.codec_decode(ctx, lz, version=V1)
     assert_decoded(cols, n, rows, dec)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("frame", [0, 1000, 7000, 65536, 300_000])
+def test_gpu_decompress_frame_table_shapes(tfa, orc, ctx, dev, frame):
+    """The frame table of a multi-segment packet (the segmented parse, lz4.hip frames_seg_kernel /
+    frames_join_kernel, falling back to the serial walk): one frame, frames smaller than the
+    parse's per-segment capacity allows, frames of a few KB, 64 KB and larger than a segment."""
+    rng = np.random.default_rng(frame + 3)
+    raw = b"".join(b"key%06d,%d;" % (int(a), int(b)) for a, b in rng.integers(0, 5000, (120_000, 2)))
+    body = b"\x02" + raw
+    lz = orc.lz4_packet_compress(body, frame)
+    assert host_bytes(tfa.codec_decompress(ctx, dev_bytes(lz, dev))) == body
+    # a frame header forged inside the data of a later frame must not confuse the parse: the
+    # packet with one byte less is malformed and stays an error
+    with pytest.raises(tfa.TfgError):
+        tfa.codec_decompress(ctx, dev_bytes(lz[:-1], dev))

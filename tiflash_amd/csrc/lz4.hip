@@ -321,6 +321,162 @@ __global__ void __launch_bounds__(64) lz4_decode_kernel(const uint8_t *pkt, cons
     if (lane == 0 && (bad || op != raw)) atomicOr(err, 1u);
 }
 
+// ---- the frame table in parallel: the packet in 64 KB segments, one wave each, finds the first
+// plausible frame start of its segment (two chained headers with sane sizes, then the method byte
+// again) and walks the frames from there past its end; a second
+// kernel keeps the segments the true chain runs through — entering position = the prefix max of
+// the earlier segments' exits, a segment in use must have started exactly there — and writes the
+// table. Any disagreement, a malformed header or more than FSEG_CAP frames in a segment makes the
+// host run lz4_frames_kernel instead (which also gives malformed packets their error).
+constexpr uint64_t FSEG = 64 * 1024;
+constexpr uint32_t FSEG_CAP = 32;
+struct FSeg {
+    uint64_t first, exit, raw;
+    uint32_t n, flags; // flags: 1 = a start was found, 2 = give up (bad header / overflow)
+};
+
+__device__ __forceinline__ uint32_t pkt_u32(const uint8_t *p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+// the serial walk's header checks at pos (frame bytes / raw bytes out)
+__device__ __forceinline__ bool frame_ok(const uint8_t *pkt, uint64_t bytes, uint8_t method, uint64_t pos, uint32_t &fb,
+                                         uint32_t &rb) {
+    if (pos + FRAME_HDR > bytes || pkt[pos] != method) return false;
+    fb = pkt_u32(pkt + pos + 1);
+    rb = pkt_u32(pkt + pos + 5);
+    const uint64_t expand = method == LZ4_METHOD ? 255 : 32768;
+    return fb > FRAME_HDR && pos + fb <= bytes && rb <= MAX_FRAME_RAW &&
+           (uint64_t)rb <= (uint64_t)(fb - FRAME_HDR) * expand + 16;
+}
+
+__global__ void __launch_bounds__(64) frames_seg_kernel(const uint8_t *pkt, uint64_t bytes, uint8_t method, uint64_t nseg,
+                                                        FSeg *seg, uint64_t *sfo, uint32_t *srb) {
+    const uint64_t g = blockIdx.x;
+    if (g >= nseg) return;
+    const uint32_t lane = __lane_id();
+    const uint64_t s0 = g * FSEG, s1 = min(bytes, s0 + FSEG);
+    uint64_t first = g == 0 ? 0 : ~0ull;
+    for (uint64_t base = s0; g > 0 && base < s1; base += 64 * 16) {
+        const uint64_t q0 = base + lane * 16;
+        uint64_t found = ~0ull;
+        for (uint32_t b = 0; b < 16 && q0 + b < s1; ++b) {
+            const uint64_t q = q0 + b;
+            uint32_t fb, rb, fb2, rb2;
+            // two chained headers, then the method byte (or the end): a false start inside
+            // compressed bytes passes one header check about once per few MB, not two
+            if (pkt[q] == method && frame_ok(pkt, bytes, method, q, fb, rb) &&
+                (q + fb == bytes || (frame_ok(pkt, bytes, method, q + fb, fb2, rb2) &&
+                                     (q + fb + fb2 == bytes || pkt[q + fb + fb2] == method)))) {
+                found = q;
+                break;
+            }
+        }
+        const uint64_t any = __ballot(found != ~0ull);
+        if (any) {
+            first = (uint64_t)__shfl((long long)found, (int)__builtin_ctzll(any), 64);
+            break;
+        }
+    }
+    FSeg out{first, 0, 0, 0, 0};
+    if (first != ~0ull) {
+        out.flags = 1;
+        uint64_t pos = first;
+        while (pos < s1) {
+            uint32_t fb, rb;
+            if (!frame_ok(pkt, bytes, method, pos, fb, rb) || out.n >= FSEG_CAP) {
+                out.flags |= 2;
+                break;
+            }
+            if (lane == 0) {
+                sfo[g * FSEG_CAP + out.n] = pos;
+                srb[g * FSEG_CAP + out.n] = rb;
+            }
+            ++out.n;
+            out.raw += rb;
+            pos += fb;
+        }
+        out.exit = pos;
+    }
+    if (lane == 0) seg[g] = out;
+}
+
+// one 1024-thread workgroup; out = {frames, raw bytes, 0, fall back to the serial walk}
+__global__ void __launch_bounds__(1024) frames_join_kernel(const FSeg *seg, const uint64_t *sfo, const uint32_t *srb,
+                                                           uint64_t nseg, uint64_t bytes, uint64_t *foff, uint64_t *roff,
+                                                           uint64_t max_frames, uint64_t *out) {
+    __shared__ uint64_t a[1024], b[1024], c[1024];
+    __shared__ uint64_t carry_ent, carry_k, carry_raw;
+    __shared__ int fail;
+    const uint32_t t = threadIdx.x;
+    if (t == 0) {
+        carry_ent = 0;
+        carry_k = 0;
+        carry_raw = 0;
+        fail = 0;
+    }
+    __syncthreads();
+    for (uint64_t c0 = 0; c0 < nseg; c0 += 1024) {
+        const uint64_t g = c0 + t;
+        const bool in = g < nseg;
+        FSeg sg{};
+        if (in) sg = seg[g];
+        // exclusive prefix max of the exits (segments without a start exit at 0)
+        a[t] = in && (sg.flags & 1) ? sg.exit : 0;
+        __syncthreads();
+        for (uint32_t d = 1; d < 1024; d <<= 1) {
+            const uint64_t v = t >= d ? a[t - d] : 0;
+            __syncthreads();
+            a[t] = max(a[t], v);
+            __syncthreads();
+        }
+        const uint64_t ent = max(carry_ent, t ? a[t - 1] : 0);
+        const uint64_t s1 = min(bytes, g * FSEG + FSEG);
+        const bool used = in && ent < s1;
+        if (in && (sg.flags & 2)) fail = 1;
+        if (used && sg.first != ent) fail = 1;                     // started somewhere else
+        if (in && !used && (sg.flags & 1) && sg.exit > ent) fail = 1; // a false start ran past the chain
+        b[t] = used ? sg.n : 0;
+        c[t] = used ? sg.raw : 0;
+        __syncthreads();
+        for (uint32_t d = 1; d < 1024; d <<= 1) { // inclusive prefix sums
+            const uint64_t vb = t >= d ? b[t - d] : 0, vc = t >= d ? c[t - d] : 0;
+            __syncthreads();
+            b[t] += vb;
+            c[t] += vc;
+            __syncthreads();
+        }
+        if (used) {
+            uint64_t k = carry_k + b[t] - sg.n, r = carry_raw + c[t] - sg.raw;
+            for (uint32_t i = 0; i < sg.n; ++i, ++k) {
+                if (k < max_frames) {
+                    foff[k] = sfo[g * FSEG_CAP + i];
+                    roff[k] = r;
+                }
+                r += srb[g * FSEG_CAP + i];
+            }
+        }
+        __syncthreads();
+        if (t == 1023) {
+            carry_ent = max(carry_ent, a[1023]);
+            carry_k += b[1023];
+            carry_raw += c[1023];
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        const uint64_t k = carry_k;
+        const bool ok = !fail && carry_ent == bytes;
+        if (ok && k <= max_frames) {
+            foff[k] = bytes;
+            roff[k] = carry_raw;
+        }
+        out[0] = k;
+        out[1] = carry_raw;
+        out[2] = 0;
+        out[3] = ok ? 0 : 1;
+    }
+}
+
 int read_method(Ctx *ctx, const uint8_t *packet, uint8_t *m) {
     TFG_HIP(hipMemcpyAsync(ctx->host_pinned, packet, 1, hipMemcpyDeviceToHost, ctx->stream));
     TFG_HIP(hipStreamSynchronize(ctx->stream));
@@ -409,18 +565,40 @@ int tfg_codec_decompress(tfg_ctx *ctx, const uint8_t *packet, size_t bytes, uint
     uint64_t res[3] = {0, 0, 0};
     char *sb = nullptr;
     size_t o_foff = 0, o_roff = 0;
+    const uint64_t nseg = (bytes + FSEG - 1) / FSEG;
+    const bool parallel = nseg >= 4 && nseg < (1ull << 31);
     for (int attempt = 0; attempt < 2; ++attempt) {
         Carver cv;
         o_foff = cv.take<uint64_t>(max_frames + 1);
         o_roff = cv.take<uint64_t>(max_frames + 1);
         const size_t o_res = cv.take<uint64_t>(4);
+        const size_t o_seg = cv.take<FSeg>(parallel ? nseg : 0), o_sfo = cv.take<uint64_t>(parallel ? nseg * FSEG_CAP : 0);
+        const size_t o_srb = cv.take<uint32_t>(parallel ? nseg * FSEG_CAP : 0);
         void *sp;
         if (int rc = scratch_get(ctx, cv.off, &sp)) return rc;
         sb = (char *)sp;
-        hipLaunchKernelGGL(lz4_frames_kernel, dim3(1), dim3(64), 0, ctx->stream, packet, (uint64_t)bytes, m,
-                           (uint64_t *)(sb + o_foff), (uint64_t *)(sb + o_roff), max_frames, (uint64_t *)(sb + o_res));
-        TFG_LAUNCH_CHECK();
-        if (int rc = read_back_u64(ctx, (const uint64_t *)(sb + o_res), res, 3)) return rc;
+        uint64_t *dres = (uint64_t *)(sb + o_res);
+        bool serial = !parallel;
+        if (parallel) { // the segmented parse; the serial walk when it does not agree with itself
+            ProfScope _ps(ctx, "codec.frames");
+            hipLaunchKernelGGL(frames_seg_kernel, dim3((unsigned)nseg), dim3(64), 0, ctx->stream, packet, (uint64_t)bytes, m,
+                               nseg, (FSeg *)(sb + o_seg), (uint64_t *)(sb + o_sfo), (uint32_t *)(sb + o_srb));
+            TFG_LAUNCH_CHECK();
+            hipLaunchKernelGGL(frames_join_kernel, dim3(1), dim3(1024), 0, ctx->stream, (const FSeg *)(sb + o_seg),
+                               (const uint64_t *)(sb + o_sfo), (const uint32_t *)(sb + o_srb), nseg, (uint64_t)bytes,
+                               (uint64_t *)(sb + o_foff), (uint64_t *)(sb + o_roff), max_frames, dres);
+            TFG_LAUNCH_CHECK();
+            uint64_t r4[4] = {0, 0, 0, 0};
+            if (int rc = read_back_u64(ctx, dres, r4, 4)) return rc;
+            serial = r4[3] != 0;
+            for (int q = 0; q < 3; ++q) res[q] = r4[q];
+        }
+        if (serial) {
+            hipLaunchKernelGGL(lz4_frames_kernel, dim3(1), dim3(64), 0, ctx->stream, packet, (uint64_t)bytes, m,
+                               (uint64_t *)(sb + o_foff), (uint64_t *)(sb + o_roff), max_frames, dres);
+            TFG_LAUNCH_CHECK();
+            if (int rc = read_back_u64(ctx, dres, res, 3)) return rc;
+        }
         TFG_CHECK(!res[2], TFG_ERR_INVALID_ARG, "malformed %s packet (frame headers)", m == LZ4_METHOD ? "LZ4" : "ZSTD");
         if (res[0] <= max_frames) break;
         max_frames = res[0];
