@@ -329,7 +329,7 @@ __global__ void __launch_bounds__(64) lz4_decode_kernel(const uint8_t *pkt, cons
 // table. Any disagreement, a malformed header or more than FSEG_CAP frames in a segment makes the
 // host run lz4_frames_kernel instead (which also gives malformed packets their error).
 constexpr uint64_t FSEG = 64 * 1024;
-constexpr uint32_t FSEG_CAP = 32;
+constexpr uint32_t FSEG_CAP = 256; // a 64 KB frame of one repeated byte compresses to ~270 B
 struct FSeg {
     uint64_t first, exit, raw;
     uint32_t n, flags; // flags: 1 = a start was found, 2 = give up (bad header / overflow)
