@@ -645,8 +645,9 @@ __device__ __forceinline__ void block_append(uint32_t mask, const uint32_t (&val
 
 // One workgroup per ZCHUNK output bytes of a packet frame (cbase: prefix of the frames' chunk
 // counts); 16 bytes a thread.  Literal bytes are written to `out` and point at themselves
-// (src[g] = g); a match byte points at its source byte (src[g] = g - off) and joins the list of
-// match bytes.
+// (src[g] = g); a match byte points at its source byte (src[g] = g - off, or for byte j >= off of
+// an overlapping match the byte j % off of the period before it) and joins the list of match
+// bytes.
 __global__ void __launch_bounds__(256) zstd_expand_kernel(const uint64_t *roff, uint64_t f0, uint32_t nf,
                                                           const uint32_t *cbase, const uint32_t *bases, const tfz::ZRec *recs,
                                                           const uint8_t *lits, uint64_t nlits, uint8_t *out, uint32_t *src,
@@ -702,10 +703,14 @@ __global__ void __launch_bounds__(256) zstd_expand_kernel(const uint64_t *roff, 
                 const uint64_t li = (uint64_t)rec.c + (b - rec.a);
                 if (li < nlits) out[g] = lits[li];
                 else bad = true;
-            } else if (rec.d == 0 || rec.d > b) {
+            } else if (rec.d == 0 || rec.d > rec.a + rec.b) {
                 bad = true;
             } else {
-                sv[k] = (uint32_t)(g - rec.d);
+                // an overlapping match (offset < length) repeats its first `off` bytes: byte j
+                // of the match points into that period before the match, one hop instead of
+                // j / off (long runs of one byte no longer make long chains)
+                const uint32_t ms = rec.a + rec.b, j = b - ms;
+                sv[k] = (uint32_t)(g0 + ms - rec.d + (j < rec.d ? j : j % rec.d));
                 mmask |= 1u << k;
             }
         }
