@@ -233,6 +233,10 @@ def sender_payloads(rng):
     # literal alphabets past 128 symbols: FSE-compressed Huffman weights
     yield rng.integers(0, 1000, 40_000).astype(np.int64).tobytes()
     yield (rng.geometric(0.02, 200_000) % 256).astype(np.uint8).tobytes()
+    # all three repeat offsets, with and without literals before the match (the ll = 0 shift)
+    words = [bytes(rng.integers(0, 256, w, dtype=np.uint8)) for w in (11, 13, 17)]
+    yield b"".join(words[k] + (b"" if k else bytes([j & 255])) for j, k in enumerate(rng.integers(0, 3, 20_000)))
+    yield np.arange(0, 300_000, 3, dtype=np.int64).tobytes()          # an Int64 column
     yield bytes(rng.integers(0, 256, 3000, dtype=np.uint8)) * 3 + bytes(rng.integers(200, 256, 9000, dtype=np.uint8))
 
 

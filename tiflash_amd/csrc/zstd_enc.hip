@@ -691,7 +691,8 @@ __global__ void __launch_bounds__(64) zstd_encode_kernel(const uint8_t *src, uin
     uint2 *seq_end = (uint2 *)(lt + 2ull * ZE_FRAME); // sequence q at seq_end[-1 - q]
 
     // ---- matcher
-    uint32_t nlit = 0, nseq = 0, rep = 1;
+    uint32_t nlit = 0, nseq = 0;
+    uint32_t r1 = 1, r2 = 4, r3 = 8; // the repeat offsets (RFC 8878 §3.1.1.5: initial 1, 4, 8)
     auto copy_lits = [&](uint32_t a, uint32_t b) __attribute__((always_inline)) {
         for (uint32_t i = lane; i < b - a; i += 64) lt[nlit + i] = s[a + i];
         nlit += b - a;
@@ -712,16 +713,20 @@ __global__ void __launch_bounds__(64) zstd_encode_kernel(const uint8_t *src, uin
             uint32_t w = 0;
             if (valid) w = (uint32_t)s[pos] | ((uint32_t)s[pos + 1] << 8) | ((uint32_t)s[pos + 2] << 16) | ((uint32_t)s[pos + 3] << 24);
             const uint32_t h = (w * 2654435761u) >> (32 - ZE_HASH);
-            // candidates: the table slot, and the repeat offset in force at the chunk's start
-            // (preferred: its offset costs a repeat code while it stays in force)
-            const uint32_t rep0 = rep;
-            uint32_t wr = ~w;
-            if (valid && pos >= rep0)
-                wr = (uint32_t)s[pos - rep0] | ((uint32_t)s[pos - rep0 + 1] << 8) | ((uint32_t)s[pos - rep0 + 2] << 16) |
-                     ((uint32_t)s[pos - rep0 + 3] << 24);
+            // candidates: the table slot, and the first of the three repeat offsets in force at
+            // the chunk's start whose 4 bytes match (preferred: a repeat code costs a few bits)
+            auto word_at = [&](uint32_t p) __attribute__((always_inline)) {
+                return (uint32_t)s[p] | ((uint32_t)s[p + 1] << 8) | ((uint32_t)s[p + 2] << 16) | ((uint32_t)s[p + 3] << 24);
+            };
+            uint32_t roff = 0;
+            if (valid && pos >= ip) {
+                if (pos >= r1 && word_at(pos - r1) == w) roff = r1;
+                else if (pos >= r2 && word_at(pos - r2) == w) roff = r2;
+                else if (pos >= r3 && word_at(pos - r3) == w) roff = r3;
+            }
             const uint32_t tref = tpos[h], rw = tseq[h];
-            const bool by_rep = valid && pos >= ip && wr == w;
-            const bool by_tab = valid && pos >= ip && tref < pos && rw == w && (!by_rep || tref != pos - rep0);
+            const bool by_rep = roff != 0;
+            const bool by_tab = valid && pos >= ip && tref < pos && rw == w && (!by_rep || tref != pos - roff);
             const uint64_t mrep = __ballot(by_rep), mtab = __ballot(by_tab);
             uint64_t mask = mrep | mtab, covered = 0;
             auto extend = [&](uint32_t at, uint32_t from) __attribute__((always_inline)) {
@@ -741,20 +746,33 @@ __global__ void __launch_bounds__(64) zstd_encode_kernel(const uint8_t *src, uin
                 const uint32_t j = (uint32_t)__builtin_ctzll(mask);
                 const uint32_t at = cbase + j;
                 // the longer of the two candidates; the repeat offset when within a byte
-                const uint32_t ml_r = (mrep >> j) & 1 ? extend(at, at - rep0) : 0;
+                const uint32_t rofj = (uint32_t)__builtin_amdgcn_readlane((int)roff, (int)j);
+                const uint32_t ml_r = (mrep >> j) & 1 ? extend(at, at - rofj) : 0;
                 const uint32_t tfrom = (uint32_t)__builtin_amdgcn_readlane((int)tref, (int)j);
                 const uint32_t ml_t = (mtab >> j) & 1 ? extend(at, tfrom) : 0;
                 const bool use_rep = ml_r >= ZE_MINMATCH && ml_r + 1 >= ml_t;
-                const uint32_t ml = use_rep ? ml_r : ml_t, from = use_rep ? at - rep0 : tfrom;
+                const uint32_t ml = use_rep ? ml_r : ml_t, from = use_rep ? at - rofj : tfrom;
                 if (ml < ZE_MINMATCH) {
                     mask &= mask - 1;
                     continue;
                 }
                 const uint32_t ll = at - anchor, off = at - from;
                 copy_lits(anchor, at);
-                uint32_t ofv = off + 3;
-                if (off == rep && ll > 0) ofv = 1; // repeat offset 1 (history unchanged)
-                rep = off;
+                // the offset value and the repeat-offset history (RFC 8878 §3.1.1.5): with
+                // literals before it 1 / 2 / 3 are R1 / R2 / R3, without them R2 / R3 / R1 - 1;
+                // any offset other than R1 becomes R1, the others shifting down behind it
+                uint32_t ofv;
+                if (ll > 0 && off == r1) {
+                    ofv = 1;
+                } else {
+                    if (off == r2) ofv = ll > 0 ? 2 : 1;
+                    else if (off == r3) ofv = ll > 0 ? 3 : 2;
+                    else if (ll == 0 && off == r1 - 1) ofv = 3;
+                    else ofv = off + 3;
+                    if (off != r2) r3 = r2;
+                    r2 = r1;
+                    r1 = off;
+                }
                 if (lane == 0) seq_end[-1 - (int64_t)nseq] = make_uint2(ll | (ml << 16), ofv);
                 ++nseq;
                 ip = at + ml;
