@@ -66,9 +66,10 @@ typedef enum tfg_type {
     TFG_DECIMAL256 = 14, /* 256-bit payload (precision <= 65), four little-endian 64-bit limbs, two's
                           * complement: the reference's Decimal256 (boost checked_int256_t,
                           * libs/libcommon/include/common/types.h:35) as a fixed-width value; sum
-                          * results and sum arguments only */
+                          * results, sum / min / max / first_row arguments */
     TFG_STRING = 20,     /* ColumnString: chars (every row ends with '\0') + UInt64 end offsets
-                          * (Columns/ColumnString.h:50-54); GROUP BY keys only */
+                          * (Columns/ColumnString.h:50-54); GROUP BY keys and min / max / first_row
+                          * arguments */
     TFG_KEYS128 = 21,    /* a packed 16-byte GROUP BY key (see tfg_agg_create_keys): the device
                           * form the keys128 / key_string methods aggregate on, and the form
                           * partial results travel in between the two phases of an aggregation */
@@ -117,23 +118,53 @@ typedef enum tfg_logic_op {
 #define TFG_ARG_PREC(p) ((int)(p) << 16)
 #define TFG_ARG_TYPE(w) ((w) & 0xFF)
 #define TFG_ARG_PREC_OF(w) (((w) >> 16) & 0xFF)
+/* the collator of a String min / max argument (SingleValueDataString::setCollators,
+ * AggregateFunctionMinMaxAny.h:272-275): a tfg_collator */
+#define TFG_ARG_COLLATOR(c) ((int)(c) << 24)
+#define TFG_ARG_COLLATOR_OF(w) (((w) >> 24) & 0x7F)
 typedef enum tfg_agg_kind {
     TFG_AGG_SUM = 0,
     TFG_AGG_COUNT = 1,     /* count(arg): non-NULL rows of arg */
     TFG_AGG_COUNT_ALL = 2, /* count(*) / count(1): arg ignored */
-    /* min / max / first_row (AggregateFunctionMinMaxAny.cpp:39-46,155-159; AggregateFunctionMinData /
-     * MaxData / FirstRowData, AggregateFunctionMinMaxAny.h): fixed-width numeric arguments (Int*,
-     * UInt*, Float*, Decimal32 / Decimal64); the result has the argument's type and width.  NULL
-     * arguments are skipped (AggregateFunctionNullUnary); a group whose argument is NULL in every row
-     * yields NULL.  first_row returns the argument of one row of the group: the reference keeps the
-     * first row it processes, whose order is not fixed (threads, merges); here it is the row whose
-     * value orders last, so equal-valued groups (a GROUP BY column carried as first_row) are exact.
-     * Float order is IEEE total order (-0 < +0; NaN past +inf), where the reference's `<` leaves
-     * ties and NaN to row order.  Decimal128 / Decimal256 arguments: TFG_ERR_NOT_IMPLEMENTED. */
+    /* min / max / first_row (AggregateFunctionMinMaxAny.cpp:39-46,85-98,155-159; SingleValueDataFixed /
+     * SingleValueDataString, AggregateFunctionMinMaxAny.h:40-456): every argument type on the path —
+     * Int*, UInt*, Float*, Decimal32..Decimal256 and String; the result has the argument's type.
+     *   min / max: NULL arguments are skipped (AggregateFunctionNullUnary); a group whose argument is
+     *     NULL in every row yields NULL (Nullable result), without key and without rows the type's
+     *     default (non-Nullable argument: SingleValueDataFixed::insertResultInto -> insertDefault).
+     *     Numeric arguments keep an order key (Float order is IEEE total order: -0 < +0, NaN past
+     *     +inf, where the reference's `<` leaves ties and NaN to row order).  Decimal128 / Decimal256
+     *     compare as signed integers; String compares as SingleValueDataString::less / greater do:
+     *     the collator's compareFastPath over the row INCLUDING its terminating '\0'
+     *     (getDataAtWithTerminatingZero), so padding collators do not trim; without a collator, bytes.
+     *     Of equal values (equal under the collator) the first row in input order is kept
+     *     (changeIfLess / changeIfGreater are strict).
+     *   first_row: the first row in input order (changeFirstTime), NULL included: a NULL first row
+     *     makes the result NULL and later rows do not replace it (AggregateFunctionFirstRowNull,
+     *     AggregateFunctionNull.h:193-330); without rows the result is NULL.
+     *   "Input order" is the order of the rows of one consume, consumes in call order, and for
+     *   tfg_agg_merge the destination's groups before the source's — the reference's answer with one
+     *   thread (its multi-threaded answer depends on thread scheduling and merge order).
+     * String arguments: the args[i] / states[i] entry of the consume calls is a HOST pointer to a
+     * tfg_str_col, and the out_states[i] entry of the result calls a HOST pointer to a tfg_str_out
+     * (tfg_agg_result_type reports TFG_STRING, width 8: the end offsets). */
     TFG_AGG_MIN = 3,
     TFG_AGG_MAX = 4,
     TFG_AGG_FIRST_ROW = 5,
 } tfg_agg_kind;
+/* A String column argument / partial state (ColumnString: chars, each row ending in '\0', and
+ * UInt64 end offsets), DEVICE pointers in a host struct. */
+typedef struct tfg_str_col {
+    const uint8_t *chars;
+    const uint64_t *offsets;
+} tfg_str_col;
+/* A String result column: DEVICE buffers for the end offsets (one per group) and the chars
+ * (chars_capacity bytes; tfg_agg_result_chars gives the bytes needed). */
+typedef struct tfg_str_out {
+    uint8_t *chars;
+    uint64_t *offsets;
+    uint64_t chars_capacity;
+} tfg_str_out;
 
 /* Join kinds (ASTTableJoin::Kind, dbms/src/Interpreters/Join.h). Strictness ALL. */
 typedef enum tfg_join_kind {
@@ -381,6 +412,10 @@ int tfg_agg_result_keys(tfg_agg *agg, void *const *out_key_cols, uint64_t *const
                         uint64_t capacity, uint64_t chars_capacity, uint64_t *out_groups_host, uint64_t *out_chars_host);
 /* Result type of agg i (tfg_type) and its width in bytes. */
 int tfg_agg_result_type(tfg_agg *agg, int i, int *out_type, int *out_width);
+/* Chars bytes (terminators included) of the String result of agg i (min / max / first_row over a
+ * String argument) as tfg_agg_result / tfg_agg_result_keys would write them now; 0 for other
+ * aggregates. */
+int tfg_agg_result_chars(tfg_agg *agg, int i, uint64_t *out_bytes);
 
 /* ---------------------------------------------------------------- a18-a21 hash join */
 typedef struct tfg_join tfg_join;

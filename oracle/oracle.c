@@ -679,6 +679,10 @@ struct orc_agg {
     uint64_t *acc_w[ORC_MAX_AGGS]; /* Decimal256 accumulators: 4 little-endian limbs per group */
     double *acc_f[ORC_MAX_AGGS];
     uint64_t *cnt[ORC_MAX_AGGS]; /* non-NULL rows seen */
+    int coll[ORC_MAX_AGGS];       /* String min / max: the collator (TFG_ARG_COLLATOR) */
+    uint8_t **sval[ORC_MAX_AGGS]; /* String min / max / first_row: the value's bytes with its '\0' */
+    size_t *slen[ORC_MAX_AGGS];
+    uint8_t *fnull[ORC_MAX_AGGS]; /* first_row: the first row was NULL (AggregateFunctionFirstRowNull flag 2) */
     int64_t null_group;           /* group index of the NULL key, -1 */
 };
 
@@ -723,6 +727,7 @@ static void load_i256(int t, const void *p, size_t i, uint64_t *x)
     x[2] = x[3] = v < 0 ? ~0ull : 0ull;
 }
 
+static int64_t agg_new_group(orc_agg *a, uint64_t key, uint8_t is_null);
 orc_agg *orc_agg_create(int key_type, int n_aggs, const int *kinds, const int *arg_types)
 {
     if (n_aggs > ORC_MAX_AGGS) return NULL;
@@ -734,10 +739,14 @@ orc_agg *orc_agg_create(int key_type, int n_aggs, const int *kinds, const int *a
         a->kinds[i] = kinds[i];
         a->arg_types[i] = w & 0xFF;
         a->prec[i] = (w >> 16) & 0xFF;
+        a->coll[i] = (w >> 24) & 0x7F;
         a->wide[i] = kinds[i] == TFG_AGG_SUM && orc_sum_result_prec(w) > 38;
     }
     hmap_init(&a->map);
     a->null_group = -1;
+    /* without key the one group exists before any row (Aggregator::convertToBlocks emits it for an
+     * empty input: without_key states are created up front, Aggregator.cpp:1132-1160) */
+    if (key_type == 0) agg_new_group(a, 0, 0);
     return a;
 }
 
@@ -752,6 +761,11 @@ void orc_agg_destroy(orc_agg *a)
         free(a->acc_w[i]);
         free(a->acc_f[i]);
         free(a->cnt[i]);
+        if (a->sval[i])
+            for (size_t g = 0; g < a->n_groups; ++g) free(a->sval[i][g]);
+        free(a->sval[i]);
+        free(a->slen[i]);
+        free(a->fnull[i]);
     }
     free(a);
 }
@@ -767,6 +781,9 @@ static int64_t agg_new_group(orc_agg *a, uint64_t key, uint8_t is_null)
             a->acc_w[i] = (uint64_t *)realloc(a->acc_w[i], nc * 4 * sizeof(uint64_t));
             a->acc_f[i] = (double *)realloc(a->acc_f[i], nc * sizeof(double));
             a->cnt[i] = (uint64_t *)realloc(a->cnt[i], nc * sizeof(uint64_t));
+            a->sval[i] = (uint8_t **)realloc(a->sval[i], nc * sizeof(uint8_t *));
+            a->slen[i] = (size_t *)realloc(a->slen[i], nc * sizeof(size_t));
+            a->fnull[i] = (uint8_t *)realloc(a->fnull[i], nc);
         }
         a->cap_groups = nc;
     }
@@ -778,6 +795,9 @@ static int64_t agg_new_group(orc_agg *a, uint64_t key, uint8_t is_null)
         memset(a->acc_w[i] + 4 * g, 0, 32);
         a->acc_f[i][g] = 0.0;
         a->cnt[i][g] = 0;
+        a->sval[i][g] = NULL;
+        a->slen[i][g] = 0;
+        a->fnull[i][g] = 0;
     }
     return (int64_t)g;
 }
@@ -798,56 +818,205 @@ static int64_t agg_lookup(orc_agg *a, uint64_t key, int is_null)
     return *slot;
 }
 
-/* min / max / first_row (AggregateFunctionMinMaxAny.h: SingleValueDataFixed::changeIfLess /
- * changeIfGreater / changeFirstTime; AggregateFunctionFirstRowData): the value is kept in acc_i
- * (integers, as __int128) or acc_f (floats), cnt counts the rows that set or offered a value, and for
- * first_row limb 0 of acc_w records "the first row was NULL" (AggregateFunctionFirstRowNull, flag 2:
- * a NULL first row makes the result NULL and later rows do not replace it). */
+/* min / max / first_row (AggregateFunctionMinMaxAny.h: SingleValueDataFixed / SingleValueDataString
+ * changeIfLess / changeIfGreater / changeFirstTime, :40-456; AggregateFunctionFirstRowData): the value
+ * is kept in acc_i (integers and Decimal32..128, as __int128), acc_w (Decimal256, 4 limbs), acc_f
+ * (floats) or sval / slen (String: the row's bytes with its terminating zero, as
+ * getDataAtWithTerminatingZero hands them to the state); cnt counts the rows that set or offered a
+ * value, and fnull records "the first row was NULL" for first_row (AggregateFunctionFirstRowNull,
+ * flag 2: a NULL first row makes the result NULL and later rows do not replace it). */
 static int is_ord_kind(int k) { return k == TFG_AGG_MIN || k == TFG_AGG_MAX || k == TFG_AGG_FIRST_ROW; }
+
+/* A String argument or partial state: a host struct naming the chars and end offsets (tfg_str_col) */
+typedef struct {
+    const uint8_t *chars;
+    const uint64_t *offsets;
+} orc_str_col;
+/* A String result: chars (orc_agg_result_chars bytes) and end offsets */
+typedef struct {
+    uint8_t *chars;
+    uint64_t *offsets;
+} orc_str_out;
+
+/* GeneralCICollator::compare (TiDB/Collation/Collator.cpp:395-413): RightTrim both, then the
+ * characters' weights pairwise; a proper prefix orders first */
+static int gci_compare(const uint8_t *s1, size_t l1, const uint8_t *s2, size_t l2)
+{
+    while (l1 > 0 && s1[l1 - 1] == ' ') --l1;
+    while (l2 > 0 && s2[l2 - 1] == ' ') --l2;
+    size_t o1 = 0, o2 = 0;
+    while (o1 < l1 && o2 < l2) {
+        const int w1 = (int)orc_general_ci_weight(orc_utf8_next(s1, l1, &o1));
+        const int w2 = (int)orc_general_ci_weight(orc_utf8_next(s2, l2, &o2));
+        if (w1 != w2) return w1 < w2 ? -1 : 1;
+    }
+    return (o1 < l1) - (o2 < l2);
+}
+/* UCACICollator::weight (Collator.cpp:653-676): the next weight word, decoding characters only when
+ * both words are spent (zero-weight characters skipped) */
+static void uca_next(int v0900, uint64_t *first, uint64_t *second, size_t *off, size_t len, const uint8_t *s)
+{
+    if (*first != 0) return;
+    if (*second != 0) {
+        *first = *second;
+        *second = 0;
+        return;
+    }
+    while (*off < len)
+        if (orc_uca_weight(v0900, orc_utf8_next(s, len, off), first, second)) break;
+}
+/* UCACICollator::compare (Collator.cpp:536-578): preprocess (RightTrim with padding), then the
+ * weight words 16-bit chunk by chunk from the low end; an exhausted side (word 0) decides */
+static int uca_compare(int v0900, const uint8_t *s1, size_t l1, const uint8_t *s2, size_t l2)
+{
+    if (!v0900) {
+        while (l1 > 0 && s1[l1 - 1] == ' ') --l1;
+        while (l2 > 0 && s2[l2 - 1] == ' ') --l2;
+    }
+    size_t o1 = 0, o2 = 0;
+    uint64_t f1 = 0, x1 = 0, f2 = 0, x2 = 0;
+    for (;;) {
+        uca_next(v0900, &f1, &x1, &o1, l1, s1);
+        uca_next(v0900, &f2, &x2, &o2, l2, s2);
+        if (f1 == 0 || f2 == 0) return f1 < f2 ? -1 : f1 > f2 ? 1 : 0;
+        if (f1 == f2) {
+            f1 = f2 = 0;
+            continue;
+        }
+        while (f1 != 0 && f2 != 0) {
+            if (((f1 ^ f2) & 0xFFFF) == 0) {
+                f1 >>= 16;
+                f2 >>= 16;
+            } else {
+                return (int)(f1 & 0xFFFF) < (int)(f2 & 0xFFFF) ? -1 : 1;
+            }
+        }
+    }
+}
+/* SingleValueDataString::less / greater (AggregateFunctionMinMaxAny.h:218-230) over two values WITH
+ * their terminating zero: the collator's compareFastPath (Collator.h:91-98: padding binary
+ * collators RtrimStrCompare, else compare()); without a collator StringRef operator< (memcmp of
+ * the common prefix, then the size).  The '\0' ends every value, so the padding trims stop there. */
+int orc_min_max_str_compare(int collator, const uint8_t *a, size_t la, const uint8_t *b, size_t lb)
+{
+    if (collator == TFG_COLLATOR_GENERAL_CI) return gci_compare(a, la, b, lb);
+    if (collator == TFG_COLLATOR_UNICODE_CI || collator == TFG_COLLATOR_UCA0900_AI_CI)
+        return uca_compare(collator == TFG_COLLATOR_UCA0900_AI_CI, a, la, b, lb);
+    if (collator == TFG_COLLATOR_BIN_PADDING) {
+        while (la > 0 && a[la - 1] == ' ') --la;
+        while (lb > 0 && b[lb - 1] == ' ') --lb;
+    }
+    const size_t m = la < lb ? la : lb;
+    const int c = m ? memcmp(a, b, m) : 0;
+    if (c) return c < 0 ? -1 : 1;
+    return la < lb ? -1 : la > lb ? 1 : 0;
+}
+
+static int cmp256(const uint64_t *x, const uint64_t *y)
+{
+    if ((int64_t)x[3] != (int64_t)y[3]) return (int64_t)x[3] < (int64_t)y[3] ? -1 : 1;
+    for (int k = 2; k >= 0; --k)
+        if (x[k] != y[k]) return x[k] < y[k] ? -1 : 1;
+    return 0;
+}
+static void str_row(const void *p, size_t r, const uint8_t **s, size_t *len)
+{
+    const orc_str_col *c = (const orc_str_col *)p;
+    const uint64_t b = r ? c->offsets[r - 1] : 0, e = c->offsets[r];
+    *s = c->chars + b;
+    *len = e - b; /* with the '\0' */
+}
+/* the state of group g takes row r of column p */
+static void ord_set_row(orc_agg *a, int i, int64_t g, int t, const void *p, size_t r)
+{
+    if (t == TFG_STRING) {
+        const uint8_t *v;
+        size_t len;
+        str_row(p, r, &v, &len);
+        free(a->sval[i][g]);
+        a->sval[i][g] = (uint8_t *)malloc(len ? len : 1);
+        memcpy(a->sval[i][g], v, len);
+        a->slen[i][g] = len;
+    } else if (t == TFG_DECIMAL256) {
+        memcpy(a->acc_w[i] + 4 * g, (const char *)p + 32 * r, 32);
+    } else if (is_float(t)) {
+        a->acc_f[i][g] = load_f(t, p, r);
+    } else {
+        a->acc_i[i][g] = is_unsigned(t) ? (__int128)(uint64_t)load_s(t, p, r) : load_i128(t, p, r);
+    }
+}
+/* row r of column p against group g's value: -1 / 0 / 1 */
+static int ord_cmp_row(const orc_agg *a, int i, int64_t g, int t, const void *p, size_t r)
+{
+    if (t == TFG_STRING) {
+        const uint8_t *v;
+        size_t len;
+        str_row(p, r, &v, &len);
+        return orc_min_max_str_compare(a->coll[i], v, len, a->sval[i][g], a->slen[i][g]);
+    }
+    if (t == TFG_DECIMAL256) return cmp256((const uint64_t *)((const char *)p + 32 * r), a->acc_w[i] + 4 * g);
+    if (is_float(t)) {
+        const double v = load_f(t, p, r), cur = a->acc_f[i][g];
+        return v < cur ? -1 : v > cur ? 1 : 0;
+    }
+    const __int128 v = is_unsigned(t) ? (__int128)(uint64_t)load_s(t, p, r) : load_i128(t, p, r), cur = a->acc_i[i][g];
+    return v < cur ? -1 : v > cur ? 1 : 0;
+}
 static void ord_offer(orc_agg *a, int i, int64_t g, int t, const void *p, size_t r, int is_null)
 {
     const int k = a->kinds[i];
     if (k == TFG_AGG_FIRST_ROW) {
-        if (a->cnt[i][g] || a->acc_w[i][4 * g]) return; /* changeFirstTime: only the first row */
-        if (is_null) { a->acc_w[i][4 * g] = 1; return; }
-        if (is_float(t)) a->acc_f[i][g] = load_f(t, p, r);
-        else a->acc_i[i][g] = is_unsigned(t) ? (__int128)(uint64_t)load_s(t, p, r) : (__int128)load_s(t, p, r);
+        if (a->cnt[i][g] || a->fnull[i][g]) return; /* changeFirstTime: only the first row */
+        if (is_null) { a->fnull[i][g] = 1; return; }
+        ord_set_row(a, i, g, t, p, r);
         a->cnt[i][g] = 1;
         return;
     }
     if (is_null) return; /* AggregateFunctionNullUnary skips NULL rows */
-    const int have = a->cnt[i][g] != 0;
-    if (is_float(t)) {
-        const double v = load_f(t, p, r), cur = a->acc_f[i][g];
-        if (!have || (k == TFG_AGG_MIN ? v < cur : v > cur)) a->acc_f[i][g] = v;
-    } else {
-        const __int128 v = is_unsigned(t) ? (__int128)(uint64_t)load_s(t, p, r) : (__int128)load_s(t, p, r);
-        const __int128 cur = a->acc_i[i][g];
-        if (!have || (k == TFG_AGG_MIN ? v < cur : v > cur)) a->acc_i[i][g] = v;
-    }
+    const int c = a->cnt[i][g] ? ord_cmp_row(a, i, g, t, p, r) : 0;
+    if (!a->cnt[i][g] || (k == TFG_AGG_MIN ? c < 0 : c > 0)) ord_set_row(a, i, g, t, p, r); /* strict */
     a->cnt[i][g]++;
+}
+/* dst group d takes src group g's value */
+static void ord_copy(orc_agg *dst, int i, int64_t d, const orc_agg *src, int64_t g)
+{
+    dst->acc_i[i][d] = src->acc_i[i][g];
+    dst->acc_f[i][d] = src->acc_f[i][g];
+    memcpy(dst->acc_w[i] + 4 * d, src->acc_w[i] + 4 * g, 32);
+    if (src->sval[i][g]) {
+        free(dst->sval[i][d]);
+        dst->sval[i][d] = (uint8_t *)malloc(src->slen[i][g] ? src->slen[i][g] : 1);
+        memcpy(dst->sval[i][d], src->sval[i][g], src->slen[i][g]);
+        dst->slen[i][d] = src->slen[i][g];
+    }
 }
 /* merge of one group's state (changeIfLess(to) / changeIfGreater(to) / changeFirstTime(to)) */
 static void ord_merge(orc_agg *dst, int i, int64_t d, const orc_agg *src, int64_t g)
 {
     const int k = dst->kinds[i], t = dst->arg_types[i];
-    const int dh = dst->cnt[i][d] != 0 || dst->acc_w[i][4 * d], sh = src->cnt[i][g] != 0 || src->acc_w[i][4 * g];
+    const int dh = dst->cnt[i][d] != 0 || dst->fnull[i][d], sh = src->cnt[i][g] != 0 || src->fnull[i][g];
     if (!sh) return;
     if (k == TFG_AGG_FIRST_ROW) {
         if (dh) return;
         dst->cnt[i][d] = src->cnt[i][g];
-        dst->acc_w[i][4 * d] = src->acc_w[i][4 * g];
-        dst->acc_i[i][d] = src->acc_i[i][g];
-        dst->acc_f[i][d] = src->acc_f[i][g];
+        dst->fnull[i][d] = src->fnull[i][g];
+        ord_copy(dst, i, d, src, g);
         return;
     }
-    const int take = !dst->cnt[i][d] ||
-                     (is_float(t) ? (k == TFG_AGG_MIN ? src->acc_f[i][g] < dst->acc_f[i][d] : src->acc_f[i][g] > dst->acc_f[i][d])
-                                  : (k == TFG_AGG_MIN ? src->acc_i[i][g] < dst->acc_i[i][d] : src->acc_i[i][g] > dst->acc_i[i][d]));
-    if (take) {
-        dst->acc_i[i][d] = src->acc_i[i][g];
-        dst->acc_f[i][d] = src->acc_f[i][g];
+    int take = !dst->cnt[i][d];
+    if (!take) {
+        int c;
+        if (t == TFG_STRING)
+            c = orc_min_max_str_compare(dst->coll[i], src->sval[i][g], src->slen[i][g], dst->sval[i][d], dst->slen[i][d]);
+        else if (t == TFG_DECIMAL256)
+            c = cmp256(src->acc_w[i] + 4 * g, dst->acc_w[i] + 4 * d);
+        else if (is_float(t))
+            c = src->acc_f[i][g] < dst->acc_f[i][d] ? -1 : src->acc_f[i][g] > dst->acc_f[i][d] ? 1 : 0;
+        else
+            c = src->acc_i[i][g] < dst->acc_i[i][d] ? -1 : src->acc_i[i][g] > dst->acc_i[i][d] ? 1 : 0;
+        take = k == TFG_AGG_MIN ? c < 0 : c > 0;
     }
+    if (take) ord_copy(dst, i, d, src, g);
     dst->cnt[i][d] += src->cnt[i][g];
 }
 
@@ -903,6 +1072,14 @@ void orc_agg_merge(orc_agg *dst, const orc_agg *src)
 
 size_t orc_agg_size(const orc_agg *a) { return a->n_groups; }
 
+/* chars bytes of the String result of aggregate i (orc_agg_result writes them) */
+size_t orc_agg_result_chars(const orc_agg *a, int i)
+{
+    size_t b = 0;
+    for (size_t g = 0; g < a->n_groups; ++g) b += a->cnt[i][g] ? a->slen[i][g] : 1;
+    return b;
+}
+
 static int sum_result_width(const orc_agg *a, int i)
 {
     return a->wide[i] ? 32 : is_decimal_t(a->arg_types[i]) ? 16 : 8;
@@ -921,7 +1098,16 @@ void orc_agg_result(const orc_agg *a, uint64_t *out_keys, uint8_t *out_key_null,
             if (is_ord_kind(a->kinds[i])) { /* the argument's type and width */
                 const int t = a->arg_types[i];
                 char *o = (char *)out_states[i];
-                if (t == TFG_FLOAT64) ((double *)o)[g] = a->acc_f[i][g];
+                if (t == TFG_STRING) { /* an orc_str_out; NULL / no value: the empty String */
+                    orc_str_out *so = (orc_str_out *)out_states[i];
+                    const uint64_t start = g ? so->offsets[g - 1] : 0;
+                    const size_t len = a->cnt[i][g] ? a->slen[i][g] : 1;
+                    if (a->cnt[i][g]) memcpy(so->chars + start, a->sval[i][g], len);
+                    else so->chars[start] = 0;
+                    so->offsets[g] = start + len;
+                } else if (t == TFG_DECIMAL256) memcpy(o + 32 * g, a->acc_w[i] + 4 * g, 32);
+                else if (t == TFG_DECIMAL128) memcpy(o + 16 * g, &a->acc_i[i][g], 16);
+                else if (t == TFG_FLOAT64) ((double *)o)[g] = a->acc_f[i][g];
                 else if (t == TFG_FLOAT32) ((float *)o)[g] = (float)a->acc_f[i][g];
                 else {
                     const int64_t v = (int64_t)a->acc_i[i][g];
@@ -1113,6 +1299,7 @@ void orc_aggk_consume(orc_aggk *a, const void *const *key_cols, const uint64_t *
 }
 
 size_t orc_aggk_size(const orc_aggk *a) { return orc_agg_size(a->inner); }
+size_t orc_aggk_result_chars(const orc_aggk *a, int i) { return orc_agg_result_chars(a->inner, i); }
 
 /* groups in creation order: serialized keys (out_keys: arena bytes, out_key_offsets: end offsets,
  * pass NULL to get the byte count first) and states as orc_agg_result. */

@@ -64,6 +64,10 @@ void orc_agg_consume(orc_agg *a, const void *keys, const uint8_t *key_null, cons
                      const uint8_t *const *arg_nulls, const uint8_t *mask, size_t n);
 void orc_agg_merge(orc_agg *dst, const orc_agg *src);
 size_t orc_agg_size(const orc_agg *a);
+/* String min / max / first_row results: chars bytes; String arguments / results travel as host
+ * structs {chars, offsets} (args / out_states entries), like the device ABI's tfg_str_col / _out */
+size_t orc_agg_result_chars(const orc_agg *a, int i);
+int orc_min_max_str_compare(int collator, const uint8_t *a, size_t la, const uint8_t *b, size_t lb);
 /* out_keys: u64 key bits; out_key_null; out_states[i]: 8, 16 or 32 B per group; out_state_null[i]. */
 void orc_agg_result(const orc_agg *a, uint64_t *out_keys, uint8_t *out_key_null, void *const *out_states,
                     uint8_t *const *out_state_null);
@@ -77,6 +81,7 @@ void orc_aggk_consume(orc_aggk *a, const void *const *key_cols, const uint64_t *
                       const uint8_t *const *key_nulls, const void *const *args, const uint8_t *const *arg_nulls,
                       const uint8_t *mask, size_t n);
 size_t orc_aggk_size(const orc_aggk *a);
+size_t orc_aggk_result_chars(const orc_aggk *a, int i);
 size_t orc_aggk_result(const orc_aggk *a, uint8_t *out_keys, uint64_t *out_key_offsets, void *const *out_states,
                        uint8_t *const *out_state_null);
 

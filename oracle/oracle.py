@@ -89,6 +89,12 @@ def lib():
         L.orc_aggk_size.restype = ctypes.c_size_t
         L.orc_aggk_size.argtypes = [ctypes.c_void_p]
         L.orc_aggk_result.restype = ctypes.c_size_t
+        L.orc_agg_result_chars.restype = ctypes.c_size_t
+        L.orc_agg_result_chars.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.orc_aggk_result_chars.restype = ctypes.c_size_t
+        L.orc_aggk_result_chars.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.orc_min_max_str_compare.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
+                                              ctypes.c_size_t]
         L.orc_join_create.restype = ctypes.c_void_p
         L.orc_join_destroy.argtypes = [ctypes.c_void_p]
         L.orc_join_probe.restype = ctypes.c_size_t
@@ -121,10 +127,24 @@ def _p(a):
     return ctypes.c_void_p(0) if a is None else a.ctypes.data_as(ctypes.c_void_p)
 
 
+class _StrCol(ctypes.Structure):  # orc_str_col / orc_str_out: a String column's chars + end offsets
+    _fields_ = [("chars", ctypes.c_void_p), ("offsets", ctypes.c_void_p)]
+
+
 def _ptrs(arrs):
+    """Pointer array of numpy arrays; a (chars, offsets) pair becomes a host orc_str_col (kept alive
+    on the array object)."""
     out = (ctypes.c_void_p * max(1, len(arrs)))()
+    keep = []
     for i, a in enumerate(arrs):
-        out[i] = 0 if a is None else a.ctypes.data
+        if isinstance(a, (tuple, list)):
+            c, o = np.ascontiguousarray(a[0], dtype=np.uint8), np.ascontiguousarray(a[1], dtype=np.uint64)
+            sc = _StrCol(c.ctypes.data, o.ctypes.data)
+            keep += [c, o, sc]
+            out[i] = ctypes.addressof(sc)
+        else:
+            out[i] = 0 if a is None else a.ctypes.data
+    out._keep = keep
     return out
 
 
@@ -245,6 +265,20 @@ def arith_decimal_wide(op, a, b, a_type, b_type, a_scale, b_scale, res_type, res
     return out
 
 
+def _ord_state(h, i, t, g, strs, keys_agg=False):
+    """Result buffer of a min / max / first_row state: the argument's type; Decimal128 / Decimal256
+    as (g, 2 / 4) int64 limbs; a String as a (chars, offsets) pair (recorded in strs[i])."""
+    base = t & 0xFF
+    if base == STRING:
+        nb = (lib().orc_aggk_result_chars if keys_agg else lib().orc_agg_result_chars)(h, i)
+        c, o = np.zeros(max(nb, 1), np.uint8), np.zeros(max(g, 1), np.uint64)
+        strs[i] = (c[:nb], o[:g])
+        return (c, o)
+    if base in (DECIMAL128, DECIMAL256):
+        return np.zeros((max(g, 1), 2 if base == DECIMAL128 else 4), np.int64)
+    return np.zeros(max(g, 1), NP_DTYPE[base])
+
+
 class Agg:
     """Reference-semantics Aggregator (HashMap key64 + sum/count states)."""
 
@@ -256,7 +290,12 @@ class Agg:
         self.key_type = key_type
 
     def consume(self, keys, args, key_null=None, arg_nulls=None, mask=None, n=None):
-        n = n if n is not None else (len(keys) if keys is not None else len(next(a for a in args if a is not None)))
+        if n is None:
+            if keys is not None:
+                n = len(keys)
+            else:
+                a0 = next(a for a in args if a is not None)
+                n = len(a0[1]) if isinstance(a0, (tuple, list)) else len(a0)
         lib().orc_agg_consume(self.h, _p(keys), _p(key_null), _ptrs(args), _ptrs(arg_nulls) if arg_nulls else None,
                               _p(mask), ctypes.c_size_t(n))
 
@@ -271,10 +310,11 @@ class Agg:
         keys = np.empty(g, dtype=np.uint64)
         key_null = np.empty(g, dtype=np.uint8)
         states, snull = [], []
-        for kind, t in self.aggs:
+        strs = {}
+        for i, (kind, t) in enumerate(self.aggs):
             limbs = sum_limbs(kind, t)
             if kind in (AGG_MIN, AGG_MAX, AGG_FIRST_ROW):  # the argument's type
-                states.append(np.empty(g, dtype=NP_DTYPE[t & 0xFF]))
+                states.append(_ord_state(self.h, i, t, g, strs))
             elif kind != 0:
                 states.append(np.empty(g, dtype=np.uint64))
             elif (t & 0xFF) in (FLOAT32, FLOAT64):
@@ -285,6 +325,8 @@ class Agg:
                 states.append(np.empty(g, dtype=np.int64))
             snull.append(np.empty(g, dtype=np.uint8))
         lib().orc_agg_result(self.h, _p(keys), _p(key_null), _ptrs(states), _ptrs(snull))
+        for i, (c, o) in strs.items():
+            states[i] = (c, o)
         return {"keys": keys, "key_null": key_null, "states": states, "state_null": snull}
 
     def __del__(self):
@@ -359,12 +401,15 @@ class AggKeys:
         kb = np.zeros(max(total, 1), np.uint8)
         ko = np.zeros(max(g, 1), np.uint64)
         states, snull = [], []
-        for kind, t in self.aggs:
+        strs = {}
+        for i, (kind, t) in enumerate(self.aggs):
             limbs = sum_limbs(kind, t)
-            t &= 0xFF
             if kind in (AGG_MIN, AGG_MAX, AGG_FIRST_ROW):  # the argument's type
-                states.append(np.zeros(max(g, 1), NP_DTYPE[t]))
-            elif limbs > 1:
+                states.append(_ord_state(self.h, i, t, g, strs, keys_agg=True))
+                snull.append(np.zeros(max(g, 1), np.uint8))
+                continue
+            t &= 0xFF
+            if limbs > 1:
                 states.append(np.zeros((max(g, 1), limbs), np.int64))
             elif kind == 0 and t in (FLOAT32, FLOAT64):
                 states.append(np.zeros(max(g, 1), np.float64))
@@ -372,7 +417,9 @@ class AggKeys:
                 states.append(np.zeros(max(g, 1), np.int64))
             snull.append(np.zeros(max(g, 1), np.uint8))
         lib().orc_aggk_result(self.h, _p(kb), _p(ko), _ptrs(states), _ptrs(snull))
-        return kb[:total], ko[:g], [st[:g] for st in states], [sn[:g] for sn in snull]
+        for i, co in strs.items():
+            states[i] = co
+        return kb[:total], ko[:g], [st if i in strs else st[:g] for i, st in enumerate(states)], [sn[:g] for sn in snull]
 
     def result(self):
         g = self.size()
@@ -380,12 +427,15 @@ class AggKeys:
         kb = np.zeros(max(total, 1), np.uint8)
         ko = np.zeros(max(g, 1), np.uint64)
         states, snull = [], []
-        for kind, t in self.aggs:
+        strs = {}
+        for i, (kind, t) in enumerate(self.aggs):
             limbs = sum_limbs(kind, t)
-            t &= 0xFF
             if kind in (AGG_MIN, AGG_MAX, AGG_FIRST_ROW):  # the argument's type
-                states.append(np.zeros(max(g, 1), NP_DTYPE[t]))
-            elif limbs > 1:
+                states.append(_ord_state(self.h, i, t, g, strs, keys_agg=True))
+                snull.append(np.zeros(max(g, 1), np.uint8))
+                continue
+            t &= 0xFF
+            if limbs > 1:
                 states.append(np.zeros((max(g, 1), limbs), np.int64))
             elif kind == 0 and t in (FLOAT32, FLOAT64):
                 states.append(np.zeros(max(g, 1), np.float64))
@@ -400,7 +450,11 @@ class AggKeys:
             key = self._decode(kb[s:e].tobytes())
             s = e
             vals = []
-            for st in states:
+            for j, st in enumerate(states):
+                if j in strs:  # String min / max / first_row: the value's bytes without the '\0'
+                    c, o = strs[j]
+                    vals.append(bytes(c[(int(o[i - 1]) if i else 0):int(o[i]) - 1]))
+                    continue
                 v = st[i]
                 vals.append(limbs_to_int(v) if st.ndim == 2 else v.item())
             groups.append((key, vals))

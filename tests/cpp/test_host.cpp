@@ -2129,6 +2129,124 @@ TEST(PlanAggregateMinMaxFirstRow) {
     }
 }
 
+static std::multiset<std::vector<std::string>> byteRowSet(Context &ctx, const Block &b);
+
+// min / max / first_row over String (under general_ci and binary) and Decimal128 through the planner
+// (one PipelineExec: blocks in order, so first_row is the first row) and the Aggregator's two
+// phases, against a host restatement: SingleValueDataString / SingleValueDataFixed strict
+// changeIfLess / changeIfGreater / changeFirstTime, the collator's compare over the row with its
+// '\0' (orc_min_max_str_compare), a NULL first row NULL (AggregateFunctionMinMaxAny.cpp:46,85,98,155)
+TEST(PlanAggregateWideMinMaxFirstRow) {
+    using namespace dag;
+    std::mt19937_64 rng(91);
+    const size_t n = 60000;
+    const char *alpha[] = {"a", "A", "b", "B", " ", "\xc3\xa9", "\xc3\x89", "ss", "\xc3\x9f", "z"};
+    std::vector<int64_t> k(n);
+    std::vector<std::string> s(n);
+    std::vector<uint8_t> sn(n);
+    std::vector<__int128> d(n);
+    for (size_t i = 0; i < n; ++i) {
+        k[i] = (int64_t)(rng() % 2000);
+        for (size_t j = 0, len = rng() % 4; j < len; ++j) s[i] += alpha[rng() % 10];
+        sn[i] = rng() % 5 == 0;
+        d[i] = ((__int128)((int64_t)(rng() % 200) - 100) << 70) + (__int128)(rng() % 3);
+    }
+    DataType i64, str_n, dec = DataType::decimal(38, 2);
+    str_n.type = DataType::TYPE_STRING;
+    str_n.nullable = true;
+    Block b{{makeColumn(ctx, i64, k.data(), n), i64, "k"}, {makeStringColumn(ctx, s, sn.data()), str_n, "s"},
+            {makeColumn(ctx, dec, d.data(), n), dec, "d"}};
+    auto hex = [](const __int128 &v) {
+        static const char hx[] = "0123456789abcdef";
+        std::string o;
+        const uint8_t *p = (const uint8_t *)&v;
+        for (int q = 0; q < 16; ++q) o.push_back(hx[p[q] >> 4]), o.push_back(hx[p[q] & 15]);
+        return o;
+    };
+    auto cmp = [](int coll, const std::string &a, const std::string &b) {
+        return orc_min_max_str_compare(coll, (const uint8_t *)a.c_str(), a.size() + 1, (const uint8_t *)b.c_str(), b.size() + 1);
+    };
+    struct W {
+        bool mn_has = false, mx_has = false, first = false, first_null = false;
+        std::string mn, mx, fs;
+        __int128 fd = 0;
+    };
+    std::map<int64_t, W> want;
+    for (size_t i = 0; i < n; ++i) {
+        W &w = want[k[i]];
+        if (!w.first) w.first = true, w.first_null = sn[i], w.fs = s[i], w.fd = d[i];
+        if (!sn[i] && (!w.mn_has || cmp(TFG_COLLATOR_GENERAL_CI, s[i], w.mn) < 0)) w.mn = s[i], w.mn_has = true;
+        if (!sn[i] && (!w.mx_has || cmp(TFG_COLLATOR_NONE, s[i], w.mx) > 0)) w.mx = s[i], w.mx_has = true;
+    }
+    // max(d) per key: a separate pass (strict: the first maximum)
+    std::map<int64_t, __int128> dmx;
+    for (size_t i = 0; i < n; ++i) {
+        auto it = dmx.find(k[i]);
+        if (it == dmx.end() || d[i] > it->second) dmx[k[i]] = d[i];
+    }
+    std::multiset<std::vector<std::string>> expect;
+    for (const auto &kv : want) {
+        const W &w = kv.second;
+        int64_t key = kv.first;
+        std::string khex;
+        static const char hx[] = "0123456789abcdef";
+        for (int q = 0; q < 8; ++q) {
+            const uint8_t byte = (uint8_t)((uint64_t)key >> (8 * q));
+            khex.push_back(hx[byte >> 4]), khex.push_back(hx[byte & 15]);
+        }
+        expect.insert({w.mn_has ? w.mn : "N", w.mx_has ? w.mx : "N", w.first_null ? "N" : w.fs, hex(dmx[key]),
+                       hex(w.fd), khex});
+    }
+    { // Aggregation(group by k: min(s) general_ci, max(s), first_row(s), max(d), first_row(d))
+        g_current = "PlanAggregateWideMinMaxFirstRow plan";
+        PlanContext env;
+        env.concurrency = 1;
+        env.tables["t"] = {b.cloneEmpty(), splitBlocks(ctx, b, 3)};
+        const Executor root = Executor::aggregation(
+            "agg_1", {Expr::col(0)},
+            {Expr::min(Expr::col(1), TFG_COLLATOR_GENERAL_CI), Expr::max(Expr::col(1)), Expr::firstRow(Expr::col(1)),
+             Expr::max(Expr::col(2)), Expr::firstRow(Expr::col(2))},
+            Executor::tableScan("ts_0", "t"));
+        std::vector<Block> res;
+        env.result = [&](const Block &r) { res.push_back(r); };
+        PipelineExecutorContext exec;
+        PhysicalPlan plan(ctx, exec, env);
+        plan.build(root);
+        plan.execute();
+        std::multiset<std::vector<std::string>> got;
+        for (const Block &r : res) {
+            EXPECT(r.safeGetByPosition(0).type.isString() && r.safeGetByPosition(0).type.nullable);
+            EXPECT(r.safeGetByPosition(2).type.nullable && r.safeGetByPosition(3).type.type == TFG_DECIMAL128);
+            for (const auto &row : byteRowSet(ctx, r)) got.insert(row);
+        }
+        EXPECT(got == expect);
+    }
+    { // two phases: partial blocks of three slices merged in order by a final aggregator
+        g_current = "PlanAggregateWideMinMaxFirstRow two-phase";
+        Aggregator::Params p;
+        p.src_header = b.cloneEmpty();
+        p.keys = {"k"};
+        AggregateDescription mn{"min", {"s"}, "mn"};
+        mn.collator = TFG_COLLATOR_GENERAL_CI;
+        p.aggregates = {mn, {"max", {"s"}, "mx"}, {"first_row", {"s"}, "fs"}, {"max", {"d"}, "md"},
+                        {"first_row", {"d"}, "fd"}};
+        Aggregator fin(ctx, p);
+        for (const Block &h : splitBlocks(ctx, b, 3)) {
+            Aggregator part(ctx, p);
+            part.executeOnBlock(h);
+            fin.mergeOnBlock(part.convertToBlock(false));
+        }
+        Block r = fin.convertToBlock();
+        // byteRowSet orders the columns as the block does: key first here
+        std::multiset<std::vector<std::string>> got;
+        for (auto row : byteRowSet(ctx, r)) {
+            std::rotate(row.begin(), row.begin() + 1, row.end());
+            got.insert(row);
+        }
+        EXPECT(got == expect);
+    }
+}
+
 // Join(TableScan probe, TableScan build) from descriptors: inner (pairs vs the oracle, schema =
 // left then right columns), a GROUP BY over the join (count per key), left outer (unmatched
 // probe rows carry NULL build columns), semi, and the stream engine's inner join

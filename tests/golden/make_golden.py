@@ -132,9 +132,28 @@ def aggregate_cases():
     # AggKeyOptimization case 1 (:1053-1137): 1024 rows, four groups of 256 rows (col_int = i,
     # col_tinyint = i): count(1), first_row(col_tinyint) GROUP BY col_int, col_tinyint
     first_row = {"rows": 1024, "row_types": 4, "count": [256, 256, 256, 256], "first_row_tinyint": [0, 1, 2, 3]}
+    # AggNull (:740-750, table aggnull_test.t1 :98-101): max(s1) without key over Nullable(String)
+    # s1 = {"banana", NULL, "banana"} -> {"banana"}; GROUP BY s1 -> s1 = {NULL, "banana"}
+    agg_null = {"s1": ["banana", N, "banana"], "s2": ["apple", N, "banana"], "max_s1": "banana",
+                "group_by_s1": [N, "banana"]}
+    # AggKeyOptimization cases 3, 4, 6, 7 (:1160-1245): 1024 rows in four runs of 256 ("a", 0), ("b", 1),
+    # ("c", 2), ("d", 3) of (col_string_*, col_int); count(1) and first_row(String column) GROUP BY the
+    # listed keys -> counts 256 and first_row = "a".."d"; col_string_with_collator is utf8_general_ci
+    first_row_string = {
+        "rows": 1024, "row_types": 4, "values": ["a", "b", "c", "d"], "count": [256, 256, 256, 256],
+        "cases": [{"case": 3, "keys": ["col_string_no_collator"], "arg": "col_string_no_collator"},
+                  {"case": 4, "keys": ["col_string_with_collator"], "arg": "col_string_with_collator"},
+                  {"case": 6, "keys": ["col_string_with_collator", "col_int", "col_string_no_collator"],
+                   "arg": "col_string_with_collator"},
+                  {"case": 7, "keys": ["col_string_with_collator", "col_int"], "arg": "col_string_with_collator"}],
+        "collators": {"col_string_with_collator": "utf8_general_ci", "col_string_no_collator": None},
+        "expected": ["a", "b", "c", "d"]}
+    # RepeatedAggregateFunction (:752-770): max(s1) = 3, min(s1) = 1 without key over test_table
+    repeated = {"max_s1": 3, "min_s1": 1, "sum_s2": 6}
     return {"clerk": clerk, "counts": counts, "test_table": test_table,
             "sums": [{"func": "sum(s2)", "group_by": [], "expected": [6]}],  # :755-757
-            "min_max": min_max, "first_row": first_row}
+            "min_max": min_max, "first_row": first_row, "agg_null": agg_null, "first_row_string": first_row_string,
+            "repeated": repeated}
 
 
 def sum_type_cases():

@@ -237,10 +237,3 @@ def test_min_max_reference_clerk(tfa, ctx, dev):
         key = lambda v: (v is None, v if v is not None else 0)  # noqa: E731
         assert sorted(got, key=key) == sorted(case["expected"], key=key), case
         assert len(got) == len(_clerk_groups(clerk, case["group_by"]))
-
-
-def test_min_max_unsupported_types(tfa, ctx):
-    for t, code in ((tfa.DECIMAL128, -4), (tfa.DECIMAL256, -4)):
-        with pytest.raises(tfa.TfgError) as e:
-            tfa.Aggregator(ctx, tfa.INT64, [(tfa.AGG_MIN, t)])
-        assert e.value.code == code

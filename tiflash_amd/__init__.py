@@ -33,6 +33,12 @@ STRING, KEYS128 = 20, 21  # String GROUP BY keys (chars, offsets); packed 16-byt
 NULLABLE = 0x100  # or-ed into an aggregate argument type: the argument may carry a null map
 
 
+def collate(t: int, c: int) -> int:
+    """Aggregate argument type word of a String min / max argument under collator c
+    (TFG_ARG_COLLATOR): SingleValueDataString compares with the collator."""
+    return t | (int(c) << 24)
+
+
 def prec(t: int, p: int) -> int:
     """Aggregate argument type word of a Decimal column of precision p (TFG_ARG_PREC): sum over
     Decimal(p, s) returns Decimal(min(p + 22, 65), s) — Decimal128 up to 38 digits, else
@@ -102,6 +108,58 @@ def _ptr_array(ts) -> ctypes.Array:
     for i, t in enumerate(ts):
         arr[i] = t.data_ptr() if t is not None else 0
     return arr
+
+
+class _StrCol(ctypes.Structure):  # tfg_str_col
+    _fields_ = [("chars", ctypes.c_void_p), ("offsets", ctypes.c_void_p)]
+
+
+class _StrOut(ctypes.Structure):  # tfg_str_out
+    _fields_ = [("chars", ctypes.c_void_p), ("offsets", ctypes.c_void_p), ("chars_capacity", ctypes.c_uint64)]
+
+
+def _arg_array(ts):
+    """Aggregate arguments / partial states: a tensor, None, or a String column as a (chars, offsets)
+    tensor pair, passed as a host tfg_str_col.  Returns (array, keep-alive list)."""
+    arr = (ctypes.c_void_p * max(1, len(ts)))()
+    keep = []
+    for i, t in enumerate(ts):
+        if isinstance(t, (tuple, list)):
+            sc = _StrCol(t[0].data_ptr(), t[1].data_ptr())
+            keep.append(sc)
+            arr[i] = ctypes.addressof(sc)
+        else:
+            arr[i] = t.data_ptr() if t is not None else 0
+    return arr, keep
+
+
+def _agg_states(h, n_aggs: int, g: int, dev):
+    """Result buffers of an aggregator's states: (pointer array, keep-alive, finish) — finish()
+    returns the state list (a String state as a (chars, offsets) pair)."""
+    import torch
+    arr = (ctypes.c_void_p * max(1, n_aggs))()
+    keep, outs = [], []
+    for i in range(n_aggs):
+        t, w = ctypes.c_int(), ctypes.c_int()
+        check(lib().tfg_agg_result_type(h, i, ctypes.byref(t), ctypes.byref(w)))
+        if t.value == STRING:
+            nb = ctypes.c_uint64()
+            check(lib().tfg_agg_result_chars(h, i, ctypes.byref(nb)))
+            chars = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=dev)
+            offs = torch.empty(max(g, 1), dtype=torch.int64, device=dev)
+            so = _StrOut(chars.data_ptr(), offs.data_ptr(), nb.value)
+            keep.append(so)
+            arr[i] = ctypes.addressof(so)
+            outs.append((chars[:nb.value], offs[:g]))
+            continue
+        s = _empty(g, w.value, dev)
+        if t.value == FLOAT64:
+            s = s.view(torch.float64)
+        elif t.value == FLOAT32:
+            s = s.view(torch.float32)
+        arr[i] = s.data_ptr()
+        outs.append(s)
+    return arr, keep, outs
 
 
 def _int_array(xs) -> ctypes.Array:
@@ -411,8 +469,14 @@ class Aggregator:
         ctx._children.add(self)
 
     def consume(self, keys, args: Sequence, key_nullmap=None, arg_nullmaps=None, mask=None, n=None):
-        n = n if n is not None else (keys.shape[0] if keys is not None else next(a for a in args if a is not None).shape[0])
-        check(lib().tfg_agg_consume(self.h, _p(keys), _p(key_nullmap), _ptr_array(args),
+        if n is None:
+            if keys is not None:
+                n = keys.shape[0]
+            else:
+                a0 = next(a for a in args if a is not None)
+                n = a0[1].shape[0] if isinstance(a0, (tuple, list)) else a0.shape[0]
+        av, _keep = _arg_array(args)
+        check(lib().tfg_agg_consume(self.h, _p(keys), _p(key_nullmap), av,
                                     _ptr_array(arg_nullmaps) if arg_nullmaps else ctypes.c_void_p(0), _p(mask),
                                     ctypes.c_int64(n)))
 
@@ -420,14 +484,19 @@ class Aggregator:
                          key_nullmap=None, arg_nullmaps=None, pred_type=None):
         st = scalar_type or (FLOAT64 if isinstance(scalar, float) else INT64)
         s = _scalar(st, scalar)
+        av, _keep = _arg_array(args)
         check(lib().tfg_agg_consume_filtered(self.h, pred_type or torch_type(pred_col), _p(pred_col), _p(pred_nullmap),
-                                             op, st, ctypes.byref(s), _p(keys), _p(key_nullmap), _ptr_array(args),
+                                             op, st, ctypes.byref(s), _p(keys), _p(key_nullmap), av,
                                              _ptr_array(arg_nullmaps) if arg_nullmaps else ctypes.c_void_p(0),
                                              ctypes.c_int64(pred_col.shape[0])))
 
     def consume_partial(self, keys, states: Sequence, key_nullmap=None, state_nullmaps=None):
-        n = keys.shape[0] if keys is not None else states[0].shape[0]
-        check(lib().tfg_agg_consume_partial(self.h, _p(keys), _p(key_nullmap), _ptr_array(states),
+        if keys is not None:
+            n = keys.shape[0]
+        else:
+            n = states[0][1].shape[0] if isinstance(states[0], (tuple, list)) else states[0].shape[0]
+        av, _keep = _arg_array(states)
+        check(lib().tfg_agg_consume_partial(self.h, _p(keys), _p(key_nullmap), av,
                                             _ptr_array(state_nullmaps) if state_nullmaps else ctypes.c_void_p(0),
                                             ctypes.c_int64(n)))
 
@@ -450,19 +519,10 @@ class Aggregator:
         kw = WIDTH.get(self.key_type, 8)
         keys = _empty(g, kw, dev) if self.key_type else None
         key_null = torch.empty(max(g, 1), dtype=torch.uint8, device=dev)[:g]
-        states, snulls = [], []
-        for i in range(len(self.aggs)):
-            t, w = ctypes.c_int(), ctypes.c_int()
-            check(lib().tfg_agg_result_type(self.h, i, ctypes.byref(t), ctypes.byref(w)))
-            s = _empty(g, w.value, dev)
-            if t.value == FLOAT64:
-                s = s.view(torch.float64)
-            elif t.value == FLOAT32:
-                s = s.view(torch.float32)
-            states.append(s)
-            snulls.append(torch.empty(max(g, 1), dtype=torch.uint8, device=dev)[:g])
+        sarr, _keep, states = _agg_states(self.h, len(self.aggs), g, dev)
+        snulls = [torch.empty(max(g, 1), dtype=torch.uint8, device=dev)[:g] for _ in self.aggs]
         cnt = ctypes.c_uint64()
-        check(lib().tfg_agg_result(self.h, _p(keys), _p(key_null), _ptr_array(states), _ptr_array(snulls),
+        check(lib().tfg_agg_result(self.h, _p(keys), _p(key_null), sarr, _ptr_array(snulls),
                                    ctypes.c_uint64(g), ctypes.byref(cnt)))
         return {"keys": keys, "key_null": key_null, "states": states, "state_null": snulls}
 
@@ -514,14 +574,16 @@ class KeysAggregator(Aggregator):
 
     def consume(self, keys, args: Sequence, key_nullmaps=None, arg_nullmaps=None, mask=None):
         kc, ko, n = self._key_arrays(keys)
+        av, _keep = _arg_array(args)
         check(lib().tfg_agg_consume_keys(self.h, kc, ko, _ptr_array(key_nullmaps) if key_nullmaps else ctypes.c_void_p(0),
-                                         _ptr_array(args), _ptr_array(arg_nullmaps) if arg_nullmaps else ctypes.c_void_p(0),
+                                         av, _ptr_array(arg_nullmaps) if arg_nullmaps else ctypes.c_void_p(0),
                                          _p(mask), ctypes.c_int64(n)))
 
     def consume_partial(self, keys, states: Sequence, key_nullmaps=None, state_nullmaps=None):
         kc, ko, n = self._key_arrays(keys)
+        av, _keep = _arg_array(states)
         check(lib().tfg_agg_consume_partial_keys(
-            self.h, kc, ko, _ptr_array(key_nullmaps) if key_nullmaps else ctypes.c_void_p(0), _ptr_array(states),
+            self.h, kc, ko, _ptr_array(key_nullmaps) if key_nullmaps else ctypes.c_void_p(0), av,
             _ptr_array(state_nullmaps) if state_nullmaps else ctypes.c_void_p(0), ctypes.c_int64(n)))
 
     def consume_partial_packed(self, keys16, states: Sequence, state_nullmaps=None):
@@ -548,19 +610,10 @@ class KeysAggregator(Aggregator):
                 cols.append(_empty(g, WIDTH[t], dev))
                 offs.append(None)
             nulls.append(torch.empty(max(g, 1), dtype=torch.uint8, device=dev))
-        states, snulls = [], []
-        for i in range(len(self.aggs)):
-            t, w = ctypes.c_int(), ctypes.c_int()
-            check(lib().tfg_agg_result_type(self.h, i, ctypes.byref(t), ctypes.byref(w)))
-            s = _empty(g, w.value, dev)
-            if t.value == FLOAT64:
-                s = s.view(torch.float64)
-            elif t.value == FLOAT32:
-                s = s.view(torch.float32)
-            states.append(s)
-            snulls.append(torch.empty(max(g, 1), dtype=torch.uint8, device=dev)[:g])
+        sarr, _keep, states = _agg_states(self.h, len(self.aggs), g, dev)
+        snulls = [torch.empty(max(g, 1), dtype=torch.uint8, device=dev)[:g] for _ in self.aggs]
         cnt, chars = ctypes.c_uint64(), ctypes.c_uint64()
-        rc = lib().tfg_agg_result_keys(self.h, _ptr_array(cols), _ptr_array(offs), _ptr_array(nulls), _ptr_array(states),
+        rc = lib().tfg_agg_result_keys(self.h, _ptr_array(cols), _ptr_array(offs), _ptr_array(nulls), sarr,
                                        _ptr_array(snulls), ctypes.c_uint64(g), ctypes.c_uint64(ccap),
                                        ctypes.byref(cnt), ctypes.byref(chars))
         if rc == TFG_ERR_CAPACITY and chars.value > ccap:

@@ -76,6 +76,12 @@ __global__ void __launch_bounds__(NK_T) agg_nokey_kernel(AggSpec S, RowsIO rows,
         if (!pred(r)) continue;
         for (int i = 0; i < S.n_aggs; ++i) {
             if (mode == MODE_RAW && S.kind[i] == TFG_AGG_COUNT_ALL) { p.cnt[i]++; continue; }
+            if (S.acc[i] == ACC_REF) { // row r is candidate n0 + 1 + r; first_row takes NULL rows too
+                if (S.kind[i] != TFG_AGG_FIRST_ROW && rows.val_null[i] && rows.val_null[i][r]) continue;
+                const uint64_t ref = S.ref[i].n0 + 1 + (uint64_t)r;
+                if (ref_better(S.kind[i], S.ref[i], ref, p.lo[i])) p.lo[i] = ref;
+                continue;
+            }
             if (rows.val_null[i] && rows.val_null[i][r]) continue;
             if (S.acc[i] == ACC_ORD) { // min / max / first_row: running max of order keys
                 const uint64_t k = ord_enc(S.kind[i], S.src_type[i], load_bits(rows.val[i], val_width(S, mode, i), r));
@@ -121,6 +127,8 @@ __global__ void __launch_bounds__(NK_T) agg_nokey_kernel(AggSpec S, RowsIO rows,
                     nk_add(s, i, q, &red[t].x4[i]);
                 } else if (S.acc[i] == ACC_ORD) {
                     s.lo[i] = red[t].lo[i] > s.lo[i] ? red[t].lo[i] : s.lo[i];
+                } else if (S.acc[i] == ACC_REF) {
+                    if (red[t].lo[i] && ref_better(S.kind[i], S.ref[i], red[t].lo[i], s.lo[i])) s.lo[i] = red[t].lo[i];
                 } else {
                     const uint64_t o = s.lo[i];
                     s.lo[i] += red[t].lo[i];
@@ -154,6 +162,9 @@ __global__ void agg_nokey_fold_kernel(AggSpec S, const NoKeyPartial *partials, i
             else if (S.acc[i] == ACC_ORD) {
                 uint64_t *a = (uint64_t *)st.acc[i];
                 if (p.lo[i] > a[0]) a[0] = p.lo[i];
+            } else if (S.acc[i] == ACC_REF) {
+                uint64_t *a = (uint64_t *)st.acc[i];
+                if (p.lo[i] && ref_better(S.kind[i], S.ref[i], p.lo[i], a[0])) a[0] = p.lo[i];
             }
             if (S.has_cnt[i]) st.cnt[i][0] += p.cnt[i];
         }
@@ -181,8 +192,11 @@ __global__ void agg_result_kernel(AggSpec S, GroupsIO st, uint64_t n, int key_wi
         }
         if (out_key_null) out_key_null[g] = st.key_null[g];
         for (int i = 0; i < S.n_aggs; ++i) {
-            if (res.state[i] && S.acc[i] == ACC_ORD) { // min / max / first_row: the argument's width
-                const uint64_t x = ord_dec(S.kind[i], S.src_type[i], ((const uint64_t *)st.acc[i])[g]);
+            if (S.acc[i] == ACC_REF) continue; // values and NULL flags come from the value store
+            if (res.state[i] && S.acc[i] == ACC_ORD) { // min / max: the argument's width
+                // no value (a group of NULLs, or no row without key): the type's default, 0
+                const bool none = S.has_cnt[i] && st.cnt[i][g] == 0;
+                const uint64_t x = none ? 0 : ord_dec(S.kind[i], S.src_type[i], ((const uint64_t *)st.acc[i])[g]);
                 switch (val_width(S, MODE_RAW, i)) {
                 case 1: ((uint8_t *)res.state[i])[g] = (uint8_t)x; break;
                 case 2: ((uint16_t *)res.state[i])[g] = (uint16_t)x; break;
@@ -225,6 +239,10 @@ __global__ void agg_state_add_kernel(AggSpec S, GroupsIO dst, GroupsIO src) { //
         else if (S.acc[i] == ACC_ORD) {
             const uint64_t b = ((const uint64_t *)src.acc[i])[0];
             if (b > ((uint64_t *)dst.acc[i])[0]) ((uint64_t *)dst.acc[i])[0] = b;
+        } else if (S.acc[i] == ACC_REF) { // the source's store follows the destination's n0 entries
+            const uint64_t b = ((const uint64_t *)src.acc[i])[0];
+            uint64_t *a = (uint64_t *)dst.acc[i];
+            if (b && ref_better(S.kind[i], S.ref[i], S.ref[i].n0 + b, a[0])) a[0] = S.ref[i].n0 + b;
         }
         if (S.has_cnt[i]) dst.cnt[i][0] += src.cnt[i][0];
     }
@@ -660,9 +678,106 @@ __global__ void unpack_keys_kernel(KeyPack kp, const uint4 *keys, const uint64_t
     }
 }
 
+// ---------------------------------------------------------------- row-reference value stores
+// (ACC_REF aggregates, agg_dev.h): the candidates of a consume are the store (refs 1..n0) and the
+// consumed column (n0 + 1 + r); after it every group's winning value is copied into a new store in
+// group order and the group's reference becomes g + 1.
+__global__ void ref_iota_kernel(uint64_t *out, uint64_t n0, int64_t n) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
+        out[r] = n0 + 1 + (uint64_t)r;
+}
+// a merge's source states: references into the source's store, after the destination's n0 entries
+__global__ void ref_shift_kernel(const uint64_t *in, uint64_t n0, int64_t n, uint64_t *out) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
+        out[r] = in[r] ? in[r] + n0 : 0;
+}
+
+struct RefCol {           // one candidate source
+    const uint8_t *val;   // fixed-width values, or String chars
+    const uint64_t *off;  // String: end offsets
+    const uint8_t *nul;   // NULL flags (null: none)
+};
+__device__ __forceinline__ const RefCol &ref_pick(uint64_t ref, uint64_t n0, const RefCol &s0, const RefCol &s1,
+                                                  uint64_t &idx) {
+    idx = ref > n0 ? ref - n0 - 1 : ref - 1;
+    return ref > n0 ? s1 : s0;
+}
+
+__global__ void ref_store_fixed_kernel(uint64_t *acc, uint64_t G, uint64_t n0, int w, RefCol s0, RefCol s1,
+                                       uint8_t *val, uint8_t *nul) {
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < G; g += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t ref = acc[g];
+        uint64_t q[4] = {0, 0, 0, 0};
+        uint8_t isnull = 1;
+        if (ref) {
+            uint64_t idx;
+            const RefCol &c = ref_pick(ref, n0, s0, s1, idx);
+            isnull = c.nul ? (c.nul[idx] != 0) : 0;
+            if (!isnull) {
+                if (w >= 8) {
+                    for (int k = 0; k < w / 8; ++k) q[k] = reinterpret_cast<const uint64_t *>(c.val)[idx * (w / 8) + k];
+                } else {
+                    q[0] = load_bits(c.val, w, (int64_t)idx);
+                }
+            }
+            acc[g] = g + 1;
+        }
+        nul[g] = isnull;
+        switch (w) { // a NULL or absent value stores the default, 0 (ColumnNullable::insertDefault)
+        case 1: val[g] = (uint8_t)q[0]; break;
+        case 2: reinterpret_cast<uint16_t *>(val)[g] = (uint16_t)q[0]; break;
+        case 4: reinterpret_cast<uint32_t *>(val)[g] = (uint32_t)q[0]; break;
+        default:
+            for (int k = 0; k < w / 8; ++k) reinterpret_cast<uint64_t *>(val)[g * (w / 8) + k] = q[k];
+        }
+    }
+}
+
+// String store: bytes of each group's value with its '\0' (NULL / absent: the empty String)
+__global__ void ref_store_len_kernel(const uint64_t *acc, uint64_t G, uint64_t n0, RefCol s0, RefCol s1, uint64_t *len) {
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < G; g += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t ref = acc[g];
+        uint64_t l = 1;
+        if (ref) {
+            uint64_t idx;
+            const RefCol &c = ref_pick(ref, n0, s0, s1, idx);
+            if (!(c.nul && c.nul[idx])) l = c.off[idx] - (idx ? c.off[idx - 1] : 0);
+        }
+        len[g] = l;
+    }
+}
+__global__ void ref_store_str_kernel(uint64_t *acc, uint64_t G, uint64_t n0, RefCol s0, RefCol s1, const uint64_t *start,
+                                     uint8_t *chars, uint8_t *nul) {
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < G; g += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t ref = acc[g];
+        uint8_t *o = chars + start[g];
+        uint8_t isnull = 1;
+        if (ref) {
+            uint64_t idx;
+            const RefCol &c = ref_pick(ref, n0, s0, s1, idx);
+            isnull = c.nul ? (c.nul[idx] != 0) : 0;
+            if (!isnull) {
+                const uint64_t b = idx ? c.off[idx - 1] : 0, e = c.off[idx];
+                for (uint64_t k = b; k < e; ++k) *o++ = c.val[k];
+            }
+            acc[g] = g + 1;
+        }
+        if (isnull) *o = 0;
+        nul[g] = isnull;
+    }
+}
+
 } // namespace tfg
 
 using namespace tfg;
+
+// The value store of one ACC_REF aggregate: n entries in group order.
+struct RefStore {
+    uint8_t *val = nullptr;   // fixed: n values of the argument's width; String: chars
+    uint64_t *scan = nullptr; // String: n + 1 start offsets (scan + 1 = the end offsets)
+    uint8_t *nul = nullptr;   // NULL flags
+    uint64_t n = 0, bytes = 0;
+};
 
 struct tfg_agg {
     Ctx *ctx = nullptr;
@@ -681,6 +796,11 @@ struct tfg_agg {
     GroupsIO st[2];
     uint64_t *bucket_off[2] = {nullptr, nullptr};
     int cur = 0;
+    // row-reference aggregates (ACC_REF: first_row; min / max of Decimal128 / Decimal256 / String):
+    // their value stores and the collators of String min / max
+    bool has_ref = false;
+    int ref_coll[AGG_MAX] = {};
+    RefStore store[AGG_MAX];
     // wide keys (keys128 / key_string): key_type == TFG_KEYS_WIDE, packing spec, and a device
     // buffer holding the packed keys of the block being consumed / the result being written
     KeyPack kp{};
@@ -1053,7 +1173,8 @@ int consume_keyed(tfg_agg *a, int mode, const RowPred &pred, const void *keys, i
         if (val_nulls && val_nulls[i]) o_vnull[i] = cv.take<uint8_t>(n);
         if (val_cnts && val_cnts[i]) o_vcnt[i] = cv.take<uint64_t>(n);
         if (!vals[i]) continue;
-        if (mode == MODE_RAW || (mode == MODE_PARTIAL && S.acc[i] == ACC_ORD)) vw[i] = (int)type_width(S.src_type[i]);
+        if (S.acc[i] == ACC_REF) vw[i] = 8; // candidate references
+        else if (mode == MODE_RAW || (mode == MODE_PARTIAL && S.acc[i] == ACC_ORD)) vw[i] = (int)type_width(S.src_type[i]);
         else vw[i] = 8 * std::max(1, acc_words(S.acc[i]));
         o_val[i] = cv.take<uint4>((n * vw[i] + 15) / 16);
     }
@@ -1240,6 +1361,136 @@ int check_overflow(tfg_agg *a) {
     return fail(TFG_ERR_OVERFLOW, "Decimal256 sum overflow (DECIMAL_OVERFLOW: the sum left Int256)");
 }
 
+// ---- row-reference aggregates (ACC_REF, agg_dev.h): candidates, reference columns, store rebuild
+struct RefIn { // source 1 of an ACC_REF aggregate's candidates: the consumed column (or a merge's source store)
+    const uint8_t *val = nullptr; // fixed-width values, or String chars
+    const uint64_t *off = nullptr; // String: end offsets
+    const uint8_t *nul = nullptr;
+    uint64_t n = 0;
+};
+struct RefCall { // temporaries of one call, freed stream-ordered after its launches
+    Ctx *ctx;
+    CollatedStrings cs[AGG_MAX][2];
+    std::vector<void *> tmp;
+    explicit RefCall(Ctx *c) : ctx(c) {}
+    RefCall(const RefCall &) = delete;
+    RefCall &operator=(const RefCall &) = delete;
+    ~RefCall() {
+        for (void *p : tmp) (void)hipFreeAsync(p, ctx->stream);
+    }
+    int alloc(size_t bytes, void **p) {
+        TFG_HIP(hipMallocAsync(p, std::max<size_t>(bytes, 16), ctx->stream));
+        tmp.push_back(*p);
+        return TFG_OK;
+    }
+};
+
+void ref_store_free(Ctx *ctx, RefStore &st) {
+    if (st.val) (void)hipFreeAsync(st.val, ctx->stream);
+    if (st.scan) (void)hipFreeAsync(st.scan, ctx->stream);
+    if (st.nul) (void)hipFreeAsync(st.nul, ctx->stream);
+    st = RefStore{};
+}
+
+// S.ref[i] of every ACC_REF aggregate for one call: its store, then `in`.  String min / max under a
+// case-insensitive collator compare sort keys of the whole rows ('\0' included, no trim)
+int ref_setup(tfg_agg *a, const RefIn *in, RefCall &rc) {
+    for (int i = 0; i < a->S.n_aggs; ++i) {
+        if (a->S.acc[i] != ACC_REF) continue;
+        RefSrc &R = a->S.ref[i];
+        R = RefSrc{};
+        const RefStore &st = a->store[i];
+        R.n0 = st.n;
+        const int t = a->S.src_type[i];
+        R.v[0] = st.val;
+        R.v[1] = in[i].val;
+        if (t != TFG_STRING) {
+            R.width = (int)type_width(t);
+            continue;
+        }
+        R.o[0] = st.scan ? st.scan + 1 : nullptr;
+        R.o[1] = in[i].off;
+        const int coll = a->ref_coll[i];
+        if (a->S.kind[i] == TFG_AGG_FIRST_ROW || !collator_transforms(coll)) continue;
+        if (int r = collate_strings(a->ctx, coll, st.val, R.o[0], nullptr, nullptr, nullptr, (int64_t)st.n, rc.cs[i][0], true))
+            return r;
+        if (int r = collate_strings(a->ctx, coll, in[i].val, in[i].off, in[i].nul, nullptr, nullptr, (int64_t)in[i].n,
+                                    rc.cs[i][1], true))
+            return r;
+        R.v[0] = rc.cs[i][0].chars;
+        R.o[0] = rc.cs[i][0].offsets();
+        R.v[1] = rc.cs[i][1].chars;
+        R.o[1] = rc.cs[i][1].offsets();
+    }
+    return TFG_OK;
+}
+
+// after a call: each group's winning candidate copied into a new store in group order, the group's
+// reference set to g + 1 (0 stays: no value)
+int ref_rebuild(tfg_agg *a, const RefIn *in) {
+    Ctx *ctx = a->ctx;
+    const uint64_t G = a->n_groups;
+    const GroupsIO &st = a->st[a->cur];
+    const unsigned grid = stream_grid((int64_t)std::max<uint64_t>(G, 1), 256, 4096);
+    for (int i = 0; i < a->S.n_aggs; ++i) {
+        if (a->S.acc[i] != ACC_REF) continue;
+        RefStore &old = a->store[i];
+        const RefCol s0{old.val, old.scan ? old.scan + 1 : nullptr, old.nul}, s1{in[i].val, in[i].off, in[i].nul};
+        uint64_t *acc = (uint64_t *)st.acc[i];
+        RefStore nw;
+        nw.n = G;
+        TFG_HIP(hipMallocAsync((void **)&nw.nul, std::max<uint64_t>(G, 16), ctx->stream));
+        const int t = a->S.src_type[i];
+        if (t != TFG_STRING) {
+            const int w = (int)type_width(t);
+            TFG_HIP(hipMallocAsync((void **)&nw.val, std::max<uint64_t>(G * w, 16), ctx->stream));
+            if (G) {
+                ProfScope _ps(ctx, "agg.ref_store");
+                hipLaunchKernelGGL(ref_store_fixed_kernel, dim3(grid), dim3(256), 0, ctx->stream, acc, G, old.n, w, s0, s1,
+                                   nw.val, nw.nul);
+                TFG_LAUNCH_CHECK();
+            }
+        } else {
+            TFG_HIP(hipMallocAsync((void **)&nw.scan, (G + 1) * 8, ctx->stream));
+            uint64_t total = 0;
+            if (G) {
+                RefCall tmp(ctx);
+                void *len = nullptr, *sc = nullptr;
+                if (int rc = tmp.alloc(G * 8, &len)) return rc;
+                if (int rc = tmp.alloc(scan_tmp_bytes((int64_t)G) + 256, &sc)) return rc;
+                hipLaunchKernelGGL(ref_store_len_kernel, dim3(grid), dim3(256), 0, ctx->stream, (const uint64_t *)acc, G,
+                                   old.n, s0, s1, (uint64_t *)len);
+                TFG_LAUNCH_CHECK();
+                if (int rc = exclusive_scan_u64(ctx, (const uint64_t *)len, nw.scan, (int64_t)G, sc)) return rc;
+                if (int rc = read_back_u64(ctx, nw.scan + G, &total, 1)) return rc;
+            } else {
+                TFG_HIP(hipMemsetAsync(nw.scan, 0, 8, ctx->stream));
+            }
+            nw.bytes = total;
+            TFG_HIP(hipMallocAsync((void **)&nw.val, std::max<uint64_t>(total, 16), ctx->stream));
+            if (G) {
+                ProfScope _ps(ctx, "agg.ref_store");
+                hipLaunchKernelGGL(ref_store_str_kernel, dim3(grid), dim3(256), 0, ctx->stream, acc, G, old.n, s0, s1,
+                                   (const uint64_t *)nw.scan, nw.val, nw.nul);
+                TFG_LAUNCH_CHECK();
+            }
+        }
+        ref_store_free(ctx, old);
+        old = nw;
+    }
+    return TFG_OK;
+}
+
+// the stores after create / reset: empty, or (without key) the one group's "no value"
+int ref_reset(tfg_agg *a) {
+    if (!a->has_ref) return TFG_OK;
+    for (int i = 0; i < a->S.n_aggs; ++i)
+        if (a->S.acc[i] == ACC_REF) ref_store_free(a->ctx, a->store[i]);
+    if (!a->nokey) return TFG_OK;
+    RefIn none[AGG_MAX];
+    return ref_rebuild(a, none); // the group's references are 0 (zeroed state)
+}
+
 int consume_common(tfg_agg *a, int mode, const RowPred &pred, const void *keys, const uint8_t *key_nullmap,
                    const void *const *args, const uint8_t *const *arg_nullmaps, int64_t n) {
     TFG_CHECK(a, TFG_ERR_INVALID_ARG, "agg is null");
@@ -1249,21 +1500,54 @@ int consume_common(tfg_agg *a, int mode, const RowPred &pred, const void *keys, 
     if (int rc = set_device(a->ctx)) return rc;
     const void *vals[AGG_MAX] = {};
     const uint8_t *vnull[AGG_MAX] = {};
+    RefIn rin[AGG_MAX];
     for (int i = 0; i < a->S.n_aggs; ++i) {
         if (mode == MODE_RAW && a->S.kind[i] == TFG_AGG_COUNT_ALL) continue;
         TFG_CHECK(args && args[i], TFG_ERR_INVALID_ARG, "argument %d is null", i);
         vals[i] = args[i];
         vnull[i] = arg_nullmaps ? arg_nullmaps[i] : nullptr;
-        if (vnull[i] && mode == MODE_RAW && (a->S.kind[i] == TFG_AGG_SUM || a->S.acc[i] == ACC_ORD) && !a->S.has_cnt[i])
+        const int acc = a->S.acc[i];
+        if (vnull[i] && mode == MODE_RAW && (a->S.kind[i] == TFG_AGG_SUM || acc == ACC_ORD || acc == ACC_REF) &&
+            !a->arg_nullable[i])
             return fail(TFG_ERR_ILLEGAL_TYPE, "argument %d has a null map but was declared not nullable", i);
+        if (acc != ACC_REF) continue;
+        if (a->S.src_type[i] == TFG_STRING) { // a host tfg_str_col
+            const tfg_str_col *sc = static_cast<const tfg_str_col *>(args[i]);
+            TFG_CHECK(sc->chars && sc->offsets, TFG_ERR_INVALID_ARG, "String argument %d needs chars and offsets", i);
+            rin[i] = RefIn{sc->chars, sc->offsets, vnull[i], (uint64_t)n};
+        } else {
+            rin[i] = RefIn{static_cast<const uint8_t *>(args[i]), nullptr, vnull[i], (uint64_t)n};
+        }
+    }
+    RefCall rc(a->ctx);
+    if (a->has_ref) {
+        if (int r = ref_setup(a, rin, rc)) return r;
+        if (!a->nokey) { // keyed: every row carries its candidate reference through the partition
+            uint64_t n0 = 0;
+            for (int i = 0; i < a->S.n_aggs; ++i)
+                if (a->S.acc[i] == ACC_REF) n0 = a->store[i].n;
+            void *refs = nullptr;
+            if (int r = rc.alloc((size_t)n * 8, &refs)) return r;
+            hipLaunchKernelGGL(ref_iota_kernel, dim3(stream_grid(n, 256, 4096)), dim3(256), 0, a->ctx->stream,
+                               (uint64_t *)refs, n0, n);
+            TFG_LAUNCH_CHECK();
+            for (int i = 0; i < a->S.n_aggs; ++i) {
+                if (a->S.acc[i] != ACC_REF) continue;
+                vals[i] = refs;
+                if (a->S.kind[i] == TFG_AGG_FIRST_ROW) vnull[i] = nullptr; // a NULL first row counts
+            }
+        }
     }
     if (a->nokey) {
-        if (int rc = consume_nokey(a, mode, pred, vals, vnull, n)) return rc;
-        return check_overflow(a);
+        if (int r = consume_nokey(a, mode, pred, vals, vnull, n)) return r;
+    } else {
+        TFG_CHECK(keys, TFG_ERR_INVALID_ARG, "keys are null");
+        if (a->S.key_width == 16) TFG_CHECK(!key_nullmap, TFG_ERR_INVALID_ARG, "packed keys carry their NULL bits");
+        if (int r = consume_keyed(a, mode, pred, keys, a->S.key_width, key_nullmap, vals, vnull, nullptr, nullptr, n))
+            return r;
     }
-    TFG_CHECK(keys, TFG_ERR_INVALID_ARG, "keys are null");
-    if (a->S.key_width == 16) TFG_CHECK(!key_nullmap, TFG_ERR_INVALID_ARG, "packed keys carry their NULL bits");
-    if (int rc = consume_keyed(a, mode, pred, keys, a->S.key_width, key_nullmap, vals, vnull, nullptr, nullptr, n)) return rc;
+    if (a->has_ref)
+        if (int r = ref_rebuild(a, rin)) return r;
     return check_overflow(a);
 }
 
@@ -1278,8 +1562,11 @@ struct AggExtract {
     void *kc[8] = {};
     uint64_t *ko[8] = {};
     uint8_t *kn[8] = {};
-    void *st[AGG_MAX] = {};
+    void *st[AGG_MAX] = {};    // result entries: a device column, or (String) &so[i]
+    void *st_in[AGG_MAX] = {}; // the same states as consume arguments: the column, or (String) &sc[i]
     uint8_t *sn[AGG_MAX] = {};
+    tfg_str_out so[AGG_MAX] = {};
+    tfg_str_col sc[AGG_MAX] = {};
     Ctx *ctx = nullptr;
     ~AggExtract() {
         if (ctx) (void)hipStreamSynchronize(ctx->stream);
@@ -1332,7 +1619,17 @@ static int agg_extract(tfg_agg *a, AggExtract &e) {
         if (int rc = tfg_agg_result_type(a, i, &t, &w)) return rc;
         void *p;
         if (int rc = e.alloc(G * (size_t)w, &p)) return rc;
-        e.st[i] = p;
+        e.st[i] = e.st_in[i] = p;
+        if (t == TFG_STRING) { // min / max / first_row of a String: offsets, then the chars
+            uint64_t bytes = 0;
+            if (int rc = tfg_agg_result_chars(a, i, &bytes)) return rc;
+            void *c;
+            if (int rc = e.alloc(bytes, &c)) return rc;
+            e.so[i] = tfg_str_out{(uint8_t *)c, (uint64_t *)p, bytes};
+            e.sc[i] = tfg_str_col{(const uint8_t *)c, (const uint64_t *)p};
+            e.st[i] = &e.so[i];
+            e.st_in[i] = &e.sc[i];
+        }
         if (int rc = e.alloc(G, &p)) return rc;
         e.sn[i] = (uint8_t *)p;
     }
@@ -1374,7 +1671,7 @@ static int serial_adopt(tfg_agg *a) {
     a->sdict = d;
     a->inner = in;
     a->long_key = false;
-    if (e.G) return serial_consume(a, e.kc, e.ko, e.kn, e.st, e.sn, nullptr, (int64_t)e.G, true);
+    if (e.G) return serial_consume(a, e.kc, e.ko, e.kn, e.st_in, e.sn, nullptr, (int64_t)e.G, true);
     return TFG_OK;
 }
 
@@ -1388,7 +1685,7 @@ static int merge_through_keys(tfg_agg *dst, tfg_agg *src) {
     if (int rc = agg_extract(src, e)) return rc;
     if (e.G == 0) return TFG_OK;
     TFG_HIP(hipStreamSynchronize(src->ctx->stream));
-    return tfg_agg_consume_partial_keys(dst, e.kc, e.ko, e.kn, e.st, e.sn, (int64_t)e.G);
+    return tfg_agg_consume_partial_keys(dst, e.kc, e.ko, e.kn, e.st_in, e.sn, (int64_t)e.G);
 }
 
 extern "C" {
@@ -1439,15 +1736,28 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
             a->result_width[i] = 8 * acc_words(S.acc[i]);
             cell += 8 * lds_acc_words(S.acc[i]);
         } else if (kind == TFG_AGG_MIN || kind == TFG_AGG_MAX || kind == TFG_AGG_FIRST_ROW) {
-            if (!(is_fixed_numeric(at) || at == TFG_DECIMAL32 || at == TFG_DECIMAL64)) {
+            const bool numeric = is_fixed_numeric(at) || at == TFG_DECIMAL32 || at == TFG_DECIMAL64;
+            const bool wide = at == TFG_DECIMAL128 || at == TFG_DECIMAL256 || at == TFG_STRING;
+            const int coll = arg_types ? TFG_ARG_COLLATOR_OF(arg_types[i]) : 0;
+            if (!numeric && !wide) {
                 delete a;
-                return fail(at == TFG_DECIMAL128 || at == TFG_DECIMAL256 ? TFG_ERR_NOT_IMPLEMENTED : TFG_ERR_ILLEGAL_TYPE,
-                            "min / max / first_row over type %d not supported", at);
+                return fail(TFG_ERR_ILLEGAL_TYPE, "min / max / first_row over type %d not supported", at);
             }
-            S.acc[i] = ACC_ORD;
-            S.has_cnt[i] = nullable ? 1 : 0; // NULL result for a group of NULLs only
+            if (at == TFG_STRING && !collator_known(coll)) {
+                delete a;
+                return fail(TFG_ERR_NOT_IMPLEMENTED, "collator %d not supported", coll);
+            }
+            if (kind == TFG_AGG_FIRST_ROW || wide) { // the group keeps a reference to its winning row
+                S.acc[i] = ACC_REF;
+                S.has_cnt[i] = 0;
+                a->has_ref = true;
+                a->ref_coll[i] = at == TFG_STRING ? coll : 0;
+            } else { // numeric min / max: an order key; the count tells "no value" (NULL, or 0 without key)
+                S.acc[i] = ACC_ORD;
+                S.has_cnt[i] = (nullable || a->nokey) ? 1 : 0;
+            }
             a->result_type[i] = at;
-            a->result_width[i] = (int)type_width(at);
+            a->result_width[i] = at == TFG_STRING ? 8 : (int)type_width(at);
             cell += 8;
         } else {
             S.acc[i] = ACC_NONE;
@@ -1539,6 +1849,10 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
         TFG_HIP(hipMemsetAsync(a->blk[0], 0, bytes, ctx->stream));
         a->n_groups = 1;
     }
+    if (int rc = ref_reset(a)) {
+        tfg_agg_destroy(a);
+        return rc;
+    }
     *out = a;
     return TFG_OK;
 }
@@ -1550,6 +1864,11 @@ int tfg_agg_destroy(tfg_agg *a) {
     for (int i = 0; i < 2; ++i) {
         if (a->blk[i]) (void)hipFree(a->blk[i]);
         if (a->bucket_off[i]) (void)hipFree(a->bucket_off[i]);
+    }
+    for (int i = 0; i < AGG_MAX; ++i) {
+        if (a->store[i].val) (void)hipFree(a->store[i].val);
+        if (a->store[i].scan) (void)hipFree(a->store[i].scan);
+        if (a->store[i].nul) (void)hipFree(a->store[i].nul);
     }
     if (a->pack_buf) (void)hipFree(a->pack_buf);
     if (a->pack_err) (void)hipFree(a->pack_err);
@@ -1574,6 +1893,10 @@ int tfg_agg_reset(tfg_agg *a) {
         a->n_groups = 1;
     } else {
         a->n_groups = 0;
+    }
+    if (a->has_ref) {
+        if (int rc = set_device(a->ctx)) return rc;
+        return ref_reset(a);
     }
     return TFG_OK;
 }
@@ -1624,13 +1947,31 @@ int tfg_agg_merge(tfg_agg *dst, tfg_agg *src) {
               TFG_ERR_LOGICAL, "merging aggregators of different signatures");
     for (int i = 0; i < dst->S.n_aggs; ++i)
         TFG_CHECK(dst->S.kind[i] == src->S.kind[i] && dst->S.acc[i] == src->S.acc[i] &&
-                      dst->S.has_cnt[i] == src->S.has_cnt[i],
+                      dst->S.has_cnt[i] == src->S.has_cnt[i] &&
+                      (dst->S.acc[i] != ACC_REF ||
+                       (dst->S.src_type[i] == src->S.src_type[i] && dst->ref_coll[i] == src->ref_coll[i])),
                   TFG_ERR_LOGICAL, "merging aggregators of different signatures");
+    if (int rc = set_device(dst->ctx)) return rc;
     TFG_HIP(hipStreamSynchronize(src->ctx->stream));
+    // row-reference aggregates: the candidates are dst's store, then src's (changeFirstTime(to) /
+    // changeIfLess(to) keep dst's value on ties: Aggregator::mergeDataImpl folds src into dst)
+    RefIn rin[AGG_MAX];
+    RefCall rc(dst->ctx);
+    if (dst->has_ref) {
+        for (int i = 0; i < dst->S.n_aggs; ++i) {
+            if (dst->S.acc[i] != ACC_REF) continue;
+            const RefStore &ss = src->store[i];
+            TFG_CHECK(ss.n == src->n_groups, TFG_ERR_LOGICAL, "value store out of step with the groups");
+            rin[i] = RefIn{ss.val, ss.scan ? ss.scan + 1 : nullptr, ss.nul, ss.n};
+        }
+        if (int r = ref_setup(dst, rin, rc)) return r;
+    }
     if (dst->nokey) {
         hipLaunchKernelGGL(agg_state_add_kernel, dim3(1), dim3(64), 0, dst->ctx->stream, dst->S, dst->st[dst->cur],
                            src->st[src->cur]);
         TFG_LAUNCH_CHECK();
+        if (dst->has_ref)
+            if (int r = ref_rebuild(dst, rin)) return r;
         return check_overflow(dst);
     }
     if (src->n_groups == 0) return TFG_OK;
@@ -1640,11 +1981,21 @@ int tfg_agg_merge(tfg_agg *dst, tfg_agg *src) {
     for (int i = 0; i < src->S.n_aggs; ++i) {
         vals[i] = g.acc[i];
         cnts[i] = g.cnt[i];
+        if (src->S.acc[i] != ACC_REF) continue;
+        void *sh = nullptr; // src's references, moved past dst's store
+        if (int r = rc.alloc(src->n_groups * 8, &sh)) return r;
+        hipLaunchKernelGGL(ref_shift_kernel, dim3(stream_grid((int64_t)src->n_groups, 256, 4096)), dim3(256), 0,
+                           dst->ctx->stream, (const uint64_t *)g.acc[i], dst->store[i].n, (int64_t)src->n_groups,
+                           (uint64_t *)sh);
+        TFG_LAUNCH_CHECK();
+        vals[i] = sh;
     }
     RowPred pred{};
-    if (int rc = consume_keyed(dst, MODE_STATE, pred, g.key, dst->S.key_width == 16 ? 16 : 8, g.key_null, vals, nullptr,
-                               cnts, src->bucket_off[src->cur], (int64_t)src->n_groups))
-        return rc;
+    if (int r = consume_keyed(dst, MODE_STATE, pred, g.key, dst->S.key_width == 16 ? 16 : 8, g.key_null, vals, nullptr,
+                              cnts, src->bucket_off[src->cur], (int64_t)src->n_groups))
+        return r;
+    if (dst->has_ref)
+        if (int r = ref_rebuild(dst, rin)) return r;
     return check_overflow(dst);
 }
 
@@ -1677,12 +2028,46 @@ int tfg_agg_result(tfg_agg *a, void *out_keys, uint8_t *out_key_nullmap, void *c
         rp.state[i] = out_states ? out_states[i] : nullptr;
         rp.state_null[i] = out_state_nullmaps ? out_state_nullmaps[i] : nullptr;
     }
+    const uint64_t G = a->n_groups;
+    for (int i = 0; i < a->S.n_aggs; ++i) { // a String result must fit before anything is written
+        if (a->S.acc[i] != ACC_REF || a->S.src_type[i] != TFG_STRING || !rp.state[i]) continue;
+        const tfg_str_out *so = static_cast<const tfg_str_out *>(rp.state[i]);
+        TFG_CHECK(so->offsets && (so->chars || a->store[i].bytes == 0), TFG_ERR_INVALID_ARG,
+                  "String result %d needs chars and offsets", i);
+        if (a->store[i].bytes > so->chars_capacity)
+            return fail(TFG_ERR_CAPACITY, "String result %d needs %llu chars bytes, capacity %llu", i,
+                        (unsigned long long)a->store[i].bytes, (unsigned long long)so->chars_capacity);
+    }
+    if (int rc = set_device(a->ctx)) return rc;
     { ProfScope _ps(a->ctx, "agg.result");
     hipLaunchKernelGGL(agg_result_kernel, dim3(stream_grid((int64_t)a->n_groups, 256, 4096)), dim3(256), 0,
                        a->ctx->stream, a->S, a->st[a->cur], a->n_groups, a->S.key_width,
                        a->nokey ? nullptr : out_keys, out_key_nullmap, rp);
     }
     TFG_LAUNCH_CHECK();
+    for (int i = 0; i < a->S.n_aggs; ++i) { // row-reference aggregates: their stores are the result
+        if (a->S.acc[i] != ACC_REF) continue;
+        const RefStore &st = a->store[i];
+        TFG_CHECK(st.n == G, TFG_ERR_LOGICAL, "value store out of step with the groups");
+        hipStream_t sm = a->ctx->stream;
+        if (rp.state_null[i]) TFG_HIP(hipMemcpyAsync(rp.state_null[i], st.nul, G, hipMemcpyDeviceToDevice, sm));
+        if (!rp.state[i]) continue;
+        if (a->S.src_type[i] == TFG_STRING) {
+            const tfg_str_out *so = static_cast<const tfg_str_out *>(rp.state[i]);
+            TFG_HIP(hipMemcpyAsync(so->offsets, st.scan + 1, G * 8, hipMemcpyDeviceToDevice, sm));
+            if (st.bytes) TFG_HIP(hipMemcpyAsync(so->chars, st.val, st.bytes, hipMemcpyDeviceToDevice, sm));
+        } else {
+            TFG_HIP(hipMemcpyAsync(rp.state[i], st.val, G * type_width(a->S.src_type[i]), hipMemcpyDeviceToDevice, sm));
+        }
+    }
+    return TFG_OK;
+}
+
+int tfg_agg_result_chars(tfg_agg *a, int i, uint64_t *out_bytes) {
+    TFG_CHECK(a && out_bytes, TFG_ERR_INVALID_ARG, "null argument");
+    if (a->sdict) return tfg_agg_result_chars(a->inner, i, out_bytes);
+    TFG_CHECK(i >= 0 && i < a->S.n_aggs, TFG_ERR_INVALID_ARG, "bad aggregate index");
+    *out_bytes = (a->S.acc[i] == ACC_REF && a->S.src_type[i] == TFG_STRING) ? a->store[i].bytes : 0;
     return TFG_OK;
 }
 

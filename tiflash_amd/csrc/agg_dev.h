@@ -17,13 +17,28 @@ constexpr int BT_BIG = 1024; // for tables too large for two workgroups per CU (
 constexpr int LDS_TABLE_BYTES = 100 * 1024;  // preferred table size (two workgroups per CU)
 constexpr int LDS_TABLE_MAX = 150 * 1024;    // largest table (one 16-wave workgroup per CU)
 
-enum AccKind { ACC_NONE = 0, ACC_I64 = 1, ACC_F64 = 2, ACC_I128 = 3, ACC_I256 = 4, ACC_ORD = 5 };
+enum AccKind { ACC_NONE = 0, ACC_I64 = 1, ACC_F64 = 2, ACC_I128 = 3, ACC_I256 = 4, ACC_ORD = 5, ACC_REF = 6 };
 // 64-bit words of an accumulator of kind k
 __host__ __device__ constexpr int acc_words(int k) { return k == ACC_I256 ? 4 : k == ACC_I128 ? 2 : k == ACC_NONE ? 0 : 1; }
 // ... and in an LDS table: a Decimal256 sum carries a fifth limb there, the sign extension of
 // the exact sum, so a sum past Int256 is detected when the table is flushed (lds_add_i256)
 __host__ __device__ constexpr int lds_acc_words(int k) { return k == ACC_I256 ? 5 : acc_words(k); }
 enum RowMode { MODE_RAW = 0, MODE_PARTIAL = 1, MODE_STATE = 2 };
+
+// Row-reference aggregates (ACC_REF: first_row of any type, min / max of Decimal128 / Decimal256 /
+// String).  The state of a group is a u64 reference to one candidate value, 0 = no value yet.
+// The candidates of one consume are the aggregator's value store (one entry per group of the
+// previous state: refs 1 .. n0) followed by the consumed column (row r: ref n0 + 1 + r; a merge:
+// the source aggregator's store).  References order candidates in input order, so "first row" is
+// the smallest reference and equal min / max values keep the smallest one (the reference's strict
+// changeIfLess / changeIfGreater / changeFirstTime).  After the consume the winning values are
+// copied into a new store in group order (agg.hip, ref_materialise) and every state becomes g + 1.
+struct RefSrc {
+    const uint8_t *v[2];  // [0] store, [1] consumed column: fixed-width values, or String compare bytes
+    const uint64_t *o[2]; // String compare bytes: end offsets (row i = [o[i - 1], o[i]) with o[-1] = 0)
+    uint64_t n0;          // store entries
+    int width;            // fixed: 16 / 32 (signed little-endian limbs compared); 0 = String bytes
+};
 
 struct AggSpec {
     int key_width; // bytes of the key column (1,2,4,8); 0 = without key
@@ -46,6 +61,7 @@ struct AggSpec {
     int bbits;          // bucket radix bits: the in-table slot group comes from the 32 bits of
                         // key * 2^64/phi just below them (one multiply instead of a mixer) ...
     unsigned ngroups;   // ... scaled to the table's cap / GS groups (any count: LDS-sized tables)
+    RefSrc ref[AGG_MAX]; // ACC_REF aggregates: this call's candidates
 };
 
 // Columnar row source staged by the bucket pass (bucket-major).
@@ -152,6 +168,49 @@ __host__ __device__ __forceinline__ uint64_t ord_enc(int kind, int type, uint64_
 }
 __host__ __device__ __forceinline__ uint64_t ord_dec(int kind, int type, uint64_t k) {
     return ord_unbase(type, kind == TFG_AGG_MIN ? ~k : k);
+}
+
+// three-way compare of candidates a, b (>= 1) of a RefSrc: signed limbs, or bytes then length
+// (memcmp order of the compare bytes: raw rows, or collator sort keys)
+__device__ __forceinline__ int ref_cmp(const RefSrc &R, uint64_t a, uint64_t b) {
+    const int sa = a > R.n0, sb = b > R.n0;
+    const uint64_t ia = sa ? a - R.n0 - 1 : a - 1, ib = sb ? b - R.n0 - 1 : b - 1;
+    if (R.width) {
+        const int nw = R.width >> 3;
+        const uint64_t *pa = reinterpret_cast<const uint64_t *>(R.v[sa]) + ia * nw;
+        const uint64_t *pb = reinterpret_cast<const uint64_t *>(R.v[sb]) + ib * nw;
+        const int64_t ha = (int64_t)pa[nw - 1], hb = (int64_t)pb[nw - 1];
+        if (ha != hb) return ha < hb ? -1 : 1;
+        for (int k = nw - 2; k >= 0; --k)
+            if (pa[k] != pb[k]) return pa[k] < pb[k] ? -1 : 1;
+        return 0;
+    }
+    const uint64_t a0 = ia ? R.o[sa][ia - 1] : 0, a1 = R.o[sa][ia] - 1; // the row's '\0' excluded:
+    const uint64_t b0 = ib ? R.o[sb][ib - 1] : 0, b1 = R.o[sb][ib] - 1; // both rows end with it
+    const uint8_t *pa = R.v[sa] + a0, *pb = R.v[sb] + b0;
+    const uint64_t la = a1 - a0, lb = b1 - b0, m = la < lb ? la : lb;
+    for (uint64_t k = 0; k < m; ++k)
+        if (pa[k] != pb[k]) return pa[k] < pb[k] ? -1 : 1;
+    return la < lb ? -1 : la > lb ? 1 : 0;
+}
+// does candidate a replace the state b (0 = empty)?
+__device__ __forceinline__ bool ref_better(int kind, const RefSrc &R, uint64_t a, uint64_t b) {
+    if (b == 0) return true;
+    if (kind == TFG_AGG_FIRST_ROW) return a < b;
+    int c = ref_cmp(R, a, b);
+    if (kind == TFG_AGG_MIN) c = -c;
+    return c > 0 || (c == 0 && a < b);
+}
+// lock-free fold of candidate `mine` into a u64 state cell (LDS or global): every CAS attempt is
+// independent, so lanes of one wave contending for a cell never wait on each other
+__device__ __forceinline__ void ref_combine(uint64_t *cell, uint64_t mine, const RefSrc &R, int kind) {
+    if (mine == 0) return;
+    uint64_t cur = __hip_atomic_load(cell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (ref_better(kind, R, mine, cur)) {
+        const uint64_t prev = atomicCAS((unsigned long long *)cell, (unsigned long long)cur, (unsigned long long)mine);
+        if (prev == cur) return;
+        cur = prev;
+    }
 }
 
 __device__ __forceinline__ void lds_add_i128(uint64_t *cell, uint64_t lo, uint64_t hi) {
@@ -543,6 +602,11 @@ struct Table {
 #pragma unroll
         for (int i = 0; i < NA; ++i) {
             const int kind = S.kind[i];
+            if (S.acc[i] == ACC_REF) { // row references: NULL rows of min / max arrive without a reference
+                if (mode != MODE_STATE && v.vnull[i]) continue;
+                ref_combine(acc_cell(i, cell), v.lo[i], S.ref[i], kind);
+                continue;
+            }
             if (S.acc[i] == ACC_ORD) { // min / max / first_row: max of order keys
                 if (mode == MODE_STATE) {
                     atomicMax((unsigned long long *)acc_cell(i, cell), (unsigned long long)v.lo[i]);
@@ -611,6 +675,8 @@ struct Table {
                 atomicAdd((unsigned long long *)acc_cell(i, cell), ((const unsigned long long *)grp.acc[i])[g]);
             } else if (S.acc[i] == ACC_ORD) {
                 atomicMax((unsigned long long *)acc_cell(i, cell), ((const unsigned long long *)grp.acc[i])[g]);
+            } else if (S.acc[i] == ACC_REF) {
+                ref_combine(acc_cell(i, cell), ((const uint64_t *)grp.acc[i])[g], S.ref[i], S.kind[i]);
             }
             if (S.has_cnt[i]) atomicAdd((unsigned long long *)cnt_cell(i, cell), grp.cnt[i][g]);
         }
@@ -655,6 +721,7 @@ struct Table {
 
 // width in bytes of value column i for a row mode
 __device__ __forceinline__ int val_width(const AggSpec &S, int mode, int i) {
+    if (S.acc[i] == ACC_REF) return 8; // row references in every mode
     // partial min / max / first_row values have the argument's type (the result type)
     if (mode == MODE_PARTIAL && S.acc[i] == ACC_ORD) mode = MODE_RAW;
     if (mode != MODE_RAW) return S.acc[i] == ACC_I256 ? 32 : S.acc[i] == ACC_I128 ? 16 : 8;

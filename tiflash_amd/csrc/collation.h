@@ -39,8 +39,10 @@ struct CollatedStrings {
 };
 
 // Sort keys of rows sel[i] (sel32 / sel64; both null: rows 0..n-1) of a ColumnString under
-// `collator` (collator_transforms).  NULL rows (nullmap) get an empty key.
+// `collator` (collator_transforms).  NULL rows (nullmap) get an empty key.  whole: the sort key of
+// the row with its terminating '\0' and without the padding trim (collator->compare over
+// getDataAtWithTerminatingZero, as SingleValueDataString compares min / max candidates).
 int collate_strings(Ctx *ctx, int collator, const uint8_t *chars, const uint64_t *offsets, const uint8_t *nullmap,
-                    const uint32_t *sel32, const uint64_t *sel64, int64_t n, CollatedStrings &out);
+                    const uint32_t *sel32, const uint64_t *sel64, int64_t n, CollatedStrings &out, bool whole = false);
 
 } // namespace tfg

@@ -35,13 +35,19 @@ struct RowSpan {
     const uint8_t *limit; // one past the row's '\0'
 };
 
+// whole: the row with its terminating '\0' and no trim (the bytes SingleValueDataString compares,
+// getDataAtWithTerminatingZero: a padding collator's right-trim stops at the '\0')
 __device__ __forceinline__ RowSpan row_span(const uint8_t *chars, const uint64_t *offsets, const uint8_t *nullmap,
-                                            int64_t r) {
+                                            int64_t r, bool whole) {
     RowSpan sp{chars, 0, chars};
     if (nullmap && nullmap[r]) return sp;
     const uint64_t b = r ? offsets[r - 1] : 0, e = offsets[r];
     sp.s = chars + b;
     sp.limit = chars + e;
+    if (whole) {
+        sp.len = e - b;
+        return sp;
+    }
     uint64_t len = e - b - 1; // ColumnString rows end with '\0'
     while (len > 0 && sp.s[len - 1] == ' ') --len;
     sp.len = len;
@@ -78,9 +84,9 @@ __device__ __forceinline__ int64_t pick(const uint32_t *s32, const uint64_t *s64
 }
 
 __global__ void gci_len_kernel(const uint8_t *chars, const uint64_t *offsets, const uint8_t *nullmap,
-                               const uint32_t *s32, const uint64_t *s64, int64_t n, uint64_t *len_out) {
+                               const uint32_t *s32, const uint64_t *s64, int64_t n, bool whole, uint64_t *len_out) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const RowSpan sp = row_span(chars, offsets, nullmap, pick(s32, s64, i));
+        const RowSpan sp = row_span(chars, offsets, nullmap, pick(s32, s64, i), whole);
         uint64_t off = 0, nc = 0;
         while (off < sp.len) {
             (void)decode_utf8(sp, off);
@@ -91,10 +97,10 @@ __global__ void gci_len_kernel(const uint8_t *chars, const uint64_t *offsets, co
 }
 
 __global__ void gci_write_kernel(const uint8_t *chars, const uint64_t *offsets, const uint8_t *nullmap,
-                                 const uint32_t *s32, const uint64_t *s64, int64_t n, const uint64_t *start,
+                                 const uint32_t *s32, const uint64_t *s64, int64_t n, bool whole, const uint64_t *start,
                                  uint8_t *out) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const RowSpan sp = row_span(chars, offsets, nullmap, pick(s32, s64, i));
+        const RowSpan sp = row_span(chars, offsets, nullmap, pick(s32, s64, i), whole);
         uint8_t *o = out + start[i];
         uint64_t off = 0;
         while (off < sp.len) {
@@ -168,17 +174,18 @@ __device__ __forceinline__ uint32_t uca_chunk_bytes(uint64_t w) { return w ? 2u 
 
 // 0400 pads (right-trims ' '); 0900 keeps trailing spaces
 template <bool V0900>
-__device__ __forceinline__ RowSpan uca_span(const uint8_t *chars, const uint64_t *offsets, const uint8_t *nullmap, int64_t r) {
-    RowSpan sp = row_span(chars, offsets, nullmap, r);
-    if (V0900 && !(nullmap && nullmap[r])) sp.len = (uint64_t)(sp.limit - sp.s) - 1;
+__device__ __forceinline__ RowSpan uca_span(const uint8_t *chars, const uint64_t *offsets, const uint8_t *nullmap, int64_t r,
+                                            bool whole) {
+    RowSpan sp = row_span(chars, offsets, nullmap, r, whole);
+    if (V0900 && !whole && !(nullmap && nullmap[r])) sp.len = (uint64_t)(sp.limit - sp.s) - 1;
     return sp;
 }
 
 template <bool V0900>
 __global__ void uca_len_kernel(const uint8_t *chars, const uint64_t *offsets, const uint8_t *nullmap,
-                               const uint32_t *s32, const uint64_t *s64, int64_t n, uint64_t *len_out) {
+                               const uint32_t *s32, const uint64_t *s64, int64_t n, bool whole, uint64_t *len_out) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const RowSpan sp = uca_span<V0900>(chars, offsets, nullmap, pick(s32, s64, i));
+        const RowSpan sp = uca_span<V0900>(chars, offsets, nullmap, pick(s32, s64, i), whole);
         uint64_t off = 0, bytes = 0;
         while (off < sp.len) {
             uint64_t f, s;
@@ -190,10 +197,10 @@ __global__ void uca_len_kernel(const uint8_t *chars, const uint64_t *offsets, co
 
 template <bool V0900>
 __global__ void uca_write_kernel(const uint8_t *chars, const uint64_t *offsets, const uint8_t *nullmap,
-                                 const uint32_t *s32, const uint64_t *s64, int64_t n, const uint64_t *start,
+                                 const uint32_t *s32, const uint64_t *s64, int64_t n, bool whole, const uint64_t *start,
                                  uint8_t *out) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const RowSpan sp = uca_span<V0900>(chars, offsets, nullmap, pick(s32, s64, i));
+        const RowSpan sp = uca_span<V0900>(chars, offsets, nullmap, pick(s32, s64, i), whole);
         uint8_t *o = out + start[i];
         uint64_t off = 0;
         while (off < sp.len) {
@@ -233,7 +240,7 @@ CollatedStrings::~CollatedStrings() {
 }
 
 int collate_strings(Ctx *ctx, int collator, const uint8_t *chars, const uint64_t *offsets, const uint8_t *nullmap,
-                    const uint32_t *sel32, const uint64_t *sel64, int64_t n, CollatedStrings &out) {
+                    const uint32_t *sel32, const uint64_t *sel64, int64_t n, CollatedStrings &out, bool whole) {
     TFG_CHECK(collator_transforms(collator), TFG_ERR_NOT_IMPLEMENTED, "collator %d has no sort-key transform",
               collator);
     const bool uca = collator != TFG_COLLATOR_GENERAL_CI, v0900 = collator == TFG_COLLATOR_UCA0900_AI_CI;
@@ -254,13 +261,13 @@ int collate_strings(Ctx *ctx, int collator, const uint8_t *chars, const uint64_t
     const unsigned grid = stream_grid(n, 256, 4096);
     if (!uca)
         hipLaunchKernelGGL(gci_len_kernel, dim3(grid), dim3(256), 0, ctx->stream, chars, offsets, nullmap, sel32, sel64,
-                           n, len);
+                           n, whole, len);
     else if (v0900)
         hipLaunchKernelGGL(uca_len_kernel<true>, dim3(grid), dim3(256), 0, ctx->stream, chars, offsets, nullmap, sel32,
-                           sel64, n, len);
+                           sel64, n, whole, len);
     else
         hipLaunchKernelGGL(uca_len_kernel<false>, dim3(grid), dim3(256), 0, ctx->stream, chars, offsets, nullmap, sel32,
-                           sel64, n, len);
+                           sel64, n, whole, len);
     TFG_LAUNCH_CHECK();
     void *tmp = nullptr;
     TFG_HIP(hipMallocAsync(&tmp, scan_tmp_bytes(n) + 256, ctx->stream));
@@ -270,13 +277,13 @@ int collate_strings(Ctx *ctx, int collator, const uint8_t *chars, const uint64_t
     TFG_HIP(hipMallocAsync((void **)&out.chars, total + 16, ctx->stream));
     if (!uca)
         hipLaunchKernelGGL(gci_write_kernel, dim3(grid), dim3(256), 0, ctx->stream, chars, offsets, nullmap, sel32, sel64,
-                           n, out.scan, out.chars);
+                           n, whole, out.scan, out.chars);
     else if (v0900)
         hipLaunchKernelGGL(uca_write_kernel<true>, dim3(grid), dim3(256), 0, ctx->stream, chars, offsets, nullmap, sel32,
-                           sel64, n, out.scan, out.chars);
+                           sel64, n, whole, out.scan, out.chars);
     else
         hipLaunchKernelGGL(uca_write_kernel<false>, dim3(grid), dim3(256), 0, ctx->stream, chars, offsets, nullmap, sel32,
-                           sel64, n, out.scan, out.chars);
+                           sel64, n, whole, out.scan, out.chars);
     TFG_LAUNCH_CHECK();
     TFG_HIP(hipFreeAsync(len, ctx->stream));
     TFG_HIP(hipFreeAsync(tmp, ctx->stream));

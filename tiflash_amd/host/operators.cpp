@@ -57,12 +57,17 @@ Aggregator::Aggregator(Context &ctx, const Params &params) : ctx_(ctx), params_(
         } else {
             throw Exception("Unknown aggregate function " + d.function, ErrorCodes::NOT_IMPLEMENTED);
         }
+        if (at.isString() && kind != TFG_AGG_MIN && kind != TFG_AGG_MAX && kind != TFG_AGG_FIRST_ROW &&
+            kind != TFG_AGG_COUNT)
+            throw Exception(d.function + " over a String column", ErrorCodes::ILLEGAL_TYPE_OF_ARGUMENT);
         kinds_.push_back(kind);
         arg_types_.push_back(at);
+        const int dev_type = at.isString() ? (int)TFG_STRING : at.type;
         arg_types.push_back(kind == TFG_AGG_COUNT_ALL
                                 ? 0
-                                : (at.type | (at.nullable ? TFG_ARG_NULLABLE : 0) |
-                                   (at.isDecimal() ? TFG_ARG_PREC(at.precision()) : 0)));
+                                : (dev_type | (at.nullable ? TFG_ARG_NULLABLE : 0) |
+                                   (at.isDecimal() ? TFG_ARG_PREC(at.precision()) : 0) |
+                                   (at.isString() && kind != TFG_AGG_COUNT ? TFG_ARG_COLLATOR(d.collator) : 0)));
         arg_scales.push_back(at.scale);
     }
     if (kinds_.empty()) { // only key references: the device aggregator still needs one aggregate
@@ -101,8 +106,16 @@ Aggregator::~Aggregator() {
     if (agg_) tfg_agg_destroy(agg_);
 }
 
+// the device argument of a column: its values, or (String) a tfg_str_col kept in `strs`
+static const void *devArg(const ColumnPtr &c, std::vector<std::unique_ptr<tfg_str_col>> &strs) {
+    if (!c->type.isString()) return c->dataPtr();
+    strs.push_back(std::make_unique<tfg_str_col>(
+        tfg_str_col{(const uint8_t *)c->dataPtr(), c->offsets ? (const uint64_t *)c->offsets->data() : nullptr}));
+    return strs.back().get();
+}
+
 void Aggregator::argPointers(const Block &b, std::vector<const void *> &args, std::vector<const uint8_t *> &nulls,
-                             std::vector<ColumnPtr> &hold) const {
+                             std::vector<ColumnPtr> &hold, std::vector<std::unique_ptr<tfg_str_col>> &strs) const {
     for (size_t i = 0; i < params_.aggregates.size() + (hidden_count_ ? 1 : 0); ++i) {
         if (i < params_.aggregates.size() && dev_index_[i] < 0) continue; // a key reference
         const int k = hidden_count_ ? TFG_AGG_COUNT_ALL : kinds_[dev_index_[i]];
@@ -113,7 +126,7 @@ void Aggregator::argPointers(const Block &b, std::vector<const void *> &args, st
         }
         ColumnPtr c = materialize(ctx_, b.getByName(params_.aggregates[i].argument_names[0]).column);
         hold.push_back(c);
-        args.push_back(c->dataPtr());
+        args.push_back(k == TFG_AGG_COUNT ? c->dataPtr() : devArg(c, strs)); // count reads the null map only
         nulls.push_back(c->nullPtr());
     }
 }
@@ -123,7 +136,8 @@ void Aggregator::executeOnBlock(const Block &block, const FilterPtr &filter) {
     std::vector<const void *> args;
     std::vector<const uint8_t *> nulls;
     std::vector<ColumnPtr> hold;
-    argPointers(block, args, nulls, hold);
+    std::vector<std::unique_ptr<tfg_str_col>> strs;
+    argPointers(block, args, nulls, hold, strs);
     if (packed_) {
         std::vector<const void *> kc;
         std::vector<const uint64_t *> ko;
@@ -159,7 +173,8 @@ void Aggregator::executeOnBlockFiltered(const Block &block, const std::string &p
     std::vector<const void *> args;
     std::vector<const uint8_t *> nulls;
     std::vector<ColumnPtr> hold;
-    argPointers(block, args, nulls, hold);
+    std::vector<std::unique_ptr<tfg_str_col>> strs;
+    argPointers(block, args, nulls, hold, strs);
     ColumnPtr key;
     if (!params_.keys.empty()) key = materialize(ctx_, block.getByName(params_.keys[0]).column);
     ColumnPtr p = materialize(ctx_, block.getByName(pred).column);
@@ -174,11 +189,12 @@ void Aggregator::mergeOnBlock(const Block &partial) {
     std::vector<const void *> states;
     std::vector<const uint8_t *> nulls;
     std::vector<ColumnPtr> hold;
+    std::vector<std::unique_ptr<tfg_str_col>> strs;
     for (size_t i = 0; i < params_.aggregates.size(); ++i) {
         if (dev_index_[i] < 0) continue; // a key reference: the keys carry it
         ColumnPtr c = materialize(ctx_, partial.getByName(params_.aggregates[i].column_name).column);
         hold.push_back(c);
-        states.push_back(c->dataPtr());
+        states.push_back(devArg(c, strs));
         nulls.push_back(c->nullPtr());
     }
     std::shared_ptr<DeviceBuffer> zeros;
@@ -229,11 +245,29 @@ Block Aggregator::convertToBlock(bool final) const {
     std::vector<std::shared_ptr<IColumn>> states;
     std::vector<void *> sp;
     std::vector<uint8_t *> snp;
+    std::vector<std::unique_ptr<tfg_str_out>> souts; // String results (min / max / first_row of a String)
     for (size_t i = 0; i < kinds_.size(); ++i) { // the device aggregates
         int t = 0, w = 0;
         check(tfg_agg_result_type(agg_, (int)i, &t, &w), "tfg_agg_result_type");
         auto c = std::make_shared<IColumn>();
         const bool ord = kinds_[i] == TFG_AGG_MIN || kinds_[i] == TFG_AGG_MAX || kinds_[i] == TFG_AGG_FIRST_ROW;
+        if (t == TFG_STRING) {
+            uint64_t bytes = 0;
+            check(tfg_agg_result_chars(agg_, (int)i, &bytes), "tfg_agg_result_chars");
+            c->type.type = DataType::TYPE_STRING;
+            c->type.nullable = arg_types_[i].nullable || kinds_[i] == TFG_AGG_FIRST_ROW;
+            c->rows = g;
+            c->chars = bytes;
+            c->data = std::make_shared<DeviceBuffer>(ctx_, std::max<uint64_t>(bytes, 1));
+            c->offsets = std::make_shared<DeviceBuffer>(ctx_, std::max<size_t>(g, 1) * 8);
+            if (c->type.nullable) c->nullmap = std::make_shared<DeviceBuffer>(ctx_, std::max<size_t>(g, 1));
+            souts.push_back(std::make_unique<tfg_str_out>(
+                tfg_str_out{(uint8_t *)c->data->data(), (uint64_t *)c->offsets->data(), bytes}));
+            sp.push_back(souts.back().get());
+            snp.push_back(c->nullmap ? (uint8_t *)c->nullmap->data() : nullptr);
+            states.push_back(c);
+            continue;
+        }
         c->type.type = t;
         c->type.scale = kinds_[i] == TFG_AGG_SUM || ord ? arg_types_[i].scale : 0;
         if (ord) c->type.prec = arg_types_[i].prec; // min / max / first_row: the argument's type

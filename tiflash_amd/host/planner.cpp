@@ -66,8 +66,16 @@ static Expr unaryAgg(ExprType tp, Expr arg) {
     e.children.push_back(std::move(arg));
     return e;
 }
-Expr Expr::min(Expr arg) { return unaryAgg(ExprType::Min, std::move(arg)); }
-Expr Expr::max(Expr arg) { return unaryAgg(ExprType::Max, std::move(arg)); }
+Expr Expr::min(Expr arg, int collator) {
+    Expr e = unaryAgg(ExprType::Min, std::move(arg));
+    e.collator = collator;
+    return e;
+}
+Expr Expr::max(Expr arg, int collator) {
+    Expr e = unaryAgg(ExprType::Max, std::move(arg));
+    e.collator = collator;
+    return e;
+}
 Expr Expr::firstRow(Expr arg) { return unaryAgg(ExprType::First, std::move(arg)); }
 Expr Expr::count() {
     Expr e;
@@ -355,6 +363,7 @@ AggPlan planAggregation(Context &ctx, const dag::Executor &e, const Block &heade
             // AggregateFunctionMinMaxAny.cpp:155-159 (tipb Min / Max / First -> min / max / first_row,
             // DAGUtils.cpp:69)
             d.function = f.tp == ExprType::Min ? "min" : f.tp == ExprType::Max ? "max" : "first_row";
+            d.collator = f.collator; // IAggregateFunction::setCollators (String min / max)
             if (f.children.size() != 1) throw Exception(d.function + " needs one argument", ErrorCodes::BAD_ARGUMENTS);
         } else {
             unsupported("this aggregate function");

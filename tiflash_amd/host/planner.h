@@ -51,6 +51,7 @@ struct Expr {
     Field literal;              // Int64 / Uint64 / Float64 / MysqlDecimal
     ScalarFuncSig sig = ScalarFuncSig::LTInt;
     std::vector<Expr> children; // ScalarFunc operands; aggregate arguments (count(*): none)
+    int collator = TFG_COLLATOR_NONE; // field_type.collate of a min / max over a String (tfg_collator)
 
     static Expr col(int64_t offset);
     static Expr i64(int64_t v);
@@ -62,8 +63,8 @@ struct Expr {
     static Expr count();          // count(*)
     static Expr count(Expr arg);  // count(arg): non-NULL values
     // tipb::ExprType::Min / Max / First (first_row: TiDB's GROUP BY output columns, DAGUtils.cpp:69)
-    static Expr min(Expr arg);
-    static Expr max(Expr arg);
+    static Expr min(Expr arg, int collator = TFG_COLLATOR_NONE);
+    static Expr max(Expr arg, int collator = TFG_COLLATOR_NONE);
     static Expr firstRow(Expr arg);
 };
 

@@ -272,6 +272,9 @@ struct AggregateDescription {
     std::string function;                    // "sum" | "count" | "min" | "max" | "first_row"
     std::vector<std::string> argument_names; // count() has none
     std::string column_name;
+    // min / max over a String: the collator the comparisons use (IAggregateFunction::setCollators,
+    // SingleValueDataString::setCollators, AggregateFunctionMinMaxAny.h:272-275)
+    int collator = TFG_COLLATOR_NONE;
 };
 using AggregateDescriptions = std::vector<AggregateDescription>;
 
@@ -319,8 +322,9 @@ private:
     std::vector<int> dev_index_;
     std::vector<int> ref_key_; // aggregate i -> the key index it repeats (-1: none)
     bool hidden_count_ = false; // every aggregate repeats a key: the device aggregator counts rows
+    // String arguments / states travel as tfg_str_col structs held in `strs`
     void argPointers(const Block &b, std::vector<const void *> &args, std::vector<const uint8_t *> &nulls,
-                     std::vector<ColumnPtr> &hold) const;
+                     std::vector<ColumnPtr> &hold, std::vector<std::unique_ptr<tfg_str_col>> &strs) const;
     void insertAggregateColumns(Block &out, const std::vector<std::shared_ptr<IColumn>> &states,
                                 const std::vector<ColumnPtr> &keys, size_t g) const;
     void keyPointers(const Block &b, std::vector<const void *> &cols, std::vector<const uint64_t *> &offs,
