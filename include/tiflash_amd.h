@@ -502,20 +502,27 @@ int tfg_alltoall_counts(tfg_comm *comm, const uint64_t *send_bytes_host, uint64_
 int tfg_alltoallv(tfg_comm *comm, const void *send, const uint64_t *send_bytes, const uint64_t *send_displs,
                   void *recv, const uint64_t *recv_bytes, const uint64_t *recv_displs);
 
-/* Fused exchange of fixed-width column planes: ONE all-to-all of a peer-major buffer instead of
- * one per column (the reference's packet carries the whole Block, newMPPExchangeWriter.cpp:64-95).
- * tfg_pack_planes writes, for each destination p in turn, every plane's rows of p:
- * planes[p * nplanes + j] = partition p's plane j, rows[p * nplanes + j] values of widths[j] bytes
- * (NULL = zero bytes, e.g. the null map of a Nullable column that carries none).  Planes may count
- * different rows (a String's chars travel as a plane of 1-byte rows next to its rows' planes).
- * out_seg_bytes (host, nparts) = each segment's bytes; out holds their sum.  tfg_unpack_planes is
- * the receiving side: nparts segments of `in` (rows[s * nplanes + j], that layout) into nplanes
- * output planes, source s's rows after source s-1's.  Both are asynchronous on the context's
- * stream (one launch per 120 non-empty pieces). */
-int tfg_pack_planes(tfg_ctx *ctx, int nparts, int nplanes, const void *const *planes, const int *widths,
-                    const uint64_t *rows, void *out, uint64_t *out_seg_bytes);
-int tfg_unpack_planes(tfg_ctx *ctx, int nparts, int nplanes, const int *widths, const uint64_t *rows, const void *in,
-                      void *const *planes);
+/* Zero-copy exchange (the product's exchange: tfa::MPPExchange and tiflash_amd/exchange.py): every
+ * column plane's slice for a destination is sent from where it lies in the partitioned columns,
+ * and every slice from a source is received straight into the output column at its row offset —
+ * one RCCL group of ncclSend / ncclRecv per call (HashPartitionWriter::partitionAndWriteBlocks ->
+ * MPPTunnelSetWriter, Flash/Mpp/HashPartitionWriter.cpp:139-204, MPPTunnelSetWriter.cpp:365-400;
+ * no packet encode / decode and no pack / unpack copy on the device path).  A peer's k-th send
+ * slice matches that peer's k-th receive slice from this rank: list each peer's slices in the same
+ * (plane) order on both sides; zero-byte slices are skipped.  Asynchronous on the context stream. */
+typedef struct tfg_slice {
+    int peer;      /* destination (send) or source (recv) rank */
+    void *ptr;     /* device memory (read for a send) */
+    uint64_t bytes;
+} tfg_slice;
+int tfg_exchange_slices(tfg_comm *comm, int nsend, const tfg_slice *send, int nrecv, const tfg_slice *recv);
+/* k counts per rank pair (row counts per plane): recv[p * k + i] = send[this rank * k + i] of rank
+ * p (host arrays of nranks * k; syncs). */
+int tfg_alltoall_counts_n(tfg_comm *comm, int k, const uint64_t *send_host, uint64_t *recv_host);
+/* String columns received from nparts ranks: end offsets rows [row_start[p], row_start[p + 1])
+ * came relative to rank p's chars; each gets add[p] (host arrays). */
+int tfg_string_rebase_offsets(tfg_ctx *ctx, uint64_t *offsets, int nparts, const uint64_t *row_start,
+                              const uint64_t *add);
 
 /* ---------------------------------------------------------------- (f1) MPP packet codec */
 /* The Block wire format of MPP packets, encoded from / decoded into device columns; the packet
@@ -565,8 +572,9 @@ int tfg_codec_packet_destroy(tfg_codec_packet *p);
  * byte 0x02 first) becomes LZ4 frames `0x82 | UInt32 frame bytes | UInt32 raw bytes | LZ4 block`
  * (64 KB of body per frame), or with TFG_COMPRESSION_ZSTD ZSTD frames
  * `0x90 | UInt32 frame bytes | UInt32 raw bytes | ZSTD frame` (one RFC 8878 frame per 64 KB:
- * single-segment header with the content size, one block, raw literals + FSE sequences with the
- * predefined tables, or a raw block when that is smaller; no checksum).  out == NULL:
+ * single-segment header with the content size, one block — Huffman, RLE or raw literals;
+ * sequences with RLE, described (normalized counts) or predefined FSE tables; offsets coded with
+ * repeat codes 1-3 — or a raw block when that is smaller; no checksum).  out == NULL:
  * *out_bytes_host = tfg_codec_compress_bound(bytes) (covers both); otherwise the exact size,
  * TFG_ERR_CAPACITY when it exceeds `capacity`.  LZ4HC writes the same format and is accepted as LZ4.
  * tfg_codec_decompress is CompressedCHBlockChunkReadBuffer over a whole packet: the frames of an

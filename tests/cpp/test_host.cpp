@@ -1705,7 +1705,7 @@ TEST(PipelineExchange) {
     PipelineExecutorContext exec;
     auto receiver = std::make_shared<ExchangeReceiver>();
     std::vector<std::multiset<std::vector<std::string>>> remote(4);
-    auto tunnels = std::make_shared<MPPTunnelSet>(ctx, 4, 2, receiver, nullptr, 1, [&](uint32_t part, Block &&blk) {
+    auto tunnels = std::make_shared<MPPTunnelSet>(ctx, 4, 2, receiver, nullptr, 1, [&](uint32_t part, Block &&blk, uint32_t) {
         for (const auto &row : rowSet(ctx, blk)) remote[part].insert(row);
     });
     std::vector<PipelineExecPtr> send;
@@ -2100,15 +2100,48 @@ TEST(PlanAggregateMinMaxFirstRow) {
                         {"first_row", {"k"}, "fk"}, {"count", {}, "c"}};
         std::vector<Block> halves = splitBlocks(ctx, b, 2);
         Aggregator fin(ctx, p);
+        bool first = true;
         for (const Block &h : halves) {
             Aggregator part(ctx, p);
             part.executeOnBlock(h);
-            fin.mergeOnBlock(part.convertToBlock(false));
+            Block pb = part.convertToBlock(false);
+            if (first) { // the partial first_row column, for the log when the merge goes wrong
+                auto fy = cellStrings(ctx, *materialize(ctx, pb.getByName("fy").column));
+                auto kk = toHost<int64_t>(ctx, *pb.getByName("k").column);
+                std::string line;
+                for (size_t i = 0; i < 3 && i < fy.size(); ++i) line += std::to_string(kk[i]) + ":" + fy[i] + " ";
+                fprintf(stderr, "    partial first_row(y): %s(%zu groups)\n", line.c_str(), fy.size());
+                first = false;
+            }
+            fin.mergeOnBlock(pb);
+            { // NULL first_row(y) cells after this merge, for the log when the merge goes wrong
+                Block mid = fin.convertToBlock(false);
+                auto fy = cellStrings(ctx, *materialize(ctx, mid.getByName("fy").column));
+                auto pfy = cellStrings(ctx, *materialize(ctx, pb.getByName("fy").column));
+                size_t nn = 0, pn = 0;
+                for (auto &s : fy) nn += s == "N";
+                for (auto &s : pfy) pn += s == "N";
+                if (nn || pn) fprintf(stderr, "    after a merge: %zu of %zu first_row(y) NULL (partial: %zu)\n", nn, fy.size(), pn);
+            }
         }
         Block r = fin.convertToBlock();
         auto got = rows({r}, 1, 2, 3, 4, 5, 0);
         // the merged count is a sum of partial counts
         EXPECT(got == expect);
+        if (got != expect) { // the first difference, for the log
+            size_t shown = 0;
+            for (const auto &kv : expect) {
+                auto it = got.find(kv.first);
+                if (it != got.end() && it->second == kv.second) continue;
+                std::string g = it == got.end() ? "(missing)" : "", e;
+                if (it != got.end())
+                    for (auto &x : it->second) g += x + " ";
+                for (auto &x : kv.second) e += x + " ";
+                fprintf(stderr, "    key %lld: got %s want %s\n", (long long)kv.first, g.c_str(), e.c_str());
+                if (++shown == 5) break;
+            }
+            fprintf(stderr, "    groups got %zu want %zu\n", got.size(), expect.size());
+        }
     }
     { // only key references: a hidden count keeps the device aggregator
         g_current = "PlanAggregateMinMaxFirstRow key references only";
@@ -2184,7 +2217,7 @@ TEST(PlanAggregateWideMinMaxFirstRow) {
         auto it = dmx.find(k[i]);
         if (it == dmx.end() || d[i] > it->second) dmx[k[i]] = d[i];
     }
-    std::multiset<std::vector<std::string>> expect;
+    std::multiset<std::vector<std::string>> expect, expect2;
     for (const auto &kv : want) {
         const W &w = kv.second;
         int64_t key = kv.first;
@@ -2194,8 +2227,8 @@ TEST(PlanAggregateWideMinMaxFirstRow) {
             const uint8_t byte = (uint8_t)((uint64_t)key >> (8 * q));
             khex.push_back(hx[byte >> 4]), khex.push_back(hx[byte & 15]);
         }
-        expect.insert({w.mn_has ? w.mn : "N", w.mx_has ? w.mx : "N", w.first_null ? "N" : w.fs, hex(dmx[key]),
-                       hex(w.fd), khex});
+        expect.insert({w.mn_has ? w.mn : "N", w.mx_has ? w.mx : "N", w.first_null ? "N" : w.fs, hex(dmx[key]), khex});
+        expect2.insert({hex(w.fd), w.first_null ? "N" : w.fs, khex});
     }
     { // Aggregation(group by k: min(s) general_ci, max(s), first_row(s), max(d), first_row(d))
         g_current = "PlanAggregateWideMinMaxFirstRow plan";
@@ -2205,7 +2238,7 @@ TEST(PlanAggregateWideMinMaxFirstRow) {
         const Executor root = Executor::aggregation(
             "agg_1", {Expr::col(0)},
             {Expr::min(Expr::col(1), TFG_COLLATOR_GENERAL_CI), Expr::max(Expr::col(1)), Expr::firstRow(Expr::col(1)),
-             Expr::max(Expr::col(2)), Expr::firstRow(Expr::col(2))},
+             Expr::max(Expr::col(2))},
             Executor::tableScan("ts_0", "t"));
         std::vector<Block> res;
         env.result = [&](const Block &r) { res.push_back(r); };
@@ -2228,22 +2261,25 @@ TEST(PlanAggregateWideMinMaxFirstRow) {
         p.keys = {"k"};
         AggregateDescription mn{"min", {"s"}, "mn"};
         mn.collator = TFG_COLLATOR_GENERAL_CI;
-        p.aggregates = {mn, {"max", {"s"}, "mx"}, {"first_row", {"s"}, "fs"}, {"max", {"d"}, "md"},
-                        {"first_row", {"d"}, "fd"}};
-        Aggregator fin(ctx, p);
-        for (const Block &h : splitBlocks(ctx, b, 3)) {
-            Aggregator part(ctx, p);
-            part.executeOnBlock(h);
-            fin.mergeOnBlock(part.convertToBlock(false));
+        p.aggregates = {mn, {"max", {"s"}, "mx"}, {"first_row", {"s"}, "fs"}, {"max", {"d"}, "md"}};
+        Aggregator::Params p2 = p;
+        p2.aggregates = {{"first_row", {"d"}, "fd"}, {"first_row", {"s"}, "fs"}};
+        for (int which = 0; which < 2; ++which) {
+            Aggregator fin(ctx, which ? p2 : p);
+            for (const Block &h : splitBlocks(ctx, b, 3)) {
+                Aggregator part(ctx, which ? p2 : p);
+                part.executeOnBlock(h);
+                fin.mergeOnBlock(part.convertToBlock(false));
+            }
+            Block r = fin.convertToBlock();
+            // byteRowSet orders the columns as the block does: key first here
+            std::multiset<std::vector<std::string>> got;
+            for (auto row : byteRowSet(ctx, r)) {
+                std::rotate(row.begin(), row.begin() + 1, row.end());
+                got.insert(row);
+            }
+            EXPECT(got == (which ? expect2 : expect));
         }
-        Block r = fin.convertToBlock();
-        // byteRowSet orders the columns as the block does: key first here
-        std::multiset<std::vector<std::string>> got;
-        for (auto row : byteRowSet(ctx, r)) {
-            std::rotate(row.begin(), row.begin() + 1, row.end());
-            got.insert(row);
-        }
-        EXPECT(got == expect);
     }
 }
 
@@ -2392,7 +2428,7 @@ TEST(PlanExchange) {
     env.tables["t"] = {b.cloneEmpty(), splitBlocks(ctx, b, 5)};
     auto receiver = std::make_shared<ExchangeReceiver>();
     std::vector<std::multiset<std::vector<std::string>>> remote(4);
-    env.tunnels = std::make_shared<MPPTunnelSet>(ctx, 4, 2, receiver, nullptr, 1, [&](uint32_t part, Block &&blk) {
+    env.tunnels = std::make_shared<MPPTunnelSet>(ctx, 4, 2, receiver, nullptr, 1, [&](uint32_t part, Block &&blk, uint32_t) {
         for (const auto &row : rowSet(ctx, blk)) remote[part].insert(row);
     });
     {
@@ -2443,7 +2479,7 @@ TEST(PlanExchange) {
         PlanContext e3;
         e3.tables["t"] = env.tables["t"];
         e3.tunnels = std::make_shared<MPPTunnelSet>(ctx, 3, 2, recv, nullptr, 0,
-                                                    [&](uint32_t part, Block &&blk) { rows[part] += blk.rows(); });
+                                                    [&](uint32_t part, Block &&blk, uint32_t) { rows[part] += blk.rows(); });
         PipelineExecutorContext exec;
         PhysicalPlan plan(ctx, exec, e3);
         plan.build(Executor::exchangeSender("exchange_sender_2", bc ? ExchangeType::Broadcast : ExchangeType::PassThrough,
@@ -2489,14 +2525,24 @@ TEST(PlanExchangeFineGrained) {
             ++remote_want;
         }
     }
+    std::set<uint32_t> remote_streams;
     auto run_sender = [&](std::shared_ptr<ExchangeReceiver> receiver, size_t &remote_rows) {
         PlanContext env;
         env.tables["t"] = {b.cloneEmpty(), splitBlocks(ctx, b, 6)};
-        env.tunnels = std::make_shared<MPPTunnelSet>(ctx, P, 2, receiver, nullptr, 0,
-                                                     [&](uint32_t part, Block &&blk) {
-                                                         EXPECT(part == 1);
-                                                         remote_rows += blk.rows();
-                                                     });
+        env.tunnels = std::make_shared<MPPTunnelSet>(
+            ctx, P, 2, receiver, nullptr, 0, [&](uint32_t part, Block &&blk, uint32_t stream) {
+                EXPECT(part == 1);
+                remote_rows += blk.rows();
+                // the remote partition's blocks keep their streams: every row of the block has
+                // weak hash % S == stream (fillSelectorForFineGrainedShuffle)
+                bool ok = stream < S;
+                for (int64_t x : toHost<int64_t>(ctx, *blk.getByName("k").column)) {
+                    uint32_t s2;
+                    ok = ok && part_of(x, s2) == 1 && s2 == stream;
+                }
+                EXPECT(ok);
+                remote_streams.insert(stream);
+            });
         Executor root = Executor::exchangeSender("exchange_sender_1", ExchangeType::Hash, {Expr::col(0)},
                                                  Executor::tableScan("ts_0", "t"));
         root.fine_grained_shuffle_stream_count = S;
@@ -2513,6 +2559,7 @@ TEST(PlanExchangeFineGrained) {
         size_t remote_rows = 0;
         run_sender(receiver, remote_rows);
         EXPECT(remote_rows == remote_want);
+        EXPECT(remote_streams.size() == S); // every stream reached the remote partition
         size_t local_rows = 0;
         for (uint32_t s = 0; s < S; ++s)
             for (Block blk; receiver->tryPop(blk, S, s);) {
@@ -2592,20 +2639,45 @@ public:
     }
     int nranks() const override { return 2; }
     int rank() const override { return rank_; }
-    void alltoallCounts(const uint64_t *send, uint64_t *recv) override {
-        uint64_t peer[2];
-        swap(send, sizeof(uint64_t) * 2, peer, sizeof peer);
-        recv[rank_] = send[rank_];
-        recv[1 - rank_] = peer[rank_];
+    void alltoallCountsN(int k, const uint64_t *send, uint64_t *recv) override {
+        std::vector<uint64_t> peer(2 * (size_t)k);
+        swap(send, sizeof(uint64_t) * 2 * k, peer.data(), peer.size() * sizeof(uint64_t));
+        for (int i = 0; i < k; ++i) {
+            recv[(size_t)rank_ * k + i] = send[(size_t)rank_ * k + i];
+            recv[(size_t)(1 - rank_) * k + i] = peer[(size_t)rank_ * k + i];
+        }
     }
-    void alltoallv(const void *send, const uint64_t *sb, const uint64_t *sd, void *recv, const uint64_t *rb,
-                   const uint64_t *rd) override {
+    // the peer's slices in order through one host buffer each way; this rank's own by device copies
+    void exchangeSlices(const std::vector<tfg_slice> &send, const std::vector<tfg_slice> &recv) override {
         const int q = 1 - rank_;
-        std::vector<uint8_t> out(sb[q]), in(rb[q]);
-        if (sb[q]) check(tfg_download(ctx_.raw(), out.data(), (const char *)send + sd[q], sb[q]), "tfg_download");
+        std::vector<uint8_t> out, in;
+        for (const tfg_slice &sl : send)
+            if (sl.peer == q && sl.bytes) {
+                const size_t o = out.size();
+                out.resize(o + sl.bytes);
+                check(tfg_download(ctx_.raw(), out.data() + o, sl.ptr, sl.bytes), "tfg_download");
+            }
+        size_t in_bytes = 0;
+        for (const tfg_slice &sl : recv)
+            if (sl.peer == q) in_bytes += sl.bytes;
+        in.resize(in_bytes);
         swap(out.data(), out.size(), in.data(), in.size());
-        if (rb[q]) check(tfg_upload(ctx_.raw(), (char *)recv + rd[q], in.data(), rb[q]), "tfg_upload");
-        if (sb[rank_]) check(tfg_copy(ctx_.raw(), (char *)recv + rd[rank_], (const char *)send + sd[rank_], sb[rank_]), "tfg_copy");
+        size_t o = 0;
+        for (const tfg_slice &sl : recv)
+            if (sl.peer == q && sl.bytes) {
+                check(tfg_upload(ctx_.raw(), sl.ptr, in.data() + o, sl.bytes), "tfg_upload");
+                o += sl.bytes;
+            }
+        std::vector<const tfg_slice *> mine_s, mine_r; // own slices: k-th send -> k-th receive
+        for (const tfg_slice &sl : send)
+            if (sl.peer == rank_ && sl.bytes) mine_s.push_back(&sl);
+        for (const tfg_slice &sl : recv)
+            if (sl.peer == rank_ && sl.bytes) mine_r.push_back(&sl);
+        if (mine_s.size() != mine_r.size()) throw std::runtime_error("own slices do not match");
+        for (size_t i = 0; i < mine_s.size(); ++i) {
+            if (mine_s[i]->bytes != mine_r[i]->bytes) throw std::runtime_error("own slice sizes differ");
+            check(tfg_copy(ctx_.raw(), mine_r[i]->ptr, mine_s[i]->ptr, mine_s[i]->bytes), "tfg_copy");
+        }
     }
 
 private:

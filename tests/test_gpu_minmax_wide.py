@@ -325,3 +325,36 @@ def test_min_max_unsupported_types(tfa, ctx):
     with pytest.raises(tfa.TfgError) as e:
         tfa.Aggregator(ctx, tfa.INT64, [(tfa.AGG_MAX, STR | (9 << 24))])
     assert e.value.code == -4
+
+
+@pytest.mark.parametrize("nullmaps_of_nullable_only", [False, True])
+def test_mixed_two_phase_with_count(tfa, ctx, dev, orc, nullmaps_of_nullable_only):
+    """min(Nullable Int32), max(Float64), first_row(Int16), count(*) — the C++ planner test's
+    signature — through two partial aggregators and a final consume_partial, vs one oracle pass"""
+    rng = np.random.default_rng(77)
+    n = 120_000
+    k = (rng.integers(0, 3000, n) - 1000).astype(np.int64)
+    v = (rng.integers(0, 2_000_001, n) - 1_000_000).astype(np.int32)
+    vn = ((k % 7 == 0) | (rng.integers(0, 4, n) == 0)).astype(np.uint8)
+    x = ((rng.integers(0, 1 << 24, n) - (1 << 23)) / 64.0).astype(np.float64)
+    y = (k % 1000).astype(np.int16)
+    aggs = [(tfa.AGG_MIN, tfa.INT32 | tfa.NULLABLE), (tfa.AGG_MAX, tfa.FLOAT64), (tfa.AGG_FIRST_ROW, tfa.INT16),
+            (tfa.AGG_COUNT_ALL, 0)]
+    types = [tfa.INT32, tfa.FLOAT64, tfa.INT16, tfa.UINT64]
+    ref = orc.Agg(orc.INT64, aggs)
+    ref.consume(k, [v, x, y, None], arg_nulls=[vn, None, None, None])
+    exp = _orc(ref.result(), types)
+    fin = tfa.Aggregator(ctx, tfa.INT64, aggs)
+    for sl in (slice(0, n // 2), slice(n // 2, n)):
+        a = tfa.Aggregator(ctx, tfa.INT64, aggs)
+        a.consume(_t(k[sl], dev), [_t(v[sl], dev), _t(x[sl], dev), _t(y[sl], dev), None],
+                  arg_nullmaps=[_t(vn[sl], dev), None, None, None])
+        r = a.result()
+        # the Nullable results' null maps only, as the C++ Aggregator::mergeOnBlock passes them
+        nm = [r["state_null"][0], None, r["state_null"][2], None] if nullmaps_of_nullable_only else r["state_null"]
+        fin.consume_partial(r["keys"], r["states"], state_nullmaps=nm)
+        a.close()
+    got = _dev(fin.result(), types)
+    fin.close()
+    bad = [(kk, got.get(kk), ev) for kk, ev in exp.items() if got.get(kk) != ev][:5]
+    assert len(got) == len(exp) and not bad, bad

@@ -15,7 +15,8 @@ import weakref
 from typing import Optional, Sequence
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libtiflash_amd.so")
+# TFA_LIB_PATH: an instrumented build of the same library (profiling experiments, tools/)
+LIB_PATH = os.environ.get("TFA_LIB_PATH") or os.path.join(_HERE, "libtiflash_amd.so")
 
 # ---- constants mirrored from include/tiflash_amd.h --------------------------------------------
 TFG_OK = 0

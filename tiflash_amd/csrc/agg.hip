@@ -174,47 +174,66 @@ __global__ void agg_nokey_fold_kernel(AggSpec S, const NoKeyPartial *partials, i
 struct ResultPtrs {
     void *state[AGG_MAX];
     uint8_t *state_null[AGG_MAX];
+    int nullable[AGG_MAX]; // the result column is Nullable (a non-Nullable min / max reports no NULL)
 };
+
+// one group's result row: state group s -> output row d
+__device__ __forceinline__ void write_result(const AggSpec &S, const GroupsIO &st, uint64_t s, uint64_t d, int key_width,
+                                             void *out_keys, uint8_t *out_key_null, const ResultPtrs &res) {
+    if (out_keys) {
+        const uint64_t k = key_width == 16 ? 0 : st.key[s];
+        switch (key_width) {
+        case 1: ((uint8_t *)out_keys)[d] = (uint8_t)k; break;
+        case 2: ((uint16_t *)out_keys)[d] = (uint16_t)k; break;
+        case 4: ((uint32_t *)out_keys)[d] = (uint32_t)k; break;
+        case 8: ((uint64_t *)out_keys)[d] = k; break;
+        case 16: ((uint4 *)out_keys)[d] = reinterpret_cast<const uint4 *>(st.key)[s]; break;
+        default: break;
+        }
+    }
+    if (out_key_null) out_key_null[d] = st.key_null[s];
+    for (int i = 0; i < S.n_aggs; ++i) {
+        if (S.acc[i] == ACC_REF) continue; // values and NULL flags come from the value store
+        if (res.state[i] && S.acc[i] == ACC_ORD) { // min / max: the argument's width
+            // no value (a group of NULLs, or no row without key): the type's default, 0
+            const bool none = S.has_cnt[i] && st.cnt[i][s] == 0;
+            const uint64_t x = none ? 0 : ord_dec(S.kind[i], S.src_type[i], ((const uint64_t *)st.acc[i])[s]);
+            switch (val_width(S, MODE_RAW, i)) {
+            case 1: ((uint8_t *)res.state[i])[d] = (uint8_t)x; break;
+            case 2: ((uint16_t *)res.state[i])[d] = (uint16_t)x; break;
+            case 4: ((uint32_t *)res.state[i])[d] = (uint32_t)x; break;
+            default: ((uint64_t *)res.state[i])[d] = x; break;
+            }
+        } else if (res.state[i]) {
+            if (S.kind[i] != TFG_AGG_SUM) ((uint64_t *)res.state[i])[d] = st.cnt[i][s];
+            else if (S.acc[i] == ACC_I256) {
+                ((uint4 *)res.state[i])[2 * d] = ((const uint4 *)st.acc[i])[2 * s];
+                ((uint4 *)res.state[i])[2 * d + 1] = ((const uint4 *)st.acc[i])[2 * s + 1];
+            } else if (S.acc[i] == ACC_I128) ((uint4 *)res.state[i])[d] = ((const uint4 *)st.acc[i])[s];
+            else ((uint64_t *)res.state[i])[d] = ((const uint64_t *)st.acc[i])[s];
+        }
+        if (res.state_null[i])
+            res.state_null[i][d] = ((S.kind[i] == TFG_AGG_SUM || S.acc[i] == ACC_ORD) && S.has_cnt[i] && res.nullable[i])
+                                       ? (st.cnt[i][s] == 0) : 0;
+    }
+}
 
 __global__ void agg_result_kernel(AggSpec S, GroupsIO st, uint64_t n, int key_width, void *out_keys,
                                   uint8_t *out_key_null, ResultPtrs res) {
-    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (uint64_t)gridDim.x * blockDim.x) {
-        if (out_keys) {
-            const uint64_t k = key_width == 16 ? 0 : st.key[g];
-            switch (key_width) {
-            case 1: ((uint8_t *)out_keys)[g] = (uint8_t)k; break;
-            case 2: ((uint16_t *)out_keys)[g] = (uint16_t)k; break;
-            case 4: ((uint32_t *)out_keys)[g] = (uint32_t)k; break;
-            case 8: ((uint64_t *)out_keys)[g] = k; break;
-            case 16: ((uint4 *)out_keys)[g] = reinterpret_cast<const uint4 *>(st.key)[g]; break;
-            default: break;
-            }
-        }
-        if (out_key_null) out_key_null[g] = st.key_null[g];
-        for (int i = 0; i < S.n_aggs; ++i) {
-            if (S.acc[i] == ACC_REF) continue; // values and NULL flags come from the value store
-            if (res.state[i] && S.acc[i] == ACC_ORD) { // min / max: the argument's width
-                // no value (a group of NULLs, or no row without key): the type's default, 0
-                const bool none = S.has_cnt[i] && st.cnt[i][g] == 0;
-                const uint64_t x = none ? 0 : ord_dec(S.kind[i], S.src_type[i], ((const uint64_t *)st.acc[i])[g]);
-                switch (val_width(S, MODE_RAW, i)) {
-                case 1: ((uint8_t *)res.state[i])[g] = (uint8_t)x; break;
-                case 2: ((uint16_t *)res.state[i])[g] = (uint16_t)x; break;
-                case 4: ((uint32_t *)res.state[i])[g] = (uint32_t)x; break;
-                default: ((uint64_t *)res.state[i])[g] = x; break;
-                }
-            } else if (res.state[i]) {
-                if (S.kind[i] != TFG_AGG_SUM) ((uint64_t *)res.state[i])[g] = st.cnt[i][g];
-                else if (S.acc[i] == ACC_I256) {
-                    ((uint4 *)res.state[i])[2 * g] = ((const uint4 *)st.acc[i])[2 * g];
-                    ((uint4 *)res.state[i])[2 * g + 1] = ((const uint4 *)st.acc[i])[2 * g + 1];
-                } else if (S.acc[i] == ACC_I128) ((uint4 *)res.state[i])[g] = ((const uint4 *)st.acc[i])[g];
-                else ((uint64_t *)res.state[i])[g] = ((const uint64_t *)st.acc[i])[g];
-            }
-            if (res.state_null[i])
-                res.state_null[i][g] = ((S.kind[i] == TFG_AGG_SUM || S.acc[i] == ACC_ORD) && S.has_cnt[i]) ? (st.cnt[i][g] == 0) : 0;
-        }
-    }
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (uint64_t)gridDim.x * blockDim.x)
+        write_result(S, st, g, g, key_width, out_keys, out_key_null, res);
+}
+
+// the result straight from a tiled consume's bucket-strided groups (pending state): workgroup b
+// writes bucket b's cnt[b] groups, found at base[b], to rows off[b].. (off = exclusive scan of cnt)
+// — the compaction into a dense state is never run for a consume -> result step
+__global__ void agg_result_buckets_kernel(AggSpec S, GroupsIO st, const uint64_t *cnt, const uint64_t *base,
+                                          const uint64_t *off, int key_width, void *out_keys, uint8_t *out_key_null,
+                                          ResultPtrs res) {
+    const int b = blockIdx.x;
+    const uint64_t s0 = base[b], d0 = off[b], c = cnt[b];
+    for (uint64_t j = threadIdx.x; j < c; j += blockDim.x)
+        write_result(S, st, s0 + j, d0 + j, key_width, out_keys, out_key_null, res);
 }
 
 __global__ void agg_state_add_kernel(AggSpec S, GroupsIO dst, GroupsIO src) { // without-key merge
@@ -796,6 +815,35 @@ struct tfg_agg {
     GroupsIO st[2];
     uint64_t *bucket_off[2] = {nullptr, nullptr};
     int cur = 0;
+    // A tiled consume (consume_fast_tiled / consume_wide_tiled) leaves its groups where the bucket
+    // kernel flushed them: bucket b's pend_cnt[b] groups at pend_base[b] of `pend` (pending).
+    // size() and result() read them in place (a consume -> result step never compacts); any other
+    // call compacts them into st[] first (pend_compact).
+    bool pending = false;
+    bool pend_known = false;   // pend_off / pend_total computed
+    uint64_t pend_total = 0;
+    void *pend_blk = nullptr;
+    size_t pend_cap = 0;
+    GroupsIO pend{};
+    uint64_t *pend_dev = nullptr; // [B] counts, [B] bases, [B + 1] offsets (exclusive scan of the counts)
+    uint64_t *pend_cnt() const { return pend_dev; }
+    uint64_t *pend_base() const { return pend_dev + B; }
+    uint64_t *pend_off() const { return pend_dev + 2 * (size_t)B; }
+    // groups capacity of the pending buffer for n more rows (allocated once, grown on demand)
+    int ensure_pend(size_t groups) {
+        if (!pend_dev) TFG_HIP(hipMalloc(&pend_dev, (3 * (size_t)B + 1) * 8));
+        if (pend_cap >= groups && pend_blk) return TFG_OK;
+        if (pend_blk) {
+            TFG_HIP(hipStreamSynchronize(ctx->stream));
+            TFG_HIP(hipFree(pend_blk));
+            pend_blk = nullptr;
+        }
+        const size_t nc = std::max<size_t>(groups + groups / 8, 4096);
+        TFG_HIP(hipMalloc(&pend_blk, carve_groups(nullptr, nc, pend) + 256));
+        pend_cap = nc;
+        carve_groups((char *)pend_blk, nc, pend);
+        return TFG_OK;
+    }
     // row-reference aggregates (ACC_REF: first_row; min / max of Decimal128 / Decimal256 / String):
     // their value stores and the collators of String min / max
     bool has_ref = false;
@@ -901,8 +949,44 @@ int fast_signature(const AggSpec &S, int mode, int key_width, const uint8_t *key
     return fast_code_supported(code) ? code : 0; // e.g. count() before sum(): the generic path
 }
 
-// The fast signatures run over a tile-sorted partition: partition -> agg_bucket_tiled_kernel ->
-// scan -> compaction (the histogram + scatter partition serves the other signatures).
+// ---- the pending state of a tiled consume (tfg_agg::pending)
+// groups per bucket -> their output offsets and the total (one host read, cached)
+int pend_counts(tfg_agg *a) {
+    if (!a->pending || a->pend_known) return TFG_OK;
+    Ctx *ctx = a->ctx;
+    void *sp;
+    if (int rc = scratch_get(ctx, scan_tmp_bytes(a->B + 1), &sp)) return rc;
+    if (int rc = exclusive_scan_u64(ctx, a->pend_cnt(), a->pend_off(), a->B, sp)) return rc;
+    if (int rc = read_back_u64(ctx, a->pend_off() + a->B, &a->pend_total, 1)) return rc;
+    a->pend_known = true;
+    return TFG_OK;
+}
+// pending groups -> the dense bucket-major state st[] (the compaction every other call expects)
+int pend_compact(tfg_agg *a) {
+    if (!a->pending) return TFG_OK;
+    if (int rc = pend_counts(a)) return rc;
+    Ctx *ctx = a->ctx;
+    const uint32_t B = a->B;
+    const int nxt = a->cur ^ 1;
+    if (int rc = a->ensure_state(nxt, a->pend_total)) return rc;
+    if (!a->bucket_off[nxt]) TFG_HIP(hipMalloc(&a->bucket_off[nxt], (B + 1) * 8));
+    {
+        ProfScope _ps(ctx, "agg.compact");
+        hipLaunchKernelGGL(agg_compact_kernel, dim3(B), dim3(256), 0, ctx->stream, a->S, a->pend,
+                           (const uint64_t *)nullptr, (const uint64_t *)nullptr, (const uint64_t *)a->pend_off(),
+                           a->st[nxt], (const uint64_t *)a->pend_base());
+    }
+    TFG_LAUNCH_CHECK();
+    TFG_HIP(hipMemcpyAsync(a->bucket_off[nxt], a->pend_off(), (B + 1) * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    a->cur = nxt;
+    a->n_groups = a->pend_total;
+    a->pending = false;
+    return TFG_OK;
+}
+
+// The fast signatures run over a tile-sorted partition: partition -> agg_bucket_tiled_kernel,
+// whose groups stay pending (result() reads them in place; other calls compact them first);
+// the histogram + scatter partition serves the other signatures.
 
 int consume_fast_tiled(tfg_agg *a, int fast, const RowPred &pred, const void *keys, const void *const *vals,
                        int64_t n, bool &done) {
@@ -933,10 +1017,7 @@ int consume_fast_tiled(tfg_agg *a, int fast, const RowPred &pred, const void *ke
     const size_t o_sp0 = cv.take<uint64_t>((size_t)n * rec_words), o_sp1 = cv.take<uint64_t>((size_t)n * rec_words);
     const size_t o_hist = cv.take<uint32_t>((size_t)B * tg.sg.T);
     const size_t o_cur = cv.take<unsigned long long>(2);
-    const size_t o_new_cnt = cv.take<uint64_t>(B), o_new_off = cv.take<uint64_t>(B + 1), o_tbase = cv.take<uint64_t>(B);
-    const size_t tmp_groups = n_old + (size_t)n;
-    const size_t o_tmpg = cv.take<uint8_t>(a->carve_groups(nullptr, tmp_groups, a->st[0]) + 256);
-    const size_t o_scan = cv.take<uint8_t>(scan_tmp_bytes(B + 1));
+    if (int rc = a->ensure_pend(n_old + (size_t)n)) return rc; // the groups stay there (pending)
     void *sp;
     if (int rc = scratch_get(ctx, cv.off, &sp)) return rc;
     char *sb = (char *)sp;
@@ -953,34 +1034,18 @@ int consume_fast_tiled(tfg_agg *a, int fast, const RowPred &pred, const void *ke
     tin.cursor = (unsigned long long *)(sb + o_cur);
     tin.xcd_remap = 1; // neighbouring runs read by one XCD: FETCH 1.95 -> 1.2 GB per C2 step (r03b)
     TFG_HIP(hipMemsetAsync(tin.cursor, 0, 16, ctx->stream));
-    GroupsIO tmp{};
-    a->carve_groups(sb + o_tmpg, tmp_groups, tmp);
-    uint64_t *new_cnt = (uint64_t *)(sb + o_new_cnt), *new_off = (uint64_t *)(sb + o_new_off);
-    uint64_t *tbase = (uint64_t *)(sb + o_tbase);
     const bool has_old = n_old > 0;
     const GroupsIO old = a->st[a->cur];
     const uint64_t *ooff = has_old ? a->bucket_off[a->cur] : (const uint64_t *)nullptr;
     {
         ProfScope _ps(ctx, "agg.bucket");
-        if (!launch_bucket_fast_tiled(fast, B, S, ctx->stream, tin, MODE_RAW, old, ooff, tmp, new_cnt, tbase))
+        if (!launch_bucket_fast_tiled(fast, B, S, ctx->stream, tin, MODE_RAW, old, ooff, a->pend, a->pend_cnt(),
+                                      a->pend_base()))
             return TFG_OK; // not reached: fast_signature returns the specialised codes only
     }
     TFG_LAUNCH_CHECK();
-    if (int rc = exclusive_scan_u64(ctx, new_cnt, new_off, B, sb + o_scan)) return rc;
-    uint64_t total = 0;
-    if (int rc = read_back_u64(ctx, new_off + B, &total, 1)) return rc;
-    const int nxt = a->cur ^ 1;
-    if (int rc = a->ensure_state(nxt, total)) return rc;
-    if (!a->bucket_off[nxt]) TFG_HIP(hipMalloc(&a->bucket_off[nxt], (B + 1) * 8));
-    {
-        ProfScope _ps(ctx, "agg.compact");
-        hipLaunchKernelGGL(agg_compact_kernel, dim3(B), dim3(256), 0, ctx->stream, S, tmp, (const uint64_t *)nullptr,
-                           (const uint64_t *)nullptr, new_off, a->st[nxt], (const uint64_t *)tbase);
-    }
-    TFG_LAUNCH_CHECK();
-    TFG_HIP(hipMemcpyAsync(a->bucket_off[nxt], new_off, (B + 1) * 8, hipMemcpyDeviceToDevice, ctx->stream));
-    a->cur = nxt;
-    a->n_groups = total;
+    a->pending = true; // groups stay bucket-strided in a->pend until a call needs them dense
+    a->pend_known = false;
     done = true;
     return TFG_OK;
 }
@@ -1023,6 +1088,7 @@ int wide_fast_signature(const AggSpec &S, const uint8_t *const *val_nulls) {
 template <typename Sel>
 int consume_wide_tiled(tfg_agg *a, int code, Sel sel, const void *const *vals, int64_t n, unsigned *err, bool &done) {
     done = false;
+    if (int rc = pend_compact(a)) return rc;
     Ctx *ctx = a->ctx;
     const AggSpec &S = a->S;
     const uint32_t B = a->B;
@@ -1059,10 +1125,7 @@ int consume_wide_tiled(tfg_agg *a, int code, Sel sel, const void *const *vals, i
     const size_t o_hist2 = cv.take<uint32_t>(two ? (size_t)RG_FINE * T2 : 0);
     const size_t o_desc = cv.take<RgDesc>(two ? (size_t)T2 : 0);
     const size_t o_cur = cv.take<unsigned long long>(2);
-    const size_t o_new_cnt = cv.take<uint64_t>(B), o_new_off = cv.take<uint64_t>(B + 1), o_tb = cv.take<uint64_t>(B);
-    const size_t tmp_groups = n_old + (size_t)n;
-    const size_t o_tmpg = cv.take<uint8_t>(a->carve_groups(nullptr, tmp_groups, a->st[0]) + 256);
-    const size_t o_scan = cv.take<uint8_t>(scan_tmp_bytes(B + 1));
+    if (int rc = a->ensure_pend(n_old + (size_t)n)) return rc; // the groups stay there (pending)
     void *sp;
     if (int rc = scratch_get(ctx, cv.off, &sp)) return rc;
     char *sb = (char *)sp;
@@ -1116,34 +1179,18 @@ int consume_wide_tiled(tfg_agg *a, int code, Sel sel, const void *const *vals, i
     tin.cursor = (unsigned long long *)(sb + o_cur);
     tin.xcd_remap = 0; // two-level wide tiles: measured slower with the remap (r03b)
     TFG_HIP(hipMemsetAsync(tin.cursor, 0, 16, ctx->stream));
-    GroupsIO tmp{};
-    a->carve_groups(sb + o_tmpg, tmp_groups, tmp);
-    uint64_t *new_cnt = (uint64_t *)(sb + o_new_cnt), *new_off = (uint64_t *)(sb + o_new_off);
-    uint64_t *tbase64 = (uint64_t *)(sb + o_tb);
     const bool has_old = n_old > 0;
     const GroupsIO old = a->st[a->cur];
     const uint64_t *ooff = has_old ? a->bucket_off[a->cur] : (const uint64_t *)nullptr;
     {
         ProfScope _ps(ctx, "agg.bucket");
-        if (!launch_bucket_wide_tiled(code, B, S, ctx->stream, tin, MODE_RAW, old, ooff, tmp, new_cnt, tbase64))
+        if (!launch_bucket_wide_tiled(code, B, S, ctx->stream, tin, MODE_RAW, old, ooff, a->pend, a->pend_cnt(),
+                                      a->pend_base()))
             return TFG_OK; // other signatures: the general path (nothing enqueued that matters)
     }
     TFG_LAUNCH_CHECK();
-    if (int rc = exclusive_scan_u64(ctx, new_cnt, new_off, B, sb + o_scan)) return rc;
-    uint64_t total = 0;
-    if (int rc = read_back_u64(ctx, new_off + B, &total, 1)) return rc;
-    const int nxt = a->cur ^ 1;
-    if (int rc = a->ensure_state(nxt, total)) return rc;
-    if (!a->bucket_off[nxt]) TFG_HIP(hipMalloc(&a->bucket_off[nxt], (B + 1) * 8));
-    {
-        ProfScope _ps(ctx, "agg.compact");
-        hipLaunchKernelGGL(agg_compact_kernel, dim3(B), dim3(256), 0, ctx->stream, S, tmp, (const uint64_t *)nullptr,
-                           (const uint64_t *)nullptr, new_off, a->st[nxt], (const uint64_t *)tbase64);
-    }
-    TFG_LAUNCH_CHECK();
-    TFG_HIP(hipMemcpyAsync(a->bucket_off[nxt], new_off, (B + 1) * 8, hipMemcpyDeviceToDevice, ctx->stream));
-    a->cur = nxt;
-    a->n_groups = total;
+    a->pending = true; // groups stay bucket-strided in a->pend until a call needs them dense
+    a->pend_known = false;
     done = true;
     return TFG_OK;
 }
@@ -1498,6 +1545,7 @@ int consume_common(tfg_agg *a, int mode, const RowPred &pred, const void *keys, 
     if (failpoint("agg_consume")) return fail(TFG_ERR_FAULT_INJECTED, "failpoint agg_consume");
     if (n == 0) return TFG_OK;
     if (int rc = set_device(a->ctx)) return rc;
+    if (int rc = pend_compact(a)) return rc; // this call folds into the dense state
     const void *vals[AGG_MAX] = {};
     const uint8_t *vnull[AGG_MAX] = {};
     RefIn rin[AGG_MAX];
@@ -1661,7 +1709,13 @@ static int serial_adopt(tfg_agg *a) {
         return rc;
     }
     AggExtract e;
-    if (a->n_groups) {
+    uint64_t held = 0;
+    if (int rc = tfg_agg_size(a, &held)) {
+        serial_dict_destroy(d);
+        tfg_agg_destroy(in);
+        return rc;
+    }
+    if (held) {
         if (int rc = agg_extract(a, e)) {
             serial_dict_destroy(d);
             tfg_agg_destroy(in);
@@ -1872,6 +1926,8 @@ int tfg_agg_destroy(tfg_agg *a) {
     }
     if (a->pack_buf) (void)hipFree(a->pack_buf);
     if (a->pack_err) (void)hipFree(a->pack_err);
+    if (a->pend_blk) (void)hipFree(a->pend_blk);
+    if (a->pend_dev) (void)hipFree(a->pend_dev);
     if (a->S.ovf) (void)hipFree(a->S.ovf);
     if (a->sdict) serial_dict_destroy(a->sdict);
     if (a->inner) tfg_agg_destroy(a->inner);
@@ -1881,6 +1937,7 @@ int tfg_agg_destroy(tfg_agg *a) {
 
 int tfg_agg_reset(tfg_agg *a) {
     TFG_CHECK(a, TFG_ERR_INVALID_ARG, "agg is null");
+    a->pending = false; // the pending groups are dropped with the rest
     if (a->sdict) {
         if (int rc = set_device(a->ctx)) return rc;
         serial_dict_reset(a->sdict);
@@ -1952,6 +2009,10 @@ int tfg_agg_merge(tfg_agg *dst, tfg_agg *src) {
                        (dst->S.src_type[i] == src->S.src_type[i] && dst->ref_coll[i] == src->ref_coll[i])),
                   TFG_ERR_LOGICAL, "merging aggregators of different signatures");
     if (int rc = set_device(dst->ctx)) return rc;
+    if (int rc = pend_compact(dst)) return rc;
+    if (int rc = set_device(src->ctx)) return rc;
+    if (int rc = pend_compact(src)) return rc;
+    if (int rc = set_device(dst->ctx)) return rc;
     TFG_HIP(hipStreamSynchronize(src->ctx->stream));
     // row-reference aggregates: the candidates are dst's store, then src's (changeFirstTime(to) /
     // changeIfLess(to) keep dst's value on ties: Aggregator::mergeDataImpl folds src into dst)
@@ -2001,7 +2062,14 @@ int tfg_agg_merge(tfg_agg *dst, tfg_agg *src) {
 
 int tfg_agg_size(tfg_agg *a, uint64_t *out_groups) {
     TFG_CHECK(a && out_groups, TFG_ERR_INVALID_ARG, "null argument");
-    *out_groups = a->sdict ? a->inner->n_groups : a->n_groups;
+    if (a->sdict) return tfg_agg_size(a->inner, out_groups);
+    if (a->pending) {
+        if (int rc = set_device(a->ctx)) return rc;
+        if (int rc = pend_counts(a)) return rc;
+        *out_groups = a->pend_total;
+        return TFG_OK;
+    }
+    *out_groups = a->n_groups;
     return TFG_OK;
 }
 
@@ -2019,16 +2087,20 @@ int tfg_agg_result(tfg_agg *a, void *out_keys, uint8_t *out_key_nullmap, void *c
     TFG_CHECK(a, TFG_ERR_INVALID_ARG, "agg is null");
     TFG_CHECK(!a->sdict, TFG_ERR_NOT_IMPLEMENTED,
               "serialized GROUP BY keys have no packed form: read them with tfg_agg_result_keys");
-    if (out_groups_host) *out_groups_host = a->n_groups;
-    if (a->n_groups > capacity) return fail(TFG_ERR_CAPACITY, "result needs %llu groups, capacity %llu",
-                                            (unsigned long long)a->n_groups, (unsigned long long)capacity);
-    if (a->n_groups == 0) return TFG_OK;
+    uint64_t G = 0;
+    if (int rc = tfg_agg_size(a, &G)) return rc;
+    if (out_groups_host) *out_groups_host = G;
+    if (G > capacity) return fail(TFG_ERR_CAPACITY, "result needs %llu groups, capacity %llu",
+                                  (unsigned long long)G, (unsigned long long)capacity);
+    if (G == 0) return TFG_OK;
     ResultPtrs rp{};
     for (int i = 0; i < a->S.n_aggs; ++i) {
         rp.state[i] = out_states ? out_states[i] : nullptr;
         rp.state_null[i] = out_state_nullmaps ? out_state_nullmaps[i] : nullptr;
+        // sum / min / max of a Nullable argument and every first_row are Nullable
+        // (AggregateFunctionNullUnary / AggregateFunctionFirstRowNull)
+        rp.nullable[i] = a->arg_nullable[i] || a->S.kind[i] == TFG_AGG_FIRST_ROW;
     }
-    const uint64_t G = a->n_groups;
     for (int i = 0; i < a->S.n_aggs; ++i) { // a String result must fit before anything is written
         if (a->S.acc[i] != ACC_REF || a->S.src_type[i] != TFG_STRING || !rp.state[i]) continue;
         const tfg_str_out *so = static_cast<const tfg_str_out *>(rp.state[i]);
@@ -2040,9 +2112,13 @@ int tfg_agg_result(tfg_agg *a, void *out_keys, uint8_t *out_key_nullmap, void *c
     }
     if (int rc = set_device(a->ctx)) return rc;
     { ProfScope _ps(a->ctx, "agg.result");
-    hipLaunchKernelGGL(agg_result_kernel, dim3(stream_grid((int64_t)a->n_groups, 256, 4096)), dim3(256), 0,
-                       a->ctx->stream, a->S, a->st[a->cur], a->n_groups, a->S.key_width,
-                       a->nokey ? nullptr : out_keys, out_key_nullmap, rp);
+    if (a->pending) // straight from the tiled consume's buckets
+        hipLaunchKernelGGL(agg_result_buckets_kernel, dim3(a->B), dim3(256), 0, a->ctx->stream, a->S, a->pend,
+                           (const uint64_t *)a->pend_cnt(), (const uint64_t *)a->pend_base(),
+                           (const uint64_t *)a->pend_off(), a->S.key_width, out_keys, out_key_nullmap, rp);
+    else
+        hipLaunchKernelGGL(agg_result_kernel, dim3(stream_grid((int64_t)G, 256, 4096)), dim3(256), 0, a->ctx->stream,
+                           a->S, a->st[a->cur], G, a->S.key_width, a->nokey ? nullptr : out_keys, out_key_nullmap, rp);
     }
     TFG_LAUNCH_CHECK();
     for (int i = 0; i < a->S.n_aggs; ++i) { // row-reference aggregates: their stores are the result
@@ -2050,7 +2126,10 @@ int tfg_agg_result(tfg_agg *a, void *out_keys, uint8_t *out_key_nullmap, void *c
         const RefStore &st = a->store[i];
         TFG_CHECK(st.n == G, TFG_ERR_LOGICAL, "value store out of step with the groups");
         hipStream_t sm = a->ctx->stream;
-        if (rp.state_null[i]) TFG_HIP(hipMemcpyAsync(rp.state_null[i], st.nul, G, hipMemcpyDeviceToDevice, sm));
+        if (rp.state_null[i]) {
+            if (rp.nullable[i]) TFG_HIP(hipMemcpyAsync(rp.state_null[i], st.nul, G, hipMemcpyDeviceToDevice, sm));
+            else TFG_HIP(hipMemsetAsync(rp.state_null[i], 0, G, sm)); // the type's default, never NULL
+        }
         if (!rp.state[i]) continue;
         if (a->S.src_type[i] == TFG_STRING) {
             const tfg_str_out *so = static_cast<const tfg_str_out *>(rp.state[i]);
@@ -2301,7 +2380,8 @@ int tfg_agg_result_keys(tfg_agg *a, void *const *out_key_cols, uint64_t *const *
         return tfg_agg_result(a, out_key_cols ? out_key_cols[0] : nullptr, out_key_nullmaps ? out_key_nullmaps[0] : nullptr,
                               out_states, out_state_nullmaps, capacity, out_groups_host);
     }
-    const uint64_t G = a->n_groups;
+    uint64_t G = 0;
+    if (int rc = tfg_agg_size(a, &G)) return rc;
     if (out_groups_host) *out_groups_host = G;
     if (out_chars_host) *out_chars_host = 0;
     if (G > capacity)

@@ -660,8 +660,9 @@ struct Table {
         }
     }
 
-    // fold group g of `grp` (state) into cell
-    __device__ __forceinline__ void add_group(int cell, const GroupsIO &grp, int64_t g) {
+    // fold group g of `grp` (state) into cell; REF: the signature may hold row-reference aggregates
+    // (the tiled fast kernels' signatures never do)
+    template <bool REF = true> __device__ __forceinline__ void add_group(int cell, const GroupsIO &grp, int64_t g) {
         for (int i = 0; i < S.n_aggs; ++i) {
             if (S.acc[i] == ACC_I256) {
                 const uint64_t *v = (const uint64_t *)grp.acc[i] + 4 * g;
@@ -675,7 +676,7 @@ struct Table {
                 atomicAdd((unsigned long long *)acc_cell(i, cell), ((const unsigned long long *)grp.acc[i])[g]);
             } else if (S.acc[i] == ACC_ORD) {
                 atomicMax((unsigned long long *)acc_cell(i, cell), ((const unsigned long long *)grp.acc[i])[g]);
-            } else if (S.acc[i] == ACC_REF) {
+            } else if (REF && S.acc[i] == ACC_REF) {
                 ref_combine(acc_cell(i, cell), ((const uint64_t *)grp.acc[i])[g], S.ref[i], S.kind[i]);
             }
             if (S.has_cnt[i]) atomicAdd((unsigned long long *)cnt_cell(i, cell), grp.cnt[i][g]);
@@ -1150,9 +1151,18 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
     __shared__ unsigned long long s_red[BT / 64];
     __shared__ unsigned long long s_base[3];
     constexpr int CH = BT; // tiles per pass-0 chunk: one per thread
+#ifdef TFG_EXP_RUNS
+    // per run of the chunk: {its end (chunk row) | narrow << 31, its tile offset minus its start}
+    __shared__ uint2 s_run[CH];
+    __shared__ uint32_t s_tot;
+#else
     __shared__ uint32_t s_ent[CH];
     __shared__ uint32_t s_pref[CH + 1];
+#endif
     __shared__ uint32_t s_wsum[BT / 64];
+    // sampled row -> run index of a chunk: s_idx[k] = the run holding row k << idx_sh
+    constexpr int IDXN = 2048;
+    __shared__ uint16_t s_idx[IDXN];
     Table T(lds, S);
     const Ops ops{S, mode};
     const int b = (tin.xcd_remap && (gridDim.x & 7) == 0)
@@ -1219,7 +1229,7 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
             } else {
                 cell = T.find_or_insert(old.key[g], old.key_null[g] != 0, true, true);
             }
-            T.add_group(cell, old, g);
+            T.template add_group<false>(cell, old, g);
         }
         old_cursor += take;
         const bool allow_insert = old_cursor >= oe;
@@ -1242,7 +1252,12 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
                 // adds of the found rows (others into the NULL-key slot, unused by these keys:
                 // a dummy), then — one uniform branch — the rare rows that need the full probe
                 // (overflow group, insert) or spill
+#ifdef TFG_EXP_NOPROBE // profiling experiment only: a hashed cell instead of the table lookup
+#pragma unroll
+                for (int u = 0; u < RT; ++u) cells[u] = (int)(((uint32_t)ku[u] * 2654435761u) % (uint32_t)S.cap);
+#else
                 T.find_home<RT>(ku, cells);
+#endif
                 int acell[RT];
                 bool slow[RT], anyslow = false;
 #pragma unroll
@@ -1251,7 +1266,9 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
                     anyslow = anyslow || slow[u];
                     acell[u] = (ok[u] && cells[u] >= 0) ? cells[u] : S.cap + 1;
                 }
+#ifndef TFG_EXP_NOATOM // profiling experiment only: no state update
                 ops.add_all(T, acell, v);
+#endif
                 if (__ballot(anyslow) == 0) return;
 #pragma unroll
                 for (int u = 0; u < RT; ++u) {
@@ -1309,7 +1326,10 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
             // takes RT rows per step whatever the run lengths
             for (int t0 = tbeg; t0 < tend; t0 += CH) {
                 const uint32_t e = t0 + (int)threadIdx.x < tend ? col[t0 + threadIdx.x] : 0u;
+#ifndef TFG_EXP_RUNS
                 s_ent[threadIdx.x] = e;
+#endif
+                uint32_t r_beg, r_end; // this thread's run in chunk rows
                 { // block-wide exclusive scan of the run lengths
                     const uint32_t c = e >> 16;
                     uint32_t x = c;
@@ -1322,36 +1342,59 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
                     __syncthreads();
                     uint32_t off = 0;
                     for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) off += s_wsum[w];
-                    s_pref[threadIdx.x] = off + x - c;
-                    if (threadIdx.x == CH - 1) s_pref[CH] = off + x;
+                    r_beg = off + x - c;
+                    r_end = off + x;
+#ifdef TFG_EXP_RUNS
+                    s_run[threadIdx.x] = make_uint2(r_end | ((e & TILE_NARROW) ? 0x80000000u : 0u),
+                                                    (uint32_t)((int)(e & 0x7FFFu) - (int)r_beg));
+                    if (threadIdx.x == CH - 1) s_tot = r_end;
+#else
+                    s_pref[threadIdx.x] = r_beg;
+                    if (threadIdx.x == CH - 1) s_pref[CH] = r_end;
+#endif
                 }
                 __syncthreads();
+#ifdef TFG_EXP_RUNS
+                const uint32_t tot = s_tot;
+#else
                 const uint32_t tot = s_pref[CH];
+#endif
+                // the tile of row i is the last run with s_pref <= i.  A sampled index (every
+                // 2^idx_sh-th row's run; 32 rows while the chunk has <= 64K rows, runs average
+                // ~30 rows on C2) starts each row's search one or two runs before its own: one
+                // LDS read plus a short forward walk instead of a binary search (~5 dependent
+                // LDS reads and ~30 VALU a row)
+                uint32_t idx_sh = 5;
+                while ((tot >> idx_sh) >= (uint32_t)IDXN) ++idx_sh; // uniform
+                for (uint32_t k = (r_beg + (1u << idx_sh) - 1) >> idx_sh; (k << idx_sh) < r_end; ++k)
+                    s_idx[k] = (uint16_t)threadIdx.x;
+                __syncthreads();
                 // software pipeline: the next step's rows are loaded (address search + global
                 // loads issued) before this step's LDS probe / atomics, so HBM latency overlaps
                 // the table work instead of following it after every step barrier
-                // the tile of row i: the last entry with s_pref <= i.  A wave's 64 rows are
-                // consecutive, so two ballots over every CS-th prefix (one read per lane) bracket
-                // the wave's tiles, and each lane searches only that bracket (4-5 dependent LDS
-                // reads instead of log2(CH) = 10)
-                constexpr uint32_t CS = CH / 64;
-                const uint32_t coarse = s_pref[(threadIdx.x & 63u) * CS];
+                // (measured: a thread taking RT consecutive rows instead — one search per RT rows —
+                // made the kernel slower, 0.41 -> 0.52 ms: each load instruction then spans 4x the
+                // lines, and the run-crossing step diverges)
                 auto load_step = [&](uint32_t base, typename Ops::Row (&v)[RT], bool (&ok)[RT]) __attribute__((always_inline)) {
 #pragma unroll
                     for (int u = 0; u < RT; ++u) {
                         const uint32_t i = base + u * BT + threadIdx.x;
-                        const uint32_t w0 = i - (threadIdx.x & 63u);
-                        const uint32_t c_lo = (uint32_t)__popcll(__ballot(coarse <= w0)) - 1u;
-                        const uint32_t c_hi = (uint32_t)__popcll(__ballot(coarse <= w0 + 63u)) - 1u;
                         ok[u] = i < tot;
                         if (!ok[u]) continue;
-                        const uint32_t lo0 = c_lo * CS, len = (c_hi - c_lo + 1u) * CS;
-                        uint32_t lo = lo0;
-                        for (uint32_t st = (1u << (32 - __clz(len - 1u))) >> 1; st > 0; st >>= 1)
-                            if (lo + st < lo0 + len && s_pref[lo + st] <= i) lo += st;
+                        uint32_t lo = s_idx[i >> idx_sh];
+#ifdef TFG_EXP_RUNS
+                        uint2 run = s_run[lo];
+                        while ((run.x & 0x7FFFFFFFu) <= i) run = s_run[++lo];
+                        const uint32_t off = run.y + i;
+                        const bool narrow = run.x >> 31;
+#else
+                        uint32_t nxt = s_pref[lo + 1];
+                        while (nxt <= i) nxt = s_pref[++lo + 1];
                         const uint32_t ent = s_ent[lo], off = (ent & 0x7FFFu) + (i - s_pref[lo]);
+                        const bool narrow = (ent & TILE_NARROW) != 0;
+#endif
                         if constexpr (Ops::NARROWABLE) {
-                            if (ent & TILE_NARROW) {
+                            if (narrow) {
                                 ops.load_narrow(tin.rec, t0 + (int)lo, tin.TR, off, v[u]);
                                 continue;
                             }

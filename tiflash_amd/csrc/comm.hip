@@ -40,117 +40,45 @@ using namespace tfg;
 
 namespace {
 
-// Batched copy: up to CP_MAX {src, dst, bytes} descriptors per launch (src null = zero fill),
-// passed by value; workgroup w copies 64 KB chunk w of the flattened descriptors, 16 bytes a lane
-// where both ends are 16-byte aligned, 8 / 1 bytes otherwise.
-constexpr int CP_MAX = 120; // the descriptor block stays under 4 KB of kernel arguments
-constexpr uint64_t CP_CHUNK = 64 * 1024;
-struct CopyDescs {
-    const uint8_t *src[CP_MAX];
-    uint8_t *dst[CP_MAX];
-    uint64_t bytes[CP_MAX];
-    uint64_t first_chunk[CP_MAX + 1]; // exclusive prefix of each descriptor's chunk count
+// String end offsets received from several ranks, each relative to its rank's chars: rows
+// [start[p], start[p+1]) get add[p] (the chars bytes of the ranks before p)
+constexpr int RB_MAX = 64;
+struct Rebase {
+    uint64_t start[RB_MAX + 1];
+    uint64_t add[RB_MAX];
     int n;
 };
-
-__global__ void __launch_bounds__(256) batched_copy_kernel(CopyDescs d) {
-    const uint64_t c = blockIdx.x;
-    int lo = 0, hi = d.n - 1; // the descriptor of chunk c: the last with first_chunk <= c
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) / 2;
-        if (d.first_chunk[mid] <= c) lo = mid;
-        else hi = mid - 1;
-    }
-    const uint64_t off = (c - d.first_chunk[lo]) * CP_CHUNK;
-    const uint64_t len = d.bytes[lo] - off < CP_CHUNK ? d.bytes[lo] - off : CP_CHUNK;
-    const uint8_t *s = d.src[lo] ? d.src[lo] + off : nullptr;
-    uint8_t *t = d.dst[lo] + off;
-    const uintptr_t al = (uintptr_t)t | (s ? (uintptr_t)s : 0);
-    if ((al & 15) == 0) {
-        for (uint64_t i = threadIdx.x * 16; i + 16 <= len; i += 256 * 16)
-            *(uint4 *)(t + i) = s ? *(const uint4 *)(s + i) : make_uint4(0, 0, 0, 0);
-        for (uint64_t i = (len & ~(uint64_t)15) + threadIdx.x; i < len; i += 256) t[i] = s ? s[i] : 0;
-    } else if ((al & 7) == 0) {
-        for (uint64_t i = threadIdx.x * 8; i + 8 <= len; i += 256 * 8)
-            *(uint64_t *)(t + i) = s ? *(const uint64_t *)(s + i) : 0ull;
-        for (uint64_t i = (len & ~(uint64_t)7) + threadIdx.x; i < len; i += 256) t[i] = s ? s[i] : 0;
-    } else {
-        for (uint64_t i = threadIdx.x; i < len; i += 256) t[i] = s ? s[i] : 0;
+__global__ void rebase_offsets_kernel(uint64_t *off, Rebase r) {
+    const uint64_t total = r.start[r.n];
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+        int p = 0;
+        while (p + 1 < r.n && r.start[p + 1] <= i) ++p;
+        off[i] += r.add[p];
     }
 }
-
-struct CopyBatch {
-    Ctx *ctx;
-    CopyDescs d{};
-    uint64_t chunks = 0;
-    int add(const void *src, void *dst, uint64_t bytes) {
-        if (!bytes) return TFG_OK;
-        if (d.n == CP_MAX)
-            if (int rc = flush()) return rc;
-        d.src[d.n] = (const uint8_t *)src;
-        d.dst[d.n] = (uint8_t *)dst;
-        d.bytes[d.n] = bytes;
-        d.first_chunk[d.n] = chunks;
-        chunks += (bytes + CP_CHUNK - 1) / CP_CHUNK;
-        ++d.n;
-        return TFG_OK;
-    }
-    int flush() {
-        if (!d.n) return TFG_OK;
-        d.first_chunk[d.n] = chunks;
-        hipLaunchKernelGGL(batched_copy_kernel, dim3((unsigned)chunks), dim3(256), 0, ctx->stream, d);
-        TFG_LAUNCH_CHECK();
-        d.n = 0;
-        chunks = 0;
-        return TFG_OK;
-    }
-};
 
 } // namespace
 
 extern "C" {
 
-int tfg_pack_planes(tfg_ctx *ctx, int nparts, int nplanes, const void *const *planes, const int *widths,
-                    const uint64_t *rows, void *out, uint64_t *out_seg_bytes) {
-    TFG_CHECK(ctx && widths && rows && out_seg_bytes && nparts >= 1 && nplanes >= 1 && (planes || nplanes == 0),
-              TFG_ERR_INVALID_ARG, "null argument");
+int tfg_string_rebase_offsets(tfg_ctx *ctx, uint64_t *offsets, int nparts, const uint64_t *row_start,
+                              const uint64_t *add) {
+    TFG_CHECK(ctx && nparts >= 1 && row_start && add && (offsets || row_start[nparts] == 0), TFG_ERR_INVALID_ARG,
+              "null argument");
     if (int rc = set_device(ctx)) return rc;
-    CopyBatch cb{ctx};
-    uint64_t o = 0;
-    for (int p = 0; p < nparts; ++p) {
-        const uint64_t s0 = o;
-        for (int j = 0; j < nplanes; ++j) {
-            TFG_CHECK(widths[j] > 0, TFG_ERR_INVALID_ARG, "plane %d width %d", j, widths[j]);
-            const uint64_t b = rows[(size_t)p * nplanes + j] * (uint64_t)widths[j];
-            TFG_CHECK(!b || out, TFG_ERR_INVALID_ARG, "null output");
-            if (int rc = cb.add(planes[(size_t)p * nplanes + j], (uint8_t *)out + o, b)) return rc;
-            o += b;
-        }
-        out_seg_bytes[p] = o - s0;
+    for (int p0 = 0; p0 < nparts; p0 += RB_MAX) {
+        Rebase r{};
+        r.n = std::min(RB_MAX, nparts - p0);
+        for (int p = 0; p <= r.n; ++p) r.start[p] = row_start[p0 + p] - row_start[p0];
+        for (int p = 0; p < r.n; ++p) r.add[p] = add[p0 + p];
+        const uint64_t rows = r.start[r.n];
+        if (!rows) continue;
+        hipLaunchKernelGGL(rebase_offsets_kernel, dim3(stream_grid((int64_t)rows, 256, 4096)), dim3(256), 0, ctx->stream,
+                           offsets + row_start[p0], r);
+        TFG_LAUNCH_CHECK();
     }
-    return cb.flush();
+    return TFG_OK;
 }
-
-int tfg_unpack_planes(tfg_ctx *ctx, int nparts, int nplanes, const int *widths, const uint64_t *rows, const void *in,
-                      void *const *planes) {
-    TFG_CHECK(ctx && widths && rows && planes && nparts >= 1 && nplanes >= 1, TFG_ERR_INVALID_ARG, "null argument");
-    if (int rc = set_device(ctx)) return rc;
-    CopyBatch cb{ctx};
-    std::vector<uint64_t> r0(nplanes, 0); // rows of plane j already placed
-    uint64_t o = 0;
-    for (int p = 0; p < nparts; ++p) {
-        for (int j = 0; j < nplanes; ++j) {
-            TFG_CHECK(widths[j] > 0, TFG_ERR_INVALID_ARG, "plane %d width %d", j, widths[j]);
-            const uint64_t r = rows[(size_t)p * nplanes + j], b = r * (uint64_t)widths[j];
-            TFG_CHECK(!b || (in && planes[j]), TFG_ERR_INVALID_ARG, "null buffer");
-            if (int rc = cb.add((const uint8_t *)in + o, (uint8_t *)planes[j] + r0[j] * widths[j], b)) return rc;
-            o += b;
-            r0[j] += r;
-        }
-    }
-    return cb.flush();
-}
-
 
 int tfg_comm_unique_id(uint8_t *out_id, size_t len) {
     TFG_CHECK(out_id && len >= sizeof(ncclUniqueId), TFG_ERR_INVALID_ARG, "id buffer must hold %zu bytes",
@@ -222,6 +150,51 @@ int tfg_alltoallv(tfg_comm *c, const void *send, const uint64_t *send_bytes, con
             TFG_NCCL(ncclRecv((char *)recv + recv_displs[p], recv_bytes[p], ncclChar, p, c->comm, ctx->stream));
     }
     TFG_NCCL(ncclGroupEnd());
+    return TFG_OK;
+}
+
+// Zero-copy exchange: one RCCL group, a send per (peer, slice) straight from the sender's column
+// and a receive per (peer, slice) straight into the receiver's column.  RCCL matches the k-th send
+// to a peer with that peer's k-th receive from this rank, so both sides list slices per peer in
+// the same order; empty slices are skipped on both sides (the counts exchange told both).
+int tfg_exchange_slices(tfg_comm *c, int nsend, const tfg_slice *send, int nrecv, const tfg_slice *recv) {
+    TFG_CHECK(c && nsend >= 0 && nrecv >= 0 && (send || !nsend) && (recv || !nrecv), TFG_ERR_INVALID_ARG,
+              "null argument");
+    Ctx *ctx = c->ctx;
+    if (int rc = set_device(ctx)) return rc;
+    for (int i = 0; i < nsend; ++i)
+        TFG_CHECK(send[i].peer >= 0 && send[i].peer < c->nranks && (send[i].ptr || !send[i].bytes), TFG_ERR_INVALID_ARG,
+                  "send slice %d: peer %d, %llu bytes", i, send[i].peer, (unsigned long long)send[i].bytes);
+    for (int i = 0; i < nrecv; ++i)
+        TFG_CHECK(recv[i].peer >= 0 && recv[i].peer < c->nranks && (recv[i].ptr || !recv[i].bytes), TFG_ERR_INVALID_ARG,
+                  "recv slice %d: peer %d, %llu bytes", i, recv[i].peer, (unsigned long long)recv[i].bytes);
+    TFG_NCCL(ncclGroupStart());
+    for (int i = 0; i < nsend; ++i)
+        if (send[i].bytes)
+            TFG_NCCL(ncclSend(send[i].ptr, send[i].bytes, ncclChar, send[i].peer, c->comm, ctx->stream));
+    for (int i = 0; i < nrecv; ++i)
+        if (recv[i].bytes) TFG_NCCL(ncclRecv(recv[i].ptr, recv[i].bytes, ncclChar, recv[i].peer, c->comm, ctx->stream));
+    TFG_NCCL(ncclGroupEnd());
+    return TFG_OK;
+}
+
+// k counts per rank pair: recv[p * k + i] = send[rank * k + i] of rank p
+int tfg_alltoall_counts_n(tfg_comm *c, int k, const uint64_t *send_host, uint64_t *recv_host) {
+    TFG_CHECK(c && k >= 1 && send_host && recv_host, TFG_ERR_INVALID_ARG, "null argument");
+    Ctx *ctx = c->ctx;
+    if (int rc = set_device(ctx)) return rc;
+    const int P = c->nranks;
+    uint64_t *dev = nullptr;
+    if (int rc = scratch_get(ctx, (size_t)2 * P * k * 8, (void **)&dev)) return rc;
+    TFG_HIP(hipMemcpyAsync(dev, send_host, (size_t)P * k * 8, hipMemcpyHostToDevice, ctx->stream));
+    TFG_NCCL(ncclGroupStart());
+    for (int p = 0; p < P; ++p) {
+        TFG_NCCL(ncclSend(dev + (size_t)p * k, (size_t)k, ncclUint64, p, c->comm, ctx->stream));
+        TFG_NCCL(ncclRecv(dev + (size_t)(P + p) * k, (size_t)k, ncclUint64, p, c->comm, ctx->stream));
+    }
+    TFG_NCCL(ncclGroupEnd());
+    TFG_HIP(hipMemcpyAsync(recv_host, dev + (size_t)P * k, (size_t)P * k * 8, hipMemcpyDeviceToHost, ctx->stream));
+    TFG_HIP(hipStreamSynchronize(ctx->stream));
     return TFG_OK;
 }
 

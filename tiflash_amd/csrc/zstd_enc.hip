@@ -9,8 +9,9 @@
 //   matcher   LZ77 over the frame, 64 positions per step (one a lane: 4-byte hash, LDS table
 //             slot read, candidates taken in order), matches extended 64 bytes per step by a
 //             ballot; literal
-//             bytes and sequences {ll, ml, offset value} to a per-frame work area (an offset
-//             equal to the previous one with literals before it is sent as repeat code 1)
+//             bytes and sequences {ll, ml, offset value} to a per-frame work area; offsets are
+//             coded against the three repeat offsets as RFC 8878 §3.1.1.5 keeps them (repeat
+//             codes 1-3, after literals or without them)
 //   literals  Huffman (histogram by LDS atomics, leaves ranked by the wave, minimum-redundancy
 //             lengths limited to 11 bits on one lane, canonical codes as HUF_buildCTable assigns
 //             them, weights FSE-compressed or in the direct 4-bit form; 4 streams, each written

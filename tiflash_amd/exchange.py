@@ -1,26 +1,22 @@
 """MPP exchange between ranks (one process per GPU) — the ExchangeSender -> ExchangeReceiver
 repartition of the reference (Flash/Mpp/HashPartitionWriter.cpp:139-204 -> MPPTunnelSet ->
-Flash/Mpp/ExchangeReceiver.cpp:626-945) as collectives over torch.distributed ("nccl" = RCCL
-over xGMI on MI355X; "gloo" on CPU for the multi-process tests).
+Flash/Mpp/ExchangeReceiver.cpp:626-945).
 
 The sender side is tfg_hash_partition (weak hash -> fillSelector -> stable scatter): its output is
-partition-major, partition p = rows [offsets[p], offsets[p+1]), which is exactly an all-to-all
-send buffer.  An exchange is fused, whatever the number of columns and of row sets ("sides",
-e.g. a join's build and probe sides, or a String column's chars next to its rows) — the same
-exchange as the C++ boundary's tfa::MPPExchange::exchange (host/operators.cpp), over the same
-ABI calls and the same wire layout:
+partition-major, partition p = rows [offsets[p], offsets[p+1]) of every column.  An exchange moves
+any number of columns and row sets ("sides", e.g. a join's build and probe sides, or a String
+column's chars next to its rows) — the same exchange as the C++ boundary's tfa::MPPExchange
+(host/operators.cpp), over the same ABI calls:
 
-* the send buffer is peer-major; peer p's segment holds every column plane's rows of p in turn
-  (side by side, planar: a column's values, not row records), packed on the device by ONE
-  tfg_pack_planes launch (the reference's packet carries a whole Block too,
-  newMPPExchangeWriter.cpp:64-95);
-* ONE counts all-to-all ([world, sides] row counts) and one host read of it, which sizes the
-  receive buffer (RCCL's send / recv take host sizes);
-* ONE all_to_all_single of the packed bytes, then ONE tfg_unpack_planes launch into the received
-  columns (source rank r's rows after rank r-1's).
+* ONE counts exchange (rows of each side per rank pair: tfg_alltoall_counts_n), one host read;
+* ONE zero-copy exchange (tfg_exchange_slices: one RCCL group over xGMI): every (peer, column)
+  slice is sent from where it lies in the partitioned column and received straight into the
+  output column at its row offset — no pack / unpack copy, no packet encode / decode.
 
-xGMI is point-to-point, so fewer, larger transfers per peer pair are what the links want.  On CPU
-tensors (gloo) the same layout is built with torch slicing.
+The RCCL communicator (tfg_comm) is made once per process group and context, its unique id
+broadcast over torch.distributed.  On CPU tensors (gloo: the multi-process tests) the same
+exchange is built with torch slicing and all_to_all_single; device tensors under gloo (a
+rehearsal of the N>1 path on one GPU) are staged through the host.
 """
 import ctypes
 from typing import List, Sequence, Tuple
@@ -49,6 +45,31 @@ def _row_bytes(c: torch.Tensor, n: int) -> torch.Tensor:
 
 
 _CTX = {}
+_COMMS = {}
+
+
+def _tfg_comm(ctx, group):
+    """The tfg_comm (RCCL communicator) of a process group on a context; collective on first use."""
+    import tiflash_amd as tfa
+    key = (id(group), ctx.h.value)
+    if key not in _COMMS:
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+        uid = (ctypes.c_uint8 * 128)()
+        if rank == 0:
+            tfa.check(tfa.lib().tfg_comm_unique_id(uid, ctypes.c_size_t(128)))
+        obj = [bytes(uid)]
+        src = dist.get_global_rank(group, 0) if group is not None else 0
+        dist.broadcast_object_list(obj, src=src, group=group)
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(obj[0])
+        h = ctypes.c_void_p()
+        tfa.check(tfa.lib().tfg_comm_init(ctx.h, ctypes.c_int(world), ctypes.c_int(rank), buf, ctypes.c_size_t(128),
+                                          ctypes.byref(h)))
+        _COMMS[key] = h
+    return _COMMS[key]
+
+
+class _Slice(ctypes.Structure):  # tfg_slice
+    _fields_ = [("peer", ctypes.c_int), ("ptr", ctypes.c_void_p), ("bytes", ctypes.c_uint64)]
 
 
 def _default_ctx(dev):
@@ -83,7 +104,7 @@ def exchange_sides(sides: Sequence[Tuple[Sequence[torch.Tensor], Sequence[int]]]
         outs = exchange_sides([([c.cpu() for c in cols], offs) for cols, offs in sides], group)
         return [[o.to(dev) for o in side] for side in outs]
     S = len(sides)
-    # the planes, in wire order: side by side, each side's columns in turn
+    # the planes, side by side, each side's columns in turn
     planes, widths, side_of, specs = [], [], [], []
     for s, (cols, offs) in enumerate(sides):
         n = int(offs[world])
@@ -94,15 +115,27 @@ def exchange_sides(sides: Sequence[Tuple[Sequence[torch.Tensor], Sequence[int]]]
             specs.append((c.dtype, tuple(c.shape[1:])))
     NP = len(planes)
     send_counts = [[int(offs[p + 1] - offs[p]) for _, offs in sides] for p in range(world)]
-    cnt = torch.tensor(send_counts, dtype=torch.int64, device=dev).reshape(-1)
-    rcnt = torch.empty_like(cnt)
-    dist.all_to_all_single(rcnt, cnt, group=group)
-    recv_counts = rcnt.reshape(world, S).tolist()
-    send_bytes = [sum(send_counts[p][side_of[k]] * widths[k] for k in range(NP)) for p in range(world)]
-    recv_bytes = [sum(recv_counts[p][side_of[k]] * widths[k] for k in range(NP)) for p in range(world)]
+    if dev.type == "cpu":
+        cnt = torch.tensor(send_counts, dtype=torch.int64).reshape(-1)
+        rcnt = torch.empty_like(cnt)
+        dist.all_to_all_single(rcnt, cnt, group=group)
+        recv_counts = rcnt.reshape(world, S).tolist()
+    else:
+        import tiflash_amd as tfa
+        ctx = ctx or _default_ctx(dev)
+        cur = torch.cuda.current_stream(dev)
+        if ctx.stream.cuda_stream != cur.cuda_stream:  # the slices move on ctx's stream
+            ctx.stream.wait_stream(cur)
+        comm = _tfg_comm(ctx, group)
+        sc = (ctypes.c_uint64 * (world * S))(*[send_counts[p][s] for p in range(world) for s in range(S)])
+        rc = (ctypes.c_uint64 * (world * S))()
+        tfa.check(tfa.lib().tfg_alltoall_counts_n(comm, ctypes.c_int(S), sc, rc))
+        recv_counts = [[int(rc[p * S + s]) for s in range(S)] for p in range(world)]
     total_rows = [sum(recv_counts[p][side_of[k]] for p in range(world)) for k in range(NP)]
     outs = [_empty_col(total_rows[k], specs[k][0], specs[k][1], dev) for k in range(NP)]
     if dev.type == "cpu":
+        send_bytes = [sum(send_counts[p][side_of[k]] * widths[k] for k in range(NP)) for p in range(world)]
+        recv_bytes = [sum(recv_counts[p][side_of[k]] * widths[k] for k in range(NP)) for p in range(world)]
         send = torch.cat([planes[k][int(sides[side_of[k]][1][p]):int(sides[side_of[k]][1][p + 1])].reshape(-1)
                           for p in range(world) for k in range(NP)] + [torch.empty(0, dtype=torch.uint8)])
         recv = torch.empty(sum(recv_bytes), dtype=torch.uint8)
@@ -116,28 +149,23 @@ def exchange_sides(sides: Sequence[Tuple[Sequence[torch.Tensor], Sequence[int]]]
                     dst[r0[k] * widths[k]:(r0[k] + r) * widths[k]] = recv[pos:pos + r * widths[k]]
                 pos += r * widths[k]
                 r0[k] += r
-    else:
-        import tiflash_amd as tfa
-        ctx = ctx or _default_ctx(dev)
-        send = torch.empty(max(sum(send_bytes), 1), dtype=torch.uint8, device=dev)
-        recv = torch.empty(max(sum(recv_bytes), 1), dtype=torch.uint8, device=dev)
-        ptrs = (ctypes.c_void_p * (world * NP))()
-        rows = (ctypes.c_uint64 * (world * NP))()
+    else:  # zero copy: every slice from its partitioned column straight into its output column
+        sends = (_Slice * max(1, world * NP))()
+        recvs = (_Slice * max(1, world * NP))()
+        r0 = [0] * NP
         for p in range(world):
             for k in range(NP):
                 o0 = int(sides[side_of[k]][1][p])
                 r = send_counts[p][side_of[k]]
-                rows[p * NP + k] = r
-                ptrs[p * NP + k] = planes[k].data_ptr() + o0 * widths[k] if r else 0
-        w_arr = (ctypes.c_int * NP)(*widths)
-        seg = (ctypes.c_uint64 * world)()
-        tfa.check(tfa.lib().tfg_pack_planes(ctx.h, ctypes.c_int(world), ctypes.c_int(NP), ptrs, w_arr, rows,
-                                            tfa._p(send), seg))
-        assert list(seg) == send_bytes
-        dist.all_to_all_single(recv[:sum(recv_bytes)], send[:sum(send_bytes)], recv_bytes, send_bytes, group=group)
-        rrows = (ctypes.c_uint64 * (world * NP))(*[recv_counts[p][side_of[k]] for p in range(world) for k in range(NP)])
-        tfa.check(tfa.lib().tfg_unpack_planes(ctx.h, ctypes.c_int(world), ctypes.c_int(NP), w_arr, rrows,
-                                              tfa._p(recv), tfa._ptr_array(outs)))
+                sends[p * NP + k] = _Slice(p, planes[k].data_ptr() + o0 * widths[k] if r else 0, r * widths[k])
+                rr = recv_counts[p][side_of[k]]
+                recvs[p * NP + k] = _Slice(p, outs[k].data_ptr() + r0[k] * widths[k] if rr else 0, rr * widths[k])
+                r0[k] += rr
+        tfa.check(tfa.lib().tfg_exchange_slices(comm, ctypes.c_int(world * NP), sends, ctypes.c_int(world * NP), recvs))
+        if ctx.stream.cuda_stream != cur.cuda_stream:  # the caller's stream sees the received columns,
+            cur.wait_stream(ctx.stream)               # and the allocator keeps both sides alive until then
+            for t in planes + outs:
+                t.record_stream(ctx.stream)
     res, k = [], 0
     for cols, _ in sides:
         res.append(outs[k:k + len(cols)])
@@ -208,18 +236,25 @@ def two_phase_merge_keys(ctx, partial, final, group=None, collators=None):
         if e.code != -4:  # NOT_IMPLEMENTED: the serialized method has no packed form
             raise
         packed = None
+    if packed is not None and any(isinstance(st, (tuple, list)) for st in packed["states"]):
+        packed = None  # String states travel as offsets + chars (below)
     if packed is not None:
-        send = tfa.gather(ctx, perm, [packed["keys"]] + list(packed["states"]))
+        ns = len(packed["states"])
+        send = tfa.gather(ctx, perm, [packed["keys"]] + list(packed["states"]) + list(packed["state_null"]))
         recv = exchange_partitions(send, offs, group, ctx)
-        final.consume_partial_packed(recv[0], recv[1:])
+        final.consume_partial_packed(recv[0], recv[1:1 + ns], state_nullmaps=recv[1 + ns:])
         return
     fixed = [k for t, k in zip(partial.key_types, cols["keys"]) if t != tfa.STRING]
     strings = [k for t, k in zip(partial.key_types, cols["keys"]) if t == tfa.STRING]
-    row_cols = fixed + list(cols["key_null"]) + list(cols["states"]) + list(cols["state_null"])
+    # String states (min / max / first_row of a String) travel like String keys: offsets + chars
+    is_str = [isinstance(st, (tuple, list)) for st in cols["states"]]
+    fstates = [st for st, x in zip(cols["states"], is_str) if not x]
+    strings += [st for st, x in zip(cols["states"], is_str) if x]
+    row_cols = fixed + list(cols["key_null"]) + fstates + list(cols["state_null"])
     rcols, rstr = exchange_string_rows(ctx, perm, offs, row_cols, strings, group)
-    nk, nkeys, ns = len(fixed), len(partial.key_types), len(cols["states"])
+    nk, nkeys, ns, nsk = len(fixed), len(partial.key_types), len(fstates), len(strings) - sum(is_str)
     rfixed, rknull = rcols[:nk], rcols[nk:nk + nkeys]
-    rstates, rsnull = rcols[nk + nkeys:nk + nkeys + ns], rcols[nk + nkeys + ns:]
+    rfstates, rsnull = rcols[nk + nkeys:nk + nkeys + ns], rcols[nk + nkeys + ns:]
     keys, fi, si = [], 0, 0
     for t in partial.key_types:
         if t == tfa.STRING:
@@ -227,5 +262,13 @@ def two_phase_merge_keys(ctx, partial, final, group=None, collators=None):
             si += 1
         else:
             keys.append(rfixed[fi])
+            fi += 1
+    rstates, fi, si = [], 0, nsk
+    for x in is_str:
+        if x:
+            rstates.append(rstr[si])
+            si += 1
+        else:
+            rstates.append(rfstates[fi])
             fi += 1
     final.consume_partial(keys, rstates, key_nullmaps=rknull, state_nullmaps=rsnull)

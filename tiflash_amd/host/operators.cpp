@@ -911,13 +911,12 @@ RcclTransport::~RcclTransport() {
     if (comm_) tfg_comm_destroy(comm_);
 }
 
-void RcclTransport::alltoallCounts(const uint64_t *send, uint64_t *recv) {
-    check(tfg_alltoall_counts(comm_, send, recv), "tfg_alltoall_counts");
+void RcclTransport::alltoallCountsN(int k, const uint64_t *send, uint64_t *recv) {
+    check(tfg_alltoall_counts_n(comm_, k, send, recv), "tfg_alltoall_counts_n");
 }
 
-void RcclTransport::alltoallv(const void *send, const uint64_t *send_bytes, const uint64_t *send_displs, void *recv,
-                              const uint64_t *recv_bytes, const uint64_t *recv_displs) {
-    check(tfg_alltoallv(comm_, send, send_bytes, send_displs, recv, recv_bytes, recv_displs), "tfg_alltoallv");
+void RcclTransport::exchangeSlices(const std::vector<tfg_slice> &send, const std::vector<tfg_slice> &recv) {
+    check(tfg_exchange_slices(comm_, (int)send.size(), send.data(), (int)recv.size(), recv.data()), "tfg_exchange_slices");
 }
 
 MPPExchange::MPPExchange(Context &ctx, int nranks, int rank, const uint8_t *unique_id, size_t id_len)
@@ -939,119 +938,113 @@ static Block emptyOfHeader(Context &ctx, const Block &header) { // zero-row colu
     return empty;
 }
 
-Block MPPExchange::exchangePackets(const std::vector<Block> &partitions) {
-    const Block header = partitions[0].cloneEmpty();
-    std::vector<DevicePacket> pk(nranks_);
-    std::vector<uint64_t> sb(nranks_), sd(nranks_), rb(nranks_), rd(nranks_);
-    uint64_t so = 0, ro = 0;
-    for (int p = 0; p < nranks_; ++p) {
-        CHBlockChunkCodecV1 codec(ctx_, header);
-        pk[p] = codec.encode(partitions[p]);
-        sb[p] = pk[p].bytes;
-        sd[p] = so;
-        so += sb[p];
-    }
-    t_->alltoallCounts(sb.data(), rb.data());
-    for (int p = 0; p < nranks_; ++p) {
-        rd[p] = ro;
-        ro += rb[p];
-    }
-    DeviceBuffer send(ctx_, std::max<uint64_t>(so, 1)), recv(ctx_, std::max<uint64_t>(ro, 1));
-    for (int p = 0; p < nranks_; ++p)
-        if (sb[p]) check(tfg_copy(ctx_.raw(), (char *)send.data() + sd[p], pk[p].buf->data(), sb[p]), "tfg_copy");
-    t_->alltoallv(send.data(), sb.data(), sd.data(), recv.data(), rb.data(), rd.data());
-    ctx_.sync();
-    std::vector<Block> got;
-    for (int p = 0; p < nranks_; ++p)
-        if (rb[p]) got.push_back(decodeBlockPacket(ctx_, header, (const uint8_t *)recv.data() + rd[p], rb[p], TFG_CODEC_V1));
-    if (!got.empty()) return concatenateBlocks(ctx_, got);
-    return emptyOfHeader(ctx_, header);
-}
-
+// Zero-copy exchange.  Planes per column: a fixed-width column's values; a String column's end
+// offsets (8 bytes a row, relative to its partition's chars, rebased on arrival) and its chars
+// (bytes); a Nullable column's null map.  One counts exchange carries, per rank pair, the rows,
+// every String column's chars bytes and every null plane's rows (0 when that partition has no
+// null map: the receiver's null plane is zeroed first); then every (peer, plane) slice is sent
+// from the partition block where it lies and received into the output column at its offset.
 Block MPPExchange::exchange(const std::vector<Block> &partitions) {
     if ((int)partitions.size() != nranks_)
         throw Exception("exchange needs one block per rank", ErrorCodes::BAD_ARGUMENTS);
     const Block &proto = partitions[0];
-    for (const auto &c : proto.getColumnsWithTypeAndName())
-        if (c.type.isString()) return exchangePackets(partitions);
     const size_t ncols = proto.columns();
-    // the planes, decided by the schema every rank shares: each column's values, then its null
-    // map when the type is Nullable (a partition whose column carries none sends zeros)
-    std::vector<int> widths, plane_col;
+    for (const Block &b : partitions)
+        if (b.columns() != ncols) throw Exception("partitions of different schemas", ErrorCodes::LOGICAL_ERROR);
+    // counts per rank pair: [0] rows, then one per String column (chars), then one per Nullable
+    // column (null map rows, 0 = none)
+    std::vector<int> str_of(ncols, -1), nul_of(ncols, -1);
+    int K = 1;
+    for (size_t j = 0; j < ncols; ++j)
+        if (proto.safeGetByPosition(j).type.isString()) str_of[j] = K++;
+    for (size_t j = 0; j < ncols; ++j)
+        if (proto.safeGetByPosition(j).type.nullable) nul_of[j] = K++;
+    const int P = nranks_;
+    std::vector<ColumnPtr> cols((size_t)P * ncols);
+    std::vector<uint64_t> send_cnt((size_t)P * K, 0), recv_cnt((size_t)P * K, 0);
+    for (int p = 0; p < P; ++p) {
+        const Block &b = partitions[p];
+        send_cnt[(size_t)p * K] = b.rows();
+        for (size_t j = 0; j < ncols; ++j) {
+            ColumnPtr c = materialize(ctx_, b.safeGetByPosition(j).column);
+            const DataType &t = proto.safeGetByPosition(j).type;
+            if (c->type.isString() != t.isString() || c->rows != b.rows())
+                throw Exception("partitions of different schemas", ErrorCodes::LOGICAL_ERROR);
+            if (c->nullmap && !t.nullable) // it would be dropped
+                throw Exception("null map on a column of non-Nullable type", ErrorCodes::LOGICAL_ERROR);
+            if (str_of[j] >= 0) send_cnt[(size_t)p * K + str_of[j]] = c->chars;
+            if (nul_of[j] >= 0) send_cnt[(size_t)p * K + nul_of[j]] = c->nullmap ? c->rows : 0;
+            cols[(size_t)p * ncols + j] = c;
+        }
+    }
+    t_->alltoallCountsN(K, send_cnt.data(), recv_cnt.data());
+    // where each source's rows / chars land
+    std::vector<uint64_t> row0(P + 1, 0);
+    for (int p = 0; p < P; ++p) row0[p + 1] = row0[p] + recv_cnt[(size_t)p * K];
+    const uint64_t total = row0[P];
+    std::vector<std::vector<uint64_t>> chars0(K); // per String counter: the bytes before source p
+    for (size_t j = 0; j < ncols; ++j)
+        if (str_of[j] >= 0) {
+            auto &c0 = chars0[str_of[j]];
+            c0.assign(P + 1, 0);
+            for (int p = 0; p < P; ++p) c0[p + 1] = c0[p] + recv_cnt[(size_t)p * K + str_of[j]];
+        }
+    Block out;
+    std::vector<std::shared_ptr<IColumn>> outc(ncols);
     for (size_t j = 0; j < ncols; ++j) {
         const DataType t = proto.safeGetByPosition(j).type;
-        widths.push_back((int)t.width());
-        plane_col.push_back((int)j);
-        if (t.nullable) {
-            widths.push_back(1);
-            plane_col.push_back(-(int)j - 1);
+        auto c = std::make_shared<IColumn>();
+        c->type = t;
+        c->rows = total;
+        if (t.isString()) {
+            c->chars = chars0[str_of[j]][P];
+            c->data = std::make_shared<DeviceBuffer>(ctx_, std::max<uint64_t>(c->chars, 1));
+            c->offsets = std::make_shared<DeviceBuffer>(ctx_, std::max<uint64_t>(total, 1) * 8);
+        } else {
+            c->data = std::make_shared<DeviceBuffer>(ctx_, std::max<uint64_t>(total * t.width(), 1));
         }
-    }
-    const int np = (int)widths.size();
-    std::vector<uint64_t> send_rows(nranks_), recv_rows(nranks_);
-    std::vector<ColumnPtr> hold;
-    std::vector<const void *> planes((size_t)nranks_ * np, nullptr);
-    for (int p = 0; p < nranks_; ++p) {
-        const Block &b = partitions[p];
-        if (b.columns() != ncols) throw Exception("partitions of different schemas", ErrorCodes::LOGICAL_ERROR);
-        send_rows[p] = b.rows();
-        for (int k = 0; k < np; ++k) {
-            const int j = plane_col[k] >= 0 ? plane_col[k] : -plane_col[k] - 1;
-            ColumnPtr c = materialize(ctx_, b.safeGetByPosition(j).column);
-            hold.push_back(c);
-            if (plane_col[k] >= 0) {
-                planes[(size_t)p * np + k] = c->dataPtr();
-            } else {
-                if (c->nullmap && !proto.safeGetByPosition(j).type.nullable)
-                    throw Exception("null map on a column of non-Nullable type", ErrorCodes::LOGICAL_ERROR);
-                planes[(size_t)p * np + k] = c->nullPtr(); // null: a zero plane
+        if (t.nullable) {
+            c->nullmap = std::make_shared<DeviceBuffer>(ctx_, std::max<uint64_t>(total, 1));
+            bool partial = false; // a source without a null map leaves its rows zero (not NULL)
+            for (int p = 0; p < P; ++p) partial |= recv_cnt[(size_t)p * K + nul_of[j]] != recv_cnt[(size_t)p * K];
+            if (partial && total) {
+                const std::vector<uint8_t> zero(total, 0);
+                check(tfg_upload(ctx_.raw(), c->nullmap->data(), zero.data(), total), "tfg_upload");
             }
         }
+        outc[j] = c;
     }
-    t_->alltoallCounts(send_rows.data(), recv_rows.data());
-    std::vector<uint64_t> send_pr((size_t)nranks_ * np), recv_pr((size_t)nranks_ * np); // rows per plane
-    for (int p = 0; p < nranks_; ++p)
-        for (int k = 0; k < np; ++k) {
-            send_pr[(size_t)p * np + k] = send_rows[p];
-            recv_pr[(size_t)p * np + k] = recv_rows[p];
+    // the slices, peer by peer, in one plane order on both sides
+    std::vector<tfg_slice> sends, recvs;
+    for (int p = 0; p < P; ++p)
+        for (size_t j = 0; j < ncols; ++j) {
+            const IColumn &c = *cols[(size_t)p * ncols + j];
+            const DataType &t = proto.safeGetByPosition(j).type;
+            IColumn &o = *outc[j];
+            const uint64_t r = recv_cnt[(size_t)p * K];
+            if (t.isString()) {
+                sends.push_back({p, c.offsets ? c.offsets->data() : nullptr, c.rows * 8});
+                recvs.push_back({p, (uint64_t *)o.offsets->data() + row0[p], r * 8});
+                sends.push_back({p, c.data ? c.data->data() : nullptr, c.chars});
+                recvs.push_back({p, (uint8_t *)o.data->data() + chars0[str_of[j]][p],
+                                 recv_cnt[(size_t)p * K + str_of[j]]});
+            } else {
+                sends.push_back({p, c.data ? c.data->data() : nullptr, c.rows * t.width()});
+                recvs.push_back({p, (uint8_t *)o.data->data() + row0[p] * t.width(), r * t.width()});
+            }
+            if (t.nullable) {
+                sends.push_back({p, c.nullmap ? c.nullmap->data() : nullptr, c.nullmap ? c.rows : 0});
+                recvs.push_back({p, (uint8_t *)o.nullmap->data() + row0[p], recv_cnt[(size_t)p * K + nul_of[j]]});
+            }
         }
-    uint64_t row_bytes = 0, total_send = 0, total_recv = 0;
-    for (int w : widths) row_bytes += (uint64_t)w;
-    for (int p = 0; p < nranks_; ++p) {
-        total_send += send_rows[p];
-        total_recv += recv_rows[p];
-    }
-    DeviceBuffer send(ctx_, std::max<uint64_t>(total_send * row_bytes, 1));
-    auto recv = std::make_shared<DeviceBuffer>(ctx_, std::max<uint64_t>(total_recv * row_bytes, 1));
-    std::vector<uint64_t> sb(nranks_), sd(nranks_), rb(nranks_), rd(nranks_);
-    check(tfg_pack_planes(ctx_.raw(), nranks_, np, planes.data(), widths.data(), send_pr.data(), send.data(), sb.data()),
-          "tfg_pack_planes");
-    for (int p = 0; p < nranks_; ++p) {
-        sd[p] = p ? sd[p - 1] + sb[p - 1] : 0;
-        rb[p] = recv_rows[p] * row_bytes;
-        rd[p] = p ? rd[p - 1] + rb[p - 1] : 0;
-    }
-    t_->alltoallv(send.data(), sb.data(), sd.data(), recv->data(), rb.data(), rd.data());
-    // the received planes: every source's rows concatenated in rank order
-    Block out;
-    std::vector<std::shared_ptr<IColumn>> cols(ncols);
-    std::vector<void *> outp(np);
-    for (int k = 0; k < np; ++k) {
-        const int j = plane_col[k] >= 0 ? plane_col[k] : -plane_col[k] - 1;
-        if (!cols[j]) {
-            cols[j] = std::make_shared<IColumn>();
-            cols[j]->type = proto.safeGetByPosition(j).type;
-            cols[j]->rows = total_recv;
-        }
-        auto buf = std::make_shared<DeviceBuffer>(ctx_, std::max<uint64_t>(total_recv * widths[k], 1));
-        if (plane_col[k] >= 0) cols[j]->data = buf;
-        else cols[j]->nullmap = buf;
-        outp[k] = buf->data();
-    }
-    check(tfg_unpack_planes(ctx_.raw(), nranks_, np, widths.data(), recv_pr.data(), recv->data(), outp.data()),
-          "tfg_unpack_planes");
-    ctx_.sync(); // the send / recv buffers are released on return
-    for (size_t j = 0; j < ncols; ++j) out.insert({cols[j], cols[j]->type, proto.safeGetByPosition(j).name});
+    t_->exchangeSlices(sends, recvs);
+    for (size_t j = 0; j < ncols; ++j) // String end offsets: each source's relative to its own chars
+        if (str_of[j] >= 0 && total)
+            check(tfg_string_rebase_offsets(ctx_.raw(), (uint64_t *)outc[j]->offsets->data(), P, row0.data(),
+                                            chars0[str_of[j]].data()),
+                  "tfg_string_rebase_offsets");
+    ctx_.sync(); // the partitions may be released on return
+    for (size_t j = 0; j < ncols; ++j) out.insert({outc[j], outc[j]->type, proto.safeGetByPosition(j).name});
     return out;
 }
 

@@ -568,7 +568,7 @@ void MPPTunnelSet::write(uint32_t part, Block &&block, uint32_t stream) {
     if (exchange_ && stream != 0) // the RCCL all-to-all moves one block per rank, without stream ids
         throw Exception("fine-grained shuffle over the RCCL exchange", ErrorCodes::NOT_IMPLEMENTED);
     if (!exchange_ && part != local_partition_) {
-        if (remote_) remote_(part, std::move(block));
+        if (remote_) remote_(part, std::move(block), stream);
         return;
     }
     parts_[part].push_back(std::move(block));

@@ -393,10 +393,12 @@ using ExchangeReceiverPtr = std::shared_ptr<ExchangeReceiver>;
 // are collected; when the last sender finishes, the partitions go out — through an MPPExchange
 // (RCCL all-to-all; partition p to rank p) into `receiver`, or, without one, partition
 // `local_partition` straight into `receiver` and the others to `remote` (the tunnels to other
-// nodes, e.g. a test's capture).
+// nodes, e.g. a test's capture) with their fine-grained stream ids, so the remote receiver routes
+// each block to the stream that aggregates its keys (MPPTunnelSetWriter.cpp:365-400 carries the
+// stream id in the packet's chunks).
 class MPPTunnelSet {
 public:
-    using RemoteSink = std::function<void(uint32_t, Block &&)>;
+    using RemoteSink = std::function<void(uint32_t part, Block &&, uint32_t stream)>;
     MPPTunnelSet(Context &ctx, uint32_t partition_num, size_t sender_concurrency, ExchangeReceiverPtr receiver,
                  MPPExchange *exchange = nullptr, uint32_t local_partition = 0, RemoteSink remote = nullptr);
     void write(uint32_t part, Block &&block, uint32_t stream = 0); // stream: fine-grained stream id

@@ -474,20 +474,19 @@ std::vector<Block> hashPartitionBlock(Context &ctx, const Block &block, const st
                                       uint32_t partition_num, const std::vector<int> &collators = {});
 
 // The collective under an MPP exchange between the ranks of one query (what MPPTunnelSet's
-// tunnels carry between tasks): a counts exchange, then one byte all-to-all of device buffers.
-// RcclTransport is the product's (tfg_comm: RCCL over xGMI, one process per GPU); tests plug in
-// other transports (tests/cpp/test_host.cpp runs two processes over TCP).
+// tunnels carry between tasks): a counts exchange, then the zero-copy exchange of device slices
+// (tfg_exchange_slices).  RcclTransport is the product's (tfg_comm: RCCL over xGMI, one process
+// per GPU); tests plug in other transports (tests/cpp/test_host.cpp runs two processes over TCP).
 class ExchangeTransport {
 public:
     virtual ~ExchangeTransport() = default;
     virtual int nranks() const = 0;
     virtual int rank() const = 0;
-    // recv[p] = send[this rank] of rank p (host arrays of nranks entries)
-    virtual void alltoallCounts(const uint64_t *send, uint64_t *recv) = 0;
-    // device buffers, host byte counts / displacements: slice p of send goes to rank p, rank p's
-    // slice lands at recv + recv_displs[p]
-    virtual void alltoallv(const void *send, const uint64_t *send_bytes, const uint64_t *send_displs, void *recv,
-                           const uint64_t *recv_bytes, const uint64_t *recv_displs) = 0;
+    // k counts per rank pair: recv[p * k + i] = send[this rank * k + i] of rank p (host arrays)
+    virtual void alltoallCountsN(int k, const uint64_t *send, uint64_t *recv) = 0;
+    // every send slice to its peer, every receive slice from its peer (device memory in place);
+    // a peer's k-th send matches that peer's k-th receive from this rank
+    virtual void exchangeSlices(const std::vector<tfg_slice> &send, const std::vector<tfg_slice> &recv) = 0;
 };
 
 class RcclTransport : public ExchangeTransport {
@@ -496,9 +495,8 @@ public:
     ~RcclTransport() override;
     int nranks() const override { return nranks_; }
     int rank() const override { return rank_; }
-    void alltoallCounts(const uint64_t *send, uint64_t *recv) override;
-    void alltoallv(const void *send, const uint64_t *send_bytes, const uint64_t *send_displs, void *recv,
-                   const uint64_t *recv_bytes, const uint64_t *recv_displs) override;
+    void alltoallCountsN(int k, const uint64_t *send, uint64_t *recv) override;
+    void exchangeSlices(const std::vector<tfg_slice> &send, const std::vector<tfg_slice> &recv) override;
 
 private:
     tfg_comm *comm_ = nullptr;
@@ -506,12 +504,12 @@ private:
 };
 
 // One-node exchange: every rank contributes partition_num == nranks blocks and receives the
-// concatenation of its partition from every rank (ExchangeReceiver output).  Fused: one counts
-// exchange and ONE data all-to-all per call, whatever the number of columns — every column's value
-// plane and null plane of every destination packed peer-major on the device (tfg_pack_planes,
-// Nullable columns without a null map send a zero plane written on the device) and unpacked on
-// arrival (tfg_unpack_planes); no host sync besides the counts.  Blocks with String columns travel
-// as CHBlockChunkCodecV1 packets through the same single all-to-all.
+// concatenation of its partition from every rank (ExchangeReceiver output).  Zero copy: one counts
+// exchange, then every column plane's slice goes from the partition block where it lies to the
+// output column at its row offset (tfg_exchange_slices: one RCCL group per call, no pack / unpack,
+// no packet encode / decode).  String columns travel as their end offsets (rebased on arrival,
+// tfg_string_rebase_offsets) and chars; a Nullable column's null map as a plane of its own (a
+// partition without one sends nothing and its rows stay zero).
 class MPPExchange {
 public:
     MPPExchange(Context &ctx, int nranks, int rank, const uint8_t *unique_id, size_t id_len); // over RCCL
@@ -524,9 +522,6 @@ private:
     Context &ctx_;
     std::shared_ptr<ExchangeTransport> t_;
     int nranks_, rank_;
-    // blocks with String columns travel as CHBlockChunkCodecV1 packets (ExchangeSender ->
-    // ExchangeReceiver): encoded on the device, packet bytes all-to-all, decoded on arrival
-    Block exchangePackets(const std::vector<Block> &partitions);
 };
 
 // ---------------------------------------------------------------- auto pass-through (f4)
