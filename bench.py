@@ -41,6 +41,8 @@ def parse():
     ap.add_argument("--join-build", type=int, default=10_000_000)
     ap.add_argument("--join-probe", type=int, default=100_000_000)
     ap.add_argument("--no-join", action="store_true")
+    ap.add_argument("--join-v2", action="store_true",
+                    help="also time the C3 probe through JoinV2's pointer table (off by default: DESIGN §5)")
     ap.add_argument("--no-variants", action="store_true", help="skip the selectivity sweep / Int64-value legs")
     ap.add_argument("--c5-rows", type=int, default=100_000_000, help="C5 String-key GROUP BY rows per GPU (0 = skip)")
     ap.add_argument("--c5-groups", type=int, default=10_000_000)
@@ -847,8 +849,10 @@ def main():
                                   "frac": round(alg / (jms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
             "kernels_ms_per_step": {kname: round(vv[0] / args.steps, 4) for kname, vv in sorted(jprof.items())},
         }
-        # the same probe through JoinV2's tagged pointer table (no probe-side partitioning)
+        # the same probe through JoinV2's tagged pointer table (no probe-side partitioning): a parity
+        # path, not a timed leg by default (latency-bound random walks, 8x v1)
         del j
+    if world == 1 and not args.no_join and args.join_v2:
         j = tfa.Join(ctx, tfa.INT64, expected_build_rows=nb, v2=True, tagged=True)
         tb0 = time.perf_counter()
         j.build(bk, payload=[bpay])

@@ -17,6 +17,8 @@
 #include <sstream>
 
 #include <arpa/inet.h>
+#include <csignal>
+#include <execinfo.h>
 #include <netinet/in.h>
 #include <sys/socket.h>
 #include <unistd.h>
@@ -2808,7 +2810,23 @@ static int runExchangeRank(Context &ctx, int rank, int port) {
     return bad ? 1 : 0;
 }
 
+// a crash names its test and where it happened (stdout into a pipe is lost with the process)
+static void onFatalSignal(int sig) {
+    const char *head = "  FATAL signal in ";
+    (void)!write(2, head, strlen(head));
+    (void)!write(2, g_current.data(), g_current.size());
+    (void)!write(2, "\n", 1);
+    void *frames[64];
+    backtrace_symbols_fd(frames, backtrace(frames, 64), 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+
 int main(int argc, char **argv) {
+    setvbuf(stdout, nullptr, _IOLBF, 0);
+    signal(SIGSEGV, onFatalSignal);
+    signal(SIGABRT, onFatalSignal);
+    signal(SIGBUS, onFatalSignal);
     g_root = argc > 1 ? argv[1] : ".";
     const char *filter = argc > 2 ? argv[2] : nullptr;
     std::unique_ptr<Context> owned;

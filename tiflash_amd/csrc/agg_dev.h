@@ -4,6 +4,7 @@
 // which hipcc builds in parallel.
 #pragma once
 #include <algorithm>
+#include <type_traits>
 #include <vector>
 
 #include "common.h"
@@ -485,6 +486,41 @@ struct Table {
         }
     }
 
+    // Home-group lookup of R wide keys, branch-free (the wide twin of find_home): the group's four
+    // tags in one 32-byte read, the first published tag equal to the key's (tag | 1), then that
+    // cell's 16-byte key; cell[u] = the cell when the keys are equal, else -1 (not published yet,
+    // a tag collision, an overflow group, a new key: the caller's slow path, find_wide_multi)
+    template <int R>
+    __device__ __forceinline__ void find_wide_home(const uint64_t (&lo)[R], const uint64_t (&hi)[R],
+                                                   const uint64_t (&tag)[R], int (&cell)[R]) const {
+        const uint4 *wk = reinterpret_cast<const uint4 *>(base + S.wkey_off);
+        unsigned grp[R];
+        int s_hit[R];
+#pragma unroll
+        for (int u = 0; u < R; ++u) grp[u] = slot_group(tag[u]);
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            const uint4 a = *reinterpret_cast<const uint4 *>(&keys[grp[u] * GS]);
+            const uint4 b = *reinterpret_cast<const uint4 *>(&keys[grp[u] * GS + 2]);
+            const uint64_t k[GS] = {((uint64_t)a.y << 32) | a.x, ((uint64_t)a.w << 32) | a.z,
+                                    ((uint64_t)b.y << 32) | b.x, ((uint64_t)b.w << 32) | b.z};
+            int c = -1;
+#pragma unroll
+            for (int s = GS - 1; s >= 0; --s) c = k[s] == (tag[u] | 1ull) ? s : c;
+            s_hit[u] = c;
+        }
+        // a published tag was stored after its key (release): read the key after the tag
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            cell[u] = -1;
+            if (s_hit[u] < 0) continue;
+            const int c = (int)(grp[u] * GS) + s_hit[u];
+            const uint4 q = wk[c];
+            if ((((uint64_t)q.y << 32) | q.x) == lo[u] && (((uint64_t)q.w << 32) | q.z) == hi[u]) cell[u] = c;
+        }
+    }
+
     // Wide keys (keys128 / packed String keys).  A cell is claimed by a 64-bit CAS of the key's
     // tag into keys[cell]; the claimant then writes the 16-byte key to wkeys[cell] and
     // republishes the tag with bit 0 set.  A reader whose tag equals a cell's unpublished tag
@@ -839,18 +875,23 @@ template <int NA, bool W = false> struct GenericOps {
 template <int A0, int A1, int A2, bool CHECK, int R, typename Row>
 __device__ __forceinline__ void fast_add_rows(Table &T, const int (&cell)[R], const Row (&v)[R]) {
     constexpr int ops[3] = {A0, A1, A2};
+    // the op codes fix the accumulator widths (op 4: a two-word Int128 sum, else one word), so
+    // a cell's address needs no per-row look at S.acc (T.acc_cell)
+    auto acc = [&](int i, int c) __attribute__((always_inline)) {
+        return reinterpret_cast<uint64_t *>(T.base + T.S.acc_off[i]) + c * (ops[i] == 4 ? 2 : 1);
+    };
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         if (ops[i] != 4) continue;
         uint64_t old[R];
 #pragma unroll
         for (int u = 0; u < R; ++u)
-            if (!CHECK || cell[u] >= 0) old[u] = atomicAdd((unsigned long long *)T.acc_cell(i, cell[u]), (unsigned long long)v[u].v[i]);
+            if (!CHECK || cell[u] >= 0) old[u] = atomicAdd((unsigned long long *)acc(i, cell[u]), (unsigned long long)v[u].v[i]);
 #pragma unroll
         for (int u = 0; u < R; ++u) {
             if (CHECK && cell[u] < 0) continue;
             const uint64_t lo = v[u].v[i], carry = (old[u] + lo) < old[u] ? 1ull : 0ull;
-            atomicAdd((unsigned long long *)T.acc_cell(i, cell[u]) + 1,
+            atomicAdd((unsigned long long *)acc(i, cell[u]) + 1,
                       (unsigned long long)(((int64_t)lo < 0 ? ~0ull : 0ull) + carry));
         }
     }
@@ -860,8 +901,8 @@ __device__ __forceinline__ void fast_add_rows(Table &T, const int (&cell)[R], co
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
             if (ops[i] == 1) atomicAdd((unsigned long long *)T.cnt_cell(i, cell[u]), 1ull);
-            if (ops[i] == 2) atomicAdd((unsigned long long *)T.acc_cell(i, cell[u]), (unsigned long long)v[u].v[i]);
-            if (ops[i] == 3) atomicAdd((double *)T.acc_cell(i, cell[u]), __longlong_as_double((long long)v[u].v[i]));
+            if (ops[i] == 2) atomicAdd((unsigned long long *)acc(i, cell[u]), (unsigned long long)v[u].v[i]);
+            if (ops[i] == 3) atomicAdd((double *)acc(i, cell[u]), __longlong_as_double((long long)v[u].v[i]));
         }
     }
 }
@@ -896,8 +937,8 @@ template <int A0, int A1, int A2> struct FastOps {
         }
     }
     // row `off` of narrow tile `tile` (slot of TRS rows: TRS u32 keys, then TRS u64 values)
-    __device__ __forceinline__ void load_narrow(const uint64_t *rec, int64_t tile, int TRS, uint32_t off, Row &v) const {
-        const uint32_t *ks = reinterpret_cast<const uint32_t *>(rec + tile * (int64_t)TRS * 2);
+    __device__ __forceinline__ void load_narrow(const uint64_t *rec, uint64_t slot, int TRS, uint32_t off, Row &v) const {
+        const uint32_t *ks = reinterpret_cast<const uint32_t *>(rec + slot * 2);
         v.key = ks[off];
         const uint64_t w = reinterpret_cast<const uint64_t *>(ks + TRS)[off];
 #pragma unroll
@@ -962,6 +1003,7 @@ template <int NA, bool W = false> struct WideOps {
 // Wide keys on the tiled path: records {key lo, key hi, one word per summed argument}; the
 // value ops are FastOps' (1 count, 2 Int64 / UInt64 sum, 3 Float64 sum, 4 Decimal64 -> Decimal128)
 template <int A0, int A1, int A2> struct WideFastOps {
+    static constexpr bool HOME_FAST = true; // find_wide_home + add_all before the full probe
     static constexpr int op(int i) { return i == 0 ? A0 : (i == 1 ? A1 : A2); }
     static constexpr int NCOL = 2 + (A0 >= 2) + (A1 >= 2) + (A2 >= 2);
     static constexpr bool WIDE = true;
@@ -971,7 +1013,7 @@ template <int A0, int A1, int A2> struct WideFastOps {
         uint64_t key, khi;
         uint64_t v[3];
     };
-    __device__ __forceinline__ void load_narrow(const uint64_t *, int64_t, int, uint32_t, Row &) const {}
+    __device__ __forceinline__ void load_narrow(const uint64_t *, uint64_t, int, uint32_t, Row &) const {}
     const AggSpec &S;
     int mode;
     __device__ __forceinline__ void load(const RowsIO &rows, int64_t r, Row &v) const {
@@ -993,6 +1035,10 @@ template <int A0, int A1, int A2> struct WideFastOps {
     template <int R>
     __device__ __forceinline__ void add_multi(Table &T, const int (&cell)[R], const Row (&v)[R]) const {
         fast_add_rows<A0, A1, A2, true>(T, cell, v);
+    }
+    template <int R>
+    __device__ __forceinline__ void add_all(Table &T, const int (&cell)[R], const Row (&v)[R]) const {
+        fast_add_rows<A0, A1, A2, false>(T, cell, v);
     }
     __device__ __forceinline__ void store(const RowsIO &sp, int64_t w, const Row &v) const {
         uint64_t *rec = (uint64_t *)sp.key + w * NCOL;
@@ -1142,6 +1188,12 @@ struct TiledIn {
     unsigned long long *cursor; // [0] spill rows, [1] temp groups
 };
 
+// Ops with the wide home-group fast path (WideFastOps::HOME_FAST)
+template <typename Ops, typename = void> struct wide_home_fast { static constexpr bool value = false; };
+template <typename Ops> struct wide_home_fast<Ops, std::void_t<decltype(Ops::HOME_FAST)>> {
+    static constexpr bool value = Ops::HOME_FAST;
+};
+
 template <typename Ops, int BT>
 __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn tin, int mode, GroupsIO old,
                                                               const uint64_t *old_off, GroupsIO out, uint64_t *out_cnt,
@@ -1151,14 +1203,9 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
     __shared__ unsigned long long s_red[BT / 64];
     __shared__ unsigned long long s_base[3];
     constexpr int CH = BT; // tiles per pass-0 chunk: one per thread
-#ifdef TFG_EXP_RUNS
     // per run of the chunk: {its end (chunk row) | narrow << 31, its tile offset minus its start}
     __shared__ uint2 s_run[CH];
     __shared__ uint32_t s_tot;
-#else
-    __shared__ uint32_t s_ent[CH];
-    __shared__ uint32_t s_pref[CH + 1];
-#endif
     __shared__ uint32_t s_wsum[BT / 64];
     // sampled row -> run index of a chunk: s_idx[k] = the run holding row k << idx_sh
     constexpr int IDXN = 2048;
@@ -1284,13 +1331,31 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
                 }
                 return;
             }
-            if constexpr (Ops::WIDE) T.find_wide_multi<RT>(ku, kh, tg, ok, allow_insert, cells);
-            else T.find_or_insert_multi<RT>(ku, nu, ok, allow_insert, cells);
+            bool want[RT]; // rows that still need the full probe
+#pragma unroll
+            for (int u = 0; u < RT; ++u) want[u] = ok[u];
+            if constexpr (Ops::WIDE && wide_home_fast<Ops>::value) {
+                // the wide fast path: home-group lookups, the adds of the found rows (others into
+                // the unused NULL-key slot: a dummy), then only the rest through the full probe
+                int home[RT], acell[RT];
+                bool anyslow = false;
+                T.find_wide_home<RT>(ku, kh, tg, home);
+#pragma unroll
+                for (int u = 0; u < RT; ++u) {
+                    want[u] = ok[u] && home[u] < 0;
+                    anyslow = anyslow || want[u];
+                    acell[u] = (ok[u] && home[u] >= 0) ? home[u] : S.cap + 1;
+                }
+                ops.add_all(T, acell, v);
+                if (__ballot(anyslow) == 0) return;
+            }
+            if constexpr (Ops::WIDE) T.find_wide_multi<RT>(ku, kh, tg, want, allow_insert, cells);
+            else T.find_or_insert_multi<RT>(ku, nu, want, allow_insert, cells);
             int hit[RT];
 #pragma unroll
             for (int u = 0; u < RT; ++u) {
-                miss[u] = ok[u] && cells[u] < 0;
-                hit[u] = ok[u] ? cells[u] : -1;
+                miss[u] = want[u] && cells[u] < 0;
+                hit[u] = want[u] ? cells[u] : -1;
             }
             ops.add_multi(T, hit, v);
             // no barrier per step: a missing row (full table / inserts closed) looks its key up
@@ -1321,14 +1386,13 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
         if (pass == 0 && no_rows) {
             // only the bucket's older groups (seeded above) pass through
         } else if (pass == 0) {
-            // chunks of CH tiles: their runs are concatenated (prefix of the counts in LDS) and
-            // row i of the chunk finds its tile by a log2(CH)-step binary search, so every thread
-            // takes RT rows per step whatever the run lengths
+            // chunks of CH tiles: their runs are concatenated (one packed record per run in LDS:
+            // its end row | narrow << 31, and its tile offset minus its start) and row i of the
+            // chunk finds its run through a sampled index, so every thread takes RT rows per step
+            // whatever the run lengths (packed records vs separate entry / prefix arrays: one
+            // dependent LDS read less a row, agg.bucket 0.409 -> 0.404 ms, r05d)
             for (int t0 = tbeg; t0 < tend; t0 += CH) {
                 const uint32_t e = t0 + (int)threadIdx.x < tend ? col[t0 + threadIdx.x] : 0u;
-#ifndef TFG_EXP_RUNS
-                s_ent[threadIdx.x] = e;
-#endif
                 uint32_t r_beg, r_end; // this thread's run in chunk rows
                 { // block-wide exclusive scan of the run lengths
                     const uint32_t c = e >> 16;
@@ -1344,22 +1408,13 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
                     for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) off += s_wsum[w];
                     r_beg = off + x - c;
                     r_end = off + x;
-#ifdef TFG_EXP_RUNS
                     s_run[threadIdx.x] = make_uint2(r_end | ((e & TILE_NARROW) ? 0x80000000u : 0u),
                                                     (uint32_t)((int)(e & 0x7FFFu) - (int)r_beg));
                     if (threadIdx.x == CH - 1) s_tot = r_end;
-#else
-                    s_pref[threadIdx.x] = r_beg;
-                    if (threadIdx.x == CH - 1) s_pref[CH] = r_end;
-#endif
                 }
                 __syncthreads();
-#ifdef TFG_EXP_RUNS
                 const uint32_t tot = s_tot;
-#else
-                const uint32_t tot = s_pref[CH];
-#endif
-                // the tile of row i is the last run with s_pref <= i.  A sampled index (every
+                // the run of row i is the first one ending past i.  A sampled index (every
                 // 2^idx_sh-th row's run; 32 rows while the chunk has <= 64K rows, runs average
                 // ~30 rows on C2) starts each row's search one or two runs before its own: one
                 // LDS read plus a short forward walk instead of a binary search (~5 dependent
@@ -1376,30 +1431,45 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
                 // made the kernel slower, 0.41 -> 0.52 ms: each load instruction then spans 4x the
                 // lines, and the run-crossing step diverges)
                 auto load_step = [&](uint32_t base, typename Ops::Row (&v)[RT], bool (&ok)[RT]) __attribute__((always_inline)) {
+                    // the RT rows' runs are found together: their index reads, their first run
+                    // reads, then forward steps for the rows past their run's end, so the
+                    // dependent LDS round trips of the RT rows overlap (one 8-byte read a run)
+                    uint32_t ii[RT], lo[RT];
+                    uint2 run[RT];
 #pragma unroll
                     for (int u = 0; u < RT; ++u) {
-                        const uint32_t i = base + u * BT + threadIdx.x;
-                        ok[u] = i < tot;
+                        ii[u] = base + u * BT + threadIdx.x;
+                        ok[u] = ii[u] < tot;
+                        lo[u] = ok[u] ? s_idx[ii[u] >> idx_sh] : 0u;
+                    }
+#pragma unroll
+                    for (int u = 0; u < RT; ++u) run[u] = s_run[lo[u]];
+                    for (;;) {
+                        bool walk[RT], any = false;
+#pragma unroll
+                        for (int u = 0; u < RT; ++u) {
+                            walk[u] = ok[u] && (run[u].x & 0x7FFFFFFFu) <= ii[u];
+                            lo[u] += walk[u] ? 1u : 0u;
+                            any = any || walk[u];
+                        }
+                        if (!any) break;
+#pragma unroll
+                        for (int u = 0; u < RT; ++u)
+                            if (walk[u]) run[u] = s_run[lo[u]];
+                    }
+#pragma unroll
+                    for (int u = 0; u < RT; ++u) {
                         if (!ok[u]) continue;
-                        uint32_t lo = s_idx[i >> idx_sh];
-#ifdef TFG_EXP_RUNS
-                        uint2 run = s_run[lo];
-                        while ((run.x & 0x7FFFFFFFu) <= i) run = s_run[++lo];
-                        const uint32_t off = run.y + i;
-                        const bool narrow = run.x >> 31;
-#else
-                        uint32_t nxt = s_pref[lo + 1];
-                        while (nxt <= i) nxt = s_pref[++lo + 1];
-                        const uint32_t ent = s_ent[lo], off = (ent & 0x7FFFu) + (i - s_pref[lo]);
-                        const bool narrow = (ent & TILE_NARROW) != 0;
-#endif
+                        const uint32_t off = run[u].y + ii[u];
+                        // the tile's slot: T * TRS rows stay below 2^32 (the ABI caps n below 2^32)
+                        const uint64_t slot = (uint64_t)(uint32_t)(t0 + (int)lo[u]) * (uint32_t)tin.TR;
                         if constexpr (Ops::NARROWABLE) {
-                            if (narrow) {
-                                ops.load_narrow(tin.rec, t0 + (int)lo, tin.TR, off, v[u]);
+                            if (run[u].x >> 31) {
+                                ops.load_narrow(tin.rec, slot, tin.TR, off, v[u]);
                                 continue;
                             }
                         }
-                        ops.load(src, (int64_t)(t0 + (int)lo) * tin.TR + off, v[u]);
+                        ops.load(src, (int64_t)(slot + off), v[u]);
                     }
                 };
                 typename Ops::Row vn[RT];

@@ -39,6 +39,17 @@ constexpr int JCHUNK = 4096; // build rows per LDS pass (row index fits 16 bits)
 constexpr int JRPT = 4;      // probe rows per thread per step
 constexpr int JFILL = 2560;  // target build rows per partition (table load ~0.63)
 constexpr int JMAXW = 2;     // payload words per side
+// probe records and output rows stream past the partition's build records, which the probe's
+// matches re-read at random: nontemporal loads / stores keep them from evicting those lines
+#ifdef TFG_EXP_JOIN_TEMPORAL
+constexpr bool JOIN_NT = false;
+#else
+constexpr bool JOIN_NT = true;
+#endif
+template <typename T> __device__ __forceinline__ void jstore(T *p, T v) {
+    if constexpr (JOIN_NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
 
 __device__ __forceinline__ uint64_t jload_bits(const void *p, int width, int64_t i) {
     switch (width) {
@@ -237,7 +248,7 @@ __global__ void __launch_bounds__(JT) join_probe_kernel(JoinArgs A) {
 #pragma unroll
             for (int u = 0; u < JRPT; ++u) {
                 const int64_t r = st + u * JT + threadIdx.x;
-                if (r < pe) load_rec<PRW>(A.prec, (size_t)r, dst[u]);
+                if (r < pe) load_rec<PRW, JOIN_NT>(A.prec, (size_t)r, dst[u]);
             }
         };
         uint64_t rw[JRPT][PRW]; // the probe records (key + payload words)
@@ -316,23 +327,24 @@ __global__ void __launch_bounds__(JT) join_probe_kernel(JoinArgs A) {
                         const bool pair = pairs && q < cnt[u];
                         if (pos < A.capacity) {
                             if (A.pw == 0) {
-                                ((uint32_t *)A.out_p[0])[pos] = A.prows[r];
+                                jstore((uint32_t *)A.out_p[0] + pos, A.prows[r]);
                             } else {
 #pragma unroll
                                 for (int w = 0; w < PRW; ++w)
-                                    if (w < A.pw) ((uint64_t *)A.out_p[w])[pos] = (A.pw0 ? rw[u][w + 1 < PRW ? w + 1 : w] : rw[u][w]);
+                                    if (w < A.pw)
+                                        jstore((uint64_t *)A.out_p[w] + pos, A.pw0 ? rw[u][w + 1 < PRW ? w + 1 : w] : rw[u][w]);
                             }
                             if (A.out_bnull) A.out_bnull[pos] = !pair;
                             if (A.out_b[0]) {
                                 if constexpr (BW == 0) {
-                                    ((uint32_t *)A.out_b[0])[pos] = pair ? A.brows[c0 + jb] : 0xFFFFFFFFu;
+                                    jstore((uint32_t *)A.out_b[0] + pos, pair ? A.brows[c0 + jb] : 0xFFFFFFFFu);
                                 } else if (pair && q == 0) {
 #pragma unroll
-                                    for (int w = 0; w < BW; ++w) ((uint64_t *)A.out_b[w])[pos] = bp[u][w];
+                                    for (int w = 0; w < BW; ++w) jstore((uint64_t *)A.out_b[w] + pos, bp[u][w]);
                                 } else {
                                     const uint64_t *rec = A.brec + (c0 + (pair ? jb : 0)) * brw;
 #pragma unroll
-                                    for (int w = 0; w < BW; ++w) ((uint64_t *)A.out_b[w])[pos] = pair ? rec[1 + w] : 0ull;
+                                    for (int w = 0; w < BW; ++w) jstore((uint64_t *)A.out_b[w] + pos, pair ? rec[1 + w] : (uint64_t)0);
                                 }
                             }
                         }

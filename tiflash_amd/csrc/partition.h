@@ -581,6 +581,7 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
     uint32_t *fh = reinterpret_cast<uint32_t *>(lds + g.fh_off); // TILED && fine_bits: P << fine_bits bins
     if (TILED && g.fine_bits)
         for (uint32_t p = threadIdx.x; p < (P << g.fine_bits); p += ST_T) fh[p] = 0;
+    bool spec = true; // the previous tile kept a row (workgroup-uniform): keys load with the predicate
     for (uint32_t tb = begin; tb < end; tb += (uint32_t)g.TR) {
         for (uint32_t p = threadIdx.x; p < P; p += ST_T) hist[p] = 0;
         if (NARROW && threadIdx.x == 0) red[ST_T / 64 + 1] = 0;
@@ -595,21 +596,33 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             Loaded pl[HB], kl[HB];
+            // the half-batch's loads first: predicate and key words together, unless the
+            // previous tile kept no row (workgroup-uniform): then the predicate first and the keys
+            // of the rows it keeps only, so all-false input reads no key word
+            // (FilterTransformAction.cpp:134-138 skips all-false blocks)
+            bool keep[HB];
 #pragma unroll
-            for (int q = 0; q < HB; ++q) { // the half-batch's loads first ...
+            for (int q = 0; q < HB; ++q) {
                 const int j = h * HB + q;
                 const uint32_t r = tb + (uint32_t)j * ST_T + threadIdx.x;
                 if (j < per && r < end) {
                     pl[q] = pred.load(r);
-                    kl[q] = sel.load(r);
+                    if (spec) kl[q] = sel.load(r);
                 }
+            }
+#pragma unroll
+            for (int q = 0; q < HB; ++q) {
+                const int j = h * HB + q;
+                const uint32_t r = tb + (uint32_t)j * ST_T + threadIdx.x;
+                keep[q] = j < per && r < end && pred.eval(pl[q]);
+                if (!spec && keep[q]) kl[q] = sel.load(r);
             }
 #pragma unroll
             for (int q = 0; q < HB; ++q) { // ... then destinations
                 const int j = h * HB + q;
                 bq[j] = 0xFFFFFFFFu;
                 const uint32_t r = tb + (uint32_t)j * ST_T + threadIdx.x;
-                if (j < per && r < end && pred.eval(pl[q])) {
+                if (keep[q]) {
                     uint32_t b = sel.part(crc, kl[q], r);
                     if (TILED && g.fine_bits && b < (P << g.fine_bits)) {
                         atomicAdd(&fh[b], 1u);
@@ -680,6 +693,7 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
         }
         __syncthreads();
         const uint32_t kept = red[ST_T / 64];
+        spec = kept != 0;
         const uint32_t tile = blockIdx.x * (uint32_t)g.tps + (tb - begin) / (uint32_t)g.TR;
         const bool narrow = NARROW && g.allow_narrow && red[ST_T / 64 + 1] == 0;
         if constexpr (TILED)
@@ -981,15 +995,23 @@ int run_partition_tiled(Ctx *ctx, const Sel &sel, const RowPred &pred, TiledGeom
 constexpr uint32_t RS_C = 64;
 constexpr int RS_T = 512, RS_RPT = 4, RS_BR = RS_T * RS_RPT, RS_TPC = 64;
 
-template <int NW> __device__ __forceinline__ void load_rec(const uint64_t *rec, size_t pos, uint64_t (&v)[NW]) {
+// NT: a streaming (nontemporal) load, for records read once while other data must stay in L2
+template <int NW, bool NT = false>
+__device__ __forceinline__ void load_rec(const uint64_t *rec, size_t pos, uint64_t (&v)[NW]) {
     if constexpr (NW == 2) { // one 16-byte load
         typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-        const u64x2 q = reinterpret_cast<const u64x2 *>(rec)[pos];
+        const u64x2 *p = reinterpret_cast<const u64x2 *>(rec) + pos;
+        u64x2 q;
+        if constexpr (NT) q = __builtin_nontemporal_load(p);
+        else q = *p;
         v[0] = q.x;
         v[1] = q.y;
     } else {
 #pragma unroll
-        for (int w = 0; w < NW; ++w) v[w] = rec[pos * NW + w];
+        for (int w = 0; w < NW; ++w) {
+            if constexpr (NT) v[w] = __builtin_nontemporal_load(rec + pos * NW + w);
+            else v[w] = rec[pos * NW + w];
+        }
     }
 }
 

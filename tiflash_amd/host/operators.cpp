@@ -966,6 +966,10 @@ Block MPPExchange::exchange(const std::vector<Block> &partitions) {
         const Block &b = partitions[p];
         send_cnt[(size_t)p * K] = b.rows();
         for (size_t j = 0; j < ncols; ++j) {
+            if (!b.safeGetByPosition(j).column) { // a header-only block (cloneEmpty): sends nothing
+                if (b.rows()) throw Exception("column without data in a non-empty block", ErrorCodes::LOGICAL_ERROR);
+                continue;
+            }
             ColumnPtr c = materialize(ctx_, b.safeGetByPosition(j).column);
             const DataType &t = proto.safeGetByPosition(j).type;
             if (c->type.isString() != t.isString() || c->rows != b.rows())
@@ -1018,7 +1022,8 @@ Block MPPExchange::exchange(const std::vector<Block> &partitions) {
     std::vector<tfg_slice> sends, recvs;
     for (int p = 0; p < P; ++p)
         for (size_t j = 0; j < ncols; ++j) {
-            const IColumn &c = *cols[(size_t)p * ncols + j];
+            static const IColumn none{}; // a header-only block's column: no rows, no planes
+            const IColumn &c = cols[(size_t)p * ncols + j] ? *cols[(size_t)p * ncols + j] : none;
             const DataType &t = proto.safeGetByPosition(j).type;
             IColumn &o = *outc[j];
             const uint64_t r = recv_cnt[(size_t)p * K];
