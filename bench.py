@@ -660,12 +660,13 @@ def variants_leg(args, ctx, dev, f, k, v):
             agg.reset()
             agg.consume_filtered(f, tfa.LT, t, k, [v, None])
             return agg.result()
-        el, res, _ = timed(step, args, ctx, 1)
+        el, res, prof = timed(step, args, ctx, 1)
         ms = el / args.steps * 1e3
         kept = int((f < t).sum().item())
         cnt = int(res["states"][1].view(torch.int64).sum().item()) if res["keys"] is not None else 0
         sweep[f"{t}%"] = {"value": round(N * args.steps / el, 1), "ms_per_step": round(ms, 3), "kept_rows": kept,
-                          "check_ok": cnt == kept, "pipeline_frac": round(24 * N / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+                          "check_ok": cnt == kept, "pipeline_frac": round(24 * N / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                          "kernels_ms_per_step": {kn: round(vv[0] / args.steps, 4) for kn, vv in sorted(prof.items())}}
     agg.close()
     out["selectivity_sweep"] = sweep
     gen = torch.Generator(device=dev)

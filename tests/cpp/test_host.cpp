@@ -2102,29 +2102,11 @@ TEST(PlanAggregateMinMaxFirstRow) {
                         {"first_row", {"k"}, "fk"}, {"count", {}, "c"}};
         std::vector<Block> halves = splitBlocks(ctx, b, 2);
         Aggregator fin(ctx, p);
-        bool first = true;
         for (const Block &h : halves) {
             Aggregator part(ctx, p);
             part.executeOnBlock(h);
             Block pb = part.convertToBlock(false);
-            if (first) { // the partial first_row column, for the log when the merge goes wrong
-                auto fy = cellStrings(ctx, *materialize(ctx, pb.getByName("fy").column));
-                auto kk = toHost<int64_t>(ctx, *pb.getByName("k").column);
-                std::string line;
-                for (size_t i = 0; i < 3 && i < fy.size(); ++i) line += std::to_string(kk[i]) + ":" + fy[i] + " ";
-                fprintf(stderr, "    partial first_row(y): %s(%zu groups)\n", line.c_str(), fy.size());
-                first = false;
-            }
             fin.mergeOnBlock(pb);
-            { // NULL first_row(y) cells after this merge, for the log when the merge goes wrong
-                Block mid = fin.convertToBlock(false);
-                auto fy = cellStrings(ctx, *materialize(ctx, mid.getByName("fy").column));
-                auto pfy = cellStrings(ctx, *materialize(ctx, pb.getByName("fy").column));
-                size_t nn = 0, pn = 0;
-                for (auto &s : fy) nn += s == "N";
-                for (auto &s : pfy) pn += s == "N";
-                if (nn || pn) fprintf(stderr, "    after a merge: %zu of %zu first_row(y) NULL (partial: %zu)\n", nn, fy.size(), pn);
-            }
         }
         Block r = fin.convertToBlock();
         auto got = rows({r}, 1, 2, 3, 4, 5, 0);

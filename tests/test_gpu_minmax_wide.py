@@ -358,3 +358,43 @@ def test_mixed_two_phase_with_count(tfa, ctx, dev, orc, nullmaps_of_nullable_onl
     fin.close()
     bad = [(kk, got.get(kk), ev) for kk, ev in exp.items() if got.get(kk) != ev][:5]
     assert len(got) == len(exp) and not bad, bad
+
+
+
+def test_mixed_two_phase_negative_values(tfa, ctx, dev, orc):
+    """the C++ PlanAggregateMinMaxFirstRow two-phase case with its value signs: first_row(y) with
+    y = k % 1000 under C's truncating %, so negative keys carry negative first_row values;
+    partial aggregators over the two halves (each checked against the oracle), merged with
+    consume_partial (null maps of the Nullable results only)"""
+    rng = np.random.default_rng(77)
+    n = 120_000
+    k = (rng.integers(0, 3000, n) - 1000).astype(np.int64)
+    v = (rng.integers(0, 2_000_001, n) - 1_000_000).astype(np.int32)
+    vn = ((np.fmod(k, 7) == 0) | (rng.integers(0, 4, n) == 0)).astype(np.uint8)
+    x = ((rng.integers(0, 1 << 24, n) - (1 << 23)) / 64.0).astype(np.float64)
+    y = np.fmod(k, 1000).astype(np.int16)
+    aggs = [(tfa.AGG_MIN, tfa.INT32 | tfa.NULLABLE), (tfa.AGG_MAX, tfa.FLOAT64), (tfa.AGG_FIRST_ROW, tfa.INT16),
+            (tfa.AGG_COUNT_ALL, 0)]
+    types = [tfa.INT32, tfa.FLOAT64, tfa.INT16, tfa.UINT64]
+    ref = orc.Agg(orc.INT64, aggs)
+    ref.consume(k, [v, x, y, None], arg_nulls=[vn, None, None, None])
+    exp = _orc(ref.result(), types)
+    fin = tfa.Aggregator(ctx, tfa.INT64, aggs)
+    for sl in (slice(0, n // 2), slice(n // 2, n)):
+        a = tfa.Aggregator(ctx, tfa.INT64, aggs)
+        a.consume(_t(k[sl], dev), [_t(v[sl], dev), _t(x[sl], dev), _t(y[sl], dev), None],
+                  arg_nullmaps=[_t(vn[sl], dev), None, None, None])
+        res = a.result()
+        part = _dev(res, types)
+        pref = orc.Agg(orc.INT64, aggs)
+        pref.consume(k[sl], [v[sl], x[sl], y[sl], None], arg_nulls=[vn[sl], None, None, None])
+        pexp = _orc(pref.result(), types)
+        bad = [(kk, part.get(kk), ev) for kk, ev in pexp.items() if part.get(kk) != ev][:5]
+        assert len(part) == len(pexp) and not bad, ("partial", bad)
+        fin.consume_partial(res["keys"], res["states"],
+                            state_nullmaps=[res["state_null"][0], None, res["state_null"][2], None])
+        a.close()
+    got = _dev(fin.result(), types)
+    fin.close()
+    bad = [(kk, got.get(kk), ev) for kk, ev in exp.items() if got.get(kk) != ev][:5]
+    assert len(got) == len(exp) and not bad, bad

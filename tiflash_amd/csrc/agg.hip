@@ -1919,11 +1919,10 @@ int tfg_agg_destroy(tfg_agg *a) {
         if (a->blk[i]) (void)hipFree(a->blk[i]);
         if (a->bucket_off[i]) (void)hipFree(a->bucket_off[i]);
     }
-    for (int i = 0; i < AGG_MAX; ++i) {
-        if (a->store[i].val) (void)hipFree(a->store[i].val);
-        if (a->store[i].scan) (void)hipFree(a->store[i].scan);
-        if (a->store[i].nul) (void)hipFree(a->store[i].nul);
-    }
+    // the value stores come from the stream-ordered pool (hipMallocAsync): they go back the same
+    // way (hipFree of pool memory corrupts the pool: a later allocation could share the block)
+    for (int i = 0; i < AGG_MAX; ++i) ref_store_free(a->ctx, a->store[i]);
+    (void)hipStreamSynchronize(a->ctx->stream);
     if (a->pack_buf) (void)hipFree(a->pack_buf);
     if (a->pack_err) (void)hipFree(a->pack_err);
     if (a->pend_blk) (void)hipFree(a->pend_blk);

@@ -4,7 +4,6 @@
 // which hipcc builds in parallel.
 #pragma once
 #include <algorithm>
-#include <type_traits>
 #include <vector>
 
 #include "common.h"
@@ -486,41 +485,6 @@ struct Table {
         }
     }
 
-    // Home-group lookup of R wide keys, branch-free (the wide twin of find_home): the group's four
-    // tags in one 32-byte read, the first published tag equal to the key's (tag | 1), then that
-    // cell's 16-byte key; cell[u] = the cell when the keys are equal, else -1 (not published yet,
-    // a tag collision, an overflow group, a new key: the caller's slow path, find_wide_multi)
-    template <int R>
-    __device__ __forceinline__ void find_wide_home(const uint64_t (&lo)[R], const uint64_t (&hi)[R],
-                                                   const uint64_t (&tag)[R], int (&cell)[R]) const {
-        const uint4 *wk = reinterpret_cast<const uint4 *>(base + S.wkey_off);
-        unsigned grp[R];
-        int s_hit[R];
-#pragma unroll
-        for (int u = 0; u < R; ++u) grp[u] = slot_group(tag[u]);
-#pragma unroll
-        for (int u = 0; u < R; ++u) {
-            const uint4 a = *reinterpret_cast<const uint4 *>(&keys[grp[u] * GS]);
-            const uint4 b = *reinterpret_cast<const uint4 *>(&keys[grp[u] * GS + 2]);
-            const uint64_t k[GS] = {((uint64_t)a.y << 32) | a.x, ((uint64_t)a.w << 32) | a.z,
-                                    ((uint64_t)b.y << 32) | b.x, ((uint64_t)b.w << 32) | b.z};
-            int c = -1;
-#pragma unroll
-            for (int s = GS - 1; s >= 0; --s) c = k[s] == (tag[u] | 1ull) ? s : c;
-            s_hit[u] = c;
-        }
-        // a published tag was stored after its key (release): read the key after the tag
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-#pragma unroll
-        for (int u = 0; u < R; ++u) {
-            cell[u] = -1;
-            if (s_hit[u] < 0) continue;
-            const int c = (int)(grp[u] * GS) + s_hit[u];
-            const uint4 q = wk[c];
-            if ((((uint64_t)q.y << 32) | q.x) == lo[u] && (((uint64_t)q.w << 32) | q.z) == hi[u]) cell[u] = c;
-        }
-    }
-
     // Wide keys (keys128 / packed String keys).  A cell is claimed by a 64-bit CAS of the key's
     // tag into keys[cell]; the claimant then writes the 16-byte key to wkeys[cell] and
     // republishes the tag with bit 0 set.  A reader whose tag equals a cell's unpublished tag
@@ -720,8 +684,11 @@ struct Table {
     }
 
     __device__ void flush(const GroupsIO &out, uint64_t out_base) {
-        for (int c = threadIdx.x; c < S.cap + 2; c += blockDim.x) {
-            bool occ;
+        // output slots: one LDS atomic per wave for its occupied cells (ballot + rank), not one
+        // per cell on the one counter
+        for (int c0 = 0; c0 < S.cap + 2; c0 += blockDim.x) {
+            const int c = c0 + (int)threadIdx.x;
+            bool occ = false;
             uint64_t key = 0;
             uint8_t isnull = 0;
             if (c < S.cap) {
@@ -729,12 +696,18 @@ struct Table {
                 occ = key != 0;
             } else if (c == S.cap) {
                 occ = ctrl->zero_used;
-            } else {
+            } else if (c == S.cap + 1) {
                 occ = ctrl->null_used;
                 isnull = 1;
             }
+            const uint64_t m = __ballot(occ);
+            if (m == 0) continue; // uniform in the wave
+            const int lane = (int)__lane_id(), first = __ffsll((unsigned long long)m) - 1;
+            unsigned long long wb = 0;
+            if (lane == first) wb = atomicAdd(&ctrl->out_count, (unsigned long long)__popcll(m));
+            wb = __shfl(wb, first, 64);
             if (!occ) continue;
-            const uint64_t pos = out_base + atomicAdd(&ctrl->out_count, 1ull);
+            const uint64_t pos = out_base + wb + (uint64_t)__popcll(m & ((1ull << lane) - 1));
             if (S.wkey_off) { // wide: the cell's 16-byte key (tags never take the side slots)
                 reinterpret_cast<uint4 *>(out.key)[pos] = reinterpret_cast<const uint4 *>(base + S.wkey_off)[c];
             } else {
@@ -1003,7 +976,6 @@ template <int NA, bool W = false> struct WideOps {
 // Wide keys on the tiled path: records {key lo, key hi, one word per summed argument}; the
 // value ops are FastOps' (1 count, 2 Int64 / UInt64 sum, 3 Float64 sum, 4 Decimal64 -> Decimal128)
 template <int A0, int A1, int A2> struct WideFastOps {
-    static constexpr bool HOME_FAST = true; // find_wide_home + add_all before the full probe
     static constexpr int op(int i) { return i == 0 ? A0 : (i == 1 ? A1 : A2); }
     static constexpr int NCOL = 2 + (A0 >= 2) + (A1 >= 2) + (A2 >= 2);
     static constexpr bool WIDE = true;
@@ -1035,10 +1007,6 @@ template <int A0, int A1, int A2> struct WideFastOps {
     template <int R>
     __device__ __forceinline__ void add_multi(Table &T, const int (&cell)[R], const Row (&v)[R]) const {
         fast_add_rows<A0, A1, A2, true>(T, cell, v);
-    }
-    template <int R>
-    __device__ __forceinline__ void add_all(Table &T, const int (&cell)[R], const Row (&v)[R]) const {
-        fast_add_rows<A0, A1, A2, false>(T, cell, v);
     }
     __device__ __forceinline__ void store(const RowsIO &sp, int64_t w, const Row &v) const {
         uint64_t *rec = (uint64_t *)sp.key + w * NCOL;
@@ -1188,12 +1156,6 @@ struct TiledIn {
     unsigned long long *cursor; // [0] spill rows, [1] temp groups
 };
 
-// Ops with the wide home-group fast path (WideFastOps::HOME_FAST)
-template <typename Ops, typename = void> struct wide_home_fast { static constexpr bool value = false; };
-template <typename Ops> struct wide_home_fast<Ops, std::void_t<decltype(Ops::HOME_FAST)>> {
-    static constexpr bool value = Ops::HOME_FAST;
-};
-
 template <typename Ops, int BT>
 __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn tin, int mode, GroupsIO old,
                                                               const uint64_t *old_off, GroupsIO out, uint64_t *out_cnt,
@@ -1331,31 +1293,13 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
                 }
                 return;
             }
-            bool want[RT]; // rows that still need the full probe
-#pragma unroll
-            for (int u = 0; u < RT; ++u) want[u] = ok[u];
-            if constexpr (Ops::WIDE && wide_home_fast<Ops>::value) {
-                // the wide fast path: home-group lookups, the adds of the found rows (others into
-                // the unused NULL-key slot: a dummy), then only the rest through the full probe
-                int home[RT], acell[RT];
-                bool anyslow = false;
-                T.find_wide_home<RT>(ku, kh, tg, home);
-#pragma unroll
-                for (int u = 0; u < RT; ++u) {
-                    want[u] = ok[u] && home[u] < 0;
-                    anyslow = anyslow || want[u];
-                    acell[u] = (ok[u] && home[u] >= 0) ? home[u] : S.cap + 1;
-                }
-                ops.add_all(T, acell, v);
-                if (__ballot(anyslow) == 0) return;
-            }
-            if constexpr (Ops::WIDE) T.find_wide_multi<RT>(ku, kh, tg, want, allow_insert, cells);
-            else T.find_or_insert_multi<RT>(ku, nu, want, allow_insert, cells);
+            if constexpr (Ops::WIDE) T.find_wide_multi<RT>(ku, kh, tg, ok, allow_insert, cells);
+            else T.find_or_insert_multi<RT>(ku, nu, ok, allow_insert, cells);
             int hit[RT];
 #pragma unroll
             for (int u = 0; u < RT; ++u) {
-                miss[u] = want[u] && cells[u] < 0;
-                hit[u] = want[u] ? cells[u] : -1;
+                miss[u] = ok[u] && cells[u] < 0;
+                hit[u] = ok[u] ? cells[u] : -1;
             }
             ops.add_multi(T, hit, v);
             // no barrier per step: a missing row (full table / inserts closed) looks its key up
@@ -1415,11 +1359,13 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
                 __syncthreads();
                 const uint32_t tot = s_tot;
                 // the run of row i is the first one ending past i.  A sampled index (every
-                // 2^idx_sh-th row's run; 32 rows while the chunk has <= 64K rows, runs average
-                // ~30 rows on C2) starts each row's search one or two runs before its own: one
-                // LDS read plus a short forward walk instead of a binary search (~5 dependent
-                // LDS reads and ~30 VALU a row)
-                uint32_t idx_sh = 5;
+                // 2^idx_sh-th row's run, as dense as IDXN allows: every row while the chunk has
+                // < 2048 rows, every 16th at C2's ~31K, where runs average ~30 rows) starts each
+                // row's search at most a few runs before its own: one LDS read plus a short
+                // forward walk instead of a binary search (~5 dependent LDS reads and ~30 VALU a
+                // row).  Sparser samples made low selectivities walk long stretches of empty runs
+                // (1 %: agg.bucket 0.38 ms with a 32-row index)
+                uint32_t idx_sh = 0;
                 while ((tot >> idx_sh) >= (uint32_t)IDXN) ++idx_sh; // uniform
                 for (uint32_t k = (r_beg + (1u << idx_sh) - 1) >> idx_sh; (k << idx_sh) < r_end; ++k)
                     s_idx[k] = (uint16_t)threadIdx.x;

@@ -583,6 +583,42 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
         for (uint32_t p = threadIdx.x; p < (P << g.fine_bits); p += ST_T) fh[p] = 0;
     bool spec = true; // the previous tile kept a row (workgroup-uniform): keys load with the predicate
     for (uint32_t tb = begin; tb < end; tb += (uint32_t)g.TR) {
+        if constexpr (TILED) {
+            if (!spec) {
+                // the previous tile kept no row: skip ahead over tiles whose predicate keeps
+                // nothing — one predicate read and one barrier each, their runs written empty —
+                // to the next tile that keeps a row (FilterTransformAction.cpp:134-138)
+                // two tiles a round: both tiles' predicate words in flight together
+                while (tb < end) {
+                    Loaded pv[2][ST_MAXR];
+#pragma unroll
+                    for (int t = 0; t < 2; ++t)
+#pragma unroll
+                        for (int j = 0; j < ST_MAXR; ++j) {
+                            const uint32_t r = tb + (uint32_t)t * (uint32_t)g.TR + (uint32_t)j * ST_T + threadIdx.x;
+                            if (j < per && r < end) pv[t][j] = pred.load(r);
+                        }
+                    bool any[2] = {false, false};
+#pragma unroll
+                    for (int t = 0; t < 2; ++t)
+#pragma unroll
+                        for (int j = 0; j < ST_MAXR; ++j) {
+                            const uint32_t r = tb + (uint32_t)t * (uint32_t)g.TR + (uint32_t)j * ST_T + threadIdx.x;
+                            any[t] = any[t] || (j < per && r < end && pred.eval(pv[t][j]));
+                        }
+                    if (__syncthreads_or(any[0])) break;
+                    const bool keep1 = __syncthreads_or(any[1]) != 0;
+                    const uint32_t tile = blockIdx.x * (uint32_t)g.tps + (tb - begin) / (uint32_t)g.TR;
+                    for (uint32_t p = threadIdx.x; p < P; p += ST_T) g.tile_hist[(size_t)p * g.T + tile] = 0u;
+                    tb += (uint32_t)g.TR;
+                    if (keep1 || tb >= end) break;
+                    for (uint32_t p = threadIdx.x; p < P; p += ST_T) g.tile_hist[(size_t)p * g.T + tile + 1] = 0u;
+                    tb += (uint32_t)g.TR;
+                }
+                if (tb >= end) break;
+                spec = true; // this tile keeps a row
+            }
+        }
         for (uint32_t p = threadIdx.x; p < P; p += ST_T) hist[p] = 0;
         if (NARROW && threadIdx.x == 0) red[ST_T / 64 + 1] = 0;
         __syncthreads();
@@ -769,7 +805,7 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
                 u64x2 rec;
                 rec.x = a0;
                 rec.y = a1;
-                reinterpret_cast<u64x2 *>(cols.out[0])[gp] = rec; // (nontemporal stores measured no different)
+                reinterpret_cast<u64x2 *>(cols.out[0])[gp] = rec; // (nontemporal stores measured no different, r05h)
             } else if constexpr (AOS) {
 #pragma unroll
                 for (int c = 0; c < NC8; ++c)
