@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--value-int64", action="store_true", help="Int64 value column instead of Float64 (headline leg)")
     ap.add_argument("--bucket-bits", type=int, default=0, help="aggregation radix buckets (0 = from --groups)")
     ap.add_argument("--c5-bucket-bits", type=int, default=0, help="C5 aggregation radix buckets (0 = from --c5-groups)")
+    ap.add_argument("--c5-expected-groups", type=int, default=0,
+                    help="C5 aggregators' expected_groups (their table sizing; 0 = --c5-groups)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, production) or gloo (rehearsal: all ranks may share one GPU)")
     return ap.parse_args()
@@ -361,8 +363,9 @@ def c5_leg(args, ctx, dev, world, rank):
     offs = torch.arange(1, n + 1, device=dev, dtype=torch.int64) * 10
     v = torch.randint(0, 10**9, (n,), device=dev, generator=g, dtype=torch.int64)
     aggs = [(tfa.AGG_SUM, tfa.prec(tfa.DECIMAL64, 15)), (tfa.AGG_COUNT_ALL, 0)]
-    part = tfa.KeysAggregator(ctx, [tfa.STRING], aggs, expected_groups=G, bucket_bits=args.c5_bucket_bits)
-    fin = tfa.KeysAggregator(ctx, [tfa.STRING], aggs, expected_groups=G, bucket_bits=args.c5_bucket_bits) if world > 1 else None
+    eg = args.c5_expected_groups or G
+    part = tfa.KeysAggregator(ctx, [tfa.STRING], aggs, expected_groups=eg, bucket_bits=args.c5_bucket_bits)
+    fin = tfa.KeysAggregator(ctx, [tfa.STRING], aggs, expected_groups=eg, bucket_bits=args.c5_bucket_bits) if world > 1 else None
 
     def step():
         part.reset()
@@ -659,7 +662,7 @@ def variants_leg(args, ctx, dev, f, k, v):
         def step():
             agg.reset()
             agg.consume_filtered(f, tfa.LT, t, k, [v, None])
-            return agg.result()
+            return agg.result(capacity_hint=G)
         el, res, prof = timed(step, args, ctx, 1)
         ms = el / args.steps * 1e3
         kept = int((f < t).sum().item())
@@ -678,7 +681,7 @@ def variants_leg(args, ctx, dev, f, k, v):
     def istep():
         agg.reset()
         agg.consume_filtered(f, tfa.LT, args.threshold, k, [vi, None])
-        return agg.result()
+        return agg.result(capacity_hint=G)
     el, res, _ = timed(istep, args, ctx, 1)
     ms = el / args.steps * 1e3
     kept = int((f < args.threshold).sum().item())
@@ -741,7 +744,9 @@ def main():
     def step():
         agg.reset()
         agg.consume_filtered(f, tfa.LT, args.threshold, k, [v, None])
-        res = agg.result()  # final Block of this rank (or its partial states)
+        # final Block of this rank (or its partial states); the key domain [0, G) bounds the group
+        # count, so the result buffers go over before the count is read (no mid-step round trip)
+        res = agg.result(capacity_hint=G)
         if world == 1:
             return res
         # ExchangeSender: hash-repartition partial rows by key, RCCL all-to-all, final merge

@@ -370,7 +370,12 @@ int tfg_agg_size(tfg_agg *agg, uint64_t *out_groups);
  * width (8 B for Int64/UInt64/Float64 sums and counts, 16 B for Decimal128 sums, 32 B for
  * Decimal256 sums);
  * out_state_nullmaps[i] (optional): 1 when sum saw no non-NULL value (AggregateFunctionNull).
- * Order is the table's (compare unordered, as the reference tests do). */
+ * Order is the table's (compare unordered, as the reference tests do).
+ * *out_groups_host = the group count; more than `capacity` -> TFG_ERR_CAPACITY.  When the count
+ * is not known yet (the groups of a tiled consume, no tfg_agg_size since, no first_row / wide
+ * min / max aggregate) the groups are written first and the count read after them: the first
+ * `capacity` groups are written even when TFG_ERR_CAPACITY is returned, so a caller may pass a
+ * capacity hint (e.g. the previous call's count) and retry with the reported count. */
 int tfg_agg_result(tfg_agg *agg, void *out_keys, uint8_t *out_key_nullmap, void *const *out_states,
                    uint8_t *const *out_state_nullmaps, uint64_t capacity, uint64_t *out_groups_host);
 /* Several GROUP BY keys, one String key or one 16-byte key (Aggregator::chooseAggregationMethod,

@@ -512,19 +512,35 @@ class Aggregator:
         check(lib().tfg_agg_size(self.h, ctypes.byref(g)))
         return g.value
 
-    def result(self, device=None):
-        """-> dict(keys, key_null, states[i], state_null[i]) with exactly size() rows."""
+    def result(self, device=None, capacity_hint: Optional[int] = None):
+        """-> dict(keys, key_null, states[i], state_null[i]) with exactly size() rows.
+        capacity_hint (e.g. the previous result's group count): buffers of that many groups are
+        handed over before the count is known, so the device runs the result without waiting for
+        a host round trip; a count above the hint falls back to the exact call."""
         import torch
         dev = device or torch.device("cuda", self.ctx.device)
-        g = self.size()
         kw = WIDTH.get(self.key_type, 8)
-        keys = _empty(g, kw, dev) if self.key_type else None
-        key_null = torch.empty(max(g, 1), dtype=torch.uint8, device=dev)[:g]
-        sarr, _keep, states = _agg_states(self.h, len(self.aggs), g, dev)
-        snulls = [torch.empty(max(g, 1), dtype=torch.uint8, device=dev)[:g] for _ in self.aggs]
-        cnt = ctypes.c_uint64()
-        check(lib().tfg_agg_result(self.h, _p(keys), _p(key_null), sarr, _ptr_array(snulls),
-                                   ctypes.c_uint64(g), ctypes.byref(cnt)))
+
+        def run(g):
+            keys = _empty(g, kw, dev) if self.key_type else None
+            key_null = torch.empty(max(g, 1), dtype=torch.uint8, device=dev)[:g]
+            sarr, _keep, states = _agg_states(self.h, len(self.aggs), g, dev)
+            snulls = [torch.empty(max(g, 1), dtype=torch.uint8, device=dev)[:g] for _ in self.aggs]
+            cnt = ctypes.c_uint64()
+            rc = lib().tfg_agg_result(self.h, _p(keys), _p(key_null), sarr, _ptr_array(snulls),
+                                      ctypes.c_uint64(g), ctypes.byref(cnt))
+            return rc, cnt.value, keys, key_null, states, snulls
+
+        if capacity_hint:
+            rc, n, keys, key_null, states, snulls = run(int(capacity_hint))
+            if rc == TFG_OK:
+                cut = lambda t: t if t is None else ((t[0], t[1][:n]) if isinstance(t, tuple) else t[:n])
+                return {"keys": cut(keys), "key_null": key_null[:n], "states": [cut(s) for s in states],
+                        "state_null": [x[:n] for x in snulls]}
+            if rc != TFG_ERR_CAPACITY:
+                check(rc)
+        rc, _, keys, key_null, states, snulls = run(self.size())
+        check(rc)
         return {"keys": keys, "key_null": key_null, "states": states, "state_null": snulls}
 
     def close(self):

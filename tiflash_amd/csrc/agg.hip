@@ -227,11 +227,13 @@ __global__ void agg_result_kernel(AggSpec S, GroupsIO st, uint64_t n, int key_wi
 // the result straight from a tiled consume's bucket-strided groups (pending state): workgroup b
 // writes bucket b's cnt[b] groups, found at base[b], to rows off[b].. (off = exclusive scan of cnt)
 // — the compaction into a dense state is never run for a consume -> result step
+// groups at output rows >= capacity are dropped (a result written before its group count is known)
 __global__ void agg_result_buckets_kernel(AggSpec S, GroupsIO st, const uint64_t *cnt, const uint64_t *base,
                                           const uint64_t *off, int key_width, void *out_keys, uint8_t *out_key_null,
-                                          ResultPtrs res) {
+                                          ResultPtrs res, uint64_t capacity) {
     const int b = blockIdx.x;
-    const uint64_t s0 = base[b], d0 = off[b], c = cnt[b];
+    const uint64_t s0 = base[b], d0 = off[b];
+    const uint64_t c = d0 >= capacity ? 0 : min(cnt[b], capacity - d0);
     for (uint64_t j = threadIdx.x; j < c; j += blockDim.x)
         write_result(S, st, s0 + j, d0 + j, key_width, out_keys, out_key_null, res);
 }
@@ -790,13 +792,33 @@ __global__ void ref_store_str_kernel(uint64_t *acc, uint64_t G, uint64_t n0, Ref
 
 using namespace tfg;
 
-// The value store of one ACC_REF aggregate: n entries in group order.
+// The value store of one ACC_REF aggregate: n entries in group order.  Its buffers are plain
+// device allocations that grow on demand (grow_buf) and are reused call after call: the store and
+// a spare one are swapped by every rebuild.
 struct RefStore {
     uint8_t *val = nullptr;   // fixed: n values of the argument's width; String: chars
     uint64_t *scan = nullptr; // String: n + 1 start offsets (scan + 1 = the end offsets)
     uint8_t *nul = nullptr;   // NULL flags
     uint64_t n = 0, bytes = 0;
+    size_t val_cap = 0, scan_cap = 0, nul_cap = 0;
 };
+
+// *p holds at least `bytes` (a quarter more when it grows); the old buffer is freed after the
+// stream has finished with it
+static int grow_buf(Ctx *ctx, void **p, size_t *cap, size_t bytes) {
+    bytes = std::max<size_t>(bytes, 16);
+    if (*p && *cap >= bytes) return TFG_OK;
+    if (*p) {
+        TFG_HIP(hipStreamSynchronize(ctx->stream));
+        TFG_HIP(hipFree(*p));
+        *p = nullptr;
+        *cap = 0;
+    }
+    const size_t nc = bytes + bytes / 4;
+    TFG_HIP(hipMalloc(p, nc));
+    *cap = nc;
+    return TFG_OK;
+}
 
 struct tfg_agg {
     Ctx *ctx = nullptr;
@@ -848,7 +870,13 @@ struct tfg_agg {
     // their value stores and the collators of String min / max
     bool has_ref = false;
     int ref_coll[AGG_MAX] = {};
-    RefStore store[AGG_MAX];
+    RefStore store[AGG_MAX], spare[AGG_MAX];
+    // per-aggregate row references of a call (consume: the rows' references; merge: the source's,
+    // shifted) and the String rebuild's temporaries
+    void *ref_rows[AGG_MAX] = {};
+    size_t ref_rows_cap[AGG_MAX] = {};
+    void *ref_tmp[2] = {};
+    size_t ref_tmp_cap[2] = {};
     // wide keys (keys128 / key_string): key_type == TFG_KEYS_WIDE, packing spec, and a device
     // buffer holding the packed keys of the block being consumed / the result being written
     KeyPack kp{};
@@ -951,13 +979,16 @@ int fast_signature(const AggSpec &S, int mode, int key_width, const uint8_t *key
 
 // ---- the pending state of a tiled consume (tfg_agg::pending)
 // groups per bucket -> their output offsets and the total (one host read, cached)
-int pend_counts(tfg_agg *a) {
-    if (!a->pending || a->pend_known) return TFG_OK;
+int pend_scan(tfg_agg *a) { // the output offsets on the device (no host read)
     Ctx *ctx = a->ctx;
     void *sp;
     if (int rc = scratch_get(ctx, scan_tmp_bytes(a->B + 1), &sp)) return rc;
-    if (int rc = exclusive_scan_u64(ctx, a->pend_cnt(), a->pend_off(), a->B, sp)) return rc;
-    if (int rc = read_back_u64(ctx, a->pend_off() + a->B, &a->pend_total, 1)) return rc;
+    return exclusive_scan_u64(ctx, a->pend_cnt(), a->pend_off(), a->B, sp);
+}
+int pend_counts(tfg_agg *a) {
+    if (!a->pending || a->pend_known) return TFG_OK;
+    if (int rc = pend_scan(a)) return rc;
+    if (int rc = read_back_u64(a->ctx, a->pend_off() + a->B, &a->pend_total, 1)) return rc;
     a->pend_known = true;
     return TFG_OK;
 }
@@ -1415,27 +1446,19 @@ struct RefIn { // source 1 of an ACC_REF aggregate's candidates: the consumed co
     const uint8_t *nul = nullptr;
     uint64_t n = 0;
 };
-struct RefCall { // temporaries of one call, freed stream-ordered after its launches
+struct RefCall { // the collated candidates of one call (String min / max under a case-insensitive collator)
     Ctx *ctx;
     CollatedStrings cs[AGG_MAX][2];
-    std::vector<void *> tmp;
     explicit RefCall(Ctx *c) : ctx(c) {}
     RefCall(const RefCall &) = delete;
     RefCall &operator=(const RefCall &) = delete;
-    ~RefCall() {
-        for (void *p : tmp) (void)hipFreeAsync(p, ctx->stream);
-    }
-    int alloc(size_t bytes, void **p) {
-        TFG_HIP(hipMallocAsync(p, std::max<size_t>(bytes, 16), ctx->stream));
-        tmp.push_back(*p);
-        return TFG_OK;
-    }
 };
 
-void ref_store_free(Ctx *ctx, RefStore &st) {
-    if (st.val) (void)hipFreeAsync(st.val, ctx->stream);
-    if (st.scan) (void)hipFreeAsync(st.scan, ctx->stream);
-    if (st.nul) (void)hipFreeAsync(st.nul, ctx->stream);
+// the stream is synchronized before (the buffers' last users may still run)
+void ref_store_free(RefStore &st) {
+    if (st.val) (void)hipFree(st.val);
+    if (st.scan) (void)hipFree(st.scan);
+    if (st.nul) (void)hipFree(st.nul);
     st = RefStore{};
 }
 
@@ -1482,15 +1505,15 @@ int ref_rebuild(tfg_agg *a, const RefIn *in) {
     for (int i = 0; i < a->S.n_aggs; ++i) {
         if (a->S.acc[i] != ACC_REF) continue;
         RefStore &old = a->store[i];
+        RefStore &nw = a->spare[i]; // its buffers: free since the previous rebuild
         const RefCol s0{old.val, old.scan ? old.scan + 1 : nullptr, old.nul}, s1{in[i].val, in[i].off, in[i].nul};
         uint64_t *acc = (uint64_t *)st.acc[i];
-        RefStore nw;
-        nw.n = G;
-        TFG_HIP(hipMallocAsync((void **)&nw.nul, std::max<uint64_t>(G, 16), ctx->stream));
+        if (int rc = grow_buf(ctx, (void **)&nw.nul, &nw.nul_cap, G)) return rc;
         const int t = a->S.src_type[i];
+        uint64_t total = 0;
         if (t != TFG_STRING) {
             const int w = (int)type_width(t);
-            TFG_HIP(hipMallocAsync((void **)&nw.val, std::max<uint64_t>(G * w, 16), ctx->stream));
+            if (int rc = grow_buf(ctx, (void **)&nw.val, &nw.val_cap, G * w)) return rc;
             if (G) {
                 ProfScope _ps(ctx, "agg.ref_store");
                 hipLaunchKernelGGL(ref_store_fixed_kernel, dim3(grid), dim3(256), 0, ctx->stream, acc, G, old.n, w, s0, s1,
@@ -1498,23 +1521,20 @@ int ref_rebuild(tfg_agg *a, const RefIn *in) {
                 TFG_LAUNCH_CHECK();
             }
         } else {
-            TFG_HIP(hipMallocAsync((void **)&nw.scan, (G + 1) * 8, ctx->stream));
-            uint64_t total = 0;
+            if (int rc = grow_buf(ctx, (void **)&nw.scan, &nw.scan_cap, (G + 1) * 8)) return rc;
             if (G) {
-                RefCall tmp(ctx);
-                void *len = nullptr, *sc = nullptr;
-                if (int rc = tmp.alloc(G * 8, &len)) return rc;
-                if (int rc = tmp.alloc(scan_tmp_bytes((int64_t)G) + 256, &sc)) return rc;
+                if (int rc = grow_buf(ctx, &a->ref_tmp[0], &a->ref_tmp_cap[0], G * 8)) return rc;
+                if (int rc = grow_buf(ctx, &a->ref_tmp[1], &a->ref_tmp_cap[1], scan_tmp_bytes((int64_t)G) + 256)) return rc;
                 hipLaunchKernelGGL(ref_store_len_kernel, dim3(grid), dim3(256), 0, ctx->stream, (const uint64_t *)acc, G,
-                                   old.n, s0, s1, (uint64_t *)len);
+                                   old.n, s0, s1, (uint64_t *)a->ref_tmp[0]);
                 TFG_LAUNCH_CHECK();
-                if (int rc = exclusive_scan_u64(ctx, (const uint64_t *)len, nw.scan, (int64_t)G, sc)) return rc;
+                if (int rc = exclusive_scan_u64(ctx, (const uint64_t *)a->ref_tmp[0], nw.scan, (int64_t)G, a->ref_tmp[1]))
+                    return rc;
                 if (int rc = read_back_u64(ctx, nw.scan + G, &total, 1)) return rc;
             } else {
                 TFG_HIP(hipMemsetAsync(nw.scan, 0, 8, ctx->stream));
             }
-            nw.bytes = total;
-            TFG_HIP(hipMallocAsync((void **)&nw.val, std::max<uint64_t>(total, 16), ctx->stream));
+            if (int rc = grow_buf(ctx, (void **)&nw.val, &nw.val_cap, total)) return rc;
             if (G) {
                 ProfScope _ps(ctx, "agg.ref_store");
                 hipLaunchKernelGGL(ref_store_str_kernel, dim3(grid), dim3(256), 0, ctx->stream, acc, G, old.n, s0, s1,
@@ -1522,8 +1542,10 @@ int ref_rebuild(tfg_agg *a, const RefIn *in) {
                 TFG_LAUNCH_CHECK();
             }
         }
-        ref_store_free(ctx, old);
-        old = nw;
+        nw.n = G;
+        nw.bytes = total;
+        std::swap(old, nw); // the old store's buffers become the spare ones
+        nw.n = nw.bytes = 0;
     }
     return TFG_OK;
 }
@@ -1531,8 +1553,7 @@ int ref_rebuild(tfg_agg *a, const RefIn *in) {
 // the stores after create / reset: empty, or (without key) the one group's "no value"
 int ref_reset(tfg_agg *a) {
     if (!a->has_ref) return TFG_OK;
-    for (int i = 0; i < a->S.n_aggs; ++i)
-        if (a->S.acc[i] == ACC_REF) ref_store_free(a->ctx, a->store[i]);
+    for (int i = 0; i < a->S.n_aggs; ++i) a->store[i].n = a->store[i].bytes = 0; // buffers kept
     if (!a->nokey) return TFG_OK;
     RefIn none[AGG_MAX];
     return ref_rebuild(a, none); // the group's references are 0 (zeroed state)
@@ -1574,8 +1595,8 @@ int consume_common(tfg_agg *a, int mode, const RowPred &pred, const void *keys, 
             uint64_t n0 = 0;
             for (int i = 0; i < a->S.n_aggs; ++i)
                 if (a->S.acc[i] == ACC_REF) n0 = a->store[i].n;
-            void *refs = nullptr;
-            if (int r = rc.alloc((size_t)n * 8, &refs)) return r;
+            if (int r = grow_buf(a->ctx, &a->ref_rows[0], &a->ref_rows_cap[0], (size_t)n * 8)) return r;
+            void *refs = a->ref_rows[0];
             hipLaunchKernelGGL(ref_iota_kernel, dim3(stream_grid(n, 256, 4096)), dim3(256), 0, a->ctx->stream,
                                (uint64_t *)refs, n0, n);
             TFG_LAUNCH_CHECK();
@@ -1919,10 +1940,13 @@ int tfg_agg_destroy(tfg_agg *a) {
         if (a->blk[i]) (void)hipFree(a->blk[i]);
         if (a->bucket_off[i]) (void)hipFree(a->bucket_off[i]);
     }
-    // the value stores come from the stream-ordered pool (hipMallocAsync): they go back the same
-    // way (hipFree of pool memory corrupts the pool: a later allocation could share the block)
-    for (int i = 0; i < AGG_MAX; ++i) ref_store_free(a->ctx, a->store[i]);
-    (void)hipStreamSynchronize(a->ctx->stream);
+    for (int i = 0; i < AGG_MAX; ++i) {
+        ref_store_free(a->store[i]);
+        ref_store_free(a->spare[i]);
+        if (a->ref_rows[i]) (void)hipFree(a->ref_rows[i]);
+    }
+    for (int i = 0; i < 2; ++i)
+        if (a->ref_tmp[i]) (void)hipFree(a->ref_tmp[i]);
     if (a->pack_buf) (void)hipFree(a->pack_buf);
     if (a->pack_err) (void)hipFree(a->pack_err);
     if (a->pend_blk) (void)hipFree(a->pend_blk);
@@ -2042,8 +2066,9 @@ int tfg_agg_merge(tfg_agg *dst, tfg_agg *src) {
         vals[i] = g.acc[i];
         cnts[i] = g.cnt[i];
         if (src->S.acc[i] != ACC_REF) continue;
-        void *sh = nullptr; // src's references, moved past dst's store
-        if (int r = rc.alloc(src->n_groups * 8, &sh)) return r;
+        // src's references, moved past dst's store
+        if (int r = grow_buf(dst->ctx, &dst->ref_rows[i], &dst->ref_rows_cap[i], src->n_groups * 8)) return r;
+        void *sh = dst->ref_rows[i];
         hipLaunchKernelGGL(ref_shift_kernel, dim3(stream_grid((int64_t)src->n_groups, 256, 4096)), dim3(256), 0,
                            dst->ctx->stream, (const uint64_t *)g.acc[i], dst->store[i].n, (int64_t)src->n_groups,
                            (uint64_t *)sh);
@@ -2086,6 +2111,34 @@ int tfg_agg_result(tfg_agg *a, void *out_keys, uint8_t *out_key_nullmap, void *c
     TFG_CHECK(a, TFG_ERR_INVALID_ARG, "agg is null");
     TFG_CHECK(!a->sdict, TFG_ERR_NOT_IMPLEMENTED,
               "serialized GROUP BY keys have no packed form: read them with tfg_agg_result_keys");
+    if (a->pending && !a->pend_known && !a->has_ref && capacity > 0) {
+        // groups of a tiled consume, count not read yet: the result is written first (groups
+        // past `capacity` dropped) and the count read after it, so no host round trip idles the
+        // device between the consume and the result
+        ResultPtrs rp{};
+        for (int i = 0; i < a->S.n_aggs; ++i) {
+            rp.state[i] = out_states ? out_states[i] : nullptr;
+            rp.state_null[i] = out_state_nullmaps ? out_state_nullmaps[i] : nullptr;
+            rp.nullable[i] = a->arg_nullable[i] || a->S.kind[i] == TFG_AGG_FIRST_ROW;
+        }
+        if (int rc = set_device(a->ctx)) return rc;
+        if (int rc = pend_scan(a)) return rc;
+        {
+            ProfScope _ps(a->ctx, "agg.result");
+            hipLaunchKernelGGL(agg_result_buckets_kernel, dim3(a->B), dim3(256), 0, a->ctx->stream, a->S, a->pend,
+                               (const uint64_t *)a->pend_cnt(), (const uint64_t *)a->pend_base(),
+                               (const uint64_t *)a->pend_off(), a->S.key_width, out_keys, out_key_nullmap, rp, capacity);
+        }
+        TFG_LAUNCH_CHECK();
+        if (int rc = read_back_u64(a->ctx, a->pend_off() + a->B, &a->pend_total, 1)) return rc;
+        a->pend_known = true;
+        if (out_groups_host) *out_groups_host = a->pend_total;
+        if (a->pend_total > capacity)
+            return fail(TFG_ERR_CAPACITY, "result needs %llu groups, capacity %llu (the first %llu written)",
+                        (unsigned long long)a->pend_total, (unsigned long long)capacity,
+                        (unsigned long long)capacity);
+        return TFG_OK;
+    }
     uint64_t G = 0;
     if (int rc = tfg_agg_size(a, &G)) return rc;
     if (out_groups_host) *out_groups_host = G;
@@ -2114,7 +2167,7 @@ int tfg_agg_result(tfg_agg *a, void *out_keys, uint8_t *out_key_nullmap, void *c
     if (a->pending) // straight from the tiled consume's buckets
         hipLaunchKernelGGL(agg_result_buckets_kernel, dim3(a->B), dim3(256), 0, a->ctx->stream, a->S, a->pend,
                            (const uint64_t *)a->pend_cnt(), (const uint64_t *)a->pend_base(),
-                           (const uint64_t *)a->pend_off(), a->S.key_width, out_keys, out_key_nullmap, rp);
+                           (const uint64_t *)a->pend_off(), a->S.key_width, out_keys, out_key_nullmap, rp, G);
     else
         hipLaunchKernelGGL(agg_result_kernel, dim3(stream_grid((int64_t)G, 256, 4096)), dim3(256), 0, a->ctx->stream,
                            a->S, a->st[a->cur], G, a->S.key_width, a->nokey ? nullptr : out_keys, out_key_nullmap, rp);
@@ -2393,6 +2446,7 @@ int tfg_agg_result_keys(tfg_agg *a, void *const *out_key_cols, uint64_t *const *
     Ctx *ctx = a->ctx;
     KeyOut ko{};
     uint64_t *start = nullptr;
+    bool chars_known = true;
     const unsigned grid = stream_grid((int64_t)G, 256, 4096);
     if (a->kp.kind == WK_STRING) {
         TFG_CHECK(out_key_cols && out_key_cols[0] && out_key_offsets && out_key_offsets[0], TFG_ERR_INVALID_ARG,
@@ -2406,12 +2460,17 @@ int tfg_agg_result_keys(tfg_agg *a, void *const *out_key_cols, uint64_t *const *
         hipLaunchKernelGGL(wide_str_len_kernel, dim3(grid), dim3(256), 0, ctx->stream, (const uint4 *)a->pack_buf, G, len1);
         TFG_LAUNCH_CHECK();
         if (int rc = exclusive_scan_u64(ctx, len1, start, (int64_t)G, (char *)sp + o_tmp)) return rc;
-        uint64_t chars = 0;
-        if (int rc = read_back_u64(ctx, start + G, &chars, 1)) return rc;
-        if (out_chars_host) *out_chars_host = chars;
-        if (chars > chars_capacity)
-            return fail(TFG_ERR_CAPACITY, "String keys need %llu bytes, capacity %llu", (unsigned long long)chars,
-                        (unsigned long long)chars_capacity);
+        // a packed String key holds <= 15 bytes + '\0': with room for 16 a group the capacity needs
+        // no check, and the total is read after the unpack is queued (no idle gap before it)
+        chars_known = chars_capacity < 16 * G;
+        if (chars_known) {
+            uint64_t chars = 0;
+            if (int rc = read_back_u64(ctx, start + G, &chars, 1)) return rc;
+            if (out_chars_host) *out_chars_host = chars;
+            if (chars > chars_capacity)
+                return fail(TFG_ERR_CAPACITY, "String keys need %llu bytes, capacity %llu", (unsigned long long)chars,
+                            (unsigned long long)chars_capacity);
+        }
         ko.offsets = out_key_offsets[0];
     }
     for (int j = 0; j < a->kp.nkeys; ++j) {
@@ -2424,6 +2483,8 @@ int tfg_agg_result_keys(tfg_agg *a, void *const *out_key_cols, uint64_t *const *
                            (const uint4 *)a->pack_buf, (const uint64_t *)start, G, ko);
     }
     TFG_LAUNCH_CHECK();
+    if (!chars_known && out_chars_host)
+        if (int rc = read_back_u64(ctx, start + G, out_chars_host, 1)) return rc;
     return TFG_OK;
 }
 
