@@ -398,3 +398,23 @@ def test_mixed_two_phase_negative_values(tfa, ctx, dev, orc):
     fin.close()
     bad = [(kk, got.get(kk), ev) for kk, ev in exp.items() if got.get(kk) != ev][:5]
     assert len(got) == len(exp) and not bad, bad
+
+
+def test_mixed_collators_and_decimal_blocks(tfa, ctx, dev, orc):
+    """the C++ PlanAggregateWideMinMaxFirstRow aggregate set in one aggregator: min(s) under
+    utf8_general_ci, max(s) binary, first_row(s) over a Nullable String of 0-3 (multi-byte)
+    characters, max(d) Decimal128 — three blocks, vs the oracle"""
+    rng = np.random.default_rng(91)
+    n, groups = 60_000, 2_000
+    k = rng.integers(0, groups, n).astype(np.int64)
+    alpha = ["a", "A", "b", "B", " ", "é", "É", "ss", "ß", "z"]
+    vals = ["".join(rng.choice(alpha, int(rng.integers(0, 4)))) for _ in range(n)]
+    scol = str_col(vals)
+    nul = (rng.random(n) < 0.2).astype(np.uint8)
+    _, dcol = _gen(rng, n, 13)
+    gci = STR | (3 << 24)
+    aggs = [(tfa.AGG_MIN, gci | tfa.NULLABLE), (tfa.AGG_MAX, STR | tfa.NULLABLE),
+            (tfa.AGG_FIRST_ROW, STR | tfa.NULLABLE), (tfa.AGG_MAX, 13)]
+    got, exp = _run(tfa, orc, ctx, dev, aggs, k, [scol, scol, scol, dcol], [nul, nul, nul, None], 3)
+    assert len(got) == len(exp)
+    assert got == exp

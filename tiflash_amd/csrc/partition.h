@@ -587,32 +587,19 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
             if (!spec) {
                 // the previous tile kept no row: skip ahead over tiles whose predicate keeps
                 // nothing — one predicate read and one barrier each, their runs written empty —
-                // to the next tile that keeps a row (FilterTransformAction.cpp:134-138)
-                // two tiles a round: both tiles' predicate words in flight together
+                // to the next tile that keeps a row (FilterTransformAction.cpp:134-138).  (Two
+                // tiles a round, their loads in flight together, cost the kept-row path 40 %:
+                // the partition kernel ran out of VGPRs, r05k)
                 while (tb < end) {
-                    Loaded pv[2][ST_MAXR];
+                    bool any = false;
 #pragma unroll
-                    for (int t = 0; t < 2; ++t)
-#pragma unroll
-                        for (int j = 0; j < ST_MAXR; ++j) {
-                            const uint32_t r = tb + (uint32_t)t * (uint32_t)g.TR + (uint32_t)j * ST_T + threadIdx.x;
-                            if (j < per && r < end) pv[t][j] = pred.load(r);
-                        }
-                    bool any[2] = {false, false};
-#pragma unroll
-                    for (int t = 0; t < 2; ++t)
-#pragma unroll
-                        for (int j = 0; j < ST_MAXR; ++j) {
-                            const uint32_t r = tb + (uint32_t)t * (uint32_t)g.TR + (uint32_t)j * ST_T + threadIdx.x;
-                            any[t] = any[t] || (j < per && r < end && pred.eval(pv[t][j]));
-                        }
-                    if (__syncthreads_or(any[0])) break;
-                    const bool keep1 = __syncthreads_or(any[1]) != 0;
+                    for (int j = 0; j < ST_MAXR; ++j) {
+                        const uint32_t r = tb + (uint32_t)j * ST_T + threadIdx.x;
+                        if (j < per && r < end) any = any || pred.eval(pred.load(r));
+                    }
+                    if (__syncthreads_or(any)) break;
                     const uint32_t tile = blockIdx.x * (uint32_t)g.tps + (tb - begin) / (uint32_t)g.TR;
                     for (uint32_t p = threadIdx.x; p < P; p += ST_T) g.tile_hist[(size_t)p * g.T + tile] = 0u;
-                    tb += (uint32_t)g.TR;
-                    if (keep1 || tb >= end) break;
-                    for (uint32_t p = threadIdx.x; p < P; p += ST_T) g.tile_hist[(size_t)p * g.T + tile + 1] = 0u;
                     tb += (uint32_t)g.TR;
                 }
                 if (tb >= end) break;
