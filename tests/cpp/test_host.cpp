@@ -2837,7 +2837,7 @@ int main(int argc, char **argv) {
             t.fn(ctx);
         } catch (const std::exception &e) {
             ++g_failures;
-            fprintf(stderr, "  EXCEPTION in %s: %s\n", t.name, e.what());
+            fprintf(stderr, "  EXCEPTION in %s [%s]: %s\n", t.name, g_current.c_str(), e.what());
         }
         ++ran;
         const bool ok = g_failures == before;

@@ -1015,6 +1015,11 @@ int run_partition_tiled(Ctx *ctx, const Sel &sel, const RowPred &pred, TiledGeom
 //           writes the runs out contiguously.
 // Bytes: 2 x (read + write) of the records, against 2 x (histogram read + read + write) for the
 // histogram + scatter form (run_two_pass).  Order inside a destination is unspecified.
+#ifdef TFG_EXP_RG_NT // profiling experiment: the regroup pass reads its records nontemporal
+constexpr bool RG_NT = true;
+#else
+constexpr bool RG_NT = false;
+#endif
 constexpr uint32_t RS_C = 64;
 constexpr int RS_T = 512, RS_RPT = 4, RS_BR = RS_T * RS_RPT, RS_TPC = 64;
 
@@ -1086,7 +1091,7 @@ __global__ void __launch_bounds__(RS_T) regroup_scatter_kernel(const uint64_t *r
                 if (tpre[mid] <= i) lo = mid;
                 else hi = mid;
             }
-            load_rec<NW>(rec, (size_t)(t0 + lo) * (uint32_t)TRS + tstart[lo] + (i - tpre[lo]), v[u]);
+            load_rec<NW, RG_NT>(rec, (size_t)(t0 + lo) * (uint32_t)TRS + tstart[lo] + (i - tpre[lo]), v[u]);
         }
     };
     uint64_t v[RS_RPT][NW];
