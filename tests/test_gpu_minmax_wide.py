@@ -418,3 +418,47 @@ def test_mixed_collators_and_decimal_blocks(tfa, ctx, dev, orc):
     got, exp = _run(tfa, orc, ctx, dev, aggs, k, [scol, scol, scol, dcol], [nul, nul, nul, None], 3)
     assert len(got) == len(exp)
     assert got == exp
+
+
+@pytest.mark.parametrize("which", [0, 1])
+def test_mixed_collators_two_phase_three_slices(tfa, ctx, dev, orc, which):
+    """the two-phase half of the C++ PlanAggregateWideMinMaxFirstRow: three slices, each through
+    its own partial aggregator (closed after its merge), into one final consume_partial; which=0:
+    min(s) general_ci, max(s), first_row(s), max(d); which=1: first_row(d), first_row(s)"""
+    rng = np.random.default_rng(191 + which)
+    n, groups = 60_000, 2_000
+    k = rng.integers(0, groups, n).astype(np.int64)
+    alpha = ["a", "A", "b", "B", " ", "é", "É", "ss", "ß", "z"]
+    vals = ["".join(rng.choice(alpha, int(rng.integers(0, 4)))) for _ in range(n)]
+    scol = str_col(vals)
+    nul = (rng.random(n) < 0.2).astype(np.uint8)
+    _, dcol = _gen(rng, n, 13)
+    gci = STR | (3 << 24)
+    if which == 0:
+        aggs = [(tfa.AGG_MIN, gci | tfa.NULLABLE), (tfa.AGG_MAX, STR | tfa.NULLABLE),
+                (tfa.AGG_FIRST_ROW, STR | tfa.NULLABLE), (tfa.AGG_MAX, 13)]
+        cols, nulls = [scol, scol, scol, dcol], [nul, nul, nul, None]
+    else:
+        aggs = [(tfa.AGG_FIRST_ROW, 13), (tfa.AGG_FIRST_ROW, STR | tfa.NULLABLE)]
+        cols, nulls = [dcol, scol], [None, nul]
+    types = [t for _, t in aggs]
+    ref = orc.Agg(orc.INT64, aggs)
+    ref.consume(k, [_orc_arg(c, t) for c, t in zip(cols, types)], arg_nulls=nulls)
+    exp = _orc(ref.result(), types)
+    fin = tfa.Aggregator(ctx, tfa.INT64, aggs)
+    cuts = np.linspace(0, n, 4).astype(int)
+    for b in range(3):
+        sl = slice(int(cuts[b]), int(cuts[b + 1]))
+        a = tfa.Aggregator(ctx, tfa.INT64, aggs)
+        a.consume(_t(k[sl], dev), [_arg(c, t, dev, sl) for c, t in zip(cols, types)],
+                  arg_nullmaps=[_t(x[sl], dev) if x is not None else None for x in nulls])
+        r = a.result()
+        # the Nullable results' null maps only (first_row always; min / max of a Nullable argument)
+        nm = [r["state_null"][i] if (types[i] & tfa.NULLABLE or aggs[i][0] == tfa.AGG_FIRST_ROW) else None
+              for i in range(len(aggs))]
+        fin.consume_partial(r["keys"], r["states"], state_nullmaps=nm)
+        a.close()
+    got = _dev(fin.result(), types)
+    fin.close()
+    bad = [(kk, got.get(kk), ev) for kk, ev in exp.items() if got.get(kk) != ev][:5]
+    assert len(got) == len(exp) and not bad, bad

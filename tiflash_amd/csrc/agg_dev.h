@@ -216,7 +216,7 @@ __device__ __forceinline__ void ref_combine(uint64_t *cell, uint64_t mine, const
 __device__ __forceinline__ void lds_add_i128(uint64_t *cell, uint64_t lo, uint64_t hi) {
     const uint64_t old = atomicAdd((unsigned long long *)&cell[0], (unsigned long long)lo);
     const uint64_t carry = (old + lo) < old ? 1ull : 0ull;
-    atomicAdd((unsigned long long *)&cell[1], (unsigned long long)(hi + carry));
+    if (hi + carry) atomicAdd((unsigned long long *)&cell[1], (unsigned long long)(hi + carry)); // 0: nothing to add
 }
 
 // Decimal256 sum state (AggregateFunctionSumData<Decimal256>, boost checked_int256_t): four
@@ -864,8 +864,10 @@ __device__ __forceinline__ void fast_add_rows(Table &T, const int (&cell)[R], co
         for (int u = 0; u < R; ++u) {
             if (CHECK && cell[u] < 0) continue;
             const uint64_t lo = v[u].v[i], carry = (old[u] + lo) < old[u] ? 1ull : 0ull;
-            atomicAdd((unsigned long long *)acc(i, cell[u]) + 1,
-                      (unsigned long long)(((int64_t)lo < 0 ? ~0ull : 0ull) + carry));
+            // the high word's addend (sign extension + carry) is 0 for most rows (a non-negative
+            // value without carry, a negative one with): those issue no second atomic
+            const uint64_t hi = ((int64_t)lo < 0 ? ~0ull : 0ull) + carry;
+            if (hi) atomicAdd((unsigned long long *)acc(i, cell[u]) + 1, (unsigned long long)hi);
         }
     }
 #pragma unroll

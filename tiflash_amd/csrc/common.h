@@ -34,7 +34,19 @@ bool failpoint(const char *name); // TFG_FAILPOINT=<name> injects TFG_ERR_FAULT_
     do {                                                   \
         if (!(cond)) return ::tfg::fail((code), __VA_ARGS__); \
     } while (0)
-#define TFG_LAUNCH_CHECK() TFG_HIP(hipGetLastError())
+// TFG_SYNC_CHECK=1 in the environment: every checked launch also waits for the device, so a kernel
+// fault is reported at the launch site that follows it (file:line) instead of at a later sync
+bool sync_check();
+#define TFG_STR2(x) #x
+#define TFG_STR(x) TFG_STR2(x)
+#define TFG_LAUNCH_CHECK()                                                                          \
+    do {                                                                                            \
+        TFG_HIP(hipGetLastError());                                                                 \
+        if (::tfg::sync_check()) {                                                                  \
+            hipError_t _s = hipDeviceSynchronize();                                                 \
+            if (_s != hipSuccess) return ::tfg::hip_fail(_s, "a kernel launched before " __FILE__ ":" TFG_STR(__LINE__)); \
+        }                                                                                           \
+    } while (0)
 
 // ------------------------------------------------------------------------------------------
 // context + scratch arena

@@ -36,6 +36,14 @@ int hip_fail(hipError_t e, const char *what) {
     return e == hipErrorOutOfMemory ? TFG_ERR_OOM : TFG_ERR_HIP;
 }
 
+bool sync_check() {
+    static const bool on = [] {
+        const char *v = getenv("TFG_SYNC_CHECK");
+        return v && *v && strcmp(v, "0") != 0;
+    }();
+    return on;
+}
+
 bool failpoint(const char *name) {
     const char *fp = getenv("TFG_FAILPOINT");
     return fp && strcmp(fp, name) == 0;

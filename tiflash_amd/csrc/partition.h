@@ -253,6 +253,72 @@ template <typename F> int with_pred(const RowPred &p, F &&f) {
     }
 }
 
+// Plain `T col Op scalar` predicates (4- or 8-byte T, no null map): a tile can be checked for
+// "keeps no row" with 16-byte vector loads of the column (part_scatter_staged_kernel's skip-ahead)
+template <typename P> struct PredVec {
+    static constexpr bool ok = false;
+    using E = uint64_t;
+};
+template <typename T> struct PredVec<PredT<2, T, false>> {
+    static constexpr bool ok = sizeof(T) == 4 || sizeof(T) == 8;
+    using E = T;
+};
+template <typename Pred> __device__ __forceinline__ bool pred_vec_aligned(const Pred &p, uint32_t begin) {
+    if constexpr (PredVec<Pred>::ok) {
+        using E = typename PredVec<Pred>::E;
+        return (((uintptr_t)p.col + (uintptr_t)begin * sizeof(E)) & 15) == 0;
+    } else {
+        return false;
+    }
+}
+// does any of the rows [tb, tb + per * ST_T) pass?  Thread t reads 16-byte words t, t + ST_T, ...
+// of the tile, all in flight together (ST_T: the staged scatter's workgroup size, below)
+template <int ST, int MAXR, typename Pred> __device__ __forceinline__ bool tile_any_vec(const Pred &p, uint32_t tb, int per) {
+    if constexpr (PredVec<Pred>::ok) {
+        using E = typename PredVec<Pred>::E;
+        constexpr int EPW = 16 / (int)sizeof(E);
+        constexpr int WMAX = (MAXR + EPW - 1) / EPW;
+        const uint4 *w = reinterpret_cast<const uint4 *>(reinterpret_cast<const E *>(p.col) + tb);
+        const uint32_t words = (uint32_t)per * (uint32_t)(ST / EPW);
+        // two words in flight a round (more spill the kernel's other VGPRs: it sits at 128)
+        constexpr int WB = 2;
+        bool any = false;
+#pragma unroll
+        for (int k0 = 0; k0 < WMAX; k0 += WB) {
+            uint4 x[WB];
+#pragma unroll
+            for (int k = 0; k < WB; ++k) {
+                const uint32_t i = (uint32_t)(k0 + k) * ST + threadIdx.x;
+                if (k0 + k < WMAX && i < words) x[k] = w[i];
+            }
+#pragma unroll
+            for (int k = 0; k < WB; ++k) {
+                if (k0 + k >= WMAX || (uint32_t)(k0 + k) * ST + threadIdx.x >= words) continue;
+                uint64_t b[4];
+                int nb;
+                if constexpr (sizeof(E) == 8) {
+                    b[0] = (uint64_t)x[k].x | ((uint64_t)x[k].y << 32);
+                    b[1] = (uint64_t)x[k].z | ((uint64_t)x[k].w << 32);
+                    nb = 2;
+                } else {
+                    b[0] = x[k].x, b[1] = x[k].y, b[2] = x[k].z, b[3] = x[k].w;
+                    nb = 4;
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (q >= nb) break;
+                    Loaded l{b[q], 0u};
+                    any |= p.eval(l);
+                }
+            }
+            if (any) break;
+        }
+        return any;
+    } else {
+        return true;
+    }
+}
+
 struct PartLayout {
     int64_t n;
     int64_t seg;   // rows per segment (multiple of PT)
@@ -582,6 +648,13 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
     if (TILED && g.fine_bits)
         for (uint32_t p = threadIdx.x; p < (P << g.fine_bits); p += ST_T) fh[p] = 0;
     bool spec = true; // the previous tile kept a row (workgroup-uniform): keys load with the predicate
+    // all-false tiles of a plain column predicate are checked with vector loads (16-byte aligned
+    // column and segment start)
+#ifdef TFG_EXP_SKIPVEC
+    const bool skip_vec = TILED && PredVec<Pred>::ok && pred_vec_aligned(pred, begin);
+#else
+    constexpr bool skip_vec = false;
+#endif
     for (uint32_t tb = begin; tb < end; tb += (uint32_t)g.TR) {
         if constexpr (TILED) {
             if (!spec) {
@@ -592,10 +665,17 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
                 // the partition kernel ran out of VGPRs, r05k)
                 while (tb < end) {
                     bool any = false;
+                    if (skip_vec && tb + (uint32_t)g.TR <= end) {
+                        // a whole tile of a plain `T col Op scalar` predicate: its column words
+                        // read as 16-byte vectors, all of a thread's in flight at once (one HBM
+                        // round trip a tile instead of one a row)
+                        any = tile_any_vec<ST_T, ST_MAXR>(pred, tb, per);
+                    } else {
 #pragma unroll
-                    for (int j = 0; j < ST_MAXR; ++j) {
-                        const uint32_t r = tb + (uint32_t)j * ST_T + threadIdx.x;
-                        if (j < per && r < end) any = any || pred.eval(pred.load(r));
+                        for (int j = 0; j < ST_MAXR; ++j) {
+                            const uint32_t r = tb + (uint32_t)j * ST_T + threadIdx.x;
+                            if (j < per && r < end) any = any || pred.eval(pred.load(r));
+                        }
                     }
                     if (__syncthreads_or(any)) break;
                     const uint32_t tile = blockIdx.x * (uint32_t)g.tps + (tb - begin) / (uint32_t)g.TR;
