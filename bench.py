@@ -367,14 +367,16 @@ def c5_leg(args, ctx, dev, world, rank):
     part = tfa.KeysAggregator(ctx, [tfa.STRING], aggs, expected_groups=eg, bucket_bits=args.c5_bucket_bits)
     fin = tfa.KeysAggregator(ctx, [tfa.STRING], aggs, expected_groups=eg, bucket_bits=args.c5_bucket_bits) if world > 1 else None
 
+    hint = min(G, n)  # the result's buffers before its count is read (<= G groups)
+
     def step():
         part.reset()
         part.consume([(chars, offs)], [v, None])
         if world == 1:
-            return part.result()
+            return part.result(capacity_hint=hint)
         fin.reset()
         two_phase_merge_keys(ctx, part, fin)
-        return fin.result()
+        return fin.result(capacity_hint=hint)
 
     for _ in range(args.warmup):
         step()

@@ -55,3 +55,46 @@ def test_result_capacity_hint_first_row(tfa, ctx, dev):
     assert keys.shape[0] == np.unique(k.cpu().numpy()).shape[0]
     assert np.array_equal(fr, (keys % 1000).astype(np.int16))
     assert not r["state_null"][0].cpu().numpy().any()
+
+
+@pytest.mark.parametrize("hint_scale", [0.5, 1.0, 2.0])
+def test_keys_result_capacity_hint_string(tfa, ctx, dev, hint_scale):
+    """the packed String-key result with a capacity hint (key lengths, scan and unpack over the
+    hinted slots, count read on the device) = the exact call; a hint below the count falls back"""
+    g = torch.Generator(device=dev)
+    g.manual_seed(7)
+    n, groups = 2_000_000, 150_000
+    ids = torch.randint(0, groups, (n,), device=dev, generator=g)
+    width = 1 + (ids % 7)  # keys of 2-8 bytes + '\0'
+    lens = (width + 2).to(torch.int64)
+    offs = torch.cumsum(lens, 0)
+    chars = torch.zeros(int(offs[-1].item()), dtype=torch.uint8, device=dev)
+    starts = offs - lens
+    x = ids.clone()
+    for j in range(8):
+        sel = width > j
+        chars[(starts + 1 + j)[sel]] = (48 + x % 10)[sel].to(torch.uint8)
+        x = x // 10
+    chars[starts] = ord("k")
+    v = torch.randint(0, 1 << 30, (n,), device=dev, generator=g)
+    aggs = [(tfa.AGG_SUM, tfa.INT64), (tfa.AGG_COUNT_ALL, 0)]
+    a = tfa.KeysAggregator(ctx, [tfa.STRING], aggs, expected_groups=groups)
+
+    def table(res):
+        ch, of = res["keys"][0]
+        ch, of = ch.cpu().numpy(), of.cpu().numpy()
+        s = res["states"][0].view(torch.int64).cpu().numpy()
+        c = res["states"][1].view(torch.int64).cpu().numpy()
+        out = {}
+        for i in range(len(of)):
+            out[bytes(ch[(of[i - 1] if i else 0):of[i]])] = (int(s[i]), int(c[i]))
+        return out
+
+    a.consume([(chars, offs)], [v, None])
+    exact = table(a.result())
+    a.reset()
+    a.consume([(chars, offs)], [v, None])
+    hinted = table(a.result(capacity_hint=max(1, int(len(exact) * hint_scale))))
+    a.close()
+    assert hinted == exact
+    assert sum(c for _, c in exact.values()) == n

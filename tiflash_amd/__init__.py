@@ -610,13 +610,16 @@ class KeysAggregator(Aggregator):
         """-> dict as Aggregator.result() with keys = (G, 2) int64 packed keys."""
         return Aggregator.result(self, device)
 
-    def result(self, device=None, chars_capacity=None):
+    def result(self, device=None, chars_capacity=None, capacity_hint: Optional[int] = None):
         """-> dict(keys=[col or (chars, offsets)], key_null=[uint8], states=[...], state_null=[...]).
         String keys of the serialized method may need more than 16 bytes a group: the call is
-        repeated with the size TFG_ERR_CAPACITY reports."""
+        repeated with the size TFG_ERR_CAPACITY reports.  capacity_hint: as Aggregator.result —
+        buffers of that many groups (16 chars bytes a group) handed over before the count is read;
+        a count above it falls back to the exact call."""
         import torch
         dev = device or torch.device("cuda", self.ctx.device)
-        g = self.size()
+        hinted = bool(capacity_hint) and chars_capacity is None
+        g = int(capacity_hint) if hinted else self.size()
         ccap = max(16 * g, 1) if chars_capacity is None else max(chars_capacity, 1)
         cols, offs, nulls = [], [], []
         for t in self.key_types:
@@ -633,6 +636,15 @@ class KeysAggregator(Aggregator):
         rc = lib().tfg_agg_result_keys(self.h, _ptr_array(cols), _ptr_array(offs), _ptr_array(nulls), sarr,
                                        _ptr_array(snulls), ctypes.c_uint64(g), ctypes.c_uint64(ccap),
                                        ctypes.byref(cnt), ctypes.byref(chars))
+        if hinted:
+            if rc == TFG_ERR_CAPACITY and cnt.value > g:
+                return self.result(device)
+            check(rc)
+            n = cnt.value
+            cut = lambda t: (t[0], t[1][:n]) if isinstance(t, tuple) else t[:n]
+            keys = [(c[:chars.value], o[:n]) if t == STRING else c[:n] for t, c, o in zip(self.key_types, cols, offs)]
+            return {"keys": keys, "key_null": [x[:n] for x in nulls], "states": [cut(x) for x in states],
+                    "state_null": [x[:n] for x in snulls]}
         if rc == TFG_ERR_CAPACITY and chars.value > ccap:
             return self.result(device, chars.value)
         check(rc)

@@ -655,9 +655,12 @@ __global__ void pack_keys_kernel(KeyPack kp, int64_t n, uint4 *out, unsigned *er
 }
 
 // packed String keys -> lengths + 1 (the '\0' each ColumnString row ends with)
-__global__ void wide_str_len_kernel(const uint4 *keys, uint64_t n, uint64_t *len1) {
+// n_dev (optional): the group count on the device, <= n slots (a result written before its count
+// is read): slots past it get length 0
+__global__ void wide_str_len_kernel(const uint4 *keys, uint64_t n, uint64_t *len1, const uint64_t *n_dev) {
+    const uint64_t G = n_dev ? min(*n_dev, n) : n;
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (uint64_t)gridDim.x * blockDim.x)
-        len1[g] = ((keys[g].w >> 24) & 0x7Fu) + 1;
+        len1[g] = g < G ? ((keys[g].w >> 24) & 0x7Fu) + 1 : 0;
 }
 
 // packed keys -> the key columns of the result Block (convertToBlockImplFinal's insertKeyIntoColumns)
@@ -666,7 +669,9 @@ struct KeyOut {
     uint64_t *offsets;        // String: end offsets
     uint8_t *nullmap[4];
 };
-__global__ void unpack_keys_kernel(KeyPack kp, const uint4 *keys, const uint64_t *start, uint64_t n, KeyOut ko) {
+__global__ void unpack_keys_kernel(KeyPack kp, const uint4 *keys, const uint64_t *start, uint64_t n, KeyOut ko,
+                                   const uint64_t *n_dev) {
+    if (n_dev) n = min(*n_dev, n); // the count on the device (wide_str_len_kernel)
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (uint64_t)gridDim.x * blockDim.x) {
         const uint4 q = keys[g];
         const uint64_t w[2] = {((uint64_t)q.y << 32) | q.x, ((uint64_t)q.w << 32) | q.z};
@@ -723,11 +728,19 @@ __device__ __forceinline__ const RefCol &ref_pick(uint64_t ref, uint64_t n0, con
     idx = ref > n0 ? ref - n0 - 1 : ref - 1;
     return ref > n0 ? s1 : s0;
 }
+// a state reference must name one of the n0 + n1 candidates: anything else (never dereferenced)
+// sets the aggregator's error flag and reads as "no value"
+__device__ __forceinline__ bool ref_ok(uint64_t ref, uint64_t lim, unsigned *err) {
+    if (ref <= lim) return true;
+    if (err) atomicOr(err, 2u);
+    return false;
+}
 
-__global__ void ref_store_fixed_kernel(uint64_t *acc, uint64_t G, uint64_t n0, int w, RefCol s0, RefCol s1,
-                                       uint8_t *val, uint8_t *nul) {
+__global__ void ref_store_fixed_kernel(uint64_t *acc, uint64_t G, uint64_t n0, uint64_t n1, unsigned *err, int w,
+                                       RefCol s0, RefCol s1, uint8_t *val, uint8_t *nul) {
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < G; g += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t ref = acc[g];
+        uint64_t ref = acc[g];
+        if (!ref_ok(ref, n0 + n1, err)) ref = acc[g] = 0;
         uint64_t q[4] = {0, 0, 0, 0};
         uint8_t isnull = 1;
         if (ref) {
@@ -755,9 +768,11 @@ __global__ void ref_store_fixed_kernel(uint64_t *acc, uint64_t G, uint64_t n0, i
 }
 
 // String store: bytes of each group's value with its '\0' (NULL / absent: the empty String)
-__global__ void ref_store_len_kernel(const uint64_t *acc, uint64_t G, uint64_t n0, RefCol s0, RefCol s1, uint64_t *len) {
+__global__ void ref_store_len_kernel(const uint64_t *acc, uint64_t G, uint64_t n0, uint64_t n1, unsigned *err, RefCol s0,
+                                     RefCol s1, uint64_t *len) {
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < G; g += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t ref = acc[g];
+        uint64_t ref = acc[g];
+        if (!ref_ok(ref, n0 + n1, err)) ref = 0;
         uint64_t l = 1;
         if (ref) {
             uint64_t idx;
@@ -767,10 +782,11 @@ __global__ void ref_store_len_kernel(const uint64_t *acc, uint64_t G, uint64_t n
         len[g] = l;
     }
 }
-__global__ void ref_store_str_kernel(uint64_t *acc, uint64_t G, uint64_t n0, RefCol s0, RefCol s1, const uint64_t *start,
-                                     uint8_t *chars, uint8_t *nul) {
+__global__ void ref_store_str_kernel(uint64_t *acc, uint64_t G, uint64_t n0, uint64_t n1, RefCol s0, RefCol s1,
+                                     const uint64_t *start, uint8_t *chars, uint8_t *nul) {
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < G; g += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t ref = acc[g];
+        uint64_t ref = acc[g];
+        if (ref > n0 + n1) ref = acc[g] = 0; // flagged by ref_store_len_kernel
         uint8_t *o = chars + start[g];
         uint8_t isnull = 1;
         if (ref) {
@@ -1436,6 +1452,8 @@ int check_overflow(tfg_agg *a) {
     TFG_HIP(hipStreamSynchronize(a->ctx->stream));
     if (!f) return TFG_OK;
     TFG_HIP(hipMemsetAsync(a->S.ovf, 0, sizeof f, a->ctx->stream));
+    if (f & 2) // RefSrc::err: a row reference outside its candidates (never dereferenced)
+        return fail(TFG_ERR_LOGICAL, "row-reference aggregate state out of range (internal error)");
     return fail(TFG_ERR_OVERFLOW, "Decimal256 sum overflow (DECIMAL_OVERFLOW: the sum left Int256)");
 }
 
@@ -1471,6 +1489,8 @@ int ref_setup(tfg_agg *a, const RefIn *in, RefCall &rc) {
         R = RefSrc{};
         const RefStore &st = a->store[i];
         R.n0 = st.n;
+        R.n1 = in[i].n;
+        R.err = a->S.ovf;
         const int t = a->S.src_type[i];
         R.v[0] = st.val;
         R.v[1] = in[i].val;
@@ -1516,8 +1536,8 @@ int ref_rebuild(tfg_agg *a, const RefIn *in) {
             if (int rc = grow_buf(ctx, (void **)&nw.val, &nw.val_cap, G * w)) return rc;
             if (G) {
                 ProfScope _ps(ctx, "agg.ref_store");
-                hipLaunchKernelGGL(ref_store_fixed_kernel, dim3(grid), dim3(256), 0, ctx->stream, acc, G, old.n, w, s0, s1,
-                                   nw.val, nw.nul);
+                hipLaunchKernelGGL(ref_store_fixed_kernel, dim3(grid), dim3(256), 0, ctx->stream, acc, G, old.n, in[i].n,
+                                   a->S.ovf, w, s0, s1, nw.val, nw.nul);
                 TFG_LAUNCH_CHECK();
             }
         } else {
@@ -1526,7 +1546,7 @@ int ref_rebuild(tfg_agg *a, const RefIn *in) {
                 if (int rc = grow_buf(ctx, &a->ref_tmp[0], &a->ref_tmp_cap[0], G * 8)) return rc;
                 if (int rc = grow_buf(ctx, &a->ref_tmp[1], &a->ref_tmp_cap[1], scan_tmp_bytes((int64_t)G) + 256)) return rc;
                 hipLaunchKernelGGL(ref_store_len_kernel, dim3(grid), dim3(256), 0, ctx->stream, (const uint64_t *)acc, G,
-                                   old.n, s0, s1, (uint64_t *)a->ref_tmp[0]);
+                                   old.n, in[i].n, a->S.ovf, s0, s1, (uint64_t *)a->ref_tmp[0]);
                 TFG_LAUNCH_CHECK();
                 if (int rc = exclusive_scan_u64(ctx, (const uint64_t *)a->ref_tmp[0], nw.scan, (int64_t)G, a->ref_tmp[1]))
                     return rc;
@@ -1537,8 +1557,8 @@ int ref_rebuild(tfg_agg *a, const RefIn *in) {
             if (int rc = grow_buf(ctx, (void **)&nw.val, &nw.val_cap, total)) return rc;
             if (G) {
                 ProfScope _ps(ctx, "agg.ref_store");
-                hipLaunchKernelGGL(ref_store_str_kernel, dim3(grid), dim3(256), 0, ctx->stream, acc, G, old.n, s0, s1,
-                                   (const uint64_t *)nw.scan, nw.val, nw.nul);
+                hipLaunchKernelGGL(ref_store_str_kernel, dim3(grid), dim3(256), 0, ctx->stream, acc, G, old.n, in[i].n, s0,
+                                   s1, (const uint64_t *)nw.scan, nw.val, nw.nul);
                 TFG_LAUNCH_CHECK();
             }
         }
@@ -1904,7 +1924,7 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
     S.lds_bytes = off + (int)sizeof(Ctrl) + 16;
     S.ovf = nullptr;
     for (int i = 0; i < n_aggs; ++i)
-        if (S.acc[i] == ACC_I256 && !S.ovf) {
+        if ((S.acc[i] == ACC_I256 || S.acc[i] == ACC_REF) && !S.ovf) { // Decimal256 overflow / bad reference flags
             if (hipMalloc((void **)&S.ovf, sizeof(unsigned)) != hipSuccess ||
                 hipMemsetAsync(S.ovf, 0, sizeof(unsigned), ctx->stream) != hipSuccess) {
                 if (S.ovf) (void)hipFree(S.ovf);
@@ -2106,30 +2126,45 @@ int tfg_agg_result_type(tfg_agg *a, int i, int *out_type, int *out_width) {
     return TFG_OK;
 }
 
+// a result call that may run before the group count is read: a tiled consume's pending groups,
+// count unknown, no value stores (their rebuild needs the count), room for some groups
+static bool result_early(const tfg_agg *a, uint64_t capacity) {
+    return a->pending && !a->pend_known && !a->has_ref && capacity > 0;
+}
+
+// the pending groups' result rows into `capacity` slots (rows past it dropped); the count stays on
+// the device at pend_off()[B]
+static int result_pending_launch(tfg_agg *a, void *out_keys, uint8_t *out_key_nullmap, void *const *out_states,
+                                 uint8_t *const *out_state_nullmaps, uint64_t capacity) {
+    ResultPtrs rp{};
+    for (int i = 0; i < a->S.n_aggs; ++i) {
+        rp.state[i] = out_states ? out_states[i] : nullptr;
+        rp.state_null[i] = out_state_nullmaps ? out_state_nullmaps[i] : nullptr;
+        rp.nullable[i] = a->arg_nullable[i] || a->S.kind[i] == TFG_AGG_FIRST_ROW;
+    }
+    if (int rc = pend_scan(a)) return rc;
+    {
+        ProfScope _ps(a->ctx, "agg.result");
+        hipLaunchKernelGGL(agg_result_buckets_kernel, dim3(a->B), dim3(256), 0, a->ctx->stream, a->S, a->pend,
+                           (const uint64_t *)a->pend_cnt(), (const uint64_t *)a->pend_base(),
+                           (const uint64_t *)a->pend_off(), a->S.key_width, out_keys, out_key_nullmap, rp, capacity);
+    }
+    TFG_LAUNCH_CHECK();
+    return TFG_OK;
+}
+
 int tfg_agg_result(tfg_agg *a, void *out_keys, uint8_t *out_key_nullmap, void *const *out_states,
                    uint8_t *const *out_state_nullmaps, uint64_t capacity, uint64_t *out_groups_host) {
     TFG_CHECK(a, TFG_ERR_INVALID_ARG, "agg is null");
     TFG_CHECK(!a->sdict, TFG_ERR_NOT_IMPLEMENTED,
               "serialized GROUP BY keys have no packed form: read them with tfg_agg_result_keys");
-    if (a->pending && !a->pend_known && !a->has_ref && capacity > 0) {
+    if (result_early(a, capacity)) {
         // groups of a tiled consume, count not read yet: the result is written first (groups
         // past `capacity` dropped) and the count read after it, so no host round trip idles the
         // device between the consume and the result
-        ResultPtrs rp{};
-        for (int i = 0; i < a->S.n_aggs; ++i) {
-            rp.state[i] = out_states ? out_states[i] : nullptr;
-            rp.state_null[i] = out_state_nullmaps ? out_state_nullmaps[i] : nullptr;
-            rp.nullable[i] = a->arg_nullable[i] || a->S.kind[i] == TFG_AGG_FIRST_ROW;
-        }
         if (int rc = set_device(a->ctx)) return rc;
-        if (int rc = pend_scan(a)) return rc;
-        {
-            ProfScope _ps(a->ctx, "agg.result");
-            hipLaunchKernelGGL(agg_result_buckets_kernel, dim3(a->B), dim3(256), 0, a->ctx->stream, a->S, a->pend,
-                               (const uint64_t *)a->pend_cnt(), (const uint64_t *)a->pend_base(),
-                               (const uint64_t *)a->pend_off(), a->S.key_width, out_keys, out_key_nullmap, rp, capacity);
-        }
-        TFG_LAUNCH_CHECK();
+        if (int rc = result_pending_launch(a, out_keys, out_key_nullmap, out_states, out_state_nullmaps, capacity))
+            return rc;
         if (int rc = read_back_u64(a->ctx, a->pend_off() + a->B, &a->pend_total, 1)) return rc;
         a->pend_known = true;
         if (out_groups_host) *out_groups_host = a->pend_total;
@@ -2432,18 +2467,33 @@ int tfg_agg_result_keys(tfg_agg *a, void *const *out_key_cols, uint64_t *const *
         return tfg_agg_result(a, out_key_cols ? out_key_cols[0] : nullptr, out_key_nullmaps ? out_key_nullmaps[0] : nullptr,
                               out_states, out_state_nullmaps, capacity, out_groups_host);
     }
-    uint64_t G = 0;
-    if (int rc = tfg_agg_size(a, &G)) return rc;
-    if (out_groups_host) *out_groups_host = G;
-    if (out_chars_host) *out_chars_host = 0;
-    if (G > capacity)
-        return fail(TFG_ERR_CAPACITY, "result needs %llu groups, capacity %llu", (unsigned long long)G,
-                    (unsigned long long)capacity);
-    if (G == 0) return TFG_OK;
-    if (int rc = set_device(a->ctx)) return rc;
-    if (int rc = a->ensure_pack(G)) return rc;
-    if (int rc = tfg_agg_result(a, a->pack_buf, nullptr, out_states, out_state_nullmaps, capacity, nullptr)) return rc;
     Ctx *ctx = a->ctx;
+    // before the group count is read (tfg_agg_result's early path): packed keys, key lengths,
+    // their scan and the unpack run over `capacity` slots with the count read on the device, and
+    // one host round trip at the end reads the count and the chars total.  String keys need
+    // 16 bytes of chars a slot for it (a packed String key holds <= 15 bytes + '\0')
+    const bool early = result_early(a, capacity) && (a->kp.kind != WK_STRING || chars_capacity >= 16 * capacity);
+    uint64_t G = 0;
+    const uint64_t *g_dev = nullptr;
+    if (early) {
+        if (int rc = set_device(ctx)) return rc;
+        if (int rc = a->ensure_pack(capacity)) return rc;
+        if (int rc = result_pending_launch(a, a->pack_buf, nullptr, out_states, out_state_nullmaps, capacity)) return rc;
+        G = capacity;
+        g_dev = a->pend_off() + a->B;
+    } else {
+        if (int rc = tfg_agg_size(a, &G)) return rc;
+        if (out_groups_host) *out_groups_host = G;
+        if (out_chars_host) *out_chars_host = 0;
+        if (G > capacity)
+            return fail(TFG_ERR_CAPACITY, "result needs %llu groups, capacity %llu", (unsigned long long)G,
+                        (unsigned long long)capacity);
+        if (G == 0) return TFG_OK;
+        if (int rc = set_device(ctx)) return rc;
+        if (int rc = a->ensure_pack(G)) return rc;
+        if (int rc = tfg_agg_result(a, a->pack_buf, nullptr, out_states, out_state_nullmaps, capacity, nullptr))
+            return rc;
+    }
     KeyOut ko{};
     uint64_t *start = nullptr;
     bool chars_known = true;
@@ -2457,12 +2507,13 @@ int tfg_agg_result_keys(tfg_agg *a, void *const *out_key_cols, uint64_t *const *
         if (int rc = scratch_get(ctx, cv.off, &sp)) return rc;
         uint64_t *len1 = (uint64_t *)((char *)sp + o_len);
         start = (uint64_t *)((char *)sp + o_start);
-        hipLaunchKernelGGL(wide_str_len_kernel, dim3(grid), dim3(256), 0, ctx->stream, (const uint4 *)a->pack_buf, G, len1);
+        hipLaunchKernelGGL(wide_str_len_kernel, dim3(grid), dim3(256), 0, ctx->stream, (const uint4 *)a->pack_buf, G, len1,
+                           g_dev);
         TFG_LAUNCH_CHECK();
         if (int rc = exclusive_scan_u64(ctx, len1, start, (int64_t)G, (char *)sp + o_tmp)) return rc;
         // a packed String key holds <= 15 bytes + '\0': with room for 16 a group the capacity needs
         // no check, and the total is read after the unpack is queued (no idle gap before it)
-        chars_known = chars_capacity < 16 * G;
+        chars_known = !early && chars_capacity < 16 * G;
         if (chars_known) {
             uint64_t chars = 0;
             if (int rc = read_back_u64(ctx, start + G, &chars, 1)) return rc;
@@ -2480,9 +2531,23 @@ int tfg_agg_result_keys(tfg_agg *a, void *const *out_key_cols, uint64_t *const *
     {
         ProfScope _ps(ctx, "agg.unpack_keys");
         hipLaunchKernelGGL(unpack_keys_kernel, dim3(grid), dim3(256), 0, ctx->stream, a->kp,
-                           (const uint4 *)a->pack_buf, (const uint64_t *)start, G, ko);
+                           (const uint4 *)a->pack_buf, (const uint64_t *)start, G, ko, g_dev);
     }
     TFG_LAUNCH_CHECK();
+    if (early) { // the count and the chars total in one round trip
+        uint64_t cnt = 0, chars = 0;
+        TFG_HIP(hipMemcpyAsync(&cnt, g_dev, 8, hipMemcpyDeviceToHost, ctx->stream));
+        if (start) TFG_HIP(hipMemcpyAsync(&chars, start + G, 8, hipMemcpyDeviceToHost, ctx->stream));
+        TFG_HIP(hipStreamSynchronize(ctx->stream));
+        a->pend_total = cnt;
+        a->pend_known = true;
+        if (out_groups_host) *out_groups_host = cnt;
+        if (out_chars_host) *out_chars_host = chars;
+        if (cnt > capacity)
+            return fail(TFG_ERR_CAPACITY, "result needs %llu groups, capacity %llu (the first %llu written)",
+                        (unsigned long long)cnt, (unsigned long long)capacity, (unsigned long long)capacity);
+        return TFG_OK;
+    }
     if (!chars_known && out_chars_host)
         if (int rc = read_back_u64(ctx, start + G, out_chars_host, 1)) return rc;
     return TFG_OK;

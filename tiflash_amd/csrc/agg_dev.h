@@ -37,7 +37,10 @@ struct RefSrc {
     const uint8_t *v[2];  // [0] store, [1] consumed column: fixed-width values, or String compare bytes
     const uint64_t *o[2]; // String compare bytes: end offsets (row i = [o[i - 1], o[i]) with o[-1] = 0)
     uint64_t n0;          // store entries
+    uint64_t n1;          // consumed rows (references n0 + 1 .. n0 + n1)
     int width;            // fixed: 16 / 32 (signed little-endian limbs compared); 0 = String bytes
+    unsigned *err;        // |= 2 on a reference outside 1 .. n0 + n1 or a row without its '\0' (never
+                          // dereferenced; the call then fails with TFG_ERR_LOGICAL)
 };
 
 struct AggSpec {
@@ -173,6 +176,10 @@ __host__ __device__ __forceinline__ uint64_t ord_dec(int kind, int type, uint64_
 // three-way compare of candidates a, b (>= 1) of a RefSrc: signed limbs, or bytes then length
 // (memcmp order of the compare bytes: raw rows, or collator sort keys)
 __device__ __forceinline__ int ref_cmp(const RefSrc &R, uint64_t a, uint64_t b) {
+    if (a - 1 >= R.n0 + R.n1 || b - 1 >= R.n0 + R.n1) { // 0 wraps: out of range too
+        if (R.err) atomicOr(R.err, 2u);
+        return 0;
+    }
     const int sa = a > R.n0, sb = b > R.n0;
     const uint64_t ia = sa ? a - R.n0 - 1 : a - 1, ib = sb ? b - R.n0 - 1 : b - 1;
     if (R.width) {
@@ -187,6 +194,10 @@ __device__ __forceinline__ int ref_cmp(const RefSrc &R, uint64_t a, uint64_t b) 
     }
     const uint64_t a0 = ia ? R.o[sa][ia - 1] : 0, a1 = R.o[sa][ia] - 1; // the row's '\0' excluded:
     const uint64_t b0 = ib ? R.o[sb][ib - 1] : 0, b1 = R.o[sb][ib] - 1; // both rows end with it
+    if (a1 + 1 <= a0 || b1 + 1 <= b0) { // a row of no bytes (no '\0'): malformed offsets
+        if (R.err) atomicOr(R.err, 2u);
+        return 0;
+    }
     const uint8_t *pa = R.v[sa] + a0, *pb = R.v[sb] + b0;
     const uint64_t la = a1 - a0, lb = b1 - b0, m = la < lb ? la : lb;
     for (uint64_t k = 0; k < m; ++k)

@@ -341,7 +341,7 @@ static int arith_wide(Ctx *ctx, int op, int a_type, const void *a, int a_is_cons
     const int flags = (res_type == TFG_DECIMAL256 && (a_type == TFG_DECIMAL256 || b_type == TFG_DECIMAL256)) ? 1 : 0;
     if (n <= 0) return TFG_OK;
     unsigned *flag = nullptr;
-    TFG_HIP(hipMallocAsync((void **)&flag, sizeof(unsigned), ctx->stream));
+    TFG_HIP(hipMalloc((void **)&flag, sizeof(unsigned)));
     TFG_HIP(hipMemsetAsync(flag, 0, sizeof(unsigned), ctx->stream));
     {
         ProfScope _ps(ctx, "arith.wide");
@@ -351,8 +351,8 @@ static int arith_wide(Ctx *ctx, int op, int a_type, const void *a, int a_is_cons
     TFG_LAUNCH_CHECK();
     unsigned ov = 0;
     TFG_HIP(hipMemcpyAsync(&ov, flag, sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
-    TFG_HIP(hipFreeAsync(flag, ctx->stream));
     TFG_HIP(hipStreamSynchronize(ctx->stream));
+    TFG_HIP(hipFree(flag));
     TFG_CHECK(!ov, TFG_ERR_OVERFLOW, "Decimal math overflow");
     return TFG_OK;
 }

@@ -233,10 +233,13 @@ int uca_ready(Ctx *ctx) {
 
 } // namespace
 
+// plain device allocations, freed once the stream is done with them (not the stream-ordered
+// pool: the C++ two-phase planner case faulted intermittently with pool-backed sort keys)
 CollatedStrings::~CollatedStrings() {
-    if (!ctx) return;
-    if (chars) (void)hipFreeAsync(chars, ctx->stream);
-    if (scan) (void)hipFreeAsync(scan, ctx->stream);
+    if (!ctx || (!chars && !scan)) return;
+    (void)hipStreamSynchronize(ctx->stream);
+    if (chars) (void)hipFree(chars);
+    if (scan) (void)hipFree(scan);
 }
 
 int collate_strings(Ctx *ctx, int collator, const uint8_t *chars, const uint64_t *offsets, const uint8_t *nullmap,
@@ -249,15 +252,29 @@ int collate_strings(Ctx *ctx, int collator, const uint8_t *chars, const uint64_t
     TFG_CHECK(n >= 0 && n <= ((int64_t)1 << 26), TFG_ERR_INVALID_ARG, "collated column of %lld rows", (long long)n);
     out.ctx = ctx;
     out.rows = n;
-    TFG_HIP(hipMallocAsync((void **)&out.scan, (size_t)(n + 1) * 8, ctx->stream));
+    TFG_HIP(hipMalloc((void **)&out.scan, (size_t)(n + 1) * 8));
     if (n == 0) {
         TFG_HIP(hipMemsetAsync(out.scan, 0, 8, ctx->stream));
-        TFG_HIP(hipMallocAsync((void **)&out.chars, 16, ctx->stream));
+        TFG_HIP(hipMalloc((void **)&out.chars, 16));
         return TFG_OK;
     }
     TFG_CHECK(chars && offsets, TFG_ERR_INVALID_ARG, "String column needs its chars and offsets");
+    // the lengths and the scan's work space: freed after the total's read-back (their users done)
+    struct Tmp { // error paths: wait for the stream, then free
+        hipStream_t st;
+        void *p[2];
+        void release() {
+            for (void *&q : p)
+                if (q) (void)hipFree(q), q = nullptr;
+        }
+        ~Tmp() {
+            if (p[0] || p[1]) (void)hipStreamSynchronize(st);
+            release();
+        }
+    } tm{ctx->stream, {nullptr, nullptr}};
     uint64_t *len = nullptr;
-    TFG_HIP(hipMallocAsync((void **)&len, (size_t)n * 8, ctx->stream));
+    TFG_HIP(hipMalloc((void **)&len, (size_t)n * 8));
+    tm.p[0] = len;
     const unsigned grid = stream_grid(n, 256, 4096);
     if (!uca)
         hipLaunchKernelGGL(gci_len_kernel, dim3(grid), dim3(256), 0, ctx->stream, chars, offsets, nullmap, sel32, sel64,
@@ -270,11 +287,13 @@ int collate_strings(Ctx *ctx, int collator, const uint8_t *chars, const uint64_t
                            sel64, n, whole, len);
     TFG_LAUNCH_CHECK();
     void *tmp = nullptr;
-    TFG_HIP(hipMallocAsync(&tmp, scan_tmp_bytes(n) + 256, ctx->stream));
+    TFG_HIP(hipMalloc(&tmp, scan_tmp_bytes(n) + 256));
+    tm.p[1] = tmp;
     if (int rc = exclusive_scan_u64(ctx, len, out.scan, n, tmp)) return rc;
     uint64_t total = 0;
-    if (int rc = read_back_u64(ctx, out.scan + n, &total, 1)) return rc;
-    TFG_HIP(hipMallocAsync((void **)&out.chars, total + 16, ctx->stream));
+    if (int rc = read_back_u64(ctx, out.scan + n, &total, 1)) return rc; // synchronizes the stream
+    tm.release(); // their last users (the length kernel, the scan) are done
+    TFG_HIP(hipMalloc((void **)&out.chars, total + 16));
     if (!uca)
         hipLaunchKernelGGL(gci_write_kernel, dim3(grid), dim3(256), 0, ctx->stream, chars, offsets, nullmap, sel32, sel64,
                            n, whole, out.scan, out.chars);
@@ -285,8 +304,6 @@ int collate_strings(Ctx *ctx, int collator, const uint8_t *chars, const uint64_t
         hipLaunchKernelGGL(uca_write_kernel<false>, dim3(grid), dim3(256), 0, ctx->stream, chars, offsets, nullmap, sel32,
                            sel64, n, whole, out.scan, out.chars);
     TFG_LAUNCH_CHECK();
-    TFG_HIP(hipFreeAsync(len, ctx->stream));
-    TFG_HIP(hipFreeAsync(tmp, ctx->stream));
     return TFG_OK;
 }
 
