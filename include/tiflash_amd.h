@@ -411,7 +411,11 @@ int tfg_agg_consume_partial_keys(tfg_agg *agg, const void *const *key_cols, cons
 /* convertToBlockImplFinal with the key columns restored (String: chars + end offsets).  Every
  * String key column gets chars_capacity bytes; *out_chars_host = the chars the largest String key
  * column needs (TFG_ERR_CAPACITY past chars_capacity, nothing written).  tfg_agg_result on a
- * packed-key agg writes the packed TFG_KEYS128 keys instead, which tfg_agg_consume_partial accepts. */
+ * packed-key agg writes the packed TFG_KEYS128 keys instead, which tfg_agg_consume_partial accepts.
+ * As tfg_agg_result, groups whose count is not known yet are written before it is read when
+ * chars_capacity >= 16 * capacity (packed String keys hold at most 16 bytes with the '\0'): one
+ * host round trip at the end returns the count and the chars; a count above `capacity` returns
+ * TFG_ERR_CAPACITY after writing the first `capacity` groups. */
 int tfg_agg_result_keys(tfg_agg *agg, void *const *out_key_cols, uint64_t *const *out_key_offsets,
                         uint8_t *const *out_key_nullmaps, void *const *out_states, uint8_t *const *out_state_nullmaps,
                         uint64_t capacity, uint64_t chars_capacity, uint64_t *out_groups_host, uint64_t *out_chars_host);

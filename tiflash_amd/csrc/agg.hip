@@ -909,6 +909,9 @@ struct tfg_agg {
     bool long_key = false;
     int c_kinds[AGG_MAX] = {}, c_types[AGG_MAX] = {}, c_scales[AGG_MAX] = {};
     tfg_agg_params c_params{};
+    // the kept rows of the last tiled consume (pinned, written asynchronously) and its row count
+    uint64_t *kept_host = nullptr;
+    int64_t kept_n = 0;
     void *pack_buf = nullptr;
     size_t pack_cap = 0;
     unsigned *pack_err = nullptr;
@@ -1070,7 +1073,14 @@ int consume_fast_tiled(tfg_agg *a, int fast, const RowPred &pred, const void *ke
     char *sb = (char *)sp;
     pc.out[0] = sb + o_rec;
     SelBucket8 sel{(const uint64_t *)keys, fib_shift(B)};
-    if (int rc = run_partition_tiled(ctx, sel, pred, tg, pc, (uint32_t *)(sb + o_hist), "agg.part.tiled")) return rc;
+    // the previous consume kept fewer rows than this one has tiles (e.g. a filter that keeps
+    // nothing): the partition checks all-false tiles with vector loads.  kept_host is written by an
+    // asynchronous copy at the end of the previous consume: a heuristic, a stale value only picks
+    // the other (equally exact) kernel
+    const bool sparse = a->kept_host && a->kept_n > 0 &&
+                        *(volatile uint64_t *)a->kept_host * (uint64_t)tg.sg.TR < (uint64_t)a->kept_n;
+    if (int rc = run_partition_tiled(ctx, sel, pred, tg, pc, (uint32_t *)(sb + o_hist), "agg.part.tiled", sparse))
+        return rc;
     TiledIn tin{};
     tin.rec = (const uint64_t *)(sb + o_rec);
     tin.tile_hist = (const uint32_t *)(sb + o_hist);
@@ -1091,6 +1101,12 @@ int consume_fast_tiled(tfg_agg *a, int fast, const RowPred &pred, const void *ke
             return TFG_OK; // not reached: fast_signature returns the specialised codes only
     }
     TFG_LAUNCH_CHECK();
+    if (!a->kept_host && hipHostMalloc((void **)&a->kept_host, 8, hipHostMallocDefault) != hipSuccess)
+        a->kept_host = nullptr; // no heuristic then
+    if (a->kept_host) { // this consume's kept rows (the bucket kernels' cursor), for the next one
+        TFG_HIP(hipMemcpyAsync(a->kept_host, tin.cursor, 8, hipMemcpyDeviceToHost, ctx->stream));
+        a->kept_n = n;
+    }
     a->pending = true; // groups stay bucket-strided in a->pend until a call needs them dense
     a->pend_known = false;
     done = true;
@@ -1236,6 +1252,12 @@ int consume_wide_tiled(tfg_agg *a, int code, Sel sel, const void *const *vals, i
             return TFG_OK; // other signatures: the general path (nothing enqueued that matters)
     }
     TFG_LAUNCH_CHECK();
+    if (!a->kept_host && hipHostMalloc((void **)&a->kept_host, 8, hipHostMallocDefault) != hipSuccess)
+        a->kept_host = nullptr; // no heuristic then
+    if (a->kept_host) { // this consume's kept rows (the bucket kernels' cursor), for the next one
+        TFG_HIP(hipMemcpyAsync(a->kept_host, tin.cursor, 8, hipMemcpyDeviceToHost, ctx->stream));
+        a->kept_n = n;
+    }
     a->pending = true; // groups stay bucket-strided in a->pend until a call needs them dense
     a->pend_known = false;
     done = true;
@@ -1969,6 +1991,7 @@ int tfg_agg_destroy(tfg_agg *a) {
         if (a->ref_tmp[i]) (void)hipFree(a->ref_tmp[i]);
     if (a->pack_buf) (void)hipFree(a->pack_buf);
     if (a->pack_err) (void)hipFree(a->pack_err);
+    if (a->kept_host) (void)hipHostFree(a->kept_host);
     if (a->pend_blk) (void)hipFree(a->pend_blk);
     if (a->pend_dev) (void)hipFree(a->pend_dev);
     if (a->S.ovf) (void)hipFree(a->S.ovf);

@@ -618,7 +618,7 @@ inline bool make_staged_geom(uint32_t P, const PCols &cols, bool perm, bool crc,
 
 // NC8 > 0: compile-time fast path for exactly NC8 columns of 8 bytes (keys, payloads); the
 // column loops unroll and no per-row width switch remains.  NC8 == 0: any widths.
-template <typename Sel, typename Pred, int NC8, bool AOS = false, bool TILED = false>
+template <typename Sel, typename Pred, int NC8, bool AOS = false, bool TILED = false, bool VSKIP = false>
 __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, Pred pred, PartLayout L,
                                                                    const uint64_t *offs, PCols cols, uint32_t *perm,
                                                                    StagedGeom g) {
@@ -648,13 +648,10 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
     if (TILED && g.fine_bits)
         for (uint32_t p = threadIdx.x; p < (P << g.fine_bits); p += ST_T) fh[p] = 0;
     bool spec = true; // the previous tile kept a row (workgroup-uniform): keys load with the predicate
-    // all-false tiles of a plain column predicate are checked with vector loads (16-byte aligned
-    // column and segment start)
-#ifdef TFG_EXP_SKIPVEC
-    const bool skip_vec = TILED && PredVec<Pred>::ok && pred_vec_aligned(pred, begin);
-#else
-    constexpr bool skip_vec = false;
-#endif
+    // VSKIP (input the caller expects to keep almost nothing): all-false tiles of a plain column
+    // predicate are checked with vector loads (16-byte aligned column and segment start).  Not
+    // the default: the extra live state spills 6 VGPRs of the kept-row path (partition +2 %, r05q)
+    const bool skip_vec = VSKIP && TILED && PredVec<Pred>::ok && pred_vec_aligned(pred, begin);
     for (uint32_t tb = begin; tb < end; tb += (uint32_t)g.TR) {
         if constexpr (TILED) {
             if (!spec) {
@@ -1055,9 +1052,11 @@ inline bool make_tiled_geom(Ctx *ctx, int64_t n, uint32_t P, const PCols &cols, 
     return true;
 }
 
+// sparse: the caller expects almost every tile to keep no row (its previous input kept fewer rows
+// than it has tiles): plain column predicates take the vector all-false check (VSKIP)
 template <typename Sel>
 int run_partition_tiled(Ctx *ctx, const Sel &sel, const RowPred &pred, TiledGeom tg, const PCols &cols,
-                        uint32_t *tile_hist, const char *name) {
+                        uint32_t *tile_hist, const char *name, bool sparse = false) {
     tg.sg.tile_hist = tile_hist;
     int nc8 = cols.ncols;
     for (int c = 0; c < cols.ncols; ++c)
@@ -1066,6 +1065,24 @@ int run_partition_tiled(Ctx *ctx, const Sel &sel, const RowPred &pred, TiledGeom
     ProfScope _ps(ctx, name);
     return with_pred(pred, [&](auto pr) -> int {
         using PR = decltype(pr);
+        if constexpr (PredVec<PR>::ok) {
+            if (sparse) {
+                if (nc8 == 1)
+                    hipLaunchKernelGGL((part_scatter_staged_kernel<Sel, PR, 1, true, true, true>), dim3(tg.L.G),
+                                       dim3(ST_T), tg.sg.lds_bytes, ctx->stream, sel, pr, tg.L,
+                                       (const uint64_t *)nullptr, cols, (uint32_t *)nullptr, tg.sg);
+                else if (nc8 == 2)
+                    hipLaunchKernelGGL((part_scatter_staged_kernel<Sel, PR, 2, true, true, true>), dim3(tg.L.G),
+                                       dim3(ST_T), tg.sg.lds_bytes, ctx->stream, sel, pr, tg.L,
+                                       (const uint64_t *)nullptr, cols, (uint32_t *)nullptr, tg.sg);
+                else
+                    hipLaunchKernelGGL((part_scatter_staged_kernel<Sel, PR, 3, true, true, true>), dim3(tg.L.G),
+                                       dim3(ST_T), tg.sg.lds_bytes, ctx->stream, sel, pr, tg.L,
+                                       (const uint64_t *)nullptr, cols, (uint32_t *)nullptr, tg.sg);
+                TFG_LAUNCH_CHECK();
+                return TFG_OK;
+            }
+        }
         if (nc8 == 1) // keys alone (GROUP BY with count() only)
             hipLaunchKernelGGL((part_scatter_staged_kernel<Sel, PR, 1, true, true>), dim3(tg.L.G), dim3(ST_T),
                                tg.sg.lds_bytes, ctx->stream, sel, pr, tg.L, (const uint64_t *)nullptr, cols,
@@ -1095,11 +1112,6 @@ int run_partition_tiled(Ctx *ctx, const Sel &sel, const RowPred &pred, TiledGeom
 //           writes the runs out contiguously.
 // Bytes: 2 x (read + write) of the records, against 2 x (histogram read + read + write) for the
 // histogram + scatter form (run_two_pass).  Order inside a destination is unspecified.
-#ifdef TFG_EXP_RG_NT // profiling experiment: the regroup pass reads its records nontemporal
-constexpr bool RG_NT = true;
-#else
-constexpr bool RG_NT = false;
-#endif
 constexpr uint32_t RS_C = 64;
 constexpr int RS_T = 512, RS_RPT = 4, RS_BR = RS_T * RS_RPT, RS_TPC = 64;
 
@@ -1171,7 +1183,7 @@ __global__ void __launch_bounds__(RS_T) regroup_scatter_kernel(const uint64_t *r
                 if (tpre[mid] <= i) lo = mid;
                 else hi = mid;
             }
-            load_rec<NW, RG_NT>(rec, (size_t)(t0 + lo) * (uint32_t)TRS + tstart[lo] + (i - tpre[lo]), v[u]);
+            load_rec<NW>(rec, (size_t)(t0 + lo) * (uint32_t)TRS + tstart[lo] + (i - tpre[lo]), v[u]);
         }
     };
     uint64_t v[RS_RPT][NW];
