@@ -280,8 +280,9 @@ template <int ST, int MAXR, typename Pred> __device__ __forceinline__ bool tile_
         constexpr int WMAX = (MAXR + EPW - 1) / EPW;
         const uint4 *w = reinterpret_cast<const uint4 *>(reinterpret_cast<const E *>(p.col) + tb);
         const uint32_t words = (uint32_t)per * (uint32_t)(ST / EPW);
-        // two words in flight a round (more spill the kernel's other VGPRs: it sits at 128)
-        constexpr int WB = 2;
+        // all of a thread's words in flight at once (the sparse variant only: its spills are off
+        // the path it is chosen for)
+        constexpr int WB = WMAX;
         bool any = false;
 #pragma unroll
         for (int k0 = 0; k0 < WMAX; k0 += WB) {
@@ -675,8 +676,11 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
                         }
                     }
                     if (__syncthreads_or(any)) break;
-                    const uint32_t tile = blockIdx.x * (uint32_t)g.tps + (tb - begin) / (uint32_t)g.TR;
-                    for (uint32_t p = threadIdx.x; p < P; p += ST_T) g.tile_hist[(size_t)p * g.T + tile] = 0u;
+                    if constexpr (!VSKIP) { // VSKIP: the caller zeroed the whole table up front (one
+                                            // memset instead of P strided 4-byte stores a tile)
+                        const uint32_t tile = blockIdx.x * (uint32_t)g.tps + (tb - begin) / (uint32_t)g.TR;
+                        for (uint32_t p = threadIdx.x; p < P; p += ST_T) g.tile_hist[(size_t)p * g.T + tile] = 0u;
+                    }
                     tb += (uint32_t)g.TR;
                 }
                 if (tb >= end) break;
@@ -900,6 +904,14 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
             for (uint32_t p = threadIdx.x; p < P; p += ST_T) run[p] += hist[p];
         __syncthreads();
     }
+    if constexpr (TILED) {
+        // tile slots past the segment's last row (a short last segment: it has fewer than tps
+        // tiles) hold no run: their entries are zeroed, as every consumer walks all T tiles
+        const uint32_t visited = (end - begin + (uint32_t)g.TR - 1) / (uint32_t)g.TR;
+        for (uint32_t k = visited; k < (uint32_t)g.tps; ++k)
+            for (uint32_t p = threadIdx.x; p < P; p += ST_T)
+                g.tile_hist[(size_t)p * g.T + blockIdx.x * (uint32_t)g.tps + k] = 0u;
+    }
     if (TILED && g.fine_bits)
         for (uint32_t p = threadIdx.x; p < (P << g.fine_bits); p += ST_T)
             if (fh[p]) atomicAdd(&g.fine_counts[p], fh[p]);
@@ -1067,6 +1079,8 @@ int run_partition_tiled(Ctx *ctx, const Sel &sel, const RowPred &pred, TiledGeom
         using PR = decltype(pr);
         if constexpr (PredVec<PR>::ok) {
             if (sparse) {
+                // skipped tiles leave their (destination, tile) entries to this memset
+                TFG_HIP(hipMemsetAsync(tg.sg.tile_hist, 0, (size_t)tg.L.P * tg.sg.T * 4, ctx->stream));
                 if (nc8 == 1)
                     hipLaunchKernelGGL((part_scatter_staged_kernel<Sel, PR, 1, true, true, true>), dim3(tg.L.G),
                                        dim3(ST_T), tg.sg.lds_bytes, ctx->stream, sel, pr, tg.L,
