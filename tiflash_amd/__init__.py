@@ -650,7 +650,7 @@ class KeysAggregator(Aggregator):
         check(rc)
         keys = []
         for t, c, o in zip(self.key_types, cols, offs):
-            keys.append((c[:int(o[g - 1].item())] if g else c[:0], o[:g]) if t == STRING else c[:g])
+            keys.append((c[:chars.value] if g else c[:0], o[:g]) if t == STRING else c[:g])
         return {"keys": keys, "key_null": [x[:g] for x in nulls], "states": states, "state_null": snulls}
 
 

@@ -238,6 +238,84 @@ __global__ void agg_result_buckets_kernel(AggSpec S, GroupsIO st, const uint64_t
         write_result(S, st, s0 + j, d0 + j, key_width, out_keys, out_key_null, res);
 }
 
+// ---- the fused String-key result (one packed String key, the groups of a tiled consume still in
+// their buckets): the chars of each bucket's keys, their scan, then per bucket its groups' result
+// rows with the key bytes written straight into the ColumnString — no packed-key copy, no
+// per-group length scan, no unpack pass (convertToBlockImplFinal's insertKeyIntoColumns)
+constexpr int RSK_T = 256;
+__global__ void __launch_bounds__(RSK_T) pend_key_chars_kernel(const uint4 *keys, const uint64_t *cnt, const uint64_t *base,
+                                                           uint64_t *chars) {
+    __shared__ uint64_t red[RSK_T / 64];
+    const int b = blockIdx.x;
+    const uint64_t s0 = base[b], c = cnt[b];
+    uint64_t t = 0;
+    for (uint64_t j = threadIdx.x; j < c; j += RSK_T) t += ((keys[s0 + j].w >> 24) & 0x7Fu) + 1; // bytes + '\0'
+    for (int d = 32; d > 0; d >>= 1) t += __shfl_down(t, d, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t sum = 0;
+        for (int w = 0; w < RSK_T / 64; ++w) sum += red[w];
+        chars[b] = sum;
+    }
+}
+
+// workgroup b: bucket b's groups (rows off[b].., chars from choff[b]) in chunks of RSK_T; a
+// chunk's key bytes are placed in LDS by a block scan of their lengths and copied out with
+// consecutive lanes on consecutive bytes.  Rows >= capacity and chars >= chars_capacity dropped.
+__global__ void __launch_bounds__(RSK_T) agg_result_str_keys_kernel(AggSpec S, GroupsIO st, const uint64_t *cnt,
+                                                                const uint64_t *base, const uint64_t *off,
+                                                                const uint64_t *choff, uint64_t capacity,
+                                                                uint64_t chars_capacity, uint8_t *out_chars,
+                                                                uint64_t *out_offsets, uint8_t *out_null, ResultPtrs res) {
+    __shared__ uint8_t stage[RSK_T * 16];
+    __shared__ uint32_t wsum[RSK_T / 64];
+    const int b = blockIdx.x;
+    const uint64_t s0 = base[b], d0 = off[b];
+    const uint64_t c = d0 >= capacity ? 0 : min(cnt[b], capacity - d0);
+    const uint4 *keys = reinterpret_cast<const uint4 *>(st.key);
+    uint64_t run = choff[b];
+    for (uint64_t j0 = 0; j0 < c; j0 += RSK_T) { // uniform
+        const uint64_t j = j0 + threadIdx.x;
+        const bool have = j < c;
+        uint4 q = make_uint4(0, 0, 0, 0);
+        uint32_t len1 = 0;
+        if (have) {
+            q = keys[s0 + j];
+            len1 = ((q.w >> 24) & 0x7Fu) + 1;
+        }
+        uint32_t x = len1; // block exclusive scan of the lengths
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d, 64);
+            if ((int)(threadIdx.x & 63) >= d) x += y;
+        }
+        if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = x;
+        __syncthreads();
+        uint32_t pre = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < RSK_T / 64; ++w) {
+            if (w < (int)(threadIdx.x >> 6)) pre += wsum[w];
+            tot += wsum[w];
+        }
+        const uint32_t pos = pre + x - len1;
+        if (have) {
+            const uint64_t w0 = ((uint64_t)q.y << 32) | q.x, w1 = ((uint64_t)q.w << 32) | q.z;
+            for (uint32_t i = 0; i + 1 < len1; ++i)
+                stage[pos + i] = (uint8_t)(i < 8 ? w0 >> (i * 8) : w1 >> ((i - 8) * 8));
+            stage[pos + len1 - 1] = 0;
+            out_offsets[d0 + j] = run + pos + len1;
+            if (out_null) out_null[d0 + j] = (uint8_t)(w1 >> 63);
+            write_result(S, st, s0 + j, d0 + j, 16, nullptr, nullptr, res);
+        }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < tot; i += RSK_T)
+            if (run + i < chars_capacity) out_chars[run + i] = stage[i];
+        run += tot;
+        __syncthreads(); // stage / wsum are rewritten by the next chunk
+    }
+}
+
 __global__ void agg_state_add_kernel(AggSpec S, GroupsIO dst, GroupsIO src) { // without-key merge
     if (threadIdx.x || blockIdx.x) return;
     for (int i = 0; i < S.n_aggs; ++i) {
@@ -864,6 +942,7 @@ struct tfg_agg {
     size_t pend_cap = 0;
     GroupsIO pend{};
     uint64_t *pend_dev = nullptr; // [B] counts, [B] bases, [B + 1] offsets (exclusive scan of the counts)
+    uint64_t *pend_ch = nullptr;  // fused String-key result: [B] chars per bucket, [B + 1] their scan
     uint64_t *pend_cnt() const { return pend_dev; }
     uint64_t *pend_base() const { return pend_dev + B; }
     uint64_t *pend_off() const { return pend_dev + 2 * (size_t)B; }
@@ -1994,6 +2073,7 @@ int tfg_agg_destroy(tfg_agg *a) {
     if (a->kept_host) (void)hipHostFree(a->kept_host);
     if (a->pend_blk) (void)hipFree(a->pend_blk);
     if (a->pend_dev) (void)hipFree(a->pend_dev);
+    if (a->pend_ch) (void)hipFree(a->pend_ch);
     if (a->S.ovf) (void)hipFree(a->S.ovf);
     if (a->sdict) serial_dict_destroy(a->sdict);
     if (a->inner) tfg_agg_destroy(a->inner);
@@ -2466,6 +2546,76 @@ int tfg_agg_consume_partial_keys(tfg_agg *a, const void *const *key_cols, const 
     return tfg_agg_consume_partial(a, a->pack_buf, nullptr, states, state_nullmaps, n);
 }
 
+// tfg_agg_result_keys for one String key whose groups are still in their buckets (a tiled consume,
+// no value stores): agg_result_str_keys_kernel.  With chars_capacity >= 16 * capacity every key
+// fits and nothing is read before the write (one round trip at the end for the count and chars);
+// otherwise the totals are read first and checked.
+static int result_str_keys_fused(tfg_agg *a, uint8_t *out_chars, uint64_t *out_offsets, uint8_t *out_null,
+                                 void *const *out_states, uint8_t *const *out_state_nullmaps, uint64_t capacity,
+                                 uint64_t chars_capacity, uint64_t *out_groups_host, uint64_t *out_chars_host) {
+    Ctx *ctx = a->ctx;
+    const uint32_t B = a->B;
+    if (int rc = set_device(ctx)) return rc;
+    if (!a->pend_ch) TFG_HIP(hipMalloc(&a->pend_ch, (2 * (size_t)B + 1) * 8));
+    if (out_groups_host) *out_groups_host = 0;
+    if (out_chars_host) *out_chars_host = 0;
+    if (a->pend_known && a->pend_total > capacity) {
+        if (out_groups_host) *out_groups_host = a->pend_total;
+        return fail(TFG_ERR_CAPACITY, "result needs %llu groups, capacity %llu", (unsigned long long)a->pend_total,
+                    (unsigned long long)capacity);
+    }
+    if (!a->pend_known)
+        if (int rc = pend_scan(a)) return rc;
+    hipLaunchKernelGGL(pend_key_chars_kernel, dim3(B), dim3(RSK_T), 0, ctx->stream, (const uint4 *)a->pend.key,
+                       (const uint64_t *)a->pend_cnt(), (const uint64_t *)a->pend_base(), a->pend_ch);
+    TFG_LAUNCH_CHECK();
+    void *sp;
+    if (int rc = scratch_get(ctx, scan_tmp_bytes((int64_t)B + 1), &sp)) return rc;
+    if (int rc = exclusive_scan_u64(ctx, a->pend_ch, a->pend_ch + B, (int64_t)B, sp)) return rc;
+    const uint64_t *g_dev = a->pend_off() + B, *c_dev = a->pend_ch + 2 * (size_t)B;
+    auto read_totals = [&](uint64_t &g, uint64_t &ch) -> int {
+        TFG_HIP(hipMemcpyAsync(&g, g_dev, 8, hipMemcpyDeviceToHost, ctx->stream));
+        TFG_HIP(hipMemcpyAsync(&ch, c_dev, 8, hipMemcpyDeviceToHost, ctx->stream));
+        TFG_HIP(hipStreamSynchronize(ctx->stream));
+        a->pend_total = g;
+        a->pend_known = true;
+        return TFG_OK;
+    };
+    uint64_t G = 0, chars = 0;
+    if (chars_capacity < 16 * capacity) { // not every key fits for sure: the totals first
+        if (int rc = read_totals(G, chars)) return rc;
+        if (out_groups_host) *out_groups_host = G;
+        if (out_chars_host) *out_chars_host = chars;
+        if (G > capacity)
+            return fail(TFG_ERR_CAPACITY, "result needs %llu groups, capacity %llu", (unsigned long long)G,
+                        (unsigned long long)capacity);
+        if (chars > chars_capacity)
+            return fail(TFG_ERR_CAPACITY, "String keys need %llu bytes, capacity %llu", (unsigned long long)chars,
+                        (unsigned long long)chars_capacity);
+    }
+    ResultPtrs rp{};
+    for (int i = 0; i < a->S.n_aggs; ++i) {
+        rp.state[i] = out_states ? out_states[i] : nullptr;
+        rp.state_null[i] = out_state_nullmaps ? out_state_nullmaps[i] : nullptr;
+        rp.nullable[i] = a->arg_nullable[i] || a->S.kind[i] == TFG_AGG_FIRST_ROW;
+    }
+    {
+        ProfScope _ps(ctx, "agg.result");
+        hipLaunchKernelGGL(agg_result_str_keys_kernel, dim3(B), dim3(RSK_T), 0, ctx->stream, a->S, a->pend,
+                           (const uint64_t *)a->pend_cnt(), (const uint64_t *)a->pend_base(),
+                           (const uint64_t *)a->pend_off(), (const uint64_t *)a->pend_ch + B, capacity, chars_capacity,
+                           out_chars, out_offsets, out_null, rp);
+    }
+    TFG_LAUNCH_CHECK();
+    if (int rc = read_totals(G, chars)) return rc; // the count and the chars in one round trip
+    if (out_groups_host) *out_groups_host = G;
+    if (out_chars_host) *out_chars_host = chars;
+    if (G > capacity)
+        return fail(TFG_ERR_CAPACITY, "result needs %llu groups, capacity %llu (the first %llu written)",
+                    (unsigned long long)G, (unsigned long long)capacity, (unsigned long long)capacity);
+    return TFG_OK;
+}
+
 int tfg_agg_result_keys(tfg_agg *a, void *const *out_key_cols, uint64_t *const *out_key_offsets,
                         uint8_t *const *out_key_nullmaps, void *const *out_states, uint8_t *const *out_state_nullmaps,
                         uint64_t capacity, uint64_t chars_capacity, uint64_t *out_groups_host, uint64_t *out_chars_host) {
@@ -2489,6 +2639,13 @@ int tfg_agg_result_keys(tfg_agg *a, void *const *out_key_cols, uint64_t *const *
         if (out_chars_host) *out_chars_host = 0;
         return tfg_agg_result(a, out_key_cols ? out_key_cols[0] : nullptr, out_key_nullmaps ? out_key_nullmaps[0] : nullptr,
                               out_states, out_state_nullmaps, capacity, out_groups_host);
+    }
+    if (a->pending && !a->has_ref && a->kp.kind == WK_STRING && capacity > 0) {
+        TFG_CHECK(out_key_cols && out_key_cols[0] && out_key_offsets && out_key_offsets[0], TFG_ERR_INVALID_ARG,
+                  "String result needs chars and offsets");
+        return result_str_keys_fused(a, (uint8_t *)out_key_cols[0], out_key_offsets[0],
+                                     out_key_nullmaps ? out_key_nullmaps[0] : nullptr, out_states, out_state_nullmaps,
+                                     capacity, chars_capacity, out_groups_host, out_chars_host);
     }
     Ctx *ctx = a->ctx;
     // before the group count is read (tfg_agg_result's early path): packed keys, key lengths,

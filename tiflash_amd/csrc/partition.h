@@ -320,6 +320,54 @@ template <int ST, int MAXR, typename Pred> __device__ __forceinline__ bool tile_
     }
 }
 
+// tile_any_vec for the tiles at tb and tb + tr together (2 x the words in flight)
+template <int ST, int MAXR, typename Pred>
+__device__ __forceinline__ void tile_any_vec2(const Pred &p, uint32_t tb, int per, uint32_t tr, bool &any0, bool &any1) {
+    any0 = any1 = true;
+    if constexpr (PredVec<Pred>::ok) {
+        using E = typename PredVec<Pred>::E;
+        constexpr int EPW = 16 / (int)sizeof(E);
+        constexpr int WMAX = (MAXR + EPW - 1) / EPW;
+        const uint4 *w0 = reinterpret_cast<const uint4 *>(reinterpret_cast<const E *>(p.col) + tb);
+        const uint4 *w1 = reinterpret_cast<const uint4 *>(reinterpret_cast<const E *>(p.col) + tb + tr);
+        const uint32_t words = (uint32_t)per * (uint32_t)(ST / EPW);
+        uint4 x[2][WMAX];
+#pragma unroll
+        for (int k = 0; k < WMAX; ++k) {
+            const uint32_t i = (uint32_t)k * ST + threadIdx.x;
+            if (i < words) {
+                x[0][k] = w0[i];
+                x[1][k] = w1[i];
+            }
+        }
+        bool a[2] = {false, false};
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int k = 0; k < WMAX; ++k) {
+                if ((uint32_t)k * ST + threadIdx.x >= words) continue;
+                uint64_t b[4];
+                int nb;
+                if constexpr (sizeof(E) == 8) {
+                    b[0] = (uint64_t)x[t][k].x | ((uint64_t)x[t][k].y << 32);
+                    b[1] = (uint64_t)x[t][k].z | ((uint64_t)x[t][k].w << 32);
+                    nb = 2;
+                } else {
+                    b[0] = x[t][k].x, b[1] = x[t][k].y, b[2] = x[t][k].z, b[3] = x[t][k].w;
+                    nb = 4;
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (q >= nb) break;
+                    Loaded l{b[q], 0u};
+                    a[t] |= p.eval(l);
+                }
+            }
+        any0 = a[0];
+        any1 = a[1];
+    }
+}
+
 struct PartLayout {
     int64_t n;
     int64_t seg;   // rows per segment (multiple of PT)
@@ -662,6 +710,20 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
                 // tiles a round, their loads in flight together, cost the kept-row path 40 %:
                 // the partition kernel ran out of VGPRs, r05k)
                 while (tb < end) {
+                    if constexpr (VSKIP) {
+                        if (skip_vec && tb + 2u * (uint32_t)g.TR <= end) {
+                            // two whole tiles a round, all their words in flight together
+                            bool a0, a1;
+                            tile_any_vec2<ST_T, ST_MAXR>(pred, tb, per, (uint32_t)g.TR, a0, a1);
+                            if (__syncthreads_or(a0)) break;
+                            if (__syncthreads_or(a1)) {
+                                tb += (uint32_t)g.TR;
+                                break;
+                            }
+                            tb += 2u * (uint32_t)g.TR;
+                            continue;
+                        }
+                    }
                     bool any = false;
                     if (skip_vec && tb + (uint32_t)g.TR <= end) {
                         // a whole tile of a plain `T col Op scalar` predicate: its column words
