@@ -28,7 +28,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # demangled name -> short name (first match wins)
 NAME_MAP = [
     (r"part_hist_kernel<tfg::SelBucket", "agg.part.hist"),
-    (r"part_scatter_staged_kernel<tfg::SelBucket.*true, true>", "agg.part.tiled"),
+    (r"part_scatter_staged_kernel<tfg::SelBucket.*true, true(, (true|false))?>", "agg.part.tiled"),
     (r"part_scatter.*<tfg::SelBucket", "agg.part.scatter"),
     (r"agg_bucket_tiled_kernel<tfg::WideFastOps", "agg.wide.bucket.tiled"),
     (r"agg_bucket_tiled_kernel<tfg::FastOps", "agg.bucket.tiled"),
@@ -43,7 +43,7 @@ NAME_MAP = [
     (r"agg_result_kernel", "agg.result"),
     (r"part_hist_kernel<tfg::SelRec8", "part.hist.pass2"),
     (r"part_scatter_staged_kernel<tfg::SelRec8", "part.scatter.pass2"),
-    (r"part_scatter_staged_kernel<tfg::SelJoin.*true, true>", "join.part.tiled"),
+    (r"part_scatter_staged_kernel<tfg::SelJoin.*true, true(, (true|false))?>", "join.part.tiled"),
     (r"regroup_scatter_kernel", "join.part.regroup"),
     (r"part_hist_kernel<tfg::SelJoin", "join.part.hist"),
     (r"part_scatter.*<tfg::SelJoin", "join.part.scatter"),
