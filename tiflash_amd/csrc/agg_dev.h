@@ -1193,9 +1193,19 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
     const uint32_t *col = tin.tile_hist + (size_t)(tin.tile_base ? (b & ((1 << tin.fine_bits) - 1)) : b) * tin.T;
     const int tbeg = tin.tile_base ? (int)tin.tile_base[b >> tin.fine_bits] : 0;
     const int tend = tin.tile_base ? (int)tin.tile_base[(b >> tin.fine_bits) + 1] : tin.T;
-    // rows of this bucket
+    // rows of this bucket.  e0: this thread's entry of the first chunk of tiles, kept for pass 0
+    // (one global round trip less a bucket: C5's buckets span one chunk)
     unsigned long long tot = 0;
-    for (int t = tbeg + (int)threadIdx.x; t < tend; t += BT) tot += col[t] >> 16;
+    uint32_t e0 = 0;
+    {
+        int t = tbeg + (int)threadIdx.x;
+        if (Ops::WIDE && t < tend) { // (one-level buckets walk ~12K tiles: nothing to keep)
+            e0 = col[t];
+            tot += e0 >> 16;
+            t += BT;
+        }
+        for (; t < tend; t += BT) tot += col[t] >> 16;
+    }
     for (int d = 32; d > 0; d >>= 1) tot += __shfl_down(tot, d, 64);
     if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = tot;
     __syncthreads();
@@ -1204,24 +1214,32 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
         os = (int64_t)old_off[b];
         oe = (int64_t)old_off[b + 1];
     }
+    unsigned long long rows_b = 0; // every thread sums the wave totals (no round trip through thread 0)
+#pragma unroll
+    for (int w = 0; w < BT / 64; ++w) rows_b += s_red[w];
+    const bool no_rows = rows_b == 0; // a bucket no kept row reached: pass 0 has nothing to walk
+    // thread 0 reserves the spill rows and temp groups; the atomics' results are stored after
+    // the table clear below, so their round trip overlaps it
+    unsigned long long r0 = 0, r1 = 0;
     if (threadIdx.x == 0) {
-        unsigned long long t = 0;
-        for (int w = 0; w < BT / 64; ++w) t += s_red[w];
-        s_base[0] = atomicAdd(&tin.cursor[0], t);
-        s_base[1] = atomicAdd(&tin.cursor[1], t + (unsigned long long)(oe - os));
-        s_base[2] = t;
+        r0 = atomicAdd(&tin.cursor[0], rows_b);
+        r1 = atomicAdd(&tin.cursor[1], rows_b + (unsigned long long)(oe - os));
         T.ctrl->out_count = 0;
     }
-    __syncthreads();
-    const uint64_t sbase = s_base[0], out_base = s_base[1];
-    const bool no_rows = s_base[2] == 0; // a bucket no kept row reached: pass 0 has nothing to walk
     if (no_rows && os == oe) { // nothing at all: no table to build or flush
         if (threadIdx.x == 0) {
             out_cnt[b] = 0;
-            tmp_base[b] = out_base;
+            tmp_base[b] = r1;
         }
         return;
     }
+    T.clear(); // pass 0's table
+    if (threadIdx.x == 0) {
+        s_base[0] = r0;
+        s_base[1] = r1;
+    }
+    __syncthreads();
+    const uint64_t sbase = s_base[0], out_base = s_base[1];
     // the two spill regions as plain pointers, chosen per pass by value (an array of RowsIO
     // indexed by the pass would live in scratch memory)
     RowsIO src{};
@@ -1234,8 +1252,10 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
         RowsIO rows{}, spill{};
         rows.key = (pass & 1) ? reg0 : reg1;  // pass p >= 1 reads region (p - 1) & 1
         spill.key = (pass & 1) ? reg1 : reg0; // ... and spills into region p & 1
-        T.clear();
-        __syncthreads();
+        if (pass > 0) { // pass 0's table was cleared with the prologue
+            T.clear();
+            __syncthreads();
+        }
         if (threadIdx.x == 0) T.ctrl->spill_w = 0;
         int64_t take = oe - old_cursor;
         if (take > S.maxfill) take = S.maxfill;
@@ -1349,7 +1369,7 @@ __global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn
             // whatever the run lengths (packed records vs separate entry / prefix arrays: one
             // dependent LDS read less a row, agg.bucket 0.409 -> 0.404 ms, r05d)
             for (int t0 = tbeg; t0 < tend; t0 += CH) {
-                const uint32_t e = t0 + (int)threadIdx.x < tend ? col[t0 + threadIdx.x] : 0u;
+                const uint32_t e = (Ops::WIDE && t0 == tbeg) ? e0 : (t0 + (int)threadIdx.x < tend ? col[t0 + threadIdx.x] : 0u);
                 uint32_t r_beg, r_end; // this thread's run in chunk rows
                 { // block-wide exclusive scan of the run lengths
                     const uint32_t c = e >> 16;
