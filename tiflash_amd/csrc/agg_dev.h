@@ -1169,8 +1169,11 @@ struct TiledIn {
     unsigned long long *cursor; // [0] spill rows, [1] temp groups
 };
 
+// the 512-thread form runs where two workgroups' tables fit one CU's LDS: held to 128 VGPRs (4
+// waves per SIMD) so that both workgroups are resident (at 131 the second never fit)
 template <typename Ops, int BT>
-__global__ void __launch_bounds__(BT) agg_bucket_tiled_kernel(AggSpec S, TiledIn tin, int mode, GroupsIO old,
+__global__ void __launch_bounds__(BT) __attribute__((amdgpu_waves_per_eu(BT <= 512 ? 4 : 1)))
+agg_bucket_tiled_kernel(AggSpec S, TiledIn tin, int mode, GroupsIO old,
                                                               const uint64_t *old_off, GroupsIO out, uint64_t *out_cnt,
                                                               uint64_t *tmp_base) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
