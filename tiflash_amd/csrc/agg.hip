@@ -2004,7 +2004,7 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
         fill_num = fill_big;
     }
     if (const char *tc = getenv("TFG_AGG_TABLE_CELLS")) { // tuning experiments: cells a bucket table
-        const int c = atoi(tc) & ~255;
+        const int c = atoi(tc) & ~63;
         if (c >= 256 && (size_t)(c + 2) * cell <= (size_t)LDS_TABLE_MAX) {
             cap = c;
             fill_num = fill_big;
