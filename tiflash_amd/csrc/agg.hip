@@ -2003,6 +2003,24 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
         cap = c2;
         fill_num = fill_big;
     }
+    if (wide && !a->nokey) {
+        // wide keys: the probe is latency-bound, so two 8-wave workgroups per CU (the 512-thread
+        // kernel at 128 VGPRs) beat one 16-wave workgroup with a larger, emptier table: C5 1472
+        // cells at ~42 % load 4.37 ms vs 2048 at ~30 % 4.66 ms (r05z).  The largest table (64-cell
+        // steps) whose LDS plus that kernel's ~8.5 KB of static LDS fits half a CU, if the bucket
+        // fills at most 45 % of it
+        size_t per_cell = 8 + 16; // tag + 16-byte key
+        for (int i = 0; i < n_aggs; ++i) {
+            if (S.acc[i] != ACC_NONE) per_cell += 8 * (size_t)lds_acc_words(S.acc[i]);
+            if (S.has_cnt[i]) per_cell += 8;
+        }
+        const size_t dyn = 80 * 1024 - 8704 - sizeof(Ctrl) - 16;
+        const int c2 = (int)((dyn / per_cell - 2) & ~(size_t)63);
+        if (c2 >= 256 && per_bucket * 100 <= (int64_t)c2 * 45 && c2 * fill_big / 8 >= need) {
+            cap = c2;
+            fill_num = fill_big;
+        }
+    }
     if (const char *tc = getenv("TFG_AGG_TABLE_CELLS")) { // tuning experiments: cells a bucket table
         const int c = atoi(tc) & ~63;
         if (c >= 256 && (size_t)(c + 2) * cell <= (size_t)LDS_TABLE_MAX) {
