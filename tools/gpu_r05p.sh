@@ -6,7 +6,7 @@ set -e
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 TFG_SYNC_CHECK=1 timeout -k 10 300 tiflash_amd/host/build/test_host $PWD > gpurun_out/r05p_cpp.log 2>&1 || true
 if grep -q "HIP error" gpurun_out/r05p_cpp.log; then echo FAULT_SEEN; exit 0; fi
-timeout -k 10 200 python -u -m pytest -v --timeout 150 --timeout-method thread tests/test_gpu_minmax_wide.py -k "three_slices or mixed_collators" > gpurun_out/r05p_wide.log 2>&1 || { echo WIDE_FAIL; tail -5 gpurun_out/r05p_wide.log; exit 0; }
+timeout -k 10 200 python -u -m pytest -v --timeout 150 --timeout-method thread tests/test_gpu_minmax_wide.py tests/test_gpu_result_hint.py -k "three_slices or mixed_collators or hint" > gpurun_out/r05p_wide.log 2>&1 || { echo WIDE_FAIL; tail -5 gpurun_out/r05p_wide.log; exit 0; }
 B="python3 bench.py --no-cpu --codec-rows 0 --steps 10 --warmup 3"
 for bb in 12 13 14; do
   timeout -k 10 200 $B --no-join --no-variants --rows 1000000 --c5-bucket-bits $bb > gpurun_out/r05p_c5bb$bb.json 2> gpurun_out/r05p_c5bb$bb.err
