@@ -1976,9 +1976,9 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
     // wide keys may use up to 2^14 buckets: their two-level partition (coarse B >> 6, fine 64)
     // stays within 256 coarse destinations.  Their probe (tag, then the 16-byte key) is
     // latency-bound and slows sharply with the load factor, so they aim at ~3/8 of the largest
-    // table: C5's 10M groups -> 16384 buckets at ~30% load (wide bucket kernel 1.92 ms, against
-    // 2.67 ms at 8192 buckets / ~60% and 3.72 ms at 4096 / ~80%; smaller tables with more
-    // workgroups per CU measured slower: 1024 cells 3.71 ms, 1536 cells 2.84 ms, r03 sweep)
+    // table: C5's 10M groups -> 16384 buckets (wide bucket kernel 1.92 ms, against 2.67 ms at
+    // 8192 buckets / ~60% and 3.72 ms at 4096 / ~80%, r03); the table itself is then sized for
+    // two workgroups per CU (below)
     const int max_bits = wide ? 14 : 12;
     if (bbits <= 0) {
         const int64_t cells_max = LDS_TABLE_MAX / cell;
