@@ -419,6 +419,13 @@ int tfg_agg_consume_partial_keys(tfg_agg *agg, const void *const *key_cols, cons
 int tfg_agg_result_keys(tfg_agg *agg, void *const *out_key_cols, uint64_t *const *out_key_offsets,
                         uint8_t *const *out_key_nullmaps, void *const *out_states, uint8_t *const *out_state_nullmaps,
                         uint64_t capacity, uint64_t chars_capacity, uint64_t *out_groups_host, uint64_t *out_chars_host);
+/* IColumn::updateWeakHash32 of the aggregator's key columns (Columns/ColumnString.cpp:1228-1327,
+ * ColumnVector.cpp:483-535, ColumnNullable.cpp:131-173) computed from the packed TFG_KEYS128 keys
+ * tfg_agg_result writes for a packed-key aggregator: h[i] is updated as the unpacked key columns
+ * would update it (the two-phase sender routes its partial groups without unpacking them,
+ * HashBaseWriterHelper.cpp:46-62).  TFG_ERR_NOT_IMPLEMENTED for an aggregator without packed keys
+ * (the serialized method). */
+int tfg_agg_weak_hash_packed(tfg_agg *agg, const void *packed_keys, int64_t n, uint32_t *h);
 /* Result type of agg i (tfg_type) and its width in bytes. */
 int tfg_agg_result_type(tfg_agg *agg, int i, int *out_type, int *out_width);
 /* Chars bytes (terminators included) of the String result of agg i (min / max / first_row over a

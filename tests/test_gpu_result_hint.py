@@ -98,3 +98,47 @@ def test_keys_result_capacity_hint_string(tfa, ctx, dev, hint_scale):
     a.close()
     assert hinted == exact
     assert sum(c for _, c in exact.values()) == n
+
+
+def _str_col(dev, words):
+    """a ColumnString (chars with '\\0' per row, UInt64 end offsets) of python bytes rows"""
+    buf = b"".join(w + b"\0" for w in words)
+    chars = torch.tensor(list(buf), dtype=torch.uint8, device=dev)
+    offs = torch.tensor(np.cumsum([len(w) + 1 for w in words]), dtype=torch.int64, device=dev)
+    return chars, offs
+
+
+def _rows(res, nstr):
+    cols = []
+    for j in range(nstr):
+        ch, of = res["keys"][j]
+        ch, of = ch.cpu().numpy(), of.cpu().numpy()
+        assert len(ch) == (of[-1] if len(of) else 0)  # each column ends at its own last offset
+        cols.append([bytes(ch[(of[i - 1] if i else 0):of[i] - 1]) for i in range(len(of))])
+    c = res["states"][0].view(torch.int64).cpu().numpy()
+    return sorted(zip(*cols, c.tolist()))
+
+
+@pytest.mark.parametrize("hint", [10, 5000])
+def test_keys_result_capacity_hint_serialized(tfa, ctx, dev, hint):
+    """hinted results of the serialized method: String keys longer than 15 bytes need more than
+    16 chars bytes a group, so the hinted call reports TFG_ERR_CAPACITY with cnt <= hint and the
+    front end retries with the reported chars; two String key columns come back
+    each sliced at its own last offset"""
+    rng = np.random.default_rng(11)
+    n, groups = 20_000, 400
+    ids = rng.integers(0, groups, n)
+    long_w = [b"a-rather-long-string-key-%05d" % i for i in ids]   # 29 bytes: the serialized method
+    short_w = [b"s%d" % (i % 7) for i in ids]
+    a = tfa.KeysAggregator(ctx, [tfa.STRING, tfa.STRING], [(tfa.AGG_COUNT_ALL, 0)], expected_groups=groups)
+    c1, o1 = _str_col(dev, long_w)
+    c2, o2 = _str_col(dev, short_w)
+    a.consume([(c1, o1), (c2, o2)], [None])
+    exact = _rows(a.result(), 2)
+    got = _rows(a.result(capacity_hint=hint), 2)
+    a.close()
+    want = {}
+    for x, y in zip(long_w, short_w):
+        want[(x, y)] = want.get((x, y), 0) + 1
+    assert exact == sorted((x, y, c) for (x, y), c in want.items())
+    assert got == exact

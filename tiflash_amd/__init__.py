@@ -24,6 +24,7 @@ ERRORS = {
     -1: "INVALID_ARG", -2: "HIP", -3: "OOM", -4: "NOT_IMPLEMENTED", -5: "SIZE_MISMATCH",
     -6: "ILLEGAL_TYPE", -7: "LOGICAL", -8: "CAPACITY", -9: "NO_DEVICE", -10: "FAULT_INJECTED", -11: "OVERFLOW",
 }
+TFG_ERR_NOT_IMPLEMENTED = -4
 TFG_ERR_CAPACITY = -8
 TFG_ERR_NO_DEVICE = -9
 TFG_ERR_OVERFLOW = -11
@@ -610,6 +611,21 @@ class KeysAggregator(Aggregator):
         """-> dict as Aggregator.result() with keys = (G, 2) int64 packed keys."""
         return Aggregator.result(self, device)
 
+    def holds_packed(self) -> bool:
+        """True while the keys are held packed (16 bytes), False once the serialized method holds
+        them (String sort keys past 15 bytes, String + fixed tuples, wide tuples)."""
+        rc = lib().tfg_agg_weak_hash_packed(self.h, ctypes.c_void_p(0), ctypes.c_int64(0), ctypes.c_void_p(0))
+        if rc == TFG_ERR_NOT_IMPLEMENTED:
+            return False
+        check(rc)
+        return True
+
+    def weak_hash_packed(self, keys16, h):
+        """h (int32, n) updated with IColumn::updateWeakHash32 of the key columns the packed keys
+        (result_packed()["keys"]) stand for."""
+        check(lib().tfg_agg_weak_hash_packed(self.h, _p(keys16), ctypes.c_int64(keys16.shape[0]), _p(h)))
+        return h
+
     def result(self, device=None, chars_capacity=None, capacity_hint: Optional[int] = None):
         """-> dict(keys=[col or (chars, offsets)], key_null=[uint8], states=[...], state_null=[...]).
         String keys of the serialized method may need more than 16 bytes a group: the call is
@@ -636,22 +652,23 @@ class KeysAggregator(Aggregator):
         rc = lib().tfg_agg_result_keys(self.h, _ptr_array(cols), _ptr_array(offs), _ptr_array(nulls), sarr,
                                        _ptr_array(snulls), ctypes.c_uint64(g), ctypes.c_uint64(ccap),
                                        ctypes.byref(cnt), ctypes.byref(chars))
-        if hinted:
-            if rc == TFG_ERR_CAPACITY and cnt.value > g:
-                return self.result(device)
-            check(rc)
-            n = cnt.value
-            cut = lambda t: (t[0], t[1][:n]) if isinstance(t, tuple) else t[:n]
-            keys = [(c[:chars.value], o[:n]) if t == STRING else c[:n] for t, c, o in zip(self.key_types, cols, offs)]
-            return {"keys": keys, "key_null": [x[:n] for x in nulls], "states": [cut(x) for x in states],
-                    "state_null": [x[:n] for x in snulls]}
-        if rc == TFG_ERR_CAPACITY and chars.value > ccap:
+        if hinted and rc == TFG_ERR_CAPACITY:
+            # more groups than the hint (the exact call sizes them), or String keys needing more
+            # than 16 chars bytes a group (the serialized method): retry with the reported chars
+            return self.result(device, chars.value if cnt.value <= g and chars.value > ccap else None)
+        if not hinted and rc == TFG_ERR_CAPACITY and chars.value > ccap:
             return self.result(device, chars.value)
         check(rc)
+        n = cnt.value if hinted else g
+        # each String key column ends at its own last offset (chars reports the largest column's)
+        ends = iter(torch.stack([o[n - 1] for t, o in zip(self.key_types, offs) if t == STRING]).tolist()
+                    if n and STRING in self.key_types else [])
         keys = []
         for t, c, o in zip(self.key_types, cols, offs):
-            keys.append((c[:chars.value] if g else c[:0], o[:g]) if t == STRING else c[:g])
-        return {"keys": keys, "key_null": [x[:g] for x in nulls], "states": states, "state_null": snulls}
+            keys.append((c[:next(ends)] if n else c[:0], o[:n]) if t == STRING else c[:n])
+        cut = lambda x: (x[0], x[1][:n]) if isinstance(x, tuple) else x[:n]
+        return {"keys": keys, "key_null": [x[:n] for x in nulls], "states": [cut(x) for x in states] if hinted else states,
+                "state_null": [x[:n] for x in snulls]}
 
 
 # ---- a18-a21 join -----------------------------------------------------------------------------

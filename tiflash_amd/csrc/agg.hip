@@ -19,6 +19,8 @@
 // Group state is columnar in HBM: key bits (u64), NULL-key flag, per aggregate an accumulator
 // (Int64/UInt64/Float64 or Int128) and a non-NULL row count.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "common.h"
@@ -238,6 +240,35 @@ __global__ void agg_result_buckets_kernel(AggSpec S, GroupsIO st, const uint64_t
         write_result(S, st, s0 + j, d0 + j, key_width, out_keys, out_key_null, res);
 }
 
+
+// The same for B <= RSCAN_MAXB buckets without the scan launches before it: workgroup (b, part)
+// sums the counts of buckets 0 .. b - 1 itself (B words from L2), writes rows [part * c / SPLIT,
+// (part + 1) * c / SPLIT) of bucket b, and part 0 publishes off[b] (the last bucket also
+// off[B] = the group count) for the calls that read the offsets after it
+constexpr int RSCAN_MAXB = 1024, RSCAN_SPLIT = 4;
+__global__ void __launch_bounds__(256) agg_result_buckets_scan_kernel(AggSpec S, GroupsIO st, const uint64_t *cnt,
+                                                                     const uint64_t *base, uint64_t *off, int B,
+                                                                     int key_width, void *out_keys, uint8_t *out_key_null,
+                                                                     ResultPtrs res, uint64_t capacity) {
+    __shared__ uint64_t wsum[4];
+    const int b = (int)(blockIdx.x / RSCAN_SPLIT), part = (int)(blockIdx.x % RSCAN_SPLIT);
+    uint64_t x = 0;
+    for (int i = threadIdx.x; i < b; i += 256) x += cnt[i];
+    for (int d = 32; d > 0; d >>= 1) x += __shfl_down(x, d, 64);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = x;
+    __syncthreads();
+    const uint64_t d0 = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    const uint64_t cb = cnt[b];
+    if (part == 0 && threadIdx.x == 0) {
+        off[b] = d0;
+        if (b == B - 1) off[B] = d0 + cb;
+    }
+    const uint64_t c = d0 >= capacity ? 0 : min(cb, capacity - d0);
+    const uint64_t j0 = c * (uint64_t)part / RSCAN_SPLIT, j1 = c * (uint64_t)(part + 1) / RSCAN_SPLIT;
+    const uint64_t s0 = base[b];
+    for (uint64_t j = j0 + threadIdx.x; j < j1; j += 256)
+        write_result(S, st, s0 + j, d0 + j, key_width, out_keys, out_key_null, res);
+}
 // ---- the fused String-key result (one packed String key, the groups of a tiled consume still in
 // their buckets): the chars of each bucket's keys, their scan, then per bucket its groups' result
 // rows with the key bytes written straight into the ColumnString — no packed-key copy, no
@@ -782,6 +813,82 @@ __global__ void unpack_keys_kernel(KeyPack kp, const uint4 *keys, const uint64_t
     }
 }
 
+// IColumn::updateWeakHash32 of the key columns, read from their packed form (the sender of a
+// two-phase GROUP BY hashes the partial groups it holds packed, without unpacking them first):
+// a String key is its bytes (<= 15, right-trimmed already for BIN_PADDING, a sort key already for
+// the case-insensitive collators) hashed as ::updateWeakHash32(bytes) (Hash.h:148-214); fixed keys
+// are their values as hash_key_row feeds them to crc32q; a NULL key leaves the hash as it is
+// (ColumnNullable.cpp:131-173)
+struct PackTypes {
+    int type[4];
+};
+__global__ void __launch_bounds__(256) weak_hash_packed_kernel(KeyPack kp, PackTypes pt, const uint4 *keys, int64_t n,
+                                                               uint32_t *h) {
+    __shared__ uint32_t crc[8][256];
+    load_crc_lds(crc);
+    __syncthreads();
+    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (int64_t)gridDim.x * blockDim.x) {
+        const uint4 q = keys[g];
+        const uint64_t w0 = ((uint64_t)q.y << 32) | q.x, w1 = ((uint64_t)q.w << 32) | q.z;
+        uint32_t x = h[g];
+        if (kp.kind == WK_STRING) {
+            if (!(w1 >> 63)) {
+                const int len = (int)((w1 >> 56) & 0x7F);
+                const uint64_t hi = w1 & 0x00FFFFFFFFFFFFFFull; // bytes 8..14
+                if (len < 8) {
+                    x = crc32c_u64(crc, x, w0 | ((uint64_t)len << 56)); // w0 holds only the len bytes
+                } else {
+                    x = crc32c_u64(crc, x, w0);
+                    const int tail = len - 8;
+                    if (tail) { // the 8 bytes ending at len, the low 8 - tail of them masked off
+                        const int sh = 8 * tail; // bytes [len - 8, len) = (hi:w0) >> 8 * (len - 8)
+                        uint64_t word = (w0 >> sh) | (hi << (64 - sh));
+                        word &= ~0ull << (8 * (8 - tail));
+                        x = crc32c_u64(crc, x, word | (uint64_t)tail);
+                    }
+                }
+            }
+            h[g] = x;
+            continue;
+        }
+        const uint64_t nb = kp.off[kp.nkeys - 1] + kp.width[kp.nkeys - 1] <= 15 ? (w1 >> 56) : 0;
+        for (int j = 0; j < kp.nkeys; ++j) {
+            if ((nb >> j) & 1) continue; // NULL
+            const int wd = kp.width[j], o = kp.off[j];
+            const uint64_t lo = o < 8 ? (w0 >> (o * 8)) | (o > 0 ? w1 << ((8 - o) * 8) : 0) : w1 >> ((o - 8) * 8);
+            uint64_t v;
+            switch (pt.type[j]) {
+            case TFG_INT8: v = (uint64_t)(int64_t)(int8_t)lo; break;
+            case TFG_INT16: v = (uint64_t)(int64_t)(int16_t)lo; break;
+            case TFG_INT32: case TFG_DECIMAL32: v = (uint64_t)(int64_t)(int32_t)lo; break;
+            case TFG_UINT8: v = lo & 0xFF; break;
+            case TFG_UINT16: v = lo & 0xFFFF; break;
+            case TFG_UINT32: v = lo & 0xFFFFFFFFull; break;
+            case TFG_FLOAT32: {
+                const uint32_t u = (uint32_t)lo;
+                float f;
+                memcpy(&f, &u, 4);
+                v = float_to_u64_x86(f);
+                break;
+            }
+            case TFG_FLOAT64: {
+                double d;
+                memcpy(&d, &lo, 8);
+                v = float_to_u64_x86(d);
+                break;
+            }
+            case TFG_DECIMAL128: // a single 16-byte key at offset 0
+                x = crc32c_u64(crc, x, w0);
+                x = crc32c_u64(crc, x, w1);
+                continue;
+            default: v = wd == 8 ? lo : lo; break; // Int64 / UInt64 / Decimal64
+            }
+            x = crc32c_u64(crc, x, v);
+        }
+        h[g] = x;
+    }
+}
+
 // ---------------------------------------------------------------- row-reference value stores
 // (ACC_REF aggregates, agg_dev.h): the candidates of a consume are the store (refs 1..n0) and the
 // consumed column (n0 + 1 + r); after it every group's winning value is copied into a new store in
@@ -941,14 +1048,17 @@ struct tfg_agg {
     void *pend_blk = nullptr;
     size_t pend_cap = 0;
     GroupsIO pend{};
-    uint64_t *pend_dev = nullptr; // [B] counts, [B] bases, [B + 1] offsets (exclusive scan of the counts)
+    uint64_t *pend_dev = nullptr; // [B] counts, [B] bases, [B + 1] offsets (exclusive scan of the counts),
+                                  // [2] the bucket kernels' cursors (kept rows, temp groups)
     uint64_t *pend_ch = nullptr;  // fused String-key result: [B] chars per bucket, [B + 1] their scan
     uint64_t *pend_cnt() const { return pend_dev; }
     uint64_t *pend_base() const { return pend_dev + B; }
     uint64_t *pend_off() const { return pend_dev + 2 * (size_t)B; }
+    // after pend_off()[B]: one read-back of two words gives the group count and the kept rows
+    unsigned long long *pend_cursor() const { return (unsigned long long *)(pend_dev + 3 * (size_t)B + 1); }
     // groups capacity of the pending buffer for n more rows (allocated once, grown on demand)
     int ensure_pend(size_t groups) {
-        if (!pend_dev) TFG_HIP(hipMalloc(&pend_dev, (3 * (size_t)B + 1) * 8));
+        if (!pend_dev) TFG_HIP(hipMalloc(&pend_dev, (3 * (size_t)B + 3) * 8));
         if (pend_cap >= groups && pend_blk) return TFG_OK;
         if (pend_blk) {
             TFG_HIP(hipStreamSynchronize(ctx->stream));
@@ -989,8 +1099,9 @@ struct tfg_agg {
     int c_kinds[AGG_MAX] = {}, c_types[AGG_MAX] = {}, c_scales[AGG_MAX] = {};
     tfg_agg_params c_params{};
     // the kept rows of the last tiled consume (pinned, written asynchronously) and its row count
-    uint64_t *kept_host = nullptr;
+    uint64_t kept_rows = 0; // read with the group count (pend_cursor()[0]); kept_n = 0: unknown
     int64_t kept_n = 0;
+    int64_t consumed_n = 0; // rows of the last tiled consume
     void *pack_buf = nullptr;
     size_t pack_cap = 0;
     unsigned *pack_err = nullptr;
@@ -1083,12 +1194,21 @@ int pend_scan(tfg_agg *a) { // the output offsets on the device (no host read)
     if (int rc = scratch_get(ctx, scan_tmp_bytes(a->B + 1), &sp)) return rc;
     return exclusive_scan_u64(ctx, a->pend_cnt(), a->pend_off(), a->B, sp);
 }
+// the group count (pend_off()[B]) and, beside it, the kept rows of the tiled consume (the bucket
+// kernels' first cursor) in one read-back
+int pend_read_total(tfg_agg *a) {
+    uint64_t w[2];
+    if (int rc = read_back_u64(a->ctx, a->pend_off() + a->B, w, 2)) return rc;
+    a->pend_total = w[0];
+    a->kept_rows = w[1];
+    a->kept_n = a->consumed_n;
+    a->pend_known = true;
+    return TFG_OK;
+}
 int pend_counts(tfg_agg *a) {
     if (!a->pending || a->pend_known) return TFG_OK;
     if (int rc = pend_scan(a)) return rc;
-    if (int rc = read_back_u64(a->ctx, a->pend_off() + a->B, &a->pend_total, 1)) return rc;
-    a->pend_known = true;
-    return TFG_OK;
+    return pend_read_total(a);
 }
 // pending groups -> the dense bucket-major state st[] (the compaction every other call expects)
 int pend_compact(tfg_agg *a) {
@@ -1145,7 +1265,7 @@ int consume_fast_tiled(tfg_agg *a, int fast, const RowPred &pred, const void *ke
     const size_t o_rec = cv.take<uint64_t>((size_t)tg.out_rows * rec_words);
     const size_t o_sp0 = cv.take<uint64_t>((size_t)n * rec_words), o_sp1 = cv.take<uint64_t>((size_t)n * rec_words);
     const size_t o_hist = cv.take<uint32_t>((size_t)B * tg.sg.T);
-    const size_t o_cur = cv.take<unsigned long long>(2);
+    const size_t o_flags = cv.take<uint8_t>((size_t)tg.sg.T); // the sparse variant's tile flags
     if (int rc = a->ensure_pend(n_old + (size_t)n)) return rc; // the groups stay there (pending)
     void *sp;
     if (int rc = scratch_get(ctx, cv.off, &sp)) return rc;
@@ -1153,12 +1273,13 @@ int consume_fast_tiled(tfg_agg *a, int fast, const RowPred &pred, const void *ke
     pc.out[0] = sb + o_rec;
     SelBucket8 sel{(const uint64_t *)keys, fib_shift(B)};
     // the previous consume kept fewer rows than this one has tiles (e.g. a filter that keeps
-    // nothing): the partition checks all-false tiles with vector loads.  kept_host is written by an
-    // asynchronous copy at the end of the previous consume: a heuristic, a stale value only picks
-    // the other (equally exact) kernel
-    const bool sparse = a->kept_host && a->kept_n > 0 &&
-                        *(volatile uint64_t *)a->kept_host * (uint64_t)tg.sg.TR < (uint64_t)a->kept_n;
-    if (int rc = run_partition_tiled(ctx, sel, pred, tg, pc, (uint32_t *)(sb + o_hist), "agg.part.tiled", sparse))
+    // nothing): the partition checks all-false tiles with vector loads.  kept_rows was read with
+    // the previous consume's group count: a heuristic, a stale value only picks the other
+    // (equally exact) kernel
+    const bool sparse = a->kept_n > 0 && a->kept_rows * (uint64_t)tg.sg.TR < (uint64_t)a->kept_n;
+    tg.sg.zero2 = a->pend_cursor(); // the bucket kernel's cursors, zeroed by the partition
+    if (int rc = run_partition_tiled(ctx, sel, pred, tg, pc, (uint32_t *)(sb + o_hist), "agg.part.tiled", sparse,
+                                     (uint8_t *)(sb + o_flags)))
         return rc;
     TiledIn tin{};
     tin.rec = (const uint64_t *)(sb + o_rec);
@@ -1167,9 +1288,8 @@ int consume_fast_tiled(tfg_agg *a, int fast, const RowPred &pred, const void *ke
     tin.TR = tg.sg.TRS; // tile slot stride
     tin.spill[0] = (uint64_t *)(sb + o_sp0);
     tin.spill[1] = (uint64_t *)(sb + o_sp1);
-    tin.cursor = (unsigned long long *)(sb + o_cur);
+    tin.cursor = a->pend_cursor();
     tin.xcd_remap = 1; // neighbouring runs read by one XCD: FETCH 1.95 -> 1.2 GB per C2 step (r03b)
-    TFG_HIP(hipMemsetAsync(tin.cursor, 0, 16, ctx->stream));
     const bool has_old = n_old > 0;
     const GroupsIO old = a->st[a->cur];
     const uint64_t *ooff = has_old ? a->bucket_off[a->cur] : (const uint64_t *)nullptr;
@@ -1180,12 +1300,10 @@ int consume_fast_tiled(tfg_agg *a, int fast, const RowPred &pred, const void *ke
             return TFG_OK; // not reached: fast_signature returns the specialised codes only
     }
     TFG_LAUNCH_CHECK();
-    if (!a->kept_host && hipHostMalloc((void **)&a->kept_host, 8, hipHostMallocDefault) != hipSuccess)
-        a->kept_host = nullptr; // no heuristic then
-    if (a->kept_host) { // this consume's kept rows (the bucket kernels' cursor), for the next one
-        TFG_HIP(hipMemcpyAsync(a->kept_host, tin.cursor, 8, hipMemcpyDeviceToHost, ctx->stream));
-        a->kept_n = n;
-    }
+    // this consume's kept rows (the bucket kernels' cursor) are read with the group count, for the
+    // next consume's all-false tile choice (no read-back of their own)
+    a->consumed_n = n;
+    a->kept_n = 0;
     a->pending = true; // groups stay bucket-strided in a->pend until a call needs them dense
     a->pend_known = false;
     done = true;
@@ -1266,7 +1384,6 @@ int consume_wide_tiled(tfg_agg *a, int code, Sel sel, const void *const *vals, i
     const size_t o_tbase = cv.take<uint32_t>(B1 + 1);
     const size_t o_hist2 = cv.take<uint32_t>(two ? (size_t)RG_FINE * T2 : 0);
     const size_t o_desc = cv.take<RgDesc>(two ? (size_t)T2 : 0);
-    const size_t o_cur = cv.take<unsigned long long>(2);
     if (int rc = a->ensure_pend(n_old + (size_t)n)) return rc; // the groups stay there (pending)
     void *sp;
     if (int rc = scratch_get(ctx, cv.off, &sp)) return rc;
@@ -1274,13 +1391,13 @@ int consume_wide_tiled(tfg_agg *a, int code, Sel sel, const void *const *vals, i
     pc.out[0] = sb + o_rec1;
     sel.shift = fib_shift(B1);
     if (err) TFG_HIP(hipMemsetAsync(err, 0, sizeof(unsigned), ctx->stream));
+    tg.sg.zero2 = a->pend_cursor(); // the bucket kernel's cursors, zeroed by the partition
     if (int rc = run_partition_tiled(ctx, sel, RowPred{}, tg, pc, (uint32_t *)(sb + o_hist1), "agg.part.tiled"))
         return rc;
     if (err) { // a String key longer than 15 bytes: the serialized method, not this one
-        unsigned e = 0;
-        TFG_HIP(hipMemcpyAsync(&e, err, sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
-        TFG_HIP(hipStreamSynchronize(ctx->stream));
-        if (e) {
+        uint64_t e = 0;
+        if (int rc = read_back_u64(ctx, (const uint64_t *)err, &e, 1)) return rc; // pinned: no staging copy
+        if ((unsigned)e) {
             a->long_key = true;
             return fail(TFG_ERR_NOT_IMPLEMENTED, "String GROUP BY key longer than 15 bytes (serialized method)");
         }
@@ -1318,9 +1435,8 @@ int consume_wide_tiled(tfg_agg *a, int code, Sel sel, const void *const *vals, i
         tin.tile_base = tbase;
         tin.fine_bits = RG_FINE_BITS;
     }
-    tin.cursor = (unsigned long long *)(sb + o_cur);
+    tin.cursor = a->pend_cursor();
     tin.xcd_remap = 0; // two-level wide tiles: measured slower with the remap (r03b)
-    TFG_HIP(hipMemsetAsync(tin.cursor, 0, 16, ctx->stream));
     const bool has_old = n_old > 0;
     const GroupsIO old = a->st[a->cur];
     const uint64_t *ooff = has_old ? a->bucket_off[a->cur] : (const uint64_t *)nullptr;
@@ -1331,12 +1447,10 @@ int consume_wide_tiled(tfg_agg *a, int code, Sel sel, const void *const *vals, i
             return TFG_OK; // other signatures: the general path (nothing enqueued that matters)
     }
     TFG_LAUNCH_CHECK();
-    if (!a->kept_host && hipHostMalloc((void **)&a->kept_host, 8, hipHostMallocDefault) != hipSuccess)
-        a->kept_host = nullptr; // no heuristic then
-    if (a->kept_host) { // this consume's kept rows (the bucket kernels' cursor), for the next one
-        TFG_HIP(hipMemcpyAsync(a->kept_host, tin.cursor, 8, hipMemcpyDeviceToHost, ctx->stream));
-        a->kept_n = n;
-    }
+    // this consume's kept rows (the bucket kernels' cursor) are read with the group count, for the
+    // next consume's all-false tile choice (no read-back of their own)
+    a->consumed_n = n;
+    a->kept_n = 0;
     a->pending = true; // groups stay bucket-strided in a->pend until a call needs them dense
     a->pend_known = false;
     done = true;
@@ -1486,6 +1600,16 @@ int consume_keyed(tfg_agg *a, int mode, const RowPred &pred, const void *keys, i
         if (!launch_bucket_fast(fast, B, S, ctx->stream, rows, rows1, mode, stage_off, old, ooff, tmp, new_cnt)) {
             bool w256 = false; // a Decimal256 sum: rows carry 4-limb values
             for (int i = 0; i < S.n_aggs; ++i) w256 = w256 || S.acc[i] == ACC_I256;
+#ifdef TFG_EXP_POOL
+            if (getenv("TFG_POOLDBG"))
+                for (int i = 0; i < S.n_aggs; ++i)
+                    if (S.acc[i] == ACC_REF)
+                        fprintf(stderr, "POOL launch agg %p ref[%d] v %p %p o %p %p n0 %llu n1 %llu nb %llu %llu\n",
+                                (void *)a, i, (const void *)S.ref[i].v[0], (const void *)S.ref[i].v[1],
+                                (const void *)S.ref[i].o[0], (const void *)S.ref[i].o[1],
+                                (unsigned long long)S.ref[i].n0, (unsigned long long)S.ref[i].n1,
+                                (unsigned long long)S.ref[i].nb[0], (unsigned long long)S.ref[i].nb[1]);
+#endif
             launch_bucket_generic(key_width == 16, w256, B, S, ctx->stream, rows, rows1, mode, stage_off, old, ooff, tmp,
                                   new_cnt);
         }
@@ -1555,6 +1679,8 @@ int check_overflow(tfg_agg *a) {
     TFG_HIP(hipMemsetAsync(a->S.ovf, 0, sizeof f, a->ctx->stream));
     if (f & 2) // RefSrc::err: a row reference outside its candidates (never dereferenced)
         return fail(TFG_ERR_LOGICAL, "row-reference aggregate state out of range (internal error)");
+    if (f & 4) // RefSrc::err: a candidate's String bytes past its buffer (never dereferenced)
+        return fail(TFG_ERR_LOGICAL, "row-reference String candidate past its buffer (internal error)");
     return fail(TFG_ERR_OVERFLOW, "Decimal256 sum overflow (DECIMAL_OVERFLOW: the sum left Int256)");
 }
 
@@ -1564,11 +1690,16 @@ struct RefIn { // source 1 of an ACC_REF aggregate's candidates: the consumed co
     const uint64_t *off = nullptr; // String: end offsets
     const uint8_t *nul = nullptr;
     uint64_t n = 0;
+    uint64_t bytes = ~0ull; // String chars bytes when known (a merge's source store)
 };
 struct RefCall { // the collated candidates of one call (String min / max under a case-insensitive collator)
-    Ctx *ctx;
+    tfg_agg *a;
     CollatedStrings cs[AGG_MAX][2];
-    explicit RefCall(Ctx *c) : ctx(c) {}
+    explicit RefCall(tfg_agg *agg) : a(agg) {}
+    // the candidates named in S.ref die with the call: no later launch may carry their pointers
+    ~RefCall() {
+        for (auto &r : a->S.ref) r = RefSrc{};
+    }
     RefCall(const RefCall &) = delete;
     RefCall &operator=(const RefCall &) = delete;
 };
@@ -1595,6 +1726,8 @@ int ref_setup(tfg_agg *a, const RefIn *in, RefCall &rc) {
         const int t = a->S.src_type[i];
         R.v[0] = st.val;
         R.v[1] = in[i].val;
+        R.nb[0] = st.bytes;
+        R.nb[1] = in[i].bytes; // a consumed column's chars: size not passed (~0)
         if (t != TFG_STRING) {
             R.width = (int)type_width(t);
             continue;
@@ -1610,8 +1743,10 @@ int ref_setup(tfg_agg *a, const RefIn *in, RefCall &rc) {
             return r;
         R.v[0] = rc.cs[i][0].chars;
         R.o[0] = rc.cs[i][0].offsets();
+        R.nb[0] = rc.cs[i][0].bytes;
         R.v[1] = rc.cs[i][1].chars;
         R.o[1] = rc.cs[i][1].offsets();
+        R.nb[1] = rc.cs[i][1].bytes;
     }
     return TFG_OK;
 }
@@ -1709,7 +1844,7 @@ int consume_common(tfg_agg *a, int mode, const RowPred &pred, const void *keys, 
             rin[i] = RefIn{static_cast<const uint8_t *>(args[i]), nullptr, vnull[i], (uint64_t)n};
         }
     }
-    RefCall rc(a->ctx);
+    RefCall rc(a);
     if (a->has_ref) {
         if (int r = ref_setup(a, rin, rc)) return r;
         if (!a->nokey) { // keyed: every row carries its candidate reference through the partition
@@ -1748,7 +1883,6 @@ int consume_common(tfg_agg *a, int mode, const RowPred &pred, const void *keys, 
 struct AggExtract {
     uint64_t G = 0;
     int nkeys = 0, n_aggs = 0;
-    std::vector<void *> bufs;
     void *kc[8] = {};
     uint64_t *ko[8] = {};
     uint8_t *kn[8] = {};
@@ -1757,19 +1891,19 @@ struct AggExtract {
     uint8_t *sn[AGG_MAX] = {};
     tfg_str_out so[AGG_MAX] = {};
     tfg_str_col sc[AGG_MAX] = {};
-    Ctx *ctx = nullptr;
+    Ctx *ctx = nullptr;  // the buffers live in its call arena (no allocation in steady state) ...
+    Ctx *user = nullptr; // ... and are read by this context's stream too (a merge's destination)
     ~AggExtract() {
-        if (ctx) (void)hipStreamSynchronize(ctx->stream);
-        for (void *p : bufs) (void)hipFree(p);
+        if (!ctx) return;
+        if (user && user != ctx && user->stream != ctx->stream) (void)hipStreamSynchronize(user->stream);
+        arena_drop(ctx);
     }
-    int alloc(size_t bytes, void **p) {
-        TFG_HIP(hipMalloc(p, std::max<size_t>(bytes, 8)));
-        bufs.push_back(*p);
-        return TFG_OK;
-    }
+    int alloc(size_t bytes, void **p) { return arena_alloc(ctx, std::max<size_t>(bytes, 8), p); }
 };
 
 static int agg_extract(tfg_agg *a, AggExtract &e) {
+    TFG_CHECK(!e.ctx, TFG_ERR_LOGICAL, "extract reused");
+    arena_hold(a->ctx); // dropped by e's destructor
     e.ctx = a->ctx;
     uint64_t G = 0;
     if (int rc = tfg_agg_size(a, &G)) return rc;
@@ -1878,6 +2012,7 @@ static int merge_through_keys(tfg_agg *dst, tfg_agg *src) {
         TFG_CHECK(dst->key_types[j] == src->key_types[j], TFG_ERR_LOGICAL, "merging aggregators of different signatures");
     TFG_HIP(hipStreamSynchronize(src->ctx->stream));
     AggExtract e;
+    e.user = dst->ctx;
     if (int rc = agg_extract(src, e)) return rc;
     if (e.G == 0) return TFG_OK;
     TFG_HIP(hipStreamSynchronize(src->ctx->stream));
@@ -2022,8 +2157,10 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
         }
     }
     if (const char *tc = getenv("TFG_AGG_TABLE_CELLS")) { // tuning experiments: cells a bucket table
+        // bounded by what a CU's 160 KB leaves beside the largest bucket kernel's static LDS
+        // (the tiled 1024-thread kernel's run records and sampled run index: ~12.5 KB)
         const int c = atoi(tc) & ~63;
-        if (c >= 256 && (size_t)(c + 2) * cell <= (size_t)LDS_TABLE_MAX) {
+        if (c >= 256 && (size_t)(c + 2) * cell + sizeof(Ctrl) + 16 <= (size_t)(LDS_CU_BYTES - BUCKET_STATIC_LDS_MAX)) {
             cap = c;
             fill_num = fill_big;
         }
@@ -2095,7 +2232,6 @@ int tfg_agg_destroy(tfg_agg *a) {
         if (a->ref_tmp[i]) (void)hipFree(a->ref_tmp[i]);
     if (a->pack_buf) (void)hipFree(a->pack_buf);
     if (a->pack_err) (void)hipFree(a->pack_err);
-    if (a->kept_host) (void)hipHostFree(a->kept_host);
     if (a->pend_blk) (void)hipFree(a->pend_blk);
     if (a->pend_dev) (void)hipFree(a->pend_dev);
     if (a->pend_ch) (void)hipFree(a->pend_ch);
@@ -2188,13 +2324,13 @@ int tfg_agg_merge(tfg_agg *dst, tfg_agg *src) {
     // row-reference aggregates: the candidates are dst's store, then src's (changeFirstTime(to) /
     // changeIfLess(to) keep dst's value on ties: Aggregator::mergeDataImpl folds src into dst)
     RefIn rin[AGG_MAX];
-    RefCall rc(dst->ctx);
+    RefCall rc(dst);
     if (dst->has_ref) {
         for (int i = 0; i < dst->S.n_aggs; ++i) {
             if (dst->S.acc[i] != ACC_REF) continue;
             const RefStore &ss = src->store[i];
             TFG_CHECK(ss.n == src->n_groups, TFG_ERR_LOGICAL, "value store out of step with the groups");
-            rin[i] = RefIn{ss.val, ss.scan ? ss.scan + 1 : nullptr, ss.nul, ss.n};
+            rin[i] = RefIn{ss.val, ss.scan ? ss.scan + 1 : nullptr, ss.nul, ss.n, ss.bytes};
         }
         if (int r = ref_setup(dst, rin, rc)) return r;
     }
@@ -2270,6 +2406,14 @@ static int result_pending_launch(tfg_agg *a, void *out_keys, uint8_t *out_key_nu
         rp.state_null[i] = out_state_nullmaps ? out_state_nullmaps[i] : nullptr;
         rp.nullable[i] = a->arg_nullable[i] || a->S.kind[i] == TFG_AGG_FIRST_ROW;
     }
+    if (a->B <= (uint32_t)RSCAN_MAXB) { // the offsets computed by the result kernel itself
+        ProfScope _ps(a->ctx, "agg.result");
+        hipLaunchKernelGGL(agg_result_buckets_scan_kernel, dim3(a->B * RSCAN_SPLIT), dim3(256), 0, a->ctx->stream,
+                           a->S, a->pend, (const uint64_t *)a->pend_cnt(), (const uint64_t *)a->pend_base(),
+                           a->pend_off(), (int)a->B, a->S.key_width, out_keys, out_key_nullmap, rp, capacity);
+        TFG_LAUNCH_CHECK();
+        return TFG_OK;
+    }
     if (int rc = pend_scan(a)) return rc;
     {
         ProfScope _ps(a->ctx, "agg.result");
@@ -2293,8 +2437,7 @@ int tfg_agg_result(tfg_agg *a, void *out_keys, uint8_t *out_key_nullmap, void *c
         if (int rc = set_device(a->ctx)) return rc;
         if (int rc = result_pending_launch(a, out_keys, out_key_nullmap, out_states, out_state_nullmaps, capacity))
             return rc;
-        if (int rc = read_back_u64(a->ctx, a->pend_off() + a->B, &a->pend_total, 1)) return rc;
-        a->pend_known = true;
+        if (int rc = pend_read_total(a)) return rc;
         if (out_groups_host) *out_groups_host = a->pend_total;
         if (a->pend_total > capacity)
             return fail(TFG_ERR_CAPACITY, "result needs %llu groups, capacity %llu (the first %llu written)",
@@ -2357,6 +2500,20 @@ int tfg_agg_result(tfg_agg *a, void *out_keys, uint8_t *out_key_nullmap, void *c
     return TFG_OK;
 }
 
+int tfg_agg_weak_hash_packed(tfg_agg *a, const void *packed_keys, int64_t n, uint32_t *h) {
+    TFG_CHECK(a, TFG_ERR_INVALID_ARG, "agg is null");
+    TFG_CHECK(!a->sdict && a->kp.kind, TFG_ERR_NOT_IMPLEMENTED, "the aggregator holds no packed keys");
+    if (n <= 0) return TFG_OK; // n = 0: does the aggregator hold packed keys?
+    TFG_CHECK(packed_keys && h, TFG_ERR_INVALID_ARG, "null argument");
+    if (int rc = set_device(a->ctx)) return rc;
+    PackTypes pt{};
+    for (int j = 0; j < a->kp.nkeys && j < 4; ++j) pt.type[j] = a->key_types[j];
+    hipLaunchKernelGGL(weak_hash_packed_kernel, dim3(stream_grid(n, 256, 4096)), dim3(256), 0, a->ctx->stream, a->kp, pt,
+                       (const uint4 *)packed_keys, n, h);
+    TFG_LAUNCH_CHECK();
+    return TFG_OK;
+}
+
 int tfg_agg_result_chars(tfg_agg *a, int i, uint64_t *out_bytes) {
     TFG_CHECK(a && out_bytes, TFG_ERR_INVALID_ARG, "null argument");
     if (a->sdict) return tfg_agg_result_chars(a->inner, i, out_bytes);
@@ -2385,8 +2542,8 @@ static int pack_keys(tfg_agg *a, const void *const *key_cols, const uint64_t *co
         kp.offsets = key_offsets[0];
     }
     if (int rc = a->ensure_pack((size_t)n)) return rc;
-    if (!a->pack_err) TFG_HIP(hipMalloc(&a->pack_err, sizeof(unsigned)));
-    TFG_HIP(hipMemsetAsync(a->pack_err, 0, sizeof(unsigned), a->ctx->stream));
+    if (!a->pack_err) TFG_HIP(hipMalloc(&a->pack_err, 8));
+    TFG_HIP(hipMemsetAsync(a->pack_err, 0, 8, a->ctx->stream));
     {
         ProfScope _ps(a->ctx, "agg.pack_keys");
         hipLaunchKernelGGL(pack_keys_kernel, dim3(stream_grid(n, 256 * 4, 8192)), dim3(256), 0, a->ctx->stream, kp, n,
@@ -2394,10 +2551,9 @@ static int pack_keys(tfg_agg *a, const void *const *key_cols, const uint64_t *co
     }
     TFG_LAUNCH_CHECK();
     if (kp.kind == WK_STRING) {
-        unsigned err = 0;
-        TFG_HIP(hipMemcpyAsync(&err, a->pack_err, sizeof(unsigned), hipMemcpyDeviceToHost, a->ctx->stream));
-        TFG_HIP(hipStreamSynchronize(a->ctx->stream));
-        if (err) {
+        uint64_t err = 0;
+        if (int rc = read_back_u64(a->ctx, (const uint64_t *)a->pack_err, &err, 1)) return rc;
+        if ((unsigned)err) {
             a->long_key = true; // key_string past 15 bytes: the serialized method takes them
             return fail(TFG_ERR_NOT_IMPLEMENTED, "String GROUP BY key longer than 15 bytes");
         }
@@ -2536,7 +2692,7 @@ static int consume_keys_packed(tfg_agg *a, const void *const *key_cols, const ui
     if (code && a->kp.kind == WK_STRING) {
         TFG_CHECK(key_cols && key_cols[0] && key_offsets && key_offsets[0], TFG_ERR_INVALID_ARG,
                   "String key needs its chars and offsets");
-        if (!a->pack_err) TFG_HIP(hipMalloc(&a->pack_err, sizeof(unsigned)));
+        if (!a->pack_err) TFG_HIP(hipMalloc(&a->pack_err, 8));
         SelWideStr sel{(const uint8_t *)key_cols[0], key_offsets[0], key_nullmaps ? key_nullmaps[0] : nullptr,
                        a->kp.collator, a->pack_err, 0};
         bool done = false;
@@ -2598,11 +2754,16 @@ static int result_str_keys_fused(tfg_agg *a, uint8_t *out_chars, uint64_t *out_o
     if (int rc = scratch_get(ctx, scan_tmp_bytes((int64_t)B + 1), &sp)) return rc;
     if (int rc = exclusive_scan_u64(ctx, a->pend_ch, a->pend_ch + B, (int64_t)B, sp)) return rc;
     const uint64_t *g_dev = a->pend_off() + B, *c_dev = a->pend_ch + 2 * (size_t)B;
-    auto read_totals = [&](uint64_t &g, uint64_t &ch) -> int {
-        TFG_HIP(hipMemcpyAsync(&g, g_dev, 8, hipMemcpyDeviceToHost, ctx->stream));
-        TFG_HIP(hipMemcpyAsync(&ch, c_dev, 8, hipMemcpyDeviceToHost, ctx->stream));
+    auto read_totals = [&](uint64_t &g, uint64_t &ch) -> int { // pinned words: one sync, no staging
+        uint64_t *hp = ctx->host_pinned;
+        TFG_HIP(hipMemcpyAsync(hp, g_dev, 16, hipMemcpyDeviceToHost, ctx->stream)); // count, kept rows
+        TFG_HIP(hipMemcpyAsync(hp + 2, c_dev, 8, hipMemcpyDeviceToHost, ctx->stream));
         TFG_HIP(hipStreamSynchronize(ctx->stream));
+        g = hp[0];
+        ch = hp[2];
         a->pend_total = g;
+        a->kept_rows = hp[1];
+        a->kept_n = a->consumed_n;
         a->pend_known = true;
         return TFG_OK;
     };
@@ -2681,10 +2842,12 @@ int tfg_agg_result_keys(tfg_agg *a, void *const *out_key_cols, uint64_t *const *
     uint64_t G = 0;
     const uint64_t *g_dev = nullptr;
     if (early) {
+        // the pending buffer holds at most pend_cap groups: a generous hint sizes nothing past it
+        const uint64_t ecap = std::min<uint64_t>(capacity, a->pend_cap);
         if (int rc = set_device(ctx)) return rc;
-        if (int rc = a->ensure_pack(capacity)) return rc;
-        if (int rc = result_pending_launch(a, a->pack_buf, nullptr, out_states, out_state_nullmaps, capacity)) return rc;
-        G = capacity;
+        if (int rc = a->ensure_pack(ecap)) return rc;
+        if (int rc = result_pending_launch(a, a->pack_buf, nullptr, out_states, out_state_nullmaps, ecap)) return rc;
+        G = ecap;
         g_dev = a->pend_off() + a->B;
     } else {
         if (int rc = tfg_agg_size(a, &G)) return rc;
@@ -2740,11 +2903,15 @@ int tfg_agg_result_keys(tfg_agg *a, void *const *out_key_cols, uint64_t *const *
     }
     TFG_LAUNCH_CHECK();
     if (early) { // the count and the chars total in one round trip
-        uint64_t cnt = 0, chars = 0;
-        TFG_HIP(hipMemcpyAsync(&cnt, g_dev, 8, hipMemcpyDeviceToHost, ctx->stream));
-        if (start) TFG_HIP(hipMemcpyAsync(&chars, start + G, 8, hipMemcpyDeviceToHost, ctx->stream));
+        uint64_t *hp = ctx->host_pinned; // pinned words: one sync, no staging
+        TFG_HIP(hipMemcpyAsync(hp, g_dev, 16, hipMemcpyDeviceToHost, ctx->stream)); // count, kept rows
+        hp[2] = 0;
+        if (start) TFG_HIP(hipMemcpyAsync(hp + 2, start + G, 8, hipMemcpyDeviceToHost, ctx->stream));
         TFG_HIP(hipStreamSynchronize(ctx->stream));
+        const uint64_t cnt = hp[0], chars = hp[2];
         a->pend_total = cnt;
+        a->kept_rows = hp[1];
+        a->kept_n = a->consumed_n;
         a->pend_known = true;
         if (out_groups_host) *out_groups_host = cnt;
         if (out_chars_host) *out_chars_host = chars;

@@ -16,6 +16,8 @@ constexpr int BT = 512;      // bucket kernel threads (8 waves; 2-3 workgroups p
 constexpr int BT_BIG = 1024; // for tables too large for two workgroups per CU (16 waves)
 constexpr int LDS_TABLE_BYTES = 100 * 1024;  // preferred table size (two workgroups per CU)
 constexpr int LDS_TABLE_MAX = 150 * 1024;    // largest table (one 16-wave workgroup per CU)
+constexpr int LDS_CU_BYTES = 160 * 1024;     // gfx950 LDS per CU
+constexpr int BUCKET_STATIC_LDS_MAX = 13 * 1024; // upper bound of the bucket kernels' static LDS
 
 enum AccKind { ACC_NONE = 0, ACC_I64 = 1, ACC_F64 = 2, ACC_I128 = 3, ACC_I256 = 4, ACC_ORD = 5, ACC_REF = 6 };
 // 64-bit words of an accumulator of kind k
@@ -38,9 +40,11 @@ struct RefSrc {
     const uint64_t *o[2]; // String compare bytes: end offsets (row i = [o[i - 1], o[i]) with o[-1] = 0)
     uint64_t n0;          // store entries
     uint64_t n1;          // consumed rows (references n0 + 1 .. n0 + n1)
+    uint64_t nb[2];       // String compare bytes: bytes of v[i] when known (~0 otherwise)
     int width;            // fixed: 16 / 32 (signed little-endian limbs compared); 0 = String bytes
-    unsigned *err;        // |= 2 on a reference outside 1 .. n0 + n1 or a row without its '\0' (never
-                          // dereferenced; the call then fails with TFG_ERR_LOGICAL)
+    unsigned *err;        // |= 2 on a reference outside 1 .. n0 + n1 or a row without its '\0', |= 4 on
+                          // a row's bytes past nb (never dereferenced; the call then fails with
+                          // TFG_ERR_LOGICAL)
 };
 
 struct AggSpec {
@@ -196,6 +200,20 @@ __device__ __forceinline__ int ref_cmp(const RefSrc &R, uint64_t a, uint64_t b) 
     const uint64_t b0 = ib ? R.o[sb][ib - 1] : 0, b1 = R.o[sb][ib] - 1; // both rows end with it
     if (a1 + 1 <= a0 || b1 + 1 <= b0) { // a row of no bytes (no '\0'): malformed offsets
         if (R.err) atomicOr(R.err, 2u);
+        return 0;
+    }
+    if (a1 >= R.nb[sa] || b1 >= R.nb[sb]) { // a row past its buffer's bytes
+        const unsigned was = R.err ? atomicOr(R.err, 4u) : 4u;
+#ifdef TFG_EXP_POOL
+        if (!(was & 4u))
+            printf("EXP ref_cmp bound: a=%llu b=%llu n0=%llu n1=%llu a0=%llu a1=%llu nb=%llu b0=%llu b1=%llu nb=%llu "
+               "v=%p %p o=%p %p\n",
+               (unsigned long long)a, (unsigned long long)b, (unsigned long long)R.n0, (unsigned long long)R.n1,
+               (unsigned long long)a0, (unsigned long long)a1, (unsigned long long)R.nb[sa], (unsigned long long)b0,
+               (unsigned long long)b1, (unsigned long long)R.nb[sb], R.v[0], R.v[1], R.o[0], R.o[1]);
+#else
+        (void)was;
+#endif
         return 0;
     }
     const uint8_t *pa = R.v[sa] + a0, *pb = R.v[sb] + b0;

@@ -340,8 +340,7 @@ static int arith_wide(Ctx *ctx, int op, int a_type, const void *a, int a_is_cons
     }
     const int flags = (res_type == TFG_DECIMAL256 && (a_type == TFG_DECIMAL256 || b_type == TFG_DECIMAL256)) ? 1 : 0;
     if (n <= 0) return TFG_OK;
-    unsigned *flag = nullptr;
-    TFG_HIP(hipMalloc((void **)&flag, sizeof(unsigned)));
+    unsigned *flag = (unsigned *)(ctx->dev_counter + 62); // the context's own flag word (no allocation)
     TFG_HIP(hipMemsetAsync(flag, 0, sizeof(unsigned), ctx->stream));
     {
         ProfScope _ps(ctx, "arith.wide");
@@ -349,11 +348,9 @@ static int arith_wide(Ctx *ctx, int op, int a_type, const void *a, int a_is_cons
                            res_type, mul_div, flags, n, out, flag);
     }
     TFG_LAUNCH_CHECK();
-    unsigned ov = 0;
-    TFG_HIP(hipMemcpyAsync(&ov, flag, sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
-    TFG_HIP(hipStreamSynchronize(ctx->stream));
-    TFG_HIP(hipFree(flag));
-    TFG_CHECK(!ov, TFG_ERR_OVERFLOW, "Decimal math overflow");
+    uint64_t ov = 0;
+    if (int rc = read_back_u64(ctx, ctx->dev_counter + 62, &ov, 1)) return rc;
+    TFG_CHECK(!(unsigned)ov, TFG_ERR_OVERFLOW, "Decimal math overflow");
     return TFG_OK;
 }
 

@@ -25,12 +25,13 @@ inline bool collator_known(int collator) {
     return collator >= TFG_COLLATOR_NONE && collator <= TFG_COLLATOR_UCA0900_AI_CI;
 }
 
-// A collated column in stream-ordered device memory, freed (stream-ordered) with the object.
+// A collated column in the context's call arena (DevArena, common.h), held until the object dies.
 struct CollatedStrings {
     Ctx *ctx = nullptr;
     uint8_t *chars = nullptr;
     uint64_t *scan = nullptr; // n + 1 start offsets; offsets() = scan + 1 = end offsets
     int64_t rows = 0;
+    uint64_t bytes = 0; // sort-key bytes in `chars` (every row's key ends before it)
     const uint64_t *offsets() const { return scan + 1; }
     CollatedStrings() = default;
     CollatedStrings(const CollatedStrings &) = delete;

@@ -1,5 +1,8 @@
 // collation.hip — sort keys of the case-insensitive collators (see collation.h for the reference map).
+#include <cstdio>
+#include <cstdlib>
 #include <mutex>
+#include <vector>
 
 #include "collation.h"
 #include "collation_data.h"
@@ -96,19 +99,29 @@ __global__ void gci_len_kernel(const uint8_t *chars, const uint64_t *offsets, co
     }
 }
 
+// every row writes inside its slot [start[i], start[i + 1]) of the `total` bytes (the lengths
+// pass computed the slots): a scan that disagrees can never write outside the buffer
+__device__ __forceinline__ void put_byte(uint8_t *&o, const uint8_t *lim, uint8_t v) {
+    if (o < lim) *o = v;
+    ++o;
+}
+
 __global__ void gci_write_kernel(const uint8_t *chars, const uint64_t *offsets, const uint8_t *nullmap,
                                  const uint32_t *s32, const uint64_t *s64, int64_t n, bool whole, const uint64_t *start,
-                                 uint8_t *out) {
+                                 uint64_t total, uint8_t *out) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const RowSpan sp = row_span(chars, offsets, nullmap, pick(s32, s64, i), whole);
-        uint8_t *o = out + start[i];
+        const uint64_t b = start[i], e = start[i + 1];
+        if (b > e || e > total) continue;
+        uint8_t *o = out + b;
+        const uint8_t *lim = out + e;
         uint64_t off = 0;
         while (off < sp.len) {
             const uint32_t w = gci_weight(gci_runs_dev, decode_utf8(sp, off));
-            *o++ = (uint8_t)(w >> 8);
-            *o++ = (uint8_t)w;
+            put_byte(o, lim, (uint8_t)(w >> 8));
+            put_byte(o, lim, (uint8_t)w);
         }
-        *o = 0;
+        put_byte(o, lim, 0);
     }
 }
 
@@ -198,21 +211,24 @@ __global__ void uca_len_kernel(const uint8_t *chars, const uint64_t *offsets, co
 template <bool V0900>
 __global__ void uca_write_kernel(const uint8_t *chars, const uint64_t *offsets, const uint8_t *nullmap,
                                  const uint32_t *s32, const uint64_t *s64, int64_t n, bool whole, const uint64_t *start,
-                                 uint8_t *out) {
+                                 uint64_t total, uint8_t *out) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const RowSpan sp = uca_span<V0900>(chars, offsets, nullmap, pick(s32, s64, i), whole);
-        uint8_t *o = out + start[i];
+        const uint64_t b = start[i], e = start[i + 1];
+        if (b > e || e > total) continue;
+        uint8_t *o = out + b;
+        const uint8_t *lim = out + e;
         uint64_t off = 0;
         while (off < sp.len) {
             uint64_t w[2];
             if (!uca_weight<V0900>(decode_utf8(sp, off), w[0], w[1])) continue;
             for (int h = 0; h < 2; ++h)
                 for (uint64_t x = w[h]; x != 0; x >>= 16) {
-                    *o++ = (uint8_t)(x >> 8);
-                    *o++ = (uint8_t)x;
+                    put_byte(o, lim, (uint8_t)(x >> 8));
+                    put_byte(o, lim, (uint8_t)x);
                 }
         }
-        *o = 0;
+        put_byte(o, lim, 0);
     }
 }
 
@@ -233,48 +249,109 @@ int uca_ready(Ctx *ctx) {
 
 } // namespace
 
-// plain device allocations, freed once the stream is done with them (not the stream-ordered
-// pool: the C++ two-phase planner case faulted intermittently with pool-backed sort keys)
+// The sort keys and their scan live in the context's call arena (DevArena): no allocation in
+// steady state, and nothing to free — the arena is reused by the next call on the same stream.
+// TFG_EXP_POOL (experiment builds only): the stream-ordered pool of round 5 instead, with an
+// allocation log (TFG_POOLDBG=1) for the fault analysis of DESIGN §4.3.
+#ifdef TFG_EXP_POOL
+static bool pool_dbg() {
+    static const bool on = getenv("TFG_POOLDBG") != nullptr;
+    return on;
+}
+// Non-faulting form of the experiment: the pool never returns memory to the system (release
+// threshold = max), so a read after a free sees the poison written at the free (0xFF: offsets far
+// past every buffer, caught by ref_cmp's bounds) instead of an unmapped page; every block carries
+// 4 KB of canary after its bytes, checked at the free (an overrun by its own writer or a
+// neighbour's wild write)
+constexpr size_t CANARY = 4096;
+struct PoolBlock {
+    void *p;
+    size_t bytes;
+};
+static std::vector<PoolBlock> &pool_blocks() {
+    static std::vector<PoolBlock> v;
+    return v;
+}
+static bool pool_env(const char *name, bool dflt) {
+    const char *v = getenv(name);
+    return v && *v ? *v == '1' : dflt;
+}
+static int coll_alloc(Ctx *ctx, void **p, size_t bytes, const char *what) {
+    static bool once = [] {
+        if (!pool_env("TFG_POOL_KEEP", true)) return true; // the default threshold (0: trim at syncs)
+        hipMemPool_t pool;
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+            uint64_t thr = ~0ull;
+            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+        }
+        return true;
+    }();
+    (void)once;
+    TFG_HIP(hipMallocAsync(p, bytes + CANARY, ctx->stream));
+    TFG_HIP(hipMemsetAsync((char *)*p + bytes, 0xA5, CANARY, ctx->stream));
+    pool_blocks().push_back({*p, bytes});
+    if (pool_dbg()) fprintf(stderr, "POOL alloc %s %p +%zu (stream %p)\n", what, *p, bytes, (void *)ctx->stream);
+    return TFG_OK;
+}
+static void coll_free(Ctx *ctx, void *p, const char *what) {
+    if (!p) return;
+    size_t bytes = 0;
+    auto &v = pool_blocks();
+    for (size_t i = 0; i < v.size(); ++i)
+        if (v[i].p == p) {
+            bytes = v[i].bytes;
+            v.erase(v.begin() + (long)i);
+            break;
+        }
+    static const bool sync_check = pool_env("TFG_POOL_SYNCFREE", false); // the canary read-back syncs
+    std::vector<uint8_t> c(CANARY);
+    if (sync_check && hipMemcpyAsync(c.data(), (char *)p + bytes, CANARY, hipMemcpyDeviceToHost, ctx->stream) == hipSuccess &&
+        hipStreamSynchronize(ctx->stream) == hipSuccess) {
+        size_t bad = 0, first = CANARY;
+        for (size_t i = 0; i < CANARY; ++i)
+            if (c[i] != 0xA5) bad++, first = std::min(first, i);
+        if (bad) fprintf(stderr, "POOL CANARY %s %p +%zu: %zu bytes overwritten from +%zu\n", what, p, bytes, bad, first);
+    }
+    if (pool_dbg()) fprintf(stderr, "POOL free %s %p\n", what, p);
+    (void)hipMemsetAsync(p, 0xFF, bytes, ctx->stream); // poison: a later reader sees offsets past everything
+    (void)hipFreeAsync(p, ctx->stream);
+}
+#else
+static int coll_alloc(Ctx *ctx, void **p, size_t bytes, const char *) { return arena_alloc(ctx, bytes, p); }
+static void coll_free(Ctx *, void *, const char *) {}
+#endif
+
 CollatedStrings::~CollatedStrings() {
-    if (!ctx || (!chars && !scan)) return;
-    (void)hipStreamSynchronize(ctx->stream);
-    if (chars) (void)hipFree(chars);
-    if (scan) (void)hipFree(scan);
+    if (!ctx) return;
+    coll_free(ctx, chars, "chars");
+    coll_free(ctx, scan, "scan");
+    arena_drop(ctx);
 }
 
 int collate_strings(Ctx *ctx, int collator, const uint8_t *chars, const uint64_t *offsets, const uint8_t *nullmap,
                     const uint32_t *sel32, const uint64_t *sel64, int64_t n, CollatedStrings &out, bool whole) {
     TFG_CHECK(collator_transforms(collator), TFG_ERR_NOT_IMPLEMENTED, "collator %d has no sort-key transform",
               collator);
+    TFG_CHECK(!out.ctx, TFG_ERR_LOGICAL, "collated column reused");
     const bool uca = collator != TFG_COLLATOR_GENERAL_CI, v0900 = collator == TFG_COLLATOR_UCA0900_AI_CI;
     if (uca)
         if (int rc = uca_ready(ctx)) return rc;
     TFG_CHECK(n >= 0 && n <= ((int64_t)1 << 26), TFG_ERR_INVALID_ARG, "collated column of %lld rows", (long long)n);
+    arena_hold(ctx); // dropped by out's destructor
     out.ctx = ctx;
     out.rows = n;
-    TFG_HIP(hipMalloc((void **)&out.scan, (size_t)(n + 1) * 8));
+    if (int rc = coll_alloc(ctx, (void **)&out.scan, (size_t)(n + 1) * 8, "scan")) return rc;
     if (n == 0) {
         TFG_HIP(hipMemsetAsync(out.scan, 0, 8, ctx->stream));
-        TFG_HIP(hipMalloc((void **)&out.chars, 16));
-        return TFG_OK;
+        return coll_alloc(ctx, (void **)&out.chars, 16, "chars");
     }
     TFG_CHECK(chars && offsets, TFG_ERR_INVALID_ARG, "String column needs its chars and offsets");
-    // the lengths and the scan's work space: freed after the total's read-back (their users done)
-    struct Tmp { // error paths: wait for the stream, then free
-        hipStream_t st;
-        void *p[2];
-        void release() {
-            for (void *&q : p)
-                if (q) (void)hipFree(q), q = nullptr;
-        }
-        ~Tmp() {
-            if (p[0] || p[1]) (void)hipStreamSynchronize(st);
-            release();
-        }
-    } tm{ctx->stream, {nullptr, nullptr}};
+    // the lengths and the scan's work space (dead after the total's read-back)
     uint64_t *len = nullptr;
-    TFG_HIP(hipMalloc((void **)&len, (size_t)n * 8));
-    tm.p[0] = len;
+    void *tmp = nullptr;
+    if (int rc = coll_alloc(ctx, (void **)&len, (size_t)n * 8, "len")) return rc;
     const unsigned grid = stream_grid(n, 256, 4096);
     if (!uca)
         hipLaunchKernelGGL(gci_len_kernel, dim3(grid), dim3(256), 0, ctx->stream, chars, offsets, nullmap, sel32, sel64,
@@ -286,23 +363,23 @@ int collate_strings(Ctx *ctx, int collator, const uint8_t *chars, const uint64_t
         hipLaunchKernelGGL(uca_len_kernel<false>, dim3(grid), dim3(256), 0, ctx->stream, chars, offsets, nullmap, sel32,
                            sel64, n, whole, len);
     TFG_LAUNCH_CHECK();
-    void *tmp = nullptr;
-    TFG_HIP(hipMalloc(&tmp, scan_tmp_bytes(n) + 256));
-    tm.p[1] = tmp;
+    if (int rc = coll_alloc(ctx, &tmp, scan_tmp_bytes(n) + 256, "tmp")) return rc;
     if (int rc = exclusive_scan_u64(ctx, len, out.scan, n, tmp)) return rc;
     uint64_t total = 0;
     if (int rc = read_back_u64(ctx, out.scan + n, &total, 1)) return rc; // synchronizes the stream
-    tm.release(); // their last users (the length kernel, the scan) are done
-    TFG_HIP(hipMalloc((void **)&out.chars, total + 16));
+    coll_free(ctx, len, "len");
+    coll_free(ctx, tmp, "tmp");
+    if (int rc = coll_alloc(ctx, (void **)&out.chars, total + 16, "chars")) return rc;
+    out.bytes = total;
     if (!uca)
         hipLaunchKernelGGL(gci_write_kernel, dim3(grid), dim3(256), 0, ctx->stream, chars, offsets, nullmap, sel32, sel64,
-                           n, whole, out.scan, out.chars);
+                           n, whole, out.scan, total, out.chars);
     else if (v0900)
         hipLaunchKernelGGL(uca_write_kernel<true>, dim3(grid), dim3(256), 0, ctx->stream, chars, offsets, nullmap, sel32,
-                           sel64, n, whole, out.scan, out.chars);
+                           sel64, n, whole, out.scan, total, out.chars);
     else
         hipLaunchKernelGGL(uca_write_kernel<false>, dim3(grid), dim3(256), 0, ctx->stream, chars, offsets, nullmap, sel32,
-                           sel64, n, whole, out.scan, out.chars);
+                           sel64, n, whole, out.scan, total, out.chars);
     TFG_LAUNCH_CHECK();
     return TFG_OK;
 }

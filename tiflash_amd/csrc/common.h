@@ -60,11 +60,28 @@ struct ProfTotal {
     uint64_t count = 0;
 };
 
+// Device buffers that live for one call but whose sizes are known only inside it (collated sort
+// keys, their scans): carved from chunks the context keeps, so steady-state calls never allocate.
+// Every buffer of a call holds the arena (ArenaHold); when the last hold is dropped the arena is
+// empty again — its chunks are reused by the next call, whose kernels run after this call's on the
+// same stream.  The first call that outgrows the chunks adds one; at the next reset the chunks
+// are merged into one (a sync + free then, never in steady state).
+struct DevArena {
+    struct Chunk {
+        char *p;
+        size_t cap;
+    };
+    std::vector<Chunk> chunks;
+    size_t cur = 0, off = 0; // bump position: chunk `cur`, byte `off`
+    int holds = 0;
+};
+
 struct Ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     void *scratch = nullptr;
     size_t scratch_bytes = 0;
+    DevArena arena;
     uint64_t *dev_counter = nullptr; // small device scratch for counts (64 x u64)
     uint64_t *host_pinned = nullptr; // pinned host words for count read-back
     int cu_count = 256;
@@ -87,6 +104,19 @@ int prof_resolve(Ctx *ctx);
 // Returns a device pointer to at least `bytes` of scratch (grows the arena; growth syncs the
 // stream).  The region is reused by the next call: callers carve it, never keep it.
 int scratch_get(Ctx *ctx, size_t bytes, void **out);
+
+// The call arena (DevArena): arena_alloc needs a hold; arena_hold / arena_drop count the holds.
+int arena_alloc(Ctx *ctx, size_t bytes, void **out);
+void arena_hold(Ctx *ctx);
+void arena_drop(Ctx *ctx);
+void arena_free_all(Ctx *ctx); // context teardown (the stream synchronized)
+struct ArenaScope {
+    Ctx *c;
+    explicit ArenaScope(Ctx *ctx) : c(ctx) { arena_hold(c); }
+    ~ArenaScope() { arena_drop(c); }
+    ArenaScope(const ArenaScope &) = delete;
+    ArenaScope &operator=(const ArenaScope &) = delete;
+};
 
 struct Carver {
     size_t off = 0;

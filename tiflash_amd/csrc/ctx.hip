@@ -96,6 +96,53 @@ int scratch_get(Ctx *ctx, size_t bytes, void **out) {
     return TFG_OK;
 }
 
+void arena_hold(Ctx *ctx) { ++ctx->arena.holds; }
+
+void arena_free_all(Ctx *ctx) {
+    for (auto &c : ctx->arena.chunks) (void)hipFree(c.p);
+    ctx->arena = DevArena{};
+}
+
+void arena_drop(Ctx *ctx) {
+    DevArena &A = ctx->arena;
+    if (--A.holds > 0) return;
+    A.holds = 0;
+    A.cur = A.off = 0;
+    if (A.chunks.size() > 1) { // outgrown during the call: one chunk of the high-water size
+        size_t total = 0;
+        for (auto &c : A.chunks) total += c.cap;
+        (void)hipStreamSynchronize(ctx->stream);
+        arena_free_all(ctx);
+        void *p = nullptr;
+        if (hipMalloc(&p, total) == hipSuccess) A.chunks.push_back({(char *)p, total});
+    }
+}
+
+int arena_alloc(Ctx *ctx, size_t bytes, void **out) {
+    DevArena &A = ctx->arena;
+    TFG_CHECK(A.holds > 0, TFG_ERR_LOGICAL, "arena_alloc without a hold");
+    bytes = (std::max<size_t>(bytes, 1) + 255) & ~size_t(255);
+    while (A.cur < A.chunks.size()) {
+        DevArena::Chunk &c = A.chunks[A.cur];
+        if (A.off + bytes <= c.cap) {
+            *out = c.p + A.off;
+            A.off += bytes;
+            return TFG_OK;
+        }
+        ++A.cur;
+        A.off = 0;
+    }
+    size_t cap = std::max<size_t>(bytes, (size_t)4 << 20);
+    for (auto &c : A.chunks) cap = std::max(cap, c.cap); // at least double the arena
+    void *p = nullptr;
+    TFG_HIP(hipMalloc(&p, cap));
+    A.chunks.push_back({(char *)p, cap});
+    A.cur = A.chunks.size() - 1;
+    A.off = bytes;
+    *out = p;
+    return TFG_OK;
+}
+
 static hipEvent_t prof_take(Ctx *ctx) {
     if (!ctx->prof_pool.empty()) {
         hipEvent_t e = ctx->prof_pool.back();
@@ -244,6 +291,29 @@ __global__ void __launch_bounds__(SCAN_T) scan_apply_kernel(const TIn *in, uint6
     }
 }
 
+// n <= SCAN_T * SMALL_I: one workgroup scans everything (one launch instead of three)
+constexpr int SMALL_I = 16;
+template <typename TIn>
+__global__ void __launch_bounds__(SCAN_T) scan_small_kernel(const TIn *in, uint64_t *out, int64_t n) {
+    __shared__ uint64_t lds[64];
+    const int64_t base = (int64_t)threadIdx.x * SMALL_I;
+    uint64_t v[SMALL_I];
+    uint64_t s = 0;
+#pragma unroll
+    for (int i = 0; i < SMALL_I; ++i) {
+        v[i] = base + i < n ? (uint64_t)in[base + i] : 0;
+        s += v[i];
+    }
+    uint64_t tot;
+    uint64_t off = block_scan_excl<uint64_t>(s, lds, &tot);
+#pragma unroll
+    for (int i = 0; i < SMALL_I; ++i) {
+        if (base + i < n) out[base + i] = off;
+        off += v[i];
+    }
+    if (threadIdx.x == 0) out[n] = tot;
+}
+
 size_t scan_tmp_bytes(int64_t n) {
     int64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
     return (size_t)(nb + 1) * sizeof(uint64_t) + 256;
@@ -255,6 +325,12 @@ template <typename TIn> static int scan_impl(Ctx *ctx, const TIn *in, uint64_t *
     int64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
     if (nb == 0) {
         TFG_HIP(hipMemsetAsync(out, 0, sizeof(uint64_t), ctx->stream));
+        return TFG_OK;
+    }
+    if (n <= (int64_t)SCAN_T * SMALL_I) {
+        ProfScope _ps(ctx, "scan");
+        hipLaunchKernelGGL(scan_small_kernel<TIn>, dim3(1), dim3(SCAN_T), 0, ctx->stream, in, out, n);
+        TFG_LAUNCH_CHECK();
         return TFG_OK;
     }
     uint64_t *bs = (uint64_t *)tmp;
@@ -328,6 +404,7 @@ int tfg_ctx_destroy(tfg_ctx *ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     else (void)hipDeviceSynchronize();
     if (ctx->scratch) (void)hipFree(ctx->scratch);
+    arena_free_all(ctx);
     for (auto &e : ctx->prof_pending) {
         (void)hipEventDestroy(e.start);
         (void)hipEventDestroy(e.stop);
@@ -341,6 +418,9 @@ int tfg_ctx_destroy(tfg_ctx *ctx) {
 
 int tfg_ctx_set_stream(tfg_ctx *ctx, void *stream) {
     TFG_CHECK(ctx, TFG_ERR_INVALID_ARG, "ctx is null");
+    // the scratch and the call arena are reused in stream order: the old stream's last readers
+    // finish before the new stream's first writers start
+    if ((hipStream_t)stream != ctx->stream) TFG_HIP(hipStreamSynchronize(ctx->stream));
     ctx->stream = (hipStream_t)stream;
     return TFG_OK;
 }

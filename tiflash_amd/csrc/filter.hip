@@ -475,8 +475,10 @@ int tfg_filter_string(tfg_ctx *ctx, const uint8_t *mask, int64_t n, const uint8_
     Carver cv;
     size_t o_lens = cv.take<uint64_t>(n), o_starts = cv.take<uint64_t>(n + 1), o_ends = cv.take<uint64_t>(n);
     size_t o_tmp = cv.take<uint8_t>(scan_tmp_bytes(n));
+    ArenaScope hold(ctx); // the call's buffers: reused by the next call on this stream, never freed here
     uint64_t *mine;
-    if (int rc = tfg_buf_alloc(ctx, cv.off, (void **)&mine)) return rc;
+    if (int rc = set_device(ctx)) return rc;
+    if (int rc = arena_alloc(ctx, cv.off, (void **)&mine)) return rc;
     char *sb = (char *)mine;
     uint64_t *lens = (uint64_t *)(sb + o_lens), *starts = (uint64_t *)(sb + o_starts), *ends = (uint64_t *)(sb + o_ends);
     unsigned grid = stream_grid(n, 256, 8192);
@@ -499,8 +501,6 @@ int tfg_filter_string(tfg_ctx *ctx, const uint8_t *mask, int64_t n, const uint8_
             if (!rc && out_bytes_host) rc = read_back_u64(ctx, starts + n, out_bytes_host, 1);
         }
     }
-    (void)hipStreamSynchronize(ctx->stream);
-    (void)hipFree(mine);
     return rc;
 }
 
@@ -515,8 +515,10 @@ int tfg_gather_string(tfg_ctx *ctx, const uint32_t *perm, int64_t n, const uint8
     Carver cv;
     size_t o_lens = cv.take<uint64_t>(n), o_starts = cv.take<uint64_t>(n + 1);
     size_t o_tmp = cv.take<uint8_t>(scan_tmp_bytes(n));
+    ArenaScope hold(ctx); // the call's buffers: reused by the next call on this stream, never freed here
     uint64_t *mine;
-    if (int rc = tfg_buf_alloc(ctx, cv.off, (void **)&mine)) return rc;
+    if (int rc = set_device(ctx)) return rc;
+    if (int rc = arena_alloc(ctx, cv.off, (void **)&mine)) return rc;
     char *sb = (char *)mine;
     uint64_t *lens = (uint64_t *)(sb + o_lens), *starts = (uint64_t *)(sb + o_starts);
     const unsigned grid = stream_grid(n, 256, 8192);
@@ -537,8 +539,6 @@ int tfg_gather_string(tfg_ctx *ctx, const uint32_t *perm, int64_t n, const uint8
             hipLaunchKernelGGL(string_gather_copy_kernel, dim3(stream_grid(n * 64, 256, 8192)), dim3(256), 0,
                                ctx->stream, perm, chars, offsets, n, starts, out_chars);
     }
-    (void)hipStreamSynchronize(ctx->stream);
-    (void)hipFree(mine);
     return rc;
 }
 

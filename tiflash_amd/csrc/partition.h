@@ -606,6 +606,62 @@ constexpr int ST_MAXR = 8;     // rows per thread per tile (TR <= 8192 < 2^16: r
 // tiles a round in the sparse variant's all-false check (four measured slower: 0 % C2 0.364 vs
 // 0.344 ms, r05ad — not memory-level parallelism but the per-round barriers bound it)
 constexpr int SKIP_NT = 2;
+constexpr int FLAG_TPS_MAX = 512; // tiles a segment may have for the tile-flag pre-pass
+
+// tile_flags[g * tps + k] = does tile k of segment g keep a row?  One 256-thread workgroup a tile,
+// its predicate words read as 16-byte vectors (a full, aligned tile) or row by row, all in flight
+// together: the predicate column streams at HBM rate across the whole chip (the partition kernel,
+// one workgroup a CU walking its tiles in turn, reads it at ~3.3 TB/s)
+constexpr int TF_T = 256;
+template <typename Pred>
+__global__ void __launch_bounds__(TF_T) tile_flags_kernel(Pred pred, PartLayout L, int TR, int tps, uint8_t *flags) {
+    const uint32_t gseg = blockIdx.x / (uint32_t)tps, k = blockIdx.x % (uint32_t)tps;
+    const int64_t begin = (int64_t)gseg * L.seg, end = std::min<int64_t>(begin + L.seg, L.n);
+    const int64_t tb = begin + (int64_t)k * TR, te = std::min<int64_t>(tb + TR, end);
+    bool any = false;
+    if (tb < te) {
+        if constexpr (PredVec<Pred>::ok) {
+            using E = typename PredVec<Pred>::E;
+            constexpr int EPW = 16 / (int)sizeof(E);
+            const E *col = reinterpret_cast<const E *>(pred.col);
+            const bool vec = ((((uintptr_t)(col + tb)) & 15) == 0);
+            const int64_t nv = vec ? (te - tb) / EPW : 0; // whole 16-byte words
+            const uint4 *w = reinterpret_cast<const uint4 *>(col + tb);
+            constexpr int WB = 8;
+            for (int64_t i0 = threadIdx.x; i0 < nv && !any; i0 += (int64_t)WB * TF_T) {
+                uint4 x[WB];
+#pragma unroll
+                for (int q = 0; q < WB; ++q)
+                    if (i0 + (int64_t)q * TF_T < nv) x[q] = w[i0 + (int64_t)q * TF_T];
+#pragma unroll
+                for (int q = 0; q < WB; ++q) {
+                    if (i0 + (int64_t)q * TF_T >= nv) continue;
+                    uint64_t b[4];
+                    int nb;
+                    if constexpr (sizeof(E) == 8) {
+                        b[0] = (uint64_t)x[q].x | ((uint64_t)x[q].y << 32);
+                        b[1] = (uint64_t)x[q].z | ((uint64_t)x[q].w << 32);
+                        nb = 2;
+                    } else {
+                        b[0] = x[q].x, b[1] = x[q].y, b[2] = x[q].z, b[3] = x[q].w;
+                        nb = 4;
+                    }
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        if (e >= nb) break;
+                        Loaded l{b[e], 0u};
+                        any |= pred.eval(l);
+                    }
+                }
+            }
+            for (int64_t r = tb + nv * EPW + threadIdx.x; r < te; r += TF_T) any |= pred.eval(pred.load(r));
+        } else {
+            for (int64_t r = tb + threadIdx.x; r < te; r += TF_T) any |= pred.eval(pred.load(r));
+        }
+    }
+    any = __syncthreads_or(any);
+    if (threadIdx.x == 0) flags[blockIdx.x] = any ? 1 : 0;
+}
 
 struct StagedGeom {
     int TR;          // rows per tile (multiple of ST_T)
@@ -630,6 +686,13 @@ struct StagedGeom {
     int fine_bits;
     int fh_off;
     uint32_t *fine_counts;
+    // TILED: two words the next kernel (the bucket kernel's cursors) needs zeroed — written by
+    // workgroup 0 here instead of by a memset launch of their own
+    unsigned long long *zero2;
+    // VSKIP with flags: tile_flags[t] = tile t keeps a row (tile_flags_kernel, a pass of its own
+    // over the predicate column with every workgroup of the chip), so all-false tiles are skipped
+    // without reading a word of theirs in this kernel
+    const uint8_t *tile_flags;
     int allow_narrow; // TILED narrow tiles (u32 keys) permitted: consumers that read records
                       // word by word (regroup_scatter_kernel) need the wide form
 };
@@ -663,6 +726,8 @@ inline bool make_staged_geom(uint32_t P, const PCols &cols, bool perm, bool crc,
     g.fh_off = g.red_off + (ST_T / 64 + 2) * 4; // red[]: per-wave sums + the tile total
     g.fine_bits = fine_bits;
     g.fine_counts = nullptr;
+    g.zero2 = nullptr;
+    g.tile_flags = nullptr;
     g.allow_narrow = 1;
     g.lds_bytes = g.fh_off + (int)fh_bytes;
     return true;
@@ -686,6 +751,8 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
     uint32_t *red = reinterpret_cast<uint32_t *>(lds + g.red_off); // ST_T/64 + 1 words
     if constexpr (!TILED)
         for (uint32_t p = threadIdx.x; p < P; p += ST_T) run[p] = offs[(int64_t)p * L.G + blockIdx.x];
+    if constexpr (TILED)
+        if (g.zero2 && blockIdx.x == 0 && threadIdx.x < 2) g.zero2[threadIdx.x] = 0ull;
     if constexpr (Sel::needs_crc) load_crc_lds(crc);
     // row indices fit 32 bits (the ABI caps n below 2^32)
     const uint32_t begin = (uint32_t)((int64_t)blockIdx.x * L.seg);
@@ -704,9 +771,19 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
     // predicate are checked with vector loads (16-byte aligned column and segment start).  Not
     // the default: the extra live state spills 6 VGPRs of the kept-row path (partition +2 %, r05q)
     const bool skip_vec = VSKIP && TILED && PredVec<Pred>::ok && pred_vec_aligned(pred, begin);
+    __shared__ uint8_t s_flags[VSKIP ? FLAG_TPS_MAX : 1];
+    if constexpr (VSKIP) {
+        if (g.tile_flags) { // this segment's tile flags (the host checks tps <= FLAG_TPS_MAX)
+            for (int k = threadIdx.x; k < g.tps; k += ST_T) s_flags[k] = g.tile_flags[(size_t)blockIdx.x * g.tps + k];
+            __syncthreads();
+            spec = false; // the first tile is checked too
+        }
+    }
     for (uint32_t tb = begin; tb < end; tb += (uint32_t)g.TR) {
         if constexpr (TILED) {
-            if (!spec) {
+            bool use_flags = false;
+            if constexpr (VSKIP) use_flags = g.tile_flags != nullptr;
+            if (!spec || use_flags) {
                 // the previous tile kept no row: skip ahead over tiles whose predicate keeps
                 // nothing — one predicate read and one barrier each, their runs written empty —
                 // to the next tile that keeps a row (FilterTransformAction.cpp:134-138).  (Two
@@ -714,6 +791,11 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
                 // the partition kernel ran out of VGPRs, r05k)
                 while (tb < end) {
                     if constexpr (VSKIP) {
+                        if (g.tile_flags) { // one LDS byte a tile (loaded at the start), no barrier
+                            if (s_flags[(tb - begin) / (uint32_t)g.TR]) break;
+                            tb += (uint32_t)g.TR;
+                            continue;
+                        }
                         if (skip_vec && tb + (uint32_t)SKIP_NT * (uint32_t)g.TR <= end) {
                             // SKIP_NT whole tiles a round, all their words in flight together
                             bool a[SKIP_NT];
@@ -749,7 +831,7 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
                     tb += (uint32_t)g.TR;
                 }
                 if (tb >= end) break;
-                spec = true; // this tile keeps a row
+                spec = !use_flags; // this tile keeps a row (with flags: its keys load for kept rows only)
             }
         }
         for (uint32_t p = threadIdx.x; p < P; p += ST_T) hist[p] = 0;
@@ -1133,7 +1215,7 @@ inline bool make_tiled_geom(Ctx *ctx, int64_t n, uint32_t P, const PCols &cols, 
 // than it has tiles): plain column predicates take the vector all-false check (VSKIP)
 template <typename Sel>
 int run_partition_tiled(Ctx *ctx, const Sel &sel, const RowPred &pred, TiledGeom tg, const PCols &cols,
-                        uint32_t *tile_hist, const char *name, bool sparse = false) {
+                        uint32_t *tile_hist, const char *name, bool sparse = false, uint8_t *flags = nullptr) {
     tg.sg.tile_hist = tile_hist;
     int nc8 = cols.ncols;
     for (int c = 0; c < cols.ncols; ++c)
@@ -1146,6 +1228,12 @@ int run_partition_tiled(Ctx *ctx, const Sel &sel, const RowPred &pred, TiledGeom
             if (sparse) {
                 // skipped tiles leave their (destination, tile) entries to this memset
                 TFG_HIP(hipMemsetAsync(tg.sg.tile_hist, 0, (size_t)tg.L.P * tg.sg.T * 4, ctx->stream));
+                if (flags && tg.sg.tps <= FLAG_TPS_MAX) { // every tile's "keeps a row" first
+                    hipLaunchKernelGGL((tile_flags_kernel<PR>), dim3((unsigned)tg.sg.T), dim3(TF_T), 0, ctx->stream, pr,
+                                       tg.L, tg.sg.TR, tg.sg.tps, flags);
+                    TFG_LAUNCH_CHECK();
+                    tg.sg.tile_flags = flags;
+                }
                 if (nc8 == 1)
                     hipLaunchKernelGGL((part_scatter_staged_kernel<Sel, PR, 1, true, true, true>), dim3(tg.L.G),
                                        dim3(ST_T), tg.sg.lds_bytes, ctx->stream, sel, pr, tg.L,

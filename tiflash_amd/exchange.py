@@ -45,14 +45,31 @@ def _row_bytes(c: torch.Tensor, n: int) -> torch.Tensor:
 
 
 _CTX = {}
-_COMMS = {}
+
+
+class _Comm:
+    """A tfg_comm owned by its context: destroyed by Context.close() (before tfg_ctx_destroy), so
+    no communicator outlives the stream it enqueues on."""
+
+    def __init__(self, h, group):
+        self.h = h
+        self.group = group  # held: the cache key is id(group), which must not be reused while we live
+
+    def close(self):
+        import tiflash_amd as tfa
+        if self.h is not None and self.h.value:
+            tfa.lib().tfg_comm_destroy(self.h)
+        self.h = None
 
 
 def _tfg_comm(ctx, group):
-    """The tfg_comm (RCCL communicator) of a process group on a context; collective on first use."""
+    """The tfg_comm (RCCL communicator) of a process group on a context; collective on first use.
+    Cached on the context object itself (ctx._comms), so a closed context's communicators are gone
+    with it and a new context never finds a stale one."""
     import tiflash_amd as tfa
-    key = (id(group), ctx.h.value)
-    if key not in _COMMS:
+    comms = ctx.__dict__.setdefault("_comms", {})
+    key = id(group)
+    if key not in comms:
         world, rank = dist.get_world_size(group), dist.get_rank(group)
         uid = (ctypes.c_uint8 * 128)()
         if rank == 0:
@@ -64,8 +81,10 @@ def _tfg_comm(ctx, group):
         h = ctypes.c_void_p()
         tfa.check(tfa.lib().tfg_comm_init(ctx.h, ctypes.c_int(world), ctypes.c_int(rank), buf, ctypes.c_size_t(128),
                                           ctypes.byref(h)))
-        _COMMS[key] = h
-    return _COMMS[key]
+        c = _Comm(h, group)
+        comms[key] = c
+        ctx._children.add(c)
+    return comms[key].h
 
 
 class _Slice(ctypes.Structure):  # tfg_slice
@@ -212,12 +231,31 @@ def two_phase_merge_keys(ctx, partial, final, group=None, collators=None):
     (C5): the partial aggregation's rows are routed by the reference's hash of the key columns
     (IColumn::updateWeakHash32 -> fillSelector, HashBaseWriterHelper.cpp:46-84) and the final
     aggregation merges them (mergeOnBlock).  Keys travel packed (16 bytes) while the partial
-    aggregator holds them packed; once it has moved to the serialized method (a String sort key
-    over 15 bytes, String + fixed keys, wide tuples) they travel as their key columns — Strings
-    as chars + lengths — with the states, still in one data all-to-all.  `partial` and `final`
-    are tiflash_amd.KeysAggregator objects of the same signature."""
+    aggregator holds them packed: its result is written ONCE, packed, and the weak hash of the key
+    columns is computed from the packed keys (tfg_agg_weak_hash_packed) — no unpacked copy of the
+    partial groups.  Once it has moved to the serialized method (a String sort key over 15 bytes,
+    String + fixed keys, wide tuples), or a state is a String (min / max / first_row of a String),
+    the groups travel as their key columns — Strings as chars + lengths — with the states, still in
+    one data all-to-all.  `partial` and `final` are tiflash_amd.KeysAggregator objects of the same
+    signature."""
     import tiflash_amd as tfa
     world = dist.get_world_size(group)
+    str_states = any((t & 0xFF) == tfa.STRING and k in (tfa.AGG_MIN, tfa.AGG_MAX, tfa.AGG_FIRST_ROW)
+                     for k, t in partial.aggs)  # the type word's low byte (collator / precision above)
+    if partial.holds_packed() and not str_states:
+        packed = partial.result_packed()
+        keys16 = packed["keys"]
+        n = keys16.shape[0]
+        h = torch.empty(n, dtype=torch.int32, device=keys16.device)
+        tfa.check(tfa.lib().tfg_weak_hash_init(ctx.h, tfa._p(h), tfa.ctypes.c_int64(n)))
+        partial.weak_hash_packed(keys16, h)
+        sel = tfa.fill_selector(ctx, h, world)
+        perm, offs = tfa.partition(ctx, sel, world)
+        ns = len(packed["states"])
+        send = tfa.gather(ctx, perm, [keys16] + list(packed["states"]) + list(packed["state_null"]))
+        recv = exchange_partitions(send, offs, group, ctx)
+        final.consume_partial_packed(recv[0], recv[1:1 + ns], state_nullmaps=recv[1 + ns:])
+        return
     cols = partial.result()
     n = partial.size()
     dev = cols["key_null"][0].device
@@ -230,20 +268,6 @@ def two_phase_merge_keys(ctx, partial, final, group=None, collators=None):
             tfa.weak_hash(ctx, [k], types=[t], nullmaps=[kn], h=h)
     sel = tfa.fill_selector(ctx, h, world)
     perm, offs = tfa.partition(ctx, sel, world)
-    try:
-        packed = partial.result_packed()
-    except tfa.TfgError as e:
-        if e.code != -4:  # NOT_IMPLEMENTED: the serialized method has no packed form
-            raise
-        packed = None
-    if packed is not None and any(isinstance(st, (tuple, list)) for st in packed["states"]):
-        packed = None  # String states travel as offsets + chars (below)
-    if packed is not None:
-        ns = len(packed["states"])
-        send = tfa.gather(ctx, perm, [packed["keys"]] + list(packed["states"]) + list(packed["state_null"]))
-        recv = exchange_partitions(send, offs, group, ctx)
-        final.consume_partial_packed(recv[0], recv[1:1 + ns], state_nullmaps=recv[1 + ns:])
-        return
     fixed = [k for t, k in zip(partial.key_types, cols["keys"]) if t != tfa.STRING]
     strings = [k for t, k in zip(partial.key_types, cols["keys"]) if t == tfa.STRING]
     # String states (min / max / first_row of a String) travel like String keys: offsets + chars
