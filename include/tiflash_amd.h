@@ -219,6 +219,9 @@ int tfg_upload(tfg_ctx *ctx, void *dst_dev, const void *src_host, size_t bytes);
 int tfg_download(tfg_ctx *ctx, void *dst_host, const void *src_dev, size_t bytes);
 /* Device-to-device copy, asynchronous on the context's stream (column concatenation / COW copies). */
 int tfg_copy(tfg_ctx *ctx, void *dst_dev, const void *src_dev, size_t bytes);
+/* Device memset on the context's stream (asynchronous): `bytes` bytes of dst_dev set to `value`
+ * (e.g. a received column's null map before the slices that carry one land in it). */
+int tfg_memset(tfg_ctx *ctx, void *dst_dev, int value, size_t bytes);
 
 /* Size in bytes of one value of `type`, 0 if unknown. */
 size_t tfg_type_width(int type);

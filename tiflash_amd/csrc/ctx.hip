@@ -496,6 +496,14 @@ int tfg_copy(tfg_ctx *ctx, void *dst_dev, const void *src_dev, size_t bytes) {
     return TFG_OK;
 }
 
+int tfg_memset(tfg_ctx *ctx, void *dst_dev, int value, size_t bytes) {
+    TFG_CHECK(ctx, TFG_ERR_INVALID_ARG, "ctx is null");
+    if (!bytes) return TFG_OK;
+    TFG_CHECK(dst_dev, TFG_ERR_INVALID_ARG, "null buffer");
+    TFG_HIP(hipMemsetAsync(dst_dev, value, bytes, ctx->stream));
+    return TFG_OK;
+}
+
 int tfg_download(tfg_ctx *ctx, void *dst_host, const void *src_dev, size_t bytes) {
     TFG_CHECK(ctx, TFG_ERR_INVALID_ARG, "ctx is null");
     if (!bytes) return TFG_OK;

@@ -298,8 +298,7 @@ Block concatenateBlocks(Context &ctx, const std::vector<Block> &blocks) {
                 if (c.nullmap) {
                     check(tfg_copy(ctx.raw(), (char *)col->nullmap->data() + r0, c.nullmap->data(), c.rows), "tfg_copy");
                 } else if (c.rows) {
-                    std::vector<uint8_t> z(c.rows, 0);
-                    check(tfg_upload(ctx.raw(), (char *)col->nullmap->data() + r0, z.data(), c.rows), "tfg_upload");
+                    check(tfg_memset(ctx.raw(), (char *)col->nullmap->data() + r0, 0, c.rows), "tfg_memset");
                 }
                 r0 += c.rows;
             }

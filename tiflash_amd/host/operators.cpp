@@ -362,8 +362,7 @@ void Aggregator::insertAggregateColumns(Block &out, const std::vector<std::share
         auto c = std::make_shared<IColumn>(*k); // shares the key's buffers
         c->type.nullable = true;
         c->nullmap = std::make_shared<DeviceBuffer>(ctx_, std::max<size_t>(g, 1));
-        const std::vector<uint8_t> zero(std::max<size_t>(g, 1), 0);
-        check(tfg_upload(ctx_.raw(), c->nullmap->data(), zero.data(), zero.size()), "tfg_upload");
+        check(tfg_memset(ctx_.raw(), c->nullmap->data(), 0, std::max<size_t>(g, 1)), "tfg_memset");
         out.insert({c, c->type, name});
     }
 }
@@ -554,8 +553,7 @@ Block Join::joinBlockWithCondition(const Block &probe_block) {
         f.transform(tmp, mask, /*return_filter=*/true); // Nullable(UInt8) folded: v && !null
         if (!tmp) { // constant false: no pair passes
             pass = std::make_shared<DeviceBuffer>(ctx_, count);
-            std::vector<uint8_t> z(count, 0);
-            check(tfg_upload(ctx_.raw(), pass->data(), z.data(), count), "tfg_upload");
+            check(tfg_memset(ctx_.raw(), pass->data(), 0, count), "tfg_memset");
         } else if (mask) {
             pass = mask->data;
         }
@@ -567,8 +565,7 @@ Block Join::joinBlockWithCondition(const Block &probe_block) {
         return filterByMask(ctx_, joined, pass, count);
     }
     auto flags = std::make_shared<DeviceBuffer>(ctx_, std::max<size_t>(n, 1));
-    std::vector<uint8_t> zeros(std::max<size_t>(n, 1), 0);
-    check(tfg_upload(ctx_.raw(), flags->data(), zeros.data(), zeros.size()), "tfg_upload");
+    check(tfg_memset(ctx_.raw(), flags->data(), 0, std::max<size_t>(n, 1)), "tfg_memset");
     check(tfg_join_mark(ctx_.raw(), (const uint32_t *)pi->data(), pass ? (const uint8_t *)pass->data() : nullptr,
                         (int64_t)count, (uint8_t *)flags->data()),
           "tfg_join_mark");
@@ -592,7 +589,7 @@ Block Join::joinBlockWithCondition(const Block &probe_block) {
         m->rows = n;
         m->data = kind_ == JoinKind::LeftOuterSemi ? flags : notflags;
         m->nullmap = std::make_shared<DeviceBuffer>(ctx_, std::max<size_t>(n, 1));
-        check(tfg_upload(ctx_.raw(), m->nullmap->data(), zeros.data(), zeros.size()), "tfg_upload");
+        check(tfg_memset(ctx_.raw(), m->nullmap->data(), 0, std::max<size_t>(n, 1)), "tfg_memset");
         out.insert({m, i8, match_helper_});
         ctx_.sync();
         return out;
@@ -1011,10 +1008,8 @@ Block MPPExchange::exchange(const std::vector<Block> &partitions) {
             c->nullmap = std::make_shared<DeviceBuffer>(ctx_, std::max<uint64_t>(total, 1));
             bool partial = false; // a source without a null map leaves its rows zero (not NULL)
             for (int p = 0; p < P; ++p) partial |= recv_cnt[(size_t)p * K + nul_of[j]] != recv_cnt[(size_t)p * K];
-            if (partial && total) {
-                const std::vector<uint8_t> zero(total, 0);
-                check(tfg_upload(ctx_.raw(), c->nullmap->data(), zero.data(), total), "tfg_upload");
-            }
+            if (partial && total) // a device memset, ordered before the slices that land on it
+                check(tfg_memset(ctx_.raw(), c->nullmap->data(), 0, total), "tfg_memset");
         }
         outc[j] = c;
     }
