@@ -421,7 +421,110 @@ def c5_leg(args, ctx, dev, world, rank):
         if o is not None:
             o.close()
     del chars, offs, v
+    if world == 1 and not args.no_variants:
+        out["var_len_keys"] = c5_var_len_leg(args, ctx, dev)
     return out
+
+
+def var_len_keys_torch(ids):
+    """SURVEY §8(d)'s C5 variant, 1- to 11-byte keys: id i -> the first L = 1 + i % 11 digits of
+    the 11-digit x = i * 2654435761 mod 10^11 (tests/test_gpu_full_scale.py var_len_keys is the
+    same map in numpy).  Returns (chars, end offsets) of the ColumnString."""
+    import torch
+    L = 1 + ids % 11
+    x = (ids * 2654435761) % 10**11
+    offs = torch.cumsum(L + 1, 0)
+    starts = offs - (L + 1)
+    chars = torch.zeros(int(offs[-1].item()), dtype=torch.uint8, device=ids.device)
+    for j in range(11):
+        sel = L > j
+        chars[starts[sel] + j] = (48 + (x[sel] // 10 ** (10 - j)) % 10).to(torch.uint8)
+    return chars, offs
+
+
+def c5_var_len_leg(args, ctx, dev):
+    """The C5 step over 1- to 11-byte String keys (StringHashMap's size classes, reference
+    Common/HashTable/StringHashTable.h:211-310), c5_rows rows over c5_groups ids (the short
+    lengths collapse: ~5.3M distinct keys), with its CPU restatement beside it."""
+    import torch
+
+    import tiflash_amd as tfa
+    n, G = args.c5_rows, args.c5_groups
+    g = torch.Generator(device=dev)
+    g.manual_seed(17)
+    ids = torch.randint(0, G, (n,), device=dev, generator=g, dtype=torch.int64)
+    chars, offs = var_len_keys_torch(ids)
+    del ids
+    v = torch.randint(0, 10**9, (n,), device=dev, generator=g, dtype=torch.int64)
+    aggs = [(tfa.AGG_SUM, tfa.prec(tfa.DECIMAL64, 15)), (tfa.AGG_COUNT_ALL, 0)]
+    part = tfa.KeysAggregator(ctx, [tfa.STRING], aggs, expected_groups=G)
+    hint = min(G, n)
+
+    def step():
+        part.reset()
+        part.consume([(chars, offs)], [v, None])
+        return part.result(capacity_hint=hint)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ctx.profile(True)
+    ctx.profile_reset()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    prof = ctx.profile_read()
+    ctx.profile(False)
+    cnt_total = int(res["states"][1].view(torch.int64).sum().item())
+    groups = int(res["states"][1].shape[0])
+    ms = el / args.steps * 1e3
+    alg = 8 * n + int(chars.numel()) + 8 * n  # offsets + chars + value
+    out = {"metric": "rows/s on GROUP BY a 1- to 11-byte String key sum(Decimal64)->Decimal128 + count",
+           "value": round(n * args.steps / el, 1), "unit": "rows/s", "ms_per_step": round(ms, 3),
+           "config": {"rows": n, "ids": G, "key_bytes": "1-11 (mean %.1f)" % (chars.numel() / n - 1)},
+           "check": {"count_total": cnt_total, "rows_total": n, "groups": groups, "ok": cnt_total == n},
+           "pipeline_roofline": {"algorithmic_bytes_per_step": alg, "achieved": round(alg / (ms * 1e-3) / 1e9, 1),
+                                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+           "kernels_ms_per_step": {kname: round(vv[0] / args.steps, 4) for kname, vv in sorted(prof.items())}}
+    part.close()
+    del chars, offs, v
+    if not args.no_cpu:
+        out["cpu_baseline"] = cpu_var_len_baseline(args)
+    return out
+
+
+def cpu_var_len_baseline(args):
+    """oracle/cpu_baseline_str.c over the same 1-11-byte key distribution (numpy copy of
+    var_len_keys_torch), its full batch, median of 3."""
+    import numpy as np
+    from oracle import oracle as orc
+    cores, host = host_cores()
+    threads = args.cpu_threads or cores
+    n, G = args.c5_rows, args.c5_groups
+    rng = np.random.default_rng(17)
+    ids = rng.integers(0, G, n)
+    L = 1 + ids % 11
+    x = (ids * 2654435761) % 10**11
+    offs = np.cumsum(L + 1).astype(np.uint64)
+    starts = offs.astype(np.int64) - (L + 1)
+    chars = np.zeros(int(offs[-1]), np.uint8)
+    for j in range(11):
+        sel = L > j
+        chars[starts[sel] + j] = 48 + (x[sel] // 10 ** (10 - j)) % 10
+    del ids, L, x, starts
+    v = rng.integers(0, 10**9, n, dtype=np.int64)
+    times = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        orc.bench_string_agg(chars, offs, v, threads)
+        times.append(time.perf_counter() - t0)
+    med = statistics.median(times)
+    return {"value": round(n / med, 1), "unit": "rows/s", "cores": threads, "kind": "port", "host": host,
+            "sample": f"{n} rows x 3 runs (median), 1-11-byte digit keys over {G} ids, the same StringHashMap "
+                      f"restatement as the k%08d leg (oracle/cpu_baseline_str.c)"}
 
 
 def lz4_leg(args, ctx, pkt):

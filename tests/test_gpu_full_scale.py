@@ -12,7 +12,10 @@ row for row — the sizes the bench runs, where the kernels take paths small tes
   tables at ~30 % load.  Spill passes are not reached at this load; the forced-spill cases (16
   buckets at the C5 shape) are in tests/test_gpu_keys_agg.py.  Checked group by group against
   orc.AggKeys (Aggregator with key_string / StringHashMap restated; reference
-  Aggregator.cpp:566-1246).  Decimal sums are exact 128-bit integers: bit-exact."""
+  Aggregator.cpp:566-1246).  Decimal sums are exact 128-bit integers: bit-exact.
+* C5 with 1- to 11-byte keys (SURVEY §8(d)'s variable-length variant; bench.py's var_len_keys
+  sub-leg): the same aggregation over digit keys of every length up to 11 bytes — every tile
+  narrow (20-byte rows, partition.h WNARROW) — against the oracle, group by group."""
 import numpy as np
 import pytest
 import torch
@@ -94,6 +97,66 @@ def test_c5_full_scale_string_groupby_matches_oracle(tfa, ctx, dev, orc):
     oid = (ok * (10 ** np.arange(7, -1, -1, dtype=np.int64))).sum(axis=1)
     go, oo = np.argsort(gid), np.argsort(oid)
     np.testing.assert_array_equal(gid[go], oid[oo])
+    np.testing.assert_array_equal(gcnt[go], ocnt[oo])
+    np.testing.assert_array_equal(gsum[go], osum[oo])
+    assert int(gcnt.sum()) == n
+
+
+def var_len_keys(ids):
+    """The C5 variable-length key set (bench.py's string_agg var_len_keys sub-leg): key of id i =
+    the first L = 1 + i % 11 digits of the 11-digit x = i * 2654435761 mod 10^11 (1-11 bytes)."""
+    L = 1 + ids % 11
+    x = (ids.astype(np.int64) * 2654435761) % 10**11
+    offs = np.cumsum(L + 1).astype(np.uint64)
+    starts = offs.astype(np.int64) - (L + 1)
+    chars = np.zeros(int(offs[-1]), np.uint8)
+    for j in range(11):
+        sel = L > j
+        chars[starts[sel] + j] = 48 + (x[sel] // 10 ** (10 - j)) % 10
+    return chars, offs
+
+
+def _digit_codes(chars, ends, lens):
+    """rows of digit keys -> int64 codes len * 10^11 + value (unique per key)"""
+    starts = ends - lens
+    val = np.zeros(len(ends), np.int64)
+    for j in range(11):
+        sel = lens > j
+        val[sel] = val[sel] * 10 + (chars[starts[sel] + j].astype(np.int64) - 48)
+    return lens.astype(np.int64) * 10**11 + val
+
+
+def test_c5_full_scale_var_len_keys_matches_oracle(tfa, ctx, dev, orc):
+    """SURVEY §8(d)'s C5 variant: 1- to 11-byte String keys (StringHashMap's size classes,
+    Common/HashTable/StringHashTable.h:211-310) at the full 100M rows, vs the oracle's GROUP BY"""
+    n, G = 100_000_000, 10_000_000
+    rng = np.random.default_rng(17)
+    ids = rng.integers(0, G, n)
+    v = rng.integers(0, 10**9, n, dtype=np.int64)
+    chars, offs = var_len_keys(ids)
+    del ids
+    aggs = [(tfa.AGG_SUM, tfa.prec(tfa.DECIMAL64, 15)), (tfa.AGG_COUNT_ALL, 0)]
+    agg = tfa.KeysAggregator(ctx, [tfa.STRING], aggs, expected_groups=G)
+    agg.consume([(torch.from_numpy(chars).to(dev), torch.from_numpy(offs.view(np.int64)).to(dev))],
+                [torch.from_numpy(v).to(dev), None])
+    res = agg.result()
+    gchars, goffs = (t.cpu().numpy() for t in res["keys"][0])
+    gsum = res["states"][0].cpu().numpy().view(np.int64).reshape(-1, 2)
+    gcnt = res["states"][1].cpu().numpy().view(np.int64)
+    agg.close()
+    gends = goffs.astype(np.int64)
+    glen = np.diff(np.concatenate([[0], gends])) - 1  # the '\0' excluded
+    gcode = _digit_codes(gchars, gends - 1, glen)
+    ref = orc.AggKeys([orc.STRING], [(0, orc.prec(orc.DECIMAL64, 15)), (2, 0)])
+    ref.consume([(chars, offs)], [v, None])
+    kb, ko, (osum, ocnt), _ = ref.result_arrays()
+    # serialised key per group: NULL byte, u64 length, the bytes
+    oends = ko.astype(np.int64)
+    olen = np.diff(np.concatenate([[0], oends])) - 9
+    ocode = _digit_codes(kb, oends, olen)
+    assert len(gcode) == len(ocode) and len(np.unique(gcode)) == len(gcode)
+    go, oo = np.argsort(gcode), np.argsort(ocode)
+    np.testing.assert_array_equal(gcode[go], ocode[oo])
     np.testing.assert_array_equal(gcnt[go], ocnt[oo])
     np.testing.assert_array_equal(gsum[go], osum[oo])
     assert int(gcnt.sum()) == n

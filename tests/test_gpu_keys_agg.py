@@ -168,6 +168,65 @@ def test_string_key_two_level_tiled(tfa, ctx, dev, orc, collator, nullable, grou
     check_same(got, ref.result())
 
 
+@pytest.mark.parametrize("nullable", [False, True])
+def test_wide_narrow_tiles_mixed(tfa, ctx, dev, orc, nullable):
+    """Narrow wide-key tiles (WNARROW, partition.h: keys with bytes 11-14 zero travel as 20-byte
+    rows — u64 lo, u32 hi of bytes 8-10 + the length / NULL byte, u64 value) next to 24-byte tiles:
+    the first part of the input has keys of <= 11 bytes (every tile narrow), the rest mixes in keys
+    of 12-15 bytes, so the regroup pass reads narrow and wide pass-1 tiles and writes both kinds;
+    11 / 12-byte boundary keys, NULL keys (the NULL bit in byte 15) and two blocks (the second seeds
+    the first one's groups)."""
+    rng = np.random.default_rng(31 + nullable)
+    n, groups = 3_000_000, 900_000
+    ids = rng.integers(0, groups, n)
+    long_from = n // 2
+    strs = []
+    for r, i in enumerate(ids):
+        base = b"w%010d" % i  # 11 bytes: the widest narrow key
+        if r < long_from:
+            strs.append(base[: 1 + (i % 11)])
+        else:
+            strs.append(base + b"xyzw"[: i % 5])  # 11-15 bytes
+    knull = (rng.random(n) < 0.01).astype(np.uint8) if nullable else None
+    d = rng.integers(-10**12, 10**12, n, dtype=np.int64)
+    aggs = [(tfa.AGG_SUM, tfa.prec(tfa.DECIMAL64, 15)), (tfa.AGG_COUNT_ALL, 0)]
+    agg = tfa.KeysAggregator(ctx, [tfa.STRING], aggs, expected_groups=groups * 2)
+    cut = n // 4
+    for lo, hi in ((0, cut), (cut, n)):
+        c2, o2 = str_col(strs[lo:hi])
+        agg.consume([to_dev((c2, o2), dev)], [to_dev(d[lo:hi], dev), None],
+                    key_nullmaps=[to_dev(knull[lo:hi], dev)] if nullable else None)
+    got = gpu_groups(agg.result(), [20])
+    chars, offs = str_col(strs)
+    ref = orc.AggKeys([orc.STRING], [(0, orc.prec(orc.DECIMAL64, 15)), (2, 0)])
+    ref.consume([(chars, offs)], [d, None], key_nulls=[knull] if nullable else None)
+    check_same(got, ref.result())
+
+
+def test_fixed_keys_narrow_tiles(tfa, ctx, dev, orc):
+    """keys128 of (Int32, Int32) — 8 key bytes, always narrow — and (Int64, UInt32) whose byte 11
+    is set for some rows only: narrow and 24-byte tiles side by side, one level and two levels."""
+    rng = np.random.default_rng(33)
+    for n, groups in ((400_000, 50_000), (3_000_000, 1_200_000)):
+        gid = rng.integers(0, groups, n)
+        a = (gid % 5000).astype(np.int32)
+        b = (gid // 5000).astype(np.int32) - 77
+        v = rng.integers(-10**9, 10**9, n, dtype=np.int64)
+        aggs = [(tfa.AGG_SUM, tfa.INT64), (tfa.AGG_COUNT_ALL, 0)]
+        agg = tfa.KeysAggregator(ctx, [tfa.INT32, tfa.INT32], aggs, expected_groups=groups)
+        agg.consume([to_dev(a, dev), to_dev(b, dev)], [to_dev(v, dev), None])
+        ref = orc.AggKeys([orc.INT32, orc.INT32], [(0, orc.INT64), (2, 0)])
+        ref.consume([a, b], [v, None])
+        check_same(gpu_groups(agg.result(), [tfa.INT32, tfa.INT32]), ref.result())
+        c = gid.astype(np.int64) * 3
+        e = np.where(gid % 3 == 0, (gid % 1000) << 24, gid % 1000).astype(np.uint32)  # byte 11 of the key: e's top byte
+        agg2 = tfa.KeysAggregator(ctx, [tfa.INT64, tfa.UINT32], aggs, expected_groups=groups)
+        agg2.consume([to_dev(c, dev), to_dev(e, dev)], [to_dev(v, dev), None])
+        ref2 = orc.AggKeys([orc.INT64, orc.UINT32], [(0, orc.INT64), (2, 0)])
+        ref2.consume([c, e], [v, None])
+        check_same(gpu_groups(agg2.result(), [tfa.INT64, tfa.UINT32]), ref2.result())
+
+
 def test_fixed_keys_two_level_tiled(tfa, ctx, dev, orc):
     """keys128 (Int32, Int64) at 1.5M groups through the packed-key wide tiled path, Float64 sum."""
     rng = np.random.default_rng(13)

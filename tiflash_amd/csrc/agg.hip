@@ -613,9 +613,11 @@ __global__ void __launch_bounds__(RG_T) regroup_tiled_kernel(const uint64_t *rec
     __shared__ uint64_t stage[RG_TR * NCOL];
     __shared__ uint32_t rpref[RG_W + 2], rent[RG_W + 2];
     __shared__ uint32_t fh[RG_FINE], fs[RG_FINE];
+    __shared__ uint32_t s_wide; // a row of this tile has a key that is not narrow (NCOL == 3)
     const int k = blockIdx.x;
     const RgDesc d = desc[k];
     if (threadIdx.x < RG_FINE) fh[threadIdx.x] = 0;
+    if (threadIdx.x == 0) s_wide = 0;
     const int c = d.c;
     if (c < 0) return;
     const int t0 = d.t0, m = d.m;
@@ -644,18 +646,35 @@ __global__ void __launch_bounds__(RG_T) regroup_tiled_kernel(const uint64_t *rec
             int lo = 0;
             for (int st = wm > 1 ? 1 << (31 - __clz(wm - 1)) : 0; st > 0; st >>= 1)
                 if (lo + st < wm && rpref[lo + st] <= x) lo += st;
-            row[q] = (int64_t)(t0 + w0 + lo) * TR1 + (rent[lo] & 0xFFFFu) + (x - rpref[lo]);
+            // the run's start in its tile (bit 15 of the entry: a narrow tile, NCOL == 3 only)
+            const uint32_t e = rent[lo];
+            row[q] = (int64_t)(t0 + w0 + lo) * TR1 + (e & (TILE_NARROW - 1)) + (x - rpref[lo]);
+            if (NCOL == 3 && (e & TILE_NARROW)) row[q] |= (int64_t)1 << 62;
         }
         __syncthreads();
     }
+    bool wide = false;
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         bq[q] = 0xFFFFFFFFu;
         if (row[q] < 0) continue;
+        if (NCOL == 3 && (row[q] >> 62)) { // narrow pass-1 tile: u64 lo [TR1], u32 hi [TR1], u64 value [TR1]
+            const int64_t rr = row[q] & (((int64_t)1 << 62) - 1);
+            const int64_t tile = rr / TR1, pos = rr - tile * TR1;
+            const uint64_t *lo = rec1 + (size_t)tile * TR1 * 3;
+            const uint32_t *hi = reinterpret_cast<const uint32_t *>(lo + TR1);
+            v[q][0] = lo[pos];
+            v[q][1] = wide_wide_hi(hi[pos]);
+            v[q][NCOL - 1] = reinterpret_cast<const uint64_t *>(hi + TR1)[pos];
+            row[q] = rr;
+            continue;
+        }
         const uint64_t *r = rec1 + row[q] * NCOL;
 #pragma unroll
         for (int w = 0; w < NCOL; ++w) v[q][w] = r[w];
+        if (NCOL == 3) wide |= !wide_hi_narrowable(v[q][1]);
     }
+    if (NCOL == 3 && wide) s_wide = 1;
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         if (row[q] < 0) continue;
@@ -663,6 +682,7 @@ __global__ void __launch_bounds__(RG_T) regroup_tiled_kernel(const uint64_t *rec
         bq[q] = f | (atomicAdd(&fh[f], 1u) << 16);
     }
     __syncthreads();
+    const bool narrow_out = NCOL == 3 && !s_wide; // every row of the tile narrow: 20 B a row out
     if (threadIdx.x < 64) { // one wave: exclusive scan of the 64 fine counts
         const uint32_t cnt = fh[threadIdx.x];
         uint32_t xs = cnt;
@@ -672,7 +692,7 @@ __global__ void __launch_bounds__(RG_T) regroup_tiled_kernel(const uint64_t *rec
             if ((int)threadIdx.x >= d) xs += y;
         }
         fs[threadIdx.x] = xs - cnt;
-        hist2[(size_t)threadIdx.x * T2 + k] = (xs - cnt) | (cnt << 16);
+        hist2[(size_t)threadIdx.x * T2 + k] = (xs - cnt) | (narrow_out ? TILE_NARROW : 0u) | (cnt << 16);
     }
     __syncthreads();
 #pragma unroll
@@ -685,6 +705,16 @@ __global__ void __launch_bounds__(RG_T) regroup_tiled_kernel(const uint64_t *rec
     __syncthreads();
     const uint32_t rows = x1 - x0;
     uint64_t *out = rec2 + (size_t)k * RG_TR * NCOL;
+    if (narrow_out) { // u64 lo [RG_TR], u32 hi [RG_TR], u64 value [RG_TR] (RG_TR even)
+        uint32_t *hi = reinterpret_cast<uint32_t *>(out + RG_TR);
+        uint64_t *val = reinterpret_cast<uint64_t *>(hi + RG_TR);
+        for (uint32_t i = threadIdx.x; i < rows; i += RG_T) {
+            out[i] = stage[i * NCOL];
+            hi[i] = wide_narrow_hi(stage[i * NCOL + 1]);
+            val[i] = stage[i * NCOL + NCOL - 1];
+        }
+        return;
+    }
     for (uint32_t i = threadIdx.x; i < rows * NCOL; i += RG_T) out[i] = stage[i];
 }
 
@@ -1698,6 +1728,10 @@ struct RefCall { // the collated candidates of one call (String min / max under 
     explicit RefCall(tfg_agg *agg) : a(agg) {}
     // the candidates named in S.ref die with the call: no later launch may carry their pointers
     ~RefCall() {
+#ifdef TFG_EXP_POOL // the fault analysis: TFG_REF_NOCLEAR=1 keeps round 5's dangling pointers
+        static const bool keep = getenv("TFG_REF_NOCLEAR") && *getenv("TFG_REF_NOCLEAR") == '1';
+        if (keep) return;
+#endif
         for (auto &r : a->S.ref) r = RefSrc{};
     }
     RefCall(const RefCall &) = delete;

@@ -1010,13 +1010,25 @@ template <int A0, int A1, int A2> struct WideFastOps {
     static constexpr int op(int i) { return i == 0 ? A0 : (i == 1 ? A1 : A2); }
     static constexpr int NCOL = 2 + (A0 >= 2) + (A1 >= 2) + (A2 >= 2);
     static constexpr bool WIDE = true;
-    static constexpr bool NARROWABLE = false;
+    // one summed argument: narrow tiles (WNARROW, partition.h) hold u64 key lo [TRS], u32 key hi
+    // [TRS], u64 value [TRS]
+    static constexpr bool NARROWABLE = NCOL == 3;
     static constexpr int pos(int i) { return 2 + (i > 0 && A0 >= 2) + (i > 1 && A1 >= 2); }
     struct Row {
         uint64_t key, khi;
         uint64_t v[3];
     };
-    __device__ __forceinline__ void load_narrow(const uint64_t *, uint64_t, int, uint32_t, Row &) const {}
+    // row `off` of the narrow tile whose slot starts at row `slot` (slot rows of NCOL words each)
+    __device__ __forceinline__ void load_narrow(const uint64_t *rec, uint64_t slot, int TRS, uint32_t off, Row &v) const {
+        const uint64_t *lo = rec + slot * NCOL;
+        const uint32_t *hi = reinterpret_cast<const uint32_t *>(lo + TRS);
+        v.key = lo[off];
+        v.khi = wide_wide_hi(hi[off]);
+        const uint64_t w = reinterpret_cast<const uint64_t *>(hi + TRS)[off];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+            if (op(i) >= 2) v.v[i] = w;
+    }
     const AggSpec &S;
     int mode;
     __device__ __forceinline__ void load(const RowsIO &rows, int64_t r, Row &v) const {

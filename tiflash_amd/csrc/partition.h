@@ -602,6 +602,15 @@ __global__ void gather_part_offsets_kernel(const uint64_t *offs, PartLayout L, u
 // addresses of one destination run, so stores coalesce into runs of TR/P rows.
 constexpr int ST_T = 1024;     // threads (16 waves)
 constexpr uint32_t TILE_NARROW = 0x8000u; // tile_hist start bit: the tile holds narrow records
+// narrow 16-byte keys (WNARROW tiles): bytes 11-14 zero, so the high word keeps bytes 8-10 and the
+// length / NULL byte 15 in 32 bits
+__host__ __device__ __forceinline__ bool wide_hi_narrowable(uint64_t hi) { return ((hi >> 24) & 0xFFFFFFFFull) == 0; }
+__host__ __device__ __forceinline__ uint32_t wide_narrow_hi(uint64_t hi) {
+    return (uint32_t)(hi & 0xFFFFFFull) | ((uint32_t)(hi >> 56) << 24);
+}
+__host__ __device__ __forceinline__ uint64_t wide_wide_hi(uint32_t h) {
+    return (uint64_t)(h & 0xFFFFFFu) | ((uint64_t)(h >> 24) << 56);
+}
 constexpr int ST_MAXR = 8;     // rows per thread per tile (TR <= 8192 < 2^16: ranks pack in 16 bits)
 // tiles a round in the sparse variant's all-false check (four measured slower: 0 % C2 0.364 vs
 // 0.344 ms, r05ad — not memory-level parallelism but the per-round barriers bound it)
@@ -763,6 +772,11 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
     // 32 bits is written as a u32 key array + a u64 value array (12 B a row instead of 16), and
     // its tile_hist entries carry TILE_NARROW; red[ST_T / 64 + 1] collects "a wide key was seen"
     constexpr bool NARROW = TILED && AOS && NC8 == 2 && !SelWideKey<Sel>::value;
+    // ... and of a 16-byte key + one value word (keys128 / key_string with one summed argument): a
+    // tile whose kept keys all have bytes 11-14 zero (<= 11 key bytes: every k%08d String key) is
+    // written as u64 key lo [TRS], u32 key hi [TRS] (bytes 8-10 and 15), u64 value [TRS]: 20 B a
+    // row instead of 24 (wide_narrow_hi / wide_wide_hi convert)
+    constexpr bool WNARROW = TILED && AOS && NC8 == 3 && SelWideKey<Sel>::value;
     uint32_t *fh = reinterpret_cast<uint32_t *>(lds + g.fh_off); // TILED && fine_bits: P << fine_bits bins
     if (TILED && g.fine_bits)
         for (uint32_t p = threadIdx.x; p < (P << g.fine_bits); p += ST_T) fh[p] = 0;
@@ -835,7 +849,7 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
             }
         }
         for (uint32_t p = threadIdx.x; p < P; p += ST_T) hist[p] = 0;
-        if (NARROW && threadIdx.x == 0) red[ST_T / 64 + 1] = 0;
+        if ((NARROW || WNARROW) && threadIdx.x == 0) red[ST_T / 64 + 1] = 0;
         __syncthreads();
         // 1. destination + rank of every row of the tile
         uint32_t bq[ST_MAXR]; // destination (low 16 bits) | rank inside the tile (high 16 bits)
@@ -908,6 +922,12 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
                 for (int j = 0; j < ST_MAXR; ++j) wide |= bq[j] != 0xFFFFFFFFu && (v[0][j] >> 32) != 0;
                 if (wide) red[ST_T / 64 + 1] = 1;
             }
+            if constexpr (WNARROW) {
+                bool wide = false;
+#pragma unroll
+                for (int j = 0; j < ST_MAXR; ++j) wide |= bq[j] != 0xFFFFFFFFu && !wide_hi_narrowable(v[1][j]);
+                if (wide) red[ST_T / 64 + 1] = 1;
+            }
         }
         __syncthreads();
         // 2. exclusive scan of the tile histogram -> start of each destination inside the tile
@@ -946,7 +966,7 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
         const uint32_t kept = red[ST_T / 64];
         spec = kept != 0;
         const uint32_t tile = blockIdx.x * (uint32_t)g.tps + (tb - begin) / (uint32_t)g.TR;
-        const bool narrow = NARROW && g.allow_narrow && red[ST_T / 64 + 1] == 0;
+        const bool narrow = (NARROW || WNARROW) && g.allow_narrow && red[ST_T / 64 + 1] == 0;
         if constexpr (TILED)
             for (uint32_t p = threadIdx.x; p < P; p += ST_T)
                 g.tile_hist[(size_t)p * g.T + tile] = pstart[p] | (narrow ? TILE_NARROW : 0u) | (hist[p] << 16);
@@ -1007,7 +1027,14 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
             if constexpr (TILED) gp = (uint64_t)tile * (uint32_t)g.TRS + pstart[b] + (s - start[b]);
             else gp = run[b] + (s - start[b]);
             if (perm) perm[gp] = sperm[s];
-            if (NARROW && narrow) { // u32 keys, then u64 values, in the tile's slot
+            if (WNARROW && narrow) { // u64 key lo, u32 key hi, u64 values, in the tile's slot
+                const uint32_t pos = pstart[b] + (s - start[b]);
+                uint64_t *lo = reinterpret_cast<uint64_t *>(cols.out[0]) + (size_t)tile * (uint32_t)g.TRS * 3;
+                uint32_t *hi = reinterpret_cast<uint32_t *>(lo + g.TRS);
+                lo[pos] = reinterpret_cast<const uint64_t *>(lds + g.stage_off[0])[s];
+                hi[pos] = wide_narrow_hi(reinterpret_cast<const uint64_t *>(lds + g.stage_off[1])[s]);
+                reinterpret_cast<uint64_t *>(hi + g.TRS)[pos] = reinterpret_cast<const uint64_t *>(lds + g.stage_off[2])[s];
+            } else if (NARROW && narrow) { // u32 keys, then u64 values, in the tile's slot
                 const uint32_t pos = pstart[b] + (s - start[b]);
                 uint32_t *ks = reinterpret_cast<uint32_t *>(reinterpret_cast<uint64_t *>(cols.out[0]) +
                                                             (size_t)tile * (uint32_t)g.TRS * 2);
