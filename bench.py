@@ -427,25 +427,30 @@ def c5_leg(args, ctx, dev, world, rank):
 
 
 def var_len_keys_torch(ids):
-    """SURVEY §8(d)'s C5 variant, 1- to 11-byte keys: id i -> the first L = 1 + i % 11 digits of
-    the 11-digit x = i * 2654435761 mod 10^11 (tests/test_gpu_full_scale.py var_len_keys is the
-    same map in numpy).  Returns (chars, end offsets) of the ColumnString."""
+    """SURVEY §8(d)'s C5 variant, 1- to 11-byte keys: group id -> every 1-, 2- and 3-byte key of
+    the 94 printable characters, then lengths 4..11 in turn, the id's value in base 94 (no key
+    is hot: c5_groups distinct keys, ~10 rows each).  tests/test_gpu_full_scale.py var_len_keys is
+    the same map in numpy.  Returns (chars, end offsets) of the ColumnString."""
     import torch
-    L = 1 + ids % 11
-    x = (ids * 2654435761) % 10**11
+    c1, c2, c3 = 94, 94 + 94**2, 94 + 94**2 + 94**3
+    r = ids - c3
+    L = torch.where(ids < c1, 1, torch.where(ids < c2, 2, torch.where(ids < c3, 3, 4 + r % 8)))
+    q = torch.where(ids < c1, ids, torch.where(ids < c2, ids - c1, torch.where(ids < c3, ids - c2, r // 8)))
+    del r
     offs = torch.cumsum(L + 1, 0)
     starts = offs - (L + 1)
     chars = torch.zeros(int(offs[-1].item()), dtype=torch.uint8, device=ids.device)
-    for j in range(11):
-        sel = L > j
-        chars[starts[sel] + j] = (48 + (x[sel] // 10 ** (10 - j)) % 10).to(torch.uint8)
+    for k in range(11):
+        sel = L > k
+        chars[(starts + L - 1 - k)[sel]] = (33 + q[sel] % 94).to(torch.uint8)
+        q = q // 94
     return chars, offs
 
 
 def c5_var_len_leg(args, ctx, dev):
     """The C5 step over 1- to 11-byte String keys (StringHashMap's size classes, reference
-    Common/HashTable/StringHashTable.h:211-310), c5_rows rows over c5_groups ids (the short
-    lengths collapse: ~5.3M distinct keys), with its CPU restatement beside it."""
+    Common/HashTable/StringHashTable.h:211-310), c5_rows rows over c5_groups ids (
+    c5_groups distinct keys of every length 1-11), with its CPU restatement beside it."""
     import torch
 
     import tiflash_amd as tfa
@@ -506,15 +511,19 @@ def cpu_var_len_baseline(args):
     n, G = args.c5_rows, args.c5_groups
     rng = np.random.default_rng(17)
     ids = rng.integers(0, G, n)
-    L = 1 + ids % 11
-    x = (ids * 2654435761) % 10**11
+    c1, c2, c3 = 94, 94 + 94**2, 94 + 94**2 + 94**3
+    r = ids - c3
+    L = np.where(ids < c1, 1, np.where(ids < c2, 2, np.where(ids < c3, 3, 4 + r % 8)))
+    q = np.where(ids < c1, ids, np.where(ids < c2, ids - c1, np.where(ids < c3, ids - c2, r // 8)))
+    del r, ids
     offs = np.cumsum(L + 1).astype(np.uint64)
     starts = offs.astype(np.int64) - (L + 1)
     chars = np.zeros(int(offs[-1]), np.uint8)
-    for j in range(11):
-        sel = L > j
-        chars[starts[sel] + j] = 48 + (x[sel] // 10 ** (10 - j)) % 10
-    del ids, L, x, starts
+    for k in range(11):
+        sel = L > k
+        chars[(starts + L - 1 - k)[sel]] = 33 + q[sel] % 94
+        q //= 94
+    del L, q, starts
     v = rng.integers(0, 10**9, n, dtype=np.int64)
     times = []
     for _ in range(3):
@@ -523,7 +532,7 @@ def cpu_var_len_baseline(args):
         times.append(time.perf_counter() - t0)
     med = statistics.median(times)
     return {"value": round(n / med, 1), "unit": "rows/s", "cores": threads, "kind": "port", "host": host,
-            "sample": f"{n} rows x 3 runs (median), 1-11-byte digit keys over {G} ids, the same StringHashMap "
+            "sample": f"{n} rows x 3 runs (median), 1-11-byte keys over {G} ids, the same StringHashMap "
                       f"restatement as the k%08d leg (oracle/cpu_baseline_str.c)"}
 
 

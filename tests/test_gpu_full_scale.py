@@ -102,28 +102,40 @@ def test_c5_full_scale_string_groupby_matches_oracle(tfa, ctx, dev, orc):
     assert int(gcnt.sum()) == n
 
 
+def var_len_split(g):
+    """group id -> (key length L in 1..11, its value q): every 1-byte key (94), every 2-byte key
+    (94^2), every 3-byte key (94^3), then lengths 4..11 in turn; distinct ids give distinct keys"""
+    c1, c2, c3 = 94, 94 + 94**2, 94 + 94**2 + 94**3
+    r = g - c3
+    L = np.where(g < c1, 1, np.where(g < c2, 2, np.where(g < c3, 3, 4 + r % 8)))
+    q = np.where(g < c1, g, np.where(g < c2, g - c1, np.where(g < c3, g - c2, r // 8)))
+    return L, q
+
+
 def var_len_keys(ids):
-    """The C5 variable-length key set (bench.py's string_agg var_len_keys sub-leg): key of id i =
-    the first L = 1 + i % 11 digits of the 11-digit x = i * 2654435761 mod 10^11 (1-11 bytes)."""
-    L = 1 + ids % 11
-    x = (ids.astype(np.int64) * 2654435761) % 10**11
+    """The C5 variable-length key set (bench.py's string_agg var_len_keys sub-leg, the same map on
+    the device): group id -> a key of 1-11 bytes from the 94 printable characters 33..126, its
+    value q written in base 94, most significant digit first.  10M ids -> 10M distinct keys."""
+    L, q = var_len_split(ids.astype(np.int64))
     offs = np.cumsum(L + 1).astype(np.uint64)
     starts = offs.astype(np.int64) - (L + 1)
     chars = np.zeros(int(offs[-1]), np.uint8)
-    for j in range(11):
-        sel = L > j
-        chars[starts[sel] + j] = 48 + (x[sel] // 10 ** (10 - j)) % 10
+    qq = q.copy()
+    for k in range(11):
+        sel = L > k
+        chars[(starts + L - 1 - k)[sel]] = 33 + (qq[sel] % 94)
+        qq //= 94
     return chars, offs
 
 
-def _digit_codes(chars, ends, lens):
-    """rows of digit keys -> int64 codes len * 10^11 + value (unique per key)"""
+def _key_codes(chars, ends, lens):
+    """rows of keys (<= 11 bytes) -> int64 codes: (L, base-94 value) packed (unique per key)"""
     starts = ends - lens
     val = np.zeros(len(ends), np.int64)
     for j in range(11):
         sel = lens > j
-        val[sel] = val[sel] * 10 + (chars[starts[sel] + j].astype(np.int64) - 48)
-    return lens.astype(np.int64) * 10**11 + val
+        val[sel] = val[sel] * 94 + (chars[starts[sel] + j].astype(np.int64) - 33)
+    return lens.astype(np.int64) << 58 | val
 
 
 def test_c5_full_scale_var_len_keys_matches_oracle(tfa, ctx, dev, orc):
@@ -133,6 +145,7 @@ def test_c5_full_scale_var_len_keys_matches_oracle(tfa, ctx, dev, orc):
     rng = np.random.default_rng(17)
     ids = rng.integers(0, G, n)
     v = rng.integers(0, 10**9, n, dtype=np.int64)
+    n_ids = len(np.unique(ids))
     chars, offs = var_len_keys(ids)
     del ids
     aggs = [(tfa.AGG_SUM, tfa.prec(tfa.DECIMAL64, 15)), (tfa.AGG_COUNT_ALL, 0)]
@@ -146,15 +159,16 @@ def test_c5_full_scale_var_len_keys_matches_oracle(tfa, ctx, dev, orc):
     agg.close()
     gends = goffs.astype(np.int64)
     glen = np.diff(np.concatenate([[0], gends])) - 1  # the '\0' excluded
-    gcode = _digit_codes(gchars, gends - 1, glen)
+    gcode = _key_codes(gchars, gends - 1, glen)
     ref = orc.AggKeys([orc.STRING], [(0, orc.prec(orc.DECIMAL64, 15)), (2, 0)])
     ref.consume([(chars, offs)], [v, None])
     kb, ko, (osum, ocnt), _ = ref.result_arrays()
     # serialised key per group: NULL byte, u64 length, the bytes
     oends = ko.astype(np.int64)
     olen = np.diff(np.concatenate([[0], oends])) - 9
-    ocode = _digit_codes(kb, oends, olen)
+    ocode = _key_codes(kb, oends, olen)
     assert len(gcode) == len(ocode) and len(np.unique(gcode)) == len(gcode)
+    assert len(gcode) == n_ids
     go, oo = np.argsort(gcode), np.argsort(ocode)
     np.testing.assert_array_equal(gcode[go], ocode[oo])
     np.testing.assert_array_equal(gcnt[go], ocnt[oo])

@@ -609,7 +609,8 @@ __global__ void regroup_desc_kernel(const uint32_t *runpref, int T1, const uint3
 template <int NCOL>
 __global__ void __launch_bounds__(RG_T) regroup_tiled_kernel(const uint64_t *rec1, const uint32_t *hist1, int T1, int TR1,
                                                              const uint32_t *runpref, const RgDesc *desc,
-                                                             uint32_t fine_shift, uint64_t *rec2, uint32_t *hist2, int T2) {
+                                                             uint32_t fine_shift, uint64_t *rec2, uint32_t *hist2, int T2,
+                                                             int narrow_ok) {
     __shared__ uint64_t stage[RG_TR * NCOL];
     __shared__ uint32_t rpref[RG_W + 2], rent[RG_W + 2];
     __shared__ uint32_t fh[RG_FINE], fs[RG_FINE];
@@ -682,7 +683,7 @@ __global__ void __launch_bounds__(RG_T) regroup_tiled_kernel(const uint64_t *rec
         bq[q] = f | (atomicAdd(&fh[f], 1u) << 16);
     }
     __syncthreads();
-    const bool narrow_out = NCOL == 3 && !s_wide; // every row of the tile narrow: 20 B a row out
+    const bool narrow_out = NCOL == 3 && narrow_ok && !s_wide; // every row of the tile narrow: 20 B a row out
     if (threadIdx.x < 64) { // one wave: exclusive scan of the 64 fine counts
         const uint32_t cnt = fh[threadIdx.x];
         uint32_t xs = cnt;
@@ -1375,6 +1376,16 @@ int wide_fast_signature(const AggSpec &S, const uint8_t *const *val_nulls) {
 // pass 1, regroup_tiled_kernel into 64 fine buckets each); then the tiled bucket kernel with
 // WideFastOps, scan and compaction.  `sel` produces the 16-byte keys (SelWide2 over packed keys,
 // SelWideStr straight from the String column).  done = false: not applicable (general path).
+// narrow 20-byte wide-key tiles (partition.h WNARROW): TFG_WIDE_NARROW=0 none, 1 pass-1 tiles
+// only (the regroup writes 24-byte tiles), 2 pass-1 and regrouped tiles (A/B knob)
+static int wide_narrow_mode() {
+    static const int m = [] {
+        const char *v = getenv("TFG_WIDE_NARROW");
+        return v && *v ? atoi(v) : 2;
+    }();
+    return m;
+}
+
 template <typename Sel>
 int consume_wide_tiled(tfg_agg *a, int code, Sel sel, const void *const *vals, int64_t n, unsigned *err, bool &done) {
     done = false;
@@ -1422,6 +1433,7 @@ int consume_wide_tiled(tfg_agg *a, int code, Sel sel, const void *const *vals, i
     sel.shift = fib_shift(B1);
     if (err) TFG_HIP(hipMemsetAsync(err, 0, sizeof(unsigned), ctx->stream));
     tg.sg.zero2 = a->pend_cursor(); // the bucket kernel's cursors, zeroed by the partition
+    tg.sg.allow_narrow = wide_narrow_mode() >= 1;
     if (int rc = run_partition_tiled(ctx, sel, RowPred{}, tg, pc, (uint32_t *)(sb + o_hist1), "agg.part.tiled"))
         return rc;
     if (err) { // a String key longer than 15 bytes: the serialized method, not this one
@@ -1452,11 +1464,11 @@ int consume_wide_tiled(tfg_agg *a, int code, Sel sel, const void *const *vals, i
         if (ncol == 3)
             hipLaunchKernelGGL(regroup_tiled_kernel<3>, dim3((unsigned)T2), dim3(RG_T), 0, ctx->stream, tin.rec,
                                tin.tile_hist, T1, tin.TR, pref, (const RgDesc *)desc, fine_shift,
-                               (uint64_t *)(sb + o_rec2), hist2, (int)T2);
+                               (uint64_t *)(sb + o_rec2), hist2, (int)T2, wide_narrow_mode() >= 2);
         else
             hipLaunchKernelGGL(regroup_tiled_kernel<2>, dim3((unsigned)T2), dim3(RG_T), 0, ctx->stream, tin.rec,
                                tin.tile_hist, T1, tin.TR, pref, (const RgDesc *)desc, fine_shift,
-                               (uint64_t *)(sb + o_rec2), hist2, (int)T2);
+                               (uint64_t *)(sb + o_rec2), hist2, (int)T2, wide_narrow_mode() >= 2);
         TFG_LAUNCH_CHECK();
         tin.rec = (const uint64_t *)(sb + o_rec2);
         tin.tile_hist = hist2;
