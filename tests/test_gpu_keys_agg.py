@@ -494,3 +494,58 @@ def test_serialized_keys_many_groups(tfa, ctx, dev, orc):
     ref = orc.AggKeys([orc.INT64, orc.STRING], [(0, orc.prec(orc.DECIMAL64, 15)), (2, 0)])
     ref.consume([k1, (chars, offs)], [d, None])
     check_same(gpu_groups(agg.result(), [tfa.INT64, 20]), ref.result())
+
+
+@pytest.mark.parametrize("collator", [0, 2])
+def test_weak_hash_packed_string_keys(tfa, ctx, dev, orc, collator):
+    """tfg_agg_weak_hash_packed (the two-phase sender's routing hash, computed from the packed
+    keys) = IColumn::updateWeakHash32 of the key column (the oracle's ColumnString hash,
+    ColumnString.cpp:1228-1327; NULL rows keep the seed, ColumnNullable.cpp:131-173): keys of 0-15
+    bytes, trailing spaces (BIN_PADDING trims them before packing and before hashing), NULLs"""
+    rng = np.random.default_rng(41 + collator)
+    vocab = vocab_strings(rng, 2000)
+    n = 40_000
+    strs = rand_strings(rng, n, vocab)
+    chars, offs = str_col(strs)
+    knull = (rng.random(n) < 0.05).astype(np.uint8)
+    agg = tfa.KeysAggregator(ctx, [tfa.STRING], [(tfa.AGG_COUNT_ALL, 0)], collators=[collator])
+    agg.consume([to_dev((chars, offs), dev)], [None], key_nullmaps=[to_dev(knull, dev)])
+    assert agg.holds_packed()
+    packed = agg.result_packed()
+    k16 = packed["keys"]
+    g = k16.shape[0]
+    h = torch.empty(g, dtype=torch.int32, device=dev)
+    tfa.check(tfa.lib().tfg_weak_hash_init(ctx.h, tfa._p(h), tfa.ctypes.c_int64(g)))
+    got = agg.weak_hash_packed(k16, h).cpu().numpy().view(np.uint32)
+    agg.close()
+    raw = k16.cpu().numpy().view(np.uint8).reshape(g, 16)
+    isnull = (raw[:, 15] >> 7).astype(np.uint8)
+    keys = [bytes(raw[i, :raw[i, 15] & 0x7F]) if not isnull[i] else b"" for i in range(g)]
+    kc, ko = str_col(keys)
+    want = orc.weak_hash_string(kc, ko, np.full(g, 0xFFFFFFFF, np.uint32), nullmap=isnull, collator=collator)
+    np.testing.assert_array_equal(got, want)
+
+
+def test_weak_hash_packed_fixed_keys(tfa, ctx, dev, orc):
+    """the same for a keys128 tuple (Int32, nullable Int64): the values at their packed offsets,
+    hashed as hash_key_row feeds them to crc32q, NULL bits in byte 15"""
+    rng = np.random.default_rng(43)
+    n = 50_000
+    a = rng.integers(-1000, 1000, n).astype(np.int32)
+    b = rng.integers(-2**40, 2**40, n).astype(np.int64) % 997
+    bn = (rng.random(n) < 0.1).astype(np.uint8)
+    agg = tfa.KeysAggregator(ctx, [tfa.INT32, tfa.INT64], [(tfa.AGG_COUNT_ALL, 0)])
+    agg.consume([to_dev(a, dev), to_dev(b, dev)], [None], key_nullmaps=[None, to_dev(bn, dev)])
+    packed = agg.result_packed()
+    k16 = packed["keys"]
+    g = k16.shape[0]
+    h = torch.empty(g, dtype=torch.int32, device=dev)
+    tfa.check(tfa.lib().tfg_weak_hash_init(ctx.h, tfa._p(h), tfa.ctypes.c_int64(g)))
+    got = agg.weak_hash_packed(k16, h).cpu().numpy().view(np.uint32)
+    agg.close()
+    raw = k16.cpu().numpy().view(np.uint8).reshape(g, 16)
+    ga = raw[:, 0:4].copy().view(np.int32).reshape(-1)
+    gb = raw[:, 4:12].copy().view(np.int64).reshape(-1)
+    nb = ((raw[:, 15] >> 1) & 1).astype(np.uint8)
+    want = orc.weak_hash([ga, gb], types=[orc.INT32, orc.INT64], nullmaps=[None, nb])
+    np.testing.assert_array_equal(got, want)

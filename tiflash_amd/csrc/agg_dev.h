@@ -849,7 +849,11 @@ __device__ __forceinline__ void store_row(const AggSpec &S, const RowsIO &rows, 
 // RPT rows per thread per step: several independent row loads in flight per thread, and one
 // barrier per step.  Misses (keys that do not fit the table, or whose older group is still
 // pending) are appended to the other row buffer (ping-pong), processed by the next pass.
+#ifndef TFG_EXP_RPT
 constexpr int RPT = 4;
+#else // experiment builds (tools/build_exp.sh) of the bucket kernels only
+constexpr int RPT = TFG_EXP_RPT;
+#endif
 
 // Row policies of the bucket kernel.  GenericOps handles every signature / mode / null map
 // through runtime switches; FastOps<A0,A1,A2> is the compile-time specialisation of the hot
@@ -1216,7 +1220,11 @@ agg_bucket_tiled_kernel(AggSpec S, TiledIn tin, int mode, GroupsIO old,
     __shared__ uint32_t s_tot;
     __shared__ uint32_t s_wsum[BT / 64];
     // sampled row -> run index of a chunk: s_idx[k] = the run holding row k << idx_sh
+#ifndef TFG_EXP_IDXN
     constexpr int IDXN = 2048;
+#else
+    constexpr int IDXN = TFG_EXP_IDXN;
+#endif
     __shared__ uint16_t s_idx[IDXN];
     Table T(lds, S);
     const Ops ops{S, mode};

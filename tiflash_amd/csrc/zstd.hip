@@ -842,18 +842,17 @@ __global__ void __launch_bounds__(64) zstd_check_kernel(const uint64_t *roff, ui
     if (wave_xxh64(p, fr.out1 - fr.out0) != fr.checksum && threadIdx.x == 0) atomicOr(err, 1u);
 }
 
-struct PoolBuf { // hipMallocAsync'd, hipFreeAsync'd on every exit
-    hipStream_t st;
+struct PoolBuf { // a call's work space from the context's call arena (common.h DevArena)
+    Ctx *ctx;
     void *p = nullptr;
     uint64_t cap = 0;
-    ~PoolBuf() {
-        if (p) (void)hipFreeAsync(p, st);
-    }
-    int reserve(uint64_t bytes) {
+    explicit PoolBuf(Ctx *c) : ctx(c) { arena_hold(ctx); }
+    ~PoolBuf() { arena_drop(ctx); }
+    PoolBuf(const PoolBuf &) = delete;
+    PoolBuf &operator=(const PoolBuf &) = delete;
+    int reserve(uint64_t bytes) { // a larger block when it grows (the smaller one returns with the call)
         if (bytes <= cap) return TFG_OK;
-        if (p) TFG_HIP(hipFreeAsync(p, st));
-        p = nullptr;
-        TFG_HIP(hipMallocAsync(&p, bytes, st));
+        if (int rc = arena_alloc(ctx, bytes, &p)) return rc;
         cap = bytes;
         return TFG_OK;
     }
@@ -864,7 +863,7 @@ struct PoolBuf { // hipMallocAsync'd, hipFreeAsync'd on every exit
 int zstd_decode_frames(Ctx *ctx, const uint8_t *packet, uint64_t nf, const uint64_t *dfo, const uint64_t *dro,
                        const uint64_t *fo, const uint64_t *ro, uint8_t *dst, unsigned *err) {
     // ---- pass 1: counts of every frame (one read-back)
-    PoolBuf cbuf{ctx->stream}, buf{ctx->stream};
+    PoolBuf cbuf(ctx), buf(ctx);
     if (int rc = cbuf.reserve(nf * sizeof(tfz::ZCounts) + 256)) return rc;
     tfz::ZCounts *dcounts = (tfz::ZCounts *)cbuf.p;
     {
