@@ -2160,10 +2160,25 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
     // table: C5's 10M groups -> 16384 buckets (wide bucket kernel 1.92 ms, against 2.67 ms at
     // 8192 buckets / ~60% and 3.72 ms at 4096 / ~80%, r03); the table itself is then sized for
     // two workgroups per CU (below)
-    const int max_bits = wide ? 14 : 12;
+    // TFG_WIDE_QUAD=1 (A/B): wide keys in 256-thread workgroups with ~38 KB of LDS, four per CU,
+    // over up to 2^15 buckets (two levels: 512 coarse x 64 fine)
+    static const bool quad_env = [] {
+        const char *v = getenv("TFG_WIDE_QUAD");
+        return v && *v == '1';
+    }();
+    const bool quad = wide && !a->nokey && quad_env;
+    size_t wide_cell = 8 + 16; // tag + 16-byte key, then the accumulators (below)
+    for (int i = 0; i < n_aggs; ++i) {
+        if (S.acc[i] != ACC_NONE) wide_cell += 8 * (size_t)lds_acc_words(S.acc[i]);
+        if (S.has_cnt[i]) wide_cell += 8;
+    }
+    // quad: the 256-thread kernel's static LDS (~6.5 KB) beside a table in a quarter of the CU
+    const int quad_cells = (int)(((40 * 1024 - 6656 - sizeof(Ctrl) - 16) / wide_cell - 2) & ~(size_t)63);
+    const int max_bits = wide ? (quad ? 15 : 14) : 12;
     if (bbits <= 0) {
         const int64_t cells_max = LDS_TABLE_MAX / cell;
-        const int64_t fit = wide ? cells_max * 3 / 8 : (cells_max * fill_big / 8) * 5 / 6;
+        const int64_t fit = quad ? (int64_t)quad_cells * 42 / 100
+                                 : wide ? cells_max * 3 / 8 : (cells_max * fill_big / 8) * 5 / 6;
         bbits = 8;
         while (bbits < max_bits && ((int64_t)1 << bbits) * fit < eg) ++bbits;
     }
@@ -2184,7 +2199,10 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
         cap = c2;
         fill_num = fill_big;
     }
-    if (wide && !a->nokey) {
+    if (quad && per_bucket * 100 <= (int64_t)quad_cells * 45 && quad_cells * fill_big / 8 >= need) {
+        cap = quad_cells;
+        fill_num = fill_big;
+    } else if (wide && !a->nokey) {
         // wide keys: the probe is latency-bound, so two 8-wave workgroups per CU (the 512-thread
         // kernel at 128 VGPRs) beat one 16-wave workgroup with a larger, emptier table: C5 1472
         // cells at ~42 % load 4.37 ms vs 2048 at ~30 % 4.66 ms (r05z).  The largest table (64-cell
@@ -2243,6 +2261,7 @@ int tfg_agg_create(tfg_ctx *ctx, int key_type, int n_aggs, const int *agg_kinds,
         }
     // one workgroup per CU anyway (LDS): make it 16 waves, and keep the in-flight insert headroom
     S.bt = S.lds_bytes > 80 * 1024 ? BT_BIG : BT;
+    if (quad && S.lds_bytes <= 40 * 1024 - 6656) S.bt = BT_QUAD; // the wide tiled kernel only (agg_bucket_wide.hip)
     S.maxfill = std::max(1, std::min(cap * fill_num / 8, cap - 8));
     if (a->nokey) {
         if (int rc = a->ensure_state(0, 1)) {

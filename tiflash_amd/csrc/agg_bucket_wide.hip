@@ -8,7 +8,12 @@ bool launch_bucket_wide_tiled(int code, int B, const AggSpec &S, hipStream_t st,
                               const GroupsIO &old, const uint64_t *ooff, const GroupsIO &tmp, uint64_t *new_cnt,
                               uint64_t *tmp_base) {
     auto go = [&](auto tag) {
-        launch_bucket_one_tiled<typename decltype(tag)::type>(B, S, st, tin, mode, old, ooff, tmp, new_cnt, tmp_base);
+        using Ops = typename decltype(tag)::type;
+        if (S.bt == BT_QUAD) // four 256-thread workgroups per CU (TFG_WIDE_QUAD)
+            hipLaunchKernelGGL((agg_bucket_tiled_kernel<Ops, BT_QUAD>), dim3(B), dim3(BT_QUAD), S.lds_bytes, st, S, tin,
+                               mode, old, ooff, tmp, new_cnt, tmp_base);
+        else
+            launch_bucket_one_tiled<Ops>(B, S, st, tin, mode, old, ooff, tmp, new_cnt, tmp_base);
         return true;
     };
     switch (code) {

@@ -14,6 +14,7 @@ namespace tfg {
 constexpr int AGG_MAX = 4;
 constexpr int BT = 512;      // bucket kernel threads (8 waves; 2-3 workgroups per CU)
 constexpr int BT_BIG = 1024; // for tables too large for two workgroups per CU (16 waves)
+constexpr int BT_QUAD = 256; // wide tiled tables of a quarter CU (four workgroups per CU)
 constexpr int LDS_TABLE_BYTES = 100 * 1024;  // preferred table size (two workgroups per CU)
 constexpr int LDS_TABLE_MAX = 150 * 1024;    // largest table (one 16-wave workgroup per CU)
 constexpr int LDS_CU_BYTES = 160 * 1024;     // gfx950 LDS per CU
