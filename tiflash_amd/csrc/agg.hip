@@ -659,14 +659,12 @@ __global__ void __launch_bounds__(RG_T) regroup_tiled_kernel(const uint64_t *rec
     for (int q = 0; q < PER; ++q) {
         bq[q] = 0xFFFFFFFFu;
         if (row[q] < 0) continue;
-        if (NCOL == 3 && (row[q] >> 62)) { // narrow pass-1 tile: u64 lo [TR1], u32 hi [TR1], u64 value [TR1]
+        if (NCOL == 3 && (row[q] >> 62)) { // narrow pass-1 tile: 20-byte records (nrec_load)
             const int64_t rr = row[q] & (((int64_t)1 << 62) - 1);
             const int64_t tile = rr / TR1, pos = rr - tile * TR1;
-            const uint64_t *lo = rec1 + (size_t)tile * TR1 * 3;
-            const uint32_t *hi = reinterpret_cast<const uint32_t *>(lo + TR1);
-            v[q][0] = lo[pos];
-            v[q][1] = wide_wide_hi(hi[pos]);
-            v[q][NCOL - 1] = reinterpret_cast<const uint64_t *>(hi + TR1)[pos];
+            uint32_t h;
+            nrec_load(rec1 + (size_t)tile * TR1 * 3, (uint32_t)pos, v[q][0], h, v[q][NCOL - 1]);
+            v[q][1] = wide_wide_hi(h);
             row[q] = rr;
             continue;
         }
@@ -706,14 +704,9 @@ __global__ void __launch_bounds__(RG_T) regroup_tiled_kernel(const uint64_t *rec
     __syncthreads();
     const uint32_t rows = x1 - x0;
     uint64_t *out = rec2 + (size_t)k * RG_TR * NCOL;
-    if (narrow_out) { // u64 lo [RG_TR], u32 hi [RG_TR], u64 value [RG_TR] (RG_TR even)
-        uint32_t *hi = reinterpret_cast<uint32_t *>(out + RG_TR);
-        uint64_t *val = reinterpret_cast<uint64_t *>(hi + RG_TR);
-        for (uint32_t i = threadIdx.x; i < rows; i += RG_T) {
-            out[i] = stage[i * NCOL];
-            hi[i] = wide_narrow_hi(stage[i * NCOL + 1]);
-            val[i] = stage[i * NCOL + NCOL - 1];
-        }
+    if (narrow_out) { // 20-byte records (nrec_store)
+        for (uint32_t i = threadIdx.x; i < rows; i += RG_T)
+            nrec_store(out, i, stage[i * NCOL], wide_narrow_hi(stage[i * NCOL + 1]), stage[i * NCOL + NCOL - 1]);
         return;
     }
     for (uint32_t i = threadIdx.x; i < rows * NCOL; i += RG_T) out[i] = stage[i];

@@ -1015,8 +1015,7 @@ template <int A0, int A1, int A2> struct WideFastOps {
     static constexpr int op(int i) { return i == 0 ? A0 : (i == 1 ? A1 : A2); }
     static constexpr int NCOL = 2 + (A0 >= 2) + (A1 >= 2) + (A2 >= 2);
     static constexpr bool WIDE = true;
-    // one summed argument: narrow tiles (WNARROW, partition.h) hold u64 key lo [TRS], u32 key hi
-    // [TRS], u64 value [TRS]
+    // one summed argument: narrow tiles (WNARROW, partition.h) hold 20-byte records (nrec_store)
     static constexpr bool NARROWABLE = NCOL == 3;
     static constexpr int pos(int i) { return 2 + (i > 0 && A0 >= 2) + (i > 1 && A1 >= 2); }
     struct Row {
@@ -1024,12 +1023,11 @@ template <int A0, int A1, int A2> struct WideFastOps {
         uint64_t v[3];
     };
     // row `off` of the narrow tile whose slot starts at row `slot` (slot rows of NCOL words each)
-    __device__ __forceinline__ void load_narrow(const uint64_t *rec, uint64_t slot, int TRS, uint32_t off, Row &v) const {
-        const uint64_t *lo = rec + slot * NCOL;
-        const uint32_t *hi = reinterpret_cast<const uint32_t *>(lo + TRS);
-        v.key = lo[off];
-        v.khi = wide_wide_hi(hi[off]);
-        const uint64_t w = reinterpret_cast<const uint64_t *>(hi + TRS)[off];
+    __device__ __forceinline__ void load_narrow(const uint64_t *rec, uint64_t slot, int, uint32_t off, Row &v) const {
+        uint32_t h;
+        uint64_t w;
+        nrec_load(rec + slot * NCOL, off, v.key, h, w);
+        v.khi = wide_wide_hi(h);
 #pragma unroll
         for (int i = 0; i < 3; ++i)
             if (op(i) >= 2) v.v[i] = w;

@@ -611,6 +611,26 @@ __host__ __device__ __forceinline__ uint32_t wide_narrow_hi(uint64_t hi) {
 __host__ __device__ __forceinline__ uint64_t wide_wide_hi(uint32_t h) {
     return (uint64_t)(h & 0xFFFFFFu) | ((uint64_t)(h >> 24) << 56);
 }
+// A narrow tile's rows are 20-byte records back to back from the slot's start: key lo (2 words),
+// narrow hi (1 word), value (2 words), 4-byte aligned.  A run of n rows is then one stretch of 20n
+// bytes; as three arrays (u64 lo [TRS], u32 hi [TRS], u64 value [TRS]) every run began and ended
+// inside a partly used line of each array, and the readers fetched 1.8x the records' bytes
+// (C5: bucket kernel 3.65 GB and regroup 3.61 GB for 2.0 GB of records, r06j)
+__device__ __forceinline__ void nrec_store(uint64_t *slot, uint32_t pos, uint64_t lo, uint32_t hi, uint64_t val) {
+    uint32_t *p = reinterpret_cast<uint32_t *>(slot) + (size_t)pos * 5;
+    p[0] = (uint32_t)lo;
+    p[1] = (uint32_t)(lo >> 32);
+    p[2] = hi;
+    p[3] = (uint32_t)val;
+    p[4] = (uint32_t)(val >> 32);
+}
+__device__ __forceinline__ void nrec_load(const uint64_t *slot, uint32_t pos, uint64_t &lo, uint32_t &hi, uint64_t &val) {
+    const uint32_t *p = reinterpret_cast<const uint32_t *>(slot) + (size_t)pos * 5;
+    const uint32_t a = p[0], b = p[1], c = p[2], d = p[3], e = p[4];
+    lo = (uint64_t)a | ((uint64_t)b << 32);
+    hi = c;
+    val = (uint64_t)d | ((uint64_t)e << 32);
+}
 constexpr int ST_MAXR = 8;     // rows per thread per tile (TR <= 8192 < 2^16: ranks pack in 16 bits)
 // tiles a round in the sparse variant's all-false check (four measured slower: 0 % C2 0.364 vs
 // 0.344 ms, r05ad — not memory-level parallelism but the per-round barriers bound it)
@@ -1027,13 +1047,12 @@ __global__ void __launch_bounds__(ST_T, 4) part_scatter_staged_kernel(Sel sel, P
             if constexpr (TILED) gp = (uint64_t)tile * (uint32_t)g.TRS + pstart[b] + (s - start[b]);
             else gp = run[b] + (s - start[b]);
             if (perm) perm[gp] = sperm[s];
-            if (WNARROW && narrow) { // u64 key lo, u32 key hi, u64 values, in the tile's slot
+            if (WNARROW && narrow) { // 20-byte records (nrec_store) in the tile's slot
                 const uint32_t pos = pstart[b] + (s - start[b]);
-                uint64_t *lo = reinterpret_cast<uint64_t *>(cols.out[0]) + (size_t)tile * (uint32_t)g.TRS * 3;
-                uint32_t *hi = reinterpret_cast<uint32_t *>(lo + g.TRS);
-                lo[pos] = reinterpret_cast<const uint64_t *>(lds + g.stage_off[0])[s];
-                hi[pos] = wide_narrow_hi(reinterpret_cast<const uint64_t *>(lds + g.stage_off[1])[s]);
-                reinterpret_cast<uint64_t *>(hi + g.TRS)[pos] = reinterpret_cast<const uint64_t *>(lds + g.stage_off[2])[s];
+                nrec_store(reinterpret_cast<uint64_t *>(cols.out[0]) + (size_t)tile * (uint32_t)g.TRS * 3, pos,
+                           reinterpret_cast<const uint64_t *>(lds + g.stage_off[0])[s],
+                           wide_narrow_hi(reinterpret_cast<const uint64_t *>(lds + g.stage_off[1])[s]),
+                           reinterpret_cast<const uint64_t *>(lds + g.stage_off[2])[s]);
             } else if (NARROW && narrow) { // u32 keys, then u64 values, in the tile's slot
                 const uint32_t pos = pstart[b] + (s - start[b]);
                 uint32_t *ks = reinterpret_cast<uint32_t *>(reinterpret_cast<uint64_t *>(cols.out[0]) +
