@@ -500,7 +500,8 @@ struct SelWideStr {
 // `fine` = 6 bits: the bucket kernel of (coarse c, fine f) then reads runs of ~RG_TR / 64 rows
 // from the tiles [tile_base[c], tile_base[c + 1]).
 #ifndef TFG_RG_TR
-#define TFG_RG_TR 1536
+#define TFG_RG_TR 1024 // r06m/n (C5, 512 threads): 1024 rows 0.97 ms, 1536 1.03, 3072 1.94; 512 / 768 /
+                       // 1024 threads at 512 / 768 / 1024 rows 1.16 / 1.41 / 1.19
 #endif
 #ifndef TFG_RG_T
 #define TFG_RG_T 512

@@ -945,14 +945,38 @@ template <int A0, int A1, int A2> struct FastOps {
                 if (op(i) >= 2) v.v[i] = rec[pos(i)];
         }
     }
-    // row `off` of narrow tile `tile` (slot of TRS rows: TRS u32 keys, then TRS u64 values)
-    __device__ __forceinline__ void load_narrow(const uint64_t *rec, uint64_t slot, int TRS, uint32_t off, Row &v) const {
-        const uint32_t *ks = reinterpret_cast<const uint32_t *>(rec + slot * 2);
-        v.key = ks[off];
-        const uint64_t w = reinterpret_cast<const uint64_t *>(ks + TRS)[off];
+    // A tiled row's words as loaded (load_raw), converted to a Row when the step uses them
+    // (unraw).  load_raw is branch-free: the same load instructions for a narrow or a 16-byte
+    // record, from a per-lane address, so the loads stay in flight across the step before (a load
+    // inside a divergent branch, or a loaded register copied at a join, is waited for there).
+    // Narrow tile slot: TRS u32 keys, then TRS u64 values; the key is read as 8 bytes (the upper
+    // half is the next key, or the first value word: discarded).  Rows past the chunk (ok false)
+    // read the first record.
+    struct Raw {
+        uint64_t w[NCOL];
+        bool nar;
+    };
+    __device__ __forceinline__ void load_raw(const uint64_t *rec, uint64_t slot, int TRS, uint32_t off, bool nar,
+                                             bool ok, Raw &r) const {
+        if constexpr (NCOL == 2) {
+            const uint32_t *ks = reinterpret_cast<const uint32_t *>(rec + slot * 2);
+            const uint64_t *kp = nar ? reinterpret_cast<const uint64_t *>(ks + off) : rec + (slot + off) * 2;
+            const uint64_t *vp = nar ? reinterpret_cast<const uint64_t *>(ks + TRS) + off : rec + (slot + off) * 2 + 1;
+            r.w[0] = *(ok ? kp : rec);
+            r.w[1] = *(ok ? vp : rec);
+            r.nar = nar;
+        } else {
+            const uint64_t *p = ok ? rec + (slot + off) * NCOL : rec;
+#pragma unroll
+            for (int c = 0; c < NCOL; ++c) r.w[c] = p[c];
+            r.nar = false;
+        }
+    }
+    __device__ __forceinline__ void unraw(const Raw &r, Row &v) const {
+        v.key = r.nar ? (r.w[0] & 0xFFFFFFFFull) : r.w[0];
 #pragma unroll
         for (int i = 0; i < 3; ++i)
-            if (op(i) >= 2) v.v[i] = w;
+            if (op(i) >= 2) v.v[i] = r.w[pos(i)];
     }
     __device__ __forceinline__ uint64_t key(const Row &v) const { return v.key; }
     __device__ __forceinline__ bool knull(const Row &) const { return false; }
@@ -1022,15 +1046,42 @@ template <int A0, int A1, int A2> struct WideFastOps {
         uint64_t key, khi;
         uint64_t v[3];
     };
-    // row `off` of the narrow tile whose slot starts at row `slot` (slot rows of NCOL words each)
-    __device__ __forceinline__ void load_narrow(const uint64_t *rec, uint64_t slot, int, uint32_t off, Row &v) const {
-        uint32_t h;
-        uint64_t w;
-        nrec_load(rec + slot * NCOL, off, v.key, h, w);
-        v.khi = wide_wide_hi(h);
+    // FastOps::load_raw / unraw.  NCOL 3: 16 bytes from the row's start (key lo, then the narrow
+    // hi word or the two hi words) and 8 bytes from its value (offset 12 in a 20-byte record, 16 in
+    // a 24-byte one); rows of a narrow slot start at 20-byte steps (4-byte aligned loads)
+    struct Raw {
+        uint4 q;
+        uint64_t w[NCOL == 3 ? 1 : NCOL];
+        bool nar;
+    };
+    __device__ __forceinline__ void load_raw(const uint64_t *rec, uint64_t slot, int, uint32_t off, bool nar, bool ok,
+                                             Raw &r) const {
+        if constexpr (NCOL == 3) {
+            const char *b = nar ? reinterpret_cast<const char *>(rec + slot * 3) + (size_t)off * 20
+                                : reinterpret_cast<const char *>(rec + (slot + off) * 3);
+            if (!ok) b = reinterpret_cast<const char *>(rec);
+            typedef unsigned u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+            typedef unsigned u32x2a4 __attribute__((ext_vector_type(2), aligned(4)));
+            const u32x4a4 q = *reinterpret_cast<const u32x4a4 *>(b);
+            const u32x2a4 w = *reinterpret_cast<const u32x2a4 *>(b + (nar ? 12 : 16));
+            r.q = make_uint4(q.x, q.y, q.z, q.w);
+            r.w[0] = (uint64_t)w.x | ((uint64_t)w.y << 32);
+            r.nar = nar;
+        } else {
+            const uint64_t *p = ok ? rec + (slot + off) * NCOL : rec;
+            const uint4 q = *reinterpret_cast<const uint4 *>(p);
+            r.q = q;
+#pragma unroll
+            for (int c = 2; c < NCOL; ++c) r.w[c] = p[c];
+            r.nar = false;
+        }
+    }
+    __device__ __forceinline__ void unraw(const Raw &r, Row &v) const {
+        v.key = ((uint64_t)r.q.y << 32) | r.q.x;
+        v.khi = r.nar ? wide_wide_hi(r.q.z) : (((uint64_t)r.q.w << 32) | r.q.z);
 #pragma unroll
         for (int i = 0; i < 3; ++i)
-            if (op(i) >= 2) v.v[i] = w;
+            if (op(i) >= 2) v.v[i] = NCOL == 3 ? r.w[0] : r.w[pos(i)];
     }
     const AggSpec &S;
     int mode;
@@ -1366,15 +1417,22 @@ agg_bucket_tiled_kernel(AggSpec S, TiledIn tin, int mode, GroupsIO old,
                 }
                 return;
             }
+#ifdef TFG_EXP_NOPROBE // profiling experiment only: a hashed cell instead of the wide lookup
+#pragma unroll
+            for (int u = 0; u < RT; ++u) cells[u] = (int)((uint32_t)(tg[u] >> 32) % (uint32_t)S.cap);
+#else
             if constexpr (Ops::WIDE) T.find_wide_multi<RT>(ku, kh, tg, ok, allow_insert, cells);
             else T.find_or_insert_multi<RT>(ku, nu, ok, allow_insert, cells);
+#endif
             int hit[RT];
 #pragma unroll
             for (int u = 0; u < RT; ++u) {
                 miss[u] = ok[u] && cells[u] < 0;
                 hit[u] = ok[u] ? cells[u] : -1;
             }
+#ifndef TFG_EXP_NOATOM // profiling experiment only: no state update
             ops.add_multi(T, hit, v);
+#endif
             // no barrier per step: a missing row (full table / inserts closed) looks its key up
             // once more and otherwise spills; an insert of the same key by another wave in this
             // step may not be visible yet, so the pass re-checks its spilled rows against the
@@ -1449,7 +1507,7 @@ agg_bucket_tiled_kernel(AggSpec S, TiledIn tin, int mode, GroupsIO old,
                 // (measured: a thread taking RT consecutive rows instead — one search per RT rows —
                 // made the kernel slower, 0.41 -> 0.52 ms: each load instruction then spans 4x the
                 // lines, and the run-crossing step diverges)
-                auto load_step = [&](uint32_t base, typename Ops::Row (&v)[RT], bool (&ok)[RT]) __attribute__((always_inline)) {
+                auto load_step = [&](uint32_t base, typename Ops::Raw (&v)[RT], bool (&ok)[RT]) __attribute__((always_inline)) {
                     // the RT rows' runs are found together: their index reads, their first run
                     // reads, then forward steps for the rows past their run's end, so the
                     // dependent LDS round trips of the RT rows overlap (one 8-byte read a run)
@@ -1476,34 +1534,83 @@ agg_bucket_tiled_kernel(AggSpec S, TiledIn tin, int mode, GroupsIO old,
                         for (int u = 0; u < RT; ++u)
                             if (walk[u]) run[u] = s_run[lo[u]];
                     }
+                    // every lane issues the same loads (Ops::load_raw: no branch, no copy of a
+                    // loaded register), so they stay in flight until the step that uses them.
+                    // (r06o: with a load in a narrow / wide branch and the loop-carried copy of
+                    // the rows, each load was waited for where it was issued — the wide kernel took
+                    // 1.64 ms, 0.89 ms with synthetic rows and no loads at all)
 #pragma unroll
                     for (int u = 0; u < RT; ++u) {
-                        if (!ok[u]) continue;
                         const uint32_t off = run[u].y + ii[u];
                         // the tile's slot: T * TRS rows stay below 2^32 (the ABI caps n below 2^32)
                         const uint64_t slot = (uint64_t)(uint32_t)(t0 + (int)lo[u]) * (uint32_t)tin.TR;
-                        if constexpr (Ops::NARROWABLE) {
-                            if (run[u].x >> 31) {
-                                ops.load_narrow(tin.rec, slot, tin.TR, off, v[u]);
-                                continue;
-                            }
+#ifdef TFG_EXP_NOLOAD // profiling experiment only: a synthetic row of the bucket instead of its record
+                        if constexpr (Ops::WIDE) {
+                            v[u].q = make_uint4((uint32_t)(b * 1000 + (int)((off * 2654435761u) % 600u)) + 1u, 0x6B000000u,
+                                                9u << 24, 0u);
+                            v[u].w[0] = off;
+                            v[u].nar = true;
+                        } else {
+                            v[u].w[0] = (uint64_t)(b * 4000 + (int)((off * 2654435761u) % 3906u)) + 1u;
+                            v[u].w[1] = off;
+                            v[u].nar = false;
                         }
-                        ops.load(src, (int64_t)(slot + off), v[u]);
+                        continue;
+#endif
+                        ops.load_raw(tin.rec, slot, tin.TR, off, Ops::NARROWABLE && (run[u].x >> 31), ok[u], v[u]);
                     }
                 };
-                typename Ops::Row vn[RT];
-                bool okn[RT];
-                if (tot > 0) load_step(0, vn, okn);
-                for (uint32_t base = 0; base < tot; base += BT * RT) {
+                auto run_step = [&](const typename Ops::Raw (&r)[RT], const bool (&okr)[RT]) __attribute__((always_inline)) {
                     typename Ops::Row v[RT];
                     bool ok[RT];
 #pragma unroll
                     for (int u = 0; u < RT; ++u) {
-                        v[u] = vn[u];
-                        ok[u] = okn[u];
+                        ops.unraw(r[u], v[u]);
+                        ok[u] = okr[u];
                     }
-                    if (base + BT * RT < tot) load_step(base + BT * RT, vn, okn);
                     step(v, ok);
+                };
+                constexpr uint32_t SZ = BT * RT;
+#ifdef TFG_EXP_C2_DB
+                constexpr bool DB = true;
+#else
+                constexpr bool DB = Ops::WIDE;
+#endif
+                if constexpr (DB) {
+                    // two register sets, alternating: the next step's rows load into the set the
+                    // current step does not use.  Each set has one load site, inside the loop, so
+                    // no loaded register is copied at the loop head (a copy waits for its load).
+                    // The loads are unconditional — rows past the chunk read its first record — so
+                    // neither set is merged at a branch's end either
+                    typename Ops::Raw ra[RT], rb[RT];
+                    bool oka[RT], okb[RT];
+                    bool have_b = false;
+                    for (uint32_t base = 0;; base += 2 * SZ) {
+                        const bool have_a = base < tot;
+                        load_step(base, ra, oka);
+                        if (have_b) run_step(rb, okb); // the previous round's second step
+                        if (!have_a) break;
+                        have_b = base + SZ < tot;
+                        load_step(base + SZ, rb, okb);
+                        run_step(ra, oka);
+                    }
+                } else {
+                    // 8-byte keys (RT = 4 rows a thread): one set, loaded a step ahead and copied
+                    // (two sets of four rows spill; r06p: C2 bucket kernel 0.425-0.43 ms with two)
+                    typename Ops::Raw rn[RT];
+                    bool okn[RT];
+                    if (tot > 0) load_step(0, rn, okn);
+                    for (uint32_t base = 0; base < tot; base += SZ) {
+                        typename Ops::Raw r[RT];
+                        bool ok[RT];
+#pragma unroll
+                        for (int u = 0; u < RT; ++u) {
+                            r[u] = rn[u];
+                            ok[u] = okn[u];
+                        }
+                        if (base + SZ < tot) load_step(base + SZ, rn, okn);
+                        run_step(r, ok);
+                    }
                 }
                 __syncthreads();
             }
