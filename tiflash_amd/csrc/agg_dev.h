@@ -546,34 +546,77 @@ struct Table {
 #pragma unroll
                     for (int s = 0; s < GS; ++s)
                         k[u][s] = __hip_atomic_load(&keys[grp[u] * GS + s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            // the group's slots as masks: empty, published same tag, unpublished same tag.  Only
+            // slots before the first empty one count; the first published same-tag slot is the
+            // candidate unless an unpublished one comes before it (then the group is re-read).
+            // One 16-byte key read a row, every row's issued together (a slot-by-slot scan reads
+            // and compares the keys one dependent LDS round trip after another)
+            int hit[R], empty[R], cand[R];
+            bool pend[R];
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                hit[u] = empty[u] = cand[u] = -1;
+                pend[u] = false;
+                if (!live[u]) continue;
+                unsigned em = 0, mm = 0, pm = 0;
+#pragma unroll
+                for (int s = 0; s < GS; ++s) {
+                    const uint64_t st = k[u][s];
+                    const bool same = (st | 1ull) == (tag[u] | 1ull);
+                    em |= (st == 0 ? 1u : 0u) << s;
+                    mm |= (same && (st & 1ull) ? 1u : 0u) << s;
+                    pm |= (same && !(st & 1ull) ? 1u : 0u) << s;
+                }
+                const unsigned lim = em ? (em & (0u - em)) - 1u : (1u << GS) - 1u;
+                mm &= lim;
+                pm &= lim;
+                empty[u] = em ? __ffs(em) - 1 : -1;
+                pend[u] = pm && (!mm || (pm & (0u - pm)) < (mm & (0u - mm)));
+                cand[u] = (!pend[u] && mm) ? __ffs(mm) - 1 : -1;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            uint4 q[R];
+#pragma unroll
+            for (int u = 0; u < R; ++u)
+                if (cand[u] >= 0) q[u] = wk[grp[u] * GS + cand[u]];
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                if (cand[u] < 0) continue;
+                if ((((uint64_t)q[u].y << 32) | q[u].x) == lo[u] && (((uint64_t)q[u].w << 32) | q[u].z) == hi[u]) {
+                    hit[u] = cand[u];
+                    continue;
+                }
+                // another key with the same tag (a 62-bit tag collision): the slots after it, one
+                // by one, to the first empty / unpublished same-tag / matching one
+                empty[u] = -1;
+                for (int s = cand[u] + 1; s < GS; ++s) {
+                    const uint64_t st = k[u][s];
+                    if (st == 0) {
+                        empty[u] = s;
+                        break;
+                    }
+                    if ((st | 1ull) != (tag[u] | 1ull)) continue;
+                    if (!(st & 1ull)) {
+                        pend[u] = true;
+                        break;
+                    }
+                    const uint4 q2 = wk[grp[u] * GS + s];
+                    if ((((uint64_t)q2.y << 32) | q2.x) == lo[u] && (((uint64_t)q2.w << 32) | q2.z) == hi[u]) {
+                        hit[u] = s;
+                        break;
+                    }
+                }
+            }
             bool any = false;
 #pragma unroll
             for (int u = 0; u < R; ++u) {
                 if (!live[u]) continue;
-                int hit = -1, empty = -1;
-                bool pend = false;
-#pragma unroll
-                for (int s = 0; s < GS; ++s) {
-                    if (empty >= 0 || hit >= 0 || pend) continue;
-                    const uint64_t st = k[u][s];
-                    if (st == 0) {
-                        empty = s;
-                    } else if ((st | 1ull) == (tag[u] | 1ull)) {
-                        if (!(st & 1ull)) {
-                            pend = true;
-                        } else {
-                            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                            const uint4 q = wk[grp[u] * GS + s];
-                            if ((((uint64_t)q.y << 32) | q.x) == lo[u] && (((uint64_t)q.w << 32) | q.z) == hi[u]) hit = s;
-                        }
-                    }
-                }
-                if (hit >= 0) {
-                    cell[u] = (int)(grp[u] * GS + hit);
+                if (hit[u] >= 0) {
+                    cell[u] = (int)(grp[u] * GS + hit[u]);
                     live[u] = false;
-                } else if (pend) {
+                } else if (pend[u]) {
                     any = true; // a same-tag key is being published: re-read this group
-                } else if (empty >= 0) {
+                } else if (empty[u] >= 0) {
                     if (!may_insert) {
                         live[u] = false;
                         continue;
@@ -586,16 +629,16 @@ struct Table {
                         live[u] = false;
                         continue;
                     }
-                    const int c = (int)(grp[u] * GS + empty);
+                    const int c = (int)(grp[u] * GS + empty[u]);
                     const uint64_t old = atomicCAS((unsigned long long *)&keys[c], 0ull, (unsigned long long)tag[u]);
                     if (old != 0) atomicSub(&ctrl->used, 1u);
                     if (old == 0) {
-                        uint4 q;
-                        q.x = (unsigned)lo[u];
-                        q.y = (unsigned)(lo[u] >> 32);
-                        q.z = (unsigned)hi[u];
-                        q.w = (unsigned)(hi[u] >> 32);
-                        wk[c] = q;
+                        uint4 w;
+                        w.x = (unsigned)lo[u];
+                        w.y = (unsigned)(lo[u] >> 32);
+                        w.z = (unsigned)hi[u];
+                        w.w = (unsigned)(hi[u] >> 32);
+                        wk[c] = w;
                         __hip_atomic_store((unsigned long long *)&keys[c], (unsigned long long)(tag[u] | 1ull),
                                            __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                         // read back: the loop's exit now depends on the publish, so it cannot be
