@@ -253,6 +253,10 @@ __global__ void __launch_bounds__(JT) join_probe_kernel(JoinArgs A) {
         };
         uint64_t rw[JRPT][PRW]; // the probe records (key + payload words)
         load_step(ps, rw);
+        // the first step's records complete here, so no use of rw inside the loop (the output
+        // stores) has to assume a load of the loop's entry may still be pending: those waits
+        // drained the next step's prefetch with it (s_waitcnt vmcnt(0) at every store)
+        __builtin_amdgcn_s_waitcnt(0);
         for (int64_t step = ps; step < pe; step += STEP) {
             unsigned head[JRPT];
             uint32_t cnt[JRPT], e[JRPT];
@@ -309,10 +313,15 @@ __global__ void __launch_bounds__(JT) join_probe_kernel(JoinArgs A) {
             else
 #pragma unroll
                 for (int u = 0; u < JRPT; ++u) total += (uint32_t)(ptotal >> (16 * u)) & 0xFFFFu;
+            // the output range is claimed BEFORE the next step's loads are issued: the wait for the
+            // atomic's result then leaves those loads in flight (vmcnt counts in issue order;
+            // claimed after them, the wait drained the prefetch with it)
+            unsigned long long claimed = 0;
+            if (total && threadIdx.x == 0) claimed = atomicAdd(A.cursor, (unsigned long long)total);
             uint64_t nx[JRPT][PRW];
             if (step + STEP < pe) load_step(step + STEP, nx);
             if (total) {
-                if (threadIdx.x == 0) L.base = atomicAdd(A.cursor, (unsigned long long)total);
+                if (threadIdx.x == 0) L.base = claimed;
                 __syncthreads();
                 const uint64_t base = L.base;
                 uint64_t pos = base + toff; // thread-major cursor (any_big)
