@@ -1304,7 +1304,14 @@ agg_bucket_tiled_kernel(AggSpec S, TiledIn tin, int mode, GroupsIO old,
                                                               const uint64_t *old_off, GroupsIO out, uint64_t *out_cnt,
                                                               uint64_t *tmp_base) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
-    constexpr int RT = Ops::WIDE ? 2 : RPT; // rows per thread per step (wide rows: 2, fewer VGPRs)
+    // rows per thread per step.  Wide rows: one (r06ab, C5, two alternating runs each: 1 row
+    // 1.276 / 1.285 ms, 2 rows 1.454 / 1.457, 3 rows 2.155 / 2.151 — 103 VGPRs and no scratch at
+    // one row, 272 B of spills at three: more waves' worth of independent steps beat more rows)
+#ifndef TFG_EXP_WRT
+    constexpr int RT = Ops::WIDE ? 1 : RPT;
+#else
+    constexpr int RT = Ops::WIDE ? TFG_EXP_WRT : RPT; // experiment: wide rows per thread per step
+#endif
     __shared__ unsigned long long s_red[BT / 64];
     __shared__ unsigned long long s_base[3];
     constexpr int CH = BT; // tiles per pass-0 chunk: one per thread
