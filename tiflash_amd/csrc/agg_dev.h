@@ -1307,10 +1307,12 @@ agg_bucket_tiled_kernel(AggSpec S, TiledIn tin, int mode, GroupsIO old,
     // rows per thread per step.  Wide rows: one (r06ab, C5, two alternating runs each: 1 row
     // 1.276 / 1.285 ms, 2 rows 1.454 / 1.457, 3 rows 2.155 / 2.151 — 103 VGPRs and no scratch at
     // one row, 272 B of spills at three: more waves' worth of independent steps beat more rows)
+    // 8-byte keys: two (r06ad, C2, two alternating runs each: agg.bucket 0.424 ms at four rows,
+    // 0.392 at two, 0.407 at one; 0.388 at two with the alternating register sets below)
 #ifndef TFG_EXP_WRT
-    constexpr int RT = Ops::WIDE ? 1 : RPT;
+    constexpr int RT = Ops::WIDE ? 1 : 2;
 #else
-    constexpr int RT = Ops::WIDE ? TFG_EXP_WRT : RPT; // experiment: wide rows per thread per step
+    constexpr int RT = Ops::WIDE ? TFG_EXP_WRT : 2; // experiment: wide rows per thread per step
 #endif
     __shared__ unsigned long long s_red[BT / 64];
     __shared__ unsigned long long s_base[3];
@@ -1621,46 +1623,22 @@ agg_bucket_tiled_kernel(AggSpec S, TiledIn tin, int mode, GroupsIO old,
                     step(v, ok);
                 };
                 constexpr uint32_t SZ = BT * RT;
-#ifdef TFG_EXP_C2_DB
-                constexpr bool DB = true;
-#else
-                constexpr bool DB = Ops::WIDE;
-#endif
-                if constexpr (DB) {
-                    // two register sets, alternating: the next step's rows load into the set the
-                    // current step does not use.  Each set has one load site, inside the loop, so
-                    // no loaded register is copied at the loop head (a copy waits for its load).
-                    // The loads are unconditional — rows past the chunk read its first record — so
-                    // neither set is merged at a branch's end either
-                    typename Ops::Raw ra[RT], rb[RT];
-                    bool oka[RT], okb[RT];
-                    bool have_b = false;
-                    for (uint32_t base = 0;; base += 2 * SZ) {
-                        const bool have_a = base < tot;
-                        load_step(base, ra, oka);
-                        if (have_b) run_step(rb, okb); // the previous round's second step
-                        if (!have_a) break;
-                        have_b = base + SZ < tot;
-                        load_step(base + SZ, rb, okb);
-                        run_step(ra, oka);
-                    }
-                } else {
-                    // 8-byte keys (RT = 4 rows a thread): one set, loaded a step ahead and copied
-                    // (two sets of four rows spill; r06p: C2 bucket kernel 0.425-0.43 ms with two)
-                    typename Ops::Raw rn[RT];
-                    bool okn[RT];
-                    if (tot > 0) load_step(0, rn, okn);
-                    for (uint32_t base = 0; base < tot; base += SZ) {
-                        typename Ops::Raw r[RT];
-                        bool ok[RT];
-#pragma unroll
-                        for (int u = 0; u < RT; ++u) {
-                            r[u] = rn[u];
-                            ok[u] = okn[u];
-                        }
-                        if (base + SZ < tot) load_step(base + SZ, rn, okn);
-                        run_step(r, ok);
-                    }
+                // two register sets, alternating: the next step's rows load into the set the
+                // current step does not use.  Each set has one load site, inside the loop, so
+                // no loaded register is copied at the loop head (a copy waits for its load).
+                // The loads are unconditional — rows past the chunk read its first record — so
+                // neither set is merged at a branch's end either
+                typename Ops::Raw ra[RT], rb[RT];
+                bool oka[RT], okb[RT];
+                bool have_b = false;
+                for (uint32_t base = 0;; base += 2 * SZ) {
+                    const bool have_a = base < tot;
+                    load_step(base, ra, oka);
+                    if (have_b) run_step(rb, okb); // the previous round's second step
+                    if (!have_a) break;
+                    have_b = base + SZ < tot;
+                    load_step(base + SZ, rb, okb);
+                    run_step(ra, oka);
                 }
                 __syncthreads();
             }
